@@ -1,0 +1,217 @@
+"""Benchmark: authz decisions/sec at 10k policies on MI355X (BASELINE.json metric).
+
+One step = one evaluation pass of the GPU hot path (TieredPolicyStores.IsAuthorized for every
+request of a device-resident batch) over a batch of synthetic SubjectAccessReviews.
+Workload (config C3 of BASELINE.json, single-GPU shard): 10,000 ABAC policies keyed on
+k8s::Group membership with when-clauses over namespace / apiGroup / resource / name (like) /
+labelSelector (containsAny), x `--batch` SARs per GPU, Zipf users with 1+Binomial(7,0.35) groups.
+Multi-GPU: one process per GPU (torchrun), the compiled image is replicated, requests are sharded
+(weak scaling: fixed batch per GPU), no collective on the decision path.
+
+Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects; see DESIGN.md §Measurement.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cedar-access-control-for-k8s_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(sars, n_reasons, has_like):
+    """B_dec = 64 + 4G + 8S + A + 16 + 4 n_reasons per decision."""
+    total = 0
+    for s, nr in zip(sars, n_reasons):
+        sp = s["spec"]
+        g = len(sp.get("groups") or [])
+        ra = sp.get("resourceAttributes") or {}
+        S = len((ra.get("labelSelector") or {}).get("requirements") or []) + len(sp.get("extra") or {})
+        A = 0
+        if has_like:
+            A = len(ra.get("name", "")) if ra else len((sp.get("nonResourceAttributes") or {}).get("path", ""))
+        total += 64 + 4 * g + 8 * S + A + 16 + 4 * nr
+    return total
+
+
+def cpu_baseline(policies_text, sars, seconds, workers):
+    """Oracle (`port`: Python restatement of cedar-go semantics) on a bounded sample, pre-built
+    EntityMaps, `workers` processes. Runs before any GPU initialisation."""
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cedar_oracle as co
+    import k8s_model as km
+
+    global _BASE
+    tiers = [co.PolicySet.from_bytes("c3.cedar", policies_text)]
+    items = []
+    for s in sars:
+        a = km.attributes_from_sar(s)
+        em, req = km.record_to_cedar_resource(a)
+        items.append((em, req))
+    _BASE = (tiers, items, seconds)
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        counts = pool.map(_cpu_worker, range(workers))
+    wall = time.perf_counter() - t0
+    n = sum(counts)
+    return {"value": n / wall, "unit": "decisions/s", "cores": workers, "kind": "port",
+            "sample": f"{n} SubjectAccessReviews (pre-built EntityMaps) x {sum(len(t.policies) for t in tiers)} policies "
+                      f"through oracle/cedar_oracle.py tiered_is_authorized, {workers} processes x ~{seconds:.0f} s"}
+
+
+_BASE = None
+
+
+def _cpu_worker(w):
+    import cedar_oracle as co
+    tiers, items, seconds = _BASE
+    t_end = time.perf_counter() + seconds
+    n = 0
+    i = w
+    while time.perf_counter() < t_end:
+        em, req = items[i % len(items)]
+        co.tiered_is_authorized(tiers, em, req)
+        n += 1
+        i += 17
+    return n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--policies", type=int, default=10_000)
+    ap.add_argument("--batch", type=int, default=65_536, help="requests per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-workers", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--latency-batches", type=int, default=40)
+    ap.add_argument("--latency-batch", type=int, default=4096)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from cedargpu import synth
+
+    pop = synth.Population(seed=7)
+    policies = synth.abac_policies(args.policies, seed=31, pop=pop)
+    sars = synth.random_sars(args.batch, seed=1000 + rank, pop=pop)
+
+    baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        workers = args.cpu_workers or max(1, min(16, (os.cpu_count() or 2) - 1))
+        baseline = cpu_baseline(policies, sars[:4096], args.cpu_seconds, workers)
+
+    import torch
+    import torch.distributed as dist
+
+    import cedargpu
+
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    device = local
+
+    t_build = time.perf_counter()
+    image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies)], epoch=1)
+    ctx = cedargpu.Context(device)
+    ctx.load(image, 1)
+    b = ctx.batch()
+    b.add_sar_json(synth.sars_json(sars))
+    t_enc = time.perf_counter()
+    b.submit()
+    b.wait()  # correctness pass: results downloaded, overflow re-runs done
+    t_first = time.perf_counter()
+    n_reasons = [b.reasons(i)[0].__len__() for i in range(len(b))]
+    alg_bytes = algorithmic_bytes(sars, n_reasons, has_like=True)
+
+    if args.warmup:
+        b.time(args.warmup)
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    kernel_ms = b.time(args.steps)  # HIP events on the evaluation stream, K launches
+    torch.cuda.synchronize(device)
+    wall_s = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([wall_s, kernel_ms], device=f"cuda:{device}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall_s, kernel_ms = float(t[0]), float(t[1])
+        dist.barrier()
+
+    # submit -> results-visible latency on small batches (includes H2D, launch, D2H)
+    lat = []
+    if rank == 0 and args.latency_batches:
+        chunk = synth.sars_json(sars[:args.latency_batch])
+        pending = []
+        for _ in range(args.latency_batches):
+            lb = ctx.batch()
+            lb.add_sar_json(chunk)
+            pending.append(lb)
+        for lb in pending:
+            t1 = time.perf_counter()
+            lb.submit()
+            lb.wait()
+            lat.append((time.perf_counter() - t1) * 1e3)
+            lb.close()
+        lat.sort()
+
+    if rank == 0:
+        ms_per_step = wall_s * 1e3 / args.steps
+        decisions = args.batch * world * args.steps
+        avg_kernel_ms = kernel_ms / args.steps
+        achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+        if os.path.exists(pmc):
+            try:
+                pj = json.load(open(pmc))
+                if pj.get("policies") == args.policies and pj.get("batch") == args.batch:
+                    traffic = pj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "authz decisions/sec (node) at 10k policies",
+            "value": decisions / wall_s,
+            "unit": "decisions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded SubjectAccessReviews + generated ABAC policies; no dataset)",
+            "config": {"workload": "C3 single-GPU shard: 10k ABAC policies (k8s::Group scope, namespace/apiGroup/"
+                                   "resource/labelSelector/like conditions) x synthetic SARs",
+                       "policies": args.policies, "requests_per_gpu": args.batch, "tiers": 1,
+                       "parallelism": f"request-sharded x{world}, image replicated"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": baseline,
+            "latency": {"batch": args.latency_batch, "p50_ms": lat[len(lat) // 2] if lat else None,
+                        "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
+                        "batches": len(lat)},
+            "host": {"encode_s": t_enc - t_build, "first_pass_s": t_first - t_enc},
+        }
+        if baseline:
+            out["speedup_vs_cpu_baseline"] = out["value"] / baseline["value"]
+        print(json.dumps(out), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,13 @@
+"""cedargpu — Python binding of the MI355X Cedar evaluator C-ABI (include/cedargpu.h).
+
+Mirrors the reference's store interface for the hot path:
+  * `MemoryStore` / `DirectoryStore` / `CRDStore` / `AVPStore` / `StaticStore` — policy sources
+    with the reference's policy-ID conventions (internal/server/store/*.go);
+  * `TieredPolicyStores.is_authorized(entities, request)` — internal/server/store/store.go:25-42,
+    evaluated on the GPU; `is_authorized_batch` evaluates many requests in one launch.
+The product path has no CPU fallback: importing this package fails loudly when libcedargpu.so
+is missing, and evaluation raises `DeviceError` when no GPU is present.
+"""
+from ._lib import CedarGPUError, CompileError, DeviceError, lib, lib_path  # noqa: F401
+from .store import (AVPStore, Batch, Context, CRDStore, DirectoryStore, MemoryStore, PolicyStore,  # noqa: F401
+                    StaticStore, TieredPolicyStores, Authorizer, ALLOW_ALL_ADMISSION, build_image, device_count)

@@ -1,0 +1,379 @@
+"""Host-side mirror of the reference's policy stores and tier walk, driving the GPU C-ABI.
+
+Reference interfaces mirrored (file:line in the reference):
+  PolicyStore                      internal/server/store/store.go:9-15
+  TieredPolicyStores.IsAuthorized  internal/server/store/store.go:25-42
+  NewMemoryStore                   internal/server/store/memory.go:17-27   (IDs policy<i>)
+  directory store                  internal/server/store/directory.go:41-82 (IDs <file>.policy<i>)
+  CRD store                        internal/server/store/crd.go:45-118      (IDs <name><i>-<uid>)
+  Verified Permissions store       internal/server/store/verified_permissions.go:58-100 (IDs <id>.<i>)
+  StaticStore / allow-all          internal/server/store/memory.go:30-43, cmd/cedar-webhook/main.go:111-116
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import threading
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+from ._lib import CG_E_RANGE, CompileError, DeviceError, _err, lib
+
+_P = ctypes.c_void_p
+
+
+def _b(s: str) -> bytes:
+    return s.encode("utf-8")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib.cg_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class PolicyStore:
+    """A policy source. `documents()` yields (kind, args) fed to the compiler."""
+
+    name = "PolicyStore"
+    load_complete = True
+
+    def documents(self):
+        raise NotImplementedError
+
+    def initial_policy_load_complete(self) -> bool:
+        return self.load_complete
+
+
+class MemoryStore(PolicyStore):
+    """store.NewMemoryStore(filename, document, loadComplete) — cedar.NewPolicySetFromBytes."""
+
+    def __init__(self, filename: str, document: str, load_complete: bool = True):
+        self.name = filename
+        self.filename = filename
+        self.document = document
+        self.load_complete = load_complete
+
+    def documents(self):
+        yield ("doc", self.filename, self.document, "policy", "")
+
+
+class DirectoryStore(PolicyStore):
+    """Directory store snapshot: {file name: content} of the *.cedar files (directory.go:51-79)."""
+
+    name = "FilePolicyStore"
+
+    def __init__(self, files: dict):
+        self.files = dict(files)
+
+    def documents(self):
+        for fname in sorted(self.files):  # os.ReadDir returns entries sorted by filename
+            if not fname.endswith(".cedar"):
+                continue
+            yield ("doc", fname, self.files[fname], f"{fname}.policy", "")
+
+
+class CRDStore(PolicyStore):
+    """Policy CRD snapshot: list of (metadata.name, metadata.uid, spec.content) (crd.go:45-118)."""
+
+    name = "CRDPolicyStore"
+
+    def __init__(self, policies: Sequence[Tuple[str, str, str]]):
+        self.policies = list(policies)
+
+    def documents(self):
+        for name, uid, content in self.policies:
+            yield ("doc", name, content, name, f"-{uid}")
+
+
+class AVPStore(PolicyStore):
+    """Amazon Verified Permissions snapshot: list of (policyId, statement) (verified_permissions.go:58-100)."""
+
+    name = "VerifiedPermissionsPolicyStore"
+
+    def __init__(self, policies: Sequence[Tuple[str, str]]):
+        self.policies = list(policies)
+
+    def documents(self):
+        for pid, stmt in self.policies:
+            yield ("doc", pid, stmt, f"{pid}.", "")
+
+
+class StaticStore(PolicyStore):
+    """StaticStore built from AST policies: explicit IDs, zero Position (admit_all_policy.go:10-19)."""
+
+    name = "StaticStore"
+
+    def __init__(self, policies: Sequence[Tuple[str, str]]):
+        self.policies = list(policies)
+
+    def documents(self):
+        for pid, text in self.policies:
+            yield ("policy", pid, "", text, True)
+
+
+ALLOW_ALL_ADMISSION = StaticStore([(
+    "allow-all-admission",
+    'permit (principal, action in [k8s::admission::Action::"create", k8s::admission::Action::"update", '
+    'k8s::admission::Action::"delete", k8s::admission::Action::"connect"], resource);')])
+
+
+def build_image(stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
+    """Compiles the tiers (one per store) into an image blob. Host only; no GPU needed."""
+    c = _P()
+    if lib.cg_compiler_create(ctypes.byref(c)):
+        raise CompileError(-1, "compiler create failed")
+    try:
+        for st in stores:
+            lib.cg_compiler_add_tier(c)
+            for d in st.documents():
+                if d[0] == "doc":
+                    _, fname, text, pre, suf = d
+                    tb = _b(text)
+                    rc = lib.cg_compiler_add_document(c, _b(fname), tb, len(tb), _b(pre), _b(suf))
+                else:
+                    _, pid, fname, text, zero = d
+                    tb = _b(text)
+                    rc = lib.cg_compiler_add_policy(c, _b(pid), _b(fname), tb, len(tb), 1 if zero else 0)
+                if rc:
+                    raise _err(rc, lib.cg_compiler_last_error(c).decode())
+        out = _P()
+        n = ctypes.c_size_t()
+        rc = lib.cg_compiler_build(c, epoch, ctypes.byref(out), ctypes.byref(n))
+        if rc:
+            raise _err(rc, lib.cg_compiler_last_error(c).decode())
+        try:
+            return ctypes.string_at(out, n.value)
+        finally:
+            lib.cg_free(out)
+    finally:
+        lib.cg_compiler_destroy(c)
+
+
+class Context:
+    """One GPU: loaded images (by epoch) and the active one."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._h = _P()
+        rc = lib.cg_ctx_create(device, ctypes.byref(self._h))
+        if rc:
+            raise DeviceError(rc, f"no usable GPU {device}")
+
+    def close(self):
+        if self._h:
+            lib.cg_ctx_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_error(self) -> str:
+        return lib.cg_last_error(self._h).decode()
+
+    def load(self, image: bytes, epoch: int, activate: bool = True):
+        buf = ctypes.create_string_buffer(image, len(image))
+        rc = lib.cg_image_load(self._h, buf, len(image), epoch)
+        if rc:
+            raise _err(rc, self.last_error())
+        if activate:
+            rc = lib.cg_image_activate(self._h, epoch)
+            if rc:
+                raise _err(rc, self.last_error())
+
+    def activate(self, epoch: int):
+        rc = lib.cg_image_activate(self._h, epoch)
+        if rc:
+            raise _err(rc, self.last_error())
+
+    def batch(self) -> "Batch":
+        return Batch(self)
+
+
+class Batch:
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._h = _P()
+        rc = lib.cg_batch_create(ctx._h, ctypes.byref(self._h))
+        if rc:
+            raise _err(rc, ctx.last_error())
+
+    def close(self):
+        if self._h:
+            lib.cg_batch_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_json(self, payload: str):
+        b = _b(payload)
+        rc = lib.cg_batch_add_json(self._h, b, len(b))
+        if rc:
+            raise _err(rc, "batch add failed")
+
+    def add(self, entities: list, request: dict):
+        self.add_json(json.dumps({"entities": entities, "request": request}))
+
+    def add_sar_json(self, payload: str):
+        """SubjectAccessReview JSON (object or array) -> entities via the C++ model (sar.cpp)."""
+        b = _b(payload)
+        rc = lib.cg_batch_add_sar_json(self._h, b, len(b))
+        if rc:
+            raise _err(rc, "SubjectAccessReview encode failed")
+
+    def authz(self, i: int) -> Tuple[int, str]:
+        """(authorizer.Decision: 0 Deny / 1 Allow / 2 NoOpinion, reason) — authorizer.go:36-85."""
+        dec = ctypes.c_int()
+        need = ctypes.c_size_t(0)
+        buf = ctypes.create_string_buffer(512)
+        rc = lib.cg_batch_authz(self._h, i, ctypes.byref(dec), buf, 512, ctypes.byref(need))
+        if rc == CG_E_RANGE and need.value > 512:
+            buf = ctypes.create_string_buffer(need.value)
+            rc = lib.cg_batch_authz(self._h, i, ctypes.byref(dec), buf, need.value, ctypes.byref(need))
+        if rc:
+            raise _err(rc, "authz result failed")
+        return dec.value, buf.value.decode("utf-8")
+
+    def __len__(self):
+        return lib.cg_batch_size(self._h)
+
+    def submit(self):
+        rc = lib.cg_batch_submit(self._h)
+        if rc:
+            raise _err(rc, "batch submit failed")
+
+    def wait(self):
+        rc = lib.cg_batch_wait(self._h, -1)
+        if rc:
+            raise _err(rc, "batch wait failed")
+
+    def decision(self, i: int) -> Tuple[bool, int]:
+        allow = ctypes.c_int()
+        tier = ctypes.c_uint32()
+        rc = lib.cg_batch_decision(self._h, i, ctypes.byref(allow), ctypes.byref(tier))
+        if rc:
+            raise _err(rc, "decision failed")
+        return bool(allow.value), tier.value
+
+    def diagnostic(self, i: int, reasons_only: bool = False) -> str:
+        need = ctypes.c_size_t(0)
+        buf = ctypes.create_string_buffer(512)
+        rc = lib.cg_batch_diagnostic(self._h, i, 1 if reasons_only else 0, buf, 512, ctypes.byref(need))
+        if rc == CG_E_RANGE and need.value > 512:
+            buf = ctypes.create_string_buffer(need.value)
+            rc = lib.cg_batch_diagnostic(self._h, i, 1 if reasons_only else 0, buf, need.value, ctypes.byref(need))
+        if rc:
+            raise _err(rc, "diagnostic failed")
+        return buf.value.decode("utf-8")
+
+    def reasons(self, i: int) -> Tuple[List[int], int]:
+        n = ctypes.c_uint32()
+        ne = ctypes.c_uint32()
+        lib.cg_batch_reasons(self._h, i, None, 0, ctypes.byref(n), ctypes.byref(ne))
+        arr = (ctypes.c_uint32 * max(n.value, 1))()
+        rc = lib.cg_batch_reasons(self._h, i, arr, n.value, ctypes.byref(n), ctypes.byref(ne))
+        if rc:
+            raise _err(rc, "reasons failed")
+        return list(arr[:n.value]), ne.value
+
+    def time(self, iters: int) -> float:
+        ms = ctypes.c_float()
+        rc = lib.cg_batch_time(self._h, iters, ctypes.byref(ms))
+        if rc:
+            raise _err(rc, "timing failed")
+        return ms.value
+
+    def bytes(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib.cg_batch_bytes(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+
+class TieredPolicyStores:
+    """store.TieredPolicyStores over GPU-compiled tiers (store.go:20-42).
+
+    `is_authorized(entities, request)` returns (decision: bool, diagnostic_json: str) exactly as
+    the reference's TieredPolicyStores.IsAuthorized + json.Marshal(diagnostic) would.
+    """
+
+    _epoch_lock = threading.Lock()
+    _next_epoch = 1
+
+    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None):
+        self.stores = list(stores)
+        self.ctx = ctx or Context(device)
+        self.reload()
+
+    def reload(self):
+        """Recompiles every store and atomically swaps the active image (hot reload)."""
+        with TieredPolicyStores._epoch_lock:
+            epoch = TieredPolicyStores._next_epoch
+            TieredPolicyStores._next_epoch += 1
+        self.image = build_image(self.stores, epoch)
+        self.ctx.load(self.image, epoch, activate=True)
+        self.epoch = epoch
+
+    def ready(self) -> bool:
+        return all(s.initial_policy_load_complete() for s in self.stores)
+
+    def is_authorized_batch(self, items: Iterable[Tuple[list, dict]]) -> List[Tuple[bool, str]]:
+        b = self.ctx.batch()
+        payload = json.dumps([{"entities": e, "request": r} for e, r in items])
+        b.add_json(payload)
+        b.submit()
+        b.wait()
+        out = []
+        for i in range(len(b)):
+            ok, _ = b.decision(i)
+            out.append((ok, b.diagnostic(i)))
+        b.close()
+        return out
+
+    def is_authorized(self, entities: list, request: dict) -> Tuple[bool, str]:
+        return self.is_authorized_batch([(entities, request)])[0]
+
+
+class Authorizer:
+    """cedarWebhookAuthorizer over GPU tiers (authorizer.go:21-85). `authorize_batch` takes
+    SubjectAccessReview dicts and returns [(authorizer.Decision, reason)]."""
+
+    DENY, ALLOW, NO_OPINION = 0, 1, 2
+
+    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None):
+        self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx)
+        self._loaded = False
+
+    def authorize_batch(self, sars: Sequence[dict]) -> List[Tuple[int, str]]:
+        if not self._loaded:  # authorizer.go:58-66 (checked after the fast paths there; see below)
+            if not self.tiers.ready():
+                return [_fast_or_noopinion(s) for s in sars]
+            self._loaded = True
+        b = self.tiers.ctx.batch()
+        b.add_sar_json(json.dumps(list(sars)))
+        b.submit()
+        b.wait()
+        out = [b.authz(i) for i in range(len(b))]
+        b.close()
+        return out
+
+    def authorize(self, sar: dict) -> Tuple[int, str]:
+        return self.authorize_batch([sar])[0]
+
+
+def _fast_or_noopinion(sar: dict) -> Tuple[int, str]:
+    """Stores not loaded: fast paths still answer first (authorizer.go:38-57), else NoOpinion."""
+    spec = sar.get("spec", {})
+    name = spec.get("user", "")
+    ra = spec.get("resourceAttributes") or {}
+    ro = ra.get("verb", (spec.get("nonResourceAttributes") or {}).get("verb", "")) in ("get", "list", "watch")
+    if name == "system:authorizer:cedar-authorizer" and ro and ra.get("group") == "cedar.k8s.aws" and ra.get("resource") == "policies":
+        return 1, "cedar authorizer is always allowed to access policies"
+    if name == "system:authorizer:cedar-authorizer" and ro and ra.get("group") == "rbac.authorization.k8s.io":
+        return 1, "cedar authorizer is always allowed to read RBAC policies"
+    return 2, ""

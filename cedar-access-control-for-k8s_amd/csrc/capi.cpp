@@ -1,0 +1,492 @@
+// C-ABI implementation (include/cedargpu.h). No exception crosses this boundary.
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include "../../include/cedargpu.h"
+#include "device.h"
+#include "engine.h"
+#include "sar.h"
+
+using namespace cg;
+
+struct cg_compiler {
+  std::vector<std::vector<DocSpec>> tiers;
+  std::string err;
+};
+
+namespace {
+struct LoadedImage {
+  std::shared_ptr<Image> host;
+  DevImage dev;
+  ~LoadedImage() { dev_image_free(&dev); }
+};
+}  // namespace
+
+struct cg_ctx {
+  int device = 0;
+  void* stream = nullptr;
+  std::mutex mu;
+  std::map<uint64_t, std::shared_ptr<LoadedImage>> images;
+  std::shared_ptr<LoadedImage> active;
+  std::string err;
+};
+
+struct cg_batch {
+  cg_ctx* ctx = nullptr;
+  std::shared_ptr<LoadedImage> img;
+  Batch host;
+  DevBatch dev;
+  bool submitted = false, done = false;
+  std::string err;
+  // items: caller-visible entries; dev >= 0 is the device request index, else a fast-path result
+  struct Item { int32_t dev; int32_t fast; };
+  std::vector<Item> items;
+  std::map<uint32_t, std::string> fast_reason;
+  ~cg_batch() { dev_batch_free(&dev); }
+  int32_t dev_of(uint32_t i) const { return i < items.size() ? items[i].dev : -1; }
+};
+
+#define GUARD(errstr, body)                                       \
+  try {                                                           \
+    body                                                          \
+  } catch (const CedarError& e) {                                 \
+    errstr = e.what();                                            \
+    return CG_E_PARSE;                                            \
+  } catch (const std::bad_alloc&) {                               \
+    errstr = "out of host memory";                                \
+    return CG_E_ARG;                                              \
+  } catch (const std::exception& e) {                             \
+    errstr = e.what();                                            \
+    return CG_E_ARG;                                              \
+  }
+
+extern "C" {
+
+const char* cg_version(void) { return "cedargpu 0.1.0 (gfx950)"; }
+void cg_free(void* p) { std::free(p); }
+
+// ---------------------------------------------------------------------------------------------
+int cg_compiler_create(cg_compiler** out) {
+  if (!out) return CG_E_ARG;
+  *out = new (std::nothrow) cg_compiler();
+  return *out ? CG_OK : CG_E_ARG;
+}
+void cg_compiler_destroy(cg_compiler* c) { delete c; }
+const char* cg_compiler_last_error(cg_compiler* c) { return c ? c->err.c_str() : "null compiler"; }
+
+int cg_compiler_add_tier(cg_compiler* c) {
+  if (!c) return CG_E_ARG;
+  c->tiers.emplace_back();
+  return CG_OK;
+}
+
+int cg_compiler_add_document(cg_compiler* c, const char* filename, const char* text, size_t len, const char* id_prefix,
+                             const char* id_suffix) {
+  if (!c || (!text && len)) return CG_E_ARG;
+  GUARD(c->err, {
+    DocSpec d;
+    d.filename = filename ? filename : "";
+    d.text.assign(text ? text : "", len);
+    d.id_prefix = id_prefix ? id_prefix : "policy";
+    d.id_suffix = id_suffix ? id_suffix : "";
+    (void)parse_policies(d.text, d.filename);  // fail at add time like cedar.NewPolicySetFromBytes
+    if (c->tiers.empty()) c->tiers.emplace_back();
+    c->tiers.back().push_back(std::move(d));
+    return CG_OK;
+  })
+}
+
+int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* filename, const char* text, size_t len,
+                           int zero_position) {
+  if (!c || !policy_id || !*policy_id || (!text && len)) return CG_E_ARG;
+  GUARD(c->err, {
+    DocSpec d;
+    d.filename = filename ? filename : "";
+    d.text.assign(text ? text : "", len);
+    d.explicit_id = policy_id;
+    d.zero_position = zero_position != 0;
+    auto ps = parse_policies(d.text, d.filename);
+    if (ps.size() != 1) { c->err = "expected exactly one policy"; return CG_E_PARSE; }
+    if (c->tiers.empty()) c->tiers.emplace_back();
+    c->tiers.back().push_back(std::move(d));
+    return CG_OK;
+  })
+}
+
+int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len) {
+  if (!c || !image || !len) return CG_E_ARG;
+  try {
+    auto img = compile_image(c->tiers, epoch);
+    auto blob = img->serialize();
+    uint8_t* p = (uint8_t*)std::malloc(blob.size());
+    if (!p) { c->err = "out of host memory"; return CG_E_ARG; }
+    std::memcpy(p, blob.data(), blob.size());
+    *image = p;
+    *len = blob.size();
+    return CG_OK;
+  } catch (const CedarError& e) {
+    c->err = e.what();
+    std::string m = e.what();
+    return (m.find("device") != std::string::npos || m.find("not supported") != std::string::npos) ? CG_E_COMPILE : CG_E_PARSE;
+  } catch (const std::exception& e) {
+    c->err = e.what();
+    return CG_E_ARG;
+  }
+}
+
+int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t* n_tiers, uint64_t* epoch) {
+  if (!image) return CG_E_ARG;
+  try {
+    auto img = Image::deserialize((const uint8_t*)image, len);
+    if (n_policies) *n_policies = img->n_pol();
+    if (n_tiers) *n_tiers = img->n_tiers();
+    if (epoch) *epoch = img->epoch;
+    return CG_OK;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+int cg_device_count(int* n) {
+  if (!n) return CG_E_ARG;
+  return dev_count(n) ? CG_E_DEVICE : CG_OK;
+}
+
+int cg_ctx_create(int device, cg_ctx** out) {
+  if (!out) return CG_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (dev_count(&n) || device < 0 || device >= n) return CG_E_DEVICE;
+  auto* c = new (std::nothrow) cg_ctx();
+  if (!c) return CG_E_ARG;
+  c->device = device;
+  if (dev_stream_create(device, &c->stream)) { delete c; return CG_E_DEVICE; }
+  *out = c;
+  return CG_OK;
+}
+
+void cg_ctx_destroy(cg_ctx* ctx) {
+  if (!ctx) return;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->active.reset();
+    ctx->images.clear();
+  }
+  dev_stream_destroy(ctx->stream);
+  delete ctx;
+}
+
+const char* cg_last_error(cg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch) {
+  if (!ctx || !image) return CG_E_ARG;
+  std::shared_ptr<Image> img;
+  try {
+    img = Image::deserialize((const uint8_t*)image, len);
+  } catch (const std::exception& e) {
+    ctx->err = e.what();
+    return CG_E_ARG;
+  }
+  img->epoch = epoch;
+  auto li = std::make_shared<LoadedImage>();
+  li->host = img;
+  if (dev_image_upload(ctx->device, *img, &li->dev)) { ctx->err = dev_last_error(); return CG_E_DEVICE; }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->images[epoch] = li;
+  return CG_OK;
+}
+
+int cg_image_activate(cg_ctx* ctx, uint64_t epoch) {
+  if (!ctx) return CG_E_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  auto it = ctx->images.find(epoch);
+  if (it == ctx->images.end()) { ctx->err = "no image loaded for epoch"; return CG_E_STATE; }
+  ctx->active = it->second;
+  return CG_OK;
+}
+
+int cg_image_active(cg_ctx* ctx, uint64_t* epoch) {
+  if (!ctx || !epoch) return CG_E_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ctx->active) return CG_E_STATE;
+  *epoch = ctx->active->host->epoch;
+  return CG_OK;
+}
+
+int cg_image_unload(cg_ctx* ctx, uint64_t epoch) {
+  if (!ctx) return CG_E_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->images.erase(epoch);  // shared_ptr: batches / active keep it alive
+  return CG_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+int cg_batch_create(cg_ctx* ctx, cg_batch** out) {
+  if (!ctx || !out) return CG_E_ARG;
+  std::shared_ptr<LoadedImage> img;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    img = ctx->active;
+  }
+  if (!img) { ctx->err = "no active image"; return CG_E_STATE; }
+  auto* b = new (std::nothrow) cg_batch();
+  if (!b) return CG_E_ARG;
+  b->ctx = ctx;
+  b->img = img;
+  b->host.img = img->host;
+  *out = b;
+  return CG_OK;
+}
+
+void cg_batch_destroy(cg_batch* b) { delete b; }
+
+int cg_batch_add_json(cg_batch* b, const char* json, size_t len) {
+  if (!b || !json) return CG_E_ARG;
+  if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
+  GUARD(b->err, {
+    JVal v = json_parse(json, len);
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    auto one = [&](const JVal& item) {
+      decode_json_item(item, ents, req);
+      b->items.push_back({(int32_t)b->host.n(), -1});
+      b->host.add(ents, req);
+    };
+    if (v.t == JVal::Arr) for (auto& item : v.arr) one(item);
+    else one(v);
+    return CG_OK;
+  })
+}
+
+int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len) {
+  if (!b || !json) return CG_E_ARG;
+  if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
+  GUARD(b->err, {
+    JVal v = json_parse(json, len);
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    auto one = [&](const JVal& sar) {
+      Attributes a = attributes_from_sar(sar);
+      std::string reason;
+      int fast = authorize_fast_path(a, reason);
+      if (fast >= 0) {
+        b->fast_reason[(uint32_t)b->items.size()] = reason;
+        b->items.push_back({-1, fast});
+        return;
+      }
+      record_to_cedar(a, ents, req);
+      b->items.push_back({(int32_t)b->host.n(), -1});
+      b->host.add(ents, req);
+    };
+    if (v.t == JVal::Arr) for (auto& s : v.arr) one(s);
+    else one(v);
+    return CG_OK;
+  })
+}
+
+int cg_sar_to_cedar_json(const char* sar_json, size_t len, char* out, size_t cap, size_t* need) {
+  if (!sar_json) return CG_E_ARG;
+  std::string s, err;
+  GUARD(err, {
+    JVal v = json_parse(sar_json, len);
+    Attributes a = attributes_from_sar(v);
+    std::string reason;
+    int fast = authorize_fast_path(a, reason);
+    if (fast >= 0) {
+      s = "{\"fast\":" + std::to_string(fast) + ",\"reason\":";
+      go_json_string(s, reason);
+      s += "}";
+    } else {
+      std::vector<EntityIn> ents;
+      RequestIn req;
+      record_to_cedar(a, ents, req);
+      auto uid = [&s](const std::pair<std::string, std::string>& u) {
+        s += "{\"type\":"; go_json_string(s, u.first); s += ",\"id\":"; go_json_string(s, u.second); s += "}";
+      };
+      s = "{\"entities\":[";
+      for (size_t k = 0; k < ents.size(); k++) {
+        if (k) s += ',';
+        s += "{\"uid\":";
+        uid({ents[k].type, ents[k].id});
+        s += ",\"attrs\":";
+        hval_to_json(ents[k].attrs, s);
+        s += ",\"parents\":[";
+        for (size_t p = 0; p < ents[k].parents.size(); p++) { if (p) s += ','; uid(ents[k].parents[p]); }
+        s += "]}";
+      }
+      s += "],\"request\":{\"principal\":";
+      uid(req.principal);
+      s += ",\"action\":";
+      uid(req.action);
+      s += ",\"resource\":";
+      uid(req.resource);
+      s += ",\"context\":";
+      hval_to_json(req.context, s);
+      s += "}}";
+    }
+  })
+  if (need) *need = s.size() + 1;
+  if (!out || cap < s.size() + 1) return CG_E_RANGE;
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  return CG_OK;
+}
+
+int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t cap, size_t* need) {
+  if (!b || !decision) return CG_E_ARG;
+  if (i >= b->items.size()) return CG_E_RANGE;
+  std::string r;
+  const auto& it = b->items[i];
+  if (it.dev < 0) {
+    *decision = it.fast;
+    r = b->fast_reason[i];
+  } else {
+    if (!b->done) return CG_E_STATE;
+    // authorizer.go:73-84 + diagnosticToReason (authorizer.go:113-124)
+    std::vector<uint32_t> rs;
+    b->host.reason_ids((uint32_t)it.dev, rs);
+    if (b->host.decision((uint32_t)it.dev)) {
+      *decision = AUTHZ_ALLOW;
+    } else if (!rs.empty()) {
+      *decision = AUTHZ_DENY;
+    } else {
+      *decision = AUTHZ_NO_OPINION;
+    }
+    if (*decision != AUTHZ_NO_OPINION && !rs.empty()) {
+      GUARD(b->err, { b->host.diagnostic_json((uint32_t)it.dev, r, false); })
+    }
+  }
+  if (need) *need = r.size() + 1;
+  if (!reason) return CG_OK;
+  if (cap < r.size() + 1) return CG_E_RANGE;
+  std::memcpy(reason, r.c_str(), r.size() + 1);
+  return CG_OK;
+}
+
+uint32_t cg_batch_size(cg_batch* b) { return b ? (uint32_t)b->items.size() : 0; }
+
+int cg_batch_submit(cg_batch* b) {
+  if (!b) return CG_E_ARG;
+  if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
+  b->host.finalize_strings();
+  if (b->host.n() == 0) { b->submitted = b->done = true; return CG_OK; }
+  if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  if (dev_eval(b->img->dev, b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  b->submitted = true;
+  return CG_OK;
+}
+
+int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
+  if (!b) return CG_E_ARG;
+  if (!b->submitted) { b->err = "batch not submitted"; return CG_E_STATE; }
+  if (b->done) return CG_OK;
+  (void)timeout_ns;  // stream sync is bounded by the kernel; the webhook deadline is enforced by the caller
+  if (dev_download(b->dev, b->host, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  // overflowed result lists: re-run just those requests with exact capacities
+  std::vector<uint32_t> idx;
+  uint32_t capr = 0, cape = 0;
+  for (uint32_t i = 0; i < b->host.n(); i++) {
+    uint32_t fl = b->host.res[2 * (size_t)i] >> 16;
+    if (!(fl & cgi::RF_VALID)) { b->err = "request left unevaluated"; return CG_E_DEVICE; }
+    if (fl & cgi::RF_OVERFLOW) {
+      idx.push_back(i);
+      capr = std::max(capr, b->host.res[2 * (size_t)i + 1] & 0xFFFF);
+      cape = std::max(cape, b->host.res[2 * (size_t)i + 1] >> 16);
+    }
+  }
+  if (!idx.empty()) {
+    capr = std::max(capr, 1u);
+    cape = std::max(cape, 1u);
+    std::vector<uint32_t> res, rf, rp, er;
+    if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, b->ctx->stream, res, rf, rp, er)) {
+      b->err = dev_last_error();
+      return CG_E_DEVICE;
+    }
+    for (size_t k = 0; k < idx.size(); k++) {
+      uint32_t i = idx[k];
+      uint32_t fl = res[2 * k] >> 16;
+      uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
+      const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
+      b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
+      b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
+    }
+  }
+  b->done = true;
+  return CG_OK;
+}
+
+int cg_batch_decision(cg_batch* b, uint32_t i, int* allow, uint32_t* tier) {
+  if (!b || !allow) return CG_E_ARG;
+  if (!b->done) return CG_E_STATE;
+  if (i >= b->items.size()) return CG_E_RANGE;
+  if (b->items[i].dev < 0) return CG_E_STATE;
+  i = (uint32_t)b->items[i].dev;
+  *allow = b->host.decision(i) ? 1 : 0;
+  if (tier) *tier = (b->host.res[2 * (size_t)i] >> 8) & 0xFF;
+  return CG_OK;
+}
+
+int cg_batch_diagnostic(cg_batch* b, uint32_t i, int reasons_only, char* buf, size_t cap, size_t* need) {
+  if (!b) return CG_E_ARG;
+  if (!b->done) return CG_E_STATE;
+  if (i >= b->items.size()) return CG_E_RANGE;
+  if (b->items[i].dev < 0) return CG_E_STATE;
+  i = (uint32_t)b->items[i].dev;
+  std::string s;
+  GUARD(b->err, { b->host.diagnostic_json(i, s, reasons_only != 0); })
+  if (need) *need = s.size() + 1;
+  if (!buf || cap < s.size() + 1) return CG_E_RANGE;
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return CG_OK;
+}
+
+int cg_batch_reasons(cg_batch* b, uint32_t i, uint32_t* idx, uint32_t cap, uint32_t* n, uint32_t* n_errors) {
+  if (!b || !n) return CG_E_ARG;
+  if (!b->done) return CG_E_STATE;
+  if (i >= b->items.size()) return CG_E_RANGE;
+  if (b->items[i].dev < 0) return CG_E_STATE;
+  i = (uint32_t)b->items[i].dev;
+  std::vector<uint32_t> rs, es;
+  b->host.reason_ids(i, rs);
+  b->host.error_recs(i, es);
+  *n = (uint32_t)rs.size();
+  if (n_errors) *n_errors = (uint32_t)(es.size() / cgi::ERR_WORDS);
+  if (idx) for (uint32_t k = 0; k < cap && k < rs.size(); k++) idx[k] = rs[k];
+  return rs.size() > cap && idx ? CG_E_RANGE : CG_OK;
+}
+
+int cg_batch_time(cg_batch* b, uint32_t iters, float* ms_total) {
+  if (!b || !ms_total) return CG_E_ARG;
+  if (!b->submitted) return CG_E_STATE;
+  if (dev_time_eval(b->img->dev, b->dev, iters, b->ctx->stream, ms_total)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  return CG_OK;
+}
+
+int cg_batch_bytes(cg_batch* b, uint64_t* batch_bytes, uint64_t* image_bytes, uint64_t* heap_bytes) {
+  if (!b) return CG_E_ARG;
+  if (batch_bytes) *batch_bytes = b->dev.bytes;
+  if (image_bytes) *image_bytes = b->img->dev.bytes;
+  if (heap_bytes) *heap_bytes = (uint64_t)b->host.heap.size() * 4;
+  return CG_OK;
+}
+
+int cg_is_authorized_json(cg_ctx* ctx, const char* item_json, size_t len, int* allow, char* diag, size_t cap, size_t* need) {
+  if (!ctx || !item_json || !allow) return CG_E_ARG;
+  cg_batch* b = nullptr;
+  int rc = cg_batch_create(ctx, &b);
+  if (rc) return rc;
+  rc = cg_batch_add_json(b, item_json, len);
+  if (!rc) rc = cg_batch_submit(b);
+  if (!rc) rc = cg_batch_wait(b, -1);
+  if (!rc) rc = cg_batch_decision(b, 0, allow, nullptr);
+  if (!rc && (diag || need)) rc = cg_batch_diagnostic(b, 0, 0, diag, cap, need);
+  if (rc) ctx->err = b->err;
+  cg_batch_destroy(b);
+  return rc;
+}
+
+}  // extern "C"

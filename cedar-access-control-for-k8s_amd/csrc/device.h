@@ -1,0 +1,51 @@
+// Device bridge (implemented in kernel.hip). Plain C++ declarations: no HIP types leak into the
+// host engine or the C-ABI.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace cg {
+
+struct Image;
+struct Batch;
+
+struct DevImage {
+  int device = -1;
+  uint32_t *pol = nullptr, *tier_end = nullptr, *code = nullptr, *cpool = nullptr, *gstr_off = nullptr, *hot = nullptr;
+  uint8_t* gstr_bytes = nullptr;
+  uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0;
+  size_t bytes = 0;
+};
+
+struct DevBatch {
+  int device = -1;
+  uint32_t *heap = nullptr, *req_base = nullptr, *req_idx = nullptr, *bstr_off = nullptr;
+  uint8_t* bstr_bytes = nullptr;
+  uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
+  uint32_t n = 0, capr = 0, cape = 0;
+  size_t heap_words = 0, bytes = 0;
+};
+
+// All functions return 0 on success, or a negative CG_E_* code with dev_last_error() set.
+const char* dev_last_error();
+int dev_count(int* n);
+int dev_select(int device);
+int dev_image_upload(int device, const Image& img, DevImage* out);
+void dev_image_free(DevImage* d);
+int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream);
+void dev_batch_free(DevBatch* d);
+// Evaluates every request of the batch into the batch's device result buffers (async on stream).
+int dev_eval(const DevImage& img, DevBatch& b, void* stream);
+// Re-evaluates the subset idx[0..n) with larger result capacities; synchronous, results on host.
+int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
+                    uint32_t cape, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
+                    std::vector<uint32_t>& rp, std::vector<uint32_t>& er);
+int dev_download(const DevBatch& b, Batch& host, void* stream);
+int dev_stream_create(int device, void** stream);
+void dev_stream_destroy(void* stream);
+int dev_stream_sync(void* stream);
+// bench support: times `iters` launches of the evaluation kernel on `stream` with HIP events
+int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_total);
+
+}  // namespace cg

@@ -1,0 +1,174 @@
+// Request encoder: (EntityMap, Request) -> one request block of the device heap.
+//
+// The reference builds a Go `cedartypes.EntityMap` + `cedar.Request` per webhook call
+// (internal/server/authorizer/authorizer.go:89-111, admission/handler.go:82-153) and hands them
+// to (*PolicySet).IsAuthorized (store/store.go:31). The encoder lays the same facts out flat:
+//   header (P/A/R UIDs, context, entity-table indices of P/A/R) | entity table | data
+// Strings are interned against the image's global table first (so policy constants and request
+// strings compare by ID), then batch-locally. Each entity row carries a pointer to its
+// transitive ancestor list (the closure of `parents` through the map), so `in` is a linear scan.
+#include <algorithm>
+#include <unordered_set>
+
+#include "engine.h"
+
+namespace cg {
+using namespace cgi;
+
+void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, Batch& b, uint32_t& w0, uint32_t& w1);
+
+uint32_t Batch::sid(const std::string& s) {
+  int32_t g = img->find(s);
+  if (g >= 0) return (uint32_t)g;
+  auto it = bsid.find(s);
+  if (it != bsid.end()) return it->second;
+  uint32_t id = img->n_gstr() + (uint32_t)bstrings.size();
+  bstrings.push_back(s);
+  bsid.emplace(s, id);
+  return id;
+}
+
+const std::string& Batch::str(uint32_t id) const {
+  static const std::string empty;
+  uint32_t ng = img->n_gstr();
+  if (id < ng) return img->strings[id];
+  if (id - ng < bstrings.size()) return bstrings[id - ng];
+  return empty;
+}
+
+namespace {
+struct PairHash {
+  size_t operator()(const std::pair<uint32_t, uint32_t>& p) const { return ((size_t)p.first << 32) ^ p.second; }
+};
+}  // namespace
+
+void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
+  std::vector<uint32_t> blk;
+  // entity table (EntityMap semantics: a repeated UID replaces the earlier entity)
+  std::vector<const EntityIn*> table;
+  std::unordered_map<std::pair<uint32_t, uint32_t>, uint32_t, PairHash> index;
+  std::vector<std::pair<uint32_t, uint32_t>> uids;
+  for (auto& e : ents) {
+    std::pair<uint32_t, uint32_t> u{sid(e.type), sid(e.id)};
+    auto it = index.find(u);
+    if (it != index.end()) { table[it->second] = &e; continue; }
+    index.emplace(u, (uint32_t)table.size());
+    table.push_back(&e);
+    uids.push_back(u);
+  }
+  const uint32_t n = (uint32_t)table.size();
+  blk.resize(RH_WORDS + (size_t)n * ENT_WORDS, 0);
+  auto uid_of = [this](const std::pair<std::string, std::string>& u) { return std::make_pair(sid(u.first), sid(u.second)); };
+  auto pu = uid_of(req.principal), au = uid_of(req.action), ru = uid_of(req.resource);
+  for (auto* u : {&pu, &au, &ru}) if (u->first > X_MASK) throw CedarError("string table overflow");
+  blk[RH_NENT] = n;
+  blk[RH_P] = mk_w0(T_ENT, pu.first); blk[RH_P + 1] = pu.second;
+  blk[RH_A] = mk_w0(T_ENT, au.first); blk[RH_A + 1] = au.second;
+  blk[RH_R] = mk_w0(T_ENT, ru.first); blk[RH_R + 1] = ru.second;
+  auto idx_of = [&](const std::pair<uint32_t, uint32_t>& u) { auto it = index.find(u); return it == index.end() ? NO_ENT : it->second; };
+  blk[RH_PIDX] = idx_of(pu);
+  blk[RH_AIDX] = idx_of(au);
+  blk[RH_RIDX] = idx_of(ru);
+  {
+    uint32_t w0, w1;
+    HVal ctx = req.context;
+    if (ctx.k != VK::Rec) { ctx = HVal(); ctx.k = VK::Rec; }
+    emit_heap_value(ctx, blk, *this, w0, w1);
+    blk[RH_CTX] = w0; blk[RH_CTX + 1] = w1;
+  }
+  // parent adjacency (ids of parents that exist in the map are followed; absent ones are leaves)
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> parents(n);
+  for (uint32_t i = 0; i < n; i++)
+    for (auto& p : table[i]->parents) {
+      auto u = uid_of(p);
+      if (std::find(parents[i].begin(), parents[i].end(), u) == parents[i].end()) parents[i].push_back(u);
+    }
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t* row = &blk[RH_WORDS + (size_t)i * ENT_WORDS];
+    row[ER_TYPE] = uids[i].first;
+    row[ER_ID] = uids[i].second;
+    uint32_t w0, w1;
+    HVal attrs = table[i]->attrs;
+    if (attrs.k != VK::Rec) { attrs = HVal(); attrs.k = VK::Rec; }
+    emit_heap_value(attrs, blk, *this, w0, w1);
+    row = &blk[RH_WORDS + (size_t)i * ENT_WORDS];  // blk may have reallocated
+    row[ER_ATTR0] = w0; row[ER_ATTR1] = w1;
+    // transitive ancestors (BFS through the map; cycles tolerated)
+    std::vector<std::pair<uint32_t, uint32_t>> anc;
+    std::unordered_set<std::pair<uint32_t, uint32_t>, PairHash> seen;
+    std::vector<uint32_t> stack{i};
+    while (!stack.empty()) {
+      uint32_t cur = stack.back();
+      stack.pop_back();
+      for (auto& p : parents[cur]) {
+        if (!seen.insert(p).second) continue;
+        anc.push_back(p);
+        auto it = index.find(p);
+        if (it != index.end()) stack.push_back(it->second);
+      }
+    }
+    std::sort(anc.begin(), anc.end());
+    uint32_t off = (uint32_t)blk.size();
+    blk.push_back((uint32_t)anc.size());
+    for (auto& a : anc) { blk.push_back(a.first); blk.push_back(a.second); }
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = mk_ref(SP_HEAP, off);
+  }
+  if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
+  if (heap.size() + blk.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
+  req_base.push_back((uint32_t)heap.size());
+  heap.insert(heap.end(), blk.begin(), blk.end());
+}
+
+void Batch::finalize_strings() {
+  bstr_off.clear();
+  bstr_bytes.clear();
+  for (auto& s : bstrings) {
+    bstr_off.push_back((uint32_t)bstr_bytes.size());
+    bstr_bytes.insert(bstr_bytes.end(), s.begin(), s.end());
+  }
+  bstr_off.push_back((uint32_t)bstr_bytes.size());
+  if (bstr_bytes.empty()) bstr_bytes.push_back(0);
+  if (heap.empty()) heap.push_back(0);
+}
+
+static std::pair<std::string, std::string> uid_from_json(const JVal& j) {
+  const JVal* u = j.get("__entity");
+  const JVal& x = u ? *u : j;
+  return {x.str_or("type"), x.str_or("id")};
+}
+
+void decode_json_item(const JVal& item, std::vector<EntityIn>& ents, RequestIn& req) {
+  const JVal* es = item.get("entities");
+  const JVal* rq = item.get("request");
+  if (!rq || rq->t != JVal::Obj) throw CedarError("item needs a \"request\" object");
+  ents.clear();
+  if (es) {
+    if (es->t != JVal::Arr) throw CedarError("\"entities\" must be an array");
+    for (auto& e : es->arr) {
+      EntityIn ei;
+      const JVal* uid = e.get("uid");
+      if (!uid) throw CedarError("entity without uid");
+      auto u = uid_from_json(*uid);
+      ei.type = u.first; ei.id = u.second;
+      const JVal* at = e.get("attrs");
+      if (at) ei.attrs = hval_from_json(*at);
+      else ei.attrs.k = VK::Rec;
+      if (ei.attrs.k != VK::Rec) throw CedarError("entity attrs must be an object");
+      const JVal* ps = e.get("parents");
+      if (ps) for (auto& p : ps->arr) ei.parents.push_back(uid_from_json(p));
+      ents.push_back(std::move(ei));
+    }
+  }
+  const JVal* p = rq->get("principal");
+  const JVal* a = rq->get("action");
+  const JVal* r = rq->get("resource");
+  if (!p || !a || !r) throw CedarError("request needs principal, action and resource");
+  req.principal = uid_from_json(*p);
+  req.action = uid_from_json(*a);
+  req.resource = uid_from_json(*r);
+  const JVal* c = rq->get("context");
+  if (c) req.context = hval_from_json(*c);
+  else { req.context = HVal(); req.context.k = VK::Rec; }
+}
+
+}  // namespace cg

@@ -1,0 +1,167 @@
+// Compiled policy image + request batch layout shared by the host compiler/encoder and the
+// gfx950 evaluation kernel. Plain integers only; included from both C++ and HIP.
+//
+// Layout in HBM (all u32 words unless noted)
+// ------------------------------------------
+// Image (replicated per GPU, read-only, uploaded once per policy epoch):
+//   pol[n_pol * POL_WORDS]   policy descriptors, in tier order (scope + code range + effect)
+//   tier_end[n_tiers]        exclusive end index of each tier in `pol`
+//   code[]                   condition bytecode, 2 words per instruction
+//   cpool[]                  constant pool (sets, records, patterns, scope action lists)
+//   gstr_off[n_gstr + 1]     byte offsets of the global (policy) string table
+//   gstr_bytes[]             string bytes
+// Batch (per submission):
+//   req_base[R]              word offset of request r's heap block in `heap`
+//   heap[]                   per-request blocks: header, entity table, attribute data
+//   bstr_off[n_bstr + 1], bstr_bytes[]  batch-local strings (ids >= n_gstr)
+//   res[R * 2], reasons_f/p[R * capr], errs[R * cape * ERR_WORDS]   results
+#pragma once
+#include <stdint.h>
+
+#if !defined(__HIPCC__) && !defined(__host__)
+#define __host__
+#define __device__
+#endif
+
+namespace cgi {
+
+// ---- value encoding (memory form: 2 words) --------------------------------------------------
+// w0 = tag << 28 | x (28 bits), w1 = y
+enum Tag : uint32_t {
+  T_NONE = 0,
+  T_BOOL = 1,    // y = 0/1
+  T_LONG = 2,    // memory: y = int32 value (sign-extended); register form: y = lo, z = hi
+  T_LONGREF = 3, // memory only: x = ref -> [lo, hi]
+  T_STR = 4,     // y = string id
+  T_ENT = 5,     // x = type string id, y = id string id
+  T_SET = 6,     // x = ref -> [n, (w0, w1) * n]
+  T_REC = 7,     // x = ref -> [n, (key, w0, w1) * n] sorted by key id
+  T_DEC = 8,     // x = ref -> [lo, hi]
+  T_IP = 9,      // x = ref -> [v6 | prefix << 8, a0, a1, a2, a3] (big-endian address bytes)
+};
+constexpr uint32_t TAG_SHIFT = 28;
+constexpr uint32_t X_MASK = 0x0FFFFFFFu;
+// refs: space (2 bits) | word offset (26 bits). Heap refs are relative to the request block.
+constexpr uint32_t SPACE_SHIFT = 26;
+constexpr uint32_t OFF_MASK = 0x03FFFFFFu;
+enum Space : uint32_t { SP_HEAP = 0, SP_CPOOL = 1, SP_LANE = 2 };
+
+__host__ __device__ constexpr inline uint32_t mk_w0(uint32_t tag, uint32_t x) { return (tag << TAG_SHIFT) | (x & X_MASK); }
+__host__ __device__ constexpr inline uint32_t mk_ref(uint32_t space, uint32_t off) { return (space << SPACE_SHIFT) | (off & OFF_MASK); }
+
+// ---- request block header -------------------------------------------------------------------
+enum ReqHdr : uint32_t {
+  RH_NENT = 0,
+  RH_P = 1,      // principal (ENT value, 2 words)
+  RH_A = 3,      // action
+  RH_R = 5,      // resource
+  RH_CTX = 7,    // context value (REC, 2 words)
+  RH_PIDX = 9,   // entity-table index of principal / action / resource (NO_ENT if absent)
+  RH_AIDX = 10,
+  RH_RIDX = 11,
+  RH_WORDS = 12, // entity table follows: n_ent * ENT_WORDS
+};
+enum EntRow : uint32_t { ER_TYPE = 0, ER_ID = 1, ER_ATTR0 = 2, ER_ATTR1 = 3, ER_ANC = 4, ER_PAD = 5, ENT_WORDS = 6 };
+constexpr uint32_t NO_ENT = 0xFFFFFFFFu;
+
+// ---- policy descriptor ----------------------------------------------------------------------
+enum ScopeK : uint32_t { SK_ANY = 0, SK_EQ = 1, SK_IN = 2, SK_IS = 3, SK_ISIN = 4, SK_INSET = 5 };
+enum PolW : uint32_t {
+  PW_FLAGS = 0,   // bit0 forbid, bits 8..15 tier
+  PW_KINDS = 1,   // p_kind | a_kind << 8 | r_kind << 16
+  PW_P_TYPE = 2,  // is-type (string id)
+  PW_P_ET = 3,    // entity type (string id)
+  PW_P_EI = 4,    // entity id (string id)
+  PW_A_ET = 5,    // eq/in: entity type; inset: count
+  PW_A_EI = 6,    // eq/in: entity id;   inset: cpool offset of (type, id) pairs
+  PW_R_TYPE = 7,
+  PW_R_ET = 8,
+  PW_R_EI = 9,
+  PW_CODE = 10,   // code word offset
+  PW_CODE_N = 11, // code words
+  PW_SLOTS = 12,  // max register slot used + 1
+  PW_LANE = 13,   // lane-scratch words needed
+  PW_R0 = 14,
+  PW_R1 = 15,
+  POL_WORDS = 16,
+};
+
+// ---- bytecode -------------------------------------------------------------------------------
+// word0 = op | d << 8 | a << 14 | b << 20 | c << 26 (6-bit slot fields); word1 = imm
+constexpr uint32_t NSLOT = 16;
+constexpr uint32_t LANE_WORDS = 192;   // per-lane scratch for runtime-built sets/records
+constexpr uint32_t VAL_DEPTH = 8;      // max nesting for deep equality on device
+enum Op : uint32_t {
+  OP_NOP = 0,
+  OP_LDV,       // d = var[imm]  (0 principal, 1 action, 2 resource, 3 context)
+  OP_LDC,       // d = value at cpool[imm] (2 words)
+  OP_LDB,       // d = bool imm
+  OP_LDS,       // d = string id imm
+  OP_ATTR,      // d = a.key(imm)
+  OP_HAS,       // d = a has key(imm)
+  OP_EQ,        // d = a == b
+  OP_NE,
+  OP_LT, OP_LE, OP_GT, OP_GE,
+  OP_ADD, OP_SUB, OP_MUL,
+  OP_NEG,       // d = -a
+  OP_NOT,       // d = !a (type-checked)
+  OP_CHKB,      // error unless a is bool
+  OP_JF,        // if a is false -> jump imm (a must be bool)
+  OP_JT,        // if a is true  -> jump imm
+  OP_JNF,       // if-then-else: if a is false jump imm (a must be bool); true falls through
+  OP_JMP,       // jump imm
+  OP_IN,        // d = a in b
+  OP_IS,        // d = a is type(imm)
+  OP_LIKE,      // d = a like pattern(cpool imm)
+  OP_CONTAINS,  // d = a.contains(b)
+  OP_CALL,      // d = a.containsAll(b) / containsAny(b) / isEmpty / ext methods; sub-op in c
+  OP_SETNEW,    // d = new lane set with capacity imm
+  OP_SETPUT,    // set d [index c] = a
+  OP_RECNEW,    // d = new lane record with n=imm (keys from cpool list in next SETPUT-like ops)
+  OP_RECPUT,    // rec d field c := (key imm, value a)
+  OP_COND,      // end of a when/unless clause: a must be bool; c = 1 for `unless`
+  OP_ERR,       // raise error: c = code, imm = aux (compile-time detected runtime error)
+  OP_HOT,       // d = hot attribute slot c (pre-resolved var.attr), errors like OP_ATTR
+  OP_HOTHAS,    // d = hot attribute slot c present
+  OP_COUNT
+};
+constexpr uint32_t NHOT = 8;  // pre-resolved (var, attribute) pairs per image
+// OP_CALL sub-ops
+enum CallOp : uint32_t {
+  CO_CONTAINS_ALL = 0, CO_CONTAINS_ANY, CO_IS_EMPTY,
+  CO_DEC_LT, CO_DEC_LE, CO_DEC_GT, CO_DEC_GE,
+  CO_IP_V4, CO_IP_V6, CO_IP_LOOPBACK, CO_IP_MULTICAST, CO_IP_IN_RANGE,
+};
+
+__host__ __device__ constexpr inline uint32_t mk_ins(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
+  return op | (d << 8) | (a << 14) | (b << 20) | (c << 26);
+}
+
+// ---- results --------------------------------------------------------------------------------
+enum Decision : uint32_t { DEC_DENY = 0, DEC_ALLOW = 1 };
+// res[2r]   = decision | tier << 8 | flags << 16
+// res[2r+1] = n_reasons | n_errors << 16
+enum ResFlags : uint32_t { RF_FORBID = 1, RF_OVERFLOW = 2, RF_VALID = 4 };
+// error record: policy, code | aux << 8, k (string id), et (string id), ei (string id), pad
+constexpr uint32_t ERR_WORDS = 6;
+enum ErrCode : uint32_t {
+  E_NONE = 0,
+  E_TYPE = 1,            // aux = expected | got << 8 (TypeName codes below)
+  E_ENTITY_MISSING = 2,  // et/ei = entity
+  E_ATTR_ENTITY = 3,     // k = attribute, et/ei = entity
+  E_ATTR_RECORD = 4,     // k = attribute
+  E_OVERFLOW = 5,
+  E_EXT = 6,             // aux = message index in image (compile-time message)
+  E_DEPTH = 7,           // value nesting beyond VAL_DEPTH (device limit)
+  E_LANE = 8,            // lane scratch exhausted (device limit)
+};
+enum TypeName : uint32_t {
+  TN_BOOL = 0, TN_LONG, TN_STRING, TN_ENTITY, TN_SET, TN_RECORD, TN_DECIMAL, TN_IP,
+  TN_ENTITY_OR_RECORD, TN_SET_OR_ENTITY, TN_UNKNOWN,
+};
+
+// ---- image blob header (host serialization) ----------------------------------------------
+constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
+constexpr uint32_t IMG_VERSION = 1;
+
+}  // namespace cgi

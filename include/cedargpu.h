@@ -1,0 +1,124 @@
+/* cedargpu — MI355X-native Cedar authorization for the cedar-access-control-for-k8s webhooks.
+ *
+ * C-ABI boundary (plain pointers and sizes; no C++ or HIP types cross it). It replaces, behind the
+ * reference's own store interface, the per-request evaluation the reference performs with
+ * cedar-go v1.1.0:
+ *
+ *   internal/server/store/store.go:9-15   PolicyStore.PolicySet() *cedar.PolicySet
+ *   internal/server/store/store.go:25-42  TieredPolicyStores.IsAuthorized(EntityMap, Request)
+ *                                         -> (cedar.Decision, cedar.Diagnostic)
+ *   internal/server/store/store.go:31     (*cedar.PolicySet).IsAuthorized  (the hot path)
+ *   internal/server/store/memory.go:18    cedar.NewPolicySetFromBytes       (IDs policy<i>)
+ *   internal/server/store/directory.go:69 cedar.NewPolicyListFromBytes      (IDs <file>.policy<i>)
+ *   internal/server/store/crd.go:51,60    per-CRD lists                     (IDs <name><i>-<uid>)
+ *   internal/server/store/verified_permissions.go:89,95                     (IDs <id>.<i>)
+ *   cmd/cedar-webhook/main.go:111-116     static allow-all-admission store
+ *
+ * Every call returns 0 (CG_OK) or a negative CG_E_* status; no exception crosses the boundary.
+ * Strings in/out are UTF-8. See INTEGRATION.md for the cgo binding a maintainer would add.
+ */
+#ifndef CEDARGPU_H
+#define CEDARGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CG_OK 0
+#define CG_E_ARG (-1)      /* bad argument / malformed JSON */
+#define CG_E_PARSE (-2)    /* Cedar syntax error (cedar.NewPolicySetFromBytes would fail) */
+#define CG_E_COMPILE (-3)  /* valid Cedar the device compiler cannot lower */
+#define CG_E_STATE (-4)    /* call out of order (no active image, batch not submitted, ...) */
+#define CG_E_DEVICE (-5)   /* HIP runtime / kernel failure (callers fail safe: authz NoOpinion, admission allow) */
+#define CG_E_TIMEOUT (-6)
+#define CG_E_RANGE (-7)    /* index out of range / buffer too small (see *need) */
+
+typedef struct cg_compiler cg_compiler;
+typedef struct cg_ctx cg_ctx;
+typedef struct cg_batch cg_batch;
+
+const char* cg_version(void);
+void cg_free(void* p);
+
+/* ---- compiler: policy documents -> serialized, versioned image (host only; no GPU needed) ---- */
+int cg_compiler_create(cg_compiler** out);
+void cg_compiler_destroy(cg_compiler* c);
+const char* cg_compiler_last_error(cg_compiler* c);
+/* Starts the next tier (one TieredPolicyStores element, store.go:20). */
+int cg_compiler_add_tier(cg_compiler* c);
+/* Adds every policy of a Cedar document to the current tier with IDs id_prefix + i + id_suffix:
+ * memory store: ("policy", ""), directory: ("<file>.policy", ""), CRD: ("<name>", "-<uid>"),
+ * AVP: ("<id>.", ""). `filename` becomes Position.filename. */
+int cg_compiler_add_document(cg_compiler* c, const char* filename, const char* text, size_t len,
+                             const char* id_prefix, const char* id_suffix);
+/* Adds exactly one policy with an explicit ID. zero_position=1 reproduces policies built from an
+ * AST (cedar.NewPolicyFromAST, e.g. allow-all-admission) whose Position is the zero value. */
+int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* filename, const char* text,
+                           size_t len, int zero_position);
+/* Compiles all tiers into an image blob (free with cg_free). */
+int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len);
+/* Number of policies / tiers of a built image blob. */
+int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t* n_tiers, uint64_t* epoch);
+
+/* ---- device context (one per GPU; requests shard across contexts, images are replicated) ---- */
+int cg_device_count(int* n);
+int cg_ctx_create(int device, cg_ctx** out);
+void cg_ctx_destroy(cg_ctx* ctx);
+const char* cg_last_error(cg_ctx* ctx);
+/* Copies and uploads an image; the caller keeps ownership of `image`. Not active until activated. */
+int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch);
+/* Atomically makes `epoch` the image new batches bind to; in-flight batches keep theirs. */
+int cg_image_activate(cg_ctx* ctx, uint64_t epoch);
+int cg_image_active(cg_ctx* ctx, uint64_t* epoch);
+/* Drops a loaded image (no-op while batches still reference it; freed when the last one goes). */
+int cg_image_unload(cg_ctx* ctx, uint64_t epoch);
+
+/* ---- batches of (EntityMap, Request) ---- */
+/* Creates a batch bound to the currently active image. */
+int cg_batch_create(cg_ctx* ctx, cg_batch** out);
+void cg_batch_destroy(cg_batch* b);
+/* Appends requests: one JSON object {"entities":[<cedar entity json>...],"request":{"principal":
+ * {"type","id"},"action":{...},"resource":{...},"context":{...}}} or a JSON array of them. */
+int cg_batch_add_json(cg_batch* b, const char* json, size_t len);
+uint32_t cg_batch_size(cg_batch* b);
+/* Encodes strings, uploads the batch to the device and launches evaluation (asynchronous). */
+int cg_batch_submit(cg_batch* b);
+/* Waits for completion (timeout_ns < 0: forever), downloads results, re-runs overflowed requests. */
+int cg_batch_wait(cg_batch* b, int64_t timeout_ns);
+/* cedar.Decision for request i: *allow = 1 (Allow) / 0 (Deny); *tier = deciding tier index. */
+int cg_batch_decision(cg_batch* b, uint32_t i, int* allow, uint32_t* tier);
+/* json.Marshal(cedar.Diagnostic) (reasons_only=0) or json.Marshal(diagnostic.Reasons) (=1).
+ * Writes at most cap bytes incl. NUL; *need = required size incl. NUL. */
+int cg_batch_diagnostic(cg_batch* b, uint32_t i, int reasons_only, char* buf, size_t cap, size_t* need);
+/* Determining-policy indices (image order) and error count for request i. */
+int cg_batch_reasons(cg_batch* b, uint32_t i, uint32_t* idx, uint32_t cap, uint32_t* n, uint32_t* n_errors);
+/* Re-launches evaluation of the resident batch `iters` times; device time via HIP events. */
+int cg_batch_time(cg_batch* b, uint32_t iters, float* ms_total);
+/* Device bytes of the batch (heap + results) and of its image. */
+int cg_batch_bytes(cg_batch* b, uint64_t* batch_bytes, uint64_t* image_bytes, uint64_t* heap_bytes);
+
+/* ---- authorization webhook path (SubjectAccessReview in, authorizer.Decision + reason out) ----
+ * Appends SubjectAccessReview JSON objects (one or an array) as the reference's /v1/authorize
+ * handler receives them (server.go:104). Applies GetAuthorizerAttributes (server.go:163-214), the
+ * Authorize fast paths (authorizer.go:38-57: self-allow, `system:` bypass) and RecordToCedarResource
+ * (authorizer.go:89-111); fast-path items are decided on the host and never reach the GPU.
+ * Store readiness (authorizer.go:58-66) is the caller's check, done before this call. */
+int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len);
+/* Host-only: the (EntityMap, Request) the SAR path builds, as {"fast":d,"reason":r} for a fast-path
+ * item or {"entities":[...],"request":{...}} (Cedar JSON) — for parity tests of the encoder. */
+int cg_sar_to_cedar_json(const char* sar_json, size_t len, char* out, size_t cap, size_t* need);
+/* authorizer.Decision for item i (0 Deny, 1 Allow, 2 NoOpinion) and the reason string the
+ * reference returns (diagnosticToReason JSON, a fast-path literal, or ""). */
+int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t cap, size_t* need);
+
+/* ---- single-request drop-in: TieredPolicyStores.IsAuthorized(EntityMap, Request) ---- */
+int cg_is_authorized_json(cg_ctx* ctx, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
+                          size_t* need);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CEDARGPU_H */

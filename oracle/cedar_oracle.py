@@ -208,8 +208,9 @@ def go_json_string(s: str) -> str:
 
 
 def go_quote(s: str) -> str:
-    """strconv.Quote-ish rendering used in messages (ASCII-safe)."""
-    return json.dumps(s)
+    """Entity-ID quoting used in error messages (escapes only backslash and double quote).
+    Error message text is not pinned by any reference test (parity unpinned)."""
+    return '"' + s.replace("\\", "\\\\").replace('"', '\\"') + '"'
 
 
 # ----------------------------------------------------------------------------------------------

@@ -14,6 +14,7 @@ Restates (file:line in /root/reference):
 from __future__ import annotations
 
 import ipaddress
+import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -234,11 +235,30 @@ def attributes_from_sar(sar: dict) -> Attributes:
         a.name = ra.get("name", "")
         a.resource_request = True
         fs = (ra.get("fieldSelector") or {}).get("requirements")
-        if fs:
-            a.field_selector = [FieldRequirement(r["key"], _sel_op(r["operator"]), (r.get("values") or [""])[0]) for r in fs]
+        if fs:  # fieldSelectorAsSelector (server.go:262-300): invalid requirements are dropped
+            for r in fs:
+                vals = list(r.get("values") or [])
+                if len(vals) > 1:
+                    continue
+                if r.get("operator") == "In" and len(vals) == 1:
+                    a.field_selector.append(FieldRequirement(r.get("key", ""), "=", vals[0]))
+                elif r.get("operator") == "NotIn" and len(vals) == 1:
+                    a.field_selector.append(FieldRequirement(r.get("key", ""), "!=", vals[0]))
         ls = (ra.get("labelSelector") or {}).get("requirements")
-        if ls:
-            a.label_selector = [LabelRequirement(r["key"], _sel_op(r["operator"]), list(r.get("values") or [])) for r in ls]
+        if ls:  # labelSelectorAsSelector (server.go:228-260) + labels.NewRequirement validation
+            for r in ls:
+                op = _sel_op(r.get("operator", ""))
+                key = r.get("key", "")
+                vals = list(r.get("values") or [])
+                if op not in ("in", "notin", "exists", "!") or not _valid_label_key(key):
+                    continue
+                if op in ("in", "notin") and not vals:
+                    continue
+                if op in ("exists", "!") and vals:
+                    continue
+                if not all(_valid_label_value(v) for v in vals):
+                    continue
+                a.label_selector.append(LabelRequirement(key, op, vals))
     nra = spec.get("nonResourceAttributes")
     if nra is not None:
         a.path = nra.get("path", "")
@@ -249,7 +269,28 @@ def attributes_from_sar(sar: dict) -> Attributes:
 
 def _sel_op(op: str) -> str:
     # metav1 LabelSelectorOperator -> selection.Operator strings
-    return {"In": "in", "NotIn": "notin", "Exists": "exists", "DoesNotExist": "!"}.get(op, op)
+    return {"In": "in", "NotIn": "notin", "Exists": "exists", "DoesNotExist": "!"}.get(op, "?")
+
+
+_NAME63 = re.compile(r"^[A-Za-z0-9]([-A-Za-z0-9_.]*[A-Za-z0-9])?$")
+_DNS_LABEL = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?$")
+
+
+def _valid_label_value(v: str) -> bool:
+    return v == "" or (len(v) <= 63 and bool(_NAME63.match(v)))
+
+
+def _valid_label_key(k: str) -> bool:
+    """k8s.io/apimachinery IsQualifiedName."""
+    parts = k.split("/")
+    if len(parts) == 1:
+        return len(k) <= 63 and bool(_NAME63.match(k))
+    if len(parts) != 2:
+        return False
+    prefix, name = parts
+    if not prefix or len(prefix) > 253 or not all(_DNS_LABEL.match(x) and len(x) <= 63 for x in prefix.split(".")):
+        return False
+    return len(name) <= 63 and bool(_NAME63.match(name))
 
 
 # ---------------------------------------------------------------------------------------------

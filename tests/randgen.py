@@ -1,0 +1,176 @@
+"""Seeded random Cedar policies + entity maps for differential testing (GPU vs oracle).
+
+Covers every operator the device evaluates: attribute access on entities/records (present,
+missing, absent entity), has, ==/!= (incl. deep set/record equality), </<=/>/>=, +,-,* with
+overflow, unary -, !, &&/|| short-circuit incl. type errors, if-then-else, in (entity / set /
+hierarchy), is / is-in, like (wildcards, escaped star), contains/containsAll/containsAny/isEmpty,
+runtime-built sets/records, decimal and ip methods, unless, multiple when clauses, context."""
+import json
+import random
+
+USERS = [f"u{i}" for i in range(6)]
+GROUPS = [f"g{i}" for i in range(6)]
+TAGS = ["t0", "t1", "t2", "t3", "prod-x", "x*y"]
+# Cedar pattern literals as they appear in policy text ("x\*y" matches the literal star)
+PATTERNS = ['"u*"', '"*1"', '"u*1"', '"*"', '"prod-*"', '"x\\*y"', '"*-*"', '"u0"', '""', '"n*s*1"', '"**"', '"t*t"']
+
+
+def q(s):
+    return json.dumps(s)
+
+
+class Gen:
+    def __init__(self, seed):
+        self.r = random.Random(seed)
+
+    def pick(self, xs):
+        return self.r.choice(xs)
+
+    def long_e(self, d=0):
+        r = self.r
+        opts = [lambda: str(r.randint(-5, 50)), lambda: "principal.age", lambda: "context.x", lambda: "resource.size",
+                lambda: "principal.info.a", lambda: "9223372036854775807", lambda: "-9223372036854775808"]
+        if d < 2:
+            opts += [lambda: f"({self.long_e(d + 1)} {r.choice(['+', '-', '*'])} {self.long_e(d + 1)})",
+                     lambda: f"-{self.long_e(d + 1)}",
+                     lambda: f"(if {self.bool_e(d + 1)} then {self.long_e(d + 1)} else {self.long_e(d + 1)})"]
+        return r.choice(opts)()
+
+    def str_e(self, d=0):
+        r = self.r
+        return r.choice([lambda: q(r.choice(USERS + TAGS + ["", "ns1"])), lambda: "principal.name",
+                         lambda: "resource.name", lambda: "resource.namespace", lambda: "principal.info.b",
+                         lambda: "context.s"])()
+
+    def ent_e(self, d=0):
+        r = self.r
+        return r.choice([lambda: "principal", lambda: "resource", lambda: "resource.owner", lambda: "action",
+                         lambda: f'k8s::Group::{q(r.choice(GROUPS))}', lambda: f'k8s::User::{q(r.choice(USERS))}'])()
+
+    def set_e(self, d=0):
+        r = self.r
+        return r.choice([lambda: "principal.tags", lambda: "resource.labels", lambda: "context.list",
+                         lambda: "[" + ", ".join(q(x) for x in r.sample(TAGS, r.randint(0, 3))) + "]",
+                         lambda: f"[{self.str_e(d + 1)}, {q(r.choice(TAGS))}]",
+                         lambda: f"[{self.long_e(d + 1)}, 3]",
+                         lambda: "[" + ", ".join(f"k8s::Group::{q(g)}" for g in r.sample(GROUPS, 2)) + "]",
+                         lambda: f'[{{"key": {q(r.choice(["k0", "k1"]))}, "value": {self.str_e(d + 1)}}}]',
+                         lambda: "principal.info.c"])()
+
+    def any_e(self, d=0):
+        return "(" + self.r.choice([self.long_e, self.str_e, self.ent_e, self.set_e, self.bool_e])(d + 1) + ")"
+
+    def bool_e(self, d=0):
+        r = self.r
+        leaves = [
+            lambda: "principal.active", lambda: "context.flag", lambda: r.choice(["true", "false"]),
+            lambda: f"{r.choice(['principal', 'resource', 'context', 'principal.info'])} has {r.choice(['name', 'namespace', 'age', 'tags', 'a', 'x', 'info', 'owner'])}",
+            lambda: f"{self.ent_e(d)} in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: f"{self.ent_e(d)} in {self.set_e(d)}",
+            lambda: f"{self.ent_e(d)} is {r.choice(['k8s::User', 'k8s::Group', 'k8s::Resource'])}",
+            lambda: f"principal is k8s::User in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: f"{self.long_e(d)} {r.choice(['<', '<=', '>', '>='])} {self.long_e(d)}",
+            lambda: f"{self.str_e(d)} {r.choice(['==', '!='])} {self.str_e(d)}",
+            lambda: f"{self.any_e(d)} {r.choice(['==', '!='])} {self.any_e(d)}",
+            lambda: f"{self.set_e(d)} == {self.set_e(d)}",
+            lambda: f"{self.str_e(d)} like {r.choice(PATTERNS)}",
+            lambda: f"{self.set_e(d)}.contains({self.any_e(d)})",
+            lambda: f"{self.set_e(d)}.{r.choice(['containsAll', 'containsAny'])}({self.set_e(d)})",
+            lambda: f"{self.set_e(d)}.isEmpty()",
+            lambda: f'resource.ip.{r.choice(["isIpv4", "isIpv6", "isLoopback", "isMulticast"])}()',
+            lambda: f'resource.ip.isInRange(ip({q(r.choice(["10.0.0.0/8", "127.0.0.0/8", "::1/128", "192.168.1.0/24"]))}))',
+            lambda: f'resource.score.{r.choice(["lessThan", "lessThanOrEqual", "greaterThan", "greaterThanOrEqual"])}(decimal({q(r.choice(["1.5", "-2.25", "0.0001"]))}))',
+            lambda: f'resource.labels.contains({{"key": {q(r.choice(["k0", "k1"]))}, "value": {self.str_e(d)}}})',
+            lambda: f'{self.any_e(d)}',  # possibly non-bool -> type errors
+        ]
+        if d < 3:
+            leaves += [lambda: f"({self.bool_e(d + 1)} && {self.bool_e(d + 1)})",
+                       lambda: f"({self.bool_e(d + 1)} || {self.bool_e(d + 1)})",
+                       lambda: f"!{self.bool_e(d + 1)}",
+                       lambda: f"(if {self.bool_e(d + 1)} then {self.bool_e(d + 1)} else {self.bool_e(d + 1)})"]
+        return r.choice(leaves)()
+
+    def scope(self, var):
+        r = self.r
+        t = r.random()
+        if t < 0.4:
+            return var
+        if var == "action":
+            if t < 0.7:
+                return "action in [" + ", ".join(f"k8s::Action::{q(v)}" for v in r.sample(["get", "list", "watch", "create"], 2)) + "]"
+            return f'action == k8s::Action::{q(r.choice(["get", "list"]))}'
+        if t < 0.55:
+            return f"{var} is {r.choice(['k8s::User', 'k8s::Resource', 'k8s::Group'])}"
+        if t < 0.7:
+            return f"{var} in k8s::Group::{q(r.choice(GROUPS))}"
+        if t < 0.85:
+            return f"{var} is k8s::User in k8s::Group::{q(r.choice(GROUPS))}"
+        if var == "principal":
+            return f"principal == k8s::User::{q(r.choice(USERS))}"
+        return f"resource == k8s::Resource::{q('r' + str(r.randint(0, 3)))}"
+
+    def policy(self):
+        r = self.r
+        eff = "forbid" if r.random() < 0.3 else "permit"
+        conds = []
+        for _ in range(r.choice([0, 1, 1, 2, 3])):
+            conds.append(f"{r.choice(['when', 'when', 'unless'])} {{ {self.bool_e()} }}")
+        ann = "@id(\"x\")\n" if r.random() < 0.2 else ""
+        return f"{ann}{eff} ({self.scope('principal')}, {self.scope('action')}, {self.scope('resource')})\n" + "\n".join(conds) + ";"
+
+    def policies(self, n):
+        return "\n".join(self.policy() for _ in range(n))
+
+    def value_attrs_user(self):
+        r = self.r
+        a = {"name": r.choice(USERS)}
+        if r.random() < 0.85:
+            a["age"] = r.choice([r.randint(0, 60), 2 ** 40, -(2 ** 35)])
+        if r.random() < 0.8:
+            a["tags"] = r.sample(TAGS, r.randint(0, 4))
+        if r.random() < 0.8:
+            info = {"a": r.randint(-3, 9), "b": r.choice(TAGS)}
+            if r.random() < 0.7:
+                info["c"] = r.sample(TAGS, r.randint(0, 3))
+            a["info"] = info
+        if r.random() < 0.8:
+            a["active"] = r.random() < 0.5
+        return a
+
+    def item(self):
+        r = self.r
+        ents = []
+        groups = r.sample(GROUPS, r.randint(0, 3))
+        puid = {"type": "k8s::User", "id": r.choice(USERS)}
+        ents.append({"uid": puid, "attrs": self.value_attrs_user(), "parents": [{"type": "k8s::Group", "id": g} for g in groups]})
+        # group hierarchy g_i -> g_{i+1}
+        for g in GROUPS:
+            if r.random() < 0.7:
+                i = int(g[1:])
+                par = [{"type": "k8s::Group", "id": f"g{i + 1}"}] if i + 1 < len(GROUPS) and r.random() < 0.6 else []
+                ents.append({"uid": {"type": "k8s::Group", "id": g}, "attrs": {"name": g}, "parents": par})
+        ruid = {"type": "k8s::Resource", "id": f"r{r.randint(0, 3)}"}
+        ra = {"name": r.choice(TAGS + USERS), "size": r.randint(-10, 100)}
+        if r.random() < 0.6:
+            ra["namespace"] = r.choice(["ns1", "ns2", "u0"])
+        if r.random() < 0.7:
+            ra["owner"] = {"__entity": {"type": "k8s::User", "id": r.choice(USERS)}}
+        if r.random() < 0.7:
+            ra["labels"] = [{"key": r.choice(["k0", "k1"]), "value": r.choice(USERS + TAGS)} for _ in range(r.randint(0, 3))]
+        if r.random() < 0.7:
+            ra["ip"] = {"__extn": {"fn": "ip", "arg": r.choice(["10.1.2.3", "127.0.0.1", "::1", "192.168.1.7/24", "224.0.0.1", "ff02::1"])}}
+        if r.random() < 0.7:
+            ra["score"] = {"__extn": {"fn": "decimal", "arg": r.choice(["1.5", "-3.0", "0.0001", "12.3456"])}}
+        if r.random() < 0.9:
+            ents.append({"uid": ruid, "attrs": ra, "parents": [{"type": "k8s::Group", "id": r.choice(GROUPS)}] if r.random() < 0.3 else []})
+        act = {"type": "k8s::Action", "id": r.choice(["get", "list", "watch", "create"])}
+        ctx = {}
+        if r.random() < 0.8:
+            ctx["x"] = r.randint(-5, 50)
+        if r.random() < 0.8:
+            ctx["flag"] = r.random() < 0.5
+        if r.random() < 0.6:
+            ctx["list"] = [r.randint(0, 5) for _ in range(r.randint(0, 3))]
+        if r.random() < 0.5:
+            ctx["s"] = r.choice(USERS)
+        return ents, {"principal": puid, "action": act, "resource": ruid, "context": ctx}

@@ -1,0 +1,98 @@
+"""CPU-only checks of the native library: it loads, exports every declared symbol, compiles the
+reference corpus, and its C++ SubjectAccessReview model matches the reference vectors / oracle."""
+import json
+import os
+import re
+
+import pytest
+
+import cedar_oracle as co
+import k8s_model as km
+from conftest import GOLDEN, ROOT
+from helpers import attrs_from, cxx_sar_to_cedar, norm_entities, sar_from_attrs
+
+import cedargpu
+from cedargpu import synth
+
+V = json.load(open(os.path.join(GOLDEN, "reference_vectors.json")))
+CORPUS = json.load(open(os.path.join(GOLDEN, "reference_corpus.json")))
+
+
+def test_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "cedargpu.h")).read()
+    declared = set(re.findall(r"\b(cg_[a-z_0-9]+)\s*\(", hdr))
+    assert len(declared) >= 30
+    for name in declared:
+        assert hasattr(cedargpu.lib, name), name
+    assert declared == set(cedargpu._lib.EXPORTED)
+
+
+def test_version():
+    assert b"gfx950" in cedargpu.lib.cg_version()
+
+
+@pytest.mark.parametrize("name", sorted(CORPUS["converter"]) + sorted(CORPUS["demo"]))
+def test_corpus_compiles(name):
+    src = CORPUS["converter"].get(name) or CORPUS["demo"][name]
+    img = cedargpu.build_image([cedargpu.MemoryStore(name, src)])
+    import ctypes
+    n, t, e = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+    assert cedargpu.lib.cg_image_info(img, len(img), ctypes.byref(n), ctypes.byref(t), ctypes.byref(e)) == 0
+    assert n.value == len(co.parse_policies(src, name))
+    assert t.value == 1
+
+
+def test_parse_error_is_reported():
+    with pytest.raises(cedargpu.CompileError):
+        cedargpu.build_image([cedargpu.MemoryStore("bad", "permit(principal, action, resource) when { 1 + };")])
+    with pytest.raises(cedargpu.CompileError):
+        cedargpu.build_image([cedargpu.MemoryStore("bad", "allow(principal, action, resource);")])
+
+
+def test_tiers_and_id_conventions_compile():
+    stores = [cedargpu.DirectoryStore({"a.cedar": "permit(principal, action, resource);", "skip.txt": "x"}),
+              cedargpu.CRDStore([("pol", "u-1", "forbid(principal, action, resource);")]),
+              cedargpu.AVPStore([("avp1", "permit(principal, action, resource);")]),
+              cedargpu.ALLOW_ALL_ADMISSION]
+    img = cedargpu.build_image(stores)
+    import ctypes
+    n, t = ctypes.c_uint32(), ctypes.c_uint32()
+    cedargpu.lib.cg_image_info(img, len(img), ctypes.byref(n), ctypes.byref(t), None)
+    assert (n.value, t.value) == (4, 4)
+
+
+@pytest.mark.parametrize("case", [c for c in V["record_to_cedar"] if not c["attributes"].get("label_selector")],
+                         ids=lambda c: c["name"])
+def test_cxx_sar_model_matches_reference_vectors(case):
+    """C++ RecordToCedarResource == authorizer_test.go:31-460 (selector-free cases: those
+    selectors use operator "=", which a SubjectAccessReview cannot express)."""
+    got = cxx_sar_to_cedar(sar_from_attrs(case["attributes"]))
+    assert norm_entities(got["entities"]) == norm_entities(case["want_entities"])
+    assert got["request"] == case["want_request"]
+
+
+def test_cxx_sar_model_matches_oracle_on_synthetic_sars():
+    sars = synth.random_sars(3000, seed=5, pop=synth.Population(seed=3, n_users=2000, n_groups=300))
+    sars.append(synth.make_sar("a", "u", ["g"], "list", ns="d", resource="pods", version="v1", label_selector=[
+        {"key": "owner", "operator": "In", "values": ["a", "b"]}, {"key": "bad key", "operator": "In", "values": ["x"]},
+        {"key": "e", "operator": "Exists"}, {"key": "x", "operator": "Exists", "values": ["v"]}]))
+    sars.append({"spec": {"user": "u", "uid": "1", "resourceAttributes": {"verb": "list", "resource": "pods", "version": "v1",
+                 "fieldSelector": {"requirements": [{"key": "a", "operator": "In", "values": ["1"]},
+                                                    {"key": "b", "operator": "NotIn", "values": ["2"]},
+                                                    {"key": "c", "operator": "Exists"}]}}}})
+    sars.append(synth.make_sar("system:authorizer:cedar-authorizer", "", [], "get", group="cedar.k8s.aws",
+                               resource="policies"))
+    sars.append(synth.make_sar("system:kube-scheduler", "", [], "get", resource="pods"))
+    n_fast = 0
+    for sar in sars:
+        got = cxx_sar_to_cedar(sar)
+        a = km.attributes_from_sar(sar)
+        if "fast" in got:
+            n_fast += 1
+            dec, reason = km.authorize([], a)
+            assert (got["fast"], got["reason"]) == (dec, reason)
+            continue
+        em, req = km.record_to_cedar_resource(a)
+        assert norm_entities(got["entities"]) == norm_entities(co.entities_to_json(em)), sar
+        assert got["request"] == co.request_to_json(req)
+    assert n_fast >= 2

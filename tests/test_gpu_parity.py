@@ -1,0 +1,207 @@
+"""GPU parity: the HIP evaluator (through the C-ABI) vs the CPU oracle, bit-exact on decisions,
+deciding tier, determining-policy IDs and the full Go-JSON diagnostic string."""
+import json
+import os
+
+import pytest
+
+import cedar_oracle as co
+import k8s_model as km
+from conftest import GOLDEN
+from helpers import sar_from_attrs
+from randgen import Gen
+
+import cedargpu
+from cedargpu import synth
+
+pytestmark = pytest.mark.gpu
+
+V = json.load(open(os.path.join(GOLDEN, "reference_vectors.json")))
+CORPUS = json.load(open(os.path.join(GOLDEN, "reference_corpus.json")))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    assert cedargpu.device_count() >= 1, "GPU tests need a GPU"
+    c = cedargpu.Context(0)
+    yield c
+    c.close()
+
+
+def oracle_tiers(stores):
+    out = []
+    for s in stores:
+        ps = co.PolicySet()
+        for d in s.documents():
+            if d[0] == "doc":
+                _, fname, text, pre, suf = d
+                for i, p in enumerate(co.parse_policies(text, fname)):
+                    ps.add(f"{pre}{i}{suf}", p)
+            else:
+                _, pid, fname, text, zero = d
+                p = co.parse_policies(text, fname)[0]
+                if zero:
+                    p.offset = p.line = p.col = 0
+                    p.filename = ""
+                ps.add(pid, p)
+        out.append(ps)
+    return out
+
+
+def check_items(ctx, stores, items):
+    """items: list of (entities_json, request_json). Compares GPU and oracle for every item."""
+    tiers = cedargpu.TieredPolicyStores(stores, ctx=ctx)
+    got = tiers.is_authorized_batch(items)
+    otiers = oracle_tiers(stores)
+    for (ents, req), (ok, diag) in zip(items, got):
+        em, r = co.entities_from_json(ents), co.request_from_json(req)
+        want_ok, want_diag, _ = co.tiered_is_authorized(otiers, em, r)
+        assert ok == want_ok, (req, diag, want_diag.to_go_json())
+        assert diag == want_diag.to_go_json(), (req,)
+    return got
+
+
+# ---------------------------------------------------------------- reference vectors
+@pytest.mark.parametrize("case", V["authorize"], ids=lambda c: c["name"])
+def test_authorize_reference_vectors_gpu(ctx, case):
+    """authorizer_test.go:462-920 end to end: SAR -> C++ model -> GPU -> decision + exact reason."""
+    store = cedargpu.MemoryStore(case["name"], case["policy"], case["store_complete"])
+    authz = cedargpu.Authorizer([store], ctx=ctx)
+    dec, reason = authz.authorize(sar_from_attrs(case["attributes"]))
+    assert dec == case["want_decision"]
+    assert reason == case["want_reason"]
+
+
+@pytest.mark.parametrize("case", V["tiers"]["cases"], ids=lambda c: c["name"])
+def test_tier_reference_vectors_gpu(ctx, case):
+    """store_test.go:21-188 on the GPU."""
+    stores = [cedargpu.MemoryStore("in-memory-test-store.cedar", s) for s in case["stores"]]
+    tiers = cedargpu.TieredPolicyStores(stores, ctx=ctx)
+    ok, diag = tiers.is_authorized(V["tiers"]["entities"], V["tiers"]["request"])
+    assert ok == case["want"]
+    assert json.loads(diag) == case["want_diag"]
+
+
+# ---------------------------------------------------------------- randomized differential
+@pytest.mark.parametrize("seed", range(12))
+def test_random_policies_vs_oracle(ctx, seed):
+    g = Gen(1000 + seed)
+    stores = [cedargpu.MemoryStore(f"t{t}.cedar", g.policies(g.r.randint(0, 12))) for t in range(g.r.randint(1, 3))]
+    items = [g.item() for _ in range(300)]
+    check_items(ctx, stores, items)
+
+
+def test_random_overflowing_result_lists(ctx):
+    """300 policies: many requests exceed the inline reason/error capacity -> re-run path."""
+    g = Gen(77)
+    stores = [cedargpu.MemoryStore("big.cedar", g.policies(300))]
+    items = [g.item() for _ in range(200)]
+    check_items(ctx, stores, items)
+
+
+# ---------------------------------------------------------------- reference corpora
+def _sar_items(n, seed):
+    sars = synth.random_sars(n, seed=seed, pop=synth.Population(seed=seed, n_users=3000, n_groups=200))
+    out = []
+    for s in sars:
+        a = km.attributes_from_sar(s)
+        if km.authorize([], a)[0] != km.DECISION_NO_OPINION or a.user.name.startswith("system:") and not (
+                a.user.name.startswith("system:serviceaccount:") or a.user.name.startswith("system:node:")):
+            continue
+        em, r = km.record_to_cedar_resource(a)
+        out.append((co.entities_to_json(em), co.request_to_json(r)))
+    return out
+
+
+def test_demo_authz_policies_vs_oracle(ctx):
+    """C1 at test scale: demo/authorization-policy.yaml x synthetic SubjectAccessReviews."""
+    stores = [cedargpu.CRDStore([(k.split(":")[1], "uid-1", v) for k, v in sorted(CORPUS["demo"].items())
+                                 if k.startswith("authorization")])]
+    check_items(ctx, stores, _sar_items(3000, 3))
+
+
+def test_converter_corpus_vs_oracle(ctx):
+    """The 13 converter golden files as a directory store tier + demo tier."""
+    files = {k: v for k, v in CORPUS["converter"].items()}
+    stores = [cedargpu.DirectoryStore(files),
+              cedargpu.MemoryStore("demo.cedar", "\n".join(v for k, v in sorted(CORPUS["demo"].items())))]
+    check_items(ctx, stores, _sar_items(2000, 9))
+
+
+def test_authorizer_sar_path_matches_oracle(ctx):
+    """Full Authorize() over SAR JSON (C++ model + GPU) vs oracle authorize()."""
+    stores = [cedargpu.MemoryStore("demo.cedar", "\n".join(v for k, v in sorted(CORPUS["demo"].items())))]
+    authz = cedargpu.Authorizer(stores, ctx=ctx)
+    sars = synth.random_sars(2000, seed=17, pop=synth.Population(seed=17, n_users=1000, n_groups=100))
+    sars.append(synth.make_sar("system:authorizer:cedar-authorizer", "", [], "get", group="rbac.authorization.k8s.io",
+                               resource="roles"))
+    got = authz.authorize_batch(sars)
+    otiers = oracle_tiers(stores)
+    for s, (dec, reason) in zip(sars, got):
+        want = km.authorize(otiers, km.attributes_from_sar(s))
+        assert (dec, reason) == want, s
+
+
+def test_admission_policies_vs_oracle(ctx):
+    """C4 at test scale: admission demo policies + allow-all tier, ConfigMap/Secret objects."""
+    stores = [cedargpu.MemoryStore("adm.cedar", "\n".join(v for k, v in sorted(CORPUS["demo"].items()) if k.startswith("admission"))),
+              cedargpu.ALLOW_ALL_ADMISSION]
+    items = []
+    objs = synth.admission_objects(600, seed=5)
+    for i, (kind, obj) in enumerate(objs):
+        op = ["CREATE", "UPDATE", "DELETE"][i % 3]
+        old = objs[(i + 1) % len(objs)][1] if op != "CREATE" else None
+        user = km.UserInfo(name=["test-user", "sample-user", f"user-{i % 200:05d}"][i % 3], uid="",
+                           groups=["requires-labels"] if i % 2 else ["viewers"])
+        req = km.AdmissionRequest(uid=f"req-{i}", operation=op, user=user, group="", version="v1",
+                                  resource=kind.lower() + "s", kind=kind, namespace=obj["metadata"]["namespace"],
+                                  name=obj["metadata"]["name"], object=obj if op != "DELETE" else None,
+                                  old_object=old if op != "CREATE" else None)
+        if op == "DELETE":
+            req.old_object = obj
+        em, r = km.admission_to_cedar(req)
+        items.append((co.entities_to_json(em), co.request_to_json(r)))
+    check_items(ctx, stores, items)
+
+
+# ---------------------------------------------------------------- edge cases
+def test_edge_cases(ctx):
+    pol = r'''
+permit (principal, action, resource) when { principal.n like "a\*b" };
+permit (principal, action, resource) when { principal.n like "*ü*" };
+forbid (principal, action, resource) when { principal.x + 1 > 0 };
+permit (principal, action, resource) when { context.big == 9223372036854775807 && context.neg == -9223372036854775808 };
+permit (principal, action, resource) when { [principal.n, principal.n] == [principal.n] };
+permit (principal, action, resource) when { {"a": [1, {"b": principal.x}]} == context.nested };
+permit (principal, action, resource) unless { principal has missing };
+'''
+    ents = [{"uid": {"type": "U", "id": "é\"q"}, "attrs": {"n": "a*b", "x": 9223372036854775807}, "parents": []}]
+    req = {"principal": {"type": "U", "id": "é\"q"}, "action": {"type": "A", "id": "a"}, "resource": {"type": "R", "id": ""},
+           "context": {"big": 9223372036854775807, "neg": -9223372036854775808, "nested": {"a": [1, {"b": 9223372036854775807}]}}}
+    ents2 = [{"uid": {"type": "U", "id": "x"}, "attrs": {"n": "xüy", "x": -1}, "parents": []}]
+    req2 = dict(req, principal={"type": "U", "id": "x"}, context={})
+    check_items(ctx, [cedargpu.MemoryStore("edge.cedar", pol)], [(ents, req), (ents2, req2), ([], req2)])
+
+
+def test_empty_tiers_and_no_entities(ctx):
+    stores = [cedargpu.MemoryStore("empty.cedar", ""), cedargpu.MemoryStore("e2.cedar", "// only a comment\n")]
+    req = {"principal": {"type": "U", "id": "a"}, "action": {"type": "A", "id": "b"}, "resource": {"type": "R", "id": "c"}}
+    check_items(ctx, stores, [([], req)])
+
+
+def test_hot_reload_epochs(ctx):
+    """Image swap: batches created before activate keep their epoch (immutable snapshot)."""
+    store = cedargpu.MemoryStore("r.cedar", "permit(principal, action, resource);")
+    tiers = cedargpu.TieredPolicyStores([store], ctx=ctx)
+    req = {"principal": {"type": "U", "id": "a"}, "action": {"type": "A", "id": "b"}, "resource": {"type": "R", "id": "c"}}
+    old = ctx.batch()
+    old.add([], req)
+    store.document = "forbid(principal, action, resource);"
+    tiers.reload()
+    new = ctx.batch()
+    new.add([], req)
+    for b in (old, new):
+        b.submit()
+        b.wait()
+    assert old.decision(0)[0] is True
+    assert new.decision(0)[0] is False
