@@ -110,15 +110,18 @@ def main():
         workers = args.cpu_workers or max(1, min(16, (os.cpu_count() or 2) - 1))
         baseline = cpu_baseline(policies, sars[:4096], args.cpu_seconds, workers)
 
+    # torch is plumbing only: the cross-rank barrier / max-reduce of timings runs over gloo on CPU
+    # tensors. torch's bundled HIP runtime is never initialised in this process (it would clash
+    # with the ROCm runtime libcedargpu.so links); device sync goes through the library.
     import torch
     import torch.distributed as dist
 
     import cedargpu
+    from cedargpu.store import device_synchronize
 
     dist_on = world > 1
     if dist_on:
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend="gloo")
     device = local
 
     t_build = time.perf_counter()
@@ -136,18 +139,18 @@ def main():
 
     if args.warmup:
         b.time(args.warmup)
+    device_synchronize(device)
     if dist_on:
         dist.barrier()
-    torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     kernel_ms = b.time(args.steps)  # HIP events on the evaluation stream, K launches
-    torch.cuda.synchronize(device)
+    device_synchronize(device)
     wall_s = time.perf_counter() - t0
     if dist_on:
-        t = torch.tensor([wall_s, kernel_ms], device=f"cuda:{device}", dtype=torch.float64)
+        dist.barrier()
+        t = torch.tensor([wall_s, kernel_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall_s, kernel_ms = float(t[0]), float(t[1])
-        dist.barrier()
 
     # submit -> results-visible latency on small batches (includes H2D, launch, D2H)
     lat = []

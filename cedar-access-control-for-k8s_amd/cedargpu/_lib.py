@@ -54,6 +54,7 @@ _SIGS = {
     "cg_compiler_build": (ctypes.c_int, [P, u64, ctypes.POINTER(P), ctypes.POINTER(sz)]),
     "cg_image_info": (ctypes.c_int, [P, sz, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u64)]),
     "cg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "cg_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "cg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(P)]),
     "cg_ctx_destroy": (None, [P]),
     "cg_last_error": (cstr, [P]),

@@ -31,6 +31,12 @@ def device_count() -> int:
     return n.value if rc == 0 else 0
 
 
+def device_synchronize(device: int = 0):
+    rc = lib.cg_device_synchronize(device)
+    if rc:
+        raise DeviceError(rc, f"hipDeviceSynchronize failed on {device}")
+
+
 class PolicyStore:
     """A policy source. `documents()` yields (kind, args) fed to the compiler."""
 

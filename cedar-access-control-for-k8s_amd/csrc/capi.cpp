@@ -157,6 +157,8 @@ int cg_device_count(int* n) {
   return dev_count(n) ? CG_E_DEVICE : CG_OK;
 }
 
+int cg_device_synchronize(int device) { return dev_synchronize(device) ? CG_E_DEVICE : CG_OK; }
+
 int cg_ctx_create(int device, cg_ctx** out) {
   if (!out) return CG_E_ARG;
   *out = nullptr;

@@ -31,6 +31,7 @@ struct DevBatch {
 const char* dev_last_error();
 int dev_count(int* n);
 int dev_select(int device);
+int dev_synchronize(int device);
 int dev_image_upload(int device, const Image& img, DevImage* out);
 void dev_image_free(DevImage* d);
 int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream);

@@ -731,6 +731,12 @@ int dev_select(int device) {
   return 0;
 }
 
+int dev_synchronize(int device) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  HIPCHK(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return 0;
+}
+
 int dev_stream_create(int device, void** stream) {
   HIPCHK(hipSetDevice(device), "hipSetDevice");
   hipStream_t s;

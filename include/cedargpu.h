@@ -65,6 +65,8 @@ int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t*
 
 /* ---- device context (one per GPU; requests shard across contexts, images are replicated) ---- */
 int cg_device_count(int* n);
+/* hipDeviceSynchronize on `device` (bench barriers; the library links ROCm's own HIP runtime). */
+int cg_device_synchronize(int device);
 int cg_ctx_create(int device, cg_ctx** out);
 void cg_ctx_destroy(cg_ctx* ctx);
 const char* cg_last_error(cg_ctx* ctx);
