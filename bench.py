@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--policies", type=int, default=10_000)
     ap.add_argument("--batch", type=int, default=65_536, help="requests per GPU per step")
+    ap.add_argument("--variant", default="full", help="policy-shape study: full | scope-only | no-group | atomic-only")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -102,7 +103,7 @@ def main():
     from cedargpu import synth
 
     pop = synth.Population(seed=7)
-    policies = synth.abac_policies(args.policies, seed=31, pop=pop)
+    policies = synth.abac_policies(args.policies, seed=31, pop=pop, variant=args.variant)
     sars = synth.random_sars(args.batch, seed=1000 + rank, pop=pop)
 
     baseline = None
@@ -199,6 +200,7 @@ def main():
             "config": {"workload": "C3 single-GPU shard: 10k ABAC policies (k8s::Group scope, namespace/apiGroup/"
                                    "resource/labelSelector/like conditions) x synthetic SARs",
                        "policies": args.policies, "requests_per_gpu": args.batch, "tiers": 1,
+                       "variant": args.variant,
                        "parallelism": f"request-sharded x{world}, image replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

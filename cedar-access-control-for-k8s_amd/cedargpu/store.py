@@ -155,6 +155,17 @@ def build_image(stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
         lib.cg_compiler_destroy(c)
 
 
+def image_stats(image: bytes) -> dict:
+    """Shape of a compiled image: policies, tiers, atom-lowered policies, hot attributes, ..."""
+    u = [ctypes.c_uint32() for _ in range(6)]
+    ep = ctypes.c_uint64()
+    if lib.cg_image_info(image, len(image), ctypes.byref(u[0]), ctypes.byref(u[1]), ctypes.byref(ep)):
+        raise ValueError("not a compiled policy image")
+    lib.cg_image_stats(image, len(image), *(ctypes.byref(x) for x in u[2:]))
+    return {"policies": u[0].value, "tiers": u[1].value, "epoch": ep.value, "atomic": u[2].value,
+            "hot": u[3].value, "actions": u[4].value, "stream_words": u[5].value}
+
+
 class Context:
     """One GPU: loaded images (by epoch) and the active one."""
 

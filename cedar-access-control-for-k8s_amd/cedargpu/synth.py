@@ -202,8 +202,29 @@ def rbac_policies(n: int, seed: int = 21, pop: Optional[Population] = None) -> s
     return "\n".join(out)
 
 
-def abac_policies(n: int, seed: int = 31, pop: Optional[Population] = None) -> str:
-    """C3: attribute-based policies keyed on group membership."""
+def abac_policies(n: int, seed: int = 31, pop: Optional[Population] = None, variant: str = "full") -> str:
+    """C3: attribute-based policies keyed on group membership.
+
+    variant (shape studies of the evaluator; `full` is the benchmark workload):
+      full        group-scoped policies with when-clauses
+      scope-only  the same scopes, conditions dropped
+      no-group    the same conditions, principal scope `principal is k8s::User` instead of `in Group`
+    """
+    text = _abac(n, seed, pop)
+    if variant == "scope-only":
+        import re
+        text = re.sub(r"\)\nwhen \{.*?\};\n", ");\n", text, flags=re.S)
+    elif variant == "no-group":
+        import re
+        text = re.sub(r'principal in k8s::Group::"[^"]*"', "principal is k8s::User", text)
+    elif variant == "atomic-only":  # drop the runtime-record (bytecode) template
+        text = "\n".join(p for p in text.split("\n\n") if "containsAny" not in p)
+    elif variant != "full":
+        raise ValueError(variant)
+    return text
+
+
+def _abac(n: int, seed: int, pop: Optional[Population]) -> str:
     pop = pop or Population()
     rng = np.random.Generator(np.random.PCG64(seed))
     out = []

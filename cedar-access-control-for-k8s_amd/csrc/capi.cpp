@@ -151,6 +151,21 @@ int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t*
   }
 }
 
+int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* n_hot, uint32_t* n_actions,
+                   uint32_t* stream_words) {
+  if (!image) return CG_E_ARG;
+  try {
+    auto img = Image::deserialize((const uint8_t*)image, len);
+    if (n_atomic) *n_atomic = img->n_atomic;
+    if (n_hot) *n_hot = (uint32_t)img->hot.size() / 2;
+    if (n_actions) *n_actions = (uint32_t)img->act.size() / 2;
+    if (stream_words) *stream_words = (uint32_t)img->pstream.size();
+    return CG_OK;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 int cg_device_count(int* n) {
   if (!n) return CG_E_ARG;

@@ -1,0 +1,1331 @@
+// gfx950 evaluation kernel: tiered Cedar authorization for a batch of requests.
+//
+// Replaces, per request, the reference's
+//   TieredPolicyStores.IsAuthorized (internal/server/store/store.go:25-42)
+//     -> cedar-go (*PolicySet).IsAuthorized (call site store.go:31)
+// Mapping onto CDNA4:
+//   * one lane = one request; the 4 waves of a 256-thread block walk the tiers' policy stream in
+//     lock step: each <=16 KiB chunk of policy records (descriptor + atoms + atom data) is copied
+//     into LDS once per block with coalesced 16-byte loads, then every wave reads each record as a
+//     wave-uniform LDS broadcast (4 x ds_read_b128 + v_readfirstlane), so all per-policy control
+//     flow is scalar;
+//   * scope tests are register-only: each request carries a 128-bit Bloom filter of its
+//     principal / resource ancestor-or-self UIDs and a 64-bit mask over the image's action
+//     table; the exact ancestor scan (independent, unrolled heap loads) runs only for lanes
+//     whose Bloom bit is set; a `__ballot` skips the policy for the wave when no lane matches;
+//   * "atomic" policies (when/unless = &&- or ||-chains of predicates over pre-resolved
+//     attributes) run as 4-word atoms against an LDS table of pre-resolved (var, attribute)
+//     values; other policies run as register bytecode (forward-only skip targets per lane);
+//   * satisfied forbids/permits and errors are appended to per-request result lists; forbid
+//     overrides permit; a tier falls through only on (Deny, no reasons, no errors).
+// No MFMA: the work is integer compares, ID equality and short scans.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "device.h"
+#include "engine.h"
+#include "image.h"
+
+using namespace cgi;
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+struct RV {
+  uint32_t w0, w1, w2;
+};
+
+__device__ __forceinline__ uint32_t tag_of(const RV& v) { return v.w0 >> TAG_SHIFT; }
+
+struct KArgs {
+  const uint32_t* __restrict__ pstream;
+  const uint32_t* __restrict__ chunks;
+  const uint32_t* __restrict__ tier_cend;
+  const uint32_t* __restrict__ cpool;
+  const uint32_t* __restrict__ gstr_off;
+  const uint8_t* __restrict__ gstr_bytes;
+  const uint32_t* __restrict__ hot;
+  const uint32_t* __restrict__ act;
+  const uint32_t* __restrict__ heap;
+  const uint32_t* __restrict__ req_base;
+  const uint32_t* __restrict__ req_idx;
+  const uint32_t* __restrict__ bstr_off;
+  const uint8_t* __restrict__ bstr_bytes;
+  uint32_t* __restrict__ res;
+  uint32_t* __restrict__ reasons_f;
+  uint32_t* __restrict__ reasons_p;
+  uint32_t* __restrict__ errs;
+  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape;
+};
+
+// Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
+// registers; the only non-inlined function (structural equality) takes plain pointers.
+struct Ctx {
+  const uint32_t* blk;    // request block (global)
+  const uint32_t* cpool;  // image constant pool (global)
+  uint32_t* lh;           // lane scratch (private): runtime-built sets/records
+  const uint32_t* hot;
+  const uint32_t* gstr_off;
+  const uint8_t* gstr_bytes;
+  const uint32_t* bstr_off;
+  const uint8_t* bstr_bytes;
+  uint32_t n_gstr;
+  uint2* hotl;  // LDS hot table, this lane's column: hotl[h * BLOCK]
+  uint32_t pt, pi, at, ai, rt, ri;
+  uint32_t pidx, aidx, ridx;
+  uint32_t nent;
+  uint32_t p_anc, p_nanc, r_anc, r_nanc;  // heap offsets of ancestor pair arrays, and counts
+  // first 8 principal ancestors, for the exact `in` test in registers (named scalars: an array
+  // here would keep the whole context out of registers)
+  uint32_t t0, i0, t1, i1, t2, i2, t3, i3, t4, i4, t5, i5, t6, i6, t7, i7;
+  uint32_t pb0, pb1, pb2, pb3;            // principal ancestor-or-self Bloom
+  uint32_t rb0, rb1, rb2, rb3;            // resource ancestor-or-self Bloom
+};
+
+// Makes a value opaque to the optimizer. Used on context fields that feed a select: otherwise
+// InstCombine turns `h == 0 ? c.pt : c.rt` into a load through a dynamic offset into the
+// context, which forces the whole per-lane context into scratch memory.
+__device__ __forceinline__ uint32_t opq(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// Selects among three per-lane values by a wave-uniform index (0, 1, else 2).
+__device__ __forceinline__ uint32_t pick3(uint32_t h, uint32_t a, uint32_t b, uint32_t c) {
+  return h == 0 ? opq(a) : (h == 1 ? opq(b) : opq(c));
+}
+
+// Value reference read (heap / constant pool / lane scratch).
+__device__ __forceinline__ uint32_t rd3(const uint32_t* blk, const uint32_t* cpool, const uint32_t* lh, uint32_t ref,
+                                        uint32_t i) {
+  const uint32_t sp = ref >> SPACE_SHIFT, off = (ref & OFF_MASK) + i;
+  if (sp == SP_HEAP) return blk[off];
+  if (sp == SP_CPOOL) return cpool[off];
+  return lh[off];
+}
+__device__ __forceinline__ uint32_t rd(const Ctx& c, uint32_t ref, uint32_t i) { return rd3(c.blk, c.cpool, c.lh, ref, i); }
+
+__device__ __forceinline__ RV load_val3(const uint32_t* blk, const uint32_t* cpool, const uint32_t* lh, uint32_t w0,
+                                        uint32_t w1) {
+  const uint32_t t = w0 >> TAG_SHIFT;
+  if (t == T_LONG) return RV{mk_w0(T_LONG, 0), w1, ((int32_t)w1 < 0) ? 0xFFFFFFFFu : 0u};
+  if (t == T_LONGREF) {
+    const uint32_t ref = w0 & X_MASK;
+    return RV{mk_w0(T_LONG, 0), rd3(blk, cpool, lh, ref, 0), rd3(blk, cpool, lh, ref, 1)};
+  }
+  return RV{w0, w1, 0};
+}
+__device__ __forceinline__ RV load_val(const Ctx& c, uint32_t w0, uint32_t w1) { return load_val3(c.blk, c.cpool, c.lh, w0, w1); }
+
+__device__ __forceinline__ uint32_t tname(const RV& v) {
+  switch (tag_of(v)) {
+    case T_BOOL: return TN_BOOL;
+    case T_LONG: return TN_LONG;
+    case T_STR: return TN_STRING;
+    case T_ENT: return TN_ENTITY;
+    case T_SET: return TN_SET;
+    case T_REC: return TN_RECORD;
+    case T_DEC: return TN_DECIMAL;
+    case T_IP: return TN_IP;
+    default: return TN_UNKNOWN;
+  }
+}
+
+// ---- equality -------------------------------------------------------------------------------
+// Shallow comparison: decides everything except (set, set) and (record, record) pairs.
+// Returns 0 false, 1 true, 2 = needs a structural comparison.
+__device__ __forceinline__ uint32_t veq_shallow(const uint32_t* blk, const uint32_t* cpool, const uint32_t* lh,
+                                                const RV& a, const RV& b) {
+  const uint32_t ta = tag_of(a), tb = tag_of(b);
+  if (ta != tb) return 0u;
+  switch (ta) {
+    case T_BOOL:
+    case T_STR: return a.w1 == b.w1 ? 1u : 0u;
+    case T_LONG: return (a.w1 == b.w1 && a.w2 == b.w2) ? 1u : 0u;
+    case T_ENT: return (a.w0 == b.w0 && a.w1 == b.w1) ? 1u : 0u;
+    case T_DEC: {
+      const uint32_t ra = a.w0 & X_MASK, rb = b.w0 & X_MASK;
+      return (rd3(blk, cpool, lh, ra, 0) == rd3(blk, cpool, lh, rb, 0) && rd3(blk, cpool, lh, ra, 1) == rd3(blk, cpool, lh, rb, 1)) ? 1u : 0u;
+    }
+    case T_IP: {
+      const uint32_t ra = a.w0 & X_MASK, rb = b.w0 & X_MASK;
+      for (uint32_t k = 0; k < 5; k++) if (rd3(blk, cpool, lh, ra, k) != rd3(blk, cpool, lh, rb, k)) return 0u;
+      return 1u;
+    }
+    case T_SET:
+    case T_REC: return (ta == T_REC && a.w1 != b.w1) ? 0u : 2u;  // records: unique keys, counts must agree
+    default: return 0u;
+  }
+}
+
+// Structural equality of two sets or two records, iterative over an explicit frame stack (no
+// recursion): set equality is mutual inclusion (lane-built sets may hold duplicates), record
+// equality is equal sorted key lists with equal values. Returns 0 false, 1 true, 2 nesting
+// beyond VAL_DEPTH (reported as E_DEPTH).
+__device__ __noinline__ uint32_t veq_struct(const uint32_t* blk, const uint32_t* cpool, const uint32_t* lh, RV a, RV b) {
+  struct Frame {
+    uint32_t ra, rb, na, nb;
+    uint32_t set, phase, i, j;  // set: 1 set, 0 record; phase: 0 a-in-b, 1 b-in-a
+  };
+  Frame st[VAL_DEPTH];
+  uint32_t sp = 0;
+  st[sp++] = Frame{a.w0 & X_MASK, b.w0 & X_MASK, a.w1, b.w1, tag_of(a) == T_SET ? 1u : 0u, 0, 0, 0};
+  bool have = false, ret = false;  // result of the child frame just popped
+  while (sp > 0) {
+    Frame& f = st[sp - 1];
+    bool done = false, res = false, pushed = false;
+    if (f.set) {
+      if (have) {  // child compared outer[i] with inner[j]
+        have = false;
+        if (ret) { f.i++; f.j = 0; } else { f.j++; }
+      }
+      for (;;) {
+        const uint32_t no = f.phase ? f.nb : f.na, ni = f.phase ? f.na : f.nb;
+        if (f.i >= no) {
+          if (f.phase == 0) { f.phase = 1; f.i = 0; f.j = 0; continue; }
+          done = true; res = true;
+          break;
+        }
+        if (f.j >= ni) { done = true; res = false; break; }
+        const uint32_t ro = f.phase ? f.rb : f.ra, rn = f.phase ? f.ra : f.rb;
+        const RV x = load_val3(blk, cpool, lh, rd3(blk, cpool, lh, ro, 1 + 2 * f.i), rd3(blk, cpool, lh, ro, 2 + 2 * f.i));
+        const RV y = load_val3(blk, cpool, lh, rd3(blk, cpool, lh, rn, 1 + 2 * f.j), rd3(blk, cpool, lh, rn, 2 + 2 * f.j));
+        const uint32_t s = veq_shallow(blk, cpool, lh, x, y);
+        if (s == 2u) {
+          if (sp >= VAL_DEPTH) return 2u;
+          st[sp++] = Frame{x.w0 & X_MASK, y.w0 & X_MASK, x.w1, y.w1, tag_of(x) == T_SET ? 1u : 0u, 0, 0, 0};
+          pushed = true;
+          break;
+        }
+        if (s) { f.i++; f.j = 0; } else { f.j++; }
+      }
+    } else {
+      if (have) {
+        have = false;
+        if (!ret) { done = true; res = false; } else { f.i++; }
+      }
+      while (!done) {
+        if (f.i >= f.na) { done = true; res = true; break; }
+        if (rd3(blk, cpool, lh, f.ra, 1 + 3 * f.i) != rd3(blk, cpool, lh, f.rb, 1 + 3 * f.i)) { done = true; res = false; break; }
+        const RV x = load_val3(blk, cpool, lh, rd3(blk, cpool, lh, f.ra, 2 + 3 * f.i), rd3(blk, cpool, lh, f.ra, 3 + 3 * f.i));
+        const RV y = load_val3(blk, cpool, lh, rd3(blk, cpool, lh, f.rb, 2 + 3 * f.i), rd3(blk, cpool, lh, f.rb, 3 + 3 * f.i));
+        const uint32_t s = veq_shallow(blk, cpool, lh, x, y);
+        if (s == 2u) {
+          if (sp >= VAL_DEPTH) return 2u;
+          st[sp++] = Frame{x.w0 & X_MASK, y.w0 & X_MASK, x.w1, y.w1, tag_of(x) == T_SET ? 1u : 0u, 0, 0, 0};
+          pushed = true;
+          break;
+        }
+        if (!s) { done = true; res = false; break; }
+        f.i++;
+      }
+    }
+    if (pushed) continue;
+    if (done) {
+      sp--;
+      have = true;
+      ret = res;
+    }
+  }
+  return ret ? 1u : 0u;
+}
+
+// full equality; `deep` set when nesting exceeds the device limit
+__device__ __forceinline__ bool veq(const Ctx& c, const RV& a, const RV& b, bool& deep) {
+  const uint32_t s = veq_shallow(c.blk, c.cpool, c.lh, a, b);
+  if (s != 2u) return s == 1u;
+  const uint32_t r = veq_struct(c.blk, c.cpool, c.lh, a, b);
+  if (r == 2u) deep = true;
+  return r == 1u;
+}
+
+// primitive equality against a register-form constant (tags equal and payload equal)
+__device__ __forceinline__ bool prim_eq(const RV& v, uint32_t c0, uint32_t c1, uint32_t c2) {
+  if (v.w0 >> TAG_SHIFT != c0 >> TAG_SHIFT) return false;
+  switch (c0 >> TAG_SHIFT) {
+    case T_LONG: return v.w1 == c1 && v.w2 == c2;
+    case T_ENT: return v.w0 == c0 && v.w1 == c1;
+    default: return v.w1 == c1;
+  }
+}
+
+// ---- records / entities (request data is always in the heap) -------------------------------
+__device__ __forceinline__ bool rec_get(const Ctx& c, const RV& rec, uint32_t key, RV& out) {
+  const uint32_t ref = rec.w0 & X_MASK, n = rec.w1;
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (rd(c, ref, 1 + 3 * mid) < key) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < n && rd(c, ref, 1 + 3 * lo) == key) {
+    out = load_val(c, rd(c, ref, 2 + 3 * lo), rd(c, ref, 3 + 3 * lo));
+    return true;
+  }
+  return false;
+}
+// heap record lookup, memory form (hot table fill)
+__device__ __forceinline__ bool rec_get_heap(const uint32_t* blk, uint32_t rw0, uint32_t n, uint32_t key, uint2& out) {
+  const uint32_t off = rw0 & OFF_MASK;
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (blk[off + 1 + 3 * mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < n && blk[off + 1 + 3 * lo] == key) {
+    out = make_uint2(blk[off + 2 + 3 * lo], blk[off + 3 + 3 * lo]);
+    return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint32_t find_ent(const Ctx& c, uint32_t et, uint32_t ei) {
+  if (et == c.pt && ei == c.pi) return opq(c.pidx);
+  if (et == c.rt && ei == c.ri) return opq(c.ridx);
+  if (et == c.at && ei == c.ai) return opq(c.aidx);
+  for (uint32_t i = 0; i < c.nent; i++) {
+    const uint32_t* row = c.blk + RH_WORDS + i * ENT_WORDS;
+    if (row[ER_TYPE] == et && row[ER_ID] == ei) return i;
+  }
+  return NO_ENT;
+}
+
+// exact membership in a heap ancestor list: pairs at blk[off + 2k], independent loads, 4 per step
+__device__ __forceinline__ bool anc_scan(const uint32_t* blk, uint32_t off, uint32_t n, uint32_t qt, uint32_t qi) {
+  bool f = false;
+  uint32_t k = 0;
+  for (; k + 4 <= n && !f; k += 4) {
+    const uint32_t* q = blk + off + 2 * k;
+    const uint32_t t0 = q[0], i0 = q[1], t1 = q[2], i1 = q[3], t2 = q[4], i2 = q[5], t3 = q[6], i3 = q[7];
+    f = (t0 == qt && i0 == qi) | (t1 == qt && i1 == qi) | (t2 == qt && i2 == qi) | (t3 == qt && i3 == qi);
+  }
+  for (; k < n && !f; k++) f = blk[off + 2 * k] == qt && blk[off + 2 * k + 1] == qi;
+  return f;
+}
+
+__device__ __forceinline__ void anc_of(const Ctx& c, uint32_t idx, uint32_t& off, uint32_t& n) {
+  off = 0; n = 0;
+  if (idx == NO_ENT) return;
+  const uint32_t ref = c.blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;
+  n = c.blk[ref];
+  off = ref + 1;
+}
+
+__device__ __forceinline__ bool anc_has(const Ctx& c, uint32_t idx, uint32_t qt, uint32_t qi) {
+  uint32_t off, n;
+  anc_of(c, idx, off, n);
+  return anc_scan(c.blk, off, n, qt, qi);
+}
+
+__device__ __forceinline__ bool ent_in(const Ctx& c, uint32_t et, uint32_t ei, uint32_t qt, uint32_t qi) {
+  if (et == qt && ei == qi) return true;
+  return anc_has(c, find_ent(c, et, ei), qt, qi);
+}
+
+__device__ __forceinline__ bool bloom_test(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t bit) {
+  const uint32_t w = bit < 64 ? (bit < 32 ? b0 : b1) : (bit < 96 ? b2 : b3);
+  return (w >> (bit & 31)) & 1u;
+}
+__device__ __forceinline__ void bloom_add(uint32_t& b0, uint32_t& b1, uint32_t& b2, uint32_t& b3, uint32_t bit) {
+  const uint32_t m = 1u << (bit & 31);
+  b0 |= bit < 32 ? m : 0u;
+  b1 |= (bit >= 32 && bit < 64) ? m : 0u;
+  b2 |= (bit >= 64 && bit < 96) ? m : 0u;
+  b3 |= bit >= 96 ? m : 0u;
+}
+
+// principal / resource `in E` with the Bloom shortcut (bit = uid_bloom_bit(et, ei), uniform)
+__device__ __forceinline__ bool p_in(const Ctx& c, uint32_t et, uint32_t ei, uint32_t bit) {
+  if (c.pt == et && c.pi == ei) return true;
+  if (!bloom_test(c.pb0, c.pb1, c.pb2, c.pb3, bit)) return false;
+  // unused entries hold ~0u
+  bool f = ((c.t0 == et) & (c.i0 == ei)) | ((c.t1 == et) & (c.i1 == ei)) | ((c.t2 == et) & (c.i2 == ei)) |
+           ((c.t3 == et) & (c.i3 == ei)) | ((c.t4 == et) & (c.i4 == ei)) | ((c.t5 == et) & (c.i5 == ei)) |
+           ((c.t6 == et) & (c.i6 == ei)) | ((c.t7 == et) & (c.i7 == ei));
+  if (!f && c.p_nanc > 8) f = anc_scan(c.blk, c.p_anc + 16, c.p_nanc - 8, et, ei);
+  return f;
+}
+__device__ __forceinline__ bool r_in(const Ctx& c, uint32_t et, uint32_t ei, uint32_t bit) {
+  if (c.rt == et && c.ri == ei) return true;
+  if (!bloom_test(c.rb0, c.rb1, c.rb2, c.rb3, bit)) return false;
+  return anc_scan(c.blk, c.r_anc, c.r_nanc, et, ei);
+}
+
+// ---- strings / like -------------------------------------------------------------------------
+__device__ __forceinline__ void str_span(const Ctx& c, uint32_t sid, const uint8_t*& p, uint32_t& len) {
+  if (sid < c.n_gstr) {
+    const uint32_t o = c.gstr_off[sid];
+    len = c.gstr_off[sid + 1] - o;
+    p = c.gstr_bytes + o;
+  } else {
+    const uint32_t j = sid - c.n_gstr;
+    const uint32_t o = c.bstr_off[j];
+    len = c.bstr_off[j + 1] - o;
+    p = c.bstr_bytes + o;
+  }
+}
+
+// pattern literal bytes: 4 per word, little-endian
+__device__ __forceinline__ uint32_t pat_byte(const uint32_t* w, uint32_t k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+
+__device__ __forceinline__ bool lit_at(const uint8_t* s, uint32_t pos, const uint32_t* w, uint32_t n) {
+  bool ok = true;
+  uint32_t k = 0;
+  for (; k + 4 <= n && ok; k += 4) {  // 4 independent byte loads per step
+    const uint32_t x = (uint32_t)s[pos + k] | ((uint32_t)s[pos + k + 1] << 8) | ((uint32_t)s[pos + k + 2] << 16) |
+                       ((uint32_t)s[pos + k + 3] << 24);
+    ok = x == w[k >> 2];
+  }
+  for (; k < n && ok; k++) ok = s[pos + k] == pat_byte(w, k);
+  return ok;
+}
+
+// `pw` points at a compiled pattern (LDS record data or global constant pool)
+template <class P>
+__device__ __forceinline__ bool like_match(const Ctx& c, uint32_t sid, P pw) {
+  const uint8_t* s;
+  uint32_t slen;
+  str_span(c, sid, s, slen);
+  const uint32_t flags = pw[0];
+  uint32_t q = 1;
+  const uint32_t plen = pw[q];
+  const uint32_t pq = q + 1;
+  q += 1 + ((plen + 3) >> 2);
+  if (!(flags & 1)) {
+    if (slen != plen) return false;
+    bool ok = true;
+    for (uint32_t k = 0; k < plen && ok; k++) ok = s[k] == ((pw[pq + (k >> 2)] >> (8 * (k & 3))) & 0xFFu);
+    return ok;
+  }
+  const uint32_t sl = pw[q];
+  const uint32_t sq = q + 1;
+  q += 1 + ((sl + 3) >> 2);
+  if (slen < plen + sl) return false;
+  bool ok = true;
+  for (uint32_t k = 0; k < plen && ok; k++) ok = s[k] == ((pw[pq + (k >> 2)] >> (8 * (k & 3))) & 0xFFu);
+  for (uint32_t k = 0; k < sl && ok; k++) ok = s[slen - sl + k] == ((pw[sq + (k >> 2)] >> (8 * (k & 3))) & 0xFFu);
+  if (!ok) return false;
+  uint32_t pos = plen;
+  const uint32_t end = slen - sl;
+  const uint32_t nmid = flags >> 8;
+  for (uint32_t m = 0; m < nmid; m++) {
+    const uint32_t ml = pw[q];
+    const uint32_t mq = q + 1;
+    q += 1 + ((ml + 3) >> 2);
+    bool found = false;
+    while (pos + ml <= end && !found) {
+      bool eq = true;
+      for (uint32_t k = 0; k < ml && eq; k++) eq = s[pos + k] == ((pw[mq + (k >> 2)] >> (8 * (k & 3))) & 0xFFu);
+      if (eq) found = true;
+      else pos++;
+    }
+    if (!found) return false;
+    pos += ml;
+  }
+  return true;
+}
+
+// ---- wave helpers ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
+  return __builtin_amdgcn_readfirstlane(x);
+}
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+struct Err {
+  uint32_t code, aux, k, et, ei;
+};
+
+__device__ __forceinline__ void type_err(Err& e, uint32_t expected, const RV& got) {
+  e.code = E_TYPE;
+  e.aux = expected | (tname(got) << 8);
+}
+
+// i64 helpers
+__device__ __forceinline__ int64_t as_i64(const RV& v) { return (int64_t)(((uint64_t)v.w2 << 32) | v.w1); }
+__device__ __forceinline__ RV from_i64(int64_t x) {
+  return RV{mk_w0(T_LONG, 0), (uint32_t)((uint64_t)x & 0xFFFFFFFFu), (uint32_t)((uint64_t)x >> 32)};
+}
+__device__ __forceinline__ RV mk_bool(bool b) { return RV{mk_w0(T_BOOL, 0), b ? 1u : 0u, 0}; }
+
+// Hot slot h of this lane: value (memory form) or a status word (tag NONE, x = error code).
+__device__ __forceinline__ uint2 hot_get(const Ctx& c, uint32_t h) { return c.hotl[h * BLOCK]; }
+__device__ __forceinline__ bool hot_ok(uint2 v) { return (v.x >> TAG_SHIFT) != T_NONE; }
+// The error ATTR would raise for a missing hot attribute.
+__device__ __forceinline__ void hot_err(const Ctx& c, uint32_t h, uint2 v, Err& e) {
+  const uint32_t var = uni(c.hot[2 * h]);
+  e.code = v.x & X_MASK;
+  e.k = uni(c.hot[2 * h + 1]);
+  e.et = pick3(var, c.pt, c.at, c.rt);
+  e.ei = pick3(var, c.pi, c.ai, c.ri);
+}
+
+// ---- atoms ---------------------------------------------------------------------------------
+// rec = this policy's LDS record (atom data lives there). Returns 0 false, 1 true, 2 error.
+// AK_RECSET helpers: compare a request value with one template operand (const or hot hole).
+__device__ __forceinline__ bool rs_opnd_eq(const Ctx& c, const RV& x, uint32_t kind, uint32_t a, uint32_t b, uint32_t d,
+                                           bool& deep) {
+  if (kind == RF_CONST) return prim_eq(x, a, b, d);
+  const uint2 hv = hot_get(c, a);  // holes were checked present before matching
+  return veq(c, x, load_val(c, hv.x, hv.y), deep);
+}
+// set-literal field: x (must be a set) equals the literal list by mutual inclusion
+__device__ __forceinline__ bool rs_set_eq(const Ctx& c, const RV& x, const uint32_t* el, uint32_t n, bool& deep) {
+  if (tag_of(x) != T_SET) return false;
+  const uint32_t ref = x.w0 & X_MASK, m = x.w1;
+  for (uint32_t i = 0; i < m; i++) {
+    const RV xi = load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i));
+    bool f = false;
+    for (uint32_t j = 0; j < n && !f; j++) f = rs_opnd_eq(c, xi, el[4 * j], el[4 * j + 1], el[4 * j + 2], el[4 * j + 3], deep);
+    if (!f) return false;
+  }
+  for (uint32_t j = 0; j < n; j++) {
+    bool f = false;
+    for (uint32_t i = 0; i < m && !f; i++) {
+      const RV xi = load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i));
+      f = rs_opnd_eq(c, xi, el[4 * j], el[4 * j + 1], el[4 * j + 2], el[4 * j + 3], deep);
+    }
+    if (!f) return false;
+  }
+  return true;
+}
+// record x == template t (sorted keys, exact key set)
+__device__ __forceinline__ bool rs_rec_eq(const Ctx& c, const uint32_t* rec, const RV& x, const uint32_t* t, bool& deep) {
+  const uint32_t nk = t[0];
+  if (tag_of(x) != T_REC || x.w1 != nk) return false;
+  const uint32_t ref = x.w0 & X_MASK;
+  for (uint32_t k = 0; k < nk; k++) {
+    const uint32_t* f = t + 1 + RS_FIELD_WORDS * k;
+    if (rd(c, ref, 1 + 3 * k) != f[0]) return false;
+    const RV xf = load_val(c, rd(c, ref, 2 + 3 * k), rd(c, ref, 3 + 3 * k));
+    const bool q = f[1] == RF_SETLIT ? rs_set_eq(c, xf, rec + f[2], f[3], deep)
+                                     : rs_opnd_eq(c, xf, f[1], f[2], f[3], f[4], deep);
+    if (!q) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ uint32_t eval_atom(const Ctx& c, const uint32_t* rec, uint32_t kind, uint32_t h, uint32_t w1,
+                                              uint32_t w2, uint32_t w3, Err& e) {
+  if (kind == AK_IS) {
+    return pick3(h, c.pt, c.at, c.rt) == w1 ? 1u : 0u;
+  }
+  if (kind == AK_IN) {
+    if (h == 0) return p_in(c, w1, w2, w3) ? 1u : 0u;
+    if (h == 2) return r_in(c, w1, w2, w3) ? 1u : 0u;
+    return ((c.at == w1 && c.ai == w2) || anc_has(c, c.aidx, w1, w2)) ? 1u : 0u;
+  }
+  const uint2 hv = hot_get(c, h);
+  if (kind == AK_HAS) return hot_ok(hv) ? 1u : 0u;
+  if (!hot_ok(hv)) { hot_err(c, h, hv, e); return 2u; }
+  const RV v = load_val(c, hv.x, hv.y);
+  switch (kind) {
+    case AK_BOOL:
+      if (tag_of(v) != T_BOOL) { type_err(e, TN_BOOL, v); return 2u; }
+      return v.w1;
+    case AK_EQ: return prim_eq(v, w1, w2, w3) ? 1u : 0u;
+    case AK_EQH: {
+      const uint2 hv2 = hot_get(c, w1);
+      if (!hot_ok(hv2)) { hot_err(c, w1, hv2, e); return 2u; }
+      bool deep = false;
+      const bool q = veq(c, v, load_val(c, hv2.x, hv2.y), deep);
+      if (deep) { e.code = E_DEPTH; return 2u; }
+      return q ? 1u : 0u;
+    }
+    case AK_INSET: {
+      bool f = false;
+      for (uint32_t k = 0; k < w2 && !f; k++) {
+        const uint32_t* el = rec + w1 + 3 * k;
+        f = prim_eq(v, uni(el[0]), uni(el[1]), uni(el[2]));
+      }
+      return f ? 1u : 0u;
+    }
+    case AK_CONTAINS: {
+      if (tag_of(v) != T_SET) { type_err(e, TN_SET, v); return 2u; }
+      const uint32_t ref = v.w0 & X_MASK, n = v.w1;
+      bool f = false;
+      for (uint32_t k = 0; k < n && !f; k++) f = prim_eq(load_val(c, rd(c, ref, 1 + 2 * k), rd(c, ref, 2 + 2 * k)), w1, w2, w3);
+      return f ? 1u : 0u;
+    }
+    case AK_LIKE:
+      if (tag_of(v) != T_STR) { type_err(e, TN_STRING, v); return 2u; }
+      return like_match(c, v.w1, rec + w1) ? 1u : 0u;
+    case AK_RECSET: {
+      const uint32_t* d = rec + w1;
+      const uint32_t nh = d[0];
+      for (uint32_t k = 0; k < nh; k++) {  // argument evaluation precedes the receiver type check
+        const uint2 hv2 = hot_get(c, d[1 + k]);
+        if (!hot_ok(hv2)) { hot_err(c, d[1 + k], hv2, e); return 2u; }
+      }
+      if (tag_of(v) != T_SET) { type_err(e, TN_SET, v); return 2u; }
+      const uint32_t ref = v.w0 & X_MASK, n = v.w1;
+      bool f = false, deep = false;
+      for (uint32_t i = 0; i < n && !f; i++) {
+        const RV x = load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i));
+        if (tag_of(x) != T_REC) continue;
+        const uint32_t* t = d + 1 + nh;
+        for (uint32_t j = 0; j < w2 && !f; j++) {
+          f = rs_rec_eq(c, rec, x, t, deep);
+          t += 1 + RS_FIELD_WORDS * t[0];
+        }
+      }
+      if (deep) { e.code = E_DEPTH; return 2u; }
+      return f ? 1u : 0u;
+    }
+    case AK_LCMP: {
+      if (tag_of(v) != T_LONG) { type_err(e, TN_LONG, v); return 2u; }
+      const int64_t x = as_i64(v), y = (int64_t)(((uint64_t)w3 << 32) | w2);
+      const bool r = w1 == 0 ? x < y : w1 == 1 ? x <= y : w1 == 2 ? x > y : x >= y;
+      return r ? 1u : 0u;
+    }
+    default: return 0u;
+  }
+}
+
+// ---- bytecode (general policies) ---------------------------------------------------------
+// Runs one policy program for the lanes with `run` set. On return run = satisfied, err = error.
+// `code` points into the LDS-staged record.
+// Register file of the bytecode machine: 24 local scalars a0..c7 (never address-taken, so
+// they stay in VGPRs) selected by wave-uniform operands through macro-expanded switches.
+#define CG_SLOT_GET(i, out) \
+  do { \
+    switch (i) { \
+      case 0: (out) = RV{a0, b0, c0}; break; \
+      case 1: (out) = RV{a1, b1, c1}; break; \
+      case 2: (out) = RV{a2, b2, c2}; break; \
+      case 3: (out) = RV{a3, b3, c3}; break; \
+      case 4: (out) = RV{a4, b4, c4}; break; \
+      case 5: (out) = RV{a5, b5, c5}; break; \
+      case 6: (out) = RV{a6, b6, c6}; break; \
+      default: (out) = RV{a7, b7, c7}; break; \
+    } \
+  } while (0)
+#define CG_SLOT_SET(i, v) \
+  do { \
+    switch (i) { \
+      case 0: a0 = (v).w0; b0 = (v).w1; c0 = (v).w2; break; \
+      case 1: a1 = (v).w0; b1 = (v).w1; c1 = (v).w2; break; \
+      case 2: a2 = (v).w0; b2 = (v).w1; c2 = (v).w2; break; \
+      case 3: a3 = (v).w0; b3 = (v).w1; c3 = (v).w2; break; \
+      case 4: a4 = (v).w0; b4 = (v).w1; c4 = (v).w2; break; \
+      case 5: a5 = (v).w0; b5 = (v).w1; c5 = (v).w2; break; \
+      case 6: a6 = (v).w0; b6 = (v).w1; c6 = (v).w2; break; \
+      default: a7 = (v).w0; b7 = (v).w1; c7 = (v).w2; break; \
+    } \
+  } while (0)
+static_assert(NSLOT == 8, "CG_SLOT_GET/SET enumerate 8 slots");
+
+__device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code, uint32_t n_ins, bool& run, bool& err,
+                                             Err& e) {
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+  uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
+  uint32_t skip = 0;
+  for (uint32_t pc = 0; pc < n_ins;) {
+    const bool on = run && skip <= pc;
+    if (__ballot(on) == 0) {
+      const uint32_t nxt = wave_min(run ? skip : 0xFFFFFFFFu);
+      if (nxt >= n_ins) break;
+      pc = nxt;
+      continue;
+    }
+    const uint2 ins = *reinterpret_cast<const uint2*>(code + 2 * pc);
+    const uint32_t w0 = uni(ins.x);
+    const uint32_t imm = uni(ins.y);
+    const uint32_t op = w0 & 0xFF, D = (w0 >> 8) & 63, A = (w0 >> 14) & 63, B = (w0 >> 20) & 63, C = w0 >> 26;
+    if (on) {
+      RV va, vb;
+      CG_SLOT_GET(A, va);
+      CG_SLOT_GET(B, vb);
+      RV out = va;
+      bool wr = true;
+      switch (op) {
+        case OP_LDV: {
+          const uint32_t o = imm == 0 ? RH_P : imm == 1 ? RH_A : imm == 2 ? RH_R : RH_CTX;
+          out = RV{c.blk[o], c.blk[o + 1], 0};
+          break;
+        }
+        case OP_LDC: out = load_val(c, c.cpool[imm], c.cpool[imm + 1]); break;
+        case OP_LDB: out = mk_bool(imm != 0); break;
+        case OP_LDS: out = RV{mk_w0(T_STR, 0), imm, 0}; break;
+        case OP_HOT: {
+          const uint2 hv = hot_get(c, C);
+          if (hot_ok(hv)) { out = load_val(c, hv.x, hv.y); break; }
+          hot_err(c, C, hv, e);
+          err = true;
+          wr = false;
+          break;
+        }
+        case OP_HOTHAS: out = mk_bool(hot_ok(hot_get(c, C))); break;
+        case OP_ATTR:
+        case OP_HAS: {
+          const uint32_t t = tag_of(va);
+          const bool has = op == OP_HAS;
+          if (t == T_ENT) {
+            const uint32_t et = va.w0 & X_MASK, ei = va.w1;
+            const uint32_t idx = find_ent(c, et, ei);
+            if (idx == NO_ENT) {
+              if (has) { out = mk_bool(false); break; }
+              e.code = E_ENTITY_MISSING; e.et = et; e.ei = ei; err = true; wr = false;
+              break;
+            }
+            const uint32_t* row = c.blk + RH_WORDS + idx * ENT_WORDS;
+            RV got;
+            const bool f = rec_get(c, RV{row[ER_ATTR0], row[ER_ATTR1], 0}, imm, got);
+            if (has) { out = mk_bool(f); break; }
+            if (!f) { e.code = E_ATTR_ENTITY; e.k = imm; e.et = et; e.ei = ei; err = true; wr = false; break; }
+            out = got;
+          } else if (t == T_REC) {
+            RV got;
+            const bool f = rec_get(c, va, imm, got);
+            if (has) { out = mk_bool(f); break; }
+            if (!f) { e.code = E_ATTR_RECORD; e.k = imm; err = true; wr = false; break; }
+            out = got;
+          } else {
+            type_err(e, TN_ENTITY_OR_RECORD, va); err = true; wr = false;
+          }
+          break;
+        }
+        case OP_EQ:
+        case OP_NE: {
+          bool deep = false;
+          const bool q = veq(c, va, vb, deep);
+          if (deep) { e.code = E_DEPTH; err = true; wr = false; break; }
+          out = mk_bool(op == OP_EQ ? q : !q);
+          break;
+        }
+        case OP_LT: case OP_LE: case OP_GT: case OP_GE:
+        case OP_ADD: case OP_SUB: case OP_MUL: {
+          if (tag_of(va) != T_LONG) { type_err(e, TN_LONG, va); err = true; wr = false; break; }
+          if (tag_of(vb) != T_LONG) { type_err(e, TN_LONG, vb); err = true; wr = false; break; }
+          const int64_t x = as_i64(va), y = as_i64(vb);
+          int64_t z = 0;
+          bool of = false;
+          switch (op) {
+            case OP_LT: out = mk_bool(x < y); break;
+            case OP_LE: out = mk_bool(x <= y); break;
+            case OP_GT: out = mk_bool(x > y); break;
+            case OP_GE: out = mk_bool(x >= y); break;
+            case OP_ADD: of = __builtin_add_overflow(x, y, &z); out = from_i64(z); break;
+            case OP_SUB: of = __builtin_sub_overflow(x, y, &z); out = from_i64(z); break;
+            default: of = __builtin_mul_overflow(x, y, &z); out = from_i64(z); break;
+          }
+          if (of) { e.code = E_OVERFLOW; err = true; wr = false; }
+          break;
+        }
+        case OP_NEG: {
+          if (tag_of(va) != T_LONG) { type_err(e, TN_LONG, va); err = true; wr = false; break; }
+          const int64_t x = as_i64(va);
+          if (x == INT64_MIN) { e.code = E_OVERFLOW; err = true; wr = false; break; }
+          out = from_i64(-x);
+          break;
+        }
+        case OP_NOT:
+          if (tag_of(va) != T_BOOL) { type_err(e, TN_BOOL, va); err = true; wr = false; break; }
+          out = mk_bool(va.w1 == 0);
+          break;
+        case OP_CHKB:
+          wr = false;
+          if (tag_of(va) != T_BOOL) { type_err(e, TN_BOOL, va); err = true; }
+          break;
+        case OP_JF:
+        case OP_JT:
+        case OP_JNF:
+          wr = false;
+          if (tag_of(va) != T_BOOL) { type_err(e, TN_BOOL, va); err = true; break; }
+          if ((op == OP_JT) == (va.w1 != 0)) skip = imm;
+          break;
+        case OP_JMP: wr = false; skip = imm; break;
+        case OP_IN: {
+          if (tag_of(va) != T_ENT) { type_err(e, TN_ENTITY, va); err = true; wr = false; break; }
+          const uint32_t et = va.w0 & X_MASK, ei = va.w1;
+          const uint32_t tb = tag_of(vb);
+          if (tb == T_ENT) { out = mk_bool(ent_in(c, et, ei, vb.w0 & X_MASK, vb.w1)); break; }
+          if (tb != T_SET) { type_err(e, TN_SET_OR_ENTITY, vb); err = true; wr = false; break; }
+          const uint32_t ref = vb.w0 & X_MASK, n = vb.w1;
+          bool bad = false;
+          for (uint32_t k = 0; k < n && !bad; k++) {
+            const RV x = load_val(c, rd(c, ref, 1 + 2 * k), rd(c, ref, 2 + 2 * k));
+            if (tag_of(x) != T_ENT) { type_err(e, TN_ENTITY, x); bad = true; }
+          }
+          if (bad) { err = true; wr = false; break; }
+          const uint32_t idx = find_ent(c, et, ei);
+          bool any = false;
+          for (uint32_t k = 0; k < n && !any; k++) {
+            const uint32_t qt = rd(c, ref, 1 + 2 * k) & X_MASK, qi = rd(c, ref, 2 + 2 * k);
+            any = (et == qt && ei == qi) || anc_has(c, idx, qt, qi);
+          }
+          out = mk_bool(any);
+          break;
+        }
+        case OP_IS:
+          if (tag_of(va) != T_ENT) { type_err(e, TN_ENTITY, va); err = true; wr = false; break; }
+          out = mk_bool((va.w0 & X_MASK) == imm);
+          break;
+        case OP_LIKE:
+          if (tag_of(va) != T_STR) { type_err(e, TN_STRING, va); err = true; wr = false; break; }
+          out = mk_bool(like_match(c, va.w1, c.cpool + imm));
+          break;
+        case OP_CONTAINS: {
+          if (tag_of(va) != T_SET) { type_err(e, TN_SET, va); err = true; wr = false; break; }
+          const uint32_t ref = va.w0 & X_MASK, n = va.w1;
+          bool deep = false, f = false;
+          for (uint32_t k = 0; k < n && !f; k++) f = veq(c, load_val(c, rd(c, ref, 1 + 2 * k), rd(c, ref, 2 + 2 * k)), vb, deep);
+          if (deep) { e.code = E_DEPTH; err = true; wr = false; break; }
+          out = mk_bool(f);
+          break;
+        }
+        case OP_CALL: {
+          if (C == CO_CONTAINS_ALL || C == CO_CONTAINS_ANY || C == CO_IS_EMPTY) {
+            if (tag_of(va) != T_SET) { type_err(e, TN_SET, va); err = true; wr = false; break; }
+            if (C == CO_IS_EMPTY) { out = mk_bool(va.w1 == 0); break; }
+            if (tag_of(vb) != T_SET) { type_err(e, TN_SET, vb); err = true; wr = false; break; }
+            const uint32_t ra = va.w0 & X_MASK, na = va.w1, rb = vb.w0 & X_MASK, nb = vb.w1;
+            bool deep = false;
+            bool all = true, any = false;
+            for (uint32_t j = 0; j < nb; j++) {
+              const RV y = load_val(c, rd(c, rb, 1 + 2 * j), rd(c, rb, 2 + 2 * j));
+              bool f = false;
+              for (uint32_t i = 0; i < na && !f; i++) f = veq(c, load_val(c, rd(c, ra, 1 + 2 * i), rd(c, ra, 2 + 2 * i)), y, deep);
+              all = all && f;
+              any = any || f;
+              if (C == CO_CONTAINS_ANY ? any : !all) break;
+            }
+            if (deep) { e.code = E_DEPTH; err = true; wr = false; break; }
+            out = mk_bool(C == CO_CONTAINS_ALL ? all : any);
+            break;
+          }
+          if (C >= CO_DEC_LT && C <= CO_DEC_GE) {
+            if (tag_of(va) != T_DEC) { type_err(e, TN_DECIMAL, va); err = true; wr = false; break; }
+            if (tag_of(vb) != T_DEC) { type_err(e, TN_DECIMAL, vb); err = true; wr = false; break; }
+            const uint32_t ra = va.w0 & X_MASK, rb = vb.w0 & X_MASK;
+            const int64_t x = (int64_t)(((uint64_t)rd(c, ra, 1) << 32) | rd(c, ra, 0));
+            const int64_t y = (int64_t)(((uint64_t)rd(c, rb, 1) << 32) | rd(c, rb, 0));
+            out = mk_bool(C == CO_DEC_LT ? x < y : C == CO_DEC_LE ? x <= y : C == CO_DEC_GT ? x > y : x >= y);
+            break;
+          }
+          // IP methods
+          if (tag_of(va) != T_IP) { type_err(e, TN_IP, va); err = true; wr = false; break; }
+          const uint32_t ra = va.w0 & X_MASK;
+          const uint32_t hdr = rd(c, ra, 0);
+          const bool v6 = (hdr & 0xFF) != 0;
+          const uint32_t a0 = rd(c, ra, 1);
+          if (C == CO_IP_V4) { out = mk_bool(!v6); break; }
+          if (C == CO_IP_V6) { out = mk_bool(v6); break; }
+          if (C == CO_IP_LOOPBACK) {
+            if (!v6) { out = mk_bool((a0 >> 24) == 127); break; }
+            out = mk_bool(a0 == 0 && rd(c, ra, 2) == 0 && rd(c, ra, 3) == 0 && rd(c, ra, 4) == 1);
+            break;
+          }
+          if (C == CO_IP_MULTICAST) {
+            out = mk_bool(v6 ? ((a0 >> 24) == 0xFF) : ((a0 >> 28) == 0xE));
+            break;
+          }
+          // isInRange(b): same family, b.prefix <= a.prefix, and a's network lies inside b's
+          if (tag_of(vb) != T_IP) { type_err(e, TN_IP, vb); err = true; wr = false; break; }
+          {
+            const uint32_t rb = vb.w0 & X_MASK;
+            const uint32_t hb = rd(c, rb, 0);
+            if ((hb & 0xFF) != (hdr & 0xFF)) { out = mk_bool(false); break; }
+            const uint32_t pa = hdr >> 8, pb = hb >> 8;
+            if (pb > pa) { out = mk_bool(false); break; }
+            const uint32_t words = v6 ? 4u : 1u;
+            bool in = true;
+            for (uint32_t k = 0; k < words; k++) {
+              const int bits = (int)pb - (int)(32 * k);
+              const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : bits <= 0 ? 0u : (0xFFFFFFFFu << (32 - bits));
+              if ((rd(c, ra, 1 + k) & mask) != (rd(c, rb, 1 + k) & mask)) in = false;
+            }
+            out = mk_bool(in);
+          }
+          break;
+        }
+        case OP_SETNEW:
+        case OP_RECNEW: {
+          const uint32_t off = imm & 0xFFFF, n = imm >> 16;
+          c.lh[off] = n;
+          out = RV{mk_w0(op == OP_SETNEW ? T_SET : T_REC, mk_ref(SP_LANE, off)), n, 0};
+          break;
+        }
+        case OP_SETPUT:
+        case OP_RECPUT: {
+          // store slot A (register form) into the container in slot D at position C
+          wr = false;
+          RV cont;
+          CG_SLOT_GET(D, cont);
+          const uint32_t base = cont.w0 & OFF_MASK, n = cont.w1;
+          const bool isrec = op == OP_RECPUT;
+          const uint32_t stride = isrec ? 3u : 2u;
+          uint32_t* slotp = c.lh + base + 1 + stride * C;
+          if (isrec) *slotp++ = imm;
+          if (tag_of(va) == T_LONG) {
+            const int64_t x = as_i64(va);
+            if (x >= INT32_MIN && x <= INT32_MAX) { slotp[0] = mk_w0(T_LONG, 0); slotp[1] = va.w1; }
+            else {
+              const uint32_t sp = base + 1 + stride * n + 2 * C;
+              c.lh[sp] = va.w1; c.lh[sp + 1] = va.w2;
+              slotp[0] = mk_w0(T_LONGREF, mk_ref(SP_LANE, sp)); slotp[1] = 0;
+            }
+          } else {
+            slotp[0] = va.w0; slotp[1] = va.w1;
+          }
+          break;
+        }
+        case OP_COND:
+          wr = false;
+          if (tag_of(va) != T_BOOL) { type_err(e, TN_BOOL, va); err = true; break; }
+          if ((C == 0) != (va.w1 != 0)) run = false;  // when-false or unless-true
+          break;
+        case OP_ERR:
+          wr = false;
+          e.code = C; e.aux = imm; err = true;
+          break;
+        default:
+          wr = false;
+          break;
+      }
+      if (err) run = false;
+      if (wr) CG_SLOT_SET(D, out);
+    }
+    pc++;
+  }
+}
+
+// ---- the kernel -----------------------------------------------------------------------------
+constexpr uint32_t CAPR_L = 8;  // reasons per lane staged in LDS before spilling to global
+
+template <bool BYTECODE>
+__global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t chunk_lds[CHUNK_WORDS];  // staged policy records
+  // per-lane reason lists of the current tier ([forbid|permit][slot][lane]); global stores inside
+  // the policy loop would serialise later heap loads behind them (in-order vmcnt)
+  __shared__ uint32_t rsn_lds[2 * CAPR_L * BLOCK];
+  extern __shared__ uint2 hot_lds[];                                          // [n_hot][BLOCK]
+  const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
+  const bool valid = gid < a.n_req;
+  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0;
+
+  uint32_t lane_scratch[LANE_WORDS];
+  Ctx c;
+  c.blk = a.heap + (valid ? a.req_base[r] : 0);
+  c.cpool = a.cpool;
+  c.lh = lane_scratch;
+  c.hot = a.hot;
+  c.gstr_off = a.gstr_off;
+  c.gstr_bytes = a.gstr_bytes;
+  c.bstr_off = a.bstr_off;
+  c.bstr_bytes = a.bstr_bytes;
+  c.n_gstr = a.n_gstr;
+  c.hotl = hot_lds + threadIdx.x;
+  c.pb0 = c.pb1 = c.pb2 = c.pb3 = 0;
+  c.rb0 = c.rb1 = c.rb2 = c.rb3 = 0;
+  c.p_anc = c.p_nanc = c.r_anc = c.r_nanc = 0;
+  uint32_t am0 = 0, am1 = 0;  // action mask over the image action table
+  if (valid) {
+    c.nent = c.blk[RH_NENT];
+    c.pt = c.blk[RH_P] & X_MASK; c.pi = c.blk[RH_P + 1];
+    c.at = c.blk[RH_A] & X_MASK; c.ai = c.blk[RH_A + 1];
+    c.rt = c.blk[RH_R] & X_MASK; c.ri = c.blk[RH_R + 1];
+    c.pidx = c.blk[RH_PIDX]; c.aidx = c.blk[RH_AIDX]; c.ridx = c.blk[RH_RIDX];
+    anc_of(c, c.pidx, c.p_anc, c.p_nanc);
+#define CG_ANC(k) \
+    c.t##k = k < c.p_nanc ? c.blk[c.p_anc + 2 * k] : 0xFFFFFFFFu; \
+    c.i##k = k < c.p_nanc ? c.blk[c.p_anc + 2 * k + 1] : 0xFFFFFFFFu;
+    CG_ANC(0) CG_ANC(1) CG_ANC(2) CG_ANC(3) CG_ANC(4) CG_ANC(5) CG_ANC(6) CG_ANC(7)
+#undef CG_ANC
+    anc_of(c, c.ridx, c.r_anc, c.r_nanc);
+    // ancestor-or-self Bloom filters of principal and resource
+    bloom_add(c.pb0, c.pb1, c.pb2, c.pb3, uid_bloom_bit(c.pt, c.pi));
+    for (uint32_t k = 0; k < c.p_nanc; k++)
+      bloom_add(c.pb0, c.pb1, c.pb2, c.pb3, uid_bloom_bit(c.blk[c.p_anc + 2 * k], c.blk[c.p_anc + 2 * k + 1]));
+    bloom_add(c.rb0, c.rb1, c.rb2, c.rb3, uid_bloom_bit(c.rt, c.ri));
+    for (uint32_t k = 0; k < c.r_nanc; k++)
+      bloom_add(c.rb0, c.rb1, c.rb2, c.rb3, uid_bloom_bit(c.blk[c.r_anc + 2 * k], c.blk[c.r_anc + 2 * k + 1]));
+  } else {
+    c.nent = 0; c.pt = c.pi = c.at = c.ai = c.rt = c.ri = 0xFFFFFFFFu;
+    c.t0 = c.t1 = c.t2 = c.t3 = c.t4 = c.t5 = c.t6 = c.t7 = 0xFFFFFFFFu;
+    c.i0 = c.i1 = c.i2 = c.i3 = c.i4 = c.i5 = c.i6 = c.i7 = 0xFFFFFFFFu;
+    c.pidx = c.aidx = c.ridx = NO_ENT;
+  }
+  if (a.amask_ok) {
+    uint32_t a_off = 0, a_n = 0;
+    if (valid) anc_of(c, c.aidx, a_off, a_n);
+    const uint32_t n_act = a.n_act;
+    for (uint32_t k = 0; k < n_act; k++) {
+      const uint32_t qt = uni(a.act[2 * k]), qi = uni(a.act[2 * k + 1]);
+      const bool hit = valid && ((c.at == qt && c.ai == qi) || (a_n && anc_scan(c.blk, a_off, a_n, qt, qi)));
+      if (hit) { if (k < 32) am0 |= 1u << k; else am1 |= 1u << (k - 32); }
+    }
+  }
+  // pre-resolve hot (var, attribute) pairs into LDS: value, or the error ATTR would raise
+  const uint32_t n_hot = a.n_hot;
+  for (uint32_t h = 0; h < n_hot; h++) {
+    const uint32_t var = uni(a.hot[2 * h]), key = uni(a.hot[2 * h + 1]);
+    uint2 v = make_uint2(mk_w0(T_NONE, E_ENTITY_MISSING), 0);
+    if (valid) {
+      if (var == 3) {
+        if (!rec_get_heap(c.blk, c.blk[RH_CTX], c.blk[RH_CTX + 1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_RECORD), 0);
+      } else {
+        const uint32_t idx = pick3(var, c.pidx, c.aidx, c.ridx);
+        if (idx != NO_ENT) {
+          const uint32_t* row = c.blk + RH_WORDS + idx * ENT_WORDS;
+          if (!rec_get_heap(c.blk, row[ER_ATTR0], row[ER_ATTR1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_ENTITY), 0);
+        }
+      }
+    }
+    c.hotl[h * BLOCK] = v;
+  }
+
+  bool decided = !valid;
+  uint32_t cbeg = 0;
+  const uint32_t n_tiers = a.n_tiers;
+  for (uint32_t t = 0; t < n_tiers; t++) {
+    const uint32_t cend = uni(a.tier_cend[t]);
+    uint32_t nf = 0, np = 0, ne = 0;
+    for (uint32_t ch = cbeg; ch < cend; ch++) {
+      // stage the chunk's policy records in LDS (block-cooperative, coalesced 16-byte loads)
+      const uint32_t c_off = uni(a.chunks[4 * ch]), c_nw = uni(a.chunks[4 * ch + 1]);
+      const uint32_t c_p0 = uni(a.chunks[4 * ch + 2]), c_p1 = uni(a.chunks[4 * ch + 3]);
+      if (!__syncthreads_or(!decided)) break;  // whole block decided: later chunks/tiers are moot
+      {
+        const uint4* src = reinterpret_cast<const uint4*>(a.pstream + c_off);
+        uint4* dst = reinterpret_cast<uint4*>(chunk_lds);
+        for (uint32_t k = threadIdx.x; k < (c_nw >> 2); k += BLOCK) dst[k] = src[k];
+      }
+      __syncthreads();
+      if (__ballot(!decided) == 0) continue;  // this wave is done; keep joining the barriers
+      uint32_t rw = 0;                         // record offset inside the chunk (words)
+      for (uint32_t p = c_p0; p < c_p1; p++) {
+        const uint32_t* rec = chunk_lds + rw;
+        const uint4* d4 = reinterpret_cast<const uint4*>(rec);
+        const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+        const uint32_t flags = uni(q0.x), kinds = uni(q0.y);
+        const uint32_t p_ty = uni(q0.z), p_et = uni(q0.w), p_ei = uni(q1.x);
+        const uint32_t a_et = uni(q1.y), a_ei = uni(q1.z);
+        const uint32_t r_ty = uni(q1.w), r_et = uni(q2.x), r_ei = uni(q2.y);
+        const uint32_t n_code = uni(q2.w), n_atom = uni(q3.x);
+        const uint32_t am0p = uni(q3.z), am1p = uni(q3.w);
+        rw += (POL_WORDS + n_code + 3) & ~3u;
+        const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
+        bool ok = !decided;
+        // action scope: one AND against the per-request action mask
+        if (ak != SK_ANY) {
+          if (a.amask_ok) {
+            ok = ok && (((am0 & am0p) | (am1 & am1p)) != 0);
+          } else if (ak == SK_EQ) {
+            ok = ok && c.at == a_et && c.ai == a_ei;
+          } else if (ak == SK_IN) {
+            ok = ok && ((c.at == a_et && c.ai == a_ei) || anc_has(c, c.aidx, a_et, a_ei));
+          } else {
+            bool any = false;
+            for (uint32_t k = 0; k < a_et; k++) {
+              const uint32_t qt = uni(a.cpool[a_ei + 2 * k]), qi = uni(a.cpool[a_ei + 2 * k + 1]);
+              any = any || (c.at == qt && c.ai == qi) || anc_has(c, c.aidx, qt, qi);
+            }
+            ok = ok && any;
+          }
+        }
+        // principal scope (type test, then Bloom-gated ancestor test)
+        if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == p_ty;
+        if (pk == SK_EQ) ok = ok && c.pt == p_et && c.pi == p_ei;
+        else if (pk == SK_IN || pk == SK_ISIN) ok = ok && p_in(c, p_et, p_ei, (flags >> 16) & 0x7F);
+        // resource scope
+        if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == r_ty;
+        if (rk == SK_EQ) ok = ok && c.rt == r_et && c.ri == r_ei;
+        else if (rk == SK_IN || rk == SK_ISIN) ok = ok && r_in(c, r_et, r_ei, (flags >> 24) & 0x7F);
+        if (__ballot(ok) == 0) continue;
+
+        // ---- conditions ----
+        bool run = ok;
+        bool err = false;
+        Err e{0, 0, 0, 0, 0};
+        if (flags & PF_ATOMIC) {
+          bool cur = true;
+          for (uint32_t i = 0; i < n_atom; i += ATOM_WORDS) {
+            if (__ballot(run) == 0) break;
+            const uint4 at = *reinterpret_cast<const uint4*>(rec + POL_WORDS + i);
+            const uint32_t w0 = uni(at.x), w1 = uni(at.y), w2 = uni(at.z), w3 = uni(at.w);
+            const uint32_t af = w0 >> 16;
+            if (af & AF_START) cur = !(af & AF_OR);
+            if (run && ((af & AF_OR) ? !cur : cur)) {
+              const uint32_t rr = eval_atom(c, rec, w0 & 0xFF, (w0 >> 8) & 0xFF, w1, w2, w3, e);
+              if (rr == 2u) { err = true; run = false; }
+              else cur = (rr != 0u) != ((af & AF_NEG) != 0);
+            }
+            if ((af & AF_END) && run && (((af & AF_UNLESS) != 0) == cur)) run = false;
+          }
+        } else if constexpr (BYTECODE) {
+          run_bytecode(c, rec + POL_WORDS, n_code >> 1, run, err, e);
+        }
+        // ---- record outcome ----
+        if (ok) {
+          if (err) {
+            if (ne < a.cape) {
+              uint32_t* er = a.errs + ((size_t)gid * a.cape + ne) * ERR_WORDS;
+              er[0] = p; er[1] = e.code | (e.aux << 8); er[2] = e.k; er[3] = e.et; er[4] = e.ei; er[5] = 0;
+            }
+            ne++;
+          } else if (run) {
+            if (flags & PF_FORBID) {
+              if (nf < CAPR_L) rsn_lds[nf * BLOCK + threadIdx.x] = p;
+              else if (nf < a.capr) a.reasons_f[(size_t)gid * a.capr + nf] = p;
+              nf++;
+            } else {
+              if (np < CAPR_L) rsn_lds[(CAPR_L + np) * BLOCK + threadIdx.x] = p;
+              else if (np < a.capr) a.reasons_p[(size_t)gid * a.capr + np] = p;
+              np++;
+            }
+          }
+        }
+      }
+    }
+    if (!decided) {
+      if (t + 1 == n_tiers || nf || np || ne) {
+        const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);
+        const uint32_t nr = nf ? nf : np;
+        uint32_t fl = RF_VALID | (nf ? RF_FORBID : 0u);
+        if (nr > a.capr || ne > a.cape) fl |= RF_OVERFLOW;
+        // flush the LDS-staged reasons of the deciding list
+        const uint32_t nflush = min(min(nr, a.capr), CAPR_L);
+        uint32_t* dst = (nf ? a.reasons_f : a.reasons_p) + (size_t)gid * a.capr;
+        const uint32_t lbase = nf ? 0u : CAPR_L;
+        for (uint32_t k = 0; k < nflush; k++) dst[k] = rsn_lds[(lbase + k) * BLOCK + threadIdx.x];
+        a.res[2 * (size_t)gid] = dec | (t << 8) | (fl << 16);
+        a.res[2 * (size_t)gid + 1] = min(nr, 0xFFFFu) | (min(ne, 0xFFFFu) << 16);
+        decided = true;
+      }
+    }
+    cbeg = cend;
+  }
+}
+
+thread_local std::string g_err;
+
+int fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return -5;  // CG_E_DEVICE
+}
+
+#define HIPCHK(x, what)                        \
+  do {                                         \
+    hipError_t _e = (x);                       \
+    if (_e != hipSuccess) return fail(_e, what); \
+  } while (0)
+
+template <class T>
+int up(T** dst, const std::vector<T>& src, size_t& bytes, hipStream_t s) {
+  size_t n = std::max<size_t>(src.size(), 1) * sizeof(T);
+  HIPCHK(hipMalloc((void**)dst, n), "hipMalloc");
+  bytes += n;
+  if (!src.empty()) HIPCHK(hipMemcpyAsync(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  return 0;
+}
+
+}  // namespace
+
+namespace cg {
+
+const char* dev_last_error() { return g_err.c_str(); }
+
+int dev_count(int* n) {
+  HIPCHK(hipGetDeviceCount(n), "hipGetDeviceCount");
+  return 0;
+}
+
+int dev_select(int device) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  return 0;
+}
+
+int dev_synchronize(int device) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  HIPCHK(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return 0;
+}
+
+int dev_stream_create(int device, void** stream) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  hipStream_t s;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  *stream = (void*)s;
+  return 0;
+}
+void dev_stream_destroy(void* stream) { if (stream) (void)hipStreamDestroy((hipStream_t)stream); }
+int dev_stream_sync(void* stream) {
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+  return 0;
+}
+
+int dev_image_upload(int device, const Image& img, DevImage* out) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  DevImage d;
+  d.device = device;
+  hipStream_t s = nullptr;
+  int rc;
+  if ((rc = up(&d.pstream, img.pstream, d.bytes, s))) return rc;
+  if ((rc = up(&d.tier_cend, img.tier_cend, d.bytes, s))) return rc;
+  if ((rc = up(&d.chunks, img.chunks, d.bytes, s))) return rc;
+  if ((rc = up(&d.cpool, img.cpool, d.bytes, s))) return rc;
+  if ((rc = up(&d.gstr_off, img.gstr_off, d.bytes, s))) return rc;
+  if ((rc = up(&d.hot, img.hot, d.bytes, s))) return rc;
+  if ((rc = up(&d.act, img.act, d.bytes, s))) return rc;
+  d.n_act = (uint32_t)img.act.size() / 2;
+  d.has_bytecode = img.n_atomic < img.n_pol() ? 1u : 0u;
+  d.amask_ok = img.amask_ok;
+  if ((rc = up(&d.gstr_bytes, img.gstr_bytes, d.bytes, s))) return rc;
+  HIPCHK(hipStreamSynchronize(s), "sync image upload");
+  d.n_pol = img.n_pol();
+  d.n_tiers = img.n_tiers();
+  d.n_gstr = img.n_gstr();
+  d.n_hot = (uint32_t)img.hot.size() / 2;
+  *out = d;
+  return 0;
+}
+
+void dev_image_free(DevImage* d) {
+  if (d->device < 0) return;
+  (void)hipSetDevice(d->device);
+  for (void* p : {(void*)d->pstream, (void*)d->tier_cend, (void*)d->chunks, (void*)d->cpool, (void*)d->gstr_off,
+                  (void*)d->hot, (void*)d->act, (void*)d->gstr_bytes})
+    if (p) (void)hipFree(p);
+  *d = DevImage();
+}
+
+int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  DevBatch d;
+  d.device = device;
+  d.n = b.n();
+  d.heap_words = b.heap.size();
+  int rc;
+  if ((rc = up(&d.heap, b.heap, d.bytes, s))) return rc;
+  if ((rc = up(&d.req_base, b.req_base, d.bytes, s))) return rc;
+  if ((rc = up(&d.bstr_off, b.bstr_off, d.bytes, s))) return rc;
+  if ((rc = up(&d.bstr_bytes, b.bstr_bytes, d.bytes, s))) return rc;
+  const size_t n = std::max<uint32_t>(b.n(), 1);
+  d.capr = b.capr;
+  d.cape = b.cape;
+  HIPCHK(hipMalloc((void**)&d.res, n * 2 * 4), "hipMalloc res");
+  HIPCHK(hipMalloc((void**)&d.reasons_f, n * d.capr * 4), "hipMalloc reasons");
+  HIPCHK(hipMalloc((void**)&d.reasons_p, n * d.capr * 4), "hipMalloc reasons");
+  HIPCHK(hipMalloc((void**)&d.errs, n * d.cape * ERR_WORDS * 4), "hipMalloc errs");
+  HIPCHK(hipMemsetAsync(d.res, 0, n * 2 * 4, s), "memset res");
+  d.bytes += n * (2 + 2 * d.capr + d.cape * ERR_WORDS) * 4;
+  *out = d;
+  return 0;
+}
+
+void dev_batch_free(DevBatch* d) {
+  if (d->device < 0) return;
+  (void)hipSetDevice(d->device);
+  for (void* p : {(void*)d->heap, (void*)d->req_base, (void*)d->req_idx, (void*)d->bstr_off, (void*)d->bstr_bytes,
+                  (void*)d->res, (void*)d->reasons_f, (void*)d->reasons_p, (void*)d->errs})
+    if (p) (void)hipFree(p);
+  *d = DevBatch();
+}
+
+static size_t lds_bytes(const DevImage& img) { return (size_t)std::max<uint32_t>(img.n_hot, 1) * BLOCK * sizeof(uint2); }
+
+static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* req_idx, uint32_t n, uint32_t* res,
+                       uint32_t* rf, uint32_t* rp, uint32_t* er, uint32_t capr, uint32_t cape) {
+  KArgs k;
+  k.pstream = img.pstream; k.tier_cend = img.tier_cend; k.chunks = img.chunks; k.cpool = img.cpool;
+  k.gstr_off = img.gstr_off; k.gstr_bytes = img.gstr_bytes; k.hot = img.hot;
+  k.heap = b.heap; k.req_base = b.req_base; k.req_idx = req_idx;
+  k.bstr_off = b.bstr_off; k.bstr_bytes = b.bstr_bytes;
+  k.res = res; k.reasons_f = rf; k.reasons_p = rp; k.errs = er;
+  k.n_pol = img.n_pol; k.n_tiers = img.n_tiers; k.n_gstr = img.n_gstr; k.n_hot = img.n_hot;
+  k.act = img.act; k.n_act = img.n_act; k.amask_ok = img.amask_ok;
+  k.n_req = n; k.capr = capr; k.cape = cape;
+  return k;
+}
+
+int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  if (b.n == 0) return 0;
+  if (img.device != b.device) { g_err = "image and batch live on different devices"; return -2; }
+  KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
+  hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((b.n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), (hipStream_t)stream, k);
+  HIPCHK(hipGetLastError(), "launch");
+  return 0;
+}
+
+// Re-evaluates a subset of requests (overflowed result lists) with larger capacities; results are
+// compact in subset order and copied to host before returning.
+int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
+                    uint32_t cape, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
+                    std::vector<uint32_t>& rp, std::vector<uint32_t>& er) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return 0;
+  for (uint32_t i = 0; i < n; i++) if (idx[i] >= b.n) { g_err = "request index out of range"; return -2; }
+  uint32_t *d_idx = nullptr, *d_res = nullptr, *d_rf = nullptr, *d_rp = nullptr, *d_er = nullptr;
+  int rc = 0;
+  auto cleanup = [&]() { for (void* p : {(void*)d_idx, (void*)d_res, (void*)d_rf, (void*)d_rp, (void*)d_er}) if (p) (void)hipFree(p); };
+  do {
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_idx, (size_t)n * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
+    if ((e = hipMalloc((void**)&d_res, (size_t)n * 2 * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
+    if ((e = hipMalloc((void**)&d_rf, (size_t)n * capr * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
+    if ((e = hipMalloc((void**)&d_rp, (size_t)n * capr * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
+    if ((e = hipMalloc((void**)&d_er, (size_t)n * cape * ERR_WORDS * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
+    if ((e = hipMemcpyAsync(d_idx, idx, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) { rc = fail(e, "H2D"); break; }
+    KArgs k = make_args(img, b, d_idx, n, d_res, d_rf, d_rp, d_er, capr, cape);
+    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
+    if ((e = hipGetLastError()) != hipSuccess) { rc = fail(e, "launch"); break; }
+    res.resize((size_t)n * 2); rf.resize((size_t)n * capr); rp.resize((size_t)n * capr); er.resize((size_t)n * cape * ERR_WORDS);
+    if ((e = hipMemcpyAsync(res.data(), d_res, res.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
+    if ((e = hipMemcpyAsync(rf.data(), d_rf, rf.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
+    if ((e = hipMemcpyAsync(rp.data(), d_rp, rp.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
+    if ((e = hipMemcpyAsync(er.data(), d_er, er.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) { rc = fail(e, "sync"); break; }
+  } while (0);
+  cleanup();
+  return rc;
+}
+
+int dev_download(const DevBatch& b, Batch& host, void* stream) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = b.n;
+  host.capr = b.capr;
+  host.cape = b.cape;
+  host.res.resize(n * 2);
+  host.reasons_f.resize(n * b.capr);
+  host.reasons_p.resize(n * b.capr);
+  host.errs.resize(n * b.cape * ERR_WORDS);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(host.res.data(), b.res, n * 2 * 4, hipMemcpyDeviceToHost, s), "D2H res");
+    HIPCHK(hipMemcpyAsync(host.reasons_f.data(), b.reasons_f, n * b.capr * 4, hipMemcpyDeviceToHost, s), "D2H");
+    HIPCHK(hipMemcpyAsync(host.reasons_p.data(), b.reasons_p, n * b.capr * 4, hipMemcpyDeviceToHost, s), "D2H");
+    HIPCHK(hipMemcpyAsync(host.errs.data(), b.errs, n * b.cape * ERR_WORDS * 4, hipMemcpyDeviceToHost, s), "D2H");
+  }
+  HIPCHK(hipStreamSynchronize(s), "sync download");
+  return 0;
+}
+
+int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_total) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0), "event");
+  HIPCHK(hipEventCreate(&e1), "event");
+  KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
+  HIPCHK(hipEventRecord(e0, s), "event record");
+  for (uint32_t i = 0; i < iters; i++)
+    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((b.n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
+  HIPCHK(hipGetLastError(), "launch");
+  HIPCHK(hipEventRecord(e1, s), "event record");
+  HIPCHK(hipEventSynchronize(e1), "event sync");
+  HIPCHK(hipEventElapsedTime(ms_total, e0, e1), "elapsed");
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 0;
+}
+
+}  // namespace cg

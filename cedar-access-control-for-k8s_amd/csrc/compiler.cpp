@@ -195,41 +195,41 @@ struct Compiler {
     return (uint32_t)I.ext_msgs.size() - 1;
   }
 
-  uint32_t pattern(const std::vector<PatPiece>& pat) {
+  // `like` pattern -> [flags (bit0 star, bits 8.. #middles), prefix, suffix, middles...], each
+  // literal as [len, bytes packed 4 per word]. Appended to `dst`; returns its offset there.
+  static uint32_t pattern_into(const std::vector<PatPiece>& pat, std::vector<uint32_t>& dst) {
     // collapse into literal runs separated by stars
     std::vector<std::string> lits;
     bool has_star = false;
-    std::string cur;
-    bool lead_star = !pat.empty() && pat[0].star;
-    (void)lead_star;
     lits.push_back("");
     for (auto& p : pat) {
       if (p.star) { has_star = true; lits.push_back(""); }
       else lits.back() += p.lit;
     }
     // lits[0] = prefix, lits.back() = suffix (when has_star), middles between (empty ones dropped)
-    uint32_t off = (uint32_t)I.cpool.size();
-    auto put_lit = [this](const std::string& s) {
-      I.cpool.push_back((uint32_t)s.size());
+    uint32_t off = (uint32_t)dst.size();
+    auto put_lit = [&dst](const std::string& s) {
+      dst.push_back((uint32_t)s.size());
       for (size_t k = 0; k < s.size(); k += 4) {
         uint32_t w = 0;
         for (size_t j = 0; j < 4 && k + j < s.size(); j++) w |= (uint32_t)(uint8_t)s[k + j] << (8 * j);
-        I.cpool.push_back(w);
+        dst.push_back(w);
       }
     };
     if (!has_star) {
-      I.cpool.push_back(0);  // flags: no star, 0 middles
+      dst.push_back(0);  // flags: no star, 0 middles
       put_lit(lits[0]);
       return off;
     }
     std::vector<std::string> mids;
     for (size_t k = 1; k + 1 < lits.size(); k++) if (!lits[k].empty()) mids.push_back(lits[k]);
-    I.cpool.push_back(1u | ((uint32_t)mids.size() << 8));
+    dst.push_back(1u | ((uint32_t)mids.size() << 8));
     put_lit(lits[0]);
     put_lit(lits.back());
     for (auto& m : mids) put_lit(m);
     return off;
   }
+  uint32_t pattern(const std::vector<PatPiece>& pat) { return pattern_into(pat, I.cpool); }
 
   void compile(const Expr& e, uint32_t d) {
     slot(d);
@@ -376,6 +376,251 @@ struct Compiler {
     for (auto& k : e.kids) count_hot(*k, cnt);
   }
 
+  // ---- atoms ----------------------------------------------------------------------------------
+  int hot_of(const Expr& e) {  // e is Attr/Has over a Var
+    if ((e.k != EK::Attr && e.k != EK::Has) || e.kids[0]->k != EK::Var) return -1;
+    auto it = hot.find({(uint32_t)var_index(e.kids[0]->name), intern(e.name)});
+    return it == hot.end() ? -1 : (int)it->second;
+  }
+  static bool is_prim(const HVal& v) { return v.k == VK::Bool || v.k == VK::Long || v.k == VK::Str || v.k == VK::Ent; }
+  void reg_form(const HVal& v, uint32_t* w) {
+    switch (v.k) {
+      case VK::Bool: w[0] = mk_w0(T_BOOL, 0); w[1] = v.b ? 1 : 0; w[2] = 0; break;
+      case VK::Long: w[0] = mk_w0(T_LONG, 0); w[1] = (uint32_t)((uint64_t)v.i & 0xFFFFFFFFu); w[2] = (uint32_t)((uint64_t)v.i >> 32); break;
+      case VK::Str: w[0] = mk_w0(T_STR, 0); w[1] = intern(v.s); w[2] = 0; break;
+      default: w[0] = mk_w0(T_ENT, intern(v.etype)); w[1] = intern(v.s); w[2] = 0; break;
+    }
+  }
+  bool lit_prim(const Expr& e, HVal& v) {
+    if (e.k == EK::Lit && is_prim(e.lit)) { v = e.lit; return true; }
+    return false;
+  }
+  // One clause element -> one atom (4 words) or false.
+  bool atom(const Expr& e0, uint32_t flags, std::vector<uint32_t>& out) {
+    const Expr* e = &e0;
+    while (e->k == EK::Not) { flags ^= AF_NEG; e = e->kids[0].get(); }
+    uint32_t w[4] = {0, 0, 0, 0};
+    auto put = [&](uint32_t kind, uint32_t h) {
+      w[0] = kind | (h << 8) | (flags << 16);
+      out.insert(out.end(), w, w + 4);
+      return true;
+    };
+    HVal c;
+    int h;
+    switch (e->k) {
+      case EK::Has:
+        if ((h = hot_of(*e)) < 0) return false;
+        return put(AK_HAS, (uint32_t)h);
+      case EK::Attr:
+        if ((h = hot_of(*e)) < 0) return false;
+        return put(AK_BOOL, (uint32_t)h);
+      case EK::Like:
+        if ((h = hot_of(*e->kids[0])) < 0 || e->kids[0]->k != EK::Attr) return false;
+        w[1] = pattern_into(e->pat, adata);
+        apatch.push_back(out.size() + 1);
+        return put(AK_LIKE, (uint32_t)h);
+      case EK::Is:
+        if (e->has_in || e->kids[0]->k != EK::Var || e->kids[0]->name == "context") return false;
+        w[1] = intern(e->name);
+        return put(AK_IS, (uint32_t)var_index(e->kids[0]->name));
+      case EK::Method: {
+        if (e->name == "contains" && e->kids.size() == 2 && e->kids[1]->k != EK::Rec) {
+        const Expr& recv = *e->kids[0];
+        const Expr& arg = *e->kids[1];
+        HVal s;
+        if (recv.k == EK::Set && fold(recv, s)) {
+          if (arg.k != EK::Attr || (h = hot_of(arg)) < 0) return false;
+          for (auto& x : s.elems) if (!is_prim(x)) return false;
+          uint32_t off = (uint32_t)adata.size();
+          for (auto& x : s.elems) { uint32_t r[3]; reg_form(x, r); adata.insert(adata.end(), r, r + 3); }
+          w[1] = off;
+          w[2] = (uint32_t)s.elems.size();
+          apatch.push_back(out.size() + 1);
+          return put(AK_INSET, (uint32_t)h);
+        }
+        if (recv.k == EK::Attr && (h = hot_of(recv)) >= 0 && lit_prim(arg, c)) {
+          reg_form(c, &w[1]);
+          return put(AK_CONTAINS, (uint32_t)h);
+        }
+        return false;
+      }
+      if (e->name == "containsAny" || e->name == "contains") {
+        // label-selector shape: hot.containsAny([{k: lit|hot|[lit|hot..]}, ..]) / hot.contains({..})
+        if (e->kids.size() != 2) return false;
+        const Expr& recv = *e->kids[0];
+        const Expr& arg = *e->kids[1];
+        if (recv.k != EK::Attr || (h = hot_of(recv)) < 0) return false;
+        std::vector<const Expr*> tmpls;
+        if (e->name == "contains") {
+          if (arg.k != EK::Rec) return false;
+          tmpls.push_back(&arg);
+        } else {
+          if (arg.k != EK::Set) return false;
+          for (auto& k : arg.kids) {
+            if (k->k != EK::Rec) return false;
+            tmpls.push_back(k.get());
+          }
+        }
+        std::vector<uint32_t> holes, body;
+        std::vector<std::pair<size_t, uint32_t>> setlits;  // (body index of field word a, body offset of list)
+        std::vector<uint32_t> lists;
+        auto elem = [&](const Expr& x, uint32_t* o) {  // o: kind + 3 operand words
+          HVal v;
+          int hh;
+          if (lit_prim(x, v)) { o[0] = RF_CONST; reg_form(v, o + 1); return true; }
+          if (x.k == EK::Attr && (hh = hot_of(x)) >= 0) {
+            o[0] = RF_HOLE; o[1] = (uint32_t)hh; o[2] = o[3] = 0;
+            holes.push_back((uint32_t)hh);
+            return true;
+          }
+          return false;
+        };
+        for (const Expr* t : tmpls) {
+          const uint32_t n = (uint32_t)t->kids.size();
+          std::vector<std::pair<uint32_t, std::array<uint32_t, 5>>> fields;
+          for (uint32_t i = 0; i < n; i++) {  // source order: holes are evaluated in this order
+            std::array<uint32_t, 5> f{intern(t->keys[i]), 0, 0, 0, 0};
+            const Expr& x = *t->kids[i];
+            if (x.k == EK::Set) {
+              f[1] = RF_SETLIT;
+              f[2] = (uint32_t)lists.size();  // patched below
+              f[3] = (uint32_t)x.kids.size();
+              for (auto& el : x.kids) {
+                uint32_t o[4];
+                if (!elem(*el, o)) return false;
+                lists.insert(lists.end(), o, o + 4);
+              }
+            } else {
+              uint32_t o[4];
+              if (!elem(x, o)) return false;
+              f[1] = o[0]; f[2] = o[1]; f[3] = o[2]; f[4] = o[3];
+            }
+            fields.emplace_back(f[0], f);
+          }
+          std::sort(fields.begin(), fields.end(), [](auto& a, auto& b) { return a.first < b.first; });
+          body.push_back(n);
+          for (auto& f : fields) {
+            if (f.second[1] == RF_SETLIT) setlits.emplace_back(body.size() + 2, f.second[2]);
+            body.insert(body.end(), f.second.begin(), f.second.end());
+          }
+        }
+        // data = [holes][templates][element lists]; offsets relative to the data start for now
+        const uint32_t off = (uint32_t)adata.size();
+        const uint32_t hdr = 1 + (uint32_t)holes.size();
+        const uint32_t lists_at = off + hdr + (uint32_t)body.size();
+        for (auto& sl : setlits) body[sl.first] = lists_at + sl.second;
+        adata.push_back((uint32_t)holes.size());
+        adata.insert(adata.end(), holes.begin(), holes.end());
+        adata.insert(adata.end(), body.begin(), body.end());
+        adata.insert(adata.end(), lists.begin(), lists.end());
+        for (auto& sl : setlits) rs_patch.push_back(off + hdr + (uint32_t)sl.first);
+        w[1] = off;
+        w[2] = (uint32_t)tmpls.size();
+        w[3] = e->name == "contains" ? 1u : 0u;
+        apatch.push_back(out.size() + 1);
+        return put(AK_RECSET, (uint32_t)h);
+      }
+      return false;
+      }
+      case EK::Bin: {
+        const Expr& l = *e->kids[0];
+        const Expr& r = *e->kids[1];
+        if (e->op == BinOp::Eq || e->op == BinOp::Ne) {
+          if (e->op == BinOp::Ne) flags ^= AF_NEG;
+          if (l.k == EK::Attr && (h = hot_of(l)) >= 0 && lit_prim(r, c)) { reg_form(c, &w[1]); return put(AK_EQ, (uint32_t)h); }
+          if (r.k == EK::Attr && (h = hot_of(r)) >= 0 && lit_prim(l, c)) { reg_form(c, &w[1]); return put(AK_EQ, (uint32_t)h); }
+          int h2;
+          if (l.k == EK::Attr && r.k == EK::Attr && (h = hot_of(l)) >= 0 && (h2 = hot_of(r)) >= 0) {
+            w[1] = (uint32_t)h2;
+            return put(AK_EQH, (uint32_t)h);
+          }
+          return false;
+        }
+        if (e->op == BinOp::In) {
+          if (l.k != EK::Var || l.name == "context" || !lit_prim(r, c) || c.k != VK::Ent) return false;
+          w[1] = intern(c.etype);
+          w[2] = intern(c.s);
+          w[3] = uid_bloom_bit(w[1], w[2]);
+          return put(AK_IN, (uint32_t)var_index(l.name));
+        }
+        if (e->op == BinOp::Lt || e->op == BinOp::Le || e->op == BinOp::Gt || e->op == BinOp::Ge) {
+          static const uint32_t code[] = {0, 1, 2, 3};
+          static const uint32_t mirror[] = {2, 3, 0, 1};
+          uint32_t op = code[(int)e->op - (int)BinOp::Lt];
+          if (l.k == EK::Attr && (h = hot_of(l)) >= 0 && lit_prim(r, c) && c.k == VK::Long) {
+          } else if (r.k == EK::Attr && (h = hot_of(r)) >= 0 && lit_prim(l, c) && c.k == VK::Long) {
+            op = mirror[op];
+          } else {
+            return false;
+          }
+          w[1] = op;
+          w[2] = (uint32_t)((uint64_t)c.i & 0xFFFFFFFFu);
+          w[3] = (uint32_t)((uint64_t)c.i >> 32);
+          return put(AK_LCMP, (uint32_t)h);
+        }
+        return false;
+      }
+      default: return false;
+    }
+  }
+  static void flatten(const Expr& e, EK kind, std::vector<const Expr*>& out) {
+    if (e.k == kind) { flatten(*e.kids[0], kind, out); flatten(*e.kids[1], kind, out); }
+    else out.push_back(&e);
+  }
+  // All when/unless clauses as atom chains, or false (then the policy uses bytecode).
+  // Output: atoms, then their data (INSET element triples, LIKE patterns) addressed relative to
+  // the policy record start; *n_atom_words = words of atoms proper.
+  std::vector<uint32_t> adata;
+  std::vector<size_t> apatch;
+  std::vector<uint32_t> rs_patch;  // adata words holding adata-relative offsets
+  bool atoms(const Policy& p, std::vector<uint32_t>& out, uint32_t* n_atom_words) {
+    adata.clear();
+    apatch.clear();
+    rs_patch.clear();
+    for (auto& c : p.conds) {
+      const Expr& root = *c.second;
+      std::vector<const Expr*> elems;
+      uint32_t base = c.first ? 0u : (uint32_t)AF_UNLESS;
+      if (root.k == EK::Or) { flatten(root, EK::Or, elems); base |= AF_OR; }
+      else flatten(root, EK::And, elems);
+      for (size_t i = 0; i < elems.size(); i++) {
+        uint32_t f = base | (i == 0 ? (uint32_t)AF_START : 0u) | (i + 1 == elems.size() ? (uint32_t)AF_END : 0u);
+        if (!atom(*elems[i], f, out)) return false;
+      }
+    }
+    *n_atom_words = (uint32_t)out.size();
+    const uint32_t base = POL_WORDS + (uint32_t)out.size();
+    for (size_t k : apatch) out[k] += base;
+    for (uint32_t k : rs_patch) adata[k] += base;
+    out.insert(out.end(), adata.begin(), adata.end());
+    return true;
+  }
+
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> act_index;  // action entity -> bit
+  void collect_actions(const Scope& s) {
+    auto add = [this](const std::pair<std::string, std::string>& e) {
+      std::pair<uint32_t, uint32_t> k{intern(e.first), intern(e.second)};
+      if (!act_index.count(k)) {
+        act_index.emplace(k, (uint32_t)act_index.size());
+        I.act.push_back(k.first);
+        I.act.push_back(k.second);
+      }
+    };
+    if (s.kind == ScopeKind::Eq || s.kind == ScopeKind::In) add(s.ent);
+    if (s.kind == ScopeKind::InSet) for (auto& e : s.ents) add(e);
+  }
+  uint64_t action_mask(const Scope& s) {
+    if (s.kind == ScopeKind::Any) return ~0ull;
+    uint64_t m = 0;
+    auto bit = [&](const std::pair<std::string, std::string>& e) {
+      uint32_t b = act_index.at({intern(e.first), intern(e.second)});
+      if (b < 64) m |= 1ull << b;
+    };
+    if (s.kind == ScopeKind::InSet) for (auto& e : s.ents) bit(e);
+    else bit(s.ent);
+    return m;
+  }
+
   void scope_words(const Scope& s, uint32_t* w_type, uint32_t* w_et, uint32_t* w_ei) {
     if (s.kind == ScopeKind::Is || s.kind == ScopeKind::IsIn) *w_type = intern(s.etype);
     if (s.kind == ScopeKind::Eq || s.kind == ScopeKind::In || s.kind == ScopeKind::IsIn) {
@@ -402,16 +647,32 @@ struct Compiler {
     } else if (p.action.kind != ScopeKind::Any) {
       throw CedarError("invalid action scope");
     }
+    if (p.principal.kind == ScopeKind::Eq || p.principal.kind == ScopeKind::In || p.principal.kind == ScopeKind::IsIn)
+      w[PW_FLAGS] |= uid_bloom_bit(w[PW_P_ET], w[PW_P_EI]) << 16;
+    if (p.resource.kind == ScopeKind::Eq || p.resource.kind == ScopeKind::In || p.resource.kind == ScopeKind::IsIn)
+      w[PW_FLAGS] |= uid_bloom_bit(w[PW_R_ET], w[PW_R_EI]) << 24;
+    uint64_t am = I.amask_ok ? action_mask(p.action) : ~0ull;
+    w[PW_AMASK0] = (uint32_t)am;
+    w[PW_AMASK1] = (uint32_t)(am >> 32);
     code0 = (uint32_t)I.code.size();
     max_slot = 0;
     lane_off = 0;
-    for (auto& c : p.conds) {
-      compile(*c.second, 0);
-      emit(OP_COND, 0, 0, 0, c.first ? 0u : 1u, 0);
+    std::vector<uint32_t> at;
+    uint32_t n_atom_words = 0;
+    if (atoms(p, at, &n_atom_words)) {
+      w[PW_FLAGS] |= PF_ATOMIC;
+      w[PW_SLOTS] = n_atom_words;
+      I.code.insert(I.code.end(), at.begin(), at.end());
+      I.n_atomic++;
+    } else {
+      for (auto& c : p.conds) {
+        compile(*c.second, 0);
+        emit(OP_COND, 0, 0, 0, c.first ? 0u : 1u, 0);
+      }
     }
     w[PW_CODE] = code0;
     w[PW_CODE_N] = (uint32_t)I.code.size() - code0;
-    w[PW_SLOTS] = max_slot;
+    if (!(w[PW_FLAGS] & PF_ATOMIC)) w[PW_SLOTS] = max_slot;
     w[PW_LANE] = lane_off;
     I.pol.insert(I.pol.end(), w, w + POL_WORDS);
   }
@@ -456,6 +717,9 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     img->hot.push_back(order[k].second.first);
     img->hot.push_back(order[k].second.second);
   }
+  for (auto& tp : parsed)
+    for (auto& p : tp) C.collect_actions(p.action);
+  img->amask_ok = img->act.size() / 2 <= MAX_ACT ? 1u : 0u;
   for (size_t t = 0; t < parsed.size(); t++) {
     for (auto& p : parsed[t]) {
       C.policy(p, (uint32_t)t);
@@ -464,6 +728,38 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
       img->meta.push_back(std::move(m));
     }
     img->tier_end.push_back(img->n_pol());
+  }
+  // device policy stream + chunk table
+  {
+    uint32_t p = 0;
+    for (uint32_t t = 0; t < img->n_tiers(); t++) {
+      uint32_t pend = img->tier_end[t];
+      uint32_t c_off = (uint32_t)img->pstream.size(), c_p0 = p;
+      auto close = [&]() {
+        uint32_t nw = (uint32_t)img->pstream.size() - c_off;
+        if (p > c_p0) {
+          img->chunks.push_back(c_off); img->chunks.push_back(nw);
+          img->chunks.push_back(c_p0); img->chunks.push_back(p);
+        }
+        c_off = (uint32_t)img->pstream.size();
+        c_p0 = p;
+      };
+      for (; p < pend; p++) {
+        const uint32_t* d = &img->pol[(size_t)p * POL_WORDS];
+        uint32_t ncode = d[PW_CODE_N];
+        uint32_t rec = (POL_WORDS + ncode + 3) & ~3u;
+        if (rec > CHUNK_WORDS) throw CedarError("policy " + img->meta[p].id + " is too large for the device policy stream");
+        if ((uint32_t)img->pstream.size() - c_off + rec > CHUNK_WORDS) close();
+        size_t base = img->pstream.size();
+        img->pstream.insert(img->pstream.end(), d, d + POL_WORDS);
+        img->pstream[base + PW_CODE] = POL_WORDS;
+        img->pstream.insert(img->pstream.end(), img->code.begin() + d[PW_CODE], img->code.begin() + d[PW_CODE] + ncode);
+        while ((img->pstream.size() - base) % 4) img->pstream.push_back(0);
+      }
+      close();
+      img->tier_cend.push_back((uint32_t)img->chunks.size() / 4);
+    }
+    if (img->pstream.empty()) img->pstream.resize(4, 0);
   }
   // global string table
   img->gstr_off.clear();
@@ -507,6 +803,8 @@ std::vector<uint8_t> Image::serialize() const {
   W w;
   w.u32(IMG_MAGIC); w.u32(IMG_VERSION); w.u64(epoch);
   w.vec(pol); w.vec(tier_end); w.vec(code); w.vec(cpool); w.vec(gstr_off); w.vec(hot); w.bytes(gstr_bytes);
+  w.vec(act); w.u32(amask_ok); w.u32(n_atomic);
+  w.vec(pstream); w.vec(chunks); w.vec(tier_cend);
   w.u32((uint32_t)strings.size());
   for (auto& s : strings) w.str(s);
   w.u32((uint32_t)meta.size());
@@ -528,6 +826,8 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->epoch = r.u64();
   img->pol = r.vec(); img->tier_end = r.vec(); img->code = r.vec(); img->cpool = r.vec();
   img->gstr_off = r.vec(); img->hot = r.vec(); img->gstr_bytes = r.bytes();
+  img->act = r.vec(); img->amask_ok = r.u32(); img->n_atomic = r.u32();
+  img->pstream = r.vec(); img->chunks = r.vec(); img->tier_cend = r.vec();
   uint32_t ns = r.u32();
   for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }
   uint32_t nm = r.u32();

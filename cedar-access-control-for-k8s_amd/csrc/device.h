@@ -12,9 +12,10 @@ struct Batch;
 
 struct DevImage {
   int device = -1;
-  uint32_t *pol = nullptr, *tier_end = nullptr, *code = nullptr, *cpool = nullptr, *gstr_off = nullptr, *hot = nullptr;
+  uint32_t *pstream = nullptr, *tier_cend = nullptr, *chunks = nullptr, *cpool = nullptr, *gstr_off = nullptr, *hot = nullptr;
+  uint32_t* act = nullptr;
   uint8_t* gstr_bytes = nullptr;
-  uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0;
+  uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0, n_act = 0, amask_ok = 0, has_bytecode = 1;
   size_t bytes = 0;
 };
 

@@ -25,6 +25,14 @@ struct PolicyMeta {
 struct Image {
   uint64_t epoch = 0;
   std::vector<uint32_t> pol, tier_end, code, cpool, gstr_off, hot;  // hot: (var, key sid) pairs
+  // device policy stream: per policy a record [descriptor (POL_WORDS) | code, padded to 4 words]
+  // with PW_CODE relative to the record; records grouped into chunks of <= CHUNK_WORDS words
+  // that never cross a tier. chunks: (word offset, words, first policy, end policy) per chunk;
+  // tier_cend[t] = end chunk index of tier t.
+  std::vector<uint32_t> pstream, chunks, tier_cend;
+  std::vector<uint32_t> act;  // action table: (type sid, id sid) pairs of every action entity in scopes
+  uint32_t amask_ok = 0;      // 1 when act has <= MAX_ACT entries (PW_AMASK* valid)
+  uint32_t n_atomic = 0;      // policies compiled to atoms (statistics)
   std::vector<uint8_t> gstr_bytes;
   std::vector<PolicyMeta> meta;
   std::vector<std::string> strings;

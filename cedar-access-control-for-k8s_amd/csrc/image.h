@@ -66,8 +66,10 @@ constexpr uint32_t NO_ENT = 0xFFFFFFFFu;
 
 // ---- policy descriptor ----------------------------------------------------------------------
 enum ScopeK : uint32_t { SK_ANY = 0, SK_EQ = 1, SK_IN = 2, SK_IS = 3, SK_ISIN = 4, SK_INSET = 5 };
+enum PolFlags : uint32_t { PF_FORBID = 1, PF_ATOMIC = 2 };
 enum PolW : uint32_t {
-  PW_FLAGS = 0,   // bit0 forbid, bits 8..15 tier
+  PW_FLAGS = 0,   // bit0 forbid, bit1 atomic (code = atoms), bits 8..15 tier,
+                  // bits 16..22 principal-entity bloom bit, bits 24..30 resource-entity bloom bit
   PW_KINDS = 1,   // p_kind | a_kind << 8 | r_kind << 16
   PW_P_TYPE = 2,  // is-type (string id)
   PW_P_ET = 3,    // entity type (string id)
@@ -79,16 +81,48 @@ enum PolW : uint32_t {
   PW_R_EI = 9,
   PW_CODE = 10,   // code word offset
   PW_CODE_N = 11, // code words
-  PW_SLOTS = 12,  // max register slot used + 1
+  PW_SLOTS = 12,  // bytecode: max register slot used + 1; atomic: words of atoms (data follows)
   PW_LANE = 13,   // lane-scratch words needed
-  PW_R0 = 14,
-  PW_R1 = 15,
+  PW_AMASK0 = 14, // action scope as a mask over the image action table (valid when n_act <= 64)
+  PW_AMASK1 = 15,
   POL_WORDS = 16,
 };
 
+// 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
+__host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_t ei) {
+  return ((et * 0x9E3779B1u) ^ (ei * 0x85EBCA77u) ^ ((ei >> 16) * 0xC2B2AE3Du)) >> 25;
+}
+
+// ---- atoms: 4-word predicates over pre-resolved (hot) attributes ----------------------------
+// word0 = kind | h << 8 | flags << 16; word1..3 = operands
+enum AtomKind : uint32_t {
+  AK_HAS = 1,     // hot h present
+  AK_BOOL,        // hot h (must be bool)
+  AK_EQ,          // hot h == const (w1 = tag word, w2 = y, w3 = z, register form; primitives only)
+  AK_EQH,         // hot h == hot w1
+  AK_INSET,       // [const primitives @record+w1 (3 words each), n = w2].contains(hot h)
+  AK_CONTAINS,    // hot h (must be set).contains(const primitive w1, w2, w3)
+  AK_LIKE,        // hot h (must be string) like pattern @record+w1
+  AK_IS,          // var h is type w1
+  AK_IN,          // var h in entity (w1 type, w2 id), w3 = bloom bit
+  AK_LCMP,        // hot h (must be long) <op w1> const long (w2 lo, w3 hi); op: 0 <, 1 <=, 2 >, 3 >=
+  AK_RECSET,      // hot h (must be set).containsAny([record templates]) (w3 = 0) / .contains(template) (w3 = 1);
+                  // templates @record+w1 (layout: RecsetLayout), w2 = number of templates
+};
+// AK_RECSET data, all offsets relative to the policy record:
+//   [n_holes, hole hot index ...]                     holes in source (evaluation) order
+//   then per template: [n_keys, (key sid, field kind, a, b, c) x n_keys]   keys ascending by sid
+//   field kind RF_CONST: a,b,c = register-form primitive; RF_HOLE: a = hot index;
+//   RF_SETLIT: a = offset of the element list, b = element count; element = (kind, x, y, z),
+//   kind RF_CONST (x,y,z register form) or RF_HOLE (x = hot index)
+enum RecsetField : uint32_t { RF_CONST = 0, RF_HOLE = 1, RF_SETLIT = 2 };
+constexpr uint32_t RS_FIELD_WORDS = 5, RS_ELEM_WORDS = 4;
+enum AtomFlags : uint32_t { AF_START = 1, AF_END = 2, AF_UNLESS = 4, AF_OR = 8, AF_NEG = 16 };
+constexpr uint32_t ATOM_WORDS = 4;
+
 // ---- bytecode -------------------------------------------------------------------------------
 // word0 = op | d << 8 | a << 14 | b << 20 | c << 26 (6-bit slot fields); word1 = imm
-constexpr uint32_t NSLOT = 16;
+constexpr uint32_t NSLOT = 8;
 constexpr uint32_t LANE_WORDS = 192;   // per-lane scratch for runtime-built sets/records
 constexpr uint32_t VAL_DEPTH = 8;      // max nesting for deep equality on device
 enum Op : uint32_t {
@@ -125,7 +159,9 @@ enum Op : uint32_t {
   OP_HOTHAS,    // d = hot attribute slot c present
   OP_COUNT
 };
-constexpr uint32_t NHOT = 8;  // pre-resolved (var, attribute) pairs per image
+constexpr uint32_t CHUNK_WORDS = 4096;  // policy-stream chunk staged in LDS (16 KiB)
+constexpr uint32_t NHOT = 16;  // pre-resolved (var, attribute) pairs per image (kept in LDS)
+constexpr uint32_t MAX_ACT = 64;  // image action table size for per-request action masks
 // OP_CALL sub-ops
 enum CallOp : uint32_t {
   CO_CONTAINS_ALL = 0, CO_CONTAINS_ANY, CO_IS_EMPTY,
@@ -162,6 +198,6 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 1;
+constexpr uint32_t IMG_VERSION = 2;
 
 }  // namespace cgi

@@ -62,6 +62,11 @@ int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* fi
 int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len);
 /* Number of policies / tiers of a built image blob. */
 int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t* n_tiers, uint64_t* epoch);
+/* Compiled-image shape (no reference counterpart; diagnostics and tests): policies lowered to
+ * predicate atoms (the rest run as bytecode), pre-resolved hot attributes, distinct action
+ * entities in scopes, policy-stream words. */
+int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* n_hot, uint32_t* n_actions,
+                   uint32_t* stream_words);
 
 /* ---- device context (one per GPU; requests shard across contexts, images are replicated) ---- */
 int cg_device_count(int* n);

@@ -121,6 +121,71 @@ class Gen:
     def policies(self, n):
         return "\n".join(self.policy() for _ in range(n))
 
+    # ---- policies the device compiler lowers to predicate atoms (conjunction/disjunction chains
+    # over request attributes), incl. the label-selector template shape
+    def sel_tmpl(self):
+        r = self.r
+        key = q(r.choice(["k0", "k1", "owner"]))
+        v = lambda: r.choice([q(r.choice(USERS + TAGS)), "principal.name", "principal.nick"])
+        t = r.random()
+        if t < 0.4:
+            vals = ", ".join(v() for _ in range(r.randint(0, 2)))
+            return f'{{"key": {key}, "operator": "in", "values": [{vals}]}}'
+        if t < 0.7:
+            return f'{{"key": {key}, "value": {v()}}}'
+        return f'{{"operator": {q(r.choice(["in", "notin"]))}, "key": {key}, "values": [{v()}]}}'
+
+    def atom_e(self):
+        r = self.r
+        return r.choice([
+            lambda: "resource has sel", lambda: "principal has nick", lambda: "principal.active",
+            lambda: f'resource.namespace == {q(r.choice(["ns1", "ns2", "u0"]))}',
+            lambda: f'resource.namespace != {q(r.choice(["ns1", "ns2"]))}',
+            lambda: f"resource.name like {r.choice(PATTERNS)}",
+            lambda: f"principal.age {r.choice(['<', '<=', '>', '>='])} {r.randint(-5, 50)}",
+            lambda: "resource.name == principal.name",
+            lambda: f'{q(r.choice(USERS))} == principal.name',
+            lambda: f"principal in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: f"principal is {r.choice(['k8s::User', 'k8s::Group'])}",
+            lambda: "[" + ", ".join(q(x) for x in r.sample(TAGS + USERS, 3)) + "].contains(resource.name)",
+            lambda: f"principal.tags.contains({q(r.choice(TAGS))})",
+            lambda: "resource.sel.containsAny([" + ", ".join(self.sel_tmpl() for _ in range(r.randint(1, 3))) + "])",
+            lambda: f"resource.sel.contains({self.sel_tmpl()})",
+            lambda: f"!resource.sel.containsAny([{self.sel_tmpl()}])",
+        ])()
+
+    def atomic_policy(self):
+        r = self.r
+        eff = "forbid" if r.random() < 0.25 else "permit"
+        conds = []
+        for _ in range(r.choice([1, 1, 2])):
+            op = " || " if r.random() < 0.3 else " && "
+            conds.append(f"{r.choice(['when', 'when', 'unless'])} {{ " + op.join(self.atom_e() for _ in range(r.randint(1, 4))) + " }")
+        return f"{eff} ({self.scope('principal')}, {self.scope('action')}, {self.scope('resource')})\n" + "\n".join(conds) + ";"
+
+    def atomic_policies(self, n):
+        return "\n".join(self.atomic_policy() for _ in range(n))
+
+    def sel_value(self):
+        r = self.r
+        if r.random() < 0.05:
+            return "not-a-set"
+        out = []
+        for _ in range(r.randint(0, 3)):
+            key = r.choice(["k0", "k1", "owner"])
+            t = r.random()
+            if t < 0.5:
+                out.append({"key": key, "operator": "in", "values": r.sample(USERS[:3] + TAGS[:2], r.randint(0, 2))})
+            elif t < 0.75:
+                out.append({"key": key, "value": r.choice(USERS[:3] + TAGS[:2])})
+            elif t < 0.85:
+                out.append({"key": key, "operator": "in", "values": [r.choice(USERS[:3])], "extra": 1})
+            elif t < 0.95:
+                out.append(r.choice(USERS))
+            else:
+                out.append({"key": key, "operator": "in", "values": [r.choice(USERS[:3]), r.choice(USERS[:3])]})
+        return out
+
     def value_attrs_user(self):
         r = self.r
         a = {"name": r.choice(USERS)}
@@ -135,6 +200,8 @@ class Gen:
             a["info"] = info
         if r.random() < 0.8:
             a["active"] = r.random() < 0.5
+        if r.random() < 0.6:
+            a["nick"] = r.choice(USERS[:3] + TAGS[:2])
         return a
 
     def item(self):
@@ -161,6 +228,8 @@ class Gen:
             ra["ip"] = {"__extn": {"fn": "ip", "arg": r.choice(["10.1.2.3", "127.0.0.1", "::1", "192.168.1.7/24", "224.0.0.1", "ff02::1"])}}
         if r.random() < 0.7:
             ra["score"] = {"__extn": {"fn": "decimal", "arg": r.choice(["1.5", "-3.0", "0.0001", "12.3456"])}}
+        if r.random() < 0.75:
+            ra["sel"] = self.sel_value()
         if r.random() < 0.9:
             ents.append({"uid": ruid, "attrs": ra, "parents": [{"type": "k8s::Group", "id": r.choice(GROUPS)}] if r.random() < 0.3 else []})
         act = {"type": "k8s::Action", "id": r.choice(["get", "list", "watch", "create"])}

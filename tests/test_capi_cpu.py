@@ -10,6 +10,7 @@ import cedar_oracle as co
 import k8s_model as km
 from conftest import GOLDEN, ROOT
 from helpers import attrs_from, cxx_sar_to_cedar, norm_entities, sar_from_attrs
+from randgen import Gen
 
 import cedargpu
 from cedargpu import synth
@@ -96,3 +97,22 @@ def test_cxx_sar_model_matches_oracle_on_synthetic_sars():
         assert norm_entities(got["entities"]) == norm_entities(co.entities_to_json(em)), sar
         assert got["request"] == co.request_to_json(req)
     assert n_fast >= 2
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_atomic_generator_lowers_every_policy_to_atoms(seed):
+    """The GPU atomic-policy parity tests only mean something if the compiler really takes the
+    atom path for them (incl. label-selector templates): every policy must lower."""
+    g = Gen(5000 + seed)
+    n = g.r.randint(1, 40)
+    img = cedargpu.build_image([cedargpu.MemoryStore("a.cedar", g.atomic_policies(n))])
+    st = cedargpu.image_stats(img)
+    assert st["policies"] == n and st["atomic"] == n, st
+
+
+def test_c3_workload_is_fully_atomic():
+    from cedargpu import synth
+    pop = synth.Population(seed=7)
+    img = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", synth.abac_policies(2000, seed=31, pop=pop))])
+    st = cedargpu.image_stats(img)
+    assert st["atomic"] == st["policies"] == 2000, st

@@ -91,6 +91,15 @@ def test_random_policies_vs_oracle(ctx, seed):
     check_items(ctx, stores, items)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_random_atomic_policies_vs_oracle(ctx, seed):
+    """Policies lowered to predicate atoms (incl. label-selector record templates)."""
+    g = Gen(5000 + seed)
+    stores = [cedargpu.MemoryStore(f"a{t}.cedar", g.atomic_policies(g.r.randint(1, 40))) for t in range(g.r.randint(1, 2))]
+    items = [g.item() for _ in range(400)]
+    check_items(ctx, stores, items)
+
+
 def test_random_overflowing_result_lists(ctx):
     """300 policies: many requests exceed the inline reason/error capacity -> re-run path."""
     g = Gen(77)
