@@ -428,6 +428,10 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       uint32_t fl = res[2 * k] >> 16;
       uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
       const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
+      // the re-run is authoritative for the whole result (the index kernel does not decide a
+      // request whose hits overflowed its staging area)
+      b->host.res[2 * (size_t)i] = res[2 * k] & ~((uint32_t)cgi::RF_OVERFLOW << 16);
+      b->host.res[2 * (size_t)i + 1] = res[2 * k + 1];
       b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
       b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
     }

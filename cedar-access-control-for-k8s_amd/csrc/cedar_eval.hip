@@ -59,7 +59,10 @@ struct KArgs {
   uint32_t* __restrict__ reasons_f;
   uint32_t* __restrict__ reasons_p;
   uint32_t* __restrict__ errs;
-  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape;
+  const uint32_t* __restrict__ btab;     // scope index (indexed kernel)
+  const uint32_t* __restrict__ brefs;
+  const uint32_t* __restrict__ bstream;
+  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask;
 };
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
@@ -74,7 +77,8 @@ struct Ctx {
   const uint32_t* bstr_off;
   const uint8_t* bstr_bytes;
   uint32_t n_gstr;
-  uint2* hotl;  // LDS hot table, this lane's column: hotl[h * BLOCK]
+  uint2* hotl;       // LDS hot table: hotl[h * hstride]
+  uint32_t hstride;  // BLOCK (per-lane columns, request-per-lane kernel) or 1 (request-per-wave)
   uint32_t pt, pi, at, ai, rt, ri;
   uint32_t pidx, aidx, ridx;
   uint32_t nent;
@@ -453,13 +457,13 @@ __device__ __forceinline__ RV from_i64(int64_t x) {
 __device__ __forceinline__ RV mk_bool(bool b) { return RV{mk_w0(T_BOOL, 0), b ? 1u : 0u, 0}; }
 
 // Hot slot h of this lane: value (memory form) or a status word (tag NONE, x = error code).
-__device__ __forceinline__ uint2 hot_get(const Ctx& c, uint32_t h) { return c.hotl[h * BLOCK]; }
+__device__ __forceinline__ uint2 hot_get(const Ctx& c, uint32_t h) { return c.hotl[h * c.hstride]; }
 __device__ __forceinline__ bool hot_ok(uint2 v) { return (v.x >> TAG_SHIFT) != T_NONE; }
 // The error ATTR would raise for a missing hot attribute.
 __device__ __forceinline__ void hot_err(const Ctx& c, uint32_t h, uint2 v, Err& e) {
-  const uint32_t var = uni(c.hot[2 * h]);
+  const uint32_t var = c.hot[2 * h];  // h may differ per lane (request-per-wave kernel)
   e.code = v.x & X_MASK;
-  e.k = uni(c.hot[2 * h + 1]);
+  e.k = c.hot[2 * h + 1];
   e.et = pick3(var, c.pt, c.at, c.rt);
   e.ei = pick3(var, c.pi, c.ai, c.ri);
 }
@@ -540,7 +544,7 @@ __device__ __forceinline__ uint32_t eval_atom(const Ctx& c, const uint32_t* rec,
       bool f = false;
       for (uint32_t k = 0; k < w2 && !f; k++) {
         const uint32_t* el = rec + w1 + 3 * k;
-        f = prim_eq(v, uni(el[0]), uni(el[1]), uni(el[2]));
+        f = prim_eq(v, el[0], el[1], el[2]);  // per-lane policy in the index kernel: no readfirstlane
       }
       return f ? 1u : 0u;
     }
@@ -921,10 +925,12 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   c.bstr_bytes = a.bstr_bytes;
   c.n_gstr = a.n_gstr;
   c.hotl = hot_lds + threadIdx.x;
+  c.hstride = BLOCK;
   c.pb0 = c.pb1 = c.pb2 = c.pb3 = 0;
   c.rb0 = c.rb1 = c.rb2 = c.rb3 = 0;
   c.p_anc = c.p_nanc = c.r_anc = c.r_nanc = 0;
-  uint32_t am0 = 0, am1 = 0;  // action mask over the image action table
+  uint32_t am0 = 0, am1 = 0;  // action mask over the image action table: action in act[k]
+  uint32_t as0 = 0, as1 = 0;  // action == act[k]
   if (valid) {
     c.nent = c.blk[RH_NENT];
     c.pt = c.blk[RH_P] & X_MASK; c.pi = c.blk[RH_P + 1];
@@ -957,8 +963,10 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
     const uint32_t n_act = a.n_act;
     for (uint32_t k = 0; k < n_act; k++) {
       const uint32_t qt = uni(a.act[2 * k]), qi = uni(a.act[2 * k + 1]);
-      const bool hit = valid && ((c.at == qt && c.ai == qi) || (a_n && anc_scan(c.blk, a_off, a_n, qt, qi)));
+      const bool self = valid && c.at == qt && c.ai == qi;
+      const bool hit = self || (valid && a_n && anc_scan(c.blk, a_off, a_n, qt, qi));
       if (hit) { if (k < 32) am0 |= 1u << k; else am1 |= 1u << (k - 32); }
+      if (self) { if (k < 32) as0 |= 1u << k; else as1 |= 1u << (k - 32); }
     }
   }
   // pre-resolve hot (var, attribute) pairs into LDS: value, or the error ATTR would raise
@@ -977,7 +985,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
         }
       }
     }
-    c.hotl[h * BLOCK] = v;
+    c.hotl[h * c.hstride] = v;
   }
 
   bool decided = !valid;
@@ -1014,8 +1022,8 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
         bool ok = !decided;
         // action scope: one AND against the per-request action mask
         if (ak != SK_ANY) {
-          if (a.amask_ok) {
-            ok = ok && (((am0 & am0p) | (am1 & am1p)) != 0);
+          if (a.amask_ok) {  // `==` tests the action itself, `in` its ancestors too
+            ok = ok && (ak == SK_EQ ? (((as0 & am0p) | (as1 & am1p)) != 0) : (((am0 & am0p) | (am1 & am1p)) != 0));
           } else if (ak == SK_EQ) {
             ok = ok && c.at == a_et && c.ai == a_ei;
           } else if (ak == SK_IN) {
@@ -1103,6 +1111,289 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   }
 }
 
+
+// ---- request-per-wave kernel over the scope index --------------------------------------------
+// One wave evaluates one request. Its lanes take the candidate policies of the buckets selected
+// by the request's principal / resource / action ancestor-or-self UIDs and types (image.h "scope
+// index"), 64 records at a time; the request context is wave-uniform and lives in scalar
+// registers. Satisfied / erroring candidates are collected in LDS and merged at the end into the
+// same result layout the request-per-lane kernel writes (policy order, deciding tier, overflow).
+constexpr uint32_t WAVES = BLOCK / 64;
+constexpr uint32_t HCAP = 64;  // hits per request staged in LDS; more -> overflow re-run
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+// LDS written by some lanes of this wave, then read by others
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WaveLds {
+  uint32_t bk[2 * 64];       // (first, count) of the non-empty buckets of one key group
+  uint32_t hp[HCAP];         // hit: global policy index
+  uint32_t hm[HCAP];         // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8
+  uint32_t hel[HCAP];        // hit is in the deciding tier and not a duplicate
+  uint32_t he[HCAP * 4];     // error words: code | aux << 8, k, et, ei
+  uint2 hot[NHOT];
+};
+
+__global__ __launch_bounds__(BLOCK) void cedar_index_kernel(KArgs a) {
+  __shared__ WaveLds wl_all[WAVES];
+  const uint32_t lane = threadIdx.x & 63;
+  WaveLds& wl = wl_all[threadIdx.x >> 6];
+  const uint32_t gid = uni(blockIdx.x * WAVES + (threadIdx.x >> 6));
+  if (gid >= a.n_req) return;  // whole wave; this kernel has no block barriers
+  const uint32_t r = a.req_idx ? uni(a.req_idx[gid]) : gid;
+
+  Ctx c;
+  c.blk = a.heap + uni(a.req_base[r]);
+  c.cpool = a.cpool;
+  c.lh = wl.he;  // atoms never address lane scratch (any valid pointer)
+  c.hot = a.hot;
+  c.gstr_off = a.gstr_off;
+  c.gstr_bytes = a.gstr_bytes;
+  c.bstr_off = a.bstr_off;
+  c.bstr_bytes = a.bstr_bytes;
+  c.n_gstr = a.n_gstr;
+  c.hotl = wl.hot;
+  c.hstride = 1;
+  c.nent = uni(c.blk[RH_NENT]);
+  c.pt = uni(c.blk[RH_P]) & X_MASK; c.pi = uni(c.blk[RH_P + 1]);
+  c.at = uni(c.blk[RH_A]) & X_MASK; c.ai = uni(c.blk[RH_A + 1]);
+  c.rt = uni(c.blk[RH_R]) & X_MASK; c.ri = uni(c.blk[RH_R + 1]);
+  c.pidx = uni(c.blk[RH_PIDX]); c.aidx = uni(c.blk[RH_AIDX]); c.ridx = uni(c.blk[RH_RIDX]);
+  anc_of(c, c.pidx, c.p_anc, c.p_nanc);
+  c.p_anc = uni(c.p_anc); c.p_nanc = uni(c.p_nanc);
+  anc_of(c, c.ridx, c.r_anc, c.r_nanc);
+  c.r_anc = uni(c.r_anc); c.r_nanc = uni(c.r_nanc);
+  uint32_t a_anc = 0, a_nanc = 0;
+  anc_of(c, c.aidx, a_anc, a_nanc);
+  a_anc = uni(a_anc); a_nanc = uni(a_nanc);
+#define CG_ANC(k) \
+  c.t##k = k < c.p_nanc ? uni(c.blk[c.p_anc + 2 * k]) : 0xFFFFFFFFu; \
+  c.i##k = k < c.p_nanc ? uni(c.blk[c.p_anc + 2 * k + 1]) : 0xFFFFFFFFu;
+  CG_ANC(0) CG_ANC(1) CG_ANC(2) CG_ANC(3) CG_ANC(4) CG_ANC(5) CG_ANC(6) CG_ANC(7)
+#undef CG_ANC
+  // ancestor-or-self Bloom filters: lane k contributes UID k, OR-reduced through ballots
+  {
+    uint32_t pb[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0};
+    for (uint32_t k0 = 0; k0 < 1 + c.p_nanc; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      const bool on = k < 1 + c.p_nanc;
+      const uint32_t bit = on ? (k == 0 ? uid_bloom_bit(c.pt, c.pi)
+                                        : uid_bloom_bit(c.blk[c.p_anc + 2 * (k - 1)], c.blk[c.p_anc + 2 * (k - 1) + 1])) : 0u;
+      for (uint32_t q = 0; q < 4; q++)
+        for (uint32_t b = 0; b < 32; b++) pb[q] |= __ballot(on && bit == 32 * q + b) ? (1u << b) : 0u;
+    }
+    for (uint32_t k0 = 0; k0 < 1 + c.r_nanc; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      const bool on = k < 1 + c.r_nanc;
+      const uint32_t bit = on ? (k == 0 ? uid_bloom_bit(c.rt, c.ri)
+                                        : uid_bloom_bit(c.blk[c.r_anc + 2 * (k - 1)], c.blk[c.r_anc + 2 * (k - 1) + 1])) : 0u;
+      for (uint32_t q = 0; q < 4; q++)
+        for (uint32_t b = 0; b < 32; b++) rb[q] |= __ballot(on && bit == 32 * q + b) ? (1u << b) : 0u;
+    }
+    c.pb0 = pb[0]; c.pb1 = pb[1]; c.pb2 = pb[2]; c.pb3 = pb[3];
+    c.rb0 = rb[0]; c.rb1 = rb[1]; c.rb2 = rb[2]; c.rb3 = rb[3];
+  }
+  // action mask over the image action table: lane k tests action k
+  uint32_t am0 = 0, am1 = 0, as0 = 0, as1 = 0;  // action in / == act[k]
+  if (a.amask_ok) {
+    const bool on = lane < a.n_act;
+    const uint32_t qt = on ? a.act[2 * lane] : 0u, qi = on ? a.act[2 * lane + 1] : 0u;
+    const bool self = on && c.at == qt && c.ai == qi;
+    const bool hit = self || (on && a_nanc && anc_scan(c.blk, a_anc, a_nanc, qt, qi));
+    const uint64_t m = __ballot(hit), ms = __ballot(self);
+    am0 = (uint32_t)m; am1 = (uint32_t)(m >> 32);
+    as0 = (uint32_t)ms; as1 = (uint32_t)(ms >> 32);
+  }
+  // hot attributes: lane h resolves attribute h
+  if (lane < a.n_hot) {
+    const uint32_t var = a.hot[2 * lane], key = a.hot[2 * lane + 1];
+    uint2 v = make_uint2(mk_w0(T_NONE, E_ENTITY_MISSING), 0);
+    if (var == 3) {
+      if (!rec_get_heap(c.blk, c.blk[RH_CTX], c.blk[RH_CTX + 1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_RECORD), 0);
+    } else {
+      const uint32_t idx = pick3(var, c.pidx, c.aidx, c.ridx);
+      if (idx != NO_ENT) {
+        const uint32_t* row = c.blk + RH_WORDS + idx * ENT_WORDS;
+        if (!rec_get_heap(c.blk, row[ER_ATTR0], row[ER_ATTR1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_ENTITY), 0);
+      }
+    }
+    wl.hot[lane] = v;
+  }
+  wave_lds_sync();
+
+  uint32_t min_tier = a.n_tiers - 1;  // lowest tier with a hit so far (uniform)
+  uint32_t nh = 0;                    // hits recorded (uniform; may exceed HCAP)
+  const uint32_t n_keys = 6 + c.p_nanc + c.r_nanc + a_nanc;
+  for (uint32_t kb = 0; kb < n_keys; kb += 64) {
+    // ---- bucket lookup: lane k probes key k ----
+    const uint32_t k = kb + lane;
+    uint32_t cat = 0, et = 0, ei = 0;
+    if (k < n_keys) {
+      uint32_t j = k;
+      if (j < 1 + c.p_nanc) {
+        cat = BK_P;
+        et = j ? c.blk[c.p_anc + 2 * (j - 1)] : c.pt;
+        ei = j ? c.blk[c.p_anc + 2 * (j - 1) + 1] : c.pi;
+      } else if ((j -= 1 + c.p_nanc) < 1 + c.r_nanc) {
+        cat = BK_R;
+        et = j ? c.blk[c.r_anc + 2 * (j - 1)] : c.rt;
+        ei = j ? c.blk[c.r_anc + 2 * (j - 1) + 1] : c.ri;
+      } else if ((j -= 1 + c.r_nanc) < 1 + a_nanc) {
+        cat = BK_A;
+        et = j ? c.blk[a_anc + 2 * (j - 1)] : c.at;
+        ei = j ? c.blk[a_anc + 2 * (j - 1) + 1] : c.ai;
+      } else {
+        j -= 1 + a_nanc;
+        cat = j == 0 ? BK_PT : (j == 1 ? BK_RT : BK_ALL);
+        et = j == 0 ? c.pt : (j == 1 ? c.rt : 0u);
+      }
+    }
+    uint32_t first = 0, cnt = 0;
+    if (cat && et < (1u << 28)) {
+      const uint32_t want = (cat << 28) | et;
+      uint32_t h = bucket_hash(cat, et, ei) & a.bmask;
+      for (;;) {
+        const uint4 e = *reinterpret_cast<const uint4*>(a.btab + (size_t)h * BT_WORDS);
+        if (e.x == 0) break;
+        if (e.x == want && e.y == ei) { first = e.z; cnt = e.w; break; }
+        h = (h + 1) & a.bmask;
+      }
+    }
+    const uint64_t bm = __ballot(cnt != 0);
+    if (cnt) {
+      const uint32_t pos = mbcnt64(bm);
+      wl.bk[2 * pos] = first;
+      wl.bk[2 * pos + 1] = cnt;
+    }
+    wave_lds_sync();
+    const uint32_t nb = popc64(bm);
+    for (uint32_t b = 0; b < nb; b++) {
+      const uint32_t bfirst = uni(wl.bk[2 * b]), bcnt = uni(wl.bk[2 * b + 1]);
+      for (uint32_t base = 0; base < bcnt; base += 64) {
+        // ---- one candidate policy per lane ----
+        const uint32_t i = base + lane;
+        bool ok = i < bcnt;
+        const uint32_t ro = ok ? a.brefs[bfirst + i] : 0u;
+        const uint32_t* rec = a.bstream + ro;
+        const uint4* d4 = reinterpret_cast<const uint4*>(rec);
+        const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+        const uint32_t flags = q0.x, kinds = q0.y;
+        const uint32_t tier = (flags >> 8) & 0xFF;
+        ok = ok && tier <= min_tier;
+        const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
+        if (ak != SK_ANY) {
+          if (a.amask_ok) {
+            ok = ok && (ak == SK_EQ ? (((as0 & q3.z) | (as1 & q3.w)) != 0) : (((am0 & q3.z) | (am1 & q3.w)) != 0));
+          } else if (ak == SK_EQ) {
+            ok = ok && c.at == q1.y && c.ai == q1.z;
+          } else if (ak == SK_IN) {
+            ok = ok && ((c.at == q1.y && c.ai == q1.z) || anc_has(c, c.aidx, q1.y, q1.z));
+          } else {
+            bool any = false;
+            for (uint32_t x = 0; ok && x < q1.y && !any; x++) {
+              const uint32_t qt = a.cpool[q1.z + 2 * x], qi = a.cpool[q1.z + 2 * x + 1];
+              any = (c.at == qt && c.ai == qi) || anc_has(c, c.aidx, qt, qi);
+            }
+            ok = ok && any;
+          }
+        }
+        if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
+        if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
+        else if (pk == SK_IN || pk == SK_ISIN) ok = ok && p_in(c, q0.w, q1.x, (flags >> 16) & 0x7F);
+        if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
+        if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
+        else if (rk == SK_IN || rk == SK_ISIN) ok = ok && r_in(c, q2.x, q2.y, (flags >> 24) & 0x7F);
+        // ---- conditions: this lane's atom chain ----
+        bool run = ok, err = false, cur = true;
+        Err e{0, 0, 0, 0, 0};
+        const uint32_t n_atom = q3.x;
+        for (uint32_t x = 0; __ballot(run && x < n_atom); x += ATOM_WORDS) {
+          if (run && x < n_atom) {
+            const uint4 at = *reinterpret_cast<const uint4*>(rec + POL_WORDS + x);
+            const uint32_t af = at.x >> 16;
+            if (af & AF_START) cur = !(af & AF_OR);
+            if ((af & AF_OR) ? !cur : cur) {
+              const uint32_t rr = eval_atom(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
+              if (rr == 2u) { err = true; run = false; }
+              else cur = (rr != 0u) != ((af & AF_NEG) != 0);
+            }
+            if ((af & AF_END) && run && (((af & AF_UNLESS) != 0) == cur)) run = false;
+          }
+        }
+        // ---- record hits ----
+        const bool hit = ok && (err || run);
+        const uint64_t hmask = __ballot(hit);
+        if (hmask) {
+          if (hit) {
+            const uint32_t pos = nh + mbcnt64(hmask);
+            if (pos < HCAP) {
+              wl.hp[pos] = q2.z;  // global policy index
+              wl.hm[pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8);
+              if (err) {
+                wl.he[4 * pos] = e.code | (e.aux << 8);
+                wl.he[4 * pos + 1] = e.k;
+                wl.he[4 * pos + 2] = e.et;
+                wl.he[4 * pos + 3] = e.ei;
+              }
+            }
+          }
+          nh += popc64(hmask);
+          min_tier = min(min_tier, wave_min(hit ? tier : 0xFFu));
+        }
+      }
+    }
+    wave_lds_sync();  // bucket list is rewritten by the next key group
+  }
+
+  // ---- merge: deciding tier, duplicates, policy order ----
+  const uint32_t t = min_tier;
+  if (nh > HCAP) {
+    if (lane == 0) {
+      a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW) << 16);
+      a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);
+    }
+    return;
+  }
+  const bool have = lane < nh;
+  const uint32_t pj = have ? wl.hp[lane] : 0xFFFFFFFFu;
+  const uint32_t mj = have ? wl.hm[lane] : 0u;
+  const uint32_t kind = mj & 0xFF;
+  bool el = have && (mj >> 8) == t;
+  for (uint32_t x = 0; x < nh; x++) {  // a policy filed under several action buckets hits twice
+    const uint32_t px = wl.hp[x];
+    if (x < lane && px == pj && (wl.hm[x] >> 8) == t) el = false;
+  }
+  wl.hel[lane] = el ? 1u : 0u;
+  wave_lds_sync();
+  const uint32_t nf = popc64(__ballot(el && kind == 1)), np = popc64(__ballot(el && kind == 0)),
+                 ne = popc64(__ballot(el && kind == 2));
+  uint32_t rank = 0;
+  for (uint32_t x = 0; x < nh; x++)
+    rank += (wl.hel[x] && (wl.hm[x] & 0xFF) == kind && wl.hp[x] < pj) ? 1u : 0u;
+  const uint32_t dk = nf ? 1u : (np ? 0u : 3u);
+  if (el && kind == dk && rank < a.capr) (nf ? a.reasons_f : a.reasons_p)[(size_t)gid * a.capr + rank] = pj;
+  if (el && kind == 2 && rank < a.cape) {
+    uint32_t* er = a.errs + ((size_t)gid * a.cape + rank) * ERR_WORDS;
+    er[0] = pj; er[1] = wl.he[4 * lane]; er[2] = wl.he[4 * lane + 1]; er[3] = wl.he[4 * lane + 2];
+    er[4] = wl.he[4 * lane + 3]; er[5] = 0;
+  }
+  if (lane == 0) {
+    const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);
+    const uint32_t nr = nf ? nf : np;
+    uint32_t fl = RF_VALID | (nf ? RF_FORBID : 0u);
+    if (nr > a.capr || ne > a.cape) fl |= RF_OVERFLOW;
+    a.res[2 * (size_t)gid] = dec | (t << 8) | (fl << 16);
+    a.res[2 * (size_t)gid + 1] = min(nr, 0xFFFFu) | (min(ne, 0xFFFFu) << 16);
+  }
+}
+
 thread_local std::string g_err;
 
 int fail(hipError_t e, const char* what) {
@@ -1173,6 +1464,11 @@ int dev_image_upload(int device, const Image& img, DevImage* out) {
   if ((rc = up(&d.gstr_off, img.gstr_off, d.bytes, s))) return rc;
   if ((rc = up(&d.hot, img.hot, d.bytes, s))) return rc;
   if ((rc = up(&d.act, img.act, d.bytes, s))) return rc;
+  if ((rc = up(&d.btab, img.btab, d.bytes, s))) return rc;
+  if ((rc = up(&d.brefs, img.brefs, d.bytes, s))) return rc;
+  if ((rc = up(&d.bstream, img.bstream, d.bytes, s))) return rc;
+  d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
+  d.indexed = img.indexed;
   d.n_act = (uint32_t)img.act.size() / 2;
   d.has_bytecode = img.n_atomic < img.n_pol() ? 1u : 0u;
   d.amask_ok = img.amask_ok;
@@ -1190,7 +1486,8 @@ void dev_image_free(DevImage* d) {
   if (d->device < 0) return;
   (void)hipSetDevice(d->device);
   for (void* p : {(void*)d->pstream, (void*)d->tier_cend, (void*)d->chunks, (void*)d->cpool, (void*)d->gstr_off,
-                  (void*)d->hot, (void*)d->act, (void*)d->gstr_bytes})
+                  (void*)d->hot, (void*)d->act, (void*)d->gstr_bytes, (void*)d->btab, (void*)d->brefs,
+                  (void*)d->bstream})
     if (p) (void)hipFree(p);
   *d = DevImage();
 }
@@ -1242,7 +1539,18 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.n_pol = img.n_pol; k.n_tiers = img.n_tiers; k.n_gstr = img.n_gstr; k.n_hot = img.n_hot;
   k.act = img.act; k.n_act = img.n_act; k.amask_ok = img.amask_ok;
   k.n_req = n; k.capr = capr; k.cape = cape;
+  k.btab = img.btab; k.brefs = img.brefs; k.bstream = img.bstream; k.bmask = img.bmask;
   return k;
+}
+
+// Launches the evaluation of n requests: the request-per-wave kernel over the scope index when the
+// image is fully indexed, else the request-per-lane policy-stream kernel.
+static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
+  if (img.indexed)
+    hipLaunchKernelGGL(cedar_index_kernel, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
+  else
+    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>,
+                       dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
 }
 
 int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
@@ -1250,7 +1558,7 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
   if (b.n == 0) return 0;
   if (img.device != b.device) { g_err = "image and batch live on different devices"; return -2; }
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
-  hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((b.n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), (hipStream_t)stream, k);
+  launch_eval(img, k, b.n, (hipStream_t)stream);
   HIPCHK(hipGetLastError(), "launch");
   return 0;
 }
@@ -1318,7 +1626,7 @@ int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
   HIPCHK(hipEventRecord(e0, s), "event record");
   for (uint32_t i = 0; i < iters; i++)
-    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((b.n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
+    launch_eval(img, k, b.n, s);
   HIPCHK(hipGetLastError(), "launch");
   HIPCHK(hipEventRecord(e1, s), "event record");
   HIPCHK(hipEventSynchronize(e1), "event sync");

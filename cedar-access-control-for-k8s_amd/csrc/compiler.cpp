@@ -680,6 +680,80 @@ struct Compiler {
 
 }  // namespace
 
+// Scope index (image.h): file each atomic policy under the candidate key set with the fewest
+// competing policies, then lay the stream records out bucket by bucket.
+static void build_scope_index(Image& img) {
+  using Key = std::array<uint32_t, 3>;
+  const uint32_t n = img.n_pol();
+  img.btab.clear(); img.brefs.clear(); img.bstream.clear();
+  img.indexed = (n > 0 && img.n_atomic == n) ? 1u : 0u;
+  if (!img.indexed) {
+    img.btab.assign(BT_WORDS, 0); img.brefs.assign(1, 0); img.bstream.assign(POL_WORDS, 0);
+    return;
+  }
+  // stream record offset of every policy
+  std::vector<uint32_t> rec_off(n), rec_len(n);
+  for (size_t ch = 0; ch < img.chunks.size(); ch += 4) {
+    uint32_t off = img.chunks[ch];
+    for (uint32_t p = img.chunks[ch + 2]; p < img.chunks[ch + 3]; p++) {
+      const uint32_t len = (POL_WORDS + img.pstream[off + PW_CODE_N] + 3) & ~3u;
+      rec_off[p] = off; rec_len[p] = len;
+      off += len;
+    }
+  }
+  std::vector<std::vector<std::vector<Key>>> opts(n);  // per policy: options, each a key list
+  std::map<Key, uint32_t> cnt;
+  for (uint32_t p = 0; p < n; p++) {
+    const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
+    const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
+    auto& o = opts[p];
+    if (pk == SK_EQ || pk == SK_IN || pk == SK_ISIN) o.push_back({Key{BK_P, d[PW_P_ET], d[PW_P_EI]}});
+    if (rk == SK_EQ || rk == SK_IN || rk == SK_ISIN) o.push_back({Key{BK_R, d[PW_R_ET], d[PW_R_EI]}});
+    if (ak == SK_EQ || ak == SK_IN) o.push_back({Key{BK_A, d[PW_A_ET], d[PW_A_EI]}});
+    if (ak == SK_INSET) {
+      std::vector<Key> ks;
+      for (uint32_t k = 0; k < d[PW_A_ET]; k++) ks.push_back(Key{BK_A, img.cpool[d[PW_A_EI] + 2 * k], img.cpool[d[PW_A_EI] + 2 * k + 1]});
+      std::sort(ks.begin(), ks.end());
+      ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+      o.push_back(ks);  // empty list: `action in []` never applies, the policy needs no bucket
+    }
+    if (rk == SK_IS || rk == SK_ISIN) o.push_back({Key{BK_RT, d[PW_R_TYPE], 0}});
+    if (pk == SK_IS || pk == SK_ISIN) o.push_back({Key{BK_PT, d[PW_P_TYPE], 0}});
+    o.push_back({Key{BK_ALL, 0, 0}});
+    for (auto& ks : o)
+      for (auto& k : ks) cnt[k]++;
+  }
+  std::map<Key, std::vector<uint32_t>> buckets;  // key -> policies (ascending: p increases)
+  for (uint32_t p = 0; p < n; p++) {
+    size_t best = 0;
+    uint64_t best_cost = ~0ull;
+    for (size_t i = 0; i < opts[p].size(); i++) {
+      uint64_t c = 0;
+      for (auto& k : opts[p][i]) c += cnt[k];
+      if (c < best_cost) { best_cost = c; best = i; }
+    }
+    for (auto& k : opts[p][best]) buckets[k].push_back(p);
+  }
+  uint32_t size = 16;
+  while (size < 2 * buckets.size()) size <<= 1;
+  img.btab.assign((size_t)size * BT_WORDS, 0);
+  for (auto& kv : buckets) {
+    const Key& k = kv.first;
+    if (k[1] >= (1u << 28)) throw CedarError("string table too large for the scope index");
+    const uint32_t first = (uint32_t)img.brefs.size();
+    for (uint32_t p : kv.second) {
+      img.brefs.push_back((uint32_t)img.bstream.size());
+      img.bstream.insert(img.bstream.end(), img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p]);
+    }
+    uint32_t h = bucket_hash(k[0], k[1], k[2]) & (size - 1);
+    while (img.btab[(size_t)h * BT_WORDS] != 0) h = (h + 1) & (size - 1);
+    uint32_t* e = &img.btab[(size_t)h * BT_WORDS];
+    e[0] = (k[0] << 28) | k[1]; e[1] = k[2]; e[2] = first; e[3] = (uint32_t)kv.second.size();
+  }
+  if (img.brefs.empty()) img.brefs.push_back(0);
+  if (img.bstream.size() < POL_WORDS) img.bstream.resize(POL_WORDS, 0);  // idle lanes read record 0
+}
+
 std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch) {
   if (tiers.empty()) throw CedarError("at least one policy tier is required");
   if (tiers.size() > 255) throw CedarError("too many tiers");
@@ -752,7 +826,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
         if ((uint32_t)img->pstream.size() - c_off + rec > CHUNK_WORDS) close();
         size_t base = img->pstream.size();
         img->pstream.insert(img->pstream.end(), d, d + POL_WORDS);
-        img->pstream[base + PW_CODE] = POL_WORDS;
+        img->pstream[base + PW_CODE] = p;
         img->pstream.insert(img->pstream.end(), img->code.begin() + d[PW_CODE], img->code.begin() + d[PW_CODE] + ncode);
         while ((img->pstream.size() - base) % 4) img->pstream.push_back(0);
       }
@@ -761,6 +835,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     }
     if (img->pstream.empty()) img->pstream.resize(4, 0);
   }
+  build_scope_index(*img);
   // global string table
   img->gstr_off.clear();
   img->gstr_bytes.clear();
@@ -805,6 +880,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.vec(pol); w.vec(tier_end); w.vec(code); w.vec(cpool); w.vec(gstr_off); w.vec(hot); w.bytes(gstr_bytes);
   w.vec(act); w.u32(amask_ok); w.u32(n_atomic);
   w.vec(pstream); w.vec(chunks); w.vec(tier_cend);
+  w.vec(btab); w.vec(brefs); w.vec(bstream); w.u32(indexed);
   w.u32((uint32_t)strings.size());
   for (auto& s : strings) w.str(s);
   w.u32((uint32_t)meta.size());
@@ -828,6 +904,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->gstr_off = r.vec(); img->hot = r.vec(); img->gstr_bytes = r.bytes();
   img->act = r.vec(); img->amask_ok = r.u32(); img->n_atomic = r.u32();
   img->pstream = r.vec(); img->chunks = r.vec(); img->tier_cend = r.vec();
+  img->btab = r.vec(); img->brefs = r.vec(); img->bstream = r.vec(); img->indexed = r.u32();
   uint32_t ns = r.u32();
   for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }
   uint32_t nm = r.u32();

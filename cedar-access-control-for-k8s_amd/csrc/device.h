@@ -1,4 +1,4 @@
-// Device bridge (implemented in kernel.hip). Plain C++ declarations: no HIP types leak into the
+// Device bridge (implemented in cedar_eval.hip). Plain C++ declarations: no HIP types leak into the
 // host engine or the C-ABI.
 #pragma once
 #include <cstddef>
@@ -14,8 +14,9 @@ struct DevImage {
   int device = -1;
   uint32_t *pstream = nullptr, *tier_cend = nullptr, *chunks = nullptr, *cpool = nullptr, *gstr_off = nullptr, *hot = nullptr;
   uint32_t* act = nullptr;
+  uint32_t *btab = nullptr, *brefs = nullptr, *bstream = nullptr;  // scope index
   uint8_t* gstr_bytes = nullptr;
-  uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0, n_act = 0, amask_ok = 0, has_bytecode = 1;
+  uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0, n_act = 0, amask_ok = 0, has_bytecode = 1, indexed = 0, bmask = 0;
   size_t bytes = 0;
 };
 

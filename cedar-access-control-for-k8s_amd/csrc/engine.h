@@ -33,6 +33,9 @@ struct Image {
   std::vector<uint32_t> act;  // action table: (type sid, id sid) pairs of every action entity in scopes
   uint32_t amask_ok = 0;      // 1 when act has <= MAX_ACT entries (PW_AMASK* valid)
   uint32_t n_atomic = 0;      // policies compiled to atoms (statistics)
+  // scope index over atomic policies (image.h "scope index"); indexed = every policy is atomic
+  std::vector<uint32_t> btab, brefs, bstream;
+  uint32_t indexed = 0;
   std::vector<uint8_t> gstr_bytes;
   std::vector<PolicyMeta> meta;
   std::vector<std::string> strings;

@@ -79,7 +79,7 @@ enum PolW : uint32_t {
   PW_R_TYPE = 7,
   PW_R_ET = 8,
   PW_R_EI = 9,
-  PW_CODE = 10,   // code word offset
+  PW_CODE = 10,   // pol[]: code word offset; stream records: global policy index (code follows)
   PW_CODE_N = 11, // code words
   PW_SLOTS = 12,  // bytecode: max register slot used + 1; atomic: words of atoms (data follows)
   PW_LANE = 13,   // lane-scratch words needed
@@ -87,6 +87,26 @@ enum PolW : uint32_t {
   PW_AMASK1 = 15,
   POL_WORDS = 16,
 };
+
+// ---- scope index (indexed evaluation path) ---------------------------------------------------
+// Every atomic policy is filed under the scope key that any request it can apply to must
+// enumerate: the principal / resource / action entity of an ==, in or is-in scope (the request
+// enumerates its ancestor-or-self UIDs), the principal / resource type of an `is` scope, or ALL.
+// An `action in [..]` list files the policy under each listed action (duplicates are removed
+// when results are merged). The kernel re-checks the full scope of every candidate.
+//   btab[4 * slot] = (cat << 28 | et, ei, first, count): open addressing, linear probing,
+//                    power-of-two size, empty slot has word0 == 0
+//   brefs[first .. first + count)  word offsets into bstream, ascending policy index
+//   bstream                        copies of the stream records in bucket order (locality)
+enum BucketCat : uint32_t { BK_P = 1, BK_R = 2, BK_A = 3, BK_PT = 4, BK_RT = 5, BK_ALL = 6 };
+constexpr uint32_t BT_WORDS = 4;
+__host__ __device__ constexpr inline uint32_t bucket_hash(uint32_t cat, uint32_t et, uint32_t ei) {
+  uint32_t h = (cat * 0x9E3779B1u) ^ (et * 0x85EBCA77u) ^ (ei * 0xC2B2AE3Du);
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  return h;
+}
 
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
 __host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_t ei) {
@@ -198,6 +218,6 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 2;
+constexpr uint32_t IMG_VERSION = 3;
 
 }  // namespace cgi

@@ -214,3 +214,45 @@ def test_hot_reload_epochs(ctx):
         b.wait()
     assert old.decision(0)[0] is True
     assert new.decision(0)[0] is False
+
+
+# ---------------------------------------------------------------- scope-index kernel paths
+def test_index_kernel_hit_overflow_reruns(ctx):
+    """More satisfied policies than the index kernel stages per request (64) -> re-run path."""
+    pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
+                     for i in range(150))
+    pols += '\nforbid (principal, action == k8s::Action::"create", resource) when { principal has nick };'
+    stores = [cedargpu.MemoryStore("many.cedar", pols)]
+    assert cedargpu.image_stats(cedargpu.build_image(stores))["atomic"] == 151
+    g = Gen(91)
+    check_items(ctx, stores, [g.item() for _ in range(300)])
+
+
+def test_index_kernel_action_hierarchy_duplicates(ctx):
+    """A policy filed under several actions of `action in [..]` is reached twice when the request
+    action's ancestors include more than one of them; it must be reported once."""
+    pols = ('permit (principal, action in [k8s::Action::"read", k8s::Action::"get", k8s::Action::"all"], resource)'
+            ' when { principal.active };\n'
+            'forbid (principal, action in [k8s::Action::"get", k8s::Action::"all"], resource is k8s::Resource)'
+            ' when { resource.size > 50 };\n'
+            'permit (principal is k8s::User, action == k8s::Action::"all", resource);\n')
+    stores = [cedargpu.MemoryStore("acts.cedar", pols)]
+    g = Gen(92)
+    items = []
+    for _ in range(200):
+        ents, req = g.item()
+        ents = ents + [{"uid": {"type": "k8s::Action", "id": "get"}, "attrs": {},
+                        "parents": [{"type": "k8s::Action", "id": "read"}, {"type": "k8s::Action", "id": "all"}]},
+                       {"uid": {"type": "k8s::Action", "id": "read"}, "attrs": {},
+                        "parents": [{"type": "k8s::Action", "id": "all"}]}]
+        req = dict(req, action={"type": "k8s::Action", "id": g.r.choice(["get", "read", "list"])})
+        items.append((ents, req))
+    check_items(ctx, stores, items)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_index_kernel_multi_tier_fallthrough(ctx, seed):
+    """Three atomic tiers: a request falls through tiers with no reasons and no errors."""
+    g = Gen(7000 + seed)
+    stores = [cedargpu.MemoryStore(f"t{t}.cedar", g.atomic_policies(g.r.randint(0, 6))) for t in range(3)]
+    check_items(ctx, stores, [g.item() for _ in range(400)])
