@@ -37,48 +37,59 @@ def algorithmic_bytes(sars, n_reasons, has_like):
     return total
 
 
-def cpu_baseline(policies_text, sars, seconds, workers):
-    """Oracle (`port`: Python restatement of cedar-go semantics) on a bounded sample, pre-built
-    EntityMaps, `workers` processes. Runs before any GPU initialisation."""
-    import multiprocessing as mp
+def oracle_items(sars):
+    """(EntityMap, Request) JSON items of the SARs that reach evaluation (the fast paths of
+    authorizer.go:38-57 never do), built by the oracle's k8s model (test infrastructure)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cedar_oracle as co
     import k8s_model as km
-
-    global _BASE
-    tiers = [co.PolicySet.from_bytes("c3.cedar", policies_text)]
-    items = []
-    for s in sars:
+    items, idx = [], []
+    for i, s in enumerate(sars):
         a = km.attributes_from_sar(s)
+        n = a.user.name
+        if n.startswith("system:") and not (n.startswith("system:serviceaccount:") or n.startswith("system:node:")):
+            continue
         em, req = km.record_to_cedar_resource(a)
-        items.append((em, req))
-    _BASE = (tiers, items, seconds)
-    ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
-        counts = pool.map(_cpu_worker, range(workers))
-    wall = time.perf_counter() - t0
-    n = sum(counts)
-    return {"value": n / wall, "unit": "decisions/s", "cores": workers, "kind": "port",
-            "sample": f"{n} SubjectAccessReviews (pre-built EntityMaps) x {sum(len(t.policies) for t in tiers)} policies "
-                      f"through oracle/cedar_oracle.py tiered_is_authorized, {workers} processes x ~{seconds:.0f} s"}
+        items.append((co.entities_to_json(em), co.request_to_json(req)))
+        idx.append(i)
+    return items, idx
 
 
-_BASE = None
+def cpu_baseline(policies_text, items, seconds, threads):
+    """C++ oracle (`port`: oracle/cedar_ref.cpp, the restatement of cedar-go's per-request linear
+    scan with a tree-walking evaluator) on `threads` host threads over pre-built EntityMaps.
+    Runs before any GPU initialisation."""
+    from cedar_ref import RefPolicySet, items_json
+    ref = RefPolicySet()
+    ref.add_tier()
+    ref.add_document("c3.cedar", policies_text)
+    ref.load_items(items_json(items))
+    n, wall = ref.bench(threads, seconds)
+    ref.close()
+    return {"value": n / wall, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} decisions in {wall:.1f} s: {len(items)} pre-built (EntityMap, Request) items from the "
+                      f"benchmark's SubjectAccessReviews x {policies_text.count(';')} policies through "
+                      f"oracle/cedar_ref.cpp (C++ restatement of cedar-go IsAuthorized, linear scan), "
+                      f"{threads} threads on {os.cpu_count()} visible CPUs"}
 
 
-def _cpu_worker(w):
-    import cedar_oracle as co
-    tiers, items, seconds = _BASE
-    t_end = time.perf_counter() + seconds
-    n = 0
-    i = w
-    while time.perf_counter() < t_end:
-        em, req = items[i % len(items)]
-        co.tiered_is_authorized(tiers, em, req)
-        n += 1
-        i += 17
-    return n
+def parity_sample(policies_text, items, idx, gpu_batch, threads):
+    """GPU authorizer answers vs the C++ oracle on a sample of the timed batch (decision + exact
+    reason string, authorizer.go:75-84 mapping)."""
+    from cedar_ref import RefPolicySet, items_json
+    ref = RefPolicySet()
+    ref.add_tier()
+    ref.add_document("c3.cedar", policies_text)
+    ref.load_items(items_json(items))
+    want = ref.evaluate(threads)
+    ref.close()
+    bad = 0
+    for (ok, _, diag, _), i in zip(want, idx):
+        wd = 1 if ok else (0 if diag.startswith('{"reasons"') else 2)
+        wr = diag if wd != 2 else ""
+        if gpu_batch.authz(i) != (wd, wr):
+            bad += 1
+    return {"requests": len(items), "mismatches": bad, "oracle": "oracle/cedar_ref.cpp"}
 
 
 def main():
@@ -89,7 +100,8 @@ def main():
     ap.add_argument("--policies", type=int, default=10_000)
     ap.add_argument("--batch", type=int, default=65_536, help="requests per GPU per step")
     ap.add_argument("--variant", default="full", help="policy-shape study: full | scope-only | no-group | atomic-only")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--parity-sample", type=int, default=2048)
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=40)
@@ -107,9 +119,10 @@ def main():
     sars = synth.random_sars(args.batch, seed=1000 + rank, pop=pop)
 
     baseline = None
+    threads = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+    items, idx = oracle_items(sars[:args.parity_sample]) if rank == 0 else ([], [])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = args.cpu_workers or max(1, min(16, (os.cpu_count() or 2) - 1))
-        baseline = cpu_baseline(policies, sars[:4096], args.cpu_seconds, workers)
+        baseline = cpu_baseline(policies, items, args.cpu_seconds, threads)
 
     # torch is plumbing only: the cross-rank barrier / max-reduce of timings runs over gloo on CPU
     # tensors. torch's bundled HIP runtime is never initialised in this process (it would clash
@@ -170,6 +183,8 @@ def main():
             lb.close()
         lat.sort()
 
+    parity = parity_sample(policies, items, idx, b, threads) if rank == 0 and items else None
+
     if rank == 0:
         ms_per_step = wall_s * 1e3 / args.steps
         decisions = args.batch * world * args.steps
@@ -206,6 +221,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": baseline,
+            "parity_sample": parity,
             "latency": {"batch": args.latency_batch, "p50_ms": lat[len(lat) // 2] if lat else None,
                         "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
                         "batches": len(lat)},
