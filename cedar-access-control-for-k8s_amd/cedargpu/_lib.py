@@ -54,6 +54,8 @@ _SIGS = {
     "cg_compiler_build": (ctypes.c_int, [P, u64, ctypes.POINTER(P), ctypes.POINTER(sz)]),
     "cg_image_info": (ctypes.c_int, [P, sz, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u64)]),
     "cg_image_stats": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u32)] * 4),
+    "cg_image_policy_atomic": (ctypes.c_int, [P, sz, u32, ctypes.POINTER(ctypes.c_int)]),
+    "cg_image_indexed": (ctypes.c_int, [P, sz, ctypes.POINTER(ctypes.c_int)]),
     "cg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "cg_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "cg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(P)]),

@@ -162,8 +162,21 @@ def image_stats(image: bytes) -> dict:
     if lib.cg_image_info(image, len(image), ctypes.byref(u[0]), ctypes.byref(u[1]), ctypes.byref(ep)):
         raise ValueError("not a compiled policy image")
     lib.cg_image_stats(image, len(image), *(ctypes.byref(x) for x in u[2:]))
+    ix = ctypes.c_int(0)
+    lib.cg_image_indexed(image, len(image), ctypes.byref(ix))
     return {"policies": u[0].value, "tiers": u[1].value, "epoch": ep.value, "atomic": u[2].value,
-            "hot": u[3].value, "actions": u[4].value, "stream_words": u[5].value}
+            "hot": u[3].value, "actions": u[4].value, "stream_words": u[5].value, "indexed": bool(ix.value)}
+
+
+def atomic_policies(image: bytes) -> List[bool]:
+    """Per policy (image order): lowered to predicate atoms (True) or bytecode."""
+    n = image_stats(image)["policies"]
+    out = []
+    for i in range(n):
+        a = ctypes.c_int(0)
+        lib.cg_image_policy_atomic(image, len(image), i, ctypes.byref(a))
+        out.append(bool(a.value))
+    return out
 
 
 class Context:

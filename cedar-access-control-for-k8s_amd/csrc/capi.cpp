@@ -157,7 +157,7 @@ int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* 
   try {
     auto img = Image::deserialize((const uint8_t*)image, len);
     if (n_atomic) *n_atomic = img->n_atomic;
-    if (n_hot) *n_hot = (uint32_t)img->hot.size() / 2;
+    if (n_hot) *n_hot = (uint32_t)img->hot.size() / cgi::HOT_WORDS;
     if (n_actions) *n_actions = (uint32_t)img->act.size() / 2;
     if (stream_words) *stream_words = (uint32_t)img->pstream.size();
     return CG_OK;
@@ -167,6 +167,28 @@ int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
+int cg_image_policy_atomic(const void* image, size_t len, uint32_t i, int* atomic) {
+  if (!image || !atomic) return CG_E_ARG;
+  try {
+    auto img = Image::deserialize((const uint8_t*)image, len);
+    if (i >= img->n_pol()) return CG_E_RANGE;
+    *atomic = (img->pol[(size_t)i * cgi::POL_WORDS + cgi::PW_FLAGS] & cgi::PF_ATOMIC) ? 1 : 0;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+  return CG_OK;
+}
+
+int cg_image_indexed(const void* image, size_t len, int* indexed) {
+  if (!image || !indexed) return CG_E_ARG;
+  try {
+    *indexed = Image::deserialize((const uint8_t*)image, len)->indexed ? 1 : 0;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+  return CG_OK;
+}
+
 int cg_device_count(int* n) {
   if (!n) return CG_E_ARG;
   return dev_count(n) ? CG_E_DEVICE : CG_OK;

@@ -62,7 +62,8 @@ struct KArgs {
   const uint32_t* __restrict__ btab;     // scope index (indexed kernel)
   const uint32_t* __restrict__ brefs;
   const uint32_t* __restrict__ bstream;
-  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask;
+  const uint32_t* __restrict__ rows;     // columnar request rows (row_words each)
+  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, row_words;
 };
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
@@ -83,6 +84,7 @@ struct Ctx {
   uint32_t pidx, aidx, ridx;
   uint32_t nent;
   uint32_t p_anc, p_nanc, r_anc, r_nanc;  // heap offsets of ancestor pair arrays, and counts
+  uint32_t a_anc, a_nanc;                 // action ancestors (probe kernel; stream kernel uses aidx)
   // first 8 principal ancestors, for the exact `in` test in registers (named scalars: an array
   // here would keep the whole context out of registers)
   uint32_t t0, i0, t1, i1, t2, i2, t3, i3, t4, i4, t5, i5, t6, i6, t7, i7;
@@ -456,16 +458,21 @@ __device__ __forceinline__ RV from_i64(int64_t x) {
 }
 __device__ __forceinline__ RV mk_bool(bool b) { return RV{mk_w0(T_BOOL, 0), b ? 1u : 0u, 0}; }
 
-// Hot slot h of this lane: value (memory form) or a status word (tag NONE, x = error code).
+// Hot slot h of this lane: the value (memory form) or a status word (tag NONE; x = error code |
+// HS_FINAL; y = block offset of the error detail the encoder resolved, image.h "hot paths").
 __device__ __forceinline__ uint2 hot_get(const Ctx& c, uint32_t h) { return c.hotl[h * c.hstride]; }
 __device__ __forceinline__ bool hot_ok(uint2 v) { return (v.x >> TAG_SHIFT) != T_NONE; }
-// The error ATTR would raise for a missing hot attribute.
+// `has` on a hot path: present -> 1, absent at the final step -> 0, failing earlier -> 2 (error)
+__device__ __forceinline__ uint32_t hot_has(uint2 v) { return hot_ok(v) ? 1u : ((v.x & HS_FINAL) ? 0u : 2u); }
+// The error attribute access raises for a non-present hot slot.
 __device__ __forceinline__ void hot_err(const Ctx& c, uint32_t h, uint2 v, Err& e) {
-  const uint32_t var = c.hot[2 * h];  // h may differ per lane (request-per-wave kernel)
-  e.code = v.x & X_MASK;
-  e.k = c.hot[2 * h + 1];
-  e.et = pick3(var, c.pt, c.at, c.rt);
-  e.ei = pick3(var, c.pi, c.ai, c.ri);
+  const uint32_t* d = c.blk + v.y;
+  const uint32_t w = d[0];
+  e.code = w & 0xFF;
+  e.aux = w >> 8;
+  e.k = d[1];
+  e.et = d[2];
+  e.ei = d[3];
 }
 
 // ---- atoms ---------------------------------------------------------------------------------
@@ -513,18 +520,36 @@ __device__ __forceinline__ bool rs_rec_eq(const Ctx& c, const uint32_t* rec, con
   return true;
 }
 
+// var h (0 principal, 1 action, 2 resource) `in` entity (qt, qi); bit = its Bloom bit
+__device__ __forceinline__ bool var_in(const Ctx& c, uint32_t h, uint32_t qt, uint32_t qi, uint32_t bit) {
+  if (h == 0) return p_in(c, qt, qi, bit);
+  if (h == 2) return r_in(c, qt, qi, bit);
+  if (c.aidx == NO_ENT && c.a_nanc) return (c.at == qt && c.ai == qi) || anc_scan(c.blk, c.a_anc, c.a_nanc, qt, qi);
+  return (c.at == qt && c.ai == qi) || anc_has(c, c.aidx, qt, qi);
+}
+
 __device__ __forceinline__ uint32_t eval_atom(const Ctx& c, const uint32_t* rec, uint32_t kind, uint32_t h, uint32_t w1,
                                               uint32_t w2, uint32_t w3, Err& e) {
   if (kind == AK_IS) {
     return pick3(h, c.pt, c.at, c.rt) == w1 ? 1u : 0u;
   }
-  if (kind == AK_IN) {
-    if (h == 0) return p_in(c, w1, w2, w3) ? 1u : 0u;
-    if (h == 2) return r_in(c, w1, w2, w3) ? 1u : 0u;
-    return ((c.at == w1 && c.ai == w2) || anc_has(c, c.aidx, w1, w2)) ? 1u : 0u;
+  if (kind == AK_IN) return var_in(c, h, w1, w2, w3) ? 1u : 0u;
+  if (kind == AK_TRUE) return 1u;
+  if (kind == AK_EQV) return (pick3(h, c.pt, c.at, c.rt) == w1 && pick3(h, c.pi, c.ai, c.ri) == w2) ? 1u : 0u;
+  if (kind == AK_INANY) {
+    bool f = false;
+    for (uint32_t k = 0; k < w2 && !f; k++) {
+      const uint32_t qt = rec[w1 + 2 * k], qi = rec[w1 + 2 * k + 1];
+      f = var_in(c, h, qt, qi, uid_bloom_bit(qt, qi));
+    }
+    return f ? 1u : 0u;
   }
   const uint2 hv = hot_get(c, h);
-  if (kind == AK_HAS) return hot_ok(hv) ? 1u : 0u;
+  if (kind == AK_HAS) {
+    const uint32_t q = hot_has(hv);
+    if (q == 2u) hot_err(c, h, hv, e);
+    return q;
+  }
   if (!hot_ok(hv)) { hot_err(c, h, hv, e); return 2u; }
   const RV v = load_val(c, hv.x, hv.y);
   switch (kind) {
@@ -664,7 +689,13 @@ __device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code,
           wr = false;
           break;
         }
-        case OP_HOTHAS: out = mk_bool(hot_ok(hot_get(c, C))); break;
+        case OP_HOTHAS: {
+          const uint2 hv = hot_get(c, C);
+          const uint32_t q = hot_has(hv);
+          if (q == 2u) { hot_err(c, C, hv, e); err = true; wr = false; break; }
+          out = mk_bool(q == 1u);
+          break;
+        }
         case OP_ATTR:
         case OP_HAS: {
           const uint32_t t = tag_of(va);
@@ -929,6 +960,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   c.pb0 = c.pb1 = c.pb2 = c.pb3 = 0;
   c.rb0 = c.rb1 = c.rb2 = c.rb3 = 0;
   c.p_anc = c.p_nanc = c.r_anc = c.r_nanc = 0;
+  c.a_anc = c.a_nanc = 0;
   uint32_t am0 = 0, am1 = 0;  // action mask over the image action table: action in act[k]
   uint32_t as0 = 0, as1 = 0;  // action == act[k]
   if (valid) {
@@ -969,23 +1001,11 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
       if (self) { if (k < 32) as0 |= 1u << k; else as1 |= 1u << (k - 32); }
     }
   }
-  // pre-resolve hot (var, attribute) pairs into LDS: value, or the error ATTR would raise
-  const uint32_t n_hot = a.n_hot;
-  for (uint32_t h = 0; h < n_hot; h++) {
-    const uint32_t var = uni(a.hot[2 * h]), key = uni(a.hot[2 * h + 1]);
-    uint2 v = make_uint2(mk_w0(T_NONE, E_ENTITY_MISSING), 0);
-    if (valid) {
-      if (var == 3) {
-        if (!rec_get_heap(c.blk, c.blk[RH_CTX], c.blk[RH_CTX + 1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_RECORD), 0);
-      } else {
-        const uint32_t idx = pick3(var, c.pidx, c.aidx, c.ridx);
-        if (idx != NO_ENT) {
-          const uint32_t* row = c.blk + RH_WORDS + idx * ENT_WORDS;
-          if (!rec_get_heap(c.blk, row[ER_ATTR0], row[ER_ATTR1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_ENTITY), 0);
-        }
-      }
-    }
-    c.hotl[h * c.hstride] = v;
+  // hot attribute paths (resolved by the encoder into the request row) into LDS
+  {
+    const uint32_t* row = a.rows + (size_t)r * a.row_words;
+    for (uint32_t h = 0; h < a.n_hot; h++)
+      c.hotl[h * c.hstride] = valid ? make_uint2(row[RW_HDR + 2 * h], row[RW_HDR + 2 * h + 1]) : make_uint2(0u, 0u);
   }
 
   bool decided = !valid;
@@ -1052,20 +1072,21 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
         bool err = false;
         Err e{0, 0, 0, 0, 0};
         if (flags & PF_ATOMIC) {
-          bool cur = true;
-          for (uint32_t i = 0; i < n_atom; i += ATOM_WORDS) {
-            if (__ballot(run) == 0) break;
-            const uint4 at = *reinterpret_cast<const uint4*>(rec + POL_WORDS + i);
+          // atom graph: each lane follows its own forward path; atom i runs for the lanes at i
+          const uint32_t na = n_atom / ATOM_WORDS;
+          uint32_t pc = run ? (na ? 0u : AT_SAT) : AT_UNSAT;
+          for (;;) {
+            const uint32_t i = wave_min(pc < na ? pc : 0xFFFFFFFFu);
+            if (i >= na) break;
+            const uint4 at = *reinterpret_cast<const uint4*>(rec + POL_WORDS + ATOM_WORDS * i);
             const uint32_t w0 = uni(at.x), w1 = uni(at.y), w2 = uni(at.z), w3 = uni(at.w);
-            const uint32_t af = w0 >> 16;
-            if (af & AF_START) cur = !(af & AF_OR);
-            if (run && ((af & AF_OR) ? !cur : cur)) {
+            if (pc == i) {
               const uint32_t rr = eval_atom(c, rec, w0 & 0xFF, (w0 >> 8) & 0xFF, w1, w2, w3, e);
-              if (rr == 2u) { err = true; run = false; }
-              else cur = (rr != 0u) != ((af & AF_NEG) != 0);
+              if (rr == 2u) { err = true; pc = AT_UNSAT; }
+              else pc = rr ? ((w0 >> 16) & 0xFF) : (w0 >> 24);
             }
-            if ((af & AF_END) && run && (((af & AF_UNLESS) != 0) == cur)) run = false;
           }
+          run = pc == AT_SAT;
         } else if constexpr (BYTECODE) {
           run_bytecode(c, rec + POL_WORDS, n_code >> 1, run, err, e);
         }
@@ -1112,14 +1133,20 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
 }
 
 
-// ---- request-per-wave kernel over the scope index --------------------------------------------
-// One wave evaluates one request. Its lanes take the candidate policies of the buckets selected
-// by the request's principal / resource / action ancestor-or-self UIDs and types (image.h "scope
-// index"), 64 records at a time; the request context is wave-uniform and lives in scalar
-// registers. Satisfied / erroring candidates are collected in LDS and merged at the end into the
-// same result layout the request-per-lane kernel writes (policy order, deciding tier, overflow).
+// ---- probe kernel: request-per-wave over the two-level scope / attribute index -----------------
+// One wave evaluates one request (image.h "scope index"):
+//   1. the request row (UIDs, ancestor-list offsets, hot paths pre-resolved by the encoder) is
+//      read with wave-uniform loads; lanes copy the hot values into LDS;
+//   2. lane k probes the level-1 table for scope key k (principal / resource / action
+//      ancestor-or-self UIDs, principal / resource types, ALL), then level 2 under each found key
+//      for the hot slots in its hmask, with the request's own value of that slot;
+//   3. the found buckets' candidate heads (descriptor + first atoms, 128 B, in bucket order) run
+//      one per lane: scope re-check, then the lane's atom graph;
+//   4. satisfied / erroring candidates are collected in LDS and merged into policy order with the
+//      deciding tier, duplicates removed, as the stream kernel writes them.
 constexpr uint32_t WAVES = BLOCK / 64;
-constexpr uint32_t HCAP = 64;  // hits per request staged in LDS; more -> overflow re-run
+constexpr uint32_t HCAP = 64;   // hits per request staged in LDS; more -> overflow re-run
+constexpr uint32_t ECAP = 128;  // found buckets staged before their candidates run
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -1131,9 +1158,20 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// inclusive prefix sum across the wave
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
 
 struct WaveLds {
-  uint32_t bk[2 * 64];       // (first, count) of the non-empty buckets of one key group
+  uint32_t efirst[ECAP];     // found bucket: first head index
+  uint32_t epre[ECAP + 1];   // exclusive prefix of candidate counts
+  uint32_t ekey[ECAP];       // bucket category (BK_P / BK_R keys fully re-checked otherwise) | et
+  uint32_t ekei[ECAP];       //   and entity id of its level-1 key
   uint32_t hp[HCAP];         // hit: global policy index
   uint32_t hm[HCAP];         // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8
   uint32_t hel[HCAP];        // hit is in the deciding tier and not a duplicate
@@ -1141,16 +1179,40 @@ struct WaveLds {
   uint2 hot[NHOT];
 };
 
-__global__ __launch_bounds__(BLOCK) void cedar_index_kernel(KArgs a) {
+// exact `in` for principal / resource against the request's ancestor-or-self list (uniform loop)
+__device__ __forceinline__ bool anc_in(const uint32_t* blk, uint32_t off, uint32_t n, uint32_t st, uint32_t si,
+                                       uint32_t qt, uint32_t qi) {
+  bool f = st == qt && si == qi;
+  for (uint32_t k = 0; k < n; k++) f = f || (uni(blk[off + 2 * k]) == qt && uni(blk[off + 2 * k + 1]) == qi);
+  return f;
+}
+
+// level-1 / level-2 probe: returns (first, count, hmask) of the matching slot, count 0 if absent
+__device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uint32_t hash, uint32_t w0, uint32_t w1,
+                                       uint32_t w2, uint32_t v0, uint32_t v1) {
+  uint32_t h = hash & bmask;
+  for (;;) {
+    const uint4 x = *reinterpret_cast<const uint4*>(btab + (size_t)h * BT_WORDS);
+    if (x.x == 0) return make_uint3(0, 0, 0);
+    if (x.x == w0 && x.y == w1 && x.z == w2) {
+      const uint4 y = *reinterpret_cast<const uint4*>(btab + (size_t)h * BT_WORDS + 4);
+      if (!(w2 & BT_L2) || (x.w == v0 && y.x == v1)) return make_uint3(y.y, y.z, x.w);
+    }
+    h = (h + 1) & bmask;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   __shared__ WaveLds wl_all[WAVES];
   const uint32_t lane = threadIdx.x & 63;
   WaveLds& wl = wl_all[threadIdx.x >> 6];
   const uint32_t gid = uni(blockIdx.x * WAVES + (threadIdx.x >> 6));
   if (gid >= a.n_req) return;  // whole wave; this kernel has no block barriers
   const uint32_t r = a.req_idx ? uni(a.req_idx[gid]) : gid;
+  const uint32_t* row = a.rows + (size_t)r * a.row_words;
 
   Ctx c;
-  c.blk = a.heap + uni(a.req_base[r]);
+  c.blk = a.heap + uni(row[RW_BLK]);
   c.cpool = a.cpool;
   c.lh = wl.he;  // atoms never address lane scratch (any valid pointer)
   c.hot = a.hot;
@@ -1161,47 +1223,26 @@ __global__ __launch_bounds__(BLOCK) void cedar_index_kernel(KArgs a) {
   c.n_gstr = a.n_gstr;
   c.hotl = wl.hot;
   c.hstride = 1;
-  c.nent = uni(c.blk[RH_NENT]);
-  c.pt = uni(c.blk[RH_P]) & X_MASK; c.pi = uni(c.blk[RH_P + 1]);
-  c.at = uni(c.blk[RH_A]) & X_MASK; c.ai = uni(c.blk[RH_A + 1]);
-  c.rt = uni(c.blk[RH_R]) & X_MASK; c.ri = uni(c.blk[RH_R + 1]);
-  c.pidx = uni(c.blk[RH_PIDX]); c.aidx = uni(c.blk[RH_AIDX]); c.ridx = uni(c.blk[RH_RIDX]);
-  anc_of(c, c.pidx, c.p_anc, c.p_nanc);
-  c.p_anc = uni(c.p_anc); c.p_nanc = uni(c.p_nanc);
-  anc_of(c, c.ridx, c.r_anc, c.r_nanc);
-  c.r_anc = uni(c.r_anc); c.r_nanc = uni(c.r_nanc);
-  uint32_t a_anc = 0, a_nanc = 0;
-  anc_of(c, c.aidx, a_anc, a_nanc);
-  a_anc = uni(a_anc); a_nanc = uni(a_nanc);
+  c.nent = 0;
+  c.pt = uni(row[RW_P]); c.pi = uni(row[RW_P + 1]);
+  c.at = uni(row[RW_A]); c.ai = uni(row[RW_A + 1]);
+  c.rt = uni(row[RW_R]); c.ri = uni(row[RW_R + 1]);
+  c.p_anc = uni(row[RW_PANC]); c.p_nanc = uni(row[RW_PN]);
+  c.r_anc = uni(row[RW_RANC]); c.r_nanc = uni(row[RW_RN]);
+  const uint32_t a_anc = uni(row[RW_AANC]), a_nanc = uni(row[RW_AN]);
+  c.a_anc = a_anc; c.a_nanc = a_nanc;
+  c.pidx = c.aidx = c.ridx = NO_ENT;
+  // `in` atoms (p_in / r_in): exact scans, first 8 principal ancestors in registers, Bloom off
+  c.pb0 = c.pb1 = c.pb2 = c.pb3 = 0xFFFFFFFFu;
+  c.rb0 = c.rb1 = c.rb2 = c.rb3 = 0xFFFFFFFFu;
 #define CG_ANC(k) \
   c.t##k = k < c.p_nanc ? uni(c.blk[c.p_anc + 2 * k]) : 0xFFFFFFFFu; \
   c.i##k = k < c.p_nanc ? uni(c.blk[c.p_anc + 2 * k + 1]) : 0xFFFFFFFFu;
   CG_ANC(0) CG_ANC(1) CG_ANC(2) CG_ANC(3) CG_ANC(4) CG_ANC(5) CG_ANC(6) CG_ANC(7)
 #undef CG_ANC
-  // ancestor-or-self Bloom filters: lane k contributes UID k, OR-reduced through ballots
-  {
-    uint32_t pb[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0};
-    for (uint32_t k0 = 0; k0 < 1 + c.p_nanc; k0 += 64) {
-      const uint32_t k = k0 + lane;
-      const bool on = k < 1 + c.p_nanc;
-      const uint32_t bit = on ? (k == 0 ? uid_bloom_bit(c.pt, c.pi)
-                                        : uid_bloom_bit(c.blk[c.p_anc + 2 * (k - 1)], c.blk[c.p_anc + 2 * (k - 1) + 1])) : 0u;
-      for (uint32_t q = 0; q < 4; q++)
-        for (uint32_t b = 0; b < 32; b++) pb[q] |= __ballot(on && bit == 32 * q + b) ? (1u << b) : 0u;
-    }
-    for (uint32_t k0 = 0; k0 < 1 + c.r_nanc; k0 += 64) {
-      const uint32_t k = k0 + lane;
-      const bool on = k < 1 + c.r_nanc;
-      const uint32_t bit = on ? (k == 0 ? uid_bloom_bit(c.rt, c.ri)
-                                        : uid_bloom_bit(c.blk[c.r_anc + 2 * (k - 1)], c.blk[c.r_anc + 2 * (k - 1) + 1])) : 0u;
-      for (uint32_t q = 0; q < 4; q++)
-        for (uint32_t b = 0; b < 32; b++) rb[q] |= __ballot(on && bit == 32 * q + b) ? (1u << b) : 0u;
-    }
-    c.pb0 = pb[0]; c.pb1 = pb[1]; c.pb2 = pb[2]; c.pb3 = pb[3];
-    c.rb0 = rb[0]; c.rb1 = rb[1]; c.rb2 = rb[2]; c.rb3 = rb[3];
-  }
-  // action mask over the image action table: lane k tests action k
-  uint32_t am0 = 0, am1 = 0, as0 = 0, as1 = 0;  // action in / == act[k]
+  if (lane < a.n_hot) wl.hot[lane] = make_uint2(row[RW_HDR + 2 * lane], row[RW_HDR + 2 * lane + 1]);
+  // action masks over the image action table: lane k tests action k (`==` and `in`)
+  uint32_t am0 = 0, am1 = 0, as0 = 0, as1 = 0;
   if (a.amask_ok) {
     const bool on = lane < a.n_act;
     const uint32_t qt = on ? a.act[2 * lane] : 0u, qi = on ? a.act[2 * lane + 1] : 0u;
@@ -1211,28 +1252,132 @@ __global__ __launch_bounds__(BLOCK) void cedar_index_kernel(KArgs a) {
     am0 = (uint32_t)m; am1 = (uint32_t)(m >> 32);
     as0 = (uint32_t)ms; as1 = (uint32_t)(ms >> 32);
   }
-  // hot attributes: lane h resolves attribute h
-  if (lane < a.n_hot) {
-    const uint32_t var = a.hot[2 * lane], key = a.hot[2 * lane + 1];
-    uint2 v = make_uint2(mk_w0(T_NONE, E_ENTITY_MISSING), 0);
-    if (var == 3) {
-      if (!rec_get_heap(c.blk, c.blk[RH_CTX], c.blk[RH_CTX + 1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_RECORD), 0);
-    } else {
-      const uint32_t idx = pick3(var, c.pidx, c.aidx, c.ridx);
-      if (idx != NO_ENT) {
-        const uint32_t* row = c.blk + RH_WORDS + idx * ENT_WORDS;
-        if (!rec_get_heap(c.blk, row[ER_ATTR0], row[ER_ATTR1], key, v)) v = make_uint2(mk_w0(T_NONE, E_ATTR_ENTITY), 0);
-      }
-    }
-    wl.hot[lane] = v;
-  }
   wave_lds_sync();
 
   uint32_t min_tier = a.n_tiers - 1;  // lowest tier with a hit so far (uniform)
   uint32_t nh = 0;                    // hits recorded (uniform; may exceed HCAP)
+  uint32_t ne = 0;                    // found buckets staged (uniform)
+
+  // runs the candidates of the staged buckets, then clears the stage
+  auto run_stage = [&]() {
+    // exclusive prefix of counts over the staged buckets (<= ECAP, two halves)
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < ne; b0 += 64) {
+      const uint32_t b = b0 + lane;
+      const uint32_t cnt = b < ne ? wl.epre[b] : 0u;  // epre holds counts until scanned
+      const uint32_t inc = wave_scan(cnt, lane);
+      wave_lds_sync();
+      if (b < ne) wl.epre[b] = carry + inc - cnt;
+      carry += __shfl(inc, 63);
+      wave_lds_sync();
+    }
+    if (lane == 0) wl.epre[ne] = carry;
+    wave_lds_sync();
+    const uint32_t total = uni(carry);
+    for (uint32_t base = 0; base < total; base += 64) {
+      const uint32_t idx = base + lane;
+      bool ok = idx < total;
+      // bucket of candidate idx: last b with epre[b] <= idx
+      uint32_t lo = 0, hi = ne;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (wl.epre[mid] <= idx) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t b = lo;
+      const uint32_t hidx = ok ? wl.efirst[b] + (idx - wl.epre[b]) : 0u;
+      const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
+      const uint4* d4 = reinterpret_cast<const uint4*>(head);
+      const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+      const uint32_t flags = q0.x, kinds = q0.y;
+      const uint32_t tier = (flags >> 8) & 0xFF;
+      ok = ok && tier <= min_tier;
+      const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
+      const uint32_t kcat = wl.ekey[b] >> 28, ket = wl.ekey[b] & X_MASK, kei = wl.ekei[b];
+      // action scope
+      if (ak != SK_ANY) {
+        if (a.amask_ok) {
+          ok = ok && (ak == SK_EQ ? (((as0 & q3.z) | (as1 & q3.w)) != 0) : (((am0 & q3.z) | (am1 & q3.w)) != 0));
+        } else if (ak == SK_EQ) {
+          ok = ok && c.at == q1.y && c.ai == q1.z;
+        } else if (ak == SK_IN) {
+          ok = ok && ((c.at == q1.y && c.ai == q1.z) || anc_scan(c.blk, a_anc, a_nanc, q1.y, q1.z));
+        } else {
+          bool any = false;
+          for (uint32_t x = 0; ok && x < q1.y && !any; x++) {
+            const uint32_t qt = a.cpool[q1.z + 2 * x], qi = a.cpool[q1.z + 2 * x + 1];
+            any = (c.at == qt && c.ai == qi) || anc_scan(c.blk, a_anc, a_nanc, qt, qi);
+          }
+          ok = ok && any;
+        }
+      }
+      // principal scope: an `in` / `is in` scope whose entity is the bucket's BK_P key holds
+      // already (the request enumerated that key from its ancestor-or-self list)
+      if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
+      if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
+      else if ((pk == SK_IN || pk == SK_ISIN) && !(kcat == BK_P && ket == q0.w && kei == q1.x))
+        ok = ok && anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, q0.w, q1.x);
+      if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
+      if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
+      else if ((rk == SK_IN || rk == SK_ISIN) && !(kcat == BK_R && ket == q2.x && kei == q2.y))
+        ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
+      // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
+      // atom data in the policy's full record at PW_EXT)
+      const uint32_t na = q3.x / ATOM_WORDS;
+      const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (q3.y = word 13)
+      uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
+      bool err = false;
+      Err e{0, 0, 0, 0, 0};
+      while (__ballot(pc < na)) {
+        if (pc < na) {
+          const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
+          const uint32_t rr = eval_atom(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
+          if (rr == 2u) { err = true; pc = AT_UNSAT; }
+          else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
+        }
+      }
+      // record hits
+      const bool hit = ok && (err || pc == AT_SAT);
+      const uint64_t hmask = __ballot(hit);
+      if (hmask) {
+        if (hit) {
+          const uint32_t pos = nh + mbcnt64(hmask);
+          if (pos < HCAP) {
+            wl.hp[pos] = q2.z;  // PW_CODE: global policy index
+            wl.hm[pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8);
+            if (err) {
+              wl.he[4 * pos] = e.code | (e.aux << 8);
+              wl.he[4 * pos + 1] = e.k;
+              wl.he[4 * pos + 2] = e.et;
+              wl.he[4 * pos + 3] = e.ei;
+            }
+          }
+        }
+        nh += popc64(hmask);
+        min_tier = min(min_tier, wave_min(hit ? tier : 0xFFu));
+      }
+    }
+    ne = 0;
+    wave_lds_sync();
+  };
+  // stages this lane's found bucket (cnt > 0), running the stage first when it could overflow
+  auto stage = [&](uint32_t first, uint32_t cnt, uint32_t key0, uint32_t key1) {
+    if (ne + 64 > ECAP) run_stage();
+    const uint64_t m = __ballot(cnt != 0);
+    if (cnt) {
+      const uint32_t pos = ne + mbcnt64(m);
+      wl.efirst[pos] = first;
+      wl.epre[pos] = cnt;
+      wl.ekey[pos] = key0;
+      wl.ekei[pos] = key1;
+    }
+    ne += popc64(m);
+    wave_lds_sync();
+  };
+
   const uint32_t n_keys = 6 + c.p_nanc + c.r_nanc + a_nanc;
   for (uint32_t kb = 0; kb < n_keys; kb += 64) {
-    // ---- bucket lookup: lane k probes key k ----
+    // ---- level-1: lane k probes scope key k ----
     const uint32_t k = kb + lane;
     uint32_t cat = 0, et = 0, ei = 0;
     if (k < n_keys) {
@@ -1255,102 +1400,26 @@ __global__ __launch_bounds__(BLOCK) void cedar_index_kernel(KArgs a) {
         et = j == 0 ? c.pt : (j == 1 ? c.rt : 0u);
       }
     }
-    uint32_t first = 0, cnt = 0;
-    if (cat && et < (1u << 28)) {
-      const uint32_t want = (cat << 28) | et;
-      uint32_t h = bucket_hash(cat, et, ei) & a.bmask;
-      for (;;) {
-        const uint4 e = *reinterpret_cast<const uint4*>(a.btab + (size_t)h * BT_WORDS);
-        if (e.x == 0) break;
-        if (e.x == want && e.y == ei) { first = e.z; cnt = e.w; break; }
-        h = (h + 1) & a.bmask;
+    const uint32_t key0 = (cat << 28) | et;
+    const uint32_t h1 = bucket_hash(cat, et, ei);
+    uint3 e1 = make_uint3(0, 0, 0);
+    if (cat && et < (1u << 28)) e1 = probe(a.btab, a.bmask, h1, key0, ei, 0, 0, 0);
+    stage(e1.x, e1.y, key0, ei);
+    // ---- level-2: one hot slot of this lane's hmask per round ----
+    uint32_t hm = e1.z;
+    while (__ballot(hm != 0)) {
+      uint3 e2 = make_uint3(0, 0, 0);
+      if (hm) {
+        const uint32_t h = __builtin_ctz(hm);
+        hm &= hm - 1;
+        const uint2 v = wl.hot[h];
+        const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
+        e2 = probe(a.btab, a.bmask, bucket_hash2(h1, h, v0, v1), key0, ei, h | BT_L2, v0, v1);
       }
+      stage(e2.x, e2.y, key0, ei);
     }
-    const uint64_t bm = __ballot(cnt != 0);
-    if (cnt) {
-      const uint32_t pos = mbcnt64(bm);
-      wl.bk[2 * pos] = first;
-      wl.bk[2 * pos + 1] = cnt;
-    }
-    wave_lds_sync();
-    const uint32_t nb = popc64(bm);
-    for (uint32_t b = 0; b < nb; b++) {
-      const uint32_t bfirst = uni(wl.bk[2 * b]), bcnt = uni(wl.bk[2 * b + 1]);
-      for (uint32_t base = 0; base < bcnt; base += 64) {
-        // ---- one candidate policy per lane ----
-        const uint32_t i = base + lane;
-        bool ok = i < bcnt;
-        const uint32_t ro = ok ? a.brefs[bfirst + i] : 0u;
-        const uint32_t* rec = a.bstream + ro;
-        const uint4* d4 = reinterpret_cast<const uint4*>(rec);
-        const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
-        const uint32_t flags = q0.x, kinds = q0.y;
-        const uint32_t tier = (flags >> 8) & 0xFF;
-        ok = ok && tier <= min_tier;
-        const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
-        if (ak != SK_ANY) {
-          if (a.amask_ok) {
-            ok = ok && (ak == SK_EQ ? (((as0 & q3.z) | (as1 & q3.w)) != 0) : (((am0 & q3.z) | (am1 & q3.w)) != 0));
-          } else if (ak == SK_EQ) {
-            ok = ok && c.at == q1.y && c.ai == q1.z;
-          } else if (ak == SK_IN) {
-            ok = ok && ((c.at == q1.y && c.ai == q1.z) || anc_has(c, c.aidx, q1.y, q1.z));
-          } else {
-            bool any = false;
-            for (uint32_t x = 0; ok && x < q1.y && !any; x++) {
-              const uint32_t qt = a.cpool[q1.z + 2 * x], qi = a.cpool[q1.z + 2 * x + 1];
-              any = (c.at == qt && c.ai == qi) || anc_has(c, c.aidx, qt, qi);
-            }
-            ok = ok && any;
-          }
-        }
-        if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
-        if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
-        else if (pk == SK_IN || pk == SK_ISIN) ok = ok && p_in(c, q0.w, q1.x, (flags >> 16) & 0x7F);
-        if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
-        if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
-        else if (rk == SK_IN || rk == SK_ISIN) ok = ok && r_in(c, q2.x, q2.y, (flags >> 24) & 0x7F);
-        // ---- conditions: this lane's atom chain ----
-        bool run = ok, err = false, cur = true;
-        Err e{0, 0, 0, 0, 0};
-        const uint32_t n_atom = q3.x;
-        for (uint32_t x = 0; __ballot(run && x < n_atom); x += ATOM_WORDS) {
-          if (run && x < n_atom) {
-            const uint4 at = *reinterpret_cast<const uint4*>(rec + POL_WORDS + x);
-            const uint32_t af = at.x >> 16;
-            if (af & AF_START) cur = !(af & AF_OR);
-            if ((af & AF_OR) ? !cur : cur) {
-              const uint32_t rr = eval_atom(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
-              if (rr == 2u) { err = true; run = false; }
-              else cur = (rr != 0u) != ((af & AF_NEG) != 0);
-            }
-            if ((af & AF_END) && run && (((af & AF_UNLESS) != 0) == cur)) run = false;
-          }
-        }
-        // ---- record hits ----
-        const bool hit = ok && (err || run);
-        const uint64_t hmask = __ballot(hit);
-        if (hmask) {
-          if (hit) {
-            const uint32_t pos = nh + mbcnt64(hmask);
-            if (pos < HCAP) {
-              wl.hp[pos] = q2.z;  // global policy index
-              wl.hm[pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8);
-              if (err) {
-                wl.he[4 * pos] = e.code | (e.aux << 8);
-                wl.he[4 * pos + 1] = e.k;
-                wl.he[4 * pos + 2] = e.et;
-                wl.he[4 * pos + 3] = e.ei;
-              }
-            }
-          }
-          nh += popc64(hmask);
-          min_tier = min(min_tier, wave_min(hit ? tier : 0xFFu));
-        }
-      }
-    }
-    wave_lds_sync();  // bucket list is rewritten by the next key group
   }
+  if (ne) run_stage();
 
   // ---- merge: deciding tier, duplicates, policy order ----
   const uint32_t t = min_tier;
@@ -1366,14 +1435,14 @@ __global__ __launch_bounds__(BLOCK) void cedar_index_kernel(KArgs a) {
   const uint32_t mj = have ? wl.hm[lane] : 0u;
   const uint32_t kind = mj & 0xFF;
   bool el = have && (mj >> 8) == t;
-  for (uint32_t x = 0; x < nh; x++) {  // a policy filed under several action buckets hits twice
+  for (uint32_t x = 0; x < nh; x++) {  // a policy filed under several keys the request has hits twice
     const uint32_t px = wl.hp[x];
     if (x < lane && px == pj && (wl.hm[x] >> 8) == t) el = false;
   }
   wl.hel[lane] = el ? 1u : 0u;
   wave_lds_sync();
   const uint32_t nf = popc64(__ballot(el && kind == 1)), np = popc64(__ballot(el && kind == 0)),
-                 ne = popc64(__ballot(el && kind == 2));
+                 nerr = popc64(__ballot(el && kind == 2));
   uint32_t rank = 0;
   for (uint32_t x = 0; x < nh; x++)
     rank += (wl.hel[x] && (wl.hm[x] & 0xFF) == kind && wl.hp[x] < pj) ? 1u : 0u;
@@ -1388,9 +1457,9 @@ __global__ __launch_bounds__(BLOCK) void cedar_index_kernel(KArgs a) {
     const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);
     const uint32_t nr = nf ? nf : np;
     uint32_t fl = RF_VALID | (nf ? RF_FORBID : 0u);
-    if (nr > a.capr || ne > a.cape) fl |= RF_OVERFLOW;
+    if (nr > a.capr || nerr > a.cape) fl |= RF_OVERFLOW;
     a.res[2 * (size_t)gid] = dec | (t << 8) | (fl << 16);
-    a.res[2 * (size_t)gid + 1] = min(nr, 0xFFFFu) | (min(ne, 0xFFFFu) << 16);
+    a.res[2 * (size_t)gid + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
   }
 }
 
@@ -1477,7 +1546,7 @@ int dev_image_upload(int device, const Image& img, DevImage* out) {
   d.n_pol = img.n_pol();
   d.n_tiers = img.n_tiers();
   d.n_gstr = img.n_gstr();
-  d.n_hot = (uint32_t)img.hot.size() / 2;
+  d.n_hot = (uint32_t)img.hot.size() / HOT_WORDS;
   *out = d;
   return 0;
 }
@@ -1502,6 +1571,8 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream) {
   int rc;
   if ((rc = up(&d.heap, b.heap, d.bytes, s))) return rc;
   if ((rc = up(&d.req_base, b.req_base, d.bytes, s))) return rc;
+  if ((rc = up(&d.rows, b.rows, d.bytes, s))) return rc;
+  d.row_words = b.row_words;
   if ((rc = up(&d.bstr_off, b.bstr_off, d.bytes, s))) return rc;
   if ((rc = up(&d.bstr_bytes, b.bstr_bytes, d.bytes, s))) return rc;
   const size_t n = std::max<uint32_t>(b.n(), 1);
@@ -1520,7 +1591,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream) {
 void dev_batch_free(DevBatch* d) {
   if (d->device < 0) return;
   (void)hipSetDevice(d->device);
-  for (void* p : {(void*)d->heap, (void*)d->req_base, (void*)d->req_idx, (void*)d->bstr_off, (void*)d->bstr_bytes,
+  for (void* p : {(void*)d->heap, (void*)d->req_base, (void*)d->rows, (void*)d->req_idx, (void*)d->bstr_off, (void*)d->bstr_bytes,
                   (void*)d->res, (void*)d->reasons_f, (void*)d->reasons_p, (void*)d->errs})
     if (p) (void)hipFree(p);
   *d = DevBatch();
@@ -1540,6 +1611,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.act = img.act; k.n_act = img.n_act; k.amask_ok = img.amask_ok;
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.brefs = img.brefs; k.bstream = img.bstream; k.bmask = img.bmask;
+  k.rows = b.rows; k.row_words = b.row_words;
   return k;
 }
 
@@ -1547,7 +1619,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
 // image is fully indexed, else the request-per-lane policy-stream kernel.
 static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
   if (img.indexed)
-    hipLaunchKernelGGL(cedar_index_kernel, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
+    hipLaunchKernelGGL(cedar_probe_kernel, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
   else
     hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>,
                        dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);

@@ -11,7 +11,10 @@
 //     through per-lane skip targets,
 //   * constant-folded set/record/extension literals in a constant pool,
 //   * `like` patterns pre-split into prefix / middle / suffix literals,
-//   * up to NHOT pre-resolved (var, attribute) pairs evaluated once per request.
+//   * up to NHOT hot attribute paths (var.k0.k1.., depth <= MAX_PATH) that the encoder resolves
+//     per request on the host into the columnar request row,
+//   * when/unless clauses over those paths as a forward-only branch graph of predicate atoms
+//     (image.h "atoms"), and a two-level scope/attribute index over all-atomic images.
 // Policy IDs follow the reference store conventions: memory `policy<i>` (memory.go:18),
 // directory `<file>.policy<i>` (directory.go:76), CRD `<name><i>-<uid>` (crd.go:60),
 // AVP `<id>.<i>` (verified_permissions.go:95), static `allow-all-admission` (main.go:112).
@@ -100,7 +103,8 @@ void emit_value_impl(const HVal& v, std::vector<uint32_t>& out, uint32_t space, 
 
 struct Compiler {
   Image& I;
-  std::map<std::pair<uint32_t, uint32_t>, uint32_t> hot;  // (var, key sid) -> hot slot
+  using Path = std::pair<uint32_t, std::vector<uint32_t>>;  // (var, key sids)
+  std::map<Path, uint32_t> hot;                             // hot path -> slot
   // per-policy state
   uint32_t code0 = 0;
   uint32_t max_slot = 0;
@@ -248,12 +252,10 @@ struct Compiler {
       case EK::Attr:
       case EK::Has: {
         const Expr& k0 = *e.kids[0];
-        if (k0.k == EK::Var) {
-          auto it = hot.find({(uint32_t)var_index(k0.name), intern(e.name)});
-          if (it != hot.end()) {
-            emit(e.k == EK::Attr ? OP_HOT : OP_HOTHAS, d, 0, 0, it->second, 0);
-            return;
-          }
+        int h = hot_of(e);
+        if (h >= 0) {
+          emit(e.k == EK::Attr ? OP_HOT : OP_HOTHAS, d, 0, 0, (uint32_t)h, 0);
+          return;
         }
         compile(k0, d);
         emit(e.k == EK::Attr ? OP_ATTR : OP_HAS, d, d, 0, 0, intern(e.name));
@@ -370,18 +372,35 @@ struct Compiler {
     throw CedarError("unsupported expression");
   }
 
-  void count_hot(const Expr& e, std::map<std::pair<uint32_t, uint32_t>, uint32_t>& cnt) {
-    if ((e.k == EK::Attr || e.k == EK::Has) && e.kids[0]->k == EK::Var)
-      cnt[{(uint32_t)var_index(e.kids[0]->name), intern(e.name)}]++;
+  // Path of an attribute-access / has chain rooted at a variable: `resource.metadata.name` and
+  // `resource.metadata has name` both have path (resource, [metadata, name]).
+  bool path_of(const Expr& e, Path& out) {
+    if (e.k != EK::Attr && e.k != EK::Has) return false;
+    std::vector<uint32_t> keys{intern(e.name)};
+    const Expr* x = e.kids[0].get();
+    while (x->k == EK::Attr) {
+      keys.push_back(intern(x->name));
+      x = x->kids[0].get();
+    }
+    if (x->k != EK::Var || keys.size() > MAX_PATH) return false;
+    std::reverse(keys.begin(), keys.end());
+    out = Path((uint32_t)var_index(x->name), std::move(keys));
+    return true;
+  }
+  void count_hot(const Expr& e, std::map<Path, uint32_t>& cnt) {
+    Path p;
+    if (path_of(e, p)) cnt[p]++;
     for (auto& k : e.kids) count_hot(*k, cnt);
   }
 
   // ---- atoms ----------------------------------------------------------------------------------
-  int hot_of(const Expr& e) {  // e is Attr/Has over a Var
-    if ((e.k != EK::Attr && e.k != EK::Has) || e.kids[0]->k != EK::Var) return -1;
-    auto it = hot.find({(uint32_t)var_index(e.kids[0]->name), intern(e.name)});
+  int hot_of(const Expr& e) {  // e is an Attr/Has chain over a Var
+    Path p;
+    if (!path_of(e, p)) return -1;
+    auto it = hot.find(p);
     return it == hot.end() ? -1 : (int)it->second;
   }
+  std::vector<uint32_t> hot_depth;  // slot -> path depth
   static bool is_prim(const HVal& v) { return v.k == VK::Bool || v.k == VK::Long || v.k == VK::Str || v.k == VK::Ent; }
   void reg_form(const HVal& v, uint32_t* w) {
     switch (v.k) {
@@ -395,14 +414,16 @@ struct Compiler {
     if (e.k == EK::Lit && is_prim(e.lit)) { v = e.lit; return true; }
     return false;
   }
-  // One clause element -> one atom (4 words) or false.
-  bool atom(const Expr& e0, uint32_t flags, std::vector<uint32_t>& out) {
+  // One leaf predicate -> one atom (kind, h, operands) or false. *neg: the atom's truth is the
+  // negation of the expression's (`!=`). Data-carrying atoms get w1 relative to adata and
+  // *patch set (re-based to the record once the atom count is known).
+  bool atom(const Expr& e0, uint32_t* w, bool* neg, bool* patch) {
     const Expr* e = &e0;
-    while (e->k == EK::Not) { flags ^= AF_NEG; e = e->kids[0].get(); }
-    uint32_t w[4] = {0, 0, 0, 0};
+    w[0] = w[1] = w[2] = w[3] = 0;
+    *neg = false;
+    *patch = false;
     auto put = [&](uint32_t kind, uint32_t h) {
-      w[0] = kind | (h << 8) | (flags << 16);
-      out.insert(out.end(), w, w + 4);
+      w[0] = kind | (h << 8);
       return true;
     };
     HVal c;
@@ -417,8 +438,12 @@ struct Compiler {
       case EK::Like:
         if ((h = hot_of(*e->kids[0])) < 0 || e->kids[0]->k != EK::Attr) return false;
         w[1] = pattern_into(e->pat, adata);
-        apatch.push_back(out.size() + 1);
+        *patch = true;
         return put(AK_LIKE, (uint32_t)h);
+      case EK::Lit:
+        if (e->lit.k != VK::Bool) return false;
+        *neg = !e->lit.b;
+        return put(AK_TRUE, 0);
       case EK::Is:
         if (e->has_in || e->kids[0]->k != EK::Var || e->kids[0]->name == "context") return false;
         w[1] = intern(e->name);
@@ -435,7 +460,7 @@ struct Compiler {
           for (auto& x : s.elems) { uint32_t r[3]; reg_form(x, r); adata.insert(adata.end(), r, r + 3); }
           w[1] = off;
           w[2] = (uint32_t)s.elems.size();
-          apatch.push_back(out.size() + 1);
+          *patch = true;
           return put(AK_INSET, (uint32_t)h);
         }
         if (recv.k == EK::Attr && (h = hot_of(recv)) >= 0 && lit_prim(arg, c)) {
@@ -517,7 +542,7 @@ struct Compiler {
         w[1] = off;
         w[2] = (uint32_t)tmpls.size();
         w[3] = e->name == "contains" ? 1u : 0u;
-        apatch.push_back(out.size() + 1);
+        *patch = true;
         return put(AK_RECSET, (uint32_t)h);
       }
       return false;
@@ -526,9 +551,16 @@ struct Compiler {
         const Expr& l = *e->kids[0];
         const Expr& r = *e->kids[1];
         if (e->op == BinOp::Eq || e->op == BinOp::Ne) {
-          if (e->op == BinOp::Ne) flags ^= AF_NEG;
+          if (e->op == BinOp::Ne) *neg = true;
           if (l.k == EK::Attr && (h = hot_of(l)) >= 0 && lit_prim(r, c)) { reg_form(c, &w[1]); return put(AK_EQ, (uint32_t)h); }
           if (r.k == EK::Attr && (h = hot_of(r)) >= 0 && lit_prim(l, c)) { reg_form(c, &w[1]); return put(AK_EQ, (uint32_t)h); }
+          const Expr* var = l.k == EK::Var ? &l : (r.k == EK::Var ? &r : nullptr);
+          const Expr& other = &l == var ? r : l;
+          if (var && var->name != "context" && lit_prim(other, c) && c.k == VK::Ent) {
+            w[1] = intern(c.etype);
+            w[2] = intern(c.s);
+            return put(AK_EQV, (uint32_t)var_index(var->name));
+          }
           int h2;
           if (l.k == EK::Attr && r.k == EK::Attr && (h = hot_of(l)) >= 0 && (h2 = hot_of(r)) >= 0) {
             w[1] = (uint32_t)h2;
@@ -537,11 +569,24 @@ struct Compiler {
           return false;
         }
         if (e->op == BinOp::In) {
-          if (l.k != EK::Var || l.name == "context" || !lit_prim(r, c) || c.k != VK::Ent) return false;
-          w[1] = intern(c.etype);
-          w[2] = intern(c.s);
-          w[3] = uid_bloom_bit(w[1], w[2]);
-          return put(AK_IN, (uint32_t)var_index(l.name));
+          if (l.k != EK::Var || l.name == "context") return false;
+          if (lit_prim(r, c) && c.k == VK::Ent) {
+            w[1] = intern(c.etype);
+            w[2] = intern(c.s);
+            w[3] = uid_bloom_bit(w[1], w[2]);
+            return put(AK_IN, (uint32_t)var_index(l.name));
+          }
+          HVal sv;
+          if (r.k == EK::Set && fold(r, sv)) {  // var in [E1, E2, ..]: entity literals only
+            for (auto& x : sv.elems) if (x.k != VK::Ent) return false;
+            uint32_t off = (uint32_t)adata.size();
+            for (auto& x : sv.elems) { adata.push_back(intern(x.etype)); adata.push_back(intern(x.s)); }
+            w[1] = off;
+            w[2] = (uint32_t)sv.elems.size();
+            *patch = true;
+            return put(AK_INANY, (uint32_t)var_index(l.name));
+          }
+          return false;
         }
         if (e->op == BinOp::Lt || e->op == BinOp::Le || e->op == BinOp::Gt || e->op == BinOp::Ge) {
           static const uint32_t code[] = {0, 1, 2, 3};
@@ -563,37 +608,151 @@ struct Compiler {
       default: return false;
     }
   }
-  static void flatten(const Expr& e, EK kind, std::vector<const Expr*>& out) {
-    if (e.k == kind) { flatten(*e.kids[0], kind, out); flatten(*e.kids[1], kind, out); }
-    else out.push_back(&e);
+  // ---- atom graph ------------------------------------------------------------------------------
+  // Labels are forward references to atom indices; L_SAT / L_UNSAT are the policy outcomes.
+  static constexpr uint32_t L_SAT = 0xFFFFFFFFu, L_UNSAT = 0xFFFFFFFEu;
+  struct AtomB {
+    uint32_t w[4];
+    uint32_t t, f;  // labels
+    bool patch;
+  };
+  std::vector<AtomB> ab;
+  std::vector<int64_t> label_at;
+  uint32_t new_label() { label_at.push_back(-1); return (uint32_t)label_at.size() - 1; }
+  void place(uint32_t l) { label_at[l] = (int64_t)ab.size(); }
+  // Lowers boolean expression e so that control reaches T when it is true and F when false.
+  bool gen(const Expr& e, uint32_t T, uint32_t F) {
+    switch (e.k) {
+      case EK::And: {
+        uint32_t l = new_label();
+        if (!gen(*e.kids[0], l, F)) return false;
+        place(l);
+        return gen(*e.kids[1], T, F);
+      }
+      case EK::Or: {
+        uint32_t l = new_label();
+        if (!gen(*e.kids[0], T, l)) return false;
+        place(l);
+        return gen(*e.kids[1], T, F);
+      }
+      case EK::Not: return gen(*e.kids[0], F, T);
+      case EK::If: {
+        uint32_t lt = new_label(), le = new_label();
+        if (!gen(*e.kids[0], lt, le)) return false;
+        place(lt);
+        if (!gen(*e.kids[1], T, F)) return false;
+        place(le);
+        return gen(*e.kids[2], T, F);
+      }
+      case EK::Is:
+        if (e.has_in) {
+          // `v is T in E`: the type test short-circuits before E is evaluated
+          if (e.kids[0]->k != EK::Var || e.kids[0]->name == "context") return false;
+          Expr is = e;
+          is.has_in = false;
+          is.kids.resize(1);
+          Expr in;
+          in.k = EK::Bin;
+          in.op = BinOp::In;
+          in.kids = {e.kids[0], e.kids[1]};
+          uint32_t l = new_label();
+          if (!gen(is, l, F)) return false;
+          place(l);
+          return gen(in, T, F);
+        }
+        break;
+      default: break;
+    }
+    AtomB a;
+    bool neg;
+    if (!atom(e, a.w, &neg, &a.patch)) return false;
+    a.t = neg ? F : T;
+    a.f = neg ? T : F;
+    ab.push_back(a);
+    return ab.size() <= MAX_ATOMS;
   }
-  // All when/unless clauses as atom chains, or false (then the policy uses bytecode).
-  // Output: atoms, then their data (INSET element triples, LIKE patterns) addressed relative to
-  // the policy record start; *n_atom_words = words of atoms proper.
+
+  // All when/unless clauses as one atom graph, or false (then the policy uses bytecode).
+  // Output: atoms, then their data (INSET element triples, LIKE patterns, ...) addressed relative
+  // to the policy record start; *n_atom_words = words of atoms proper.
   std::vector<uint32_t> adata;
-  std::vector<size_t> apatch;
   std::vector<uint32_t> rs_patch;  // adata words holding adata-relative offsets
   bool atoms(const Policy& p, std::vector<uint32_t>& out, uint32_t* n_atom_words) {
     adata.clear();
-    apatch.clear();
     rs_patch.clear();
-    for (auto& c : p.conds) {
-      const Expr& root = *c.second;
-      std::vector<const Expr*> elems;
-      uint32_t base = c.first ? 0u : (uint32_t)AF_UNLESS;
-      if (root.k == EK::Or) { flatten(root, EK::Or, elems); base |= AF_OR; }
-      else flatten(root, EK::And, elems);
-      for (size_t i = 0; i < elems.size(); i++) {
-        uint32_t f = base | (i == 0 ? (uint32_t)AF_START : 0u) | (i + 1 == elems.size() ? (uint32_t)AF_END : 0u);
-        if (!atom(*elems[i], f, out)) return false;
-      }
+    ab.clear();
+    label_at.clear();
+    for (size_t i = 0; i < p.conds.size(); i++) {
+      const bool when = p.conds[i].first;
+      const uint32_t next = i + 1 < p.conds.size() ? new_label() : L_SAT;
+      if (!gen(*p.conds[i].second, when ? next : L_UNSAT, when ? L_UNSAT : next)) return false;
+      if (next != L_SAT) place(next);
+    }
+    auto target = [&](uint32_t l) -> uint32_t {
+      if (l == L_SAT) return AT_SAT;
+      if (l == L_UNSAT) return AT_UNSAT;
+      if (label_at[l] < 0 || label_at[l] >= (int64_t)ab.size()) throw CedarError("internal: dangling atom label");
+      return (uint32_t)label_at[l];
+    };
+    const uint32_t base = POL_WORDS + ATOM_WORDS * (uint32_t)ab.size();
+    out.clear();
+    for (size_t i = 0; i < ab.size(); i++) {
+      AtomB& a = ab[i];
+      const uint32_t t = target(a.t), f = target(a.f);
+      if ((t < AT_UNSAT && t <= i) || (f < AT_UNSAT && f <= i)) throw CedarError("internal: backward atom edge");
+      out.push_back(a.w[0] | (t << 16) | (f << 24));
+      out.push_back(a.patch ? a.w[1] + base : a.w[1]);
+      out.push_back(a.w[2]);
+      out.push_back(a.w[3]);
     }
     *n_atom_words = (uint32_t)out.size();
-    const uint32_t base = POL_WORDS + (uint32_t)out.size();
-    for (size_t k : apatch) out[k] += base;
     for (uint32_t k : rs_patch) adata[k] += base;
     out.insert(out.end(), adata.begin(), adata.end());
     return true;
+  }
+
+  // Attribute key of an atomic policy (image.h "scope index", level 2): the first equality atom
+  // on the graph's entry spine (each earlier atom cannot raise and has one edge to UNSAT), whose
+  // false edge is UNSAT and whose constant has a canonical memory form.
+  struct AttrKey {
+    bool ok = false, guarded = false;
+    uint32_t h = 0, v0 = 0, v1 = 0;
+  };
+  AttrKey attr_key(const std::vector<uint32_t>& at, uint32_t n_atom_words) const {
+    AttrKey k;
+    const uint32_t n = n_atom_words / ATOM_WORDS;
+    std::vector<uint32_t> present;  // single-level hot slots known present on the spine
+    uint32_t i = 0;
+    while (i < n) {
+      const uint32_t* a = &at[ATOM_WORDS * i];
+      const uint32_t kind = a[0] & 0xFF, h = (a[0] >> 8) & 0xFF, t = (a[0] >> 16) & 0xFF, f = a[0] >> 24;
+      if (kind == AK_EQ && f == AT_UNSAT && t != AT_UNSAT) {
+        const uint32_t tag = a[1] >> TAG_SHIFT;
+        const bool small_long = tag == T_LONG && a[3] == (((int32_t)a[2] < 0) ? 0xFFFFFFFFu : 0u);
+        if (tag == T_STR || tag == T_BOOL || tag == T_ENT || small_long) {
+          k.ok = true;
+          k.h = h;
+          k.v0 = tag == T_LONG ? mk_w0(T_LONG, 0) : a[1];
+          k.v1 = a[2];
+          k.guarded = std::find(present.begin(), present.end(), h) != present.end();
+        }
+        return k;
+      }
+      const bool no_error = kind == AK_IS || kind == AK_IN || kind == AK_INANY || kind == AK_TRUE || kind == AK_EQV ||
+                            (kind == AK_HAS && hot_depth[h] == 1);
+      if (!no_error) return k;
+      uint32_t nxt;
+      if (f == AT_UNSAT && t < AT_UNSAT) {
+        nxt = t;
+        if (kind == AK_HAS) present.push_back(h);
+      } else if (t == AT_UNSAT && f < AT_UNSAT) {
+        nxt = f;
+      } else {
+        return k;
+      }
+      i = nxt;
+    }
+    return k;
   }
 
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> act_index;  // action entity -> bit
@@ -659,11 +818,13 @@ struct Compiler {
     lane_off = 0;
     std::vector<uint32_t> at;
     uint32_t n_atom_words = 0;
+    AttrKey key;
     if (atoms(p, at, &n_atom_words)) {
       w[PW_FLAGS] |= PF_ATOMIC;
       w[PW_SLOTS] = n_atom_words;
       I.code.insert(I.code.end(), at.begin(), at.end());
       I.n_atomic++;
+      key = attr_key(at, n_atom_words);
     } else {
       for (auto& c : p.conds) {
         compile(*c.second, 0);
@@ -675,23 +836,29 @@ struct Compiler {
     if (!(w[PW_FLAGS] & PF_ATOMIC)) w[PW_SLOTS] = max_slot;
     w[PW_LANE] = lane_off;
     I.pol.insert(I.pol.end(), w, w + POL_WORDS);
+    akeys.push_back(key);
   }
+  std::vector<AttrKey> akeys;  // per policy (global index)
 };
 
 }  // namespace
 
-// Scope index (image.h): file each atomic policy under the candidate key set with the fewest
-// competing policies, then lay the stream records out bucket by bucket.
-static void build_scope_index(Image& img) {
-  using Key = std::array<uint32_t, 3>;
+// Scope index (image.h "scope index"): file each policy of an all-atomic image under the key set
+// with the fewest competing policies (a level-1 scope key, refined by the policy's attribute key
+// when it has one), then lay out fixed record heads bucket by bucket and the full records in the
+// ext area.
+template <class AK>
+static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
+  using L1 = std::array<uint32_t, 3>;                   // (cat, et, ei)
+  using L2 = std::array<uint32_t, 6>;                   // (cat, et, ei, h, v0, v1)
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.brefs.clear(); img.bstream.clear();
   img.indexed = (n > 0 && img.n_atomic == n) ? 1u : 0u;
   if (!img.indexed) {
-    img.btab.assign(BT_WORDS, 0); img.brefs.assign(1, 0); img.bstream.assign(POL_WORDS, 0);
+    img.btab.assign(BT_WORDS, 0); img.brefs.assign(1, 0); img.bstream.assign(HEAD_WORDS, 0);
     return;
   }
-  // stream record offset of every policy
+  // stream record offset / length of every policy
   std::vector<uint32_t> rec_off(n), rec_len(n);
   for (size_t ch = 0; ch < img.chunks.size(); ch += 4) {
     uint32_t off = img.chunks[ch];
@@ -701,57 +868,101 @@ static void build_scope_index(Image& img) {
       off += len;
     }
   }
-  std::vector<std::vector<std::vector<Key>>> opts(n);  // per policy: options, each a key list
-  std::map<Key, uint32_t> cnt;
+  // scope options per policy (each a list of level-1 keys the request must enumerate)
+  std::vector<std::vector<std::vector<L1>>> opts(n);
   for (uint32_t p = 0; p < n; p++) {
     const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
     const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
     auto& o = opts[p];
-    if (pk == SK_EQ || pk == SK_IN || pk == SK_ISIN) o.push_back({Key{BK_P, d[PW_P_ET], d[PW_P_EI]}});
-    if (rk == SK_EQ || rk == SK_IN || rk == SK_ISIN) o.push_back({Key{BK_R, d[PW_R_ET], d[PW_R_EI]}});
-    if (ak == SK_EQ || ak == SK_IN) o.push_back({Key{BK_A, d[PW_A_ET], d[PW_A_EI]}});
+    if (pk == SK_EQ || pk == SK_IN || pk == SK_ISIN) o.push_back({L1{BK_P, d[PW_P_ET], d[PW_P_EI]}});
+    if (rk == SK_EQ || rk == SK_IN || rk == SK_ISIN) o.push_back({L1{BK_R, d[PW_R_ET], d[PW_R_EI]}});
+    if (ak == SK_EQ || ak == SK_IN) o.push_back({L1{BK_A, d[PW_A_ET], d[PW_A_EI]}});
     if (ak == SK_INSET) {
-      std::vector<Key> ks;
-      for (uint32_t k = 0; k < d[PW_A_ET]; k++) ks.push_back(Key{BK_A, img.cpool[d[PW_A_EI] + 2 * k], img.cpool[d[PW_A_EI] + 2 * k + 1]});
+      std::vector<L1> ks;
+      for (uint32_t k = 0; k < d[PW_A_ET]; k++) ks.push_back(L1{BK_A, img.cpool[d[PW_A_EI] + 2 * k], img.cpool[d[PW_A_EI] + 2 * k + 1]});
       std::sort(ks.begin(), ks.end());
       ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
       o.push_back(ks);  // empty list: `action in []` never applies, the policy needs no bucket
     }
-    if (rk == SK_IS || rk == SK_ISIN) o.push_back({Key{BK_RT, d[PW_R_TYPE], 0}});
-    if (pk == SK_IS || pk == SK_ISIN) o.push_back({Key{BK_PT, d[PW_P_TYPE], 0}});
-    o.push_back({Key{BK_ALL, 0, 0}});
-    for (auto& ks : o)
-      for (auto& k : ks) cnt[k]++;
+    if (rk == SK_IS || rk == SK_ISIN) o.push_back({L1{BK_RT, d[PW_R_TYPE], 0}});
+    if (pk == SK_IS || pk == SK_ISIN) o.push_back({L1{BK_PT, d[PW_P_TYPE], 0}});
+    o.push_back({L1{BK_ALL, 0, 0}});
   }
-  std::map<Key, std::vector<uint32_t>> buckets;  // key -> policies (ascending: p increases)
+  auto l2_of = [&](const L1& k, uint32_t p) { return L2{k[0], k[1], k[2], akeys[p].h, akeys[p].v0, akeys[p].v1}; };
+  std::map<L1, uint32_t> c1;
+  std::map<L2, uint32_t> c2;
+  for (uint32_t p = 0; p < n; p++)
+    for (auto& ks : opts[p])
+      for (auto& k : ks) {
+        if (akeys[p].ok) c2[l2_of(k, p)]++;
+        else c1[k]++;
+      }
+  std::map<L1, std::vector<uint32_t>> b1;  // level-1 unkeyed lists (ascending policy index)
+  std::map<L2, std::vector<uint32_t>> b2;
+  std::map<L1, uint32_t> hmask;
   for (uint32_t p = 0; p < n; p++) {
     size_t best = 0;
     uint64_t best_cost = ~0ull;
     for (size_t i = 0; i < opts[p].size(); i++) {
       uint64_t c = 0;
-      for (auto& k : opts[p][i]) c += cnt[k];
+      for (auto& k : opts[p][i]) c += akeys[p].ok ? c2[l2_of(k, p)] : c1[k];
       if (c < best_cost) { best_cost = c; best = i; }
     }
-    for (auto& k : opts[p][best]) buckets[k].push_back(p);
-  }
-  uint32_t size = 16;
-  while (size < 2 * buckets.size()) size <<= 1;
-  img.btab.assign((size_t)size * BT_WORDS, 0);
-  for (auto& kv : buckets) {
-    const Key& k = kv.first;
-    if (k[1] >= (1u << 28)) throw CedarError("string table too large for the scope index");
-    const uint32_t first = (uint32_t)img.brefs.size();
-    for (uint32_t p : kv.second) {
-      img.brefs.push_back((uint32_t)img.bstream.size());
-      img.bstream.insert(img.bstream.end(), img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p]);
+    for (auto& k : opts[p][best]) {
+      if (!akeys[p].ok) { b1[k].push_back(p); continue; }
+      b1[k];  // level-1 entry carries the hmask even when it has no unkeyed policies
+      hmask[k] |= 1u << akeys[p].h;
+      b2[l2_of(k, p)].push_back(p);
+      if (!akeys[p].guarded) b2[L2{k[0], k[1], k[2], akeys[p].h, MISSING_W0, 0}].push_back(p);
     }
-    uint32_t h = bucket_hash(k[0], k[1], k[2]) & (size - 1);
-    while (img.btab[(size_t)h * BT_WORDS] != 0) h = (h + 1) & (size - 1);
-    uint32_t* e = &img.btab[(size_t)h * BT_WORDS];
-    e[0] = (k[0] << 28) | k[1]; e[1] = k[2]; e[2] = first; e[3] = (uint32_t)kv.second.size();
   }
-  if (img.brefs.empty()) img.brefs.push_back(0);
-  if (img.bstream.size() < POL_WORDS) img.bstream.resize(POL_WORDS, 0);  // idle lanes read record 0
+  // record heads (bucket order) then the ext area (one full record per policy)
+  uint32_t n_heads = 0;
+  for (auto& kv : b1) n_heads += (uint32_t)kv.second.size();
+  for (auto& kv : b2) n_heads += (uint32_t)kv.second.size();
+  std::vector<uint32_t> ext(n);
+  uint32_t ext_end = n_heads * HEAD_WORDS;
+  for (uint32_t p = 0; p < n; p++) { ext[p] = ext_end; ext_end += rec_len[p]; }
+  img.bstream.assign(std::max<uint32_t>(ext_end, HEAD_WORDS), 0);
+  for (uint32_t p = 0; p < n; p++)
+    std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
+  uint32_t head = 0;
+  auto put_heads = [&](const std::vector<uint32_t>& ps) {
+    const uint32_t first = head;
+    for (uint32_t p : ps) {
+      uint32_t* hd = &img.bstream[(size_t)head * HEAD_WORDS];
+      const uint32_t* src = &img.pstream[rec_off[p]];
+      const uint32_t nw = std::min<uint32_t>(rec_len[p], HEAD_WORDS);
+      std::copy(src, src + nw, hd);
+      hd[PW_EXT] = ext[p];
+      head++;
+    }
+    return first;
+  };
+  const size_t n_entries = b1.size() + b2.size();
+  uint32_t size = 16;
+  while (size < 2 * n_entries) size <<= 1;
+  img.btab.assign((size_t)size * BT_WORDS, 0);
+  auto insert = [&](uint32_t hash, const uint32_t* e) {
+    uint32_t h = hash & (size - 1);
+    while (img.btab[(size_t)h * BT_WORDS] != 0) h = (h + 1) & (size - 1);
+    std::copy(e, e + BT_WORDS, &img.btab[(size_t)h * BT_WORDS]);
+  };
+  for (auto& kv : b1) {
+    const L1& k = kv.first;
+    if (k[1] >= (1u << 28)) throw CedarError("string table too large for the scope index");
+    const uint32_t first = put_heads(kv.second);
+    const uint32_t e[BT_WORDS] = {(k[0] << 28) | k[1], k[2], 0, hmask.count(k) ? hmask[k] : 0u, 0, first,
+                                  (uint32_t)kv.second.size(), 0};
+    insert(bucket_hash(k[0], k[1], k[2]), e);
+  }
+  for (auto& kv : b2) {
+    const L2& k = kv.first;
+    const uint32_t first = put_heads(kv.second);
+    const uint32_t e[BT_WORDS] = {(k[0] << 28) | k[1], k[2], k[3] | BT_L2, k[4], k[5], first, (uint32_t)kv.second.size(), 0};
+    insert(bucket_hash2(bucket_hash(k[0], k[1], k[2]), k[3], k[4], k[5]), e);
+  }
+  img.brefs.assign(1, 0);
 }
 
 std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch) {
@@ -778,18 +989,21 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
       }
     }
   }
-  // hot attribute selection over the whole image
-  std::map<std::pair<uint32_t, uint32_t>, uint32_t> cnt;
+  // hot attribute paths over the whole image: the NHOT most used
+  std::map<Compiler::Path, uint32_t> cnt;
   for (auto& tp : parsed)
     for (auto& p : tp)
       for (auto& c : p.conds) C.count_hot(*c.second, cnt);
-  std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> order;
+  std::vector<std::pair<uint32_t, Compiler::Path>> order;
   for (auto& kv : cnt) order.emplace_back(kv.second, kv.first);
   std::sort(order.begin(), order.end(), [](auto& a, auto& b) { return a.first != b.first ? a.first > b.first : a.second < b.second; });
   for (size_t k = 0; k < order.size() && k < NHOT; k++) {
-    C.hot[order[k].second] = (uint32_t)k;
-    img->hot.push_back(order[k].second.first);
-    img->hot.push_back(order[k].second.second);
+    const Compiler::Path& path = order[k].second;
+    C.hot[path] = (uint32_t)k;
+    C.hot_depth.push_back((uint32_t)path.second.size());
+    img->hot.push_back(path.first);
+    img->hot.push_back((uint32_t)path.second.size());
+    for (uint32_t j = 0; j < MAX_PATH; j++) img->hot.push_back(j < path.second.size() ? path.second[j] : 0u);
   }
   for (auto& tp : parsed)
     for (auto& p : tp) C.collect_actions(p.action);
@@ -835,7 +1049,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     }
     if (img->pstream.empty()) img->pstream.resize(4, 0);
   }
-  build_scope_index(*img);
+  build_scope_index(*img, C.akeys);
   // global string table
   img->gstr_off.clear();
   img->gstr_bytes.clear();

@@ -22,10 +22,10 @@ struct DevImage {
 
 struct DevBatch {
   int device = -1;
-  uint32_t *heap = nullptr, *req_base = nullptr, *req_idx = nullptr, *bstr_off = nullptr;
+  uint32_t *heap = nullptr, *req_base = nullptr, *rows = nullptr, *req_idx = nullptr, *bstr_off = nullptr;
   uint8_t* bstr_bytes = nullptr;
   uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
-  uint32_t n = 0, capr = 0, cape = 0;
+  uint32_t n = 0, capr = 0, cape = 0, row_words = 0;
   size_t heap_words = 0, bytes = 0;
 };
 

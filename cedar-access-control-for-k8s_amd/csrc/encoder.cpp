@@ -37,6 +37,35 @@ const std::string& Batch::str(uint32_t id) const {
 }
 
 namespace {
+// memory-form record lookup inside an emitted request block (the device's rec_get, on the host)
+bool blk_rec_get(const std::vector<uint32_t>& blk, uint32_t rw0, uint32_t n, uint32_t key, uint32_t& w0, uint32_t& w1) {
+  const uint32_t off = rw0 & OFF_MASK;
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (blk[off + 1 + 3 * mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < n && blk[off + 1 + 3 * lo] == key) {
+    w0 = blk[off + 2 + 3 * lo];
+    w1 = blk[off + 3 + 3 * lo];
+    return true;
+  }
+  return false;
+}
+uint32_t mem_tname(uint32_t w0) {
+  switch (w0 >> TAG_SHIFT) {
+    case T_BOOL: return TN_BOOL;
+    case T_LONG: case T_LONGREF: return TN_LONG;
+    case T_STR: return TN_STRING;
+    case T_ENT: return TN_ENTITY;
+    case T_SET: return TN_SET;
+    case T_REC: return TN_RECORD;
+    case T_DEC: return TN_DECIMAL;
+    case T_IP: return TN_IP;
+    default: return TN_UNKNOWN;
+  }
+}
 struct PairHash {
   size_t operator()(const std::pair<uint32_t, uint32_t>& p) const { return ((size_t)p.first << 32) ^ p.second; }
 };
@@ -112,6 +141,59 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
     blk.push_back((uint32_t)anc.size());
     for (auto& a : anc) { blk.push_back(a.first); blk.push_back(a.second); }
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = mk_ref(SP_HEAP, off);
+  }
+  // ---- columnar row: UIDs, ancestor lists, hot paths resolved as attribute access would ----
+  if (!row_words) row_words = img->row_words();
+  const size_t r0 = rows.size();
+  rows.resize(r0 + row_words, 0);
+  uint32_t* row = &rows[r0];
+  row[RW_P] = pu.first; row[RW_P + 1] = pu.second;
+  row[RW_A] = au.first; row[RW_A + 1] = au.second;
+  row[RW_R] = ru.first; row[RW_R + 1] = ru.second;
+  auto anc_into = [&](uint32_t idx, uint32_t w_off, uint32_t w_n) {
+    if (idx == NO_ENT) return;
+    const uint32_t ref = blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;
+    rows[r0 + w_off] = ref + 1;
+    rows[r0 + w_n] = blk[ref];
+  };
+  anc_into(blk[RH_PIDX], RW_PANC, RW_PN);
+  anc_into(blk[RH_RIDX], RW_RANC, RW_RN);
+  anc_into(blk[RH_AIDX], RW_AANC, RW_AN);
+  rows[r0 + RW_BLK] = (uint32_t)heap.size();
+  const uint32_t nh = img->n_hot();
+  for (uint32_t h = 0; h < nh; h++) {
+    const uint32_t* hp = &img->hot[(size_t)h * HOT_WORDS];
+    const uint32_t var = hp[0], depth = hp[1];
+    uint32_t w0, w1;
+    if (var == 3) { w0 = blk[RH_CTX]; w1 = blk[RH_CTX + 1]; }
+    else { const uint32_t o = var == 0 ? RH_P : var == 1 ? RH_A : RH_R; w0 = blk[o]; w1 = blk[o + 1]; }
+    uint32_t code = E_NONE, aux = 0, k = 0, et = 0, ei = 0;
+    bool fin = false;
+    for (uint32_t j = 0; j < depth && code == E_NONE; j++) {
+      const uint32_t key = hp[2 + j], tag = w0 >> TAG_SHIFT;
+      const bool last = j + 1 == depth;
+      if (tag == T_ENT) {
+        const uint32_t t = w0 & X_MASK, id = w1;
+        auto it = index.find({t, id});
+        if (it == index.end()) { code = E_ENTITY_MISSING; et = t; ei = id; fin = last; break; }
+        const uint32_t* er = &blk[RH_WORDS + it->second * ENT_WORDS];
+        if (!blk_rec_get(blk, er[ER_ATTR0], er[ER_ATTR1], key, w0, w1)) { code = E_ATTR_ENTITY; k = key; et = t; ei = id; fin = last; }
+      } else if (tag == T_REC) {
+        if (!blk_rec_get(blk, w0, w1, key, w0, w1)) { code = E_ATTR_RECORD; k = key; fin = last; }
+      } else {
+        code = E_TYPE;
+        aux = TN_ENTITY_OR_RECORD | (mem_tname(w0) << 8);
+      }
+    }
+    if (code == E_NONE) {
+      rows[r0 + RW_HDR + 2 * h] = w0;
+      rows[r0 + RW_HDR + 2 * h + 1] = w1;
+    } else {
+      const uint32_t off = (uint32_t)blk.size();
+      blk.push_back(code | (aux << 8)); blk.push_back(k); blk.push_back(et); blk.push_back(ei);
+      rows[r0 + RW_HDR + 2 * h] = mk_w0(T_NONE, code | (fin ? HS_FINAL : 0u));
+      rows[r0 + RW_HDR + 2 * h + 1] = off;
+    }
   }
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
   if (heap.size() + blk.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");

@@ -24,7 +24,7 @@ struct PolicyMeta {
 // uploaded verbatim; the rest is host-side metadata for rendering diagnostics.
 struct Image {
   uint64_t epoch = 0;
-  std::vector<uint32_t> pol, tier_end, code, cpool, gstr_off, hot;  // hot: (var, key sid) pairs
+  std::vector<uint32_t> pol, tier_end, code, cpool, gstr_off, hot;  // hot: HOT_WORDS per hot path
   // device policy stream: per policy a record [descriptor (POL_WORDS) | code, padded to 4 words]
   // with PW_CODE relative to the record; records grouped into chunks of <= CHUNK_WORDS words
   // that never cross a tier. chunks: (word offset, words, first policy, end policy) per chunk;
@@ -44,6 +44,8 @@ struct Image {
   uint32_t n_tiers() const { return (uint32_t)tier_end.size(); }
   uint32_t n_pol() const { return (uint32_t)meta.size(); }
   uint32_t n_gstr() const { return (uint32_t)strings.size(); }
+  uint32_t n_hot() const { return (uint32_t)hot.size() / cgi::HOT_WORDS; }
+  uint32_t row_words() const { return (cgi::RW_HDR + 2 * n_hot() + 3) & ~3u; }
   int32_t find(const std::string& s) const {
     auto it = sid.find(s);
     return it == sid.end() ? -1 : (int32_t)it->second;
@@ -76,6 +78,8 @@ struct RequestIn {
 struct Batch {
   std::shared_ptr<const Image> img;
   std::vector<uint32_t> heap, req_base;
+  std::vector<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
+  uint32_t row_words = 0;
   std::vector<std::string> bstrings;
   std::unordered_map<std::string, uint32_t> bsid;
   std::vector<uint32_t> bstr_off;

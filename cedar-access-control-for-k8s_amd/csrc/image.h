@@ -11,6 +11,8 @@
 //   gstr_off[n_gstr + 1]     byte offsets of the global (policy) string table
 //   gstr_bytes[]             string bytes
 // Batch (per submission):
+//   rows[R * row_words]      columnar request row: P/A/R UIDs, ancestor-list offsets and the
+//                            image's hot attribute paths pre-resolved on the host (see RowW)
 //   req_base[R]              word offset of request r's heap block in `heap`
 //   heap[]                   per-request blocks: header, entity table, attribute data
 //   bstr_off[n_bstr + 1], bstr_bytes[]  batch-local strings (ids >= n_gstr)
@@ -82,29 +84,45 @@ enum PolW : uint32_t {
   PW_CODE = 10,   // pol[]: code word offset; stream records: global policy index (code follows)
   PW_CODE_N = 11, // code words
   PW_SLOTS = 12,  // bytecode: max register slot used + 1; atomic: words of atoms (data follows)
-  PW_LANE = 13,   // lane-scratch words needed
+  PW_LANE = 13,   // bytecode: lane-scratch words needed; index heads: PW_EXT (full record offset)
   PW_AMASK0 = 14, // action scope as a mask over the image action table (valid when n_act <= 64)
   PW_AMASK1 = 15,
   POL_WORDS = 16,
 };
+constexpr uint32_t PW_EXT = PW_LANE;
 
-// ---- scope index (indexed evaluation path) ---------------------------------------------------
-// Every atomic policy is filed under the scope key that any request it can apply to must
-// enumerate: the principal / resource / action entity of an ==, in or is-in scope (the request
-// enumerates its ancestor-or-self UIDs), the principal / resource type of an `is` scope, or ALL.
-// An `action in [..]` list files the policy under each listed action (duplicates are removed
-// when results are merged). The kernel re-checks the full scope of every candidate.
-//   btab[4 * slot] = (cat << 28 | et, ei, first, count): open addressing, linear probing,
-//                    power-of-two size, empty slot has word0 == 0
-//   brefs[first .. first + count)  word offsets into bstream, ascending policy index
-//   bstream                        copies of the stream records in bucket order (locality)
+// ---- scope index (probe kernel) ---------------------------------------------------------------
+// Every policy of an all-atomic image is filed under keys that any request it can apply to (or
+// error on) must enumerate:
+//   level 1  (cat, et, ei): the principal / resource / action entity of an ==, in or is-in scope
+//            (the request enumerates its ancestor-or-self UIDs), the principal / resource type of
+//            an `is` scope, or ALL;
+//   level 2  (cat, et, ei, h, value): additionally the constant c of an equality atom hot(h) == c
+//            that every satisfying evaluation passes and that no erroring atom precedes; filed
+//            under value c, and also under MISSING_W0 when an absent h would make that atom
+//            raise (no `has h` guard before it).
+// A request probes level 1 for all its scope keys, then level 2 under each found key for every
+// hot slot in the entry's hmask with its own value of that slot (or MISSING_W0).
+// btab: open addressing, linear probing, power-of-two slots of BT_WORDS:
+//   [cat << 28 | et, ei, h | BT_L2 (level 2) or 0, hmask (level 1) or value w0, value w1,
+//    first, count, 0]; an empty slot has word0 == 0.
+// Records: bstream[first * HEAD_WORDS ...] fixed heads (descriptor + the first 4 atoms) in bucket
+// order; the head's PW_EXT is the absolute bstream offset of the full variable-length record
+// (descriptor, atoms, atom data) in the ext area, which record-relative offsets address.
 enum BucketCat : uint32_t { BK_P = 1, BK_R = 2, BK_A = 3, BK_PT = 4, BK_RT = 5, BK_ALL = 6 };
-constexpr uint32_t BT_WORDS = 4;
+constexpr uint32_t BT_WORDS = 8, BT_L2 = 0x100, HEAD_WORDS = 32, HEAD_ATOMS = 4;
 __host__ __device__ constexpr inline uint32_t bucket_hash(uint32_t cat, uint32_t et, uint32_t ei) {
   uint32_t h = (cat * 0x9E3779B1u) ^ (et * 0x85EBCA77u) ^ (ei * 0xC2B2AE3Du);
   h ^= h >> 16;
   h *= 0x7FEB352Du;
   h ^= h >> 15;
+  return h;
+}
+__host__ __device__ constexpr inline uint32_t bucket_hash2(uint32_t l1, uint32_t hslot, uint32_t v0, uint32_t v1) {
+  uint32_t h = l1 ^ ((hslot + 1) * 0x27D4EB2Fu) ^ (v0 * 0x165667B1u) ^ (v1 * 0xD3A2646Cu);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
   return h;
 }
 
@@ -113,10 +131,15 @@ __host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_
   return ((et * 0x9E3779B1u) ^ (ei * 0x85EBCA77u) ^ ((ei >> 16) * 0xC2B2AE3Du)) >> 25;
 }
 
-// ---- atoms: 4-word predicates over pre-resolved (hot) attributes ----------------------------
-// word0 = kind | h << 8 | flags << 16; word1..3 = operands
+// ---- atoms: 4-word predicates over pre-resolved (hot) attribute paths -----------------------
+// A policy's when/unless clauses lower to a forward-only branch graph of atoms:
+//   word0 = kind | h << 8 | t << 16 | f << 24   (t / f: next atom when true / false, or AT_SAT /
+//   AT_UNSAT); word1..3 = operands. `!` swaps t and f; `&&`, `||`, boolean if-then-else and
+//   clause sequencing (when: true -> next clause, false -> unsatisfied; unless: the reverse) are
+//   edges. Evaluation starts at atom 0; an atom error is the policy's error. Policies without
+//   conditions have no atoms and are satisfied by their scope.
 enum AtomKind : uint32_t {
-  AK_HAS = 1,     // hot h present
+  AK_HAS = 1,     // hot path h present (false if only its final step is missing; error otherwise)
   AK_BOOL,        // hot h (must be bool)
   AK_EQ,          // hot h == const (w1 = tag word, w2 = y, w3 = z, register form; primitives only)
   AK_EQH,         // hot h == hot w1
@@ -128,7 +151,11 @@ enum AtomKind : uint32_t {
   AK_LCMP,        // hot h (must be long) <op w1> const long (w2 lo, w3 hi); op: 0 <, 1 <=, 2 >, 3 >=
   AK_RECSET,      // hot h (must be set).containsAny([record templates]) (w3 = 0) / .contains(template) (w3 = 1);
                   // templates @record+w1 (layout: RecsetLayout), w2 = number of templates
+  AK_TRUE,        // constant true (`true`; `false` is AK_TRUE with t and f swapped)
+  AK_INANY,       // var h in [entity literals]: (type, id) pairs @record+w1, n = w2
+  AK_EQV,         // var h == entity literal (w1 type, w2 id)
 };
+constexpr uint32_t AT_UNSAT = 0xFE, AT_SAT = 0xFF, MAX_ATOMS = 0xFD;
 // AK_RECSET data, all offsets relative to the policy record:
 //   [n_holes, hole hot index ...]                     holes in source (evaluation) order
 //   then per template: [n_keys, (key sid, field kind, a, b, c) x n_keys]   keys ascending by sid
@@ -137,8 +164,32 @@ enum AtomKind : uint32_t {
 //   kind RF_CONST (x,y,z register form) or RF_HOLE (x = hot index)
 enum RecsetField : uint32_t { RF_CONST = 0, RF_HOLE = 1, RF_SETLIT = 2 };
 constexpr uint32_t RS_FIELD_WORDS = 5, RS_ELEM_WORDS = 4;
-enum AtomFlags : uint32_t { AF_START = 1, AF_END = 2, AF_UNLESS = 4, AF_OR = 8, AF_NEG = 16 };
 constexpr uint32_t ATOM_WORDS = 4;
+
+// ---- hot attribute paths ----------------------------------------------------------------------
+// hot[h * HOT_WORDS] = (var, depth, key sid x MAX_PATH): var.k0.k1... (var 0 principal, 1 action,
+// 2 resource, 3 context). The encoder resolves every hot path per request on the host into the
+// request row: the value (memory form, refs relative to the request's heap block), or a status
+// word w0 = (T_NONE tag) | HS_FINAL? | code with w1 = block offset of the error detail
+// [code | aux << 8, k, et, ei] that attribute access would raise. HS_FINAL marks a failure at the
+// path's last step that `has` reports as false (entity absent / attribute absent).
+constexpr uint32_t HOT_WORDS = 6, MAX_PATH = 4;
+constexpr uint32_t HS_FINAL = 0x100;
+// ---- request rows ----------------------------------------------------------------------------
+enum RowW : uint32_t {
+  RW_P = 0,      // principal (type sid, id sid)
+  RW_A = 2,      // action
+  RW_R = 4,      // resource
+  RW_PANC = 6,   // block-relative offset of the principal's ancestor (type, id) pairs
+  RW_RANC = 7,
+  RW_AANC = 8,
+  RW_PN = 9,     // ancestor counts
+  RW_RN = 10,
+  RW_AN = 11,
+  RW_BLK = 12,   // heap word offset of the request block
+  RW_HDR = 16,   // hot slots follow: (w0, w1) per hot path
+};
+constexpr uint32_t MISSING_W0 = 0xFFFFFFFFu;  // level-2 index key of an absent hot value
 
 // ---- bytecode -------------------------------------------------------------------------------
 // word0 = op | d << 8 | a << 14 | b << 20 | c << 26 (6-bit slot fields); word1 = imm
@@ -180,7 +231,7 @@ enum Op : uint32_t {
   OP_COUNT
 };
 constexpr uint32_t CHUNK_WORDS = 4096;  // policy-stream chunk staged in LDS (16 KiB)
-constexpr uint32_t NHOT = 16;  // pre-resolved (var, attribute) pairs per image (kept in LDS)
+constexpr uint32_t NHOT = 32;  // hot attribute paths per image (request-row columns; LDS per wave)
 constexpr uint32_t MAX_ACT = 64;  // image action table size for per-request action masks
 // OP_CALL sub-ops
 enum CallOp : uint32_t {
@@ -218,6 +269,6 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 3;
+constexpr uint32_t IMG_VERSION = 4;
 
 }  // namespace cgi

@@ -68,6 +68,11 @@ int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t*
 int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* n_hot, uint32_t* n_actions,
                    uint32_t* stream_words);
 
+/* 1 when policy i (image order) lowered to predicate atoms, 0 when it runs as bytecode. */
+int cg_image_policy_atomic(const void* image, size_t len, uint32_t i, int* atomic);
+/* 1 when the image is evaluated by the probe kernel over the scope index (all policies atomic). */
+int cg_image_indexed(const void* image, size_t len, int* indexed);
+
 /* ---- device context (one per GPU; requests shard across contexts, images are replicated) ---- */
 int cg_device_count(int* n);
 /* hipDeviceSynchronize on `device` (bench barriers; the library links ROCm's own HIP runtime). */

@@ -152,15 +152,48 @@ class Gen:
             lambda: "resource.sel.containsAny([" + ", ".join(self.sel_tmpl() for _ in range(r.randint(1, 3))) + "])",
             lambda: f"resource.sel.contains({self.sel_tmpl()})",
             lambda: f"!resource.sel.containsAny([{self.sel_tmpl()}])",
+            # nested attribute paths (host-resolved hot paths), incl. through an entity reference
+            lambda: f"principal.info.a {r.choice(['<', '>=', '=='])} {r.randint(-3, 9)}",
+            lambda: f'principal.info.b == {q(r.choice(TAGS))}',
+            lambda: "principal.info has c", lambda: "principal has info && principal.info has c",
+            lambda: f'resource.owner.name == {q(r.choice(USERS))}',
+            lambda: "resource has owner && resource.owner has name",
+            lambda: f'principal.info.c.contains({q(r.choice(TAGS))})',
+            lambda: f"context.x {r.choice(['<', '>'])} {r.randint(0, 40)}",
+            lambda: "context.flag", lambda: "context has s && context.s == principal.name",
+            # entity set membership, is-in, var == literal, constants
+            lambda: "resource in [" + ", ".join(f"k8s::Group::{q(g)}" for g in r.sample(GROUPS, 2)) + "]",
+            lambda: f"principal in [k8s::Group::{q(r.choice(GROUPS))}, k8s::User::{q(r.choice(USERS))}]",
+            lambda: f"principal is k8s::User in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: f'resource == k8s::Resource::{q("r" + str(r.randint(0, 3)))}',
+            lambda: f'principal == k8s::User::{q(r.choice(USERS))}',
+            lambda: r.choice(["true", "false"]),
         ])()
+
+    def atom_tree(self, d=0):
+        r = self.r
+        t = r.random()
+        if d >= 2 or t < 0.45:
+            return self.atom_e()
+        if t < 0.65:
+            return f"({self.atom_tree(d + 1)} && {self.atom_tree(d + 1)})"
+        if t < 0.85:
+            return f"({self.atom_tree(d + 1)} || {self.atom_tree(d + 1)})"
+        if t < 0.93:
+            return f"!({self.atom_tree(d + 1)})"
+        return f"(if {self.atom_tree(d + 1)} then {self.atom_tree(d + 1)} else {self.atom_tree(d + 1)})"
 
     def atomic_policy(self):
         r = self.r
         eff = "forbid" if r.random() < 0.25 else "permit"
         conds = []
-        for _ in range(r.choice([1, 1, 2])):
-            op = " || " if r.random() < 0.3 else " && "
-            conds.append(f"{r.choice(['when', 'when', 'unless'])} {{ " + op.join(self.atom_e() for _ in range(r.randint(1, 4))) + " }")
+        for _ in range(r.choice([0, 1, 1, 2])):
+            if r.random() < 0.5:
+                op = " || " if r.random() < 0.3 else " && "
+                body = op.join(self.atom_e() for _ in range(r.randint(1, 4)))
+            else:
+                body = self.atom_tree()
+            conds.append(f"{r.choice(['when', 'when', 'unless'])} {{ {body} }}")
         return f"{eff} ({self.scope('principal')}, {self.scope('action')}, {self.scope('resource')})\n" + "\n".join(conds) + ";"
 
     def atomic_policies(self, n):

@@ -256,3 +256,98 @@ def test_index_kernel_multi_tier_fallthrough(ctx, seed):
     g = Gen(7000 + seed)
     stores = [cedargpu.MemoryStore(f"t{t}.cedar", g.atomic_policies(g.r.randint(0, 6))) for t in range(3)]
     check_items(ctx, stores, [g.item() for _ in range(400)])
+
+
+# ---------------------------------------------------------------- probe kernel (two-level index)
+def _atomic_only(stores_texts):
+    """Drops the policies that lower to bytecode (so the image is evaluated by the probe kernel)."""
+    import cedar_oracle as _co
+    out = []
+    for name, text in stores_texts:
+        ps = _co.parse_policies(text, name)
+        b = text.encode()
+        offs = [p.offset for p in ps] + [len(b)]
+        parts = [b[offs[i]:offs[i + 1]].decode() for i in range(len(ps))]
+        out.append([name, parts])
+    for _ in range(5):
+        stores = [cedargpu.MemoryStore(n, "\n".join(parts)) for n, parts in out]
+        flags = cedargpu.atomic_policies(cedargpu.build_image(stores))
+        if all(flags):
+            return stores
+        k = 0
+        for s in out:
+            keep = []
+            for part in s[1]:
+                if flags[k]:
+                    keep.append(part)
+                k += 1
+            s[1] = keep
+    raise AssertionError("could not reduce to an all-atomic image")
+
+
+def check_items_ref(ctx, stores, items, want_indexed=None):
+    """GPU vs the C++ oracle (oracle/cedar_ref.cpp) for larger item counts."""
+    from cedar_ref import RefPolicySet, items_json
+    if want_indexed is not None:
+        assert cedargpu.image_stats(cedargpu.build_image(stores))["indexed"] == want_indexed
+    tiers = cedargpu.TieredPolicyStores(stores, ctx=ctx)
+    got = tiers.is_authorized_batch(items)
+    ref = RefPolicySet.from_stores(stores)
+    ref.load_items(items_json(items))
+    want = ref.evaluate(8)
+    ref.close()
+    for k, ((ok, diag), (wok, _, wdiag, _)) in enumerate(zip(got, want)):
+        assert (ok, diag) == (wok, wdiag), (k, items[k][1], diag, wdiag)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_probe_kernel_random_atomic(ctx, seed):
+    """All-atomic random corpora (nested paths, &&/||/!/if trees, in-sets, is-in, var == E,
+    label-selector templates, multi-tier) through the probe kernel vs the oracle."""
+    g = Gen(9000 + seed)
+    texts = [(f"p{t}.cedar", g.atomic_policies(g.r.randint(1, 60))) for t in range(g.r.randint(1, 3))]
+    stores = _atomic_only(texts)
+    items = [g.item() for _ in range(500)]
+    check_items_ref(ctx, stores, items, want_indexed=True)
+
+
+def test_probe_kernel_abac_synth(ctx):
+    """C3-shaped policies (group scopes, namespace / resource attribute keys, like, selectors)."""
+    pop = synth.Population(seed=5, n_users=2000, n_groups=60)
+    stores = [cedargpu.MemoryStore("c3.cedar", synth.abac_policies(1500, seed=5, pop=pop))]
+    sars = synth.random_sars(3000, seed=6, pop=pop)
+    items = []
+    for s in sars:
+        a = km.attributes_from_sar(s)
+        em, r = km.record_to_cedar_resource(a)
+        items.append((co.entities_to_json(em), co.request_to_json(r)))
+    check_items_ref(ctx, stores, items, want_indexed=True)
+
+
+def test_probe_kernel_rbac_synth(ctx):
+    """C2-shaped policies (RBAC converter output: principal.name / namespace attribute keys)."""
+    pop = synth.Population(seed=8, n_users=400, n_groups=40)
+    stores = [cedargpu.MemoryStore("c2.cedar", synth.rbac_policies(800, seed=8, pop=pop)),
+              cedargpu.MemoryStore("demo.cedar", "\n".join(v for k, v in sorted(CORPUS["demo"].items())
+                                                           if k.startswith("authorization")))]
+    sars = synth.random_sars(3000, seed=9, pop=pop)
+    items = []
+    for s in sars:
+        a = km.attributes_from_sar(s)
+        em, r = km.record_to_cedar_resource(a)
+        items.append((co.entities_to_json(em), co.request_to_json(r)))
+    check_items_ref(ctx, stores, items, want_indexed=True)
+
+
+def test_probe_kernel_missing_attribute_errors(ctx):
+    """Unguarded attribute-keyed equality: requests without the attribute must report the error
+    (level-2 MISSING bucket); guarded ones must not."""
+    text = ('permit (principal, action, resource) when { resource.name == "a" };\n'
+            'permit (principal, action, resource) when { resource has name && resource.name == "b" };\n'
+            'forbid (principal in k8s::Group::"g1", action, resource) when { resource.namespace == "ns1" };\n'
+            'permit (principal, action == k8s::Action::"get", resource) when { principal.info.b == "t1" };\n')
+    stores = [cedargpu.MemoryStore("m.cedar", text)]
+    g = Gen(31337)
+    items = [g.item() for _ in range(400)]
+    check_items_ref(ctx, stores, items, want_indexed=True)
+    check_items(ctx, stores, items[:100])
