@@ -437,26 +437,40 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       cape = std::max(cape, b->host.res[2 * (size_t)i + 1] >> 16);
     }
   }
-  if (!idx.empty()) {
-    capr = std::max(capr, 1u);
-    cape = std::max(cape, 1u);
+  // re-runs on the stream kernel are exact; a re-run that still overflows its capacities reports
+  // the exact counts, so a second pass with those capacities completes it
+  for (int pass = 0; pass < 3 && !idx.empty(); pass++) {
+    capr = std::max(std::min(capr, 4096u), 8u);
+    cape = std::max(std::min(cape, 4096u), 4u);
     std::vector<uint32_t> res, rf, rp, er;
     if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, b->ctx->stream, res, rf, rp, er)) {
       b->err = dev_last_error();
       return CG_E_DEVICE;
     }
+    std::vector<uint32_t> again;
+    uint32_t capr2 = 0, cape2 = 0;
     for (size_t k = 0; k < idx.size(); k++) {
       uint32_t i = idx[k];
       uint32_t fl = res[2 * k] >> 16;
       uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
+      if (fl & cgi::RF_OVERFLOW) {
+        again.push_back(i);
+        capr2 = std::max(capr2, nr);
+        cape2 = std::max(cape2, ne);
+        continue;
+      }
       const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
-      // the re-run is authoritative for the whole result (the index kernel does not decide a
-      // request whose hits overflowed its staging area)
-      b->host.res[2 * (size_t)i] = res[2 * k] & ~((uint32_t)cgi::RF_OVERFLOW << 16);
+      // the re-run is authoritative for the whole result (the probe kernel does not decide a
+      // request whose hits overflowed its staging area or that needs structural equality)
+      b->host.res[2 * (size_t)i] = res[2 * k];
       b->host.res[2 * (size_t)i + 1] = res[2 * k + 1];
       b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
       b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
     }
+    idx.swap(again);
+    capr = capr2;
+    cape = cape2;
+    if (pass == 2 && !idx.empty()) { b->err = "result lists exceed the device re-run capacity"; return CG_E_RANGE; }
   }
   b->done = true;
   return CG_OK;

@@ -63,7 +63,7 @@ struct KArgs {
   const uint32_t* __restrict__ brefs;
   const uint32_t* __restrict__ bstream;
   const uint32_t* __restrict__ rows;     // columnar request rows (row_words each)
-  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, row_words;
+  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, row_words, combo_mask;
 };
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
@@ -112,7 +112,8 @@ __device__ __forceinline__ uint32_t rd3(const uint32_t* blk, const uint32_t* cpo
   if (sp == SP_CPOOL) return cpool[off];
   return lh[off];
 }
-__device__ __forceinline__ uint32_t rd(const Ctx& c, uint32_t ref, uint32_t i) { return rd3(c.blk, c.cpool, c.lh, ref, i); }
+template <class CT>
+__device__ __forceinline__ uint32_t rd(const CT& c, uint32_t ref, uint32_t i) { return rd3(c.blk, c.cpool, c.lh, ref, i); }
 
 __device__ __forceinline__ RV load_val3(const uint32_t* blk, const uint32_t* cpool, const uint32_t* lh, uint32_t w0,
                                         uint32_t w1) {
@@ -124,7 +125,8 @@ __device__ __forceinline__ RV load_val3(const uint32_t* blk, const uint32_t* cpo
   }
   return RV{w0, w1, 0};
 }
-__device__ __forceinline__ RV load_val(const Ctx& c, uint32_t w0, uint32_t w1) { return load_val3(c.blk, c.cpool, c.lh, w0, w1); }
+template <class CT>
+__device__ __forceinline__ RV load_val(const CT& c, uint32_t w0, uint32_t w1) { return load_val3(c.blk, c.cpool, c.lh, w0, w1); }
 
 __device__ __forceinline__ uint32_t tname(const RV& v) {
   switch (tag_of(v)) {
@@ -239,10 +241,13 @@ __device__ __noinline__ uint32_t veq_struct(const uint32_t* blk, const uint32_t*
   return ret ? 1u : 0u;
 }
 
-// full equality; `deep` set when nesting exceeds the device limit
-__device__ __forceinline__ bool veq(const Ctx& c, const RV& a, const RV& b, bool& deep) {
+// full equality; `deep` set when nesting exceeds the device limit, or (STRUCT = false, the probe
+// kernel) whenever a set/record comparison is needed: the request then re-runs on the stream kernel
+template <bool STRUCT = true, class CT>
+__device__ __forceinline__ bool veq(const CT& c, const RV& a, const RV& b, bool& deep) {
   const uint32_t s = veq_shallow(c.blk, c.cpool, c.lh, a, b);
   if (s != 2u) return s == 1u;
+  if (!STRUCT) { deep = true; return false; }
   const uint32_t r = veq_struct(c.blk, c.cpool, c.lh, a, b);
   if (r == 2u) deep = true;
   return r == 1u;
@@ -362,7 +367,8 @@ __device__ __forceinline__ bool r_in(const Ctx& c, uint32_t et, uint32_t ei, uin
 }
 
 // ---- strings / like -------------------------------------------------------------------------
-__device__ __forceinline__ void str_span(const Ctx& c, uint32_t sid, const uint8_t*& p, uint32_t& len) {
+template <class CT>
+__device__ __forceinline__ void str_span(const CT& c, uint32_t sid, const uint8_t*& p, uint32_t& len) {
   if (sid < c.n_gstr) {
     const uint32_t o = c.gstr_off[sid];
     len = c.gstr_off[sid + 1] - o;
@@ -391,8 +397,8 @@ __device__ __forceinline__ bool lit_at(const uint8_t* s, uint32_t pos, const uin
 }
 
 // `pw` points at a compiled pattern (LDS record data or global constant pool)
-template <class P>
-__device__ __forceinline__ bool like_match(const Ctx& c, uint32_t sid, P pw) {
+template <class CT, class P>
+__device__ __forceinline__ bool like_match(const CT& c, uint32_t sid, P pw) {
   const uint8_t* s;
   uint32_t slen;
   str_span(c, sid, s, slen);
@@ -460,12 +466,14 @@ __device__ __forceinline__ RV mk_bool(bool b) { return RV{mk_w0(T_BOOL, 0), b ? 
 
 // Hot slot h of this lane: the value (memory form) or a status word (tag NONE; x = error code |
 // HS_FINAL; y = block offset of the error detail the encoder resolved, image.h "hot paths").
-__device__ __forceinline__ uint2 hot_get(const Ctx& c, uint32_t h) { return c.hotl[h * c.hstride]; }
+template <class CT>
+__device__ __forceinline__ uint2 hot_get(const CT& c, uint32_t h) { return c.hotl[h * c.hstride]; }
 __device__ __forceinline__ bool hot_ok(uint2 v) { return (v.x >> TAG_SHIFT) != T_NONE; }
 // `has` on a hot path: present -> 1, absent at the final step -> 0, failing earlier -> 2 (error)
 __device__ __forceinline__ uint32_t hot_has(uint2 v) { return hot_ok(v) ? 1u : ((v.x & HS_FINAL) ? 0u : 2u); }
 // The error attribute access raises for a non-present hot slot.
-__device__ __forceinline__ void hot_err(const Ctx& c, uint32_t h, uint2 v, Err& e) {
+template <class CT>
+__device__ __forceinline__ void hot_err(const CT& c, uint32_t h, uint2 v, Err& e) {
   const uint32_t* d = c.blk + v.y;
   const uint32_t w = d[0];
   e.code = w & 0xFF;
@@ -478,34 +486,37 @@ __device__ __forceinline__ void hot_err(const Ctx& c, uint32_t h, uint2 v, Err& 
 // ---- atoms ---------------------------------------------------------------------------------
 // rec = this policy's LDS record (atom data lives there). Returns 0 false, 1 true, 2 error.
 // AK_RECSET helpers: compare a request value with one template operand (const or hot hole).
-__device__ __forceinline__ bool rs_opnd_eq(const Ctx& c, const RV& x, uint32_t kind, uint32_t a, uint32_t b, uint32_t d,
+template <bool STRUCT, class CT>
+__device__ __forceinline__ bool rs_opnd_eq(const CT& c, const RV& x, uint32_t kind, uint32_t a, uint32_t b, uint32_t d,
                                            bool& deep) {
   if (kind == RF_CONST) return prim_eq(x, a, b, d);
   const uint2 hv = hot_get(c, a);  // holes were checked present before matching
-  return veq(c, x, load_val(c, hv.x, hv.y), deep);
+  return veq<STRUCT>(c, x, load_val(c, hv.x, hv.y), deep);
 }
 // set-literal field: x (must be a set) equals the literal list by mutual inclusion
-__device__ __forceinline__ bool rs_set_eq(const Ctx& c, const RV& x, const uint32_t* el, uint32_t n, bool& deep) {
+template <bool STRUCT, class CT>
+__device__ __forceinline__ bool rs_set_eq(const CT& c, const RV& x, const uint32_t* el, uint32_t n, bool& deep) {
   if (tag_of(x) != T_SET) return false;
   const uint32_t ref = x.w0 & X_MASK, m = x.w1;
   for (uint32_t i = 0; i < m; i++) {
     const RV xi = load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i));
     bool f = false;
-    for (uint32_t j = 0; j < n && !f; j++) f = rs_opnd_eq(c, xi, el[4 * j], el[4 * j + 1], el[4 * j + 2], el[4 * j + 3], deep);
+    for (uint32_t j = 0; j < n && !f; j++) f = rs_opnd_eq<STRUCT>(c, xi, el[4 * j], el[4 * j + 1], el[4 * j + 2], el[4 * j + 3], deep);
     if (!f) return false;
   }
   for (uint32_t j = 0; j < n; j++) {
     bool f = false;
     for (uint32_t i = 0; i < m && !f; i++) {
       const RV xi = load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i));
-      f = rs_opnd_eq(c, xi, el[4 * j], el[4 * j + 1], el[4 * j + 2], el[4 * j + 3], deep);
+      f = rs_opnd_eq<STRUCT>(c, xi, el[4 * j], el[4 * j + 1], el[4 * j + 2], el[4 * j + 3], deep);
     }
     if (!f) return false;
   }
   return true;
 }
 // record x == template t (sorted keys, exact key set)
-__device__ __forceinline__ bool rs_rec_eq(const Ctx& c, const uint32_t* rec, const RV& x, const uint32_t* t, bool& deep) {
+template <bool STRUCT, class CT>
+__device__ __forceinline__ bool rs_rec_eq(const CT& c, const uint32_t* rec, const RV& x, const uint32_t* t, bool& deep) {
   const uint32_t nk = t[0];
   if (tag_of(x) != T_REC || x.w1 != nk) return false;
   const uint32_t ref = x.w0 & X_MASK;
@@ -513,8 +524,8 @@ __device__ __forceinline__ bool rs_rec_eq(const Ctx& c, const uint32_t* rec, con
     const uint32_t* f = t + 1 + RS_FIELD_WORDS * k;
     if (rd(c, ref, 1 + 3 * k) != f[0]) return false;
     const RV xf = load_val(c, rd(c, ref, 2 + 3 * k), rd(c, ref, 3 + 3 * k));
-    const bool q = f[1] == RF_SETLIT ? rs_set_eq(c, xf, rec + f[2], f[3], deep)
-                                     : rs_opnd_eq(c, xf, f[1], f[2], f[3], f[4], deep);
+    const bool q = f[1] == RF_SETLIT ? rs_set_eq<STRUCT>(c, xf, rec + f[2], f[3], deep)
+                                     : rs_opnd_eq<STRUCT>(c, xf, f[1], f[2], f[3], f[4], deep);
     if (!q) return false;
   }
   return true;
@@ -528,7 +539,8 @@ __device__ __forceinline__ bool var_in(const Ctx& c, uint32_t h, uint32_t qt, ui
   return (c.at == qt && c.ai == qi) || anc_has(c, c.aidx, qt, qi);
 }
 
-__device__ __forceinline__ uint32_t eval_atom(const Ctx& c, const uint32_t* rec, uint32_t kind, uint32_t h, uint32_t w1,
+template <bool STRUCT, class CT>
+__device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, uint32_t kind, uint32_t h, uint32_t w1,
                                               uint32_t w2, uint32_t w3, Err& e) {
   if (kind == AK_IS) {
     return pick3(h, c.pt, c.at, c.rt) == w1 ? 1u : 0u;
@@ -561,8 +573,8 @@ __device__ __forceinline__ uint32_t eval_atom(const Ctx& c, const uint32_t* rec,
       const uint2 hv2 = hot_get(c, w1);
       if (!hot_ok(hv2)) { hot_err(c, w1, hv2, e); return 2u; }
       bool deep = false;
-      const bool q = veq(c, v, load_val(c, hv2.x, hv2.y), deep);
-      if (deep) { e.code = E_DEPTH; return 2u; }
+      const bool q = veq<STRUCT>(c, v, load_val(c, hv2.x, hv2.y), deep);
+      if (deep) { if (!STRUCT) return 3u; e.code = E_DEPTH; return 2u; }
       return q ? 1u : 0u;
     }
     case AK_INSET: {
@@ -598,11 +610,11 @@ __device__ __forceinline__ uint32_t eval_atom(const Ctx& c, const uint32_t* rec,
         if (tag_of(x) != T_REC) continue;
         const uint32_t* t = d + 1 + nh;
         for (uint32_t j = 0; j < w2 && !f; j++) {
-          f = rs_rec_eq(c, rec, x, t, deep);
+          f = rs_rec_eq<STRUCT>(c, rec, x, t, deep);
           t += 1 + RS_FIELD_WORDS * t[0];
         }
       }
-      if (deep) { e.code = E_DEPTH; return 2u; }
+      if (deep) { if (!STRUCT) return 3u; e.code = E_DEPTH; return 2u; }
       return f ? 1u : 0u;
     }
     case AK_LCMP: {
@@ -1081,7 +1093,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
             const uint4 at = *reinterpret_cast<const uint4*>(rec + POL_WORDS + ATOM_WORDS * i);
             const uint32_t w0 = uni(at.x), w1 = uni(at.y), w2 = uni(at.z), w3 = uni(at.w);
             if (pc == i) {
-              const uint32_t rr = eval_atom(c, rec, w0 & 0xFF, (w0 >> 8) & 0xFF, w1, w2, w3, e);
+              const uint32_t rr = eval_atom<true>(c, rec, w0 & 0xFF, (w0 >> 8) & 0xFF, w1, w2, w3, e);
               if (rr == 2u) { err = true; pc = AT_UNSAT; }
               else pc = rr ? ((w0 >> 16) & 0xFF) : (w0 >> 24);
             }
@@ -1137,13 +1149,16 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
 // One wave evaluates one request (image.h "scope index"):
 //   1. the request row (UIDs, ancestor-list offsets, hot paths pre-resolved by the encoder) is
 //      read with wave-uniform loads; lanes copy the hot values into LDS;
-//   2. lane k probes the level-1 table for scope key k (principal / resource / action
-//      ancestor-or-self UIDs, principal / resource types, ALL), then level 2 under each found key
-//      for the hot slots in its hmask, with the request's own value of that slot;
+//   2. lane k probes the level-1 table for (principal, action, resource) key k: for every key
+//      combo the image uses, the product of the request's candidate components (ancestor-or-self
+//      UIDs, type, wildcard); then level 2 under each found key for the hot slots in its hmask,
+//      with the request's own value of that slot;
 //   3. the found buckets' candidate heads (descriptor + first atoms, 128 B, in bucket order) run
-//      one per lane: scope re-check, then the lane's atom graph;
+//      one per lane: cheap scope re-check, then the lane's atom graph;
 //   4. satisfied / erroring candidates are collected in LDS and merged into policy order with the
 //      deciding tier, duplicates removed, as the stream kernel writes them.
+// Structural (set / record) equality is left to the stream kernel: such a request is flagged
+// RF_OVERFLOW and the host re-runs it there (rare: templates compare primitives).
 constexpr uint32_t WAVES = BLOCK / 64;
 constexpr uint32_t HCAP = 64;   // hits per request staged in LDS; more -> overflow re-run
 constexpr uint32_t ECAP = 128;  // found buckets staged before their candidates run
@@ -1169,9 +1184,8 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
 
 struct WaveLds {
   uint32_t efirst[ECAP];     // found bucket: first head index
-  uint32_t epre[ECAP + 1];   // exclusive prefix of candidate counts
-  uint32_t ekey[ECAP];       // bucket category (BK_P / BK_R keys fully re-checked otherwise) | et
-  uint32_t ekei[ECAP];       //   and entity id of its level-1 key
+  uint32_t epre[ECAP + 1];   // candidate counts, then their exclusive prefix
+  uint32_t ecombo[ECAP];     // key combo of the bucket's level-1 key
   uint32_t hp[HCAP];         // hit: global policy index
   uint32_t hm[HCAP];         // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8
   uint32_t hel[HCAP];        // hit is in the deciding tier and not a duplicate
@@ -1179,24 +1193,54 @@ struct WaveLds {
   uint2 hot[NHOT];
 };
 
-// exact `in` for principal / resource against the request's ancestor-or-self list (uniform loop)
+// Slim per-request context of the probe kernel (everything wave-uniform but the pointers' data).
+struct PCtx {
+  const uint32_t* blk;
+  const uint32_t* cpool;
+  uint32_t* lh;
+  const uint32_t* gstr_off;
+  const uint8_t* gstr_bytes;
+  const uint32_t* bstr_off;
+  const uint8_t* bstr_bytes;
+  uint32_t n_gstr;
+  uint2* hotl;
+  static constexpr uint32_t hstride = 1;
+  uint32_t pt, pi, at, ai, rt, ri;
+  uint32_t p_anc, p_nanc, r_anc, r_nanc, a_anc, a_nanc;
+};
+
+// X in (qt, qi) for X with UID (st, si) and ancestor pairs at blk[off + 2k]
 __device__ __forceinline__ bool anc_in(const uint32_t* blk, uint32_t off, uint32_t n, uint32_t st, uint32_t si,
                                        uint32_t qt, uint32_t qi) {
-  bool f = st == qt && si == qi;
-  for (uint32_t k = 0; k < n; k++) f = f || (uni(blk[off + 2 * k]) == qt && uni(blk[off + 2 * k + 1]) == qi);
-  return f;
+  return (st == qt && si == qi) || anc_scan(blk, off, n, qt, qi);
+}
+__device__ __forceinline__ bool var_in(const PCtx& c, uint32_t h, uint32_t qt, uint32_t qi, uint32_t) {
+  if (h == 0) return anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, qt, qi);
+  if (h == 2) return anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, qt, qi);
+  return anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, qt, qi);
 }
 
-// level-1 / level-2 probe: returns (first, count, hmask) of the matching slot, count 0 if absent
-__device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uint32_t hash, uint32_t w0, uint32_t w1,
-                                       uint32_t w2, uint32_t v0, uint32_t v1) {
+// One (principal, action, resource) component: kind KC_*, list index j of the request's
+// ancestor-or-self list (j = 0: the UID itself)
+__device__ __forceinline__ uint2 key_comp(uint32_t kc, uint32_t j, uint32_t st, uint32_t si, const uint32_t* blk,
+                                          uint32_t off) {
+  if (kc == KC_WILD) return make_uint2(KW_ANY, KW_ANY);
+  if (kc == KC_TYPE) return make_uint2(st, KW_ANY);
+  return j ? make_uint2(blk[off + 2 * (j - 1)], blk[off + 2 * (j - 1) + 1]) : make_uint2(st, si);
+}
+
+// probe: (first, count, hmask) of the slot matching key words w0..w6 (+ v0, v1 for level 2)
+__device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uint32_t hash, uint32_t w0, uint2 p, uint2 q,
+                                       uint2 r, uint32_t v0, uint32_t v1) {
   uint32_t h = hash & bmask;
   for (;;) {
-    const uint4 x = *reinterpret_cast<const uint4*>(btab + (size_t)h * BT_WORDS);
+    const uint4* sl = reinterpret_cast<const uint4*>(btab + (size_t)h * BT_WORDS);
+    const uint4 x = sl[0];
     if (x.x == 0) return make_uint3(0, 0, 0);
-    if (x.x == w0 && x.y == w1 && x.z == w2) {
-      const uint4 y = *reinterpret_cast<const uint4*>(btab + (size_t)h * BT_WORDS + 4);
-      if (!(w2 & BT_L2) || (x.w == v0 && y.x == v1)) return make_uint3(y.y, y.z, x.w);
+    if (x.x == w0 && x.y == p.x && x.z == p.y && x.w == q.x) {
+      const uint4 y = sl[1], z = sl[2];
+      if (y.x == q.y && y.y == r.x && y.z == r.y && (!(w0 & BT_L2) || (y.w == v0 && z.x == v1)))
+        return make_uint3(z.y, z.z, z.w);
     }
     h = (h + 1) & bmask;
   }
@@ -1211,35 +1255,22 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   const uint32_t r = a.req_idx ? uni(a.req_idx[gid]) : gid;
   const uint32_t* row = a.rows + (size_t)r * a.row_words;
 
-  Ctx c;
+  PCtx c;
   c.blk = a.heap + uni(row[RW_BLK]);
   c.cpool = a.cpool;
   c.lh = wl.he;  // atoms never address lane scratch (any valid pointer)
-  c.hot = a.hot;
   c.gstr_off = a.gstr_off;
   c.gstr_bytes = a.gstr_bytes;
   c.bstr_off = a.bstr_off;
   c.bstr_bytes = a.bstr_bytes;
   c.n_gstr = a.n_gstr;
   c.hotl = wl.hot;
-  c.hstride = 1;
-  c.nent = 0;
   c.pt = uni(row[RW_P]); c.pi = uni(row[RW_P + 1]);
   c.at = uni(row[RW_A]); c.ai = uni(row[RW_A + 1]);
   c.rt = uni(row[RW_R]); c.ri = uni(row[RW_R + 1]);
   c.p_anc = uni(row[RW_PANC]); c.p_nanc = uni(row[RW_PN]);
   c.r_anc = uni(row[RW_RANC]); c.r_nanc = uni(row[RW_RN]);
-  const uint32_t a_anc = uni(row[RW_AANC]), a_nanc = uni(row[RW_AN]);
-  c.a_anc = a_anc; c.a_nanc = a_nanc;
-  c.pidx = c.aidx = c.ridx = NO_ENT;
-  // `in` atoms (p_in / r_in): exact scans, first 8 principal ancestors in registers, Bloom off
-  c.pb0 = c.pb1 = c.pb2 = c.pb3 = 0xFFFFFFFFu;
-  c.rb0 = c.rb1 = c.rb2 = c.rb3 = 0xFFFFFFFFu;
-#define CG_ANC(k) \
-  c.t##k = k < c.p_nanc ? uni(c.blk[c.p_anc + 2 * k]) : 0xFFFFFFFFu; \
-  c.i##k = k < c.p_nanc ? uni(c.blk[c.p_anc + 2 * k + 1]) : 0xFFFFFFFFu;
-  CG_ANC(0) CG_ANC(1) CG_ANC(2) CG_ANC(3) CG_ANC(4) CG_ANC(5) CG_ANC(6) CG_ANC(7)
-#undef CG_ANC
+  c.a_anc = uni(row[RW_AANC]); c.a_nanc = uni(row[RW_AN]);
   if (lane < a.n_hot) wl.hot[lane] = make_uint2(row[RW_HDR + 2 * lane], row[RW_HDR + 2 * lane + 1]);
   // action masks over the image action table: lane k tests action k (`==` and `in`)
   uint32_t am0 = 0, am1 = 0, as0 = 0, as1 = 0;
@@ -1247,7 +1278,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
     const bool on = lane < a.n_act;
     const uint32_t qt = on ? a.act[2 * lane] : 0u, qi = on ? a.act[2 * lane + 1] : 0u;
     const bool self = on && c.at == qt && c.ai == qi;
-    const bool hit = self || (on && a_nanc && anc_scan(c.blk, a_anc, a_nanc, qt, qi));
+    const bool hit = self || (on && c.a_nanc && anc_scan(c.blk, c.a_anc, c.a_nanc, qt, qi));
     const uint64_t m = __ballot(hit), ms = __ballot(self);
     am0 = (uint32_t)m; am1 = (uint32_t)(m >> 32);
     as0 = (uint32_t)ms; as1 = (uint32_t)(ms >> 32);
@@ -1257,176 +1288,175 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   uint32_t min_tier = a.n_tiers - 1;  // lowest tier with a hit so far (uniform)
   uint32_t nh = 0;                    // hits recorded (uniform; may exceed HCAP)
   uint32_t ne = 0;                    // found buckets staged (uniform)
+  bool general = false;               // needs the stream kernel (structural equality)
 
-  // runs the candidates of the staged buckets, then clears the stage
-  auto run_stage = [&]() {
-    // exclusive prefix of counts over the staged buckets (<= ECAP, two halves)
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < ne; b0 += 64) {
-      const uint32_t b = b0 + lane;
-      const uint32_t cnt = b < ne ? wl.epre[b] : 0u;  // epre holds counts until scanned
-      const uint32_t inc = wave_scan(cnt, lane);
-      wave_lds_sync();
-      if (b < ne) wl.epre[b] = carry + inc - cnt;
-      carry += __shfl(inc, 63);
+  // One loop, so that the candidate stage below is emitted once: each iteration stages the
+  // buckets found by one level-1 chunk (lane k probes key k) or one level-2 round (lane k probes
+  // the next hot slot of its level-1 entry's hmask), and runs the stage when it is nearly full or
+  // when the keys are exhausted.
+  const uint32_t cm = a.combo_mask;
+  const uint32_t nP = 1 + c.p_nanc, nA = 1 + c.a_nanc, nR = 1 + c.r_nanc;
+  uint32_t n_keys = 0;
+  for (uint32_t m = cm; m; m &= m - 1) {
+    const uint32_t cb = __builtin_ctz(m);
+    n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+  }
+  uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0;
+  uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
+  for (;;) {
+    const bool l2 = __ballot(hm != 0) != 0;
+    const bool done = !l2 && kb >= n_keys;
+    if (!done) {
+      uint3 e = make_uint3(0, 0, 0);
+      if (l2) {
+        if (hm) {
+          const uint32_t h = __builtin_ctz(hm);
+          hm &= hm - 1;
+          const uint2 v = wl.hot[h];
+          const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
+          e = probe(a.btab, a.bmask, bucket_hash2(h1, h, v0, v1), w0 | BT_L2 | h, kp, ka, kr, v0, v1);
+        }
+      } else {
+        const uint32_t k = kb + lane;
+        kb += 64;
+        uint32_t j = k;
+        bool found = false;
+        for (uint32_t m = cm; m; m &= m - 1) {
+          const uint32_t cb = __builtin_ctz(m);
+          const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+          if (!found) {
+            if (j < cnt) { combo = cb; found = true; }
+            else j -= cnt;
+          }
+        }
+        if (k < n_keys) {
+          const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
+          const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
+          const uint32_t ip = j % np_, t2 = j / np_, ia = t2 % na_, ir = t2 / na_;
+          kp = key_comp(pkc, ip, c.pt, c.pi, c.blk, c.p_anc);
+          ka = key_comp(akc, ia, c.at, c.ai, c.blk, c.a_anc);
+          kr = key_comp(rkc, ir, c.rt, c.ri, c.blk, c.r_anc);
+          w0 = BT_USED | (combo << 16);
+          h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
+          e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0);
+          hm = e.z;
+        }
+      }
+      // stage this lane's found bucket
+      const uint64_t m = __ballot(e.y != 0);
+      if (e.y) {
+        const uint32_t pos = ne + mbcnt64(m);
+        wl.efirst[pos] = e.x;
+        wl.epre[pos] = e.y;
+        wl.ecombo[pos] = combo;
+      }
+      ne += popc64(m);
       wave_lds_sync();
     }
-    if (lane == 0) wl.epre[ne] = carry;
-    wave_lds_sync();
-    const uint32_t total = uni(carry);
-    for (uint32_t base = 0; base < total; base += 64) {
-      const uint32_t idx = base + lane;
-      bool ok = idx < total;
-      // bucket of candidate idx: last b with epre[b] <= idx
-      uint32_t lo = 0, hi = ne;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (wl.epre[mid] <= idx) lo = mid;
-        else hi = mid;
-      }
-      const uint32_t b = lo;
-      const uint32_t hidx = ok ? wl.efirst[b] + (idx - wl.epre[b]) : 0u;
-      const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
-      const uint4* d4 = reinterpret_cast<const uint4*>(head);
-      const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
-      const uint32_t flags = q0.x, kinds = q0.y;
-      const uint32_t tier = (flags >> 8) & 0xFF;
-      ok = ok && tier <= min_tier;
-      const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
-      const uint32_t kcat = wl.ekey[b] >> 28, ket = wl.ekey[b] & X_MASK, kei = wl.ekei[b];
-      // action scope
-      if (ak != SK_ANY) {
-        if (a.amask_ok) {
-          ok = ok && (ak == SK_EQ ? (((as0 & q3.z) | (as1 & q3.w)) != 0) : (((am0 & q3.z) | (am1 & q3.w)) != 0));
-        } else if (ak == SK_EQ) {
-          ok = ok && c.at == q1.y && c.ai == q1.z;
-        } else if (ak == SK_IN) {
-          ok = ok && ((c.at == q1.y && c.ai == q1.z) || anc_scan(c.blk, a_anc, a_nanc, q1.y, q1.z));
-        } else {
-          bool any = false;
-          for (uint32_t x = 0; ok && x < q1.y && !any; x++) {
-            const uint32_t qt = a.cpool[q1.z + 2 * x], qi = a.cpool[q1.z + 2 * x + 1];
-            any = (c.at == qt && c.ai == qi) || anc_scan(c.blk, a_anc, a_nanc, qt, qi);
+    if (done || ne + 64 > ECAP) {
+      // ---- run the staged buckets' candidates ----
+        uint32_t carry = 0;
+        for (uint32_t b0 = 0; b0 < ne; b0 += 64) {
+          const uint32_t b = b0 + lane;
+          const uint32_t cnt = b < ne ? wl.epre[b] : 0u;
+          const uint32_t inc = wave_scan(cnt, lane);
+          wave_lds_sync();
+          if (b < ne) wl.epre[b] = carry + inc - cnt;
+          carry += __shfl(inc, 63);
+          wave_lds_sync();
+        }
+        const uint32_t total = uni(carry);
+        for (uint32_t base = 0; base < total; base += 64) {
+          const uint32_t idx = base + lane;
+          bool ok = idx < total;
+          uint32_t lo = 0, hi = ne;  // bucket of candidate idx: last b with epre[b] <= idx
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (wl.epre[mid] <= idx) lo = mid;
+            else hi = mid;
           }
-          ok = ok && any;
-        }
-      }
-      // principal scope: an `in` / `is in` scope whose entity is the bucket's BK_P key holds
-      // already (the request enumerated that key from its ancestor-or-self list)
-      if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
-      if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
-      else if ((pk == SK_IN || pk == SK_ISIN) && !(kcat == BK_P && ket == q0.w && kei == q1.x))
-        ok = ok && anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, q0.w, q1.x);
-      if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
-      if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
-      else if ((rk == SK_IN || rk == SK_ISIN) && !(kcat == BK_R && ket == q2.x && kei == q2.y))
-        ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
-      // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
-      // atom data in the policy's full record at PW_EXT)
-      const uint32_t na = q3.x / ATOM_WORDS;
-      const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (q3.y = word 13)
-      uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
-      bool err = false;
-      Err e{0, 0, 0, 0, 0};
-      while (__ballot(pc < na)) {
-        if (pc < na) {
-          const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
-          const uint32_t rr = eval_atom(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
-          if (rr == 2u) { err = true; pc = AT_UNSAT; }
-          else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
-        }
-      }
-      // record hits
-      const bool hit = ok && (err || pc == AT_SAT);
-      const uint64_t hmask = __ballot(hit);
-      if (hmask) {
-        if (hit) {
-          const uint32_t pos = nh + mbcnt64(hmask);
-          if (pos < HCAP) {
-            wl.hp[pos] = q2.z;  // PW_CODE: global policy index
-            wl.hm[pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8);
-            if (err) {
-              wl.he[4 * pos] = e.code | (e.aux << 8);
-              wl.he[4 * pos + 1] = e.k;
-              wl.he[4 * pos + 2] = e.et;
-              wl.he[4 * pos + 3] = e.ei;
+          const uint32_t hidx = ok ? wl.efirst[lo] + (idx - wl.epre[lo]) : 0u;
+          const uint32_t combo = wl.ecombo[lo];
+          const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
+          const uint4* d4 = reinterpret_cast<const uint4*>(head);
+          const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+          const uint32_t flags = q0.x, kinds = q0.y;
+          const uint32_t tier = (flags >> 8) & 0xFF;
+          ok = ok && tier <= min_tier;
+          const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
+          // scope re-check; an `in` / `is in` entity matched by the bucket key's entity component
+          // holds already (the request enumerated that key from its ancestor-or-self list)
+          if (ak != SK_ANY) {
+            if (a.amask_ok) {
+              ok = ok && (ak == SK_EQ ? (((as0 & q3.z) | (as1 & q3.w)) != 0) : (((am0 & q3.z) | (am1 & q3.w)) != 0));
+            } else if (ak == SK_EQ) {
+              ok = ok && c.at == q1.y && c.ai == q1.z;
+            } else if (ak == SK_IN) {
+              ok = ok && anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, q1.y, q1.z);
+            } else if (((combo >> 2) & 1) != KC_ENT) {
+              bool any = false;
+              for (uint32_t x = 0; ok && x < q1.y && !any; x++)
+                any = anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, a.cpool[q1.z + 2 * x], a.cpool[q1.z + 2 * x + 1]);
+              ok = ok && any;
             }
           }
+          if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
+          if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
+          else if ((pk == SK_IN || pk == SK_ISIN) && (combo & 3) != KC_ENT)
+            ok = ok && anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, q0.w, q1.x);
+          if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
+          if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
+          else if ((rk == SK_IN || rk == SK_ISIN) && (combo >> 3) != KC_ENT)
+            ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
+          // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
+          // atom data in the policy's full record at PW_EXT)
+          const uint32_t na = q3.x / ATOM_WORDS;
+          const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
+          uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
+          bool err = false;
+          Err e{0, 0, 0, 0, 0};
+          while (__ballot(pc < na)) {
+            if (pc < na) {
+              const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
+              const uint32_t rr = eval_atom<false>(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
+              if (rr == 3u) { general = true; pc = AT_UNSAT; }
+              else if (rr == 2u) { err = true; pc = AT_UNSAT; }
+              else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
+            }
+          }
+          // record hits
+          const bool hit = ok && (err || pc == AT_SAT);
+          const uint64_t hmask = __ballot(hit);
+          if (hmask) {
+            if (hit) {
+              const uint32_t pos = nh + mbcnt64(hmask);
+              if (pos < HCAP) {
+                wl.hp[pos] = q2.z;  // PW_CODE: global policy index
+                wl.hm[pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8);
+                if (err) {
+                  wl.he[4 * pos] = e.code | (e.aux << 8);
+                  wl.he[4 * pos + 1] = e.k;
+                  wl.he[4 * pos + 2] = e.et;
+                  wl.he[4 * pos + 3] = e.ei;
+                }
+              }
+            }
+            nh += popc64(hmask);
+            min_tier = min(min_tier, wave_min(hit ? tier : 0xFFu));
+          }
         }
-        nh += popc64(hmask);
-        min_tier = min(min_tier, wave_min(hit ? tier : 0xFFu));
-      }
+      ne = 0;
+      wave_lds_sync();
     }
-    ne = 0;
-    wave_lds_sync();
-  };
-  // stages this lane's found bucket (cnt > 0), running the stage first when it could overflow
-  auto stage = [&](uint32_t first, uint32_t cnt, uint32_t key0, uint32_t key1) {
-    if (ne + 64 > ECAP) run_stage();
-    const uint64_t m = __ballot(cnt != 0);
-    if (cnt) {
-      const uint32_t pos = ne + mbcnt64(m);
-      wl.efirst[pos] = first;
-      wl.epre[pos] = cnt;
-      wl.ekey[pos] = key0;
-      wl.ekei[pos] = key1;
-    }
-    ne += popc64(m);
-    wave_lds_sync();
-  };
-
-  const uint32_t n_keys = 6 + c.p_nanc + c.r_nanc + a_nanc;
-  for (uint32_t kb = 0; kb < n_keys; kb += 64) {
-    // ---- level-1: lane k probes scope key k ----
-    const uint32_t k = kb + lane;
-    uint32_t cat = 0, et = 0, ei = 0;
-    if (k < n_keys) {
-      uint32_t j = k;
-      if (j < 1 + c.p_nanc) {
-        cat = BK_P;
-        et = j ? c.blk[c.p_anc + 2 * (j - 1)] : c.pt;
-        ei = j ? c.blk[c.p_anc + 2 * (j - 1) + 1] : c.pi;
-      } else if ((j -= 1 + c.p_nanc) < 1 + c.r_nanc) {
-        cat = BK_R;
-        et = j ? c.blk[c.r_anc + 2 * (j - 1)] : c.rt;
-        ei = j ? c.blk[c.r_anc + 2 * (j - 1) + 1] : c.ri;
-      } else if ((j -= 1 + c.r_nanc) < 1 + a_nanc) {
-        cat = BK_A;
-        et = j ? c.blk[a_anc + 2 * (j - 1)] : c.at;
-        ei = j ? c.blk[a_anc + 2 * (j - 1) + 1] : c.ai;
-      } else {
-        j -= 1 + a_nanc;
-        cat = j == 0 ? BK_PT : (j == 1 ? BK_RT : BK_ALL);
-        et = j == 0 ? c.pt : (j == 1 ? c.rt : 0u);
-      }
-    }
-    const uint32_t key0 = (cat << 28) | et;
-    const uint32_t h1 = bucket_hash(cat, et, ei);
-    uint3 e1 = make_uint3(0, 0, 0);
-    if (cat && et < (1u << 28)) e1 = probe(a.btab, a.bmask, h1, key0, ei, 0, 0, 0);
-    stage(e1.x, e1.y, key0, ei);
-    // ---- level-2: one hot slot of this lane's hmask per round ----
-    uint32_t hm = e1.z;
-    while (__ballot(hm != 0)) {
-      uint3 e2 = make_uint3(0, 0, 0);
-      if (hm) {
-        const uint32_t h = __builtin_ctz(hm);
-        hm &= hm - 1;
-        const uint2 v = wl.hot[h];
-        const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
-        e2 = probe(a.btab, a.bmask, bucket_hash2(h1, h, v0, v1), key0, ei, h | BT_L2, v0, v1);
-      }
-      stage(e2.x, e2.y, key0, ei);
-    }
+    if (done) break;
   }
-  if (ne) run_stage();
 
   // ---- merge: deciding tier, duplicates, policy order ----
   const uint32_t t = min_tier;
-  if (nh > HCAP) {
+  if (nh > HCAP || __ballot(general)) {
     if (lane == 0) {
       a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW) << 16);
-      a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);
+      a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
     }
     return;
   }
@@ -1538,6 +1568,7 @@ int dev_image_upload(int device, const Image& img, DevImage* out) {
   if ((rc = up(&d.bstream, img.bstream, d.bytes, s))) return rc;
   d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
   d.indexed = img.indexed;
+  d.combo_mask = img.combo_mask;
   d.n_act = (uint32_t)img.act.size() / 2;
   d.has_bytecode = img.n_atomic < img.n_pol() ? 1u : 0u;
   d.amask_ok = img.amask_ok;
@@ -1611,7 +1642,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.act = img.act; k.n_act = img.n_act; k.amask_ok = img.amask_ok;
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.brefs = img.brefs; k.bstream = img.bstream; k.bmask = img.bmask;
-  k.rows = b.rows; k.row_words = b.row_words;
+  k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   return k;
 }
 

@@ -849,10 +849,11 @@ struct Compiler {
 // ext area.
 template <class AK>
 static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
-  using L1 = std::array<uint32_t, 3>;                   // (cat, et, ei)
-  using L2 = std::array<uint32_t, 6>;                   // (cat, et, ei, h, v0, v1)
+  using L1 = std::array<uint32_t, 7>;                   // (combo, pt, pi, at, ai, rt, ri)
+  using L2 = std::pair<L1, std::array<uint32_t, 3>>;    // (+ h, v0, v1)
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.brefs.clear(); img.bstream.clear();
+  img.combo_mask = 0;
   img.indexed = (n > 0 && img.n_atomic == n) ? 1u : 0u;
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.brefs.assign(1, 0); img.bstream.assign(HEAD_WORDS, 0);
@@ -868,52 +869,42 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
       off += len;
     }
   }
-  // scope options per policy (each a list of level-1 keys the request must enumerate)
-  std::vector<std::vector<std::vector<L1>>> opts(n);
-  for (uint32_t p = 0; p < n; p++) {
-    const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
-    const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
-    auto& o = opts[p];
-    if (pk == SK_EQ || pk == SK_IN || pk == SK_ISIN) o.push_back({L1{BK_P, d[PW_P_ET], d[PW_P_EI]}});
-    if (rk == SK_EQ || rk == SK_IN || rk == SK_ISIN) o.push_back({L1{BK_R, d[PW_R_ET], d[PW_R_EI]}});
-    if (ak == SK_EQ || ak == SK_IN) o.push_back({L1{BK_A, d[PW_A_ET], d[PW_A_EI]}});
-    if (ak == SK_INSET) {
-      std::vector<L1> ks;
-      for (uint32_t k = 0; k < d[PW_A_ET]; k++) ks.push_back(L1{BK_A, img.cpool[d[PW_A_EI] + 2 * k], img.cpool[d[PW_A_EI] + 2 * k + 1]});
-      std::sort(ks.begin(), ks.end());
-      ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
-      o.push_back(ks);  // empty list: `action in []` never applies, the policy needs no bucket
-    }
-    if (rk == SK_IS || rk == SK_ISIN) o.push_back({L1{BK_RT, d[PW_R_TYPE], 0}});
-    if (pk == SK_IS || pk == SK_ISIN) o.push_back({L1{BK_PT, d[PW_P_TYPE], 0}});
-    o.push_back({L1{BK_ALL, 0, 0}});
-  }
-  auto l2_of = [&](const L1& k, uint32_t p) { return L2{k[0], k[1], k[2], akeys[p].h, akeys[p].v0, akeys[p].v1}; };
-  std::map<L1, uint32_t> c1;
-  std::map<L2, uint32_t> c2;
-  for (uint32_t p = 0; p < n; p++)
-    for (auto& ks : opts[p])
-      for (auto& k : ks) {
-        if (akeys[p].ok) c2[l2_of(k, p)]++;
-        else c1[k]++;
-      }
-  std::map<L1, std::vector<uint32_t>> b1;  // level-1 unkeyed lists (ascending policy index)
+  // most specific level-1 keys of every policy: its scope's own entity / type / wildcard
+  std::map<L1, std::vector<uint32_t>> b1;
   std::map<L2, std::vector<uint32_t>> b2;
   std::map<L1, uint32_t> hmask;
   for (uint32_t p = 0; p < n; p++) {
-    size_t best = 0;
-    uint64_t best_cost = ~0ull;
-    for (size_t i = 0; i < opts[p].size(); i++) {
-      uint64_t c = 0;
-      for (auto& k : opts[p][i]) c += akeys[p].ok ? c2[l2_of(k, p)] : c1[k];
-      if (c < best_cost) { best_cost = c; best = i; }
+    const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
+    const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
+    auto comp = [](uint32_t kind, uint32_t ty, uint32_t et, uint32_t ei, uint32_t& kc, uint32_t& t, uint32_t& i) {
+      if (kind == SK_EQ || kind == SK_IN || kind == SK_ISIN) { kc = KC_ENT; t = et; i = ei; }
+      else if (kind == SK_IS) { kc = KC_TYPE; t = ty; i = KW_ANY; }
+      else { kc = KC_WILD; t = KW_ANY; i = KW_ANY; }
+    };
+    uint32_t pkc, pt, pi, rkc, rt, ri;
+    comp(pk, d[PW_P_TYPE], d[PW_P_ET], d[PW_P_EI], pkc, pt, pi);
+    comp(rk, d[PW_R_TYPE], d[PW_R_ET], d[PW_R_EI], rkc, rt, ri);
+    std::vector<std::pair<uint32_t, uint32_t>> acts;  // action components
+    uint32_t akc = KC_ENT;
+    if (ak == SK_EQ || ak == SK_IN) acts.emplace_back(d[PW_A_ET], d[PW_A_EI]);
+    else if (ak == SK_INSET) {
+      for (uint32_t k = 0; k < d[PW_A_ET]; k++) acts.emplace_back(img.cpool[d[PW_A_EI] + 2 * k], img.cpool[d[PW_A_EI] + 2 * k + 1]);
+      std::sort(acts.begin(), acts.end());
+      acts.erase(std::unique(acts.begin(), acts.end()), acts.end());  // empty: `action in []` never applies
+    } else {
+      akc = KC_WILD;
+      acts.emplace_back(KW_ANY, KW_ANY);
     }
-    for (auto& k : opts[p][best]) {
+    const uint32_t combo = key_combo(pkc, akc, rkc);
+    for (auto& a : acts) {
+      const L1 k{combo, pt, pi, a.first, a.second, rt, ri};
+      if ((pt != KW_ANY && pt >= (1u << 28)) || (rt != KW_ANY && rt >= (1u << 28))) throw CedarError("string table too large for the scope index");
+      img.combo_mask |= 1u << combo;
       if (!akeys[p].ok) { b1[k].push_back(p); continue; }
-      b1[k];  // level-1 entry carries the hmask even when it has no unkeyed policies
+      b1[k];  // the level-1 entry carries the hmask even when it has no unkeyed policies
       hmask[k] |= 1u << akeys[p].h;
-      b2[l2_of(k, p)].push_back(p);
-      if (!akeys[p].guarded) b2[L2{k[0], k[1], k[2], akeys[p].h, MISSING_W0, 0}].push_back(p);
+      b2[L2(k, {akeys[p].h, akeys[p].v0, akeys[p].v1})].push_back(p);
+      if (!akeys[p].guarded) b2[L2(k, {akeys[p].h, MISSING_W0, 0u})].push_back(p);
     }
   }
   // record heads (bucket order) then the ext area (one full record per policy)
@@ -921,9 +912,10 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   for (auto& kv : b1) n_heads += (uint32_t)kv.second.size();
   for (auto& kv : b2) n_heads += (uint32_t)kv.second.size();
   std::vector<uint32_t> ext(n);
-  uint32_t ext_end = n_heads * HEAD_WORDS;
-  for (uint32_t p = 0; p < n; p++) { ext[p] = ext_end; ext_end += rec_len[p]; }
-  img.bstream.assign(std::max<uint32_t>(ext_end, HEAD_WORDS), 0);
+  uint64_t ext_end = (uint64_t)n_heads * HEAD_WORDS;
+  for (uint32_t p = 0; p < n; p++) { ext[p] = (uint32_t)ext_end; ext_end += rec_len[p]; }
+  if (ext_end >= (1ull << 32)) throw CedarError("scope index exceeds 16 GiB");
+  img.bstream.assign(std::max<uint64_t>(ext_end, HEAD_WORDS), 0);
   for (uint32_t p = 0; p < n; p++)
     std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
   uint32_t head = 0;
@@ -932,8 +924,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     for (uint32_t p : ps) {
       uint32_t* hd = &img.bstream[(size_t)head * HEAD_WORDS];
       const uint32_t* src = &img.pstream[rec_off[p]];
-      const uint32_t nw = std::min<uint32_t>(rec_len[p], HEAD_WORDS);
-      std::copy(src, src + nw, hd);
+      std::copy(src, src + std::min<uint32_t>(rec_len[p], HEAD_WORDS), hd);
       hd[PW_EXT] = ext[p];
       head++;
     }
@@ -948,19 +939,21 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     while (img.btab[(size_t)h * BT_WORDS] != 0) h = (h + 1) & (size - 1);
     std::copy(e, e + BT_WORDS, &img.btab[(size_t)h * BT_WORDS]);
   };
+  auto l1_hash = [](const L1& k) { return key_hash(k[0], k[1], k[2], k[3], k[4], k[5], k[6]); };
   for (auto& kv : b1) {
     const L1& k = kv.first;
-    if (k[1] >= (1u << 28)) throw CedarError("string table too large for the scope index");
     const uint32_t first = put_heads(kv.second);
-    const uint32_t e[BT_WORDS] = {(k[0] << 28) | k[1], k[2], 0, hmask.count(k) ? hmask[k] : 0u, 0, first,
-                                  (uint32_t)kv.second.size(), 0};
-    insert(bucket_hash(k[0], k[1], k[2]), e);
+    const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], 0, 0, first,
+                                  (uint32_t)kv.second.size(), hmask.count(k) ? hmask[k] : 0u, 0, 0, 0, 0};
+    insert(l1_hash(k), e);
   }
   for (auto& kv : b2) {
-    const L2& k = kv.first;
+    const L1& k = kv.first.first;
+    const auto& x = kv.first.second;
     const uint32_t first = put_heads(kv.second);
-    const uint32_t e[BT_WORDS] = {(k[0] << 28) | k[1], k[2], k[3] | BT_L2, k[4], k[5], first, (uint32_t)kv.second.size(), 0};
-    insert(bucket_hash2(bucket_hash(k[0], k[1], k[2]), k[3], k[4], k[5]), e);
+    const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16) | BT_L2 | x[0], k[1], k[2], k[3], k[4], k[5], k[6], x[1], x[2],
+                                  first, (uint32_t)kv.second.size(), 0, 0, 0, 0, 0};
+    insert(bucket_hash2(l1_hash(k), x[0], x[1], x[2]), e);
   }
   img.brefs.assign(1, 0);
 }
@@ -1094,7 +1087,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.vec(pol); w.vec(tier_end); w.vec(code); w.vec(cpool); w.vec(gstr_off); w.vec(hot); w.bytes(gstr_bytes);
   w.vec(act); w.u32(amask_ok); w.u32(n_atomic);
   w.vec(pstream); w.vec(chunks); w.vec(tier_cend);
-  w.vec(btab); w.vec(brefs); w.vec(bstream); w.u32(indexed);
+  w.vec(btab); w.vec(brefs); w.vec(bstream); w.u32(indexed); w.u32(combo_mask);
   w.u32((uint32_t)strings.size());
   for (auto& s : strings) w.str(s);
   w.u32((uint32_t)meta.size());
@@ -1118,7 +1111,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->gstr_off = r.vec(); img->hot = r.vec(); img->gstr_bytes = r.bytes();
   img->act = r.vec(); img->amask_ok = r.u32(); img->n_atomic = r.u32();
   img->pstream = r.vec(); img->chunks = r.vec(); img->tier_cend = r.vec();
-  img->btab = r.vec(); img->brefs = r.vec(); img->bstream = r.vec(); img->indexed = r.u32();
+  img->btab = r.vec(); img->brefs = r.vec(); img->bstream = r.vec(); img->indexed = r.u32(); img->combo_mask = r.u32();
   uint32_t ns = r.u32();
   for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }
   uint32_t nm = r.u32();

@@ -36,6 +36,7 @@ struct Image {
   // scope index over atomic policies (image.h "scope index"); indexed = every policy is atomic
   std::vector<uint32_t> btab, brefs, bstream;
   uint32_t indexed = 0;
+  uint32_t combo_mask = 0;  // level-1 key combos in use (bit key_combo(..))
   std::vector<uint8_t> gstr_bytes;
   std::vector<PolicyMeta> meta;
   std::vector<std::string> strings;

@@ -94,25 +94,33 @@ constexpr uint32_t PW_EXT = PW_LANE;
 // ---- scope index (probe kernel) ---------------------------------------------------------------
 // Every policy of an all-atomic image is filed under keys that any request it can apply to (or
 // error on) must enumerate:
-//   level 1  (cat, et, ei): the principal / resource / action entity of an ==, in or is-in scope
-//            (the request enumerates its ancestor-or-self UIDs), the principal / resource type of
-//            an `is` scope, or ALL;
-//   level 2  (cat, et, ei, h, value): additionally the constant c of an equality atom hot(h) == c
-//            that every satisfying evaluation passes and that no erroring atom precedes; filed
-//            under value c, and also under MISSING_W0 when an absent h would make that atom
-//            raise (no `has h` guard before it).
-// A request probes level 1 for all its scope keys, then level 2 under each found key for every
-// hot slot in the entry's hmask with its own value of that slot (or MISSING_W0).
+//   level 1  a (principal, action, resource) triple; each component is the scope's entity (==,
+//            in, is-in: the request enumerates its ancestor-or-self UIDs), its type (`is`), or a
+//            wildcard; `action in [..]` files one key per listed action. The component kinds form
+//            the key's combo (KC_*); the image records the combos in use (combo_mask) and a
+//            request probes each used combo's product of its own candidate components;
+//   level 2  the level-1 key plus (h, value): the constant c of an equality atom hot(h) == c that
+//            every satisfying evaluation passes and that no erroring atom precedes; filed under
+//            value c, and also under MISSING_W0 when an absent h would make that atom raise (no
+//            `has h` guard before it).
+// A request probes level 1 for its keys, then level 2 under each found key for every hot slot in
+// the entry's hmask, with its own value of that slot (or MISSING_W0).
 // btab: open addressing, linear probing, power-of-two slots of BT_WORDS:
-//   [cat << 28 | et, ei, h | BT_L2 (level 2) or 0, hmask (level 1) or value w0, value w1,
-//    first, count, 0]; an empty slot has word0 == 0.
+//   [BT_USED | combo << 16 | (BT_L2 | h for level 2), p type, p id, a type, a id, r type, r id,
+//    value w0, value w1, first, count, hmask (level 1), 0, 0, 0, 0]; empty slot: word0 == 0.
 // Records: bstream[first * HEAD_WORDS ...] fixed heads (descriptor + the first 4 atoms) in bucket
 // order; the head's PW_EXT is the absolute bstream offset of the full variable-length record
 // (descriptor, atoms, atom data) in the ext area, which record-relative offsets address.
-enum BucketCat : uint32_t { BK_P = 1, BK_R = 2, BK_A = 3, BK_PT = 4, BK_RT = 5, BK_ALL = 6 };
-constexpr uint32_t BT_WORDS = 8, BT_L2 = 0x100, HEAD_WORDS = 32, HEAD_ATOMS = 4;
-__host__ __device__ constexpr inline uint32_t bucket_hash(uint32_t cat, uint32_t et, uint32_t ei) {
-  uint32_t h = (cat * 0x9E3779B1u) ^ (et * 0x85EBCA77u) ^ (ei * 0xC2B2AE3Du);
+constexpr uint32_t KC_WILD = 0, KC_ENT = 1, KC_TYPE = 2;  // component kinds
+__host__ __device__ constexpr inline uint32_t key_combo(uint32_t pk, uint32_t ak, uint32_t rk) { return pk | (ak << 2) | (rk << 3); }
+constexpr uint32_t KW_ANY = 0xFFFFFFFFu;  // id of a type-only component; both words of a wildcard
+constexpr uint32_t BT_WORDS = 16, BT_USED = 0x80000000u, BT_L2 = 0x100, HEAD_WORDS = 32, HEAD_ATOMS = 4;
+__host__ __device__ constexpr inline uint32_t key_hash(uint32_t combo, uint32_t pt, uint32_t pi, uint32_t at, uint32_t ai,
+                                                       uint32_t rt, uint32_t ri) {
+  uint32_t h = combo * 0x9E3779B1u;
+  h = (h ^ pt) * 0x85EBCA77u; h = (h ^ pi) * 0xC2B2AE3Du;
+  h = (h ^ at) * 0x27D4EB2Fu; h = (h ^ ai) * 0x165667B1u;
+  h = (h ^ rt) * 0xD3A2646Cu; h = (h ^ ri) * 0xFD7046C5u;
   h ^= h >> 16;
   h *= 0x7FEB352Du;
   h ^= h >> 15;
