@@ -29,6 +29,7 @@ struct LoadedImage {
 struct cg_ctx {
   int device = 0;
   void* stream = nullptr;
+  DevPool* pool = nullptr;  // batch buffers (device + pinned staging), reused across batches
   std::mutex mu;
   std::map<uint64_t, std::shared_ptr<LoadedImage>> images;
   std::shared_ptr<LoadedImage> active;
@@ -205,6 +206,7 @@ int cg_ctx_create(int device, cg_ctx** out) {
   if (!c) return CG_E_ARG;
   c->device = device;
   if (dev_stream_create(device, &c->stream)) { delete c; return CG_E_DEVICE; }
+  if (dev_pool_create(device, &c->pool)) { dev_stream_destroy(c->stream); delete c; return CG_E_DEVICE; }
   *out = c;
   return CG_OK;
 }
@@ -216,6 +218,7 @@ void cg_ctx_destroy(cg_ctx* ctx) {
     ctx->active.reset();
     ctx->images.clear();
   }
+  dev_pool_destroy(ctx->pool);
   dev_stream_destroy(ctx->stream);
   delete ctx;
 }
@@ -413,7 +416,7 @@ int cg_batch_submit(cg_batch* b) {
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
   b->host.finalize_strings();
   if (b->host.n() == 0) { b->submitted = b->done = true; return CG_OK; }
-  if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   if (dev_eval(b->img->dev, b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   b->submitted = true;
   return CG_OK;
@@ -425,52 +428,71 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   if (b->done) return CG_OK;
   (void)timeout_ns;  // stream sync is bounded by the kernel; the webhook deadline is enforced by the caller
   if (dev_download(b->dev, b->host, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
-  // overflowed result lists: re-run just those requests with exact capacities
-  std::vector<uint32_t> idx;
-  uint32_t capr = 0, cape = 0;
+  // Overflowed result lists: re-run just those requests. Capacity overflows of the probe kernel
+  // re-run there with the exact capacities; requests it could not decide (RF_GENERAL) and any
+  // stream-kernel overflow re-run on the stream kernel, which reports exact counts, so a second
+  // pass with those capacities completes it.
+  std::vector<uint32_t> idx_probe, idx_gen;
+  uint32_t capr_p = 0, cape_p = 0, capr_g = 0, cape_g = 0;
   for (uint32_t i = 0; i < b->host.n(); i++) {
     uint32_t fl = b->host.res[2 * (size_t)i] >> 16;
     if (!(fl & cgi::RF_VALID)) { b->err = "request left unevaluated"; return CG_E_DEVICE; }
-    if (fl & cgi::RF_OVERFLOW) {
-      idx.push_back(i);
-      capr = std::max(capr, b->host.res[2 * (size_t)i + 1] & 0xFFFF);
-      cape = std::max(cape, b->host.res[2 * (size_t)i + 1] >> 16);
+    if (!(fl & cgi::RF_OVERFLOW)) continue;
+    const uint32_t nr = b->host.res[2 * (size_t)i + 1] & 0xFFFF, ne = b->host.res[2 * (size_t)i + 1] >> 16;
+    if ((fl & cgi::RF_GENERAL) || !b->img->dev.indexed) {
+      idx_gen.push_back(i); capr_g = std::max(capr_g, nr); cape_g = std::max(cape_g, ne);
+    } else {
+      idx_probe.push_back(i); capr_p = std::max(capr_p, nr); cape_p = std::max(cape_p, ne);
     }
   }
-  // re-runs on the stream kernel are exact; a re-run that still overflows its capacities reports
-  // the exact counts, so a second pass with those capacities completes it
-  for (int pass = 0; pass < 3 && !idx.empty(); pass++) {
-    capr = std::max(std::min(capr, 4096u), 8u);
-    cape = std::max(std::min(cape, 4096u), 4u);
-    std::vector<uint32_t> res, rf, rp, er;
-    if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, b->ctx->stream, res, rf, rp, er)) {
-      b->err = dev_last_error();
-      return CG_E_DEVICE;
-    }
-    std::vector<uint32_t> again;
-    uint32_t capr2 = 0, cape2 = 0;
-    for (size_t k = 0; k < idx.size(); k++) {
-      uint32_t i = idx[k];
-      uint32_t fl = res[2 * k] >> 16;
-      uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
-      if (fl & cgi::RF_OVERFLOW) {
-        again.push_back(i);
-        capr2 = std::max(capr2, nr);
-        cape2 = std::max(cape2, ne);
-        continue;
+  auto rerun = [&](std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, bool probe) -> int {
+    for (int pass = 0; pass < 3 && !idx.empty(); pass++) {
+      capr = std::max(std::min(capr, 4096u), 8u);
+      cape = std::max(std::min(cape, 4096u), 4u);
+      std::vector<uint32_t> res, rf, rp, er;
+      if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, probe, b->ctx->stream, res, rf, rp, er)) {
+        b->err = dev_last_error();
+        return CG_E_DEVICE;
       }
-      const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
-      // the re-run is authoritative for the whole result (the probe kernel does not decide a
-      // request whose hits overflowed its staging area or that needs structural equality)
-      b->host.res[2 * (size_t)i] = res[2 * k];
-      b->host.res[2 * (size_t)i + 1] = res[2 * k + 1];
-      b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
-      b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
+      std::vector<uint32_t> again;
+      uint32_t capr2 = 0, cape2 = 0;
+      for (size_t k = 0; k < idx.size(); k++) {
+        uint32_t i = idx[k];
+        uint32_t fl = res[2 * k] >> 16;
+        uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
+        if (fl & cgi::RF_OVERFLOW) {
+          again.push_back(i);
+          capr2 = std::max(capr2, nr);
+          cape2 = std::max(cape2, ne);
+          continue;
+        }
+        const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
+        b->host.res[2 * (size_t)i] = res[2 * k];
+        b->host.res[2 * (size_t)i + 1] = res[2 * k + 1];
+        b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
+        b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
+      }
+      idx.swap(again);
+      capr = capr2;
+      cape = cape2;
     }
-    idx.swap(again);
-    capr = capr2;
-    cape = cape2;
-    if (pass == 2 && !idx.empty()) { b->err = "result lists exceed the device re-run capacity"; return CG_E_RANGE; }
+    if (!idx.empty()) { b->err = "result lists exceed the device re-run capacity"; return CG_E_RANGE; }
+    return CG_OK;
+  };
+  if (!idx_probe.empty()) {
+    // a probe re-run can still find RF_GENERAL requests: those move to the stream kernel
+    int rc = rerun(idx_probe, capr_p, cape_p, true);
+    if (rc == CG_E_RANGE) {
+      for (uint32_t i : idx_probe) idx_gen.push_back(i);
+      capr_g = std::max(capr_g, 64u);
+      cape_g = std::max(cape_g, 64u);
+    } else if (rc) {
+      return rc;
+    }
+  }
+  if (!idx_gen.empty()) {
+    int rc = rerun(idx_gen, capr_g, cape_g, false);
+    if (rc) return rc;
   }
   b->done = true;
   return CG_OK;

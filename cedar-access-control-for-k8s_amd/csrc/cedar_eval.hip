@@ -23,6 +23,9 @@
 
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
 #include <string>
 
 #include "device.h"
@@ -1455,7 +1458,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   const uint32_t t = min_tier;
   if (nh > HCAP || __ballot(general)) {
     if (lane == 0) {
-      a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW) << 16);
+      a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | RF_GENERAL) << 16);
       a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
     }
     return;
@@ -1592,39 +1595,122 @@ void dev_image_free(DevImage* d) {
   *d = DevImage();
 }
 
-int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream) {
+struct DevPool {
+  int device = -1;
+  std::mutex mu;
+  std::multimap<size_t, void*> dev_free, host_free;  // size class -> idle block
+  std::vector<std::pair<void*, bool>> owned;         // (block, pinned host)
+};
+
+static size_t size_class(size_t n) {
+  size_t c = (size_t)1 << 16;
+  while (c < n) c <<= 1;
+  return c;
+}
+
+static int pool_get(DevPool* p, bool host, size_t n, void** out, size_t* cls) {
+  *cls = size_class(n);
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    auto& fl = host ? p->host_free : p->dev_free;
+    auto it = fl.find(*cls);
+    if (it != fl.end()) {
+      *out = it->second;
+      fl.erase(it);
+      return 0;
+    }
+  }
+  if (host) HIPCHK(hipHostMalloc(out, *cls, hipHostMallocDefault), "hipHostMalloc");
+  else HIPCHK(hipMalloc(out, *cls), "hipMalloc");
+  std::lock_guard<std::mutex> g(p->mu);
+  p->owned.emplace_back(*out, host);
+  return 0;
+}
+
+static void pool_put(DevPool* p, bool host, void* blk, size_t cls) {
+  if (!p || !blk) return;
+  std::lock_guard<std::mutex> g(p->mu);
+  (host ? p->host_free : p->dev_free).emplace(cls, blk);
+}
+
+int dev_pool_create(int device, DevPool** out) {
+  *out = new (std::nothrow) DevPool();
+  if (!*out) { g_err = "out of host memory"; return -1; }
+  (*out)->device = device;
+  return 0;
+}
+
+void dev_pool_destroy(DevPool* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  (void)hipDeviceSynchronize();
+  for (auto& o : p->owned) {
+    if (o.second) (void)hipHostFree(o.first);
+    else (void)hipFree(o.first);
+  }
+  delete p;
+}
+
+// One pinned staging block and one device block for the inputs (256-B aligned sections), one for
+// the results; a batch costs two copies and a memset, and no allocation once the pool is warm.
+int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, DevPool* pool) {
   HIPCHK(hipSetDevice(device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
   DevBatch d;
   d.device = device;
+  d.pool = pool;
   d.n = b.n();
   d.heap_words = b.heap.size();
-  int rc;
-  if ((rc = up(&d.heap, b.heap, d.bytes, s))) return rc;
-  if ((rc = up(&d.req_base, b.req_base, d.bytes, s))) return rc;
-  if ((rc = up(&d.rows, b.rows, d.bytes, s))) return rc;
   d.row_words = b.row_words;
-  if ((rc = up(&d.bstr_off, b.bstr_off, d.bytes, s))) return rc;
-  if ((rc = up(&d.bstr_bytes, b.bstr_bytes, d.bytes, s))) return rc;
-  const size_t n = std::max<uint32_t>(b.n(), 1);
   d.capr = b.capr;
   d.cape = b.cape;
-  HIPCHK(hipMalloc((void**)&d.res, n * 2 * 4), "hipMalloc res");
-  HIPCHK(hipMalloc((void**)&d.reasons_f, n * d.capr * 4), "hipMalloc reasons");
-  HIPCHK(hipMalloc((void**)&d.reasons_p, n * d.capr * 4), "hipMalloc reasons");
-  HIPCHK(hipMalloc((void**)&d.errs, n * d.cape * ERR_WORDS * 4), "hipMalloc errs");
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const void* src[5] = {b.heap.data(), b.req_base.data(), b.rows.data(), b.bstr_off.data(), b.bstr_bytes.data()};
+  const size_t len[5] = {b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.bstr_off.size() * 4, b.bstr_bytes.size()};
+  size_t off[5], in_bytes = 0;
+  for (int k = 0; k < 5; k++) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
+  const size_t n = std::max<uint32_t>(b.n(), 1);
+  const size_t o_res = 0, o_rf = al(n * 2 * 4), o_rp = o_rf + al(n * d.capr * 4), o_er = o_rp + al(n * d.capr * 4);
+  d.out_bytes = o_er + al(n * d.cape * ERR_WORDS * 4);
+  int rc;
+  if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) return rc;
+  if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) { pool_put(pool, false, d.in_blk, d.in_cls); return rc; }
+  if ((rc = pool_get(pool, true, std::max(in_bytes, d.out_bytes), &d.stage, &d.stage_cls))) {
+    pool_put(pool, false, d.in_blk, d.in_cls);
+    pool_put(pool, false, d.out_blk, d.out_cls);
+    return rc;
+  }
+  uint8_t* st = (uint8_t*)d.stage;
+  for (int k = 0; k < 5; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
+  uint8_t* in = (uint8_t*)d.in_blk;
+  uint8_t* o = (uint8_t*)d.out_blk;
+  d.heap = (uint32_t*)(in + off[0]);
+  d.req_base = (uint32_t*)(in + off[1]);
+  d.rows = (uint32_t*)(in + off[2]);
+  d.bstr_off = (uint32_t*)(in + off[3]);
+  d.bstr_bytes = in + off[4];
+  d.res = (uint32_t*)(o + o_res);
+  d.reasons_f = (uint32_t*)(o + o_rf);
+  d.reasons_p = (uint32_t*)(o + o_rp);
+  d.errs = (uint32_t*)(o + o_er);
+  d.bytes = in_bytes + d.out_bytes;
+  *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
+  HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
   HIPCHK(hipMemsetAsync(d.res, 0, n * 2 * 4, s), "memset res");
-  d.bytes += n * (2 + 2 * d.capr + d.cape * ERR_WORDS) * 4;
-  *out = d;
   return 0;
 }
 
 void dev_batch_free(DevBatch* d) {
   if (d->device < 0) return;
-  (void)hipSetDevice(d->device);
-  for (void* p : {(void*)d->heap, (void*)d->req_base, (void*)d->rows, (void*)d->req_idx, (void*)d->bstr_off, (void*)d->bstr_bytes,
-                  (void*)d->res, (void*)d->reasons_f, (void*)d->reasons_p, (void*)d->errs})
-    if (p) (void)hipFree(p);
+  if (d->pool) {
+    // the stream may still be reading the staging block / writing results: wait before reuse
+    (void)hipSetDevice(d->device);
+    (void)hipDeviceSynchronize();
+    pool_put(d->pool, false, d->in_blk, d->in_cls);
+    pool_put(d->pool, false, d->out_blk, d->out_cls);
+    pool_put(d->pool, true, d->stage, d->stage_cls);
+  }
+  if (d->req_idx) (void)hipFree(d->req_idx);
   *d = DevBatch();
 }
 
@@ -1669,7 +1755,7 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
 // Re-evaluates a subset of requests (overflowed result lists) with larger capacities; results are
 // compact in subset order and copied to host before returning.
 int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
-                    uint32_t cape, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
+                    uint32_t cape, bool probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
                     std::vector<uint32_t>& rp, std::vector<uint32_t>& er) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
@@ -1687,7 +1773,10 @@ int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx,
     if ((e = hipMalloc((void**)&d_er, (size_t)n * cape * ERR_WORDS * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
     if ((e = hipMemcpyAsync(d_idx, idx, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) { rc = fail(e, "H2D"); break; }
     KArgs k = make_args(img, b, d_idx, n, d_res, d_rf, d_rp, d_er, capr, cape);
-    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
+    if (probe && img.indexed)
+      hipLaunchKernelGGL(cedar_probe_kernel, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
+    else
+      hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
     if ((e = hipGetLastError()) != hipSuccess) { rc = fail(e, "launch"); break; }
     res.resize((size_t)n * 2); rf.resize((size_t)n * capr); rp.resize((size_t)n * capr); er.resize((size_t)n * cape * ERR_WORDS);
     if ((e = hipMemcpyAsync(res.data(), d_res, res.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
@@ -1710,13 +1799,18 @@ int dev_download(const DevBatch& b, Batch& host, void* stream) {
   host.reasons_f.resize(n * b.capr);
   host.reasons_p.resize(n * b.capr);
   host.errs.resize(n * b.cape * ERR_WORDS);
-  if (n) {
-    HIPCHK(hipMemcpyAsync(host.res.data(), b.res, n * 2 * 4, hipMemcpyDeviceToHost, s), "D2H res");
-    HIPCHK(hipMemcpyAsync(host.reasons_f.data(), b.reasons_f, n * b.capr * 4, hipMemcpyDeviceToHost, s), "D2H");
-    HIPCHK(hipMemcpyAsync(host.reasons_p.data(), b.reasons_p, n * b.capr * 4, hipMemcpyDeviceToHost, s), "D2H");
-    HIPCHK(hipMemcpyAsync(host.errs.data(), b.errs, n * b.cape * ERR_WORDS * 4, hipMemcpyDeviceToHost, s), "D2H");
-  }
+  if (n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
   HIPCHK(hipStreamSynchronize(s), "sync download");
+  if (!n) return 0;
+  const uint8_t* st = (const uint8_t*)b.stage;
+  const uint8_t* base = (const uint8_t*)b.out_blk;
+  auto cp = [&](std::vector<uint32_t>& v, const uint32_t* dev) {
+    if (!v.empty()) std::memcpy(v.data(), st + ((const uint8_t*)dev - base), v.size() * 4);
+  };
+  cp(host.res, b.res);
+  cp(host.reasons_f, b.reasons_f);
+  cp(host.reasons_p, b.reasons_p);
+  cp(host.errs, b.errs);
   return 0;
 }
 

@@ -20,13 +20,22 @@ struct DevImage {
   size_t bytes = 0;
 };
 
+// Per-context cache of device and pinned host buffers (size classes), so that a batch costs no
+// hipMalloc / hipFree (hipFree synchronises the device) and its copies run from pinned memory.
+struct DevPool;
+
 struct DevBatch {
   int device = -1;
+  DevPool* pool = nullptr;
+  // inputs: one device block (heap | req_base | rows | bstr_off | bstr_bytes), one copy
   uint32_t *heap = nullptr, *req_base = nullptr, *rows = nullptr, *req_idx = nullptr, *bstr_off = nullptr;
   uint8_t* bstr_bytes = nullptr;
+  // results: one device block (res | reasons_f | reasons_p | errs), one copy back
   uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
   uint32_t n = 0, capr = 0, cape = 0, row_words = 0;
   size_t heap_words = 0, bytes = 0;
+  void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)
+  size_t in_cls = 0, out_cls = 0, stage_cls = 0, out_bytes = 0;
 };
 
 // All functions return 0 on success, or a negative CG_E_* code with dev_last_error() set.
@@ -36,13 +45,17 @@ int dev_select(int device);
 int dev_synchronize(int device);
 int dev_image_upload(int device, const Image& img, DevImage* out);
 void dev_image_free(DevImage* d);
-int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream);
-void dev_batch_free(DevBatch* d);
+int dev_pool_create(int device, DevPool** out);
+void dev_pool_destroy(DevPool* p);
+// Uploads the batch's inputs (staged through a pinned block, one H2D copy) and zeroes its results.
+int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, DevPool* pool);
+void dev_batch_free(DevBatch* d);  // returns the blocks to the batch's pool
 // Evaluates every request of the batch into the batch's device result buffers (async on stream).
 int dev_eval(const DevImage& img, DevBatch& b, void* stream);
-// Re-evaluates the subset idx[0..n) with larger result capacities; synchronous, results on host.
+// Re-evaluates the subset idx[0..n) with larger result capacities (probe: on the probe kernel, for
+// an indexed image; else the stream kernel); synchronous, results on host.
 int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
-                    uint32_t cape, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
+                    uint32_t cape, bool probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
                     std::vector<uint32_t>& rp, std::vector<uint32_t>& er);
 int dev_download(const DevBatch& b, Batch& host, void* stream);
 int dev_stream_create(int device, void** stream);
