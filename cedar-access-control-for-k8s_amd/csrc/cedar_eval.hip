@@ -1163,7 +1163,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
 // Structural (set / record) equality is left to the stream kernel: such a request is flagged
 // RF_OVERFLOW and the host re-runs it there (rare: templates compare primitives).
 constexpr uint32_t WAVES = BLOCK / 64;
-constexpr uint32_t HCAP = 64;   // hits per request staged in LDS; more -> overflow re-run
+constexpr uint32_t HCAP = 256;  // hits per request staged in LDS; more -> re-run on the stream kernel
 constexpr uint32_t ECAP = 128;  // found buckets staged before their candidates run
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
@@ -1454,7 +1454,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
     if (done) break;
   }
 
-  // ---- merge: deciding tier, duplicates, policy order ----
+  // ---- merge: deciding tier, duplicates, policy order (hits in chunks of 64 lanes) ----
   const uint32_t t = min_tier;
   if (nh > HCAP || __ballot(general)) {
     if (lane == 0) {
@@ -1463,28 +1463,39 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
     }
     return;
   }
-  const bool have = lane < nh;
-  const uint32_t pj = have ? wl.hp[lane] : 0xFFFFFFFFu;
-  const uint32_t mj = have ? wl.hm[lane] : 0u;
-  const uint32_t kind = mj & 0xFF;
-  bool el = have && (mj >> 8) == t;
-  for (uint32_t x = 0; x < nh; x++) {  // a policy filed under several keys the request has hits twice
-    const uint32_t px = wl.hp[x];
-    if (x < lane && px == pj && (wl.hm[x] >> 8) == t) el = false;
+  uint32_t nf = 0, np = 0, nerr = 0;
+  for (uint32_t c0 = 0; c0 < nh; c0 += 64) {
+    const uint32_t j = c0 + lane;
+    const bool have = j < nh;
+    const uint32_t pj = have ? wl.hp[j] : 0xFFFFFFFFu;
+    const uint32_t mj = have ? wl.hm[j] : 0u;
+    const uint32_t kind = mj & 0xFF;
+    bool el = have && (mj >> 8) == t;
+    for (uint32_t x = 0; x < j && el; x++)  // a policy filed under several keys the request has hits twice
+      if (wl.hp[x] == pj && (wl.hm[x] >> 8) == t) el = false;
+    if (have) wl.hel[j] = el ? 1u : 0u;
+    nf += popc64(__ballot(el && kind == 1));
+    np += popc64(__ballot(el && kind == 0));
+    nerr += popc64(__ballot(el && kind == 2));
   }
-  wl.hel[lane] = el ? 1u : 0u;
   wave_lds_sync();
-  const uint32_t nf = popc64(__ballot(el && kind == 1)), np = popc64(__ballot(el && kind == 0)),
-                 nerr = popc64(__ballot(el && kind == 2));
-  uint32_t rank = 0;
-  for (uint32_t x = 0; x < nh; x++)
-    rank += (wl.hel[x] && (wl.hm[x] & 0xFF) == kind && wl.hp[x] < pj) ? 1u : 0u;
   const uint32_t dk = nf ? 1u : (np ? 0u : 3u);
-  if (el && kind == dk && rank < a.capr) (nf ? a.reasons_f : a.reasons_p)[(size_t)gid * a.capr + rank] = pj;
-  if (el && kind == 2 && rank < a.cape) {
-    uint32_t* er = a.errs + ((size_t)gid * a.cape + rank) * ERR_WORDS;
-    er[0] = pj; er[1] = wl.he[4 * lane]; er[2] = wl.he[4 * lane + 1]; er[3] = wl.he[4 * lane + 2];
-    er[4] = wl.he[4 * lane + 3]; er[5] = 0;
+  for (uint32_t c0 = 0; c0 < nh; c0 += 64) {
+    const uint32_t j = c0 + lane;
+    if (j < nh && wl.hel[j]) {
+      const uint32_t pj = wl.hp[j], kind = wl.hm[j] & 0xFF;
+      if (kind == dk || kind == 2) {
+        uint32_t rank = 0;
+        for (uint32_t x = 0; x < nh; x++)
+          rank += (wl.hel[x] && (wl.hm[x] & 0xFF) == kind && wl.hp[x] < pj) ? 1u : 0u;
+        if (kind == dk && rank < a.capr) (nf ? a.reasons_f : a.reasons_p)[(size_t)gid * a.capr + rank] = pj;
+        if (kind == 2 && rank < a.cape) {
+          uint32_t* er = a.errs + ((size_t)gid * a.cape + rank) * ERR_WORDS;
+          er[0] = pj; er[1] = wl.he[4 * j]; er[2] = wl.he[4 * j + 1]; er[3] = wl.he[4 * j + 2];
+          er[4] = wl.he[4 * j + 3]; er[5] = 0;
+        }
+      }
+    }
   }
   if (lane == 0) {
     const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);

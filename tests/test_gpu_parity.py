@@ -217,13 +217,15 @@ def test_hot_reload_epochs(ctx):
 
 
 # ---------------------------------------------------------------- scope-index kernel paths
-def test_index_kernel_hit_overflow_reruns(ctx):
-    """More satisfied policies than the index kernel stages per request (64) -> re-run path."""
+@pytest.mark.parametrize("n", [150, 700])
+def test_index_kernel_hit_overflow_reruns(ctx, n):
+    """Many satisfied policies: beyond the inline reason capacity (probe-kernel re-run with exact
+    capacities) and, at 700, beyond the 256 hits the probe kernel stages (stream-kernel re-run)."""
     pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
-                     for i in range(150))
+                     for i in range(n))
     pols += '\nforbid (principal, action == k8s::Action::"create", resource) when { principal has nick };'
     stores = [cedargpu.MemoryStore("many.cedar", pols)]
-    assert cedargpu.image_stats(cedargpu.build_image(stores))["atomic"] == 151
+    assert cedargpu.image_stats(cedargpu.build_image(stores))["atomic"] == n + 1
     g = Gen(91)
     check_items(ctx, stores, [g.item() for _ in range(300)])
 
