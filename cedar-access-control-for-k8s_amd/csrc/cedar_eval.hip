@@ -1191,7 +1191,7 @@ struct WaveLds {
   uint32_t ecombo[ECAP];     // key combo of the bucket's level-1 key
   uint32_t hp[HCAP];         // hit: global policy index
   uint32_t hm[HCAP];         // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8
-  uint32_t hel[HCAP];        // hit is in the deciding tier and not a duplicate
+  uint32_t hs[HCAP];         // merge: sort keys (policy index << 8 | hit slot)
   uint32_t he[HCAP * 4];     // error words: code | aux << 8, k, et, ei
   uint2 hot[NHOT];
 };
@@ -1463,39 +1463,48 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
     }
     return;
   }
-  uint32_t nf = 0, np = 0, nerr = 0;
-  for (uint32_t c0 = 0; c0 < nh; c0 += 64) {
-    const uint32_t j = c0 + lane;
-    const bool have = j < nh;
-    const uint32_t pj = have ? wl.hp[j] : 0xFFFFFFFFu;
-    const uint32_t mj = have ? wl.hm[j] : 0u;
-    const uint32_t kind = mj & 0xFF;
-    bool el = have && (mj >> 8) == t;
-    for (uint32_t x = 0; x < j && el; x++)  // a policy filed under several keys the request has hits twice
-      if (wl.hp[x] == pj && (wl.hm[x] >> 8) == t) el = false;
-    if (have) wl.hel[j] = el ? 1u : 0u;
-    nf += popc64(__ballot(el && kind == 1));
-    np += popc64(__ballot(el && kind == 0));
-    nerr += popc64(__ballot(el && kind == 2));
-  }
+  // bitonic sort of (policy index << 8 | slot) over the next power of two >= nh (<= HCAP)
+  uint32_t m = 2;
+  while (m < nh) m <<= 1;
+  for (uint32_t i = lane; i < m; i += 64) wl.hs[i] = i < nh ? ((wl.hp[i] << 8) | i) : 0xFFFFFFFFu;
   wave_lds_sync();
-  const uint32_t dk = nf ? 1u : (np ? 0u : 3u);
-  for (uint32_t c0 = 0; c0 < nh; c0 += 64) {
-    const uint32_t j = c0 + lane;
-    if (j < nh && wl.hel[j]) {
-      const uint32_t pj = wl.hp[j], kind = wl.hm[j] & 0xFF;
-      if (kind == dk || kind == 2) {
-        uint32_t rank = 0;
-        for (uint32_t x = 0; x < nh; x++)
-          rank += (wl.hel[x] && (wl.hm[x] & 0xFF) == kind && wl.hp[x] < pj) ? 1u : 0u;
-        if (kind == dk && rank < a.capr) (nf ? a.reasons_f : a.reasons_p)[(size_t)gid * a.capr + rank] = pj;
-        if (kind == 2 && rank < a.cape) {
-          uint32_t* er = a.errs + ((size_t)gid * a.cape + rank) * ERR_WORDS;
-          er[0] = pj; er[1] = wl.he[4 * j]; er[2] = wl.he[4 * j + 1]; er[3] = wl.he[4 * j + 2];
-          er[4] = wl.he[4 * j + 3]; er[5] = 0;
+  for (uint32_t k = 2; k <= m; k <<= 1) {
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      for (uint32_t i0 = 0; i0 < (m >> 1); i0 += 64) {
+        const uint32_t q = i0 + lane;  // compare-exchange pair q
+        if (q < (m >> 1)) {
+          const uint32_t lo = ((q / jj) * 2 * jj) + (q % jj), hi = lo + jj;
+          const uint32_t x = wl.hs[lo], y = wl.hs[hi];
+          const bool up = (lo & k) == 0;
+          if ((x > y) == up) { wl.hs[lo] = y; wl.hs[hi] = x; }
         }
       }
+      wave_lds_sync();
     }
+  }
+  // deciding-tier hits, duplicates (adjacent after the sort) dropped; ranks by prefix counts
+  uint32_t nf = 0, np = 0, nerr = 0;
+  for (uint32_t c0 = 0; c0 < nh; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const uint32_t key = i < nh ? wl.hs[i] : 0xFFFFFFFFu;
+    const uint32_t slot = key & 0xFF, pj = key >> 8;
+    const uint32_t mj = i < nh ? wl.hm[slot] : 0u;
+    const uint32_t kind = mj & 0xFF;
+    const bool el = i < nh && (mj >> 8) == t && (i == 0 || (wl.hs[i - 1] >> 8) != pj);
+    const uint64_t bf = __ballot(el && kind == 1), bp = __ballot(el && kind == 0), be = __ballot(el && kind == 2);
+    const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
+    // the deciding list is the forbids if any forbid is satisfied at all: decided after the loop,
+    // so both lists are written (their capacities are separate) and only one is read back
+    if (el && kind == 1 && rf < a.capr) a.reasons_f[(size_t)gid * a.capr + rf] = pj;
+    if (el && kind == 0 && rp < a.capr) a.reasons_p[(size_t)gid * a.capr + rp] = pj;
+    if (el && kind == 2 && re < a.cape) {
+      uint32_t* er = a.errs + ((size_t)gid * a.cape + re) * ERR_WORDS;
+      er[0] = pj; er[1] = wl.he[4 * slot]; er[2] = wl.he[4 * slot + 1]; er[3] = wl.he[4 * slot + 2];
+      er[4] = wl.he[4 * slot + 3]; er[5] = 0;
+    }
+    nf += popc64(bf);
+    np += popc64(bp);
+    nerr += popc64(be);
   }
   if (lane == 0) {
     const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);
