@@ -1229,7 +1229,8 @@ __device__ __forceinline__ uint2 key_comp(uint32_t kc, uint32_t j, uint32_t st, 
                                           uint32_t off) {
   if (kc == KC_WILD) return make_uint2(KW_ANY, KW_ANY);
   if (kc == KC_TYPE) return make_uint2(st, KW_ANY);
-  return j ? make_uint2(blk[off + 2 * (j - 1)], blk[off + 2 * (j - 1) + 1]) : make_uint2(st, si);
+  return j ? make_uint2(__builtin_nontemporal_load(blk + off + 2 * (j - 1)), __builtin_nontemporal_load(blk + off + 2 * (j - 1) + 1))
+           : make_uint2(st, si);
 }
 
 // probe: (first, count, hmask) of the slot matching key words w0..w6 (+ v0, v1 for level 2)
@@ -1257,9 +1258,13 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   if (gid >= a.n_req) return;  // whole wave; this kernel has no block barriers
   const uint32_t r = a.req_idx ? uni(a.req_idx[gid]) : gid;
   const uint32_t* row = a.rows + (size_t)r * a.row_words;
+  // the request row streams through once: one coalesced non-temporal load (lanes 0..15 the
+  // header, lanes 16.. the hot slots), broadcast with readlane, so it does not evict the image
+  const uint32_t rw = lane < a.row_words ? __builtin_nontemporal_load(row + lane) : 0u;
+  auto hdr = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)rw, (int)k); };
 
   PCtx c;
-  c.blk = a.heap + uni(row[RW_BLK]);
+  c.blk = a.heap + hdr(RW_BLK);
   c.cpool = a.cpool;
   c.lh = wl.he;  // atoms never address lane scratch (any valid pointer)
   c.gstr_off = a.gstr_off;
@@ -1268,13 +1273,21 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   c.bstr_bytes = a.bstr_bytes;
   c.n_gstr = a.n_gstr;
   c.hotl = wl.hot;
-  c.pt = uni(row[RW_P]); c.pi = uni(row[RW_P + 1]);
-  c.at = uni(row[RW_A]); c.ai = uni(row[RW_A + 1]);
-  c.rt = uni(row[RW_R]); c.ri = uni(row[RW_R + 1]);
-  c.p_anc = uni(row[RW_PANC]); c.p_nanc = uni(row[RW_PN]);
-  c.r_anc = uni(row[RW_RANC]); c.r_nanc = uni(row[RW_RN]);
-  c.a_anc = uni(row[RW_AANC]); c.a_nanc = uni(row[RW_AN]);
-  if (lane < a.n_hot) wl.hot[lane] = make_uint2(row[RW_HDR + 2 * lane], row[RW_HDR + 2 * lane + 1]);
+  c.pt = hdr(RW_P); c.pi = hdr(RW_P + 1);
+  c.at = hdr(RW_A); c.ai = hdr(RW_A + 1);
+  c.rt = hdr(RW_R); c.ri = hdr(RW_R + 1);
+  c.p_anc = hdr(RW_PANC); c.p_nanc = hdr(RW_PN);
+  c.r_anc = hdr(RW_RANC); c.r_nanc = hdr(RW_RN);
+  c.a_anc = hdr(RW_AANC); c.a_nanc = hdr(RW_AN);
+  {  // hot slots: row words RW_HDR.. (lanes RW_HDR.. already hold the first 48 of them)
+    const uint32_t w0 = __shfl(rw, (int)(RW_HDR + 2 * (lane & 31))), w1 = __shfl(rw, (int)(RW_HDR + 2 * (lane & 31) + 1));
+    if (lane < a.n_hot) {
+      const bool in_reg = RW_HDR + 2 * lane + 1 < 64;
+      wl.hot[lane] = in_reg ? make_uint2(w0, w1)
+                            : make_uint2(__builtin_nontemporal_load(row + RW_HDR + 2 * lane),
+                                         __builtin_nontemporal_load(row + RW_HDR + 2 * lane + 1));
+    }
+  }
   // action masks over the image action table: lane k tests action k (`==` and `in`)
   uint32_t am0 = 0, am1 = 0, as0 = 0, as1 = 0;
   if (a.amask_ok) {
@@ -1495,8 +1508,8 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
     const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
     // the deciding list is the forbids if any forbid is satisfied at all: decided after the loop,
     // so both lists are written (their capacities are separate) and only one is read back
-    if (el && kind == 1 && rf < a.capr) a.reasons_f[(size_t)gid * a.capr + rf] = pj;
-    if (el && kind == 0 && rp < a.capr) a.reasons_p[(size_t)gid * a.capr + rp] = pj;
+    if (el && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rf);
+    if (el && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_p + (size_t)gid * a.capr + rp);
     if (el && kind == 2 && re < a.cape) {
       uint32_t* er = a.errs + ((size_t)gid * a.cape + re) * ERR_WORDS;
       er[0] = pj; er[1] = wl.he[4 * slot]; er[2] = wl.he[4 * slot + 1]; er[3] = wl.he[4 * slot + 2];
