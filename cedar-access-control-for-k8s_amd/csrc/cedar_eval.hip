@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -1163,8 +1164,6 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
 // Structural (set / record) equality is left to the stream kernel: such a request is flagged
 // RF_OVERFLOW and the host re-runs it there (rare: templates compare primitives).
 constexpr uint32_t WAVES = BLOCK / 64;
-constexpr uint32_t HCAP = 256;  // hits per request staged in LDS; more -> re-run on the stream kernel
-constexpr uint32_t ECAP = 128;  // found buckets staged before their candidates run
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -1185,15 +1184,21 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
   return x;
 }
 
-struct WaveLds {
-  uint32_t efirst[ECAP];     // found bucket: first head index
-  uint32_t epre[ECAP + 1];   // candidate counts, then their exclusive prefix
-  uint32_t ecombo[ECAP];     // key combo of the bucket's level-1 key
-  uint32_t hp[HCAP];         // hit: global policy index
-  uint32_t hm[HCAP];         // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8
-  uint32_t hs[HCAP];         // merge: sort keys (policy index << 8 | hit slot)
-  uint32_t he[HCAP * 4];     // error words: code | aux << 8, k, et, ei
-  uint2 hot[NHOT];
+// Per-wave LDS of the probe kernel, one region per request segment of SEG lanes.
+template <uint32_t SEG>
+struct SegLds {
+  static constexpr uint32_t NS = 64 / SEG;     // requests per wave
+  static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : 32;  // staged buckets per request (>= 2 stages)
+  static constexpr uint32_t HC = 64;           // hits per request (more: re-run on the stream kernel)
+  static constexpr uint32_t XC = 16;           // error details per request
+  uint32_t efirst[NS][EC];   // found bucket: first head index
+  uint32_t epre[NS][EC + 1]; // candidate counts, then their exclusive prefix
+  uint32_t ecombo[NS][EC];   // key combo of the bucket's level-1 key
+  uint32_t hp[NS][HC];       // hit: global policy index
+  uint32_t hm[NS][HC];       // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
+  uint32_t hs[NS][HC];       // merge: sort keys (policy index << 8 | hit slot)
+  uint32_t he[NS][XC * 4];   // error details: code | aux << 8, k, et, ei
+  uint2 hot[NS][NHOT];
 };
 
 // Slim per-request context of the probe kernel (everything wave-uniform but the pointers' data).
@@ -1250,246 +1255,264 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
   }
 }
 
+// SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
+// (row -> level-1 probe -> level-2 probe -> head -> atom data) overlap. Collectives (ballot, scan,
+// min, broadcast) are segment-local; loops run while any segment of the wave has work.
+template <uint32_t SEG>
 __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
-  __shared__ WaveLds wl_all[WAVES];
+  using L = SegLds<SEG>;
+  constexpr uint32_t NS = L::NS;
+  __shared__ L wl_all[WAVES];
   const uint32_t lane = threadIdx.x & 63;
-  WaveLds& wl = wl_all[threadIdx.x >> 6];
-  const uint32_t gid = uni(blockIdx.x * WAVES + (threadIdx.x >> 6));
-  if (gid >= a.n_req) return;  // whole wave; this kernel has no block barriers
-  const uint32_t r = a.req_idx ? uni(a.req_idx[gid]) : gid;
+  L& wl = wl_all[threadIdx.x >> 6];
+  const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
+  const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
+  auto sballot = [&](bool p) -> uint64_t { return __ballot(p) & smask; };
+  auto sbcast = [&](uint32_t x, uint32_t k) -> uint32_t { return (uint32_t)__shfl((int)x, (int)(sbase + k)); };
+  auto smin = [&](uint32_t x) -> uint32_t {
+    for (uint32_t o = SEG / 2; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, (int)o));
+    return x;
+  };
+  auto sscan = [&](uint32_t x) -> uint32_t {  // inclusive prefix sum within the segment
+    for (uint32_t o = 1; o < SEG; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (sl >= o) x += y;
+    }
+    return x;
+  };
+  const uint32_t gid = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * NS + seg;
+  const bool valid = gid < a.n_req;
+  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0u;
   const uint32_t* row = a.rows + (size_t)r * a.row_words;
-  // the request row streams through once: one coalesced non-temporal load (lanes 0..15 the
-  // header, lanes 16.. the hot slots), broadcast with readlane, so it does not evict the image
-  const uint32_t rw = lane < a.row_words ? __builtin_nontemporal_load(row + lane) : 0u;
-  auto hdr = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)rw, (int)k); };
 
+  // the request row streams through once: non-temporal loads, header broadcast in the segment
+  const uint32_t rw = (valid && sl < RW_HDR) ? __builtin_nontemporal_load(row + sl) : 0u;
   PCtx c;
-  c.blk = a.heap + hdr(RW_BLK);
+  c.blk = a.heap + sbcast(rw, RW_BLK);
   c.cpool = a.cpool;
-  c.lh = wl.he;  // atoms never address lane scratch (any valid pointer)
+  c.lh = wl.he[seg];  // atoms never address lane scratch (any valid pointer)
   c.gstr_off = a.gstr_off;
   c.gstr_bytes = a.gstr_bytes;
   c.bstr_off = a.bstr_off;
   c.bstr_bytes = a.bstr_bytes;
   c.n_gstr = a.n_gstr;
-  c.hotl = wl.hot;
-  c.pt = hdr(RW_P); c.pi = hdr(RW_P + 1);
-  c.at = hdr(RW_A); c.ai = hdr(RW_A + 1);
-  c.rt = hdr(RW_R); c.ri = hdr(RW_R + 1);
-  c.p_anc = hdr(RW_PANC); c.p_nanc = hdr(RW_PN);
-  c.r_anc = hdr(RW_RANC); c.r_nanc = hdr(RW_RN);
-  c.a_anc = hdr(RW_AANC); c.a_nanc = hdr(RW_AN);
-  {  // hot slots: row words RW_HDR.. (lanes RW_HDR.. already hold the first 48 of them)
-    const uint32_t w0 = __shfl(rw, (int)(RW_HDR + 2 * (lane & 31))), w1 = __shfl(rw, (int)(RW_HDR + 2 * (lane & 31) + 1));
-    if (lane < a.n_hot) {
-      const bool in_reg = RW_HDR + 2 * lane + 1 < 64;
-      wl.hot[lane] = in_reg ? make_uint2(w0, w1)
-                            : make_uint2(__builtin_nontemporal_load(row + RW_HDR + 2 * lane),
-                                         __builtin_nontemporal_load(row + RW_HDR + 2 * lane + 1));
-    }
-  }
-  // action masks over the image action table: lane k tests action k (`==` and `in`)
-  uint32_t am0 = 0, am1 = 0, as0 = 0, as1 = 0;
+  c.hotl = wl.hot[seg];
+  c.pt = sbcast(rw, RW_P); c.pi = sbcast(rw, RW_P + 1);
+  c.at = sbcast(rw, RW_A); c.ai = sbcast(rw, RW_A + 1);
+  c.rt = sbcast(rw, RW_R); c.ri = sbcast(rw, RW_R + 1);
+  c.p_anc = sbcast(rw, RW_PANC); c.p_nanc = sbcast(rw, RW_PN);
+  c.r_anc = sbcast(rw, RW_RANC); c.r_nanc = sbcast(rw, RW_RN);
+  c.a_anc = sbcast(rw, RW_AANC); c.a_nanc = sbcast(rw, RW_AN);
+  for (uint32_t h = sl; h < a.n_hot; h += SEG)
+    wl.hot[seg][h] = valid ? make_uint2(__builtin_nontemporal_load(row + RW_HDR + 2 * h),
+                                        __builtin_nontemporal_load(row + RW_HDR + 2 * h + 1))
+                           : make_uint2(0u, 0u);
+  // action masks over the image action table (`==` and `in`), SEG actions per step
+  uint64_t am = 0, as = 0;
   if (a.amask_ok) {
-    const bool on = lane < a.n_act;
-    const uint32_t qt = on ? a.act[2 * lane] : 0u, qi = on ? a.act[2 * lane + 1] : 0u;
-    const bool self = on && c.at == qt && c.ai == qi;
-    const bool hit = self || (on && c.a_nanc && anc_scan(c.blk, c.a_anc, c.a_nanc, qt, qi));
-    const uint64_t m = __ballot(hit), ms = __ballot(self);
-    am0 = (uint32_t)m; am1 = (uint32_t)(m >> 32);
-    as0 = (uint32_t)ms; as1 = (uint32_t)(ms >> 32);
+    for (uint32_t k0 = 0; k0 < a.n_act; k0 += SEG) {
+      const uint32_t k = k0 + sl;
+      const bool on = valid && k < a.n_act;
+      const uint32_t qt = on ? a.act[2 * k] : 0u, qi = on ? a.act[2 * k + 1] : 0u;
+      const bool self = on && c.at == qt && c.ai == qi;
+      const bool hit = self || (on && c.a_nanc && anc_scan(c.blk, c.a_anc, c.a_nanc, qt, qi));
+      am |= (sballot(hit) >> sbase) << k0;
+      as |= (sballot(self) >> sbase) << k0;
+    }
   }
   wave_lds_sync();
 
-  uint32_t min_tier = a.n_tiers - 1;  // lowest tier with a hit so far (uniform)
-  uint32_t nh = 0;                    // hits recorded (uniform; may exceed HCAP)
-  uint32_t ne = 0;                    // found buckets staged (uniform)
+  uint32_t min_tier = a.n_tiers - 1;  // lowest tier with a hit so far (segment-uniform)
+  uint32_t nh = 0, nx = 0;            // hits / error details recorded (may exceed capacity)
+  uint32_t ne = 0;                    // found buckets staged
   bool general = false;               // needs the stream kernel (structural equality)
 
-  // One loop, so that the candidate stage below is emitted once: each iteration stages the
-  // buckets found by one level-1 chunk (lane k probes key k) or one level-2 round (lane k probes
-  // the next hot slot of its level-1 entry's hmask), and runs the stage when it is nearly full or
-  // when the keys are exhausted.
   const uint32_t cm = a.combo_mask;
   const uint32_t nP = 1 + c.p_nanc, nA = 1 + c.a_nanc, nR = 1 + c.r_nanc;
   uint32_t n_keys = 0;
-  for (uint32_t m = cm; m; m &= m - 1) {
-    const uint32_t cb = __builtin_ctz(m);
-    n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
-  }
+  if (valid)
+    for (uint32_t m = cm; m; m &= m - 1) {
+      const uint32_t cb = __builtin_ctz(m);
+      n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+    }
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   for (;;) {
-    const bool l2 = __ballot(hm != 0) != 0;
+    const bool l2 = sballot(hm != 0) != 0;
     const bool done = !l2 && kb >= n_keys;
-    if (!done) {
+    const bool all_done = __ballot(!done) == 0;
+    if (!all_done) {
       uint3 e = make_uint3(0, 0, 0);
-      if (l2) {
-        if (hm) {
-          const uint32_t h = __builtin_ctz(hm);
-          hm &= hm - 1;
-          const uint2 v = wl.hot[h];
-          const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
-          e = probe(a.btab, a.bmask, bucket_hash2(h1, h, v0, v1), w0 | BT_L2 | h, kp, ka, kr, v0, v1);
-        }
-      } else {
-        const uint32_t k = kb + lane;
-        kb += 64;
-        uint32_t j = k;
-        bool found = false;
-        for (uint32_t m = cm; m; m &= m - 1) {
-          const uint32_t cb = __builtin_ctz(m);
-          const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
-          if (!found) {
-            if (j < cnt) { combo = cb; found = true; }
-            else j -= cnt;
+      if (!done) {
+        if (l2) {
+          if (hm) {
+            const uint32_t h = __builtin_ctz(hm);
+            hm &= hm - 1;
+            const uint2 v = wl.hot[seg][h];
+            const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
+            e = probe(a.btab, a.bmask, bucket_hash2(h1, h, v0, v1), w0 | BT_L2 | h, kp, ka, kr, v0, v1);
+          }
+        } else {
+          const uint32_t k = kb + sl;
+          kb += SEG;
+          uint32_t j = k;
+          bool found = false;
+          for (uint32_t m = cm; m; m &= m - 1) {
+            const uint32_t cb = __builtin_ctz(m);
+            const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+            if (!found) {
+              if (j < cnt) { combo = cb; found = true; }
+              else j -= cnt;
+            }
+          }
+          if (k < n_keys) {
+            const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
+            const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
+            const uint32_t ip = j % np_, t2 = j / np_, ia = t2 % na_, ir = t2 / na_;
+            kp = key_comp(pkc, ip, c.pt, c.pi, c.blk, c.p_anc);
+            ka = key_comp(akc, ia, c.at, c.ai, c.blk, c.a_anc);
+            kr = key_comp(rkc, ir, c.rt, c.ri, c.blk, c.r_anc);
+            w0 = BT_USED | (combo << 16);
+            h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
+            e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0);
+            hm = e.z;
           }
         }
-        if (k < n_keys) {
-          const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
-          const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
-          const uint32_t ip = j % np_, t2 = j / np_, ia = t2 % na_, ir = t2 / na_;
-          kp = key_comp(pkc, ip, c.pt, c.pi, c.blk, c.p_anc);
-          ka = key_comp(akc, ia, c.at, c.ai, c.blk, c.a_anc);
-          kr = key_comp(rkc, ir, c.rt, c.ri, c.blk, c.r_anc);
-          w0 = BT_USED | (combo << 16);
-          h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
-          e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0);
-          hm = e.z;
-        }
       }
-      // stage this lane's found bucket
-      const uint64_t m = __ballot(e.y != 0);
+      // stage this lane's found bucket in its segment
+      const uint64_t m = sballot(e.y != 0);
       if (e.y) {
         const uint32_t pos = ne + mbcnt64(m);
-        wl.efirst[pos] = e.x;
-        wl.epre[pos] = e.y;
-        wl.ecombo[pos] = combo;
+        wl.efirst[seg][pos] = e.x;
+        wl.epre[seg][pos] = e.y;
+        wl.ecombo[seg][pos] = combo;
       }
       ne += popc64(m);
       wave_lds_sync();
     }
-    if (done || ne + 64 > ECAP) {
-      // ---- run the staged buckets' candidates ----
-        uint32_t carry = 0;
-        for (uint32_t b0 = 0; b0 < ne; b0 += 64) {
-          const uint32_t b = b0 + lane;
-          const uint32_t cnt = b < ne ? wl.epre[b] : 0u;
-          const uint32_t inc = wave_scan(cnt, lane);
-          wave_lds_sync();
-          if (b < ne) wl.epre[b] = carry + inc - cnt;
-          carry += __shfl(inc, 63);
-          wave_lds_sync();
+    if (all_done || __ballot(ne + SEG > L::EC)) {
+      // ---- run every segment's staged buckets ----
+      uint32_t carry = 0;
+      for (uint32_t b0 = 0; __ballot(b0 < ne); b0 += SEG) {
+        const uint32_t b = b0 + sl;
+        const uint32_t cnt = b < ne ? wl.epre[seg][b] : 0u;
+        const uint32_t inc = sscan(cnt);
+        wave_lds_sync();
+        if (b < ne) wl.epre[seg][b] = carry + inc - cnt;
+        carry += sbcast(inc, SEG - 1);
+        wave_lds_sync();
+      }
+      const uint32_t total = carry;
+      for (uint32_t base = 0; __ballot(base < total); base += SEG) {
+        const uint32_t idx = base + sl;
+        bool ok = idx < total;
+        uint32_t lo = 0, hi = ne;  // bucket of candidate idx: last b with epre[b] <= idx
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (wl.epre[seg][mid] <= idx) lo = mid;
+          else hi = mid;
         }
-        const uint32_t total = uni(carry);
-        for (uint32_t base = 0; base < total; base += 64) {
-          const uint32_t idx = base + lane;
-          bool ok = idx < total;
-          uint32_t lo = 0, hi = ne;  // bucket of candidate idx: last b with epre[b] <= idx
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (wl.epre[mid] <= idx) lo = mid;
-            else hi = mid;
-          }
-          const uint32_t hidx = ok ? wl.efirst[lo] + (idx - wl.epre[lo]) : 0u;
-          const uint32_t combo = wl.ecombo[lo];
-          const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
-          const uint4* d4 = reinterpret_cast<const uint4*>(head);
-          const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
-          const uint32_t flags = q0.x, kinds = q0.y;
-          const uint32_t tier = (flags >> 8) & 0xFF;
-          ok = ok && tier <= min_tier;
-          const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
-          // scope re-check; an `in` / `is in` entity matched by the bucket key's entity component
-          // holds already (the request enumerated that key from its ancestor-or-self list)
-          if (ak != SK_ANY) {
-            if (a.amask_ok) {
-              ok = ok && (ak == SK_EQ ? (((as0 & q3.z) | (as1 & q3.w)) != 0) : (((am0 & q3.z) | (am1 & q3.w)) != 0));
-            } else if (ak == SK_EQ) {
-              ok = ok && c.at == q1.y && c.ai == q1.z;
-            } else if (ak == SK_IN) {
-              ok = ok && anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, q1.y, q1.z);
-            } else if (((combo >> 2) & 1) != KC_ENT) {
-              bool any = false;
-              for (uint32_t x = 0; ok && x < q1.y && !any; x++)
-                any = anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, a.cpool[q1.z + 2 * x], a.cpool[q1.z + 2 * x + 1]);
-              ok = ok && any;
-            }
-          }
-          if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
-          if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
-          else if ((pk == SK_IN || pk == SK_ISIN) && (combo & 3) != KC_ENT)
-            ok = ok && anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, q0.w, q1.x);
-          if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
-          if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
-          else if ((rk == SK_IN || rk == SK_ISIN) && (combo >> 3) != KC_ENT)
-            ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
-          // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
-          // atom data in the policy's full record at PW_EXT)
-          const uint32_t na = q3.x / ATOM_WORDS;
-          const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
-          uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
-          bool err = false;
-          Err e{0, 0, 0, 0, 0};
-          while (__ballot(pc < na)) {
-            if (pc < na) {
-              const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
-              const uint32_t rr = eval_atom<false>(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
-              if (rr == 3u) { general = true; pc = AT_UNSAT; }
-              else if (rr == 2u) { err = true; pc = AT_UNSAT; }
-              else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
-            }
-          }
-          // record hits
-          const bool hit = ok && (err || pc == AT_SAT);
-          const uint64_t hmask = __ballot(hit);
-          if (hmask) {
-            if (hit) {
-              const uint32_t pos = nh + mbcnt64(hmask);
-              if (pos < HCAP) {
-                wl.hp[pos] = q2.z;  // PW_CODE: global policy index
-                wl.hm[pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8);
-                if (err) {
-                  wl.he[4 * pos] = e.code | (e.aux << 8);
-                  wl.he[4 * pos + 1] = e.k;
-                  wl.he[4 * pos + 2] = e.et;
-                  wl.he[4 * pos + 3] = e.ei;
-                }
-              }
-            }
-            nh += popc64(hmask);
-            min_tier = min(min_tier, wave_min(hit ? tier : 0xFFu));
+        const uint32_t hidx = ok ? wl.efirst[seg][lo] + (idx - wl.epre[seg][lo]) : 0u;
+        const uint32_t bcombo = ok ? wl.ecombo[seg][lo] : 0u;
+        const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
+        const uint4* d4 = reinterpret_cast<const uint4*>(head);
+        const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+        const uint32_t flags = q0.x, kinds = q0.y;
+        const uint32_t tier = (flags >> 8) & 0xFF;
+        ok = ok && tier <= min_tier;
+        const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
+        // scope re-check; an `in` / `is in` entity matched by the bucket key's entity component
+        // holds already (the request enumerated that key from its ancestor-or-self list)
+        if (ak != SK_ANY) {
+          if (a.amask_ok) {
+            const uint64_t pm = ((uint64_t)q3.w << 32) | q3.z;
+            ok = ok && (((ak == SK_EQ ? as : am) & pm) != 0);
+          } else if (ak == SK_EQ) {
+            ok = ok && c.at == q1.y && c.ai == q1.z;
+          } else if (ak == SK_IN) {
+            ok = ok && anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, q1.y, q1.z);
+          } else if (((bcombo >> 2) & 1) != KC_ENT) {
+            bool any = false;
+            for (uint32_t x = 0; ok && x < q1.y && !any; x++)
+              any = anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, a.cpool[q1.z + 2 * x], a.cpool[q1.z + 2 * x + 1]);
+            ok = ok && any;
           }
         }
+        if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
+        if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
+        else if ((pk == SK_IN || pk == SK_ISIN) && (bcombo & 3) != KC_ENT)
+          ok = ok && anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, q0.w, q1.x);
+        if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
+        if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
+        else if ((rk == SK_IN || rk == SK_ISIN) && (bcombo >> 3) != KC_ENT)
+          ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
+        // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
+        // atom data in the policy's full record at PW_EXT)
+        const uint32_t na = q3.x / ATOM_WORDS;
+        const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
+        uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
+        bool err = false;
+        Err e{0, 0, 0, 0, 0};
+        while (__ballot(pc < na)) {
+          if (pc < na) {
+            const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
+            const uint32_t rr = eval_atom<false>(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
+            if (rr == 3u) { general = true; pc = AT_UNSAT; }
+            else if (rr == 2u) { err = true; pc = AT_UNSAT; }
+            else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
+          }
+        }
+        // record hits (segment-local slots)
+        const bool hit = ok && (err || pc == AT_SAT);
+        const uint64_t hmask = sballot(hit), xmask = sballot(hit && err);
+        if (hit) {
+          const uint32_t pos = nh + mbcnt64(hmask);
+          const uint32_t xpos = nx + mbcnt64(xmask);
+          if (pos < L::HC) {
+            wl.hp[seg][pos] = q2.z;  // PW_CODE: global policy index
+            wl.hm[seg][pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8) | (min(xpos, 0xFFu) << 16);
+          }
+          if (err && xpos < L::XC) {
+            wl.he[seg][4 * xpos] = e.code | (e.aux << 8);
+            wl.he[seg][4 * xpos + 1] = e.k;
+            wl.he[seg][4 * xpos + 2] = e.et;
+            wl.he[seg][4 * xpos + 3] = e.ei;
+          }
+        }
+        nh += popc64(hmask);
+        nx += popc64(xmask);
+        min_tier = min(min_tier, smin(hit ? tier : 0xFFu));
+      }
       ne = 0;
       wave_lds_sync();
     }
-    if (done) break;
+    if (all_done) break;
   }
 
-  // ---- merge: deciding tier, duplicates, policy order (hits in chunks of 64 lanes) ----
+  // ---- merge: deciding tier, duplicates, policy order ----
   const uint32_t t = min_tier;
-  if (nh > HCAP || __ballot(general)) {
-    if (lane == 0) {
-      a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | RF_GENERAL) << 16);
-      a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
-    }
-    return;
+  const bool undecided = nh > L::HC || nx > L::XC || sballot(general) != 0;
+  if (valid && undecided && sl == 0) {
+    a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | RF_GENERAL) << 16);
+    a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
   }
-  // bitonic sort of (policy index << 8 | slot) over the next power of two >= nh (<= HCAP)
-  uint32_t m = 2;
-  while (m < nh) m <<= 1;
-  for (uint32_t i = lane; i < m; i += 64) wl.hs[i] = i < nh ? ((wl.hp[i] << 8) | i) : 0xFFFFFFFFu;
+  const uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge
+  // bitonic sort of (policy index << 8 | slot) over the wave's largest power of two >= nh
+  uint32_t mloc = 2;
+  while (mloc < nhm) mloc <<= 1;
+  uint32_t m = mloc;
+  for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
+  for (uint32_t i = sl; i < m; i += SEG) wl.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 8) | i) : 0xFFFFFFFFu;
   wave_lds_sync();
   for (uint32_t k = 2; k <= m; k <<= 1) {
     for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i0 = 0; i0 < (m >> 1); i0 += 64) {
-        const uint32_t q = i0 + lane;  // compare-exchange pair q
+      for (uint32_t i0 = 0; i0 < (m >> 1); i0 += SEG) {
+        const uint32_t q = i0 + sl;  // compare-exchange pair q
         if (q < (m >> 1)) {
           const uint32_t lo = ((q / jj) * 2 * jj) + (q % jj), hi = lo + jj;
-          const uint32_t x = wl.hs[lo], y = wl.hs[hi];
+          const uint32_t x = wl.hs[seg][lo], y = wl.hs[seg][hi];
           const bool up = (lo & k) == 0;
-          if ((x > y) == up) { wl.hs[lo] = y; wl.hs[hi] = x; }
+          if ((x > y) == up) { wl.hs[seg][lo] = y; wl.hs[seg][hi] = x; }
         }
       }
       wave_lds_sync();
@@ -1497,29 +1520,29 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   }
   // deciding-tier hits, duplicates (adjacent after the sort) dropped; ranks by prefix counts
   uint32_t nf = 0, np = 0, nerr = 0;
-  for (uint32_t c0 = 0; c0 < nh; c0 += 64) {
-    const uint32_t i = c0 + lane;
-    const uint32_t key = i < nh ? wl.hs[i] : 0xFFFFFFFFu;
+  for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
+    const uint32_t i = c0 + sl;
+    const bool have = i < nhm;
+    const uint32_t key = have ? wl.hs[seg][i] : 0xFFFFFFFFu;
     const uint32_t slot = key & 0xFF, pj = key >> 8;
-    const uint32_t mj = i < nh ? wl.hm[slot] : 0u;
+    const uint32_t mj = have ? wl.hm[seg][slot] : 0u;
     const uint32_t kind = mj & 0xFF;
-    const bool el = i < nh && (mj >> 8) == t && (i == 0 || (wl.hs[i - 1] >> 8) != pj);
-    const uint64_t bf = __ballot(el && kind == 1), bp = __ballot(el && kind == 0), be = __ballot(el && kind == 2);
+    const bool el = have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.hs[seg][i - 1] >> 8) != pj);
+    const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
     const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
-    // the deciding list is the forbids if any forbid is satisfied at all: decided after the loop,
-    // so both lists are written (their capacities are separate) and only one is read back
     if (el && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rf);
     if (el && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_p + (size_t)gid * a.capr + rp);
     if (el && kind == 2 && re < a.cape) {
+      const uint32_t xs = mj >> 16;
       uint32_t* er = a.errs + ((size_t)gid * a.cape + re) * ERR_WORDS;
-      er[0] = pj; er[1] = wl.he[4 * slot]; er[2] = wl.he[4 * slot + 1]; er[3] = wl.he[4 * slot + 2];
-      er[4] = wl.he[4 * slot + 3]; er[5] = 0;
+      er[0] = pj; er[1] = wl.he[seg][4 * xs]; er[2] = wl.he[seg][4 * xs + 1]; er[3] = wl.he[seg][4 * xs + 2];
+      er[4] = wl.he[seg][4 * xs + 3]; er[5] = 0;
     }
     nf += popc64(bf);
     np += popc64(bp);
     nerr += popc64(be);
   }
-  if (lane == 0) {
+  if (valid && !undecided && sl == 0) {
     const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);
     const uint32_t nr = nf ? nf : np;
     uint32_t fl = RF_VALID | (nf ? RF_FORBID : 0u);
@@ -1767,9 +1790,28 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
 
 // Launches the evaluation of n requests: the request-per-wave kernel over the scope index when the
 // image is fully indexed, else the request-per-lane policy-stream kernel.
+// Probe-kernel segment width (lanes per request): 16 by default; CEDARGPU_PROBE_SEG=32 / 64 for
+// comparisons.
+static uint32_t probe_seg() {
+  static const uint32_t seg = [] {
+    const char* e = std::getenv("CEDARGPU_PROBE_SEG");
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : 16u;
+    return (v == 32u || v == 64u) ? v : 16u;
+  }();
+  return seg;
+}
+
+static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s) {
+  const uint32_t seg = probe_seg(), per_block = WAVES * (64 / seg);
+  const dim3 grid((n + per_block - 1) / per_block);
+  if (seg == 16) hipLaunchKernelGGL(cedar_probe_kernel<16>, grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 32) hipLaunchKernelGGL(cedar_probe_kernel<32>, grid, dim3(BLOCK), 0, s, k);
+  else hipLaunchKernelGGL(cedar_probe_kernel<64>, grid, dim3(BLOCK), 0, s, k);
+}
+
 static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
   if (img.indexed)
-    hipLaunchKernelGGL(cedar_probe_kernel, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
+    launch_probe(k, n, s);
   else
     hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>,
                        dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
@@ -1807,7 +1849,7 @@ int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx,
     if ((e = hipMemcpyAsync(d_idx, idx, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) { rc = fail(e, "H2D"); break; }
     KArgs k = make_args(img, b, d_idx, n, d_res, d_rf, d_rp, d_er, capr, cape);
     if (probe && img.indexed)
-      hipLaunchKernelGGL(cedar_probe_kernel, dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
+      launch_probe(k, n, s);
     else
       hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
     if ((e = hipGetLastError()) != hipSuccess) { rc = fail(e, "launch"); break; }
