@@ -432,8 +432,8 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   // re-run there with the exact capacities; requests it could not decide (RF_GENERAL) and any
   // stream-kernel overflow re-run on the stream kernel, which reports exact counts, so a second
   // pass with those capacities completes it.
-  std::vector<uint32_t> idx_probe, idx_gen;
-  uint32_t capr_p = 0, cape_p = 0, capr_g = 0, cape_g = 0;
+  std::vector<uint32_t> idx_probe, idx_big, idx_gen;
+  uint32_t capr_p = 0, cape_p = 0, capr_b = 0, cape_b = 0, capr_g = 0, cape_g = 0;
   for (uint32_t i = 0; i < b->host.n(); i++) {
     uint32_t fl = b->host.res[2 * (size_t)i] >> 16;
     if (!(fl & cgi::RF_VALID)) { b->err = "request left unevaluated"; return CG_E_DEVICE; }
@@ -441,16 +441,20 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     const uint32_t nr = b->host.res[2 * (size_t)i + 1] & 0xFFFF, ne = b->host.res[2 * (size_t)i + 1] >> 16;
     if ((fl & cgi::RF_GENERAL) || !b->img->dev.indexed) {
       idx_gen.push_back(i); capr_g = std::max(capr_g, nr); cape_g = std::max(cape_g, ne);
+    } else if (fl & cgi::RF_BIG) {
+      idx_big.push_back(i); capr_b = std::max(capr_b, nr); cape_b = std::max(cape_b, ne);
     } else {
       idx_probe.push_back(i); capr_p = std::max(capr_p, nr); cape_p = std::max(cape_p, ne);
     }
   }
-  auto rerun = [&](std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, bool probe) -> int {
+  // re-runs a subset (mode: 1 probe kernel, 2 its large-stage variant, 0 stream kernel); requests
+  // a probe re-run cannot decide move on to the next mode
+  auto rerun = [&](std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, int mode, std::vector<uint32_t>& next) -> int {
     for (int pass = 0; pass < 3 && !idx.empty(); pass++) {
       capr = std::max(std::min(capr, 4096u), 8u);
       cape = std::max(std::min(cape, 4096u), 4u);
       std::vector<uint32_t> res, rf, rp, er;
-      if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, probe, b->ctx->stream, res, rf, rp, er)) {
+      if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->stream, res, rf, rp, er)) {
         b->err = dev_last_error();
         return CG_E_DEVICE;
       }
@@ -460,6 +464,7 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
         uint32_t i = idx[k];
         uint32_t fl = res[2 * k] >> 16;
         uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
+        if (mode && (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) { next.push_back(i); continue; }
         if (fl & cgi::RF_OVERFLOW) {
           again.push_back(i);
           capr2 = std::max(capr2, nr);
@@ -479,20 +484,18 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     if (!idx.empty()) { b->err = "result lists exceed the device re-run capacity"; return CG_E_RANGE; }
     return CG_OK;
   };
-  if (!idx_probe.empty()) {
-    // a probe re-run can still find RF_GENERAL requests: those move to the stream kernel
-    int rc = rerun(idx_probe, capr_p, cape_p, true);
-    if (rc == CG_E_RANGE) {
-      for (uint32_t i : idx_probe) idx_gen.push_back(i);
-      capr_g = std::max(capr_g, 64u);
-      cape_g = std::max(cape_g, 64u);
-    } else if (rc) {
-      return rc;
-    }
+  int rc;
+  if (!idx_probe.empty() && (rc = rerun(idx_probe, capr_p, cape_p, 1, idx_big))) return rc;
+  if (!idx_big.empty()) {
+    capr_b = std::max(capr_b, 64u);
+    cape_b = std::max(cape_b, 16u);
+    if ((rc = rerun(idx_big, capr_b, cape_b, 2, idx_gen))) return rc;
   }
   if (!idx_gen.empty()) {
-    int rc = rerun(idx_gen, capr_g, cape_g, false);
-    if (rc) return rc;
+    capr_g = std::max(capr_g, 64u);
+    cape_g = std::max(cape_g, 16u);
+    std::vector<uint32_t> none;
+    if ((rc = rerun(idx_gen, capr_g, cape_g, 0, none))) return rc;
   }
   b->done = true;
   return CG_OK;

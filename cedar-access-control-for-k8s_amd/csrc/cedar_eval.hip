@@ -1185,12 +1185,12 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
 }
 
 // Per-wave LDS of the probe kernel, one region per request segment of SEG lanes.
-template <uint32_t SEG>
+template <uint32_t SEG, uint32_t HCAP>
 struct SegLds {
   static constexpr uint32_t NS = 64 / SEG;     // requests per wave
   static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : 32;  // staged buckets per request (>= 2 stages)
-  static constexpr uint32_t HC = 64;           // hits per request (more: re-run on the stream kernel)
-  static constexpr uint32_t XC = 16;           // error details per request
+  static constexpr uint32_t HC = HCAP;         // hits per request (more: RF_BIG / RF_GENERAL re-run)
+  static constexpr uint32_t XC = HCAP >= 256 ? 64 : 16;  // error details per request
   uint32_t efirst[NS][EC];   // found bucket: first head index
   uint32_t epre[NS][EC + 1]; // candidate counts, then their exclusive prefix
   uint32_t ecombo[NS][EC];   // key combo of the bucket's level-1 key
@@ -1258,9 +1258,10 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
 // SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
 // (row -> level-1 probe -> level-2 probe -> head -> atom data) overlap. Collectives (ballot, scan,
 // min, broadcast) are segment-local; loops run while any segment of the wave has work.
-template <uint32_t SEG>
+template <uint32_t SEG, uint32_t HCAP>
 __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
-  using L = SegLds<SEG>;
+  using L = SegLds<SEG, HCAP>;
+  static_assert(L::HC <= 4096 && L::XC <= 255, "hit slots are 12-bit sort payloads, error slots 8-bit");
   constexpr uint32_t NS = L::NS;
   __shared__ L wl_all[WAVES];
   const uint32_t lane = threadIdx.x & 63;
@@ -1491,9 +1492,11 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
 
   // ---- merge: deciding tier, duplicates, policy order ----
   const uint32_t t = min_tier;
-  const bool undecided = nh > L::HC || nx > L::XC || sballot(general) != 0;
+  const bool structural = sballot(general) != 0;
+  const bool undecided = nh > L::HC || nx > L::XC || structural;
   if (valid && undecided && sl == 0) {
-    a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | RF_GENERAL) << 16);
+    const uint32_t why = (structural || L::HC >= 1024) ? RF_GENERAL : RF_BIG;
+    a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | why) << 16);
     a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
   }
   const uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge
@@ -1502,7 +1505,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
   while (mloc < nhm) mloc <<= 1;
   uint32_t m = mloc;
   for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
-  for (uint32_t i = sl; i < m; i += SEG) wl.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 8) | i) : 0xFFFFFFFFu;
+  for (uint32_t i = sl; i < m; i += SEG) wl.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
   wave_lds_sync();
   for (uint32_t k = 2; k <= m; k <<= 1) {
     for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
@@ -1524,10 +1527,10 @@ __global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
     const uint32_t i = c0 + sl;
     const bool have = i < nhm;
     const uint32_t key = have ? wl.hs[seg][i] : 0xFFFFFFFFu;
-    const uint32_t slot = key & 0xFF, pj = key >> 8;
+    const uint32_t slot = key & 0xFFF, pj = key >> 12;
     const uint32_t mj = have ? wl.hm[seg][slot] : 0u;
     const uint32_t kind = mj & 0xFF;
-    const bool el = have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.hs[seg][i - 1] >> 8) != pj);
+    const bool el = have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.hs[seg][i - 1] >> 12) != pj);
     const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
     const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
     if (el && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rf);
@@ -1801,12 +1804,15 @@ static uint32_t probe_seg() {
   return seg;
 }
 
-static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s) {
-  const uint32_t seg = probe_seg(), per_block = WAVES * (64 / seg);
+// big: the re-run variant for requests with more hits than the default stage (one request per
+// wave, 1024 hits staged)
+static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
+  const uint32_t seg = big ? 64u : probe_seg(), per_block = WAVES * (64 / seg);
   const dim3 grid((n + per_block - 1) / per_block);
-  if (seg == 16) hipLaunchKernelGGL(cedar_probe_kernel<16>, grid, dim3(BLOCK), 0, s, k);
-  else if (seg == 32) hipLaunchKernelGGL(cedar_probe_kernel<32>, grid, dim3(BLOCK), 0, s, k);
-  else hipLaunchKernelGGL(cedar_probe_kernel<64>, grid, dim3(BLOCK), 0, s, k);
+  if (big) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 16) hipLaunchKernelGGL((cedar_probe_kernel<16, 64>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 32) hipLaunchKernelGGL((cedar_probe_kernel<32, 64>), grid, dim3(BLOCK), 0, s, k);
+  else hipLaunchKernelGGL((cedar_probe_kernel<64, 64>), grid, dim3(BLOCK), 0, s, k);
 }
 
 static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
@@ -1830,7 +1836,7 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
 // Re-evaluates a subset of requests (overflowed result lists) with larger capacities; results are
 // compact in subset order and copied to host before returning.
 int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
-                    uint32_t cape, bool probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
+                    uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
                     std::vector<uint32_t>& rp, std::vector<uint32_t>& er) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
@@ -1849,7 +1855,7 @@ int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx,
     if ((e = hipMemcpyAsync(d_idx, idx, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) { rc = fail(e, "H2D"); break; }
     KArgs k = make_args(img, b, d_idx, n, d_res, d_rf, d_rp, d_er, capr, cape);
     if (probe && img.indexed)
-      launch_probe(k, n, s);
+      launch_probe(k, n, s, probe == 2);
     else
       hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
     if ((e = hipGetLastError()) != hipSuccess) { rc = fail(e, "launch"); break; }

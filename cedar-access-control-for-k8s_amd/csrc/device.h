@@ -52,10 +52,11 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
 void dev_batch_free(DevBatch* d);  // returns the blocks to the batch's pool
 // Evaluates every request of the batch into the batch's device result buffers (async on stream).
 int dev_eval(const DevImage& img, DevBatch& b, void* stream);
-// Re-evaluates the subset idx[0..n) with larger result capacities (probe: on the probe kernel, for
-// an indexed image; else the stream kernel); synchronous, results on host.
+// Re-evaluates the subset idx[0..n) with larger result capacities (probe 1: on the probe kernel,
+// 2: on its large-stage variant, for an indexed image; 0: the stream kernel); synchronous,
+// results on host.
 int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
-                    uint32_t cape, bool probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
+                    uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
                     std::vector<uint32_t>& rp, std::vector<uint32_t>& er);
 int dev_download(const DevBatch& b, Batch& host, void* stream);
 int dev_stream_create(int device, void** stream);

@@ -256,9 +256,10 @@ __host__ __device__ constexpr inline uint32_t mk_ins(uint32_t op, uint32_t d, ui
 enum Decision : uint32_t { DEC_DENY = 0, DEC_ALLOW = 1 };
 // res[2r]   = decision | tier << 8 | flags << 16
 // res[2r+1] = n_reasons | n_errors << 16
-// RF_GENERAL: the probe kernel could not decide the request (hits beyond its LDS stage, or a
-// structural set/record comparison); the host re-runs it on the stream kernel
-enum ResFlags : uint32_t { RF_FORBID = 1, RF_OVERFLOW = 2, RF_VALID = 4, RF_GENERAL = 8 };
+// RF_GENERAL: the probe kernel could not decide the request (a structural set/record
+// comparison, or hits beyond even the large re-run stage); the host re-runs it on the stream
+// kernel. RF_BIG: more hits than the probe kernel stages per request; re-run on its large variant.
+enum ResFlags : uint32_t { RF_FORBID = 1, RF_OVERFLOW = 2, RF_VALID = 4, RF_GENERAL = 8, RF_BIG = 16 };
 // error record: policy, code | aux << 8, k (string id), et (string id), ei (string id), pad
 constexpr uint32_t ERR_WORDS = 6;
 enum ErrCode : uint32_t {
