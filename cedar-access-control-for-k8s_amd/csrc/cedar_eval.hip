@@ -1841,32 +1841,41 @@ int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx,
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return 0;
+  if (!b.pool) { g_err = "batch has no buffer pool"; return -4; }
   for (uint32_t i = 0; i < n; i++) if (idx[i] >= b.n) { g_err = "request index out of range"; return -2; }
-  uint32_t *d_idx = nullptr, *d_res = nullptr, *d_rf = nullptr, *d_rp = nullptr, *d_er = nullptr;
-  int rc = 0;
-  auto cleanup = [&]() { for (void* p : {(void*)d_idx, (void*)d_res, (void*)d_rf, (void*)d_rp, (void*)d_er}) if (p) (void)hipFree(p); };
+  // one device block [idx | res | reasons_f | reasons_p | errs] and one pinned block, from the pool
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_idx = 0, o_res = al((size_t)n * 4), o_rf = o_res + al((size_t)n * 2 * 4),
+               o_rp = o_rf + al((size_t)n * capr * 4), o_er = o_rp + al((size_t)n * capr * 4),
+               total = o_er + al((size_t)n * cape * ERR_WORDS * 4);
+  void *dblk = nullptr, *hblk = nullptr;
+  size_t dcls = 0, hcls = 0;
+  int rc;
+  if ((rc = pool_get(b.pool, false, total, &dblk, &dcls))) return rc;
+  if ((rc = pool_get(b.pool, true, total, &hblk, &hcls))) { pool_put(b.pool, false, dblk, dcls); return rc; }
+  uint8_t* d8 = (uint8_t*)dblk;
+  uint8_t* h8 = (uint8_t*)hblk;
+  std::memcpy(h8 + o_idx, idx, (size_t)n * 4);
   do {
     hipError_t e;
-    if ((e = hipMalloc((void**)&d_idx, (size_t)n * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
-    if ((e = hipMalloc((void**)&d_res, (size_t)n * 2 * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
-    if ((e = hipMalloc((void**)&d_rf, (size_t)n * capr * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
-    if ((e = hipMalloc((void**)&d_rp, (size_t)n * capr * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
-    if ((e = hipMalloc((void**)&d_er, (size_t)n * cape * ERR_WORDS * 4)) != hipSuccess) { rc = fail(e, "hipMalloc"); break; }
-    if ((e = hipMemcpyAsync(d_idx, idx, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) { rc = fail(e, "H2D"); break; }
-    KArgs k = make_args(img, b, d_idx, n, d_res, d_rf, d_rp, d_er, capr, cape);
+    if ((e = hipMemcpyAsync(d8 + o_idx, h8 + o_idx, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) { rc = fail(e, "H2D"); break; }
+    KArgs k = make_args(img, b, (uint32_t*)(d8 + o_idx), n, (uint32_t*)(d8 + o_res), (uint32_t*)(d8 + o_rf),
+                        (uint32_t*)(d8 + o_rp), (uint32_t*)(d8 + o_er), capr, cape);
     if (probe && img.indexed)
       launch_probe(k, n, s, probe == 2);
     else
       hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
     if ((e = hipGetLastError()) != hipSuccess) { rc = fail(e, "launch"); break; }
-    res.resize((size_t)n * 2); rf.resize((size_t)n * capr); rp.resize((size_t)n * capr); er.resize((size_t)n * cape * ERR_WORDS);
-    if ((e = hipMemcpyAsync(res.data(), d_res, res.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
-    if ((e = hipMemcpyAsync(rf.data(), d_rf, rf.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
-    if ((e = hipMemcpyAsync(rp.data(), d_rp, rp.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
-    if ((e = hipMemcpyAsync(er.data(), d_er, er.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
+    if ((e = hipMemcpyAsync(h8 + o_res, d8 + o_res, total - o_res, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
     if ((e = hipStreamSynchronize(s)) != hipSuccess) { rc = fail(e, "sync"); break; }
+    res.assign((const uint32_t*)(h8 + o_res), (const uint32_t*)(h8 + o_res) + (size_t)n * 2);
+    rf.assign((const uint32_t*)(h8 + o_rf), (const uint32_t*)(h8 + o_rf) + (size_t)n * capr);
+    rp.assign((const uint32_t*)(h8 + o_rp), (const uint32_t*)(h8 + o_rp) + (size_t)n * capr);
+    er.assign((const uint32_t*)(h8 + o_er), (const uint32_t*)(h8 + o_er) + (size_t)n * cape * ERR_WORDS);
   } while (0);
-  cleanup();
+  if (rc) (void)hipStreamSynchronize(s);  // nothing of ours in flight before the blocks are reused
+  pool_put(b.pool, false, dblk, dcls);
+  pool_put(b.pool, true, hblk, hcls);
   return rc;
 }
 
