@@ -1258,8 +1258,8 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
 // SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
 // (row -> level-1 probe -> level-2 probe -> head -> atom data) overlap. Collectives (ballot, scan,
 // min, broadcast) are segment-local; loops run while any segment of the wave has work.
-template <uint32_t SEG, uint32_t HCAP>
-__global__ __launch_bounds__(BLOCK) void cedar_probe_kernel(KArgs a) {
+template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1>
+__global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
   using L = SegLds<SEG, HCAP>;
   static_assert(L::HC <= 4096 && L::XC <= 255, "hit slots are 12-bit sort payloads, error slots 8-bit");
   constexpr uint32_t NS = L::NS;
@@ -1806,10 +1806,24 @@ static uint32_t probe_seg() {
 
 // big: the re-run variant for requests with more hits than the default stage (one request per
 // wave, 1024 hits staged)
+// Minimum waves per SIMD the 16-lane kernel is register-allocated for (CEDARGPU_PROBE_OCC=4 / 5 for
+// comparisons; the allocator spills to scratch to meet them).
+static uint32_t probe_occ() {
+  static const uint32_t occ = [] {
+    const char* e = std::getenv("CEDARGPU_PROBE_OCC");
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : 1u;
+    return (v == 4u || v == 5u) ? v : 1u;
+  }();
+  return occ;
+}
+
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
   const uint32_t seg = big ? 64u : probe_seg(), per_block = WAVES * (64 / seg);
   const dim3 grid((n + per_block - 1) / per_block);
+  const uint32_t occ = probe_occ();
   if (big) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 16 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 16 && occ == 5) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16) hipLaunchKernelGGL((cedar_probe_kernel<16, 64>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 32) hipLaunchKernelGGL((cedar_probe_kernel<32, 64>), grid, dim3(BLOCK), 0, s, k);
   else hipLaunchKernelGGL((cedar_probe_kernel<64, 64>), grid, dim3(BLOCK), 0, s, k);
