@@ -92,6 +92,48 @@ def parity_sample(policies_text, items, idx, gpu_batch, threads):
     return {"requests": len(items), "mismatches": bad, "oracle": "oracle/cedar_ref.cpp"}
 
 
+def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=120.0):
+    """Policy hot reload after the timed region: rank 0 compiles epoch 2 (the policies plus one
+    forbid), one RCCL broadcast ships it to every GPU, each rank activates it and checks a request
+    the new forbid decides. Runs in a daemon thread with a deadline so that a stuck collective
+    cannot hang the benchmark; reports the broadcast+load+activate time."""
+    import threading
+
+    import cedargpu
+    from cedargpu import dist as cdist
+
+    out = {}
+
+    def run():
+        try:
+            uid = cdist.exchange_unique_id(rank) if dist_on else cdist.unique_id()
+            comm = cdist.Comm(device, world, rank, uid)
+            extra = 'forbid (principal, action == k8s::Action::"reload-check", resource);'
+            image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies + "\n" + extra)], epoch=2) if rank == 0 else None
+            t0 = time.perf_counter()
+            n = comm.broadcast_image(ctx, image, 2)
+            dt = time.perf_counter() - t0
+            b = ctx.batch()
+            b.add([], {"principal": {"type": "k8s::User", "id": "u"}, "action": {"type": "k8s::Action", "id": "reload-check"},
+                       "resource": {"type": "k8s::Resource", "id": "/api/v1/pods"}, "context": {}})
+            b.submit()
+            b.wait()
+            ok = b.decision(0)[0] is False and len(b.reasons(0)[0]) == 1
+            b.close()
+            comm.close()
+            out.update({"via": "rccl broadcast", "image_bytes": n, "ms": dt * 1e3, "ranks": world, "epoch": 2,
+                        "new_policy_applied": ok})
+        except Exception as e:  # reported, not fatal: the decision path does not depend on it
+            out["error"] = f"{type(e).__name__}: {e}"
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        return {"error": f"timed out after {timeout_s:.0f} s"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,6 +144,8 @@ def main():
     ap.add_argument("--variant", default="full", help="policy-shape study: full | scope-only | no-group | atomic-only")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-sample", type=int, default=2048)
+    ap.add_argument("--no-reload", dest="reload", action="store_false",
+                    help="skip the RCCL hot-reload check after the timed region")
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=200)
@@ -184,6 +228,7 @@ def main():
         lat.sort()
 
     parity = parity_sample(policies, items, idx, b, threads) if rank == 0 and items else None
+    reload = hot_reload(ctx, policies, rank, world, local, dist_on) if args.reload else None
 
     if rank == 0:
         ms_per_step = wall_s * 1e3 / args.steps
@@ -222,6 +267,7 @@ def main():
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": baseline,
             "parity_sample": parity,
+            "reload": reload,
             "latency": {"batch": args.latency_batch, "p50_ms": lat[len(lat) // 2] if lat else None,
                         "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
                         "max_ms": lat[-1] if lat else None, "batches": len(lat),

@@ -65,6 +65,11 @@ _SIGS = {
     "cg_image_activate": (ctypes.c_int, [P, u64]),
     "cg_image_active": (ctypes.c_int, [P, ctypes.POINTER(u64)]),
     "cg_image_unload": (ctypes.c_int, [P, u64]),
+    "cg_comm_unique_id": (ctypes.c_int, [P, sz]),
+    "cg_comm_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, sz, ctypes.POINTER(P)]),
+    "cg_comm_destroy": (None, [P]),
+    "cg_comm_last_error": (cstr, [P]),
+    "cg_broadcast_image": (ctypes.c_int, [P, P, ctypes.c_int, P, sz, u64, ctypes.c_int, ctypes.POINTER(sz)]),
     "cg_batch_create": (ctypes.c_int, [P, ctypes.POINTER(P)]),
     "cg_batch_destroy": (None, [P]),
     "cg_batch_add_json": (ctypes.c_int, [P, cstr, sz]),

@@ -39,6 +39,7 @@ extern "C" {
 typedef struct cg_compiler cg_compiler;
 typedef struct cg_ctx cg_ctx;
 typedef struct cg_batch cg_batch;
+typedef struct cg_comm cg_comm;
 
 const char* cg_version(void);
 void cg_free(void* p);
@@ -87,6 +88,20 @@ int cg_image_activate(cg_ctx* ctx, uint64_t epoch);
 int cg_image_active(cg_ctx* ctx, uint64_t* epoch);
 /* Drops a loaded image (no-op while batches still reference it; freed when the last one goes). */
 int cg_image_unload(cg_ctx* ctx, uint64_t epoch);
+
+/* ---- multi-GPU hot reload (RCCL over xGMI; no collective on the decision path) ----
+ * Requests shard across GPUs, each holding a replica of the image. On a policy reload (the
+ * reference swaps the PolicySet at store/directory.go:81, verified_permissions.go:99 and mutates it
+ * at crd.go:62,85,102,114) one rank compiles and cg_broadcast_image ships the blob to every GPU.
+ * cg_comm_unique_id: 128-byte RCCL id, made on one rank and shared out of band (cap >= 128). */
+int cg_comm_unique_id(uint8_t* out, size_t cap);
+int cg_comm_create(int device, int nranks, int rank, const uint8_t* id, size_t len, cg_comm** out);
+void cg_comm_destroy(cg_comm* comm);
+const char* cg_comm_last_error(cg_comm* comm);
+/* Collective over comm: root's image (len bytes) is broadcast; every rank loads it into ctx as
+ * `epoch` and activates it when activate != 0. *out_len (may be NULL) receives the blob size. */
+int cg_broadcast_image(cg_ctx* ctx, cg_comm* comm, int root, const void* image, size_t len, uint64_t epoch,
+                       int activate, size_t* out_len);
 
 /* ---- batches of (EntityMap, Request) ---- */
 /* Creates a batch bound to the currently active image. */

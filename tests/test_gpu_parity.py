@@ -358,3 +358,25 @@ def test_probe_kernel_missing_attribute_errors(ctx):
     items = [g.item() for _ in range(400)]
     check_items_ref(ctx, stores, items, want_indexed=True)
     check_items(ctx, stores, items[:100])
+
+
+# ---------------------------------------------------------------- RCCL hot reload (world size 1)
+def test_rccl_broadcast_reload(ctx):
+    """cg_broadcast_image at world size 1: the broadcast image loads and activates as a new epoch;
+    batches bound to the old epoch keep it (the swap the reference does on reload)."""
+    from cedargpu import dist as cdist
+    comm = cdist.Comm(0, 1, 0, cdist.unique_id())
+    req = {"principal": {"type": "U", "id": "a"}, "action": {"type": "A", "id": "b"}, "resource": {"type": "R", "id": "c"}}
+    img1 = cedargpu.build_image([cedargpu.MemoryStore("r.cedar", "permit(principal, action, resource);")], epoch=901)
+    assert comm.broadcast_image(ctx, img1, 901) == len(img1)
+    old = ctx.batch()
+    old.add([], req)
+    img2 = cedargpu.build_image([cedargpu.MemoryStore("r.cedar", "forbid(principal, action, resource);")], epoch=902)
+    comm.broadcast_image(ctx, img2, 902)
+    new = ctx.batch()
+    new.add([], req)
+    for b in (old, new):
+        b.submit()
+        b.wait()
+    assert old.decision(0)[0] is True and new.decision(0)[0] is False
+    comm.close()
