@@ -126,9 +126,18 @@ def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=120.0):
         except Exception as e:  # reported, not fatal: the decision path does not depend on it
             out["error"] = f"{type(e).__name__}: {e}"
 
-    th = threading.Thread(target=run, daemon=True)
-    th.start()
-    th.join(timeout_s)
+    # RCCL prints its banner on stdout; keep stdout for the one JSON line (fd-level redirect)
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        th = threading.Thread(target=run, daemon=True)
+        th.start()
+        th.join(timeout_s)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
     if th.is_alive():
         return {"error": f"timed out after {timeout_s:.0f} s"}
     return out
