@@ -143,6 +143,27 @@ def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=120.0):
     return out
 
 
+def serve(ctx, sars, threads, total, max_batch):
+    """End-to-end webhook path through the serving queue: `threads` native caller threads each
+    issue blocking cg_queue_authorize_sar calls (SAR JSON in, Decision + reason out), which the
+    queue batches onto the GPU. Host JSON parsing, SAR conversion and encoding are inside."""
+    import cedargpu
+    q = cedargpu.Queue(ctx, max_batch=max_batch, max_delay_us=0)
+    enc = [json.dumps(s, separators=(",", ":")) for s in sars]
+    q.loadgen(enc[:4096], threads, 8192)  # warm the pool's buffer classes
+    q.close()
+    q = cedargpu.Queue(ctx, max_batch=max_batch, max_delay_us=0)
+    r = q.loadgen(enc, threads, total)
+    st = q.stats()
+    q.close()
+    return {"decisions_per_s": total / r["seconds"], "requests": total, "threads": threads,
+            "p50_us": r["p50_us"], "p99_us": r["p99_us"], "max_us": r["max_us"],
+            "batches": st["batches"], "mean_batch": st["requests"] / max(1, st["batches"]),
+            "max_batch": st["max_batch"], "device_busy_frac": st["device_ns"] / 1e9 / r["seconds"],
+            "what": "cg_queue_authorize_sar per request from native threads (JSON parse, SAR conversion, "
+                    "columnar encode, batched H2D + kernel + D2H, reason rendering)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,6 +180,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=200)
     ap.add_argument("--latency-batch", type=int, default=2048)
+    ap.add_argument("--serve-threads", type=int, default=64,
+                    help="caller threads of the serving-queue check (0: skip)")
+    ap.add_argument("--serve-requests", type=int, default=262_144)
+    ap.add_argument("--serve-max-batch", type=int, default=8192)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -236,6 +261,10 @@ def main():
             lb.close()
         lat.sort()
 
+    serving = None
+    if rank == 0 and args.serve_threads and args.serve_requests:
+        serving = serve(ctx, sars, args.serve_threads, args.serve_requests, args.serve_max_batch)
+
     parity = parity_sample(policies, items, idx, b, threads) if rank == 0 and items else None
     reload = hot_reload(ctx, policies, rank, world, local, dist_on) if args.reload else None
 
@@ -277,6 +306,7 @@ def main():
             "cpu_baseline": baseline,
             "parity_sample": parity,
             "reload": reload,
+            "serving": serving,
             "latency": {"batch": args.latency_batch, "p50_ms": lat[len(lat) // 2] if lat else None,
                         "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
                         "max_ms": lat[-1] if lat else None, "batches": len(lat),

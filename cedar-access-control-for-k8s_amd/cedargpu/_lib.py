@@ -85,6 +85,15 @@ _SIGS = {
     "cg_sar_to_cedar_json": (ctypes.c_int, [cstr, sz, P, sz, ctypes.POINTER(sz)]),
     "cg_batch_authz": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
     "cg_is_authorized_json": (ctypes.c_int, [P, cstr, sz, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
+    "cg_queue_create": (ctypes.c_int, [P, u32, u32, ctypes.POINTER(P)]),
+    "cg_queue_destroy": (None, [P]),
+    "cg_queue_last_error": (cstr, []),
+    "cg_queue_authorize_sar": (ctypes.c_int, [P, cstr, sz, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
+    "cg_queue_is_authorized_json": (ctypes.c_int, [P, cstr, sz, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
+    "cg_queue_stats": (ctypes.c_int, [P] + [ctypes.POINTER(u64)] * 5),
+    "cg_queue_loadgen": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), u32, u32, u64,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                        ctypes.POINTER(u64), ctypes.POINTER(u64)]),
 }
 
 for _name, (_res, _args) in _SIGS.items():

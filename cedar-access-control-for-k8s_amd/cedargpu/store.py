@@ -14,7 +14,7 @@ from __future__ import annotations
 import ctypes
 import json
 import threading
-from typing import Iterable, List, Optional, Sequence, Tuple
+from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
 from ._lib import CG_E_RANGE, CompileError, DeviceError, _err, lib
 
@@ -323,6 +323,75 @@ class Batch:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         lib.cg_batch_bytes(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return a.value, b.value, c.value
+
+
+class Queue:
+    """Serving queue (cg_queue_*): blocking per-request calls from many threads, batched onto the
+    device. `authorize` is the webhook's Authorize (authorizer.go:36-86) for one
+    SubjectAccessReview; `is_authorized` is TieredPolicyStores.IsAuthorized for one Cedar-JSON item.
+    ctypes releases the GIL for the duration of each call, so Python threads batch together."""
+
+    def __init__(self, ctx: Context, max_batch: int = 4096, max_delay_us: int = 0):
+        self.ctx = ctx
+        self._h = _P()
+        rc = lib.cg_queue_create(ctx._h, max_batch, max_delay_us, ctypes.byref(self._h))
+        if rc:
+            raise _err(rc, "queue create failed")
+
+    def close(self):
+        if self._h:
+            lib.cg_queue_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _call(self, fn, payload: str) -> Tuple[int, str]:
+        b = _b(payload)
+        out = ctypes.c_int()
+        need = ctypes.c_size_t(0)
+        buf = ctypes.create_string_buffer(1024)
+        rc = fn(self._h, b, len(b), ctypes.byref(out), buf, 1024, ctypes.byref(need))
+        if rc == CG_E_RANGE and need.value > 1024:
+            buf = ctypes.create_string_buffer(need.value)
+            rc = fn(self._h, b, len(b), ctypes.byref(out), buf, need.value, ctypes.byref(need))
+        if rc:
+            raise _err(rc, lib.cg_queue_last_error().decode())
+        return out.value, buf.value.decode("utf-8")
+
+    def authorize(self, sar: Union[dict, str]) -> Tuple[int, str]:
+        """(authorizer.Decision: 0 Deny / 1 Allow / 2 NoOpinion, reason)."""
+        return self._call(lib.cg_queue_authorize_sar, sar if isinstance(sar, str) else json.dumps(sar))
+
+    def is_authorized(self, entities: list, request: dict) -> Tuple[bool, str]:
+        """(allow, json.Marshal(cedar.Diagnostic))."""
+        allow, diag = self._call(lib.cg_queue_is_authorized_json, json.dumps({"entities": entities, "request": request}))
+        return bool(allow), diag
+
+    def stats(self) -> dict:
+        v = [ctypes.c_uint64() for _ in range(5)]
+        rc = lib.cg_queue_stats(self._h, *[ctypes.byref(x) for x in v])
+        if rc:
+            raise _err(rc, "queue stats failed")
+        return dict(zip(("batches", "requests", "fast", "max_batch", "device_ns"), (x.value for x in v)))
+
+    def loadgen(self, sars_json: Sequence[str], threads: int, total: int) -> dict:
+        """Bench support: `threads` native threads issue `total` blocking authorize calls."""
+        enc = [_b(s) for s in sars_json]
+        arr = (ctypes.c_char_p * len(enc))(*enc)
+        lens = (ctypes.c_size_t * len(enc))(*[len(e) for e in enc])
+        secs = ctypes.c_double()
+        p50, p99, mx = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        counts = (ctypes.c_uint64 * 3)()
+        rc = lib.cg_queue_loadgen(self._h, arr, lens, len(enc), threads, total, ctypes.byref(secs), ctypes.byref(p50),
+                                  ctypes.byref(p99), ctypes.byref(mx), counts)
+        if rc:
+            raise _err(rc, lib.cg_queue_last_error().decode())
+        return {"seconds": secs.value, "p50_us": p50.value / 1e3, "p99_us": p99.value / 1e3, "max_us": mx.value / 1e3,
+                "deny": counts[0], "allow": counts[1], "no_opinion": counts[2]}
 
 
 class TieredPolicyStores:

@@ -145,6 +145,37 @@ int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t 
 int cg_is_authorized_json(cg_ctx* ctx, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
                           size_t* need);
 
+/* ---- serving queue: concurrent blocking per-request calls, batched onto the device ----
+ * Replaces the per-goroutine Authorize call of the webhook (authorizer.go:36-86; served by
+ * server.go:104 /v1/authorize). Any number of threads call cg_queue_authorize_sar concurrently;
+ * each call parses and converts its request on the calling thread, joins the open device batch
+ * and blocks until that batch is evaluated. The batch is closed at max_batch requests or when
+ * its first request has waited max_delay_us (0: as soon as the device is idle). */
+typedef struct cg_queue cg_queue;
+int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_queue** out);
+/* Drains pending batches, then stops the flusher. No call may be in flight on q. */
+void cg_queue_destroy(cg_queue* q);
+/* Error text of the calling thread's last failed cg_queue_* call. */
+const char* cg_queue_last_error(void);
+/* authorizer.Decision (0 Deny, 1 Allow, 2 NoOpinion) and reason of one SubjectAccessReview, as
+ * cg_batch_authz reports them. CG_E_RANGE: reason needs *need bytes (the decision is valid). */
+int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* decision, char* reason, size_t cap,
+                           size_t* need);
+/* TieredPolicyStores.IsAuthorized for one Cedar-JSON item (cg_batch_add_json's format) through
+ * the queue: *allow and, when diag or need is given, json.Marshal(cedar.Diagnostic). */
+int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
+                                size_t* need);
+/* Counters: device batches run, requests through the device, fast-path requests, largest batch,
+ * nanoseconds the flusher spent in submit + wait. Any pointer may be NULL. */
+int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,
+                   uint64_t* device_ns);
+/* Bench support: `threads` threads issue `total` blocking cg_queue_authorize_sar calls cycling
+ * over sars[0..n); wall seconds, per-call latency p50/p99/max (ns) and decision counts
+ * counts[0..3) = (Deny, Allow, NoOpinion). */
+int cg_queue_loadgen(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, uint32_t threads,
+                     uint64_t total, double* seconds, uint64_t* lat_p50, uint64_t* lat_p99, uint64_t* lat_max,
+                     uint64_t* counts);
+
 #ifdef __cplusplus
 }
 #endif
