@@ -1,10 +1,12 @@
 // C-ABI implementation (include/cedargpu.h). No exception crosses this boundary.
 #include <algorithm>
 #include <chrono>
+#include <cctype>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 
 #include "capi_internal.h"
 #include "sar.h"
@@ -15,6 +17,93 @@ struct cg_compiler {
   std::vector<std::vector<DocSpec>> tiers;
   std::string err;
 };
+
+namespace {
+
+// Element texts of a top-level JSON array (bracket / string balance only; each element is parsed
+// on its own afterwards). False when the text is not an array.
+bool split_array(const char* p, size_t n, std::vector<std::pair<size_t, size_t>>& out) {
+  size_t i = 0;
+  while (i < n && std::isspace((unsigned char)p[i])) i++;
+  if (i == n || p[i] != '[') return false;
+  i++;
+  int depth = 0;
+  size_t start = std::string::npos;
+  for (; i < n; i++) {
+    const char ch = p[i];
+    if (ch == '"') {
+      if (start == std::string::npos) start = i;
+      for (i++; i < n && p[i] != '"'; i++)
+        if (p[i] == '\\') i++;
+      continue;
+    }
+    if (std::isspace((unsigned char)ch)) continue;
+    if (start == std::string::npos && ch != ',' && !(depth == 0 && ch == ']')) start = i;
+    if (ch == '[' || ch == '{') depth++;
+    else if (ch == ']' || ch == '}') {
+      if (depth == 0) {  // end of the top-level array
+        if (start != std::string::npos) out.emplace_back(start, i - start);
+        return true;
+      }
+      depth--;
+    } else if (ch == ',' && depth == 0) {
+      if (start == std::string::npos) return false;
+      out.emplace_back(start, i - start);
+      start = std::string::npos;
+    }
+  }
+  return false;
+}
+
+// Worker threads for host-side bulk work: at most 16 (a GPU's share of host cores), and one per
+// 256 items.
+unsigned host_workers(size_t items) {
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = std::getenv("CEDARGPU_HOST_THREADS")) hw = (unsigned)std::max(1, std::atoi(e));
+  else hw = std::min(hw, 16u);
+  return (unsigned)std::max<size_t>(1, std::min<size_t>(hw, items / 256));
+}
+
+template <class F>
+void parallel_for(size_t n, F&& f) {
+  const unsigned t = host_workers(n);
+  if (t <= 1) { for (size_t i = 0; i < n; i++) f(i); return; }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> ws;
+  for (unsigned k = 0; k < t; k++)
+    ws.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(64)) < n;)
+        for (size_t j = i; j < std::min(n, i + 64); j++) f(j);
+    });
+  for (auto& w : ws) w.join();
+}
+
+// One SubjectAccessReview through the webhook's host steps, into `e` (or a fast-path decision).
+struct SarSlot {
+  int fast = -1;
+  std::string reason, err;
+  int rc = CG_OK;
+  EncodedRequest e;
+};
+
+void sar_to_slot(const Image& img, const char* p, size_t n, SarSlot& s) {
+  try {
+    JVal v = json_parse(p, n);
+    Attributes a = attributes_from_sar(v);
+    s.fast = authorize_fast_path(a, s.reason);
+    if (s.fast >= 0) return;
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    record_to_cedar(a, ents, req);
+    encode_request(img, ents, req, s.e);
+  } catch (const CedarError& e) {
+    s.err = e.what(); s.rc = CG_E_PARSE;
+  } catch (const std::exception& e) {
+    s.err = e.what(); s.rc = CG_E_ARG;
+  }
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -259,6 +348,28 @@ int cg_batch_add_json(cg_batch* b, const char* json, size_t len) {
 int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len) {
   if (!b || !json) return CG_E_ARG;
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
+  std::vector<std::pair<size_t, size_t>> elems;
+  if (len >= 65536 && split_array(json, len, elems) && host_workers(elems.size()) > 1) {
+    // bulk: parse, convert and encode elements on worker threads; append in order. All or nothing.
+    std::vector<SarSlot> slots(elems.size());
+    const Image& img = *b->host.img;
+    parallel_for(elems.size(), [&](size_t k) { sar_to_slot(img, json + elems[k].first, elems[k].second, slots[k]); });
+    for (auto& sl : slots)
+      if (sl.rc) { b->err = sl.err; return sl.rc; }
+    GUARD(b->err, {
+      for (auto& sl : slots) {
+        if (sl.fast >= 0) {
+          b->fast_reason[(uint32_t)b->items.size()] = std::move(sl.reason);
+          b->items.push_back({-1, sl.fast});
+          continue;
+        }
+        b->items.push_back({(int32_t)b->host.n(), -1});
+        b->host.append(sl.e);
+        sl.e = EncodedRequest();
+      }
+      return CG_OK;
+    })
+  }
   GUARD(b->err, {
     JVal v = json_parse(json, len);
     std::vector<EntityIn> ents;

@@ -378,7 +378,7 @@ __device__ __forceinline__ void str_span(const CT& c, uint32_t sid, const uint8_
     len = c.gstr_off[sid + 1] - o;
     p = c.gstr_bytes + o;
   } else {
-    const uint32_t j = sid - c.n_gstr;
+    const uint32_t j = c.blk[RH_SBASE] + (sid - c.n_gstr);  // request-local id -> batch string
     const uint32_t o = c.bstr_off[j];
     len = c.bstr_off[j + 1] - o;
     p = c.bstr_bytes + o;

@@ -1129,8 +1129,23 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
 }
 
 // exported for the encoder
-void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, Batch& b, uint32_t& w0, uint32_t& w1) {
-  auto sidf = [&b](const std::string& s) { return b.sid(s); };
+// Request strings: the image's id when the image holds the string, else a request-local id
+// (EncodedRequest).
+uint32_t request_sid(const Image& img, EncodedRequest& e, const std::string& s) {
+  const int32_t g = img.find(s);
+  if (g >= 0) return (uint32_t)g;
+  auto it = e.local.find(s);
+  if (it != e.local.end()) return it->second;
+  const uint32_t id = img.n_gstr() + (uint32_t)e.strs.size();
+  if (id > X_MASK) throw CedarError("string table overflow");
+  e.strs.push_back(s);
+  e.local.emplace(s, id);
+  return id;
+}
+
+void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, const Image& img, EncodedRequest& e, uint32_t& w0,
+                     uint32_t& w1) {
+  auto sidf = [&img, &e](const std::string& s) { return request_sid(img, e, s); };
   emit_value_impl(v, out, SP_HEAP, sidf, w0, w1);
 }
 

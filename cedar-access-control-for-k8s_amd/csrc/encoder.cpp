@@ -5,7 +5,8 @@
 // to (*PolicySet).IsAuthorized (store/store.go:31). The encoder lays the same facts out flat:
 //   header (P/A/R UIDs, context, entity-table indices of P/A/R) | entity table | data
 // Strings are interned against the image's global table first (so policy constants and request
-// strings compare by ID), then batch-locally. Each entity row carries a pointer to its
+// strings compare by ID), then request-locally, so encoding needs no batch-wide state: any thread
+// encodes a request (encode_request) and the batch appends it with copies (Batch::append). Each entity row carries a pointer to its
 // transitive ancestor list (the closure of `parents` through the map), so `in` is a linear scan.
 #include <algorithm>
 #include <unordered_set>
@@ -15,25 +16,17 @@
 namespace cg {
 using namespace cgi;
 
-void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, Batch& b, uint32_t& w0, uint32_t& w1);
+void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, const Image& img, EncodedRequest& e, uint32_t& w0,
+                     uint32_t& w1);
+uint32_t request_sid(const Image& img, EncodedRequest& e, const std::string& s);
 
-uint32_t Batch::sid(const std::string& s) {
-  int32_t g = img->find(s);
-  if (g >= 0) return (uint32_t)g;
-  auto it = bsid.find(s);
-  if (it != bsid.end()) return it->second;
-  uint32_t id = img->n_gstr() + (uint32_t)bstrings.size();
-  bstrings.push_back(s);
-  bsid.emplace(s, id);
-  return id;
-}
-
-const std::string& Batch::str(uint32_t id) const {
+const std::string& Batch::str(uint32_t i, uint32_t id) const {
   static const std::string empty;
-  uint32_t ng = img->n_gstr();
+  const uint32_t ng = img->n_gstr();
   if (id < ng) return img->strings[id];
-  if (id - ng < bstrings.size()) return bstrings[id - ng];
-  return empty;
+  if (i >= req_base.size()) return empty;
+  const size_t j = (size_t)heap[req_base[i] + RH_SBASE] + (id - ng);
+  return j < bstrings.size() ? bstrings[j] : empty;
 }
 
 namespace {
@@ -71,8 +64,10 @@ struct PairHash {
 };
 }  // namespace
 
-void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
-  std::vector<uint32_t> blk;
+void encode_request(const Image& img, const std::vector<EntityIn>& ents, const RequestIn& req, EncodedRequest& E) {
+  E.clear();
+  auto sid = [&](const std::string& s) { return request_sid(img, E, s); };
+  std::vector<uint32_t>& blk = E.blk;
   // entity table (EntityMap semantics: a repeated UID replaces the earlier entity)
   std::vector<const EntityIn*> table;
   std::unordered_map<std::pair<uint32_t, uint32_t>, uint32_t, PairHash> index;
@@ -87,7 +82,7 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
   }
   const uint32_t n = (uint32_t)table.size();
   blk.resize(RH_WORDS + (size_t)n * ENT_WORDS, 0);
-  auto uid_of = [this](const std::pair<std::string, std::string>& u) { return std::make_pair(sid(u.first), sid(u.second)); };
+  auto uid_of = [&](const std::pair<std::string, std::string>& u) { return std::make_pair(sid(u.first), sid(u.second)); };
   auto pu = uid_of(req.principal), au = uid_of(req.action), ru = uid_of(req.resource);
   for (auto* u : {&pu, &au, &ru}) if (u->first > X_MASK) throw CedarError("string table overflow");
   blk[RH_NENT] = n;
@@ -102,7 +97,7 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
     uint32_t w0, w1;
     HVal ctx = req.context;
     if (ctx.k != VK::Rec) { ctx = HVal(); ctx.k = VK::Rec; }
-    emit_heap_value(ctx, blk, *this, w0, w1);
+    emit_heap_value(ctx, blk, img, E, w0, w1);
     blk[RH_CTX] = w0; blk[RH_CTX + 1] = w1;
   }
   // parent adjacency (ids of parents that exist in the map are followed; absent ones are leaves)
@@ -119,7 +114,7 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
     uint32_t w0, w1;
     HVal attrs = table[i]->attrs;
     if (attrs.k != VK::Rec) { attrs = HVal(); attrs.k = VK::Rec; }
-    emit_heap_value(attrs, blk, *this, w0, w1);
+    emit_heap_value(attrs, blk, img, E, w0, w1);
     row = &blk[RH_WORDS + (size_t)i * ENT_WORDS];  // blk may have reallocated
     row[ER_ATTR0] = w0; row[ER_ATTR1] = w1;
     // transitive ancestors (BFS through the map; cycles tolerated)
@@ -143,10 +138,10 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = mk_ref(SP_HEAP, off);
   }
   // ---- columnar row: UIDs, ancestor lists, hot paths resolved as attribute access would ----
-  if (!row_words) row_words = img->row_words();
-  const size_t r0 = rows.size();
-  rows.resize(r0 + row_words, 0);
-  uint32_t* row = &rows[r0];
+  E.row.assign(img.row_words(), 0);
+  std::vector<uint32_t>& rows = E.row;
+  const size_t r0 = 0;
+  uint32_t* row = rows.data();
   row[RW_P] = pu.first; row[RW_P + 1] = pu.second;
   row[RW_A] = au.first; row[RW_A + 1] = au.second;
   row[RW_R] = ru.first; row[RW_R + 1] = ru.second;
@@ -159,10 +154,9 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
   anc_into(blk[RH_PIDX], RW_PANC, RW_PN);
   anc_into(blk[RH_RIDX], RW_RANC, RW_RN);
   anc_into(blk[RH_AIDX], RW_AANC, RW_AN);
-  rows[r0 + RW_BLK] = (uint32_t)heap.size();
-  const uint32_t nh = img->n_hot();
+  const uint32_t nh = img.n_hot();
   for (uint32_t h = 0; h < nh; h++) {
-    const uint32_t* hp = &img->hot[(size_t)h * HOT_WORDS];
+    const uint32_t* hp = &img.hot[(size_t)h * HOT_WORDS];
     const uint32_t var = hp[0], depth = hp[1];
     uint32_t w0, w1;
     if (var == 3) { w0 = blk[RH_CTX]; w1 = blk[RH_CTX + 1]; }
@@ -196,9 +190,25 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
     }
   }
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
-  if (heap.size() + blk.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
+}
+
+void Batch::append(EncodedRequest& e) {
+  if (!row_words) row_words = img->row_words();
+  if (e.row.size() != row_words || e.blk.size() < RH_WORDS) throw CedarError("request encoded for another image");
+  if (heap.size() + e.blk.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
+  if (bstrings.size() + e.strs.size() > 0xFFFFFFFFull) throw CedarError("batch string table overflow");
+  e.blk[RH_SBASE] = (uint32_t)bstrings.size();
+  e.row[RW_BLK] = (uint32_t)heap.size();
   req_base.push_back((uint32_t)heap.size());
-  heap.insert(heap.end(), blk.begin(), blk.end());
+  heap.insert(heap.end(), e.blk.begin(), e.blk.end());
+  rows.insert(rows.end(), e.row.begin(), e.row.end());
+  for (auto& s : e.strs) bstrings.push_back(std::move(s));
+}
+
+void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
+  EncodedRequest e;
+  encode_request(*img, ents, req, e);
+  append(e);
 }
 
 void Batch::finalize_strings() {

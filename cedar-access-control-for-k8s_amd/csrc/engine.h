@@ -75,14 +75,26 @@ struct RequestIn {
   HVal context;  // Record
 };
 
+// One request encoded position-independently, so that any thread can encode it and a batch
+// appends it with plain copies: heap references are block-relative, and strings absent from the
+// image's table are numbered request-locally (id n_gstr + j names strs[j]; the device adds the
+// request's string base, stored at RH_SBASE when the block is appended).
+struct EncodedRequest {
+  std::vector<uint32_t> blk, row;  // heap block; columnar row (RW_BLK set on append)
+  std::vector<std::string> strs;   // request-local strings
+  std::unordered_map<std::string, uint32_t> local;
+  void clear() { blk.clear(); row.clear(); strs.clear(); local.clear(); }
+};
+// Encodes (EntityMap, Request) for `img`. Thread-safe: reads the image only.
+void encode_request(const Image& img, const std::vector<EntityIn>& ents, const RequestIn& req, EncodedRequest& out);
+
 // Host side of a device batch: encoded request heap + string table; results after evaluation.
 struct Batch {
   std::shared_ptr<const Image> img;
   std::vector<uint32_t> heap, req_base;
   std::vector<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
   uint32_t row_words = 0;
-  std::vector<std::string> bstrings;
-  std::unordered_map<std::string, uint32_t> bsid;
+  std::vector<std::string> bstrings;  // request-local strings of every request, concatenated
   std::vector<uint32_t> bstr_off;
   std::vector<uint8_t> bstr_bytes;
   // results
@@ -92,16 +104,17 @@ struct Batch {
   std::unordered_map<uint32_t, std::vector<uint32_t>> big_reasons, big_errs;
 
   uint32_t n() const { return (uint32_t)req_base.size(); }
-  uint32_t sid(const std::string& s);
-  const std::string& str(uint32_t id) const;
-  void add(const std::vector<EntityIn>& ents, const RequestIn& req);
+  // string `id` as request i sees it
+  const std::string& str(uint32_t i, uint32_t id) const;
+  void add(const std::vector<EntityIn>& ents, const RequestIn& req);  // encode_request + append
+  void append(EncodedRequest& e);                                     // moves e's strings
   void finalize_strings();
   // decision: 1 allow, 0 deny; fills the Go-JSON rendering of the cedar.Diagnostic
   bool decision(uint32_t i) const;
   void diagnostic_json(uint32_t i, std::string& out, bool reasons_only) const;
   void reason_ids(uint32_t i, std::vector<uint32_t>& out) const;
   void error_recs(uint32_t i, std::vector<uint32_t>& out) const;
-  std::string error_message(const uint32_t* rec) const;
+  std::string error_message(uint32_t i, const uint32_t* rec) const;
 };
 
 // Parses a Cedar-JSON request item {"entities": [...], "request": {...}} into encoder input.

@@ -61,7 +61,8 @@ enum ReqHdr : uint32_t {
   RH_PIDX = 9,   // entity-table index of principal / action / resource (NO_ENT if absent)
   RH_AIDX = 10,
   RH_RIDX = 11,
-  RH_WORDS = 12, // entity table follows: n_ent * ENT_WORDS
+  RH_SBASE = 12, // index of the request's first string in the batch string table (bstr_off)
+  RH_WORDS = 13, // entity table follows: n_ent * ENT_WORDS
 };
 enum EntRow : uint32_t { ER_TYPE = 0, ER_ID = 1, ER_ATTR0 = 2, ER_ATTR1 = 3, ER_ANC = 4, ER_PAD = 5, ENT_WORDS = 6 };
 constexpr uint32_t NO_ENT = 0xFFFFFFFFu;

@@ -99,30 +99,40 @@ void cg_queue::run() {
 
 namespace {
 
-// Appends one converted request to the open batch (creating it on the first request) and returns
-// the batch and the request's index in it. Caller must not hold q->mu.
-int enqueue(cg_queue* q, const std::vector<EntityIn>& ents, const RequestIn& req, std::shared_ptr<QBatch>& out,
+std::shared_ptr<LoadedImage> active_image(cg_ctx* ctx, std::string& err) {
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ctx->active) err = "no active image";
+  return ctx->active;
+}
+
+// Appends one encoded request (encoded against `li`) to the open batch and returns the batch and
+// the request's index in it. A batch holds requests of one image: a request encoded against a
+// newer epoch closes the open batch first. Caller must not hold q->mu.
+int enqueue(cg_queue* q, const std::shared_ptr<LoadedImage>& li, EncodedRequest& e, std::shared_ptr<QBatch>& out,
             uint32_t& idx, std::string& err) {
   std::unique_lock<std::mutex> g(q->mu);
   q->cv_space.wait(g, [q] { return q->stop || q->ready.size() < q->max_ready; });
   if (q->stop) { err = "queue closed"; return CG_E_STATE; }
+  if (q->open && q->open->b->img != li) {
+    q->ready.push_back(std::move(q->open));
+    q->open.reset();
+    q->cv_flush.notify_one();
+  }
   if (!q->open) {
     auto qb = std::make_shared<QBatch>();
-    int rc = cg_batch_create(q->ctx, &qb->b);
-    if (rc) { err = q->ctx->err; return rc; }
+    qb->b = new (std::nothrow) cg_batch();
+    if (!qb->b) { err = "out of host memory"; return CG_E_ARG; }
+    qb->b->ctx = q->ctx;
+    qb->b->img = li;
+    qb->b->host.img = li->host;
     qb->t0 = Clock::now();
     q->open = std::move(qb);
     q->cv_flush.notify_one();  // arms the deadline
   }
   cg_batch* b = q->open->b;
   GUARD(err, {
-    b->items.push_back({(int32_t)b->host.n(), -1});
-    try {
-      b->host.add(ents, req);
-    } catch (...) {
-      b->items.pop_back();
-      throw;
-    }
+    b->host.append(e);
+    b->items.push_back({(int32_t)b->host.n() - 1, -1});
   })
   idx = (uint32_t)b->items.size() - 1;
   out = q->open;
@@ -150,6 +160,30 @@ int put_string(const std::string& s, char* buf, size_t cap, size_t* need) {
 }
 
 thread_local std::string t_err;
+
+// Encodes on the calling thread, joins the open batch, waits, and renders the caller's result
+// (authz: cg_batch_authz's Decision + reason; else cg_batch_decision + diagnostic).
+int submit_encoded(cg_queue* q, const std::vector<EntityIn>& ents, const RequestIn& req, int* out, char* buf,
+                   size_t cap, size_t* need, bool authz) {
+  auto li = active_image(q->ctx, t_err);
+  if (!li) return CG_E_STATE;
+  EncodedRequest e;
+  GUARD(t_err, { encode_request(*li->host, ents, req, e); })
+  std::shared_ptr<QBatch> qb;
+  uint32_t idx = 0;
+  int rc = enqueue(q, li, e, qb, idx, t_err);
+  if (rc) return rc;
+  q->n_requests++;
+  if ((rc = await(qb, t_err))) return rc;
+  if (authz) {
+    rc = cg_batch_authz(qb->b, idx, out, buf, cap, need);
+    if (rc && rc != CG_E_RANGE) t_err = qb->b->err;
+    return rc;
+  }
+  if ((rc = cg_batch_decision(qb->b, idx, out, nullptr))) { t_err = qb->b->err; return rc; }
+  if (!buf && !need) return CG_OK;
+  return cg_batch_diagnostic(qb->b, idx, 0, buf, cap, need);
+}
 
 }  // namespace
 
@@ -204,16 +238,10 @@ int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* d
     }
     record_to_cedar(a, ents, req);
   })
-  std::shared_ptr<QBatch> qb;
-  uint32_t idx = 0;
-  int rc = enqueue(q, ents, req, qb, idx, t_err);
-  if (rc) return rc;
-  q->n_requests++;
-  if ((rc = await(qb, t_err))) return rc;
-  rc = cg_batch_authz(qb->b, idx, decision, reason, cap, need);
-  if (rc && rc != CG_E_RANGE) t_err = qb->b->err;
-  return rc;
+  return submit_encoded(q, ents, req, decision, reason, cap, need, true);
 }
+
+
 
 int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
                                 size_t* need) {
@@ -224,15 +252,7 @@ int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, 
     JVal v = json_parse(item_json, len);
     decode_json_item(v, ents, req);
   })
-  std::shared_ptr<QBatch> qb;
-  uint32_t idx = 0;
-  int rc = enqueue(q, ents, req, qb, idx, t_err);
-  if (rc) return rc;
-  q->n_requests++;
-  if ((rc = await(qb, t_err))) return rc;
-  if ((rc = cg_batch_decision(qb->b, idx, allow, nullptr))) { t_err = qb->b->err; return rc; }
-  if (!diag && !need) return CG_OK;
-  return cg_batch_diagnostic(qb->b, idx, 0, diag, cap, need);
+  return submit_encoded(q, ents, req, allow, diag, cap, need, false);
 }
 
 int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,

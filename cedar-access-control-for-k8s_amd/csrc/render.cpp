@@ -58,7 +58,7 @@ static void quote(std::string& o, const std::string& s) {
   o += '"';
 }
 
-std::string Batch::error_message(const uint32_t* rec) const {
+std::string Batch::error_message(uint32_t i, const uint32_t* rec) const {
   const PolicyMeta& m = img->meta[rec[0]];
   uint32_t code = rec[1] & 0xFF, aux = rec[1] >> 8;
   std::string body;
@@ -67,16 +67,16 @@ std::string Batch::error_message(const uint32_t* rec) const {
       body = std::string("type error: expected ") + type_name(aux & 0xFF) + ", got " + type_name((aux >> 8) & 0xFF);
       break;
     case E_ENTITY_MISSING:
-      body = "entity `" + str(rec[3]) + "::";
-      quote(body, str(rec[4]));
+      body = "entity `" + str(i, rec[3]) + "::";
+      quote(body, str(i, rec[4]));
       body += "` does not exist";
       break;
     case E_ATTR_ENTITY:
-      body = "`" + str(rec[3]) + "::";
-      quote(body, str(rec[4]));
-      body += "` does not have the attribute `" + str(rec[2]) + "`";
+      body = "`" + str(i, rec[3]) + "::";
+      quote(body, str(i, rec[4]));
+      body += "` does not have the attribute `" + str(i, rec[2]) + "`";
       break;
-    case E_ATTR_RECORD: body = "record does not have the attribute `" + str(rec[2]) + "`"; break;
+    case E_ATTR_RECORD: body = "record does not have the attribute `" + str(i, rec[2]) + "`"; break;
     case E_OVERFLOW: body = "integer overflow"; break;
     case E_EXT: body = aux < img->ext_msgs.size() ? img->ext_msgs[aux] : "extension error"; break;
     case E_DEPTH: body = "value nesting exceeds the device evaluator limit"; break;
@@ -126,7 +126,7 @@ void Batch::diagnostic_json(uint32_t i, std::string& out, bool reasons_only) con
       out += ",\"position\":";
       pos_json(out, m);
       out += ",\"message\":";
-      go_json_string(out, error_message(rec));
+      go_json_string(out, error_message(i, rec));
       out += '}';
     }
     out += ']';

@@ -1,0 +1,84 @@
+// Host-side encoder throughput (no GPU): per-phase cost of the webhook's host steps for one
+// SubjectAccessReview — JSON parse, SAR -> attributes + fast path + entities, columnar encode —
+// single-threaded and across T threads.  Build: make -C tools encode_bench
+// Usage: encode_bench <policies.cedar> <sars.jsonl (one SAR per line)> [threads]
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+#include <thread>
+
+#include "../cedar-access-control-for-k8s_amd/csrc/engine.h"
+#include "../cedar-access-control-for-k8s_amd/csrc/sar.h"
+
+using namespace cg;
+using Clock = std::chrono::steady_clock;
+
+static std::string slurp(const char* p) {
+  std::ifstream f(p, std::ios::binary);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) { std::fprintf(stderr, "usage: %s policies.cedar sars.json [threads]\n", argv[0]); return 2; }
+  const unsigned threads = argc > 3 ? (unsigned)std::atoi(argv[3]) : 8;
+  DocSpec d;
+  d.filename = "c3.cedar";
+  d.text = slurp(argv[1]);
+  auto img = compile_image({{d}}, 1);
+  std::vector<std::string> texts;  // one SubjectAccessReview body per line
+  {
+    std::ifstream f(argv[2]);
+    for (std::string line; std::getline(f, line);)
+      if (!line.empty()) texts.push_back(line);
+  }
+  const size_t n = texts.size();
+  double t_parse = 0, t_conv = 0, t_enc = 0;
+  size_t words = 0, strs = 0;
+  for (size_t i = 0; i < n; i++) {
+    auto t0 = Clock::now();
+    JVal v = json_parse(texts[i].data(), texts[i].size());
+    auto t1 = Clock::now();
+    Attributes a = attributes_from_sar(v);
+    std::string r;
+    if (authorize_fast_path(a, r) >= 0) continue;
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    record_to_cedar(a, ents, req);
+    auto t2 = Clock::now();
+    EncodedRequest e;
+    encode_request(*img, ents, req, e);
+    auto t3 = Clock::now();
+    t_parse += std::chrono::duration<double>(t1 - t0).count();
+    t_conv += std::chrono::duration<double>(t2 - t1).count();
+    t_enc += std::chrono::duration<double>(t3 - t2).count();
+    words += e.blk.size() + e.row.size();
+    strs += e.strs.size();
+  }
+  std::printf("requests %zu  per request: parse %.2f us  convert %.2f us  encode %.2f us  (%.1f words, %.1f local strings)\n",
+              n, 1e6 * t_parse / n, 1e6 * t_conv / n, 1e6 * t_enc / n, (double)words / n, (double)strs / n);
+  auto t0 = Clock::now();
+  std::vector<std::thread> ws;
+  std::atomic<size_t> next{0};
+  for (unsigned t = 0; t < threads; t++)
+    ws.emplace_back([&] {
+      EncodedRequest e;
+      for (size_t i; (i = next++) < n;) {
+        JVal v = json_parse(texts[i].data(), texts[i].size());
+        Attributes a = attributes_from_sar(v);
+        std::string r;
+        if (authorize_fast_path(a, r) >= 0) continue;
+        std::vector<EntityIn> ents;
+        RequestIn req;
+        record_to_cedar(a, ents, req);
+        encode_request(*img, ents, req, e);
+      }
+    });
+  for (auto& w : ws) w.join();
+  const double s = std::chrono::duration<double>(Clock::now() - t0).count();
+  std::printf("%u threads: %.0f requests/s\n", threads, n / s);
+  return 0;
+}
