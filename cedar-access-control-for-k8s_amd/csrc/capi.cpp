@@ -88,6 +88,10 @@ struct SarSlot {
 
 void sar_to_slot(const Image& img, const char* p, size_t n, SarSlot& s) {
   try {
+    const int d = encode_sar_direct(img, p, n, s.e, s.fast, s.reason);
+    if (d == 2) return;
+    s.fast = -1;
+    if (d == 1) return;
     JVal v = json_parse(p, n);
     Attributes a = attributes_from_sar(v);
     s.fast = authorize_fast_path(a, s.reason);
@@ -101,6 +105,50 @@ void sar_to_slot(const Image& img, const char* p, size_t n, SarSlot& s) {
   } catch (const std::exception& e) {
     s.err = e.what(); s.rc = CG_E_ARG;
   }
+}
+
+// cg_encode_sar_check: every SAR of the array through the direct path and the general path.
+int encode_sar_check(const void* image, size_t len, const char* sars, size_t n, uint32_t* n_items, uint32_t* n_direct,
+                     uint32_t* n_mismatch, int64_t* first_mismatch) {
+  auto img = Image::deserialize((const uint8_t*)image, len);
+  std::vector<std::pair<size_t, size_t>> elems;
+  if (!split_array(sars, n, elems)) throw CedarError("expected a JSON array");
+  uint32_t nd = 0, nm = 0;
+  int64_t first = -1;
+  for (size_t k = 0; k < elems.size(); k++) {
+    const char* p = sars + elems[k].first;
+    const size_t m = elems[k].second;
+    EncodedRequest direct;
+    int fast_d = -1;
+    std::string reason_d;
+    const int d = encode_sar_direct(*img, p, m, direct, fast_d, reason_d);
+    if (!d) continue;
+    nd++;
+    JVal v = json_parse(p, m);
+    Attributes at = attributes_from_sar(v);
+    std::string reason_g;
+    const int fast_g = authorize_fast_path(at, reason_g);
+    bool same;
+    if (fast_g >= 0) {
+      same = d == 2 && fast_d == fast_g && reason_d == reason_g;
+    } else {
+      std::vector<EntityIn> ents;
+      RequestIn req;
+      record_to_cedar(at, ents, req);
+      EncodedRequest general;
+      encode_request(*img, ents, req, general);
+      same = d == 1 && direct.blk == general.blk && direct.row == general.row && direct.strs == general.strs;
+    }
+    if (!same) {
+      nm++;
+      if (first < 0) first = (int64_t)k;
+    }
+  }
+  if (n_items) *n_items = (uint32_t)elems.size();
+  if (n_direct) *n_direct = nd;
+  if (n_mismatch) *n_mismatch = nm;
+  if (first_mismatch) *first_mismatch = first;
+  return CG_OK;
 }
 
 }  // namespace
@@ -375,7 +423,7 @@ int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len) {
     std::vector<EntityIn> ents;
     RequestIn req;
     auto one = [&](const JVal& sar) {
-      Attributes a = attributes_from_sar(sar);
+      Attributes a = attributes_from_sar(sar);  // (array of < 65536 bytes, or one worker)
       std::string reason;
       int fast = authorize_fast_path(a, reason);
       if (fast >= 0) {
@@ -469,6 +517,13 @@ int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t 
   if (cap < r.size() + 1) return CG_E_RANGE;
   std::memcpy(reason, r.c_str(), r.size() + 1);
   return CG_OK;
+}
+
+int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t n, uint32_t* n_items,
+                        uint32_t* n_direct, uint32_t* n_mismatch, int64_t* first_mismatch) {
+  if (!image || !sars) return CG_E_ARG;
+  std::string err;
+  GUARD(err, { return encode_sar_check(image, len, sars, n, n_items, n_direct, n_mismatch, first_mismatch); })
 }
 
 uint32_t cg_batch_size(cg_batch* b) { return b ? (uint32_t)b->items.size() : 0; }

@@ -1054,6 +1054,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
   if (img->code.empty()) img->code.push_back(0), img->code.push_back(0);  // never empty buffers
   if (img->cpool.empty()) img->cpool.push_back(0);
   if (img->gstr_bytes.empty()) img->gstr_bytes.push_back(0);
+  img->build_lookup();
   return img;
 }
 
@@ -1125,27 +1126,56 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   uint32_t ne = r.u32();
   for (uint32_t i = 0; i < ne; i++) img->ext_msgs.push_back(r.str());
   if (img->pol.size() != (size_t)img->meta.size() * POL_WORDS) throw CedarError("corrupt image");
+  img->build_lookup();
   return img;
 }
 
 // exported for the encoder
 // Request strings: the image's id when the image holds the string, else a request-local id
 // (EncodedRequest).
-uint32_t request_sid(const Image& img, EncodedRequest& e, const std::string& s) {
+uint32_t request_sid(const Image& img, EncodedRequest& e, std::string_view s) {
+  for (uint32_t k = 0; k < e.n_memo; k++)
+    if (e.memo_p[k] == s.data() && e.memo_len[k] == s.size()) return e.memo_id[k];
+  uint32_t id;
   const int32_t g = img.find(s);
-  if (g >= 0) return (uint32_t)g;
-  auto it = e.local.find(s);
-  if (it != e.local.end()) return it->second;
-  const uint32_t id = img.n_gstr() + (uint32_t)e.strs.size();
-  if (id > X_MASK) throw CedarError("string table overflow");
-  e.strs.push_back(s);
-  e.local.emplace(s, id);
+  if (g >= 0) {
+    id = (uint32_t)g;
+  } else {
+    size_t j = 0;
+    while (j < e.strs.size() && e.strs[j] != s) j++;
+    id = img.n_gstr() + (uint32_t)j;
+    if (j == e.strs.size()) {
+      id = img.n_gstr() + (uint32_t)e.strs.size();
+      if (id > X_MASK) throw CedarError("string table overflow");
+      e.strs.emplace_back(s);
+    }
+  }
+  if (e.n_memo < EncodedRequest::MEMO) {
+    e.memo_p[e.n_memo] = s.data();
+    e.memo_len[e.n_memo] = (uint32_t)s.size();
+    e.memo_id[e.n_memo++] = id;
+  }
   return id;
+}
+
+void Image::build_lookup() {
+  size_t cap = 16;
+  while (cap < 2 * strings.size() + 16) cap <<= 1;
+  lookup.assign(cap, 0);
+  for (uint32_t i = 0; i < strings.size(); i++) {
+    const uint64_t hv = str_hash(strings[i]);
+    size_t h = hv & (cap - 1);
+    while (lookup[h]) {
+      if (strings[(uint32_t)lookup[h] - 1] == strings[i]) break;  // first id of a repeated string wins, as in `sid`
+      h = (h + 1) & (cap - 1);
+    }
+    if (!lookup[h]) lookup[h] = ((hv >> 32) << 32) | (i + 1);
+  }
 }
 
 void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, const Image& img, EncodedRequest& e, uint32_t& w0,
                      uint32_t& w1) {
-  auto sidf = [&img, &e](const std::string& s) { return request_sid(img, e, s); };
+  auto sidf = [&img, &e](const std::string& s) { return request_sid(img, e, std::string_view(s)); };
   emit_value_impl(v, out, SP_HEAP, sidf, w0, w1);
 }
 

@@ -1,0 +1,230 @@
+// The request encoder's one implementation, shared by the general path (EntityIn / HVal trees
+// decoded from Cedar JSON or built by sar.cpp) and the direct SubjectAccessReview path (views
+// into the request body), so both produce the same words for the same (EntityMap, Request).
+//
+// Source interface (Src):
+//   uint32_t n_ents();  std::string_view type(i), id(i);
+//   uint32_t n_parents(i);  std::pair<sv, sv> parent(i, k);
+//   std::pair<sv, sv> principal(), action(), resource();
+//   void emit_ctx(out, img, E, w0, w1);  void emit_attrs(i, out, img, E, w0, w1);
+//     (emit the context / entity attributes record into `out` exactly as emit_heap_value does)
+#pragma once
+#include <algorithm>
+#include <string_view>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "engine.h"
+
+namespace cg {
+
+uint32_t request_sid(const Image& img, EncodedRequest& e, std::string_view s);
+
+namespace enc {
+using namespace cgi;
+
+// memory-form record lookup inside an emitted request block (the device's rec_get, on the host)
+inline bool blk_rec_get(const std::vector<uint32_t>& blk, uint32_t rw0, uint32_t n, uint32_t key, uint32_t& w0,
+                        uint32_t& w1) {
+  const uint32_t off = rw0 & OFF_MASK;
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (blk[off + 1 + 3 * mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < n && blk[off + 1 + 3 * lo] == key) {
+    w0 = blk[off + 2 + 3 * lo];
+    w1 = blk[off + 3 + 3 * lo];
+    return true;
+  }
+  return false;
+}
+
+inline uint32_t mem_tname(uint32_t w0) {
+  switch (w0 >> TAG_SHIFT) {
+    case T_BOOL: return TN_BOOL;
+    case T_LONG: case T_LONGREF: return TN_LONG;
+    case T_STR: return TN_STRING;
+    case T_ENT: return TN_ENTITY;
+    case T_SET: return TN_SET;
+    case T_REC: return TN_RECORD;
+    case T_DEC: return TN_DECIMAL;
+    case T_IP: return TN_IP;
+    default: return TN_UNKNOWN;
+  }
+}
+
+inline uint64_t uid_key(uint32_t t, uint32_t id) { return ((uint64_t)t << 32) | id; }
+
+// UID -> entity-table index: a linear scan for the few entities of a webhook request, a hash
+// map beyond that.
+struct UidIndex {
+  std::vector<uint64_t> keys;
+  std::unordered_map<uint64_t, uint32_t> map;
+  int32_t find(uint64_t k) const {
+    if (map.empty()) {
+      for (size_t i = 0; i < keys.size(); i++)
+        if (keys[i] == k) return (int32_t)i;
+      return -1;
+    }
+    auto it = map.find(k);
+    return it == map.end() ? -1 : (int32_t)it->second;
+  }
+  void add(uint64_t k) {
+    keys.push_back(k);
+    if (!map.empty()) map.emplace(k, (uint32_t)keys.size() - 1);
+    else if (keys.size() > 32)
+      for (size_t i = 0; i < keys.size(); i++) map.emplace(keys[i], (uint32_t)i);
+  }
+};
+
+inline void emit_empty_record(std::vector<uint32_t>& out, uint32_t& w0, uint32_t& w1) {
+  const uint32_t off = (uint32_t)out.size();
+  out.push_back(0);
+  w0 = mk_w0(T_REC, mk_ref(SP_HEAP, off));
+  w1 = 0;
+}
+
+}  // namespace enc
+
+template <class Src>
+void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
+  using namespace enc;
+  E.clear();
+  auto sid = [&](std::string_view s) { return request_sid(img, E, s); };
+  std::vector<uint32_t>& blk = E.blk;
+  // entity table (EntityMap semantics: a repeated UID replaces the earlier entity)
+  std::vector<uint32_t> table;  // source entity of each table slot
+  UidIndex index;
+  const uint32_t n_in = src.n_ents();
+  for (uint32_t e = 0; e < n_in; e++) {
+    const uint32_t t = sid(src.type(e)), id = sid(src.id(e));
+    const uint64_t k = uid_key(t, id);
+    const int32_t at = index.find(k);
+    if (at >= 0) { table[(size_t)at] = e; continue; }
+    index.add(k);
+    table.push_back(e);
+  }
+  const uint32_t n = (uint32_t)table.size();
+  blk.resize(RH_WORDS + (size_t)n * ENT_WORDS, 0);
+  auto uid_of = [&](const std::pair<std::string_view, std::string_view>& u) {
+    const uint32_t t = sid(u.first);
+    return std::make_pair(t, sid(u.second));
+  };
+  const auto pu = uid_of(src.principal()), au = uid_of(src.action()), ru = uid_of(src.resource());
+  for (auto* u : {&pu, &au, &ru})
+    if (u->first > X_MASK) throw CedarError("string table overflow");
+  blk[RH_NENT] = n;
+  blk[RH_P] = mk_w0(T_ENT, pu.first); blk[RH_P + 1] = pu.second;
+  blk[RH_A] = mk_w0(T_ENT, au.first); blk[RH_A + 1] = au.second;
+  blk[RH_R] = mk_w0(T_ENT, ru.first); blk[RH_R + 1] = ru.second;
+  auto idx_of = [&](const std::pair<uint32_t, uint32_t>& u) {
+    const int32_t i = index.find(uid_key(u.first, u.second));
+    return i < 0 ? NO_ENT : (uint32_t)i;
+  };
+  blk[RH_PIDX] = idx_of(pu);
+  blk[RH_AIDX] = idx_of(au);
+  blk[RH_RIDX] = idx_of(ru);
+  {
+    uint32_t w0, w1;
+    src.emit_ctx(blk, img, E, w0, w1);
+    blk[RH_CTX] = w0; blk[RH_CTX + 1] = w1;
+  }
+  // parent adjacency (ids of parents that exist in the map are followed; absent ones are leaves)
+  std::vector<std::vector<uint64_t>> parents(n);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t np = src.n_parents(table[i]);
+    for (uint32_t k = 0; k < np; k++) {
+      const auto u = uid_of(src.parent(table[i], k));
+      const uint64_t key = uid_key(u.first, u.second);
+      if (std::find(parents[i].begin(), parents[i].end(), key) == parents[i].end()) parents[i].push_back(key);
+    }
+  }
+  std::vector<uint64_t> anc;
+  std::vector<uint32_t> stack;
+  std::unordered_set<uint64_t> seen_big;
+  for (uint32_t i = 0; i < n; i++) {
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_TYPE] = (uint32_t)(index.keys[i] >> 32);
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ID] = (uint32_t)index.keys[i];
+    uint32_t w0, w1;
+    src.emit_attrs(table[i], blk, img, E, w0, w1);
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ATTR0] = w0;
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ATTR1] = w1;
+    // transitive ancestors (through the map; cycles tolerated)
+    anc.clear();
+    seen_big.clear();
+    stack.assign(1, i);
+    while (!stack.empty()) {
+      const uint32_t cur = stack.back();
+      stack.pop_back();
+      for (const uint64_t p : parents[cur]) {
+        const bool seen = anc.size() <= 64 ? std::find(anc.begin(), anc.end(), p) != anc.end() : seen_big.count(p) > 0;
+        if (seen) continue;
+        anc.push_back(p);
+        if (anc.size() == 65) seen_big.insert(anc.begin(), anc.end());  // switch to hashing
+        else if (anc.size() > 65) seen_big.insert(p);
+        const int32_t at = index.find(p);
+        if (at >= 0) stack.push_back((uint32_t)at);
+      }
+    }
+    std::sort(anc.begin(), anc.end());
+    const uint32_t off = (uint32_t)blk.size();
+    blk.push_back((uint32_t)anc.size());
+    for (const uint64_t a : anc) { blk.push_back((uint32_t)(a >> 32)); blk.push_back((uint32_t)a); }
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = mk_ref(SP_HEAP, off);
+  }
+  // ---- columnar row: UIDs, ancestor lists, hot paths resolved as attribute access would ----
+  E.row.assign(img.row_words(), 0);
+  uint32_t* row = E.row.data();
+  row[RW_P] = pu.first; row[RW_P + 1] = pu.second;
+  row[RW_A] = au.first; row[RW_A + 1] = au.second;
+  row[RW_R] = ru.first; row[RW_R + 1] = ru.second;
+  auto anc_into = [&](uint32_t idx, uint32_t w_off, uint32_t w_n) {
+    if (idx == NO_ENT) return;
+    const uint32_t ref = blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;
+    row[w_off] = ref + 1;
+    row[w_n] = blk[ref];
+  };
+  anc_into(blk[RH_PIDX], RW_PANC, RW_PN);
+  anc_into(blk[RH_RIDX], RW_RANC, RW_RN);
+  anc_into(blk[RH_AIDX], RW_AANC, RW_AN);
+  const uint32_t nh = img.n_hot();
+  for (uint32_t h = 0; h < nh; h++) {
+    const uint32_t* hp = &img.hot[(size_t)h * HOT_WORDS];
+    const uint32_t var = hp[0], depth = hp[1];
+    uint32_t w0, w1;
+    if (var == 3) { w0 = blk[RH_CTX]; w1 = blk[RH_CTX + 1]; }
+    else { const uint32_t o = var == 0 ? RH_P : var == 1 ? RH_A : RH_R; w0 = blk[o]; w1 = blk[o + 1]; }
+    uint32_t code = E_NONE, aux = 0, k = 0, et = 0, ei = 0;
+    bool fin = false;
+    for (uint32_t j = 0; j < depth && code == E_NONE; j++) {
+      const uint32_t key = hp[2 + j], tag = w0 >> TAG_SHIFT;
+      const bool last = j + 1 == depth;
+      if (tag == T_ENT) {
+        const uint32_t t = w0 & X_MASK, id = w1;
+        const int32_t at = index.find(uid_key(t, id));
+        if (at < 0) { code = E_ENTITY_MISSING; et = t; ei = id; fin = last; break; }
+        const uint32_t* er = &blk[RH_WORDS + (size_t)at * ENT_WORDS];
+        if (!blk_rec_get(blk, er[ER_ATTR0], er[ER_ATTR1], key, w0, w1)) { code = E_ATTR_ENTITY; k = key; et = t; ei = id; fin = last; }
+      } else if (tag == T_REC) {
+        if (!blk_rec_get(blk, w0, w1, key, w0, w1)) { code = E_ATTR_RECORD; k = key; fin = last; }
+      } else {
+        code = E_TYPE;
+        aux = TN_ENTITY_OR_RECORD | (mem_tname(w0) << 8);
+      }
+    }
+    if (code == E_NONE) {
+      row[RW_HDR + 2 * h] = w0;
+      row[RW_HDR + 2 * h + 1] = w1;
+    } else {
+      const uint32_t off = (uint32_t)blk.size();
+      blk.push_back(code | (aux << 8)); blk.push_back(k); blk.push_back(et); blk.push_back(ei);
+      row[RW_HDR + 2 * h] = mk_w0(T_NONE, code | (fin ? HS_FINAL : 0u));
+      row[RW_HDR + 2 * h + 1] = off;
+    }
+  }
+  if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
+}
+
+}  // namespace cg

@@ -2,9 +2,11 @@
 #pragma once
 #include <atomic>
 #include <cstdint>
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -47,9 +49,42 @@ struct Image {
   uint32_t n_gstr() const { return (uint32_t)strings.size(); }
   uint32_t n_hot() const { return (uint32_t)hot.size() / cgi::HOT_WORDS; }
   uint32_t row_words() const { return (cgi::RW_HDR + 2 * n_hot() + 3) & ~3u; }
-  int32_t find(const std::string& s) const {
-    auto it = sid.find(s);
-    return it == sid.end() ? -1 : (int32_t)it->second;
+  // string -> id over a string_view: open addressing, entries (hash high 32 bits << 32 | id + 1),
+  // 0 = empty; size is a power of two. Built by build_lookup once the table is final.
+  std::vector<uint64_t> lookup;
+  void build_lookup();
+  int32_t find(std::string_view s) const {
+    if (lookup.empty()) {
+      auto it = sid.find(std::string(s));
+      return it == sid.end() ? -1 : (int32_t)it->second;
+    }
+    const uint64_t h = str_hash(s);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    const size_t mask = lookup.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const uint64_t v = lookup[i];
+      if (!v) return -1;
+      if ((uint32_t)(v >> 32) == tag && strings[(uint32_t)v - 1] == s) return (int32_t)((uint32_t)v - 1);
+    }
+  }
+  static uint64_t str_hash(std::string_view s) {  // 8 bytes a step, multiply-xorshift mixing
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (s.size() * 0xC2B2AE3D27D4EB4Full);
+    const char* p = s.data();
+    size_t n = s.size();
+    for (; n >= 8; n -= 8, p += 8) {
+      uint64_t w;
+      std::memcpy(&w, p, 8);
+      h = (h ^ (w * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
+      h ^= h >> 31;
+    }
+    if (n) {
+      uint64_t w = 0;
+      std::memcpy(&w, p, n);
+      h = (h ^ (w * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
+      h ^= h >> 31;
+    }
+    h *= 0xFF51AFD7ED558CCDull;
+    return h ^ (h >> 33);
   }
   std::vector<uint8_t> serialize() const;
   static std::shared_ptr<Image> deserialize(const uint8_t* p, size_t n);
@@ -81,12 +116,22 @@ struct RequestIn {
 // request's string base, stored at RH_SBASE when the block is appended).
 struct EncodedRequest {
   std::vector<uint32_t> blk, row;  // heap block; columnar row (RW_BLK set on append)
-  std::vector<std::string> strs;   // request-local strings
-  std::unordered_map<std::string, uint32_t> local;
-  void clear() { blk.clear(); row.clear(); strs.clear(); local.clear(); }
+  std::vector<std::string> strs;   // request-local strings (few per request: found by linear scan)
+  // interning memo over the source bytes' address: a value repeated from the same bytes (a group
+  // name as entity id, parent and attribute; a type-name literal) is looked up once
+  static constexpr uint32_t MEMO = 32;
+  const char* memo_p[MEMO];
+  uint32_t memo_len[MEMO], memo_id[MEMO], n_memo = 0;
+  void clear() { blk.clear(); row.clear(); strs.clear(); n_memo = 0; }
 };
 // Encodes (EntityMap, Request) for `img`. Thread-safe: reads the image only.
 void encode_request(const Image& img, const std::vector<EntityIn>& ents, const RequestIn& req, EncodedRequest& out);
+// The webhook's host steps for one SubjectAccessReview JSON body (GetAuthorizerAttributes,
+// Authorize's fast paths, RecordToCedarResource, encode_request) without intermediate trees.
+// Returns 1 with `out` encoded, 2 with a fast-path decision in fast/reason, or 0 when the body
+// uses something this path does not take (escapes, numbers, duplicate keys, malformed JSON ...):
+// the caller then runs the general path, which gives the identical encoding or error.
+int encode_sar_direct(const Image& img, const char* json, size_t n, EncodedRequest& out, int& fast, std::string& reason);
 
 // Host side of a device batch: encoded request heap + string table; results after evaluation.
 struct Batch {

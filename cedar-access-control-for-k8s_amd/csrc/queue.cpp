@@ -163,12 +163,8 @@ thread_local std::string t_err;
 
 // Encodes on the calling thread, joins the open batch, waits, and renders the caller's result
 // (authz: cg_batch_authz's Decision + reason; else cg_batch_decision + diagnostic).
-int submit_encoded(cg_queue* q, const std::vector<EntityIn>& ents, const RequestIn& req, int* out, char* buf,
+int submit_encoded(cg_queue* q, const std::shared_ptr<LoadedImage>& li, EncodedRequest& e, int* out, char* buf,
                    size_t cap, size_t* need, bool authz) {
-  auto li = active_image(q->ctx, t_err);
-  if (!li) return CG_E_STATE;
-  EncodedRequest e;
-  GUARD(t_err, { encode_request(*li->host, ents, req, e); })
   std::shared_ptr<QBatch> qb;
   uint32_t idx = 0;
   int rc = enqueue(q, li, e, qb, idx, t_err);
@@ -224,24 +220,38 @@ const char* cg_queue_last_error(void) { return t_err.c_str(); }
 int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* decision, char* reason, size_t cap,
                            size_t* need) {
   if (!q || !sar_json || !decision) return CG_E_ARG;
-  std::vector<EntityIn> ents;
-  RequestIn req;
-  GUARD(t_err, {
-    JVal v = json_parse(sar_json, len);
-    Attributes a = attributes_from_sar(v);
+  auto li = active_image(q->ctx, t_err);
+  if (!li) return CG_E_STATE;
+  EncodedRequest e;
+  {
+    int fast = -1;
     std::string r;
-    int fast = authorize_fast_path(a, r);
-    if (fast >= 0) {
+    int d;
+    GUARD(t_err, { d = encode_sar_direct(*li->host, sar_json, len, e, fast, r); })
+    if (d == 2) {
       q->n_fast++;
       *decision = fast;
       return put_string(r, reason, cap, need);
     }
-    record_to_cedar(a, ents, req);
-  })
-  return submit_encoded(q, ents, req, decision, reason, cap, need, true);
+    if (d == 0) {  // the general path: JSON tree, Attributes, entities
+      std::vector<EntityIn> ents;
+      RequestIn req;
+      GUARD(t_err, {
+        JVal v = json_parse(sar_json, len);
+        Attributes a = attributes_from_sar(v);
+        fast = authorize_fast_path(a, r);
+        if (fast >= 0) {
+          q->n_fast++;
+          *decision = fast;
+          return put_string(r, reason, cap, need);
+        }
+        record_to_cedar(a, ents, req);
+        encode_request(*li->host, ents, req, e);
+      })
+    }
+  }
+  return submit_encoded(q, li, e, decision, reason, cap, need, true);
 }
-
-
 
 int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
                                 size_t* need) {
@@ -252,7 +262,11 @@ int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, 
     JVal v = json_parse(item_json, len);
     decode_json_item(v, ents, req);
   })
-  return submit_encoded(q, ents, req, allow, diag, cap, need, false);
+  auto li = active_image(q->ctx, t_err);
+  if (!li) return CG_E_STATE;
+  EncodedRequest e;
+  GUARD(t_err, { encode_request(*li->host, ents, req, e); })
+  return submit_encoded(q, li, e, allow, diag, cap, need, false);
 }
 
 int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,

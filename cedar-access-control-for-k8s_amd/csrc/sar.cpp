@@ -9,8 +9,13 @@
 //   UserToCedarEntity                                              internal/server/entities/user.go:35-100
 //   ResourceRequestToPath                                          internal/server/entities/authorization.go:13-30
 #include <algorithm>
+#include <array>
 #include <cctype>
+#include <cstring>
+#include <deque>
+#include <string_view>
 
+#include "encode_impl.h"
 #include "sar.h"
 
 namespace cg {
@@ -298,6 +303,447 @@ void record_to_cedar(const Attributes& a, std::vector<EntityIn>& ents, RequestIn
   ents.push_back(std::move(re));
   req.context = HVal();
   req.context.k = VK::Rec;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Direct path: SubjectAccessReview bytes -> encoded request, without JVal / Attributes / HVal
+// trees. It restates the same functions as above over views into the body and hands the entities
+// to the shared encode_impl, so it yields the general path's exact words. Anything outside the
+// plain shape (escapes, numbers, duplicate extra keys, malformed JSON, ...) returns 0 and the
+// caller takes the general path.
+namespace {
+
+using SV = std::string_view;
+struct Bail {};
+
+struct Scan {
+  const char* p;
+  const char* e;
+  void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++; }
+  char peek() { ws(); if (p >= e) throw Bail{}; return *p; }
+  void expect(char c) { if (peek() != c) throw Bail{}; p++; }
+  SV str() {
+    expect('"');
+    const char* st = p;
+    while (p < e && *p != '"') {
+      if (*p == '\\') throw Bail{};
+      p++;
+    }
+    if (p >= e) throw Bail{};
+    return SV(st, (size_t)(p++ - st));
+  }
+  void lit(const char* w, size_t n) {
+    if ((size_t)(e - p) < n || std::memcmp(p, w, n)) throw Bail{};
+    p += n;
+  }
+  void skip(int depth) {
+    if (depth > 200) throw Bail{};
+    switch (peek()) {
+      case '{': obj([&](SV) { skip(depth + 1); }); return;
+      case '[': arr([&] { skip(depth + 1); }); return;
+      case '"': str(); return;
+      case 't': lit("true", 4); return;
+      case 'f': lit("false", 5); return;
+      case 'n': lit("null", 4); return;
+      default: throw Bail{};  // numbers and anything else: general path
+    }
+  }
+  template <class F>
+  void obj(F&& on_key) {
+    expect('{');
+    if (peek() == '}') { p++; return; }
+    for (;;) {
+      SV k = str();
+      expect(':');
+      on_key(k);
+      const char c = peek();
+      p++;
+      if (c == ',') continue;
+      if (c == '}') return;
+      throw Bail{};
+    }
+  }
+  template <class F>
+  void arr(F&& on_elem) {
+    expect('[');
+    if (peek() == ']') { p++; return; }
+    for (;;) {
+      on_elem();
+      const char c = peek();
+      p++;
+      if (c == ',') continue;
+      if (c == ']') return;
+      throw Bail{};
+    }
+  }
+  // str_or: the string, or "" for any other value (which is skipped)
+  SV str_or_skip() {
+    if (peek() == '"') return str();
+    skip(1);
+    return SV();
+  }
+  void strings(std::vector<SV>& out) {  // an array's string elements; a non-array gives none
+    if (peek() != '[') { skip(1); return; }
+    arr([&] { if (peek() == '"') out.push_back(str()); else skip(1); });
+  }
+};
+
+struct Req3 { SV key, op; std::vector<SV> values; bool is_obj = false; };
+
+void requirements(Scan& sc, std::vector<Req3>& out) {  // {"requirements": [{key, operator, values}]}
+  if (sc.peek() != '{') { sc.skip(1); return; }
+  bool seen_reqs = false;
+  sc.obj([&](SV k) {
+    if (k != "requirements" || seen_reqs) { sc.skip(1); return; }
+    seen_reqs = true;
+    if (sc.peek() != '[') { sc.skip(1); return; }
+    sc.arr([&] {
+      Req3 r;
+      if (sc.peek() != '{') { sc.skip(1); out.push_back(std::move(r)); return; }
+      r.is_obj = true;
+      bool sk = false, so = false, sv = false;
+      sc.obj([&](SV f) {
+        if (f == "key" && !sk) { sk = true; r.key = sc.str_or_skip(); }
+        else if (f == "operator" && !so) { so = true; r.op = sc.str_or_skip(); }
+        else if (f == "values" && !sv) { sv = true; sc.strings(r.values); }
+        else sc.skip(1);
+      });
+      out.push_back(std::move(r));
+    });
+  });
+}
+
+struct SarView {
+  SV user, uid;
+  std::vector<SV> groups;
+  std::vector<std::pair<SV, std::vector<SV>>> extra;
+  bool ra = false, nra = false;
+  SV verb, ns, group, version, resource, subresource, name, path, nra_verb;
+  std::vector<Req3> fsel, lsel;
+};
+
+void scan_sar(Scan& sc, SarView& v, std::deque<std::string>& arena) {
+  bool spec = false;
+  if (sc.peek() != '{') throw Bail{};
+  sc.obj([&](SV k) {
+    if (k != "spec" || spec) { sc.skip(1); return; }
+    spec = true;
+    if (sc.peek() != '{') throw Bail{};
+    uint32_t seen = 0;
+    auto first = [&](uint32_t bit) { const bool f = !(seen & bit); seen |= bit; return f; };
+    sc.obj([&](SV f) {
+      if (f == "user" && first(1)) v.user = sc.str_or_skip();
+      else if (f == "uid" && first(2)) v.uid = sc.str_or_skip();
+      else if (f == "groups" && first(4)) sc.strings(v.groups);
+      else if (f == "extra" && first(8)) {
+        if (sc.peek() != '{') { sc.skip(1); return; }
+        sc.obj([&](SV ek) {
+          SV key = ek;
+          if (std::any_of(ek.begin(), ek.end(), [](char c) { return c >= 'A' && c <= 'Z'; })) {
+            std::string low(ek);
+            for (auto& ch : low) ch = (char)std::tolower((unsigned char)ch);  // server.go:210
+            arena.push_back(std::move(low));
+            key = arena.back();
+          }
+          for (auto& x : v.extra) if (x.first == key) throw Bail{};  // merged keys: general path
+          v.extra.emplace_back(key, std::vector<SV>());
+          sc.strings(v.extra.back().second);
+        });
+      } else if (f == "resourceAttributes" && first(16)) {
+        if (sc.peek() != '{') { sc.skip(1); return; }
+        v.ra = true;
+        uint32_t rs = 0;
+        auto rfirst = [&](uint32_t bit) { const bool fr = !(rs & bit); rs |= bit; return fr; };
+        sc.obj([&](SV r) {
+          if (r == "verb" && rfirst(1)) v.verb = sc.str_or_skip();
+          else if (r == "namespace" && rfirst(2)) v.ns = sc.str_or_skip();
+          else if (r == "group" && rfirst(4)) v.group = sc.str_or_skip();
+          else if (r == "version" && rfirst(8)) v.version = sc.str_or_skip();
+          else if (r == "resource" && rfirst(16)) v.resource = sc.str_or_skip();
+          else if (r == "subresource" && rfirst(32)) v.subresource = sc.str_or_skip();
+          else if (r == "name" && rfirst(64)) v.name = sc.str_or_skip();
+          else if (r == "fieldSelector" && rfirst(128)) requirements(sc, v.fsel);
+          else if (r == "labelSelector" && rfirst(256)) requirements(sc, v.lsel);
+          else sc.skip(1);
+        });
+      } else if (f == "nonResourceAttributes" && first(32)) {
+        if (sc.peek() != '{') { sc.skip(1); return; }
+        v.nra = true;
+        uint32_t ns = 0;
+        sc.obj([&](SV r) {
+          if (r == "path" && !(ns & 1)) { ns |= 1; v.path = sc.str_or_skip(); }
+          else if (r == "verb" && !(ns & 2)) { ns |= 2; v.nra_verb = sc.str_or_skip(); }
+          else sc.skip(1);
+        });
+      } else {
+        sc.skip(1);
+      }
+    });
+  });
+  sc.ws();
+  if (sc.p != sc.e) throw Bail{};
+  if (!spec) throw Bail{};
+}
+
+// Flat value tree: strings, sets and records of the SAR entity model.
+struct LTree {
+  struct Node { uint8_t k; SV s; uint32_t first, n; };  // k: 0 string, 1 set, 2 record
+  std::vector<Node> nodes;
+  std::vector<uint32_t> kids;
+  std::vector<SV> keys;  // record field names, parallel to kids
+  uint32_t str(SV s) { nodes.push_back({0, s, 0, 0}); return (uint32_t)nodes.size() - 1; }
+  uint32_t str_set(const std::vector<SV>& vs) {  // str_set above: duplicates dropped
+    std::vector<uint32_t> el;
+    for (size_t i = 0; i < vs.size(); i++) {
+      bool dup = false;
+      for (size_t j = 0; j < i && !dup; j++) dup = vs[j] == vs[i];
+      if (!dup) el.push_back(str(vs[i]));
+    }
+    return set(el);
+  }
+  uint32_t set(const std::vector<uint32_t>& el) {
+    nodes.push_back({1, SV(), (uint32_t)kids.size(), (uint32_t)el.size()});
+    for (uint32_t x : el) { kids.push_back(x); keys.emplace_back(); }
+    return (uint32_t)nodes.size() - 1;
+  }
+  uint32_t rec(std::initializer_list<std::pair<SV, uint32_t>> f) {
+    nodes.push_back({2, SV(), (uint32_t)kids.size(), (uint32_t)f.size()});
+    for (auto& kv : f) { kids.push_back(kv.second); keys.push_back(kv.first); }
+    return (uint32_t)nodes.size() - 1;
+  }
+  uint32_t rec(const std::vector<std::pair<SV, uint32_t>>& f) {
+    nodes.push_back({2, SV(), (uint32_t)kids.size(), (uint32_t)f.size()});
+    for (auto& kv : f) { kids.push_back(kv.second); keys.push_back(kv.first); }
+    return (uint32_t)nodes.size() - 1;
+  }
+  // emit_value_impl (compiler.cpp) for these three kinds
+  void emit(uint32_t ni, std::vector<uint32_t>& out, const Image& img, EncodedRequest& E, uint32_t& w0,
+            uint32_t& w1) const {
+    using namespace cgi;
+    const Node& nd = nodes[ni];
+    if (nd.k == 0) { w0 = mk_w0(T_STR, 0); w1 = request_sid(img, E, nd.s); return; }
+    if (nd.k == 1) {
+      uint32_t ew[64];
+      std::vector<uint32_t> big;
+      uint32_t* w = nd.n <= 32 ? ew : (big.resize(2 * (size_t)nd.n), big.data());
+      for (uint32_t j = 0; j < nd.n; j++) emit(kids[nd.first + j], out, img, E, w[2 * j], w[2 * j + 1]);
+      const uint32_t off = (uint32_t)out.size();
+      out.push_back(nd.n);
+      out.insert(out.end(), w, w + 2 * (size_t)nd.n);
+      w0 = mk_w0(T_SET, mk_ref(SP_HEAP, off)); w1 = nd.n;
+      return;
+    }
+    std::array<uint32_t, 3> fw[8];  // the model's records have at most 7 fields
+    if (nd.n > 8) throw CedarError("record too wide for the direct SAR path");
+    for (uint32_t j = 0; j < nd.n; j++) {
+      uint32_t a, b;
+      emit(kids[nd.first + j], out, img, E, a, b);
+      fw[j] = {request_sid(img, E, keys[nd.first + j]), a, b};
+    }
+    std::sort(fw, fw + nd.n, [](const std::array<uint32_t, 3>& x, const std::array<uint32_t, 3>& y) { return x[0] < y[0]; });
+    const uint32_t off = (uint32_t)out.size();
+    out.push_back(nd.n);
+    for (uint32_t j = 0; j < nd.n; j++) { out.push_back(fw[j][0]); out.push_back(fw[j][1]); out.push_back(fw[j][2]); }
+    w0 = mk_w0(T_REC, mk_ref(SP_HEAP, off)); w1 = nd.n;
+  }
+};
+
+constexpr uint32_t NO_ATTRS = 0xFFFFFFFFu;
+
+struct LEnt {
+  SV type, id;
+  uint32_t attrs = NO_ATTRS;  // record node, or the empty record
+  std::vector<std::pair<SV, SV>> parents;
+};
+
+// the SAR's (EntityMap, Request) as an encode_impl source
+struct LSrc {
+  const LTree& t;
+  const std::vector<LEnt>& ents;
+  std::pair<SV, SV> p, a, r;
+  uint32_t n_ents() const { return (uint32_t)ents.size(); }
+  SV type(uint32_t i) const { return ents[i].type; }
+  SV id(uint32_t i) const { return ents[i].id; }
+  uint32_t n_parents(uint32_t i) const { return (uint32_t)ents[i].parents.size(); }
+  std::pair<SV, SV> parent(uint32_t i, uint32_t k) const { return ents[i].parents[k]; }
+  std::pair<SV, SV> principal() const { return p; }
+  std::pair<SV, SV> action() const { return a; }
+  std::pair<SV, SV> resource() const { return r; }
+  void emit_ctx(std::vector<uint32_t>& out, const Image&, EncodedRequest&, uint32_t& w0, uint32_t& w1) const {
+    enc::emit_empty_record(out, w0, w1);
+  }
+  void emit_attrs(uint32_t i, std::vector<uint32_t>& out, const Image& img, EncodedRequest& E, uint32_t& w0,
+                  uint32_t& w1) const {
+    if (ents[i].attrs == NO_ATTRS) enc::emit_empty_record(out, w0, w1);
+    else t.emit(ents[i].attrs, out, img, E, w0, w1);
+  }
+};
+
+bool sv_starts(SV s, SV p) { return s.substr(0, p.size()) == p; }
+
+// i-th ':'-separated field of s
+SV colon_field(SV s, int i) {
+  size_t st = 0;
+  for (int k = 0; k < i; k++) st = s.find(':', st) + 1;
+  const size_t e = s.find(':', st);
+  return s.substr(st, e == SV::npos ? SV::npos : e - st);
+}
+
+}  // namespace
+
+int encode_sar_direct(const Image& img, const char* json, size_t n, EncodedRequest& out, int& fast, std::string& reason) {
+  SarView v;
+  std::deque<std::string> arena;
+  try {
+    Scan sc{json, json + n};
+    scan_sar(sc, v, arena);
+  } catch (const Bail&) {
+    return 0;
+  }
+  const bool resource_request = v.nra ? false : v.ra;
+  const SV verb = v.nra ? v.nra_verb : v.verb;
+  const SV api_group = v.group, resource = v.resource;
+  // Authorize fast paths (authorize_fast_path above)
+  const bool ro = verb == "get" || verb == "list" || verb == "watch";
+  if (v.user == kSelf && ro && api_group == "cedar.k8s.aws" && resource == "policies") {
+    fast = AUTHZ_ALLOW;
+    reason = "cedar authorizer is always allowed to access policies";
+    return 2;
+  }
+  if (v.user == kSelf && ro && api_group == "rbac.authorization.k8s.io") {
+    fast = AUTHZ_ALLOW;
+    reason = "cedar authorizer is always allowed to read RBAC policies";
+    return 2;
+  }
+  if (sv_starts(v.user, "system:") && !sv_starts(v.user, "system:serviceaccount:") && !sv_starts(v.user, "system:node:")) {
+    fast = AUTHZ_NO_OPINION;
+    reason.clear();
+    return 2;
+  }
+  // RecordToCedarResource / UserToCedarEntity (record_to_cedar, user_to_cedar above)
+  LTree t;
+  std::vector<LEnt> ents;
+  ents.reserve(v.groups.size() + 2);
+  LEnt pe;
+  for (SV g : v.groups) {
+    LEnt ge;
+    ge.type = kGroup;
+    ge.id = g;
+    ge.attrs = t.rec({{"name", t.str(g)}});
+    ents.push_back(std::move(ge));
+    const std::pair<SV, SV> pu{kGroup, g};
+    if (std::find(pe.parents.begin(), pe.parents.end(), pu) == pe.parents.end()) pe.parents.push_back(pu);
+  }
+  SV ptype = kUser, pname = v.user, pns;
+  bool sa = false;
+  const auto colons = std::count(v.user.begin(), v.user.end(), ':');
+  if (sv_starts(v.user, "system:node:") && colons == 2) { ptype = kNode; pname = colon_field(v.user, 2); }
+  if (sv_starts(v.user, "system:serviceaccount:") && colons == 3) {
+    ptype = kSA;
+    sa = true;
+    pname = colon_field(v.user, 3);
+    pns = colon_field(v.user, 2);
+  }
+  {
+    std::vector<std::pair<SV, uint32_t>> f{{"name", t.str(pname)}};
+    if (sa) f.emplace_back("namespace", t.str(pns));
+    if (!v.extra.empty()) {
+      std::vector<uint32_t> xs;
+      for (auto& kv : v.extra) xs.push_back(t.rec({{"key", t.str(kv.first)}, {"values", t.str_set(kv.second)}}));
+      f.emplace_back("extra", t.set(xs));
+    }
+    pe.attrs = t.rec(f);
+  }
+  pe.type = ptype;
+  pe.id = v.uid;
+  ents.push_back(std::move(pe));
+  LEnt re;
+  if (!resource_request) {
+    re.type = kNonResourceURL;
+    re.id = v.path;
+    re.attrs = t.rec({{"path", t.str(v.path)}});
+  } else if (verb == "impersonate") {
+    if (resource == "serviceaccounts") {
+      re.type = kSA;
+      arena.push_back("system:serviceaccount:" + std::string(v.ns) + ":" + std::string(v.name));
+      re.id = arena.back();
+      re.attrs = t.rec({{"name", t.str(v.name)}, {"namespace", t.str(v.ns)}});
+    } else if (resource == "uids") {
+      re.type = kPrincipalUID;
+      re.id = v.name;
+    } else if (resource == "users") {
+      re.type = kUser;
+      SV nm = v.name;
+      if (sv_starts(v.name, "system:node:") && std::count(v.name.begin(), v.name.end(), ':') == 2) {
+        re.type = kNode;
+        nm = colon_field(v.name, 2);
+      }
+      re.attrs = t.rec({{"name", t.str(nm)}});
+      re.id = v.name;
+    } else if (resource == "groups") {
+      re.type = kGroup;
+      re.id = v.name;
+      re.attrs = t.rec({{"name", t.str(v.name)}});
+    } else if (resource == "userextras") {
+      re.type = kExtra;
+      re.id = v.subresource;
+      std::vector<std::pair<SV, uint32_t>> f{{"key", t.str(v.subresource)}};
+      if (!v.name.empty()) f.emplace_back("value", t.str(v.name));
+      re.attrs = t.rec(f);
+    }
+  } else {
+    re.type = kResource;
+    {  // resource_request_to_path
+      std::string path = v.group.empty() ? std::string("/api") : "/apis/" + std::string(v.group);
+      path += '/';
+      path += v.version;
+      if (!v.ns.empty()) { path += "/namespaces/"; path += v.ns; }
+      path += '/';
+      path += v.resource;
+      if (!v.name.empty()) { path += '/'; path += v.name; }
+      if (!v.subresource.empty()) { path += '/'; path += v.subresource; }
+      arena.push_back(std::move(path));
+      re.id = arena.back();
+    }
+    std::vector<std::pair<SV, uint32_t>> f{{"apiGroup", t.str(v.group)}, {"resource", t.str(v.resource)}};
+    if (!v.name.empty()) f.emplace_back("name", t.str(v.name));
+    if (!v.subresource.empty()) f.emplace_back("subresource", t.str(v.subresource));
+    if (!v.ns.empty()) f.emplace_back("namespace", t.str(v.ns));
+    std::vector<uint32_t> ls;
+    for (auto& r : v.lsel) {  // attributes_from_sar's labelSelector filter
+      if (!r.is_obj) continue;
+      SV op;
+      if (r.op == "In") op = "in";
+      else if (r.op == "NotIn") op = "notin";
+      else if (r.op == "Exists") op = "exists";
+      else if (r.op == "DoesNotExist") op = "!";
+      else continue;
+      if (!valid_label_key(std::string(r.key))) continue;
+      if ((op == "in" || op == "notin") && r.values.empty()) continue;
+      if ((op == "exists" || op == "!") && !r.values.empty()) continue;
+      bool ok = true;
+      for (SV x : r.values) if (!valid_label_value(std::string(x))) ok = false;
+      if (!ok) continue;
+      ls.push_back(t.rec({{"key", t.str(r.key)}, {"operator", t.str(op)}, {"values", t.str_set(r.values)}}));
+    }
+    if (!ls.empty()) f.emplace_back("labelSelector", t.set(ls));
+    std::vector<uint32_t> fs;
+    for (auto& r : v.fsel) {
+      if (!r.is_obj || r.values.size() > 1) continue;
+      SV op;
+      if (r.op == "In" && r.values.size() == 1) op = "=";
+      else if (r.op == "NotIn" && r.values.size() == 1) op = "!=";
+      else continue;
+      fs.push_back(t.rec({{"field", t.str(r.key)}, {"operator", t.str(op)}, {"value", t.str(r.values[0])}}));
+    }
+    if (!fs.empty()) f.emplace_back("fieldSelector", t.set(fs));
+    re.attrs = t.rec(f);
+  }
+  const std::pair<SV, SV> ru{re.type, re.id};
+  ents.push_back(std::move(re));
+  const std::pair<SV, SV> pu{ptype, v.uid}, au{kAction, verb};
+  encode_impl(img, LSrc{t, ents, pu, au, ru}, out);
+  return 1;
 }
 
 }  // namespace cg

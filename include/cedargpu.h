@@ -137,6 +137,12 @@ int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len);
 /* Host-only: the (EntityMap, Request) the SAR path builds, as {"fast":d,"reason":r} for a fast-path
  * item or {"entities":[...],"request":{...}} (Cedar JSON) — for parity tests of the encoder. */
 int cg_sar_to_cedar_json(const char* sar_json, size_t len, char* out, size_t cap, size_t* need);
+/* Host-only consistency check of the SubjectAccessReview encoders: every element of the JSON
+ * array `sars` goes through the direct path (views into the body, no trees) and the general path
+ * (JSON tree -> Attributes -> entities -> encoder) for `image`; *n_direct counts the elements the
+ * direct path took, *n_mismatch those whose encodings (or fast-path results) differ. */
+int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t n, uint32_t* n_items,
+                        uint32_t* n_direct, uint32_t* n_mismatch, int64_t* first_mismatch);
 /* authorizer.Decision for item i (0 Deny, 1 Allow, 2 NoOpinion) and the reason string the
  * reference returns (diagnosticToReason JSON, a fast-path literal, or ""). */
 int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t cap, size_t* need);
