@@ -64,10 +64,11 @@ struct KArgs {
   uint32_t* __restrict__ reasons_p;
   uint32_t* __restrict__ errs;
   const uint32_t* __restrict__ btab;     // scope index (indexed kernel)
-  const uint32_t* __restrict__ brefs;
+  const uint32_t* __restrict__ bfilt;    // key filter (image.h filt_*)
   const uint32_t* __restrict__ bstream;
   const uint32_t* __restrict__ rows;     // columnar request rows (row_words each)
-  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, row_words, combo_mask;
+  unsigned long long* stats;             // probe-kernel work counters (STATS variant only)
+  uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
 };
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
@@ -1238,11 +1239,25 @@ __device__ __forceinline__ uint2 key_comp(uint32_t kc, uint32_t j, uint32_t st, 
            : make_uint2(st, si);
 }
 
+// key filter: false = the key is certainly absent from the scope index
+__device__ __forceinline__ bool filt_maybe(const uint32_t* bfilt, uint32_t fmask, uint32_t hash) {
+  const uint32_t y = filt_mix(hash), bits = filt_bits(y);
+  const uint2 w = *reinterpret_cast<const uint2*>(bfilt + 2 * (size_t)(y & fmask));
+  bool ok = true;
+  for (uint32_t j = 0; j < 3; j++) {
+    const uint32_t b = (bits >> (6 * j)) & 63u;
+    ok = ok && (((b < 32 ? w.x : w.y) >> (b & 31)) & 1u);
+  }
+  return ok;
+}
+
 // probe: (first, count, hmask) of the slot matching key words w0..w6 (+ v0, v1 for level 2)
+template <bool ST = false>
 __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uint32_t hash, uint32_t w0, uint2 p, uint2 q,
-                                       uint2 r, uint32_t v0, uint32_t v1) {
+                                       uint2 r, uint32_t v0, uint32_t v1, uint32_t& steps) {
   uint32_t h = hash & bmask;
   for (;;) {
+    if (ST) steps++;
     const uint4* sl = reinterpret_cast<const uint4*>(btab + (size_t)h * BT_WORDS);
     const uint4 x = sl[0];
     if (x.x == 0) return make_uint3(0, 0, 0);
@@ -1258,8 +1273,13 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
 // SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
 // (row -> level-1 probe -> level-2 probe -> head -> atom data) overlap. Collectives (ballot, scan,
 // min, broadcast) are segment-local; loops run while any segment of the wave has work.
-template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1>
+// STATS: also counts the work per request into a.stats (profiling variant, CEDARGPU_PROBE_STATS=1):
+// [0] requests [1] level-1 keys [2] level-1 buckets found [3] level-2 probes [4] level-2 buckets
+// found [5] table slots visited [6] candidate heads [7] heads passing the scope re-check
+// [8] atoms evaluated [9] hits [10] stage flushes [11] candidate passes [12] wave cycles (s_memtime)
+template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false>
 __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
+  const uint64_t t_start = STATS ? clock64() : 0;
   using L = SegLds<SEG, HCAP>;
   static_assert(L::HC <= 4096 && L::XC <= 255, "hit slots are 12-bit sort payloads, error slots 8-bit");
   constexpr uint32_t NS = L::NS;
@@ -1338,6 +1358,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
     }
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
+  uint32_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // STATS only (per lane)
   for (;;) {
     const bool l2 = sballot(hm != 0) != 0;
     const bool done = !l2 && kb >= n_keys;
@@ -1351,7 +1372,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
             hm &= hm - 1;
             const uint2 v = wl.hot[seg][h];
             const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
-            e = probe(a.btab, a.bmask, bucket_hash2(h1, h, v0, v1), w0 | BT_L2 | h, kp, ka, kr, v0, v1);
+            const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
+            if (filt_maybe(a.bfilt, a.fmask, h2))
+              e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, st[5]);
+            if (STATS) { st[3]++; st[4] += e.y != 0; }
           }
         } else {
           const uint32_t k = kb + sl;
@@ -1375,8 +1399,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
             kr = key_comp(rkc, ir, c.rt, c.ri, c.blk, c.r_anc);
             w0 = BT_USED | (combo << 16);
             h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
-            e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0);
+            if (filt_maybe(a.bfilt, a.fmask, h1)) e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5]);
             hm = e.z;
+            if (STATS) { st[1]++; st[2] += e.y != 0; }
           }
         }
       }
@@ -1452,12 +1477,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
         const uint32_t na = q3.x / ATOM_WORDS;
         const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
         uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
+        if (STATS) { st[6] += idx < total; st[7] += ok; st[11] += sl == 0; }
         bool err = false;
         Err e{0, 0, 0, 0, 0};
         while (__ballot(pc < na)) {
           if (pc < na) {
             const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
             const uint32_t rr = eval_atom<false>(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
+            if (STATS) st[8]++;
             if (rr == 3u) { general = true; pc = AT_UNSAT; }
             else if (rr == 2u) { err = true; pc = AT_UNSAT; }
             else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
@@ -1465,6 +1492,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
         }
         // record hits (segment-local slots)
         const bool hit = ok && (err || pc == AT_SAT);
+        if (STATS) st[9] += hit;
         const uint64_t hmask = sballot(hit), xmask = sballot(hit && err);
         if (hit) {
           const uint32_t pos = nh + mbcnt64(hmask);
@@ -1485,9 +1513,24 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
         min_tier = min(min_tier, smin(hit ? tier : 0xFFu));
       }
       ne = 0;
+      if (STATS && sl == 0) st[10]++;
       wave_lds_sync();
     }
     if (all_done) break;
+  }
+  if (STATS) {
+    if (valid && sl == 0) st[0] = 1;
+    for (uint32_t i = 0; i < 12; i++) {
+      uint32_t x = valid ? st[i] : 0u;
+      for (uint32_t o = SEG / 2; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, (int)o);
+      if (sl == 0 && x) atomicAdd(a.stats + i, (unsigned long long)x);
+    }
+    if (lane == 0) {
+      const unsigned long long dt = (unsigned long long)(clock64() - t_start);
+      atomicAdd(a.stats + 12, dt);
+      atomicMax(a.stats + 13, dt);
+      atomicAdd(a.stats + 14, 1ull);
+    }
   }
 
   // ---- merge: deciding tier, duplicates, policy order ----
@@ -1626,9 +1669,10 @@ int dev_image_upload(int device, const Image& img, DevImage* out) {
   if ((rc = up(&d.hot, img.hot, d.bytes, s))) return rc;
   if ((rc = up(&d.act, img.act, d.bytes, s))) return rc;
   if ((rc = up(&d.btab, img.btab, d.bytes, s))) return rc;
-  if ((rc = up(&d.brefs, img.brefs, d.bytes, s))) return rc;
+  if ((rc = up(&d.bfilt, img.bfilt, d.bytes, s))) return rc;
   if ((rc = up(&d.bstream, img.bstream, d.bytes, s))) return rc;
   d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
+  d.fmask = (uint32_t)(img.bfilt.size() / 2) - 1;
   d.indexed = img.indexed;
   d.combo_mask = img.combo_mask;
   d.n_act = (uint32_t)img.act.size() / 2;
@@ -1648,7 +1692,7 @@ void dev_image_free(DevImage* d) {
   if (d->device < 0) return;
   (void)hipSetDevice(d->device);
   for (void* p : {(void*)d->pstream, (void*)d->tier_cend, (void*)d->chunks, (void*)d->cpool, (void*)d->gstr_off,
-                  (void*)d->hot, (void*)d->act, (void*)d->gstr_bytes, (void*)d->btab, (void*)d->brefs,
+                  (void*)d->hot, (void*)d->act, (void*)d->gstr_bytes, (void*)d->btab, (void*)d->bfilt,
                   (void*)d->bstream})
     if (p) (void)hipFree(p);
   *d = DevImage();
@@ -1786,8 +1830,9 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.n_pol = img.n_pol; k.n_tiers = img.n_tiers; k.n_gstr = img.n_gstr; k.n_hot = img.n_hot;
   k.act = img.act; k.n_act = img.n_act; k.amask_ok = img.amask_ok;
   k.n_req = n; k.capr = capr; k.cape = cape;
-  k.btab = img.btab; k.brefs = img.brefs; k.bstream = img.bstream; k.bmask = img.bmask;
+  k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
+  k.stats = nullptr;
   return k;
 }
 
@@ -1818,10 +1863,36 @@ static uint32_t probe_occ() {
   return occ;
 }
 
+// CEDARGPU_PROBE_STATS=1: every default-variant launch runs the counting variant, synchronously,
+// and prints its per-request work profile to stderr (profiling only).
+static bool probe_stats() {
+  static const bool on = std::getenv("CEDARGPU_PROBE_STATS") != nullptr;
+  return on;
+}
+
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
   const uint32_t seg = big ? 64u : probe_seg(), per_block = WAVES * (64 / seg);
   const dim3 grid((n + per_block - 1) / per_block);
   const uint32_t occ = probe_occ();
+  if (!big && probe_stats()) {
+    static unsigned long long* dstats = nullptr;
+    if (!dstats && hipMalloc((void**)&dstats, 16 * sizeof(unsigned long long)) != hipSuccess) return;
+    KArgs ks = k;
+    ks.stats = dstats;
+    unsigned long long h[16] = {0};
+    (void)hipMemsetAsync(dstats, 0, sizeof(h), s);
+    hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, true>), grid, dim3(BLOCK), 0, s, ks);
+    (void)hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    const double r = h[0] ? (double)h[0] : 1.0, w = h[14] ? (double)h[14] : 1.0;
+    std::fprintf(stderr,
+                 "probe stats: requests %llu | per request: L1 keys %.2f found %.2f | L2 probes %.2f found %.2f | "
+                 "slots %.2f | heads %.2f scope-ok %.2f | atoms %.2f | hits %.2f | stage flushes %.2f | "
+                 "candidate passes %.2f | wave cycles mean %.0f max %llu\n",
+                 h[0], h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[5] / r, h[6] / r, h[7] / r, h[8] / r, h[9] / r,
+                 h[10] / r, h[11] / r, h[12] / w, h[13]);
+    return;
+  }
   if (big) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16 && occ == 5) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5>), grid, dim3(BLOCK), 0, s, k);

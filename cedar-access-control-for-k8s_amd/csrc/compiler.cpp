@@ -852,11 +852,11 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   using L1 = std::array<uint32_t, 7>;                   // (combo, pt, pi, at, ai, rt, ri)
   using L2 = std::pair<L1, std::array<uint32_t, 3>>;    // (+ h, v0, v1)
   const uint32_t n = img.n_pol();
-  img.btab.clear(); img.brefs.clear(); img.bstream.clear();
+  img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
   img.combo_mask = 0;
   img.indexed = (n > 0 && img.n_atomic == n) ? 1u : 0u;
   if (!img.indexed) {
-    img.btab.assign(BT_WORDS, 0); img.brefs.assign(1, 0); img.bstream.assign(HEAD_WORDS, 0);
+    img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
     return;
   }
   // stream record offset / length of every policy
@@ -940,12 +940,24 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     std::copy(e, e + BT_WORDS, &img.btab[(size_t)h * BT_WORDS]);
   };
   auto l1_hash = [](const L1& k) { return key_hash(k[0], k[1], k[2], k[3], k[4], k[5], k[6]); };
+  size_t blocks = 16;
+  while (blocks * 4 < n_entries) blocks <<= 1;  // >= 16 bits per entry
+  img.bfilt.assign(2 * blocks, 0);
+  auto filt_add = [&](uint32_t hash) {
+    const uint32_t y = filt_mix(hash), bits = filt_bits(y);
+    const size_t blk = y & (blocks - 1);
+    for (uint32_t j = 0; j < 3; j++) {
+      const uint32_t b = (bits >> (6 * j)) & 63u;
+      img.bfilt[2 * blk + (b >> 5)] |= 1u << (b & 31);
+    }
+  };
   for (auto& kv : b1) {
     const L1& k = kv.first;
     const uint32_t first = put_heads(kv.second);
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], 0, 0, first,
                                   (uint32_t)kv.second.size(), hmask.count(k) ? hmask[k] : 0u, 0, 0, 0, 0};
     insert(l1_hash(k), e);
+    filt_add(l1_hash(k));
   }
   for (auto& kv : b2) {
     const L1& k = kv.first.first;
@@ -954,8 +966,8 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16) | BT_L2 | x[0], k[1], k[2], k[3], k[4], k[5], k[6], x[1], x[2],
                                   first, (uint32_t)kv.second.size(), 0, 0, 0, 0, 0};
     insert(bucket_hash2(l1_hash(k), x[0], x[1], x[2]), e);
+    filt_add(bucket_hash2(l1_hash(k), x[0], x[1], x[2]));
   }
-  img.brefs.assign(1, 0);
 }
 
 std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch) {
@@ -1088,7 +1100,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.vec(pol); w.vec(tier_end); w.vec(code); w.vec(cpool); w.vec(gstr_off); w.vec(hot); w.bytes(gstr_bytes);
   w.vec(act); w.u32(amask_ok); w.u32(n_atomic);
   w.vec(pstream); w.vec(chunks); w.vec(tier_cend);
-  w.vec(btab); w.vec(brefs); w.vec(bstream); w.u32(indexed); w.u32(combo_mask);
+  w.vec(btab); w.vec(bfilt); w.vec(bstream); w.u32(indexed); w.u32(combo_mask);
   w.u32((uint32_t)strings.size());
   for (auto& s : strings) w.str(s);
   w.u32((uint32_t)meta.size());
@@ -1112,7 +1124,11 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->gstr_off = r.vec(); img->hot = r.vec(); img->gstr_bytes = r.bytes();
   img->act = r.vec(); img->amask_ok = r.u32(); img->n_atomic = r.u32();
   img->pstream = r.vec(); img->chunks = r.vec(); img->tier_cend = r.vec();
-  img->btab = r.vec(); img->brefs = r.vec(); img->bstream = r.vec(); img->indexed = r.u32(); img->combo_mask = r.u32();
+  img->btab = r.vec(); img->bfilt = r.vec(); img->bstream = r.vec(); img->indexed = r.u32(); img->combo_mask = r.u32();
+  {
+    const size_t nb = img->btab.size() / BT_WORDS, nf = img->bfilt.size();
+    if (!nb || (nb & (nb - 1)) || nf < 2 || (nf & (nf - 1))) throw CedarError("corrupt image (scope index)");
+  }
   uint32_t ns = r.u32();
   for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }
   uint32_t nm = r.u32();

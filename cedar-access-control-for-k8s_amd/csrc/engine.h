@@ -36,7 +36,7 @@ struct Image {
   uint32_t amask_ok = 0;      // 1 when act has <= MAX_ACT entries (PW_AMASK* valid)
   uint32_t n_atomic = 0;      // policies compiled to atoms (statistics)
   // scope index over atomic policies (image.h "scope index"); indexed = every policy is atomic
-  std::vector<uint32_t> btab, brefs, bstream;
+  std::vector<uint32_t> btab, bfilt, bstream;  // bfilt: key filter, 2 words per block
   uint32_t indexed = 0;
   uint32_t combo_mask = 0;  // level-1 key combos in use (bit key_combo(..))
   std::vector<uint8_t> gstr_bytes;

@@ -135,6 +135,20 @@ __host__ __device__ constexpr inline uint32_t bucket_hash2(uint32_t l1, uint32_t
   return h;
 }
 
+// Key filter of the scope index (bfilt): a blocked Bloom filter over the level-1 and level-2 key
+// hashes, 3 bits in one 64-bit block (two words) per key, about 16 bits per entry. Most probes
+// miss (a request enumerates ~11 level-1 keys and finds ~0.3), and a miss then costs one small,
+// cache-resident load instead of a walk over 64-byte table slots.
+__host__ __device__ constexpr inline uint32_t filt_mix(uint32_t x) {
+  x ^= 0x5BD1E995u;
+  x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+  return x;
+}
+// bits (b0 | b1 << 6 | b2 << 12) of hash x's 64-bit block
+__host__ __device__ constexpr inline uint32_t filt_bits(uint32_t y) {
+  return ((y >> 14) & 63u) | (((y >> 20) & 63u) << 6) | (((y * 0x9E3779B1u) >> 26) << 12);
+}
+
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
 __host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_t ei) {
   return ((et * 0x9E3779B1u) ^ (ei * 0x85EBCA77u) ^ ((ei >> 16) * 0xC2B2AE3Du)) >> 25;
