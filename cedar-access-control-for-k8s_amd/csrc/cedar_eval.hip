@@ -26,6 +26,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <algorithm>
 #include <vector>
 #include <string>
 
@@ -1273,10 +1274,12 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
 // SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
 // (row -> level-1 probe -> level-2 probe -> head -> atom data) overlap. Collectives (ballot, scan,
 // min, broadcast) are segment-local; loops run while any segment of the wave has work.
-// STATS: also counts the work per request into a.stats (profiling variant, CEDARGPU_PROBE_STATS=1):
-// [0] requests [1] level-1 keys [2] level-1 buckets found [3] level-2 probes [4] level-2 buckets
-// found [5] table slots visited [6] candidate heads [7] heads passing the scope re-check
-// [8] atoms evaluated [9] hits [10] stage flushes [11] candidate passes [12] wave cycles (s_memtime)
+// STATS: also records, per wave, its work and phase times at a.stats[wave * 16 + i] (profiling
+// variant, CEDARGPU_PROBE_STATS=1): [0] requests [1] level-1 keys [2] level-1 buckets found
+// [3] level-2 probes [4] level-2 buckets found [5] table slots visited [6] candidate heads
+// [7] heads passing the scope re-check [8] atoms evaluated [9] hits [10] stage flushes
+// [11] candidate passes; cycles (s_memtime) in [12] row / hot / action loading [13] key probing
+// [14] candidate evaluation [15] merge and result writes
 template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false>
 __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
   const uint64_t t_start = STATS ? clock64() : 0;
@@ -1343,6 +1346,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
   }
   wave_lds_sync();
 
+  const uint64_t t_load = STATS ? clock64() : 0;
+  uint64_t t_cand = 0;
   uint32_t min_tier = a.n_tiers - 1;  // lowest tier with a hit so far (segment-uniform)
   uint32_t nh = 0, nx = 0;            // hits / error details recorded (may exceed capacity)
   uint32_t ne = 0;                    // found buckets staged
@@ -1417,6 +1422,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
       wave_lds_sync();
     }
     if (all_done || __ballot(ne + SEG > L::EC)) {
+      const uint64_t t_c0 = STATS ? clock64() : 0;
       // ---- run every segment's staged buckets ----
       uint32_t carry = 0;
       for (uint32_t b0 = 0; __ballot(b0 < ne); b0 += SEG) {
@@ -1515,24 +1521,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
       ne = 0;
       if (STATS && sl == 0) st[10]++;
       wave_lds_sync();
+      if (STATS) t_cand += clock64() - t_c0;
     }
     if (all_done) break;
   }
-  if (STATS) {
-    if (valid && sl == 0) st[0] = 1;
-    for (uint32_t i = 0; i < 12; i++) {
-      uint32_t x = valid ? st[i] : 0u;
-      for (uint32_t o = SEG / 2; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, (int)o);
-      if (sl == 0 && x) atomicAdd(a.stats + i, (unsigned long long)x);
-    }
-    if (lane == 0) {
-      const unsigned long long dt = (unsigned long long)(clock64() - t_start);
-      atomicAdd(a.stats + 12, dt);
-      atomicMax(a.stats + 13, dt);
-      atomicAdd(a.stats + 14, 1ull);
-    }
-  }
-
+  const uint64_t t_loop = STATS ? clock64() : 0;
   // ---- merge: deciding tier, duplicates, policy order ----
   const uint32_t t = min_tier;
   const bool structural = sballot(general) != 0;
@@ -1595,6 +1588,22 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
     if (nr > a.capr || nerr > a.cape) fl |= RF_OVERFLOW;
     a.res[2 * (size_t)gid] = dec | (t << 8) | (fl << 16);
     a.res[2 * (size_t)gid + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
+  }
+  if (STATS) {
+    if (valid && sl == 0) st[0] = 1;
+    const uint64_t t_end = clock64();
+    unsigned long long* w = a.stats + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
+    for (uint32_t i = 0; i < 12; i++) {
+      uint32_t x = valid ? st[i] : 0u;
+      for (uint32_t o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, (int)o);
+      if (lane == 0) w[i] = x;
+    }
+    if (lane == 0) {
+      w[12] = t_load - t_start;
+      w[13] = (t_loop - t_load) - t_cand;
+      w[14] = t_cand;
+      w[15] = t_end - t_loop;
+    }
   }
 }
 
@@ -1875,22 +1884,33 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
   const dim3 grid((n + per_block - 1) / per_block);
   const uint32_t occ = probe_occ();
   if (!big && probe_stats()) {
-    static unsigned long long* dstats = nullptr;
-    if (!dstats && hipMalloc((void**)&dstats, 16 * sizeof(unsigned long long)) != hipSuccess) return;
+    const size_t nw = (size_t)grid.x * WAVES;
+    unsigned long long* dstats = nullptr;
+    if (hipMalloc((void**)&dstats, nw * 16 * sizeof(unsigned long long)) != hipSuccess) return;
     KArgs ks = k;
     ks.stats = dstats;
-    unsigned long long h[16] = {0};
-    (void)hipMemsetAsync(dstats, 0, sizeof(h), s);
+    std::vector<unsigned long long> h(nw * 16);
+    (void)hipMemsetAsync(dstats, 0, h.size() * sizeof(unsigned long long), s);
     hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, true>), grid, dim3(BLOCK), 0, s, ks);
-    (void)hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(h.data(), dstats, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
-    const double r = h[0] ? (double)h[0] : 1.0, w = h[14] ? (double)h[14] : 1.0;
+    (void)hipFree(dstats);
+    double sum[16] = {0};
+    std::vector<unsigned long long> tot(nw);
+    for (size_t w = 0; w < nw; w++) {
+      for (int i = 0; i < 16; i++) sum[i] += (double)h[w * 16 + i];
+      tot[w] = h[w * 16 + 12] + h[w * 16 + 13] + h[w * 16 + 14] + h[w * 16 + 15];
+    }
+    std::sort(tot.begin(), tot.end());
+    const double r = sum[0] > 0 ? sum[0] : 1.0, W = (double)nw;
     std::fprintf(stderr,
-                 "probe stats: requests %llu | per request: L1 keys %.2f found %.2f | L2 probes %.2f found %.2f | "
+                 "probe stats: requests %.0f | per request: L1 keys %.2f found %.2f | L2 probes %.2f found %.2f | "
                  "slots %.2f | heads %.2f scope-ok %.2f | atoms %.2f | hits %.2f | stage flushes %.2f | "
-                 "candidate passes %.2f | wave cycles mean %.0f max %llu\n",
-                 h[0], h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[5] / r, h[6] / r, h[7] / r, h[8] / r, h[9] / r,
-                 h[10] / r, h[11] / r, h[12] / w, h[13]);
+                 "candidate passes %.2f\n  per wave cycles: load %.0f probe %.0f candidates %.0f merge %.0f | total p50 %llu "
+                 "p90 %llu p99 %llu max %llu\n",
+                 sum[0], sum[1] / r, sum[2] / r, sum[3] / r, sum[4] / r, sum[5] / r, sum[6] / r, sum[7] / r, sum[8] / r,
+                 sum[9] / r, sum[10] / r, sum[11] / r, sum[12] / W, sum[13] / W, sum[14] / W, sum[15] / W, tot[nw / 2],
+                 tot[nw * 9 / 10], tot[nw * 99 / 100], tot[nw - 1]);
     return;
   }
   if (big) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024>), grid, dim3(BLOCK), 0, s, k);
