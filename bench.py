@@ -180,7 +180,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=200)
     ap.add_argument("--latency-batch", type=int, default=2048)
-    ap.add_argument("--serve-threads", type=int, default=64,
+    ap.add_argument("--serve-threads", type=int, default=256,
                     help="caller threads of the serving-queue check (0: skip)")
     ap.add_argument("--serve-requests", type=int, default=262_144)
     ap.add_argument("--serve-max-batch", type=int, default=8192)
