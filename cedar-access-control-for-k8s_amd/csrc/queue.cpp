@@ -3,20 +3,20 @@
 //
 // The reference's webhook answers each SubjectAccessReview in its own goroutine with one
 // PolicySet.IsAuthorized call (internal/server/authorizer/authorizer.go:36-86). Here every caller
-// thread parses and converts its own request (SAR -> attributes -> fast path -> entities, the
-// reference's RecordToCedarResource at authorizer.go:89) outside any lock, appends the columnar
-// encoding to the open batch under the queue lock, and blocks. One flusher thread closes the open
-// batch when it holds `max_batch` requests or its oldest request has waited `max_delay_us`, runs
-// it (one H2D copy, one kernel launch, one D2H copy, overflow re-runs), and wakes its callers, who
-// render their own decision and reason in parallel. While a batch is on the device the next one
-// fills, so the batch size adapts to the offered load.
+// thread parses, converts and encodes its own request (SAR -> attributes -> fast path -> entities
+// -> position-independent request block) with no lock held, hands the block to one of 16 stripes
+// (a mutex held for one pointer push) and sleeps. One flusher thread drains the stripes into a
+// device batch (at most `max_batch` requests; with `max_delay_us` > 0 it first lets the batch fill
+// for that long after its first request), submits it, builds the next batch while the device runs
+// this one, then publishes the results with one futex wake for every waiting caller. Callers
+// render their own decision and reason in parallel. The batch size adapts to the offered load.
 #include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <thread>
 
 #include "capi_internal.h"
@@ -29,13 +29,29 @@ namespace {
 
 struct QBatch {
   cg_batch* b = nullptr;
-  Clock::time_point t0;  // arrival of the first request
-  std::mutex mu;
-  std::condition_variable cv;
-  bool done = false;
   int rc = CG_OK;
   std::string err;
   ~QBatch() { cg_batch_destroy(b); }
+};
+
+// One caller's request, on the caller's stack until its result is published.
+struct Ticket {
+  std::shared_ptr<LoadedImage> img;  // the image the request was encoded against
+  EncodedRequest e;
+  Clock::time_point t;
+  // set by the flusher
+  std::shared_ptr<QBatch> qb;
+  uint32_t idx = 0;
+  std::atomic<uint64_t> seq{0};  // the request's batch is published when done_seq reaches seq
+  int rc = CG_OK;    // a request the batch could not take (error set, no batch)
+  std::string err;
+};
+
+constexpr uint32_t STRIPES = 16;
+
+struct alignas(64) Stripe {
+  std::mutex mu;
+  std::vector<Ticket*> q;
 };
 
 }  // namespace
@@ -44,56 +60,107 @@ struct cg_queue {
   cg_ctx* ctx = nullptr;
   uint32_t max_batch = 4096;
   Clock::duration max_delay{};
-  uint32_t max_ready = 4;  // closed batches waiting for the device before callers block
-  std::mutex mu;
-  std::condition_variable cv_flush, cv_space;
-  std::shared_ptr<QBatch> open;
-  std::deque<std::shared_ptr<QBatch>> ready;
-  bool stop = false;
+  Stripe stripes[STRIPES];
+  std::atomic<uint32_t> pending{0};     // tickets in the stripes (the flusher sleeps on it at 0)
+  std::atomic<uint64_t> done_seq{0};    // batches published (callers sleep on it)
+  std::atomic<uint32_t> next_stripe{0};
+  std::atomic<bool> stop{false};
   std::thread flusher;
-  std::string err;
   std::atomic<uint64_t> n_batches{0}, n_requests{0}, n_fast{0}, max_seen{0}, device_ns{0};
 
   void run();
+  void publish(uint64_t seq) {
+    done_seq.store(seq, std::memory_order_release);
+    done_seq.notify_all();
+  }
 };
 
 void cg_queue::run() {
-  for (;;) {
+  std::deque<Ticket*> backlog;  // drained, not yet batched (over max_batch, or another image)
+  std::vector<Ticket*> grab;
+  uint64_t seq = 0;
+  struct InFlight {
     std::shared_ptr<QBatch> qb;
-    {
-      std::unique_lock<std::mutex> g(mu);
-      for (;;) {
-        if (!ready.empty()) {
-          qb = std::move(ready.front());
-          ready.pop_front();
-          cv_space.notify_all();
-          break;
-        }
-        if (open && (stop || Clock::now() - open->t0 >= max_delay)) {
-          qb = std::move(open);
-          open.reset();
-          break;
-        }
-        if (stop) return;
-        if (open) cv_flush.wait_until(g, open->t0 + max_delay);
-        else cv_flush.wait(g);
+    uint64_t seq = 0;
+    Clock::time_point t;
+  };
+  std::vector<InFlight> flight;  // at most one batch on the device while the next is built
+  auto drain = [&] {
+    for (auto& st : stripes) {
+      {
+        std::lock_guard<std::mutex> g(st.mu);
+        if (st.q.empty()) continue;
+        grab.swap(st.q);
+      }
+      pending.fetch_sub((uint32_t)grab.size(), std::memory_order_relaxed);
+      for (Ticket* t : grab) backlog.push_back(t);
+      grab.clear();
+    }
+  };
+  auto finish = [&](InFlight& f) {
+    int rc = f.qb->rc;
+    if (!rc) rc = cg_batch_wait(f.qb->b, -1);
+    device_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - f.t).count();
+    if (rc) {
+      f.qb->rc = rc;
+      f.qb->err = f.qb->b->err;
+    }
+    publish(f.seq);
+  };
+  for (;;) {
+    drain();
+    if (backlog.empty()) {
+      if (!flight.empty()) {  // nothing to build: finish the batch on the device
+        finish(flight.back());
+        flight.clear();
+        continue;
+      }
+      if (stop.load()) return;
+      pending.wait(0, std::memory_order_acquire);
+      continue;
+    }
+    if (max_delay.count() > 0) {  // let the batch fill, counted from its first request
+      const auto until = backlog.front()->t + max_delay;
+      while (backlog.size() < max_batch && Clock::now() < until && !stop.load()) {
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        drain();
       }
     }
-    const auto t = Clock::now();
-    int rc = cg_batch_submit(qb->b);
-    if (!rc) rc = cg_batch_wait(qb->b, -1);
-    device_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t).count();
+    // build the next batch from the backlog (one image per batch)
+    auto qb = std::make_shared<QBatch>();
+    const std::shared_ptr<LoadedImage> img = backlog.front()->img;
+    qb->b = new cg_batch();
+    qb->b->ctx = ctx;
+    qb->b->img = img;
+    qb->b->host.img = img->host;
+    const uint64_t my = ++seq;
+    while (!backlog.empty() && qb->b->items.size() < max_batch && backlog.front()->img == img) {
+      Ticket* t = backlog.front();
+      backlog.pop_front();
+      t->seq.store(my, std::memory_order_relaxed);
+      try {
+        qb->b->host.append(t->e);
+        qb->b->items.push_back({(int32_t)qb->b->host.n() - 1, -1});
+        t->qb = qb;
+        t->idx = (uint32_t)qb->b->items.size() - 1;
+      } catch (const std::exception& ex) {
+        t->rc = CG_E_ARG;
+        t->err = ex.what();
+      }
+    }
     n_batches++;
     const uint64_t n = qb->b->items.size();
     for (uint64_t m = max_seen.load(); n > m && !max_seen.compare_exchange_weak(m, n);) {
     }
-    {
-      std::lock_guard<std::mutex> g(qb->mu);
-      qb->rc = rc;
-      if (rc) qb->err = qb->b->err;
-      qb->done = true;
+    // the previous batch finishes before this one is submitted (one stream; its download first)
+    if (!flight.empty()) {
+      finish(flight.back());
+      flight.clear();
     }
-    qb->cv.notify_all();
+    InFlight f{qb, my, Clock::now()};
+    qb->rc = cg_batch_submit(qb->b);
+    if (qb->rc) qb->err = qb->b->err;
+    flight.push_back(std::move(f));
   }
 }
 
@@ -105,50 +172,29 @@ std::shared_ptr<LoadedImage> active_image(cg_ctx* ctx, std::string& err) {
   return ctx->active;
 }
 
-// Appends one encoded request (encoded against `li`) to the open batch and returns the batch and
-// the request's index in it. A batch holds requests of one image: a request encoded against a
-// newer epoch closes the open batch first. Caller must not hold q->mu.
-int enqueue(cg_queue* q, const std::shared_ptr<LoadedImage>& li, EncodedRequest& e, std::shared_ptr<QBatch>& out,
-            uint32_t& idx, std::string& err) {
-  std::unique_lock<std::mutex> g(q->mu);
-  q->cv_space.wait(g, [q] { return q->stop || q->ready.size() < q->max_ready; });
-  if (q->stop) { err = "queue closed"; return CG_E_STATE; }
-  if (q->open && q->open->b->img != li) {
-    q->ready.push_back(std::move(q->open));
-    q->open.reset();
-    q->cv_flush.notify_one();
-  }
-  if (!q->open) {
-    auto qb = std::make_shared<QBatch>();
-    qb->b = new (std::nothrow) cg_batch();
-    if (!qb->b) { err = "out of host memory"; return CG_E_ARG; }
-    qb->b->ctx = q->ctx;
-    qb->b->img = li;
-    qb->b->host.img = li->host;
-    qb->t0 = Clock::now();
-    q->open = std::move(qb);
-    q->cv_flush.notify_one();  // arms the deadline
-  }
-  cg_batch* b = q->open->b;
-  GUARD(err, {
-    b->host.append(e);
-    b->items.push_back({(int32_t)b->host.n() - 1, -1});
-  })
-  idx = (uint32_t)b->items.size() - 1;
-  out = q->open;
-  if (b->items.size() >= q->max_batch) {
-    q->ready.push_back(std::move(q->open));
-    q->open.reset();
-    q->cv_flush.notify_one();
-  }
-  return CG_OK;
-}
+thread_local uint32_t t_stripe = 0xFFFFFFFFu;
 
-int await(std::shared_ptr<QBatch>& qb, std::string& err) {
-  std::unique_lock<std::mutex> g(qb->mu);
-  qb->cv.wait(g, [&] { return qb->done; });
-  if (qb->rc) err = qb->err;
-  return qb->rc;
+// Hands the ticket to the flusher and sleeps until its batch is published.
+int wait_ticket(cg_queue* q, Ticket& t, std::string& err) {
+  if (q->stop.load()) { err = "queue closed"; return CG_E_STATE; }
+  if (t_stripe == 0xFFFFFFFFu) t_stripe = q->next_stripe.fetch_add(1) % STRIPES;
+  t.t = Clock::now();
+  {
+    Stripe& st = q->stripes[t_stripe];
+    std::lock_guard<std::mutex> g(st.mu);
+    st.q.push_back(&t);
+  }
+  if (q->pending.fetch_add(1, std::memory_order_release) == 0) q->pending.notify_one();
+  // the ticket's seq is written by the flusher before it publishes; read it only once published
+  for (;;) {
+    const uint64_t d = q->done_seq.load(std::memory_order_acquire);
+    const uint64_t my = t.seq.load(std::memory_order_relaxed);
+    if (my && d >= my) break;
+    q->done_seq.wait(d, std::memory_order_acquire);
+  }
+  if (t.rc) { err = t.err; return t.rc; }
+  if (t.qb->rc) { err = t.qb->err; return t.qb->rc; }
+  return CG_OK;
 }
 
 int put_string(const std::string& s, char* buf, size_t cap, size_t* need) {
@@ -161,24 +207,21 @@ int put_string(const std::string& s, char* buf, size_t cap, size_t* need) {
 
 thread_local std::string t_err;
 
-// Encodes on the calling thread, joins the open batch, waits, and renders the caller's result
+// Queues the caller's encoded request, waits for its batch and renders the caller's result
 // (authz: cg_batch_authz's Decision + reason; else cg_batch_decision + diagnostic).
-int submit_encoded(cg_queue* q, const std::shared_ptr<LoadedImage>& li, EncodedRequest& e, int* out, char* buf,
-                   size_t cap, size_t* need, bool authz) {
-  std::shared_ptr<QBatch> qb;
-  uint32_t idx = 0;
-  int rc = enqueue(q, li, e, qb, idx, t_err);
+int submit_ticket(cg_queue* q, Ticket& t, int* out, char* buf, size_t cap, size_t* need, bool authz) {
+  int rc = wait_ticket(q, t, t_err);
   if (rc) return rc;
   q->n_requests++;
-  if ((rc = await(qb, t_err))) return rc;
+  cg_batch* b = t.qb->b;
   if (authz) {
-    rc = cg_batch_authz(qb->b, idx, out, buf, cap, need);
-    if (rc && rc != CG_E_RANGE) t_err = qb->b->err;
+    rc = cg_batch_authz(b, t.idx, out, buf, cap, need);
+    if (rc && rc != CG_E_RANGE) t_err = b->err;
     return rc;
   }
-  if ((rc = cg_batch_decision(qb->b, idx, out, nullptr))) { t_err = qb->b->err; return rc; }
+  if ((rc = cg_batch_decision(b, t.idx, out, nullptr))) { t_err = b->err; return rc; }
   if (!buf && !need) return CG_OK;
-  return cg_batch_diagnostic(qb->b, idx, 0, buf, cap, need);
+  return cg_batch_diagnostic(b, t.idx, 0, buf, cap, need);
 }
 
 }  // namespace
@@ -205,13 +248,10 @@ int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_q
 
 void cg_queue_destroy(cg_queue* q) {
   if (!q) return;
-  {
-    std::lock_guard<std::mutex> g(q->mu);
-    q->stop = true;
-  }
-  q->cv_flush.notify_all();
-  q->cv_space.notify_all();
-  if (q->flusher.joinable()) q->flusher.join();  // drains ready and open batches first
+  q->stop.store(true);
+  q->pending.fetch_add(1);  // wakes the flusher, which finishes what it holds and returns
+  q->pending.notify_one();
+  if (q->flusher.joinable()) q->flusher.join();
   delete q;
 }
 
@@ -220,9 +260,11 @@ const char* cg_queue_last_error(void) { return t_err.c_str(); }
 int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* decision, char* reason, size_t cap,
                            size_t* need) {
   if (!q || !sar_json || !decision) return CG_E_ARG;
-  auto li = active_image(q->ctx, t_err);
-  if (!li) return CG_E_STATE;
-  EncodedRequest e;
+  Ticket t;
+  t.img = active_image(q->ctx, t_err);
+  if (!t.img) return CG_E_STATE;
+  const std::shared_ptr<LoadedImage>& li = t.img;
+  EncodedRequest& e = t.e;
   {
     int fast = -1;
     std::string r;
@@ -250,7 +292,7 @@ int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* d
       })
     }
   }
-  return submit_encoded(q, li, e, decision, reason, cap, need, true);
+  return submit_ticket(q, t, decision, reason, cap, need, true);
 }
 
 int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
@@ -262,11 +304,11 @@ int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, 
     JVal v = json_parse(item_json, len);
     decode_json_item(v, ents, req);
   })
-  auto li = active_image(q->ctx, t_err);
-  if (!li) return CG_E_STATE;
-  EncodedRequest e;
-  GUARD(t_err, { encode_request(*li->host, ents, req, e); })
-  return submit_encoded(q, li, e, allow, diag, cap, need, false);
+  Ticket t;
+  t.img = active_image(q->ctx, t_err);
+  if (!t.img) return CG_E_STATE;
+  GUARD(t_err, { encode_request(*t.img->host, ents, req, t.e); })
+  return submit_ticket(q, t, allow, diag, cap, need, false);
 }
 
 int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,
