@@ -87,6 +87,10 @@ _SIGS = {
     "cg_is_authorized_json": (ctypes.c_int, [P, cstr, sz, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
     "cg_encode_sar_check": (ctypes.c_int, [P, sz, cstr, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
                                            ctypes.POINTER(u32), ctypes.POINTER(i64)]),
+    "cg_batch_add_admission_json": (ctypes.c_int, [P, cstr, sz]),
+    "cg_batch_admit": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), P, sz,
+                                      ctypes.POINTER(sz)]),
+    "cg_admission_to_cedar_json": (ctypes.c_int, [cstr, sz, P, sz, ctypes.POINTER(sz)]),
     "cg_queue_create": (ctypes.c_int, [P, u32, u32, ctypes.POINTER(P)]),
     "cg_queue_destroy": (None, [P]),
     "cg_queue_last_error": (cstr, []),

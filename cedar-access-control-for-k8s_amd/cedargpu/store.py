@@ -257,6 +257,27 @@ class Batch:
         if rc:
             raise _err(rc, "SubjectAccessReview encode failed")
 
+    def add_admission_json(self, payload: str):
+        """AdmissionReview JSON (object or array) -> entities via the C++ model (admission.cpp)."""
+        b = _b(payload)
+        rc = lib.cg_batch_add_admission_json(self._h, b, len(b))
+        if rc:
+            raise _err(rc, "AdmissionReview encode failed")
+
+    def admit(self, i: int) -> Tuple[bool, int, str]:
+        """(allowed, HTTP status code, message) of admission.Response — handler.go:43-80."""
+        allowed, code = ctypes.c_int(), ctypes.c_int()
+        need = ctypes.c_size_t(0)
+        buf = ctypes.create_string_buffer(512)
+        rc = lib.cg_batch_admit(self._h, i, ctypes.byref(allowed), ctypes.byref(code), buf, 512, ctypes.byref(need))
+        if rc == CG_E_RANGE and need.value > 512:
+            buf = ctypes.create_string_buffer(need.value)
+            rc = lib.cg_batch_admit(self._h, i, ctypes.byref(allowed), ctypes.byref(code), buf, need.value,
+                                    ctypes.byref(need))
+        if rc:
+            raise _err(rc, "admission result failed")
+        return bool(allowed.value), code.value, buf.value.decode("utf-8")
+
     def authz(self, i: int) -> Tuple[int, str]:
         """(authorizer.Decision: 0 Deny / 1 Allow / 2 NoOpinion, reason) — authorizer.go:36-85."""
         dec = ctypes.c_int()
@@ -463,6 +484,43 @@ class Authorizer:
 
     def authorize(self, sar: dict) -> Tuple[int, str]:
         return self.authorize_batch([sar])[0]
+
+
+class AdmissionHandler:
+    """cedarHandler over GPU tiers (handler.go:43-167). The last store should be
+    `ALLOW_ALL_ADMISSION` (main.go:111-116). `handle_batch` takes AdmissionReview dicts and returns
+    [(allowed, HTTP status code, message)]."""
+
+    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None):
+        self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx)
+
+    def handle_batch(self, reviews: Sequence[dict]) -> List[Tuple[bool, int, str]]:
+        if not self.tiers.ready():  # handler.go:49-57: allow until every store has loaded
+            return [(True, 200, "") for _ in reviews]
+        b = self.tiers.ctx.batch()
+        b.add_admission_json(json.dumps(list(reviews)))
+        b.submit()
+        b.wait()
+        out = [b.admit(i) for i in range(len(b))]
+        b.close()
+        return out
+
+    def handle(self, review: dict) -> Tuple[bool, int, str]:
+        return self.handle_batch([review])[0]
+
+
+def admission_to_cedar_json(review: dict) -> dict:
+    """Host-only: the (EntityMap, Request) the admission path builds (cg_admission_to_cedar_json)."""
+    b = _b(json.dumps(review))
+    need = ctypes.c_size_t(0)
+    buf = ctypes.create_string_buffer(1 << 16)
+    rc = lib.cg_admission_to_cedar_json(b, len(b), buf, 1 << 16, ctypes.byref(need))
+    if rc == CG_E_RANGE and need.value > (1 << 16):
+        buf = ctypes.create_string_buffer(need.value)
+        rc = lib.cg_admission_to_cedar_json(b, len(b), buf, need.value, ctypes.byref(need))
+    if rc:
+        raise _err(rc, "admission conversion failed")
+    return json.loads(buf.value.decode("utf-8"))
 
 
 def _fast_or_noopinion(sar: dict) -> Tuple[int, str]:

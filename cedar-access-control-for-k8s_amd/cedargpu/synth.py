@@ -273,3 +273,57 @@ def admission_objects(n: int, seed: int = 41) -> List[Tuple[str, dict]]:
                                                                "labels": labels}, "data": data}
         out.append((kind, obj))
     return out
+
+
+def admission_reviews(n: int, seed: int = 43, objects: Optional[List[Tuple[str, dict]]] = None) -> List[dict]:
+    """C4 AdmissionReview requests (admission.k8s.io/v1) over ConfigMap / Secret objects, as the
+    reference's /v1/admit handler receives them: CREATE / UPDATE / DELETE with object / oldObject,
+    users with groups."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    objs = objects or admission_objects(max(n, 2), seed=seed)
+    out = []
+    for i in range(n):
+        kind, obj = objs[i % len(objs)]
+        op = ["CREATE", "UPDATE", "DELETE"][int(rng.integers(0, 3))]
+        old = objs[(i + 1) % len(objs)][1]
+        user = {"username": ["test-user", "sample-user", f"user-{int(rng.integers(0, 200)):05d}"][i % 3], "uid": "",
+                "groups": ["requires-labels"] if rng.random() < 0.5 else ["viewers", "system:authenticated"]}
+        req = {"uid": f"req-{i}", "kind": {"group": "", "version": "v1", "kind": kind},
+               "resource": {"group": "", "version": "v1", "resource": kind.lower() + "s"},
+               "name": obj["metadata"]["name"], "namespace": obj["metadata"]["namespace"], "operation": op,
+               "userInfo": user,
+               "object": obj if op != "DELETE" else None,
+               "oldObject": (obj if op == "DELETE" else old) if op != "CREATE" else None}
+        out.append({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": req})
+    return out
+
+
+def admission_policies(n: int, seed: int = 3) -> str:
+    """C4: admission forbids on ConfigMap / Secret objects (name prefix globs, label and data
+    key/value contains, has-guards, oldObject comparisons), the shapes of demo/admission-policy.yaml."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    acts = ['k8s::admission::Action::"create"', 'k8s::admission::Action::"update"', 'k8s::admission::Action::"delete"']
+    out = []
+    for i in range(n):
+        kind = "ConfigMap" if rng.random() < 0.6 else "Secret"
+        user = ["test-user", "sample-user", f"user-{int(rng.integers(0, 200)):05d}"][int(rng.integers(0, 3))]
+        t = rng.random()
+        if t < 0.3:
+            out.append(f'forbid (\n  principal is k8s::User,\n  action in [{acts[0]}, {acts[1]}],\n  resource is core::v1::{kind}\n)\n'
+                       f'when {{ principal.name == {json.dumps(user)} && resource.metadata.name like "prod-*" }};\n')
+        elif t < 0.55:
+            out.append(f'forbid (\n  principal is k8s::User in k8s::Group::"requires-labels",\n  action in [{", ".join(acts)}],\n'
+                       f'  resource is core::v1::{kind}\n)\nunless {{ resource has metadata && resource.metadata has labels && '
+                       f'resource.metadata.labels.contains({{"key": "owner", "value": principal.name}}) }};\n')
+        elif t < 0.8:
+            ns = f"ns-{int(rng.integers(0, 20)):03d}"
+            lab = f"label-{int(rng.integers(0, 40))}"
+            out.append(f'forbid (\n  principal,\n  action == {acts[1]},\n  resource is core::v1::{kind}\n)\n'
+                       f'when {{ resource.metadata.namespace == {json.dumps(ns)} && resource has oldObject && '
+                       f'resource.oldObject.metadata has labels && '
+                       f'resource.oldObject.metadata.labels.contains({{"key": {json.dumps(lab)}, "value": "v{int(rng.integers(0, 5))}"}}) }};\n')
+        else:
+            out.append(f'forbid (\n  principal,\n  action in [{acts[0]}, {acts[1]}],\n  resource is core::v1::{kind}\n)\n'
+                       f'when {{ resource has data && resource.data.contains({{"key": "key{int(rng.integers(0, 9))}", '
+                       f'"value": "value{int(rng.integers(0, 100))}"}}) }};\n')
+    return "\n".join(out)

@@ -8,6 +8,7 @@
 #include <mutex>
 #include <thread>
 
+#include "admission.h"
 #include "capi_internal.h"
 #include "sar.h"
 
@@ -149,6 +150,33 @@ int encode_sar_check(const void* image, size_t len, const char* sars, size_t n, 
   if (n_mismatch) *n_mismatch = nm;
   if (first_mismatch) *first_mismatch = first;
   return CG_OK;
+}
+
+// {"entities":[...],"request":{...}} (Cedar JSON) of an (EntityMap, Request)
+void cedar_item_json(const std::vector<EntityIn>& ents, const RequestIn& req, std::string& s) {
+  auto uid = [&s](const std::pair<std::string, std::string>& u) {
+    s += "{\"type\":"; go_json_string(s, u.first); s += ",\"id\":"; go_json_string(s, u.second); s += "}";
+  };
+  s = "{\"entities\":[";
+  for (size_t k = 0; k < ents.size(); k++) {
+    if (k) s += ',';
+    s += "{\"uid\":";
+    uid({ents[k].type, ents[k].id});
+    s += ",\"attrs\":";
+    hval_to_json(ents[k].attrs, s);
+    s += ",\"parents\":[";
+    for (size_t p = 0; p < ents[k].parents.size(); p++) { if (p) s += ','; uid(ents[k].parents[p]); }
+    s += "]}";
+  }
+  s += "],\"request\":{\"principal\":";
+  uid(req.principal);
+  s += ",\"action\":";
+  uid(req.action);
+  s += ",\"resource\":";
+  uid(req.resource);
+  s += ",\"context\":";
+  hval_to_json(req.context, s);
+  s += "}}";
 }
 
 }  // namespace
@@ -457,29 +485,7 @@ int cg_sar_to_cedar_json(const char* sar_json, size_t len, char* out, size_t cap
       std::vector<EntityIn> ents;
       RequestIn req;
       record_to_cedar(a, ents, req);
-      auto uid = [&s](const std::pair<std::string, std::string>& u) {
-        s += "{\"type\":"; go_json_string(s, u.first); s += ",\"id\":"; go_json_string(s, u.second); s += "}";
-      };
-      s = "{\"entities\":[";
-      for (size_t k = 0; k < ents.size(); k++) {
-        if (k) s += ',';
-        s += "{\"uid\":";
-        uid({ents[k].type, ents[k].id});
-        s += ",\"attrs\":";
-        hval_to_json(ents[k].attrs, s);
-        s += ",\"parents\":[";
-        for (size_t p = 0; p < ents[k].parents.size(); p++) { if (p) s += ','; uid(ents[k].parents[p]); }
-        s += "]}";
-      }
-      s += "],\"request\":{\"principal\":";
-      uid(req.principal);
-      s += ",\"action\":";
-      uid(req.action);
-      s += ",\"resource\":";
-      uid(req.resource);
-      s += ",\"context\":";
-      hval_to_json(req.context, s);
-      s += "}}";
+      cedar_item_json(ents, req, s);
     }
   })
   if (need) *need = s.size() + 1;
@@ -524,6 +530,90 @@ int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t 
   if (!image || !sars) return CG_E_ARG;
   std::string err;
   GUARD(err, { return encode_sar_check(image, len, sars, n, n_items, n_direct, n_mismatch, first_mismatch); })
+}
+
+int cg_batch_add_admission_json(cg_batch* b, const char* json, size_t len) {
+  if (!b || !json) return CG_E_ARG;
+  if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
+  GUARD(b->err, {
+    JVal v = json_parse(json, len);
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    auto one = [&](const JVal& review) {
+      const AdmissionRequest a = admission_request_from_json(review);
+      std::string err;
+      const int o = admission_to_cedar(a, ents, req, err);
+      const uint32_t i = (uint32_t)b->items.size();
+      if (o == ADM_EVAL) {
+        b->items.push_back({(int32_t)b->host.n(), -1});
+        b->host.add(ents, req);
+      } else {
+        b->items.push_back({-1, o});
+        if (o == ADM_ERROR) b->fast_reason[i] = err;
+      }
+    };
+    if (v.t == JVal::Arr) for (auto& r : v.arr) one(r);
+    else one(v);
+    return CG_OK;
+  })
+}
+
+int cg_batch_admit(cg_batch* b, uint32_t i, int* allowed, int* code, char* msg, size_t cap, size_t* need) {
+  if (!b || !allowed) return CG_E_ARG;
+  if (i >= b->items.size()) return CG_E_RANGE;
+  std::string m;
+  int c = 200;
+  const auto& it = b->items[i];
+  if (it.dev < 0) {
+    if (it.fast == ADM_SKIP) {
+      *allowed = 1;
+    } else {  // admission.Errored(http.StatusInternalServerError, err)
+      *allowed = 0;
+      c = 500;
+      m = b->fast_reason[i];
+    }
+  } else {
+    if (!b->done) return CG_E_STATE;
+    const uint32_t d = (uint32_t)it.dev;
+    *allowed = b->host.decision(d) ? 1 : 0;
+    std::vector<uint32_t> rs;
+    b->host.reason_ids(d, rs);
+    if (!*allowed && !rs.empty()) {  // json.Marshal(diagnostics.Reasons) (handler.go:62-66)
+      GUARD(b->err, { b->host.diagnostic_json(d, m, true); })
+    }
+  }
+  if (code) *code = c;
+  if (need) *need = m.size() + 1;
+  if (!msg) return CG_OK;
+  if (cap < m.size() + 1) return CG_E_RANGE;
+  std::memcpy(msg, m.c_str(), m.size() + 1);
+  return CG_OK;
+}
+
+int cg_admission_to_cedar_json(const char* review_json, size_t len, char* out, size_t cap, size_t* need) {
+  if (!review_json) return CG_E_ARG;
+  std::string s, err;
+  GUARD(err, {
+    JVal v = json_parse(review_json, len);
+    const AdmissionRequest a = admission_request_from_json(v);
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    std::string e;
+    const int o = admission_to_cedar(a, ents, req, e);
+    if (o == ADM_SKIP) {
+      s = "{\"skip\":true}";
+    } else if (o == ADM_ERROR) {
+      s = "{\"error\":";
+      go_json_string(s, e);
+      s += "}";
+    } else {
+      cedar_item_json(ents, req, s);
+    }
+  })
+  if (need) *need = s.size() + 1;
+  if (!out || cap < s.size() + 1) return CG_E_RANGE;
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  return CG_OK;
 }
 
 uint32_t cg_batch_size(cg_batch* b) { return b ? (uint32_t)b->items.size() : 0; }

@@ -55,7 +55,7 @@ struct cg_batch {
   // items: caller-visible entries; dev >= 0 is the device request index, else a fast-path result
   struct Item { int32_t dev; int32_t fast; };
   std::vector<Item> items;
-  std::map<uint32_t, std::string> fast_reason;
+  std::map<uint32_t, std::string> fast_reason;  // authz fast paths: the reason; admission: error text
   ~cg_batch() { dev_batch_free(&dev); }
   int32_t dev_of(uint32_t i) const { return i < items.size() ? items[i].dev : -1; }
 };

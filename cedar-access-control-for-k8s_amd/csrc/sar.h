@@ -30,5 +30,9 @@ Attributes attributes_from_sar(const JVal& sar);
 int authorize_fast_path(const Attributes& a, std::string& reason);
 std::string resource_request_to_path(const Attributes& a);
 void record_to_cedar(const Attributes& a, std::vector<EntityIn>& ents, RequestIn& req);
+// UserToCedarEntity (internal/server/entities/user.go:35-100): group entities, then the principal
+void user_to_cedar(const std::string& name, const std::string& uid, const std::vector<std::string>& groups,
+                   const std::vector<std::pair<std::string, std::vector<std::string>>>& extra, std::vector<EntityIn>& ents,
+                   std::pair<std::string, std::string>& principal);
 
 }  // namespace cg

@@ -147,6 +147,23 @@ int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t 
  * reference returns (diagnosticToReason JSON, a fast-path literal, or ""). */
 int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t cap, size_t* need);
 
+/* ---- admission webhook path (AdmissionReview in, allowed + status message out) ----
+ * Appends AdmissionReview JSON objects ({"request": {...}}, a bare request object, or an array) as
+ * the reference's /v1/admit handler receives them. Applies cedarHandler.Handle / review
+ * (handler.go:43-153): the skipped namespaces (kube-system, cedar-k8s-authz-system), the principal
+ * entities (entities/user.go), the resource entity flattened from the object / oldObject JSON
+ * (UnstructuredToRecord + walkObject, entities/admission.go:123-369), the oldObject linkage, the
+ * admission action entities and the request context. Store readiness (handler.go:49-57) is the
+ * caller's check. The image must carry the trailing allow-all tier (cmd/cedar-webhook/main.go:111-116). */
+int cg_batch_add_admission_json(cg_batch* b, const char* json, size_t len);
+/* admission.Response for item i: *allowed; *code = 200, or 500 when the review failed
+ * (admission.Errored; msg = the error text); msg = json.Marshal(diagnostics.Reasons) for a denial
+ * with reasons (handler.go:62-66), else "". CG_E_RANGE: msg needs *need bytes. */
+int cg_batch_admit(cg_batch* b, uint32_t i, int* allowed, int* code, char* msg, size_t cap, size_t* need);
+/* Host-only: the (EntityMap, Request) the admission path builds, as Cedar JSON
+ * {"entities":[...],"request":{...}}, or {"skip":true}, or {"error":"..."} — for encoder parity tests. */
+int cg_admission_to_cedar_json(const char* review_json, size_t len, char* out, size_t cap, size_t* need);
+
 /* ---- single-request drop-in: TieredPolicyStores.IsAuthorized(EntityMap, Request) ---- */
 int cg_is_authorized_json(cg_ctx* ctx, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
                           size_t* need);

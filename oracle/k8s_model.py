@@ -311,6 +311,13 @@ _KV_STRING_MAP = {
     "meta": {"v1": {"LabelSelector": ["matchLabels"], "ObjectMeta": ["annotations", "labels"]}},
 }
 _IP_KEYS = ("podIP", "clusterIP", "loadBalancerIP", "hostIP", "ip", "podIPs", "hostIPs")
+# knownKeyValueStringSliceMapAttributes (admission.go:266-283): the reference asserts each value
+# to []string, which a decoded JSON array never is, so the walk stops at once: an empty set
+_KV_SLICE_MAP = {
+    "authentication": {"v1": {"UserInfo": ["extra"]}},
+    "authorization": {"v1": {"SubjectAccessReview": ["extra"]}},
+    "certificates": {"v1": {"CertificateSigningRequest": ["extra"]}},
+}
 
 
 class WalkError(Exception):
@@ -318,6 +325,8 @@ class WalkError(Exception):
 
 
 def _kv_set(obj: dict):
+    if not isinstance(obj, dict):
+        raise WalkError("key/value map attribute is not an object")  # a Go type-assertion panic
     out = []
     for kk, vv in obj.items():
         if not isinstance(vv, str):
@@ -335,6 +344,11 @@ def walk_object(depth: int, group: str, version: str, kind: str, key: str, obj):
     names = _KV_STRING_MAP.get(group, {}).get(version, {}).get(kind)
     if names and key in names:
         return _kv_set(obj)
+    names = _KV_SLICE_MAP.get(group, {}).get(version, {}).get(kind)
+    if names and key in names:
+        if not isinstance(obj, dict):
+            raise WalkError("key/value slice map attribute is not an object")
+        return CSet([])
     if isinstance(obj, dict) and key in ("labels", "annotations"):
         return _kv_set(obj)
     if isinstance(obj, dict):
@@ -348,7 +362,11 @@ def walk_object(depth: int, group: str, version: str, kind: str, key: str, obj):
             return None
         return Record(rec)
     if isinstance(obj, list):
-        return CSet([walk_object(depth - 1, group, version, kind, key, x) for x in obj])
+        items = [walk_object(depth - 1, group, version, kind, key, x) for x in obj]
+        if any(x is None for x in items):
+            # the reference builds cedar.NewSet over a nil Value here; reported as an error
+            raise WalkError("unsupported nil value in a list")
+        return CSet(items)
     if isinstance(obj, bool):
         return obj
     if isinstance(obj, str):
@@ -399,6 +417,7 @@ class AdmissionRequest:
     subresource: str = ""
     object: Optional[dict] = None
     old_object: Optional[dict] = None
+    kind_version: Optional[str] = None  # req.Kind.Version when it differs from req.Resource.Version
 
 
 def _admission_path(req: AdmissionRequest) -> str:
@@ -410,9 +429,28 @@ def _admission_path(req: AdmissionRequest) -> str:
 def _admission_resource_entity(req: AdmissionRequest, raw: Optional[dict]) -> Entity:
     if raw is None:
         raise WalkError("unstructured data is nil")
+    if not isinstance(raw, dict) or not isinstance(raw.get("kind"), str) or not raw.get("kind"):
+        raise WalkError("Object 'Kind' is missing")  # unstructured decoding requires kind
     group = req.group or "core"
-    attrs = unstructured_to_record(raw, group, req.version, req.kind)
-    return Entity(EntityUID(f"{group}::{req.version}::{req.kind}", _admission_path(req)), attrs, ())
+    kver = req.kind_version if req.kind_version is not None else req.version
+    attrs = unstructured_to_record(raw, group, kver, req.kind)
+    return Entity(EntityUID(f"{group}::{kver}::{req.kind}", _admission_path(req)), attrs, ())
+
+
+def admission_request_from_review(review: dict) -> AdmissionRequest:
+    """An AdmissionReview ({"request": {...}}) as controller-runtime's admission.Request."""
+    q = review.get("request", review)
+    u = q.get("userInfo") or {}
+    extra = {k: [x for x in v if isinstance(x, str)] for k, v in (u.get("extra") or {}).items()}
+    return AdmissionRequest(
+        uid=q.get("uid", ""), operation=q.get("operation", ""),
+        user=UserInfo(u.get("username", ""), u.get("uid", ""), [g for g in u.get("groups") or [] if isinstance(g, str)],
+                      extra),
+        group=(q.get("resource") or {}).get("group", ""), version=(q.get("resource") or {}).get("version", ""),
+        resource=(q.get("resource") or {}).get("resource", ""), kind=(q.get("kind") or {}).get("kind", ""),
+        namespace=q.get("namespace", ""), name=q.get("name", ""), subresource=q.get("subResource", ""),
+        object=q.get("object"), old_object=q.get("oldObject"),
+        kind_version=(q.get("kind") or {}).get("version", ""))
 
 
 def admission_to_cedar(req: AdmissionRequest) -> Tuple[EntityMap, Request]:
