@@ -92,6 +92,73 @@ def parity_sample(policies_text, items, idx, gpu_batch, threads):
     return {"requests": len(items), "mismatches": bad, "oracle": "oracle/cedar_ref.cpp"}
 
 
+def secondary_configs(ctx, n_req, threads, sample=512):
+    """The other single-GPU BASELINE configs, run after the timed region (not part of `value`):
+    C2 = 1k RBAC-converted policies x SubjectAccessReviews, C4 = 1k admission forbids plus the
+    static allow-all tier x AdmissionReviews on ConfigMaps / Secrets. Per config: device
+    decisions/s (HIP events over 5 launches of the resident batch), host encode rate (the C++ SAR
+    / admission models), and a parity sample against the C++ oracle."""
+    import cedargpu
+    from cedargpu import synth
+    from cedar_ref import RefPolicySet, items_json
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cedar_oracle as co
+    import k8s_model as km
+    out = {}
+
+    def run(name, stores, payload, add, result, want_of, items, idx, what):
+        image = cedargpu.build_image(stores, epoch=100 + len(out))
+        ctx.load(image, 100 + len(out))
+        b = ctx.batch()
+        t0 = time.perf_counter()
+        add(b, payload)
+        enc_s = time.perf_counter() - t0
+        b.submit()
+        b.wait()
+        ms = b.time(5) / 5
+        ref = RefPolicySet.from_stores(stores)
+        ref.load_items(items_json(items))
+        want = ref.evaluate(threads)
+        ref.close()
+        bad = sum(1 for w, i in zip(want, idx) if result(b, i) != want_of(w))
+        out[name] = {"what": what, "requests": len(b), "kernel_ms": ms, "decisions_per_s": len(b) / (ms * 1e-3),
+                     "host_encode_per_s": len(b) / enc_s,
+                     "parity_sample": {"requests": len(items), "mismatches": bad, "oracle": "oracle/cedar_ref.cpp"}}
+        b.close()
+
+    pop = synth.Population(seed=21)
+    sars = synth.random_sars(n_req, seed=2000, pop=pop)
+    items, idx = oracle_items(sars[:sample])
+
+    def authz_want(w):
+        ok, _, diag, _ = w
+        d = 1 if ok else (0 if diag.startswith('{"reasons"') else 2)
+        return (d, diag if d != 2 else "")
+
+    run("c2_rbac_1k", [cedargpu.MemoryStore("rbac.cedar", synth.rbac_policies(1000, seed=21, pop=pop))],
+        synth.sars_json(sars), lambda b, p: b.add_sar_json(p), lambda b, i: b.authz(i), authz_want, items, idx,
+        "1k RBAC-converted policies x synthetic SubjectAccessReviews (authorizer.Decision + reason)")
+
+    reviews = synth.admission_reviews(n_req, seed=4000)
+    items, idx = [], []
+    for i, r in enumerate(reviews[:sample]):
+        em, req = km.admission_to_cedar(km.admission_request_from_review(r))
+        items.append((co.entities_to_json(em), co.request_to_json(req)))
+        idx.append(i)
+
+    def admit_want(w):
+        ok, _, _, reasons = w
+        return (ok, 200, reasons if not ok and reasons not in ("", "[]", "null") else "")
+
+    run("c4_admission_1k", [cedargpu.MemoryStore("adm.cedar", synth.admission_policies(1000, seed=3)),
+                            cedargpu.ALLOW_ALL_ADMISSION],
+        json.dumps(reviews, separators=(",", ":")), lambda b, p: b.add_admission_json(p), lambda b, i: b.admit(i),
+        admit_want, items, idx,
+        "1k admission forbids + allow-all tier x synthetic AdmissionReviews on ConfigMaps / Secrets "
+        "(allowed + message)")
+    return out
+
+
 def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=120.0):
     """Policy hot reload after the timed region: rank 0 compiles epoch 2 (the policies plus one
     forbid), one RCCL broadcast ships it to every GPU, each rank activates it and checks a request
@@ -184,6 +251,8 @@ def main():
                     help="caller threads of the serving-queue check (0: skip)")
     ap.add_argument("--serve-requests", type=int, default=262_144)
     ap.add_argument("--serve-max-batch", type=int, default=8192)
+    ap.add_argument("--configs-requests", type=int, default=32_768,
+                    help="requests per secondary config (C2, C4) after the timed region (0: skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -266,6 +335,8 @@ def main():
         serving = serve(ctx, sars, args.serve_threads, args.serve_requests, args.serve_max_batch)
 
     parity = parity_sample(policies, items, idx, b, threads) if rank == 0 and items else None
+    configs = (secondary_configs(ctx, args.configs_requests, threads)
+               if rank == 0 and world == 1 and args.configs_requests else None)
     reload = hot_reload(ctx, policies, rank, world, local, dist_on) if args.reload else None
 
     if rank == 0:
@@ -307,6 +378,7 @@ def main():
             "parity_sample": parity,
             "reload": reload,
             "serving": serving,
+            "configs": configs,
             "latency": {"batch": args.latency_batch, "p50_ms": lat[len(lat) // 2] if lat else None,
                         "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
                         "max_ms": lat[-1] if lat else None, "batches": len(lat),

@@ -535,6 +535,48 @@ int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t 
 int cg_batch_add_admission_json(cg_batch* b, const char* json, size_t len) {
   if (!b || !json) return CG_E_ARG;
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
+  std::vector<std::pair<size_t, size_t>> elems;
+  if (len >= 65536 && split_array(json, len, elems) && host_workers(elems.size()) > 1) {
+    // bulk: parse, flatten and encode reviews on worker threads; append in order. All or nothing.
+    struct Slot {
+      int outcome = ADM_EVAL, rc = CG_OK;
+      std::string err;
+      EncodedRequest e;
+    };
+    std::vector<Slot> slots(elems.size());
+    const Image& img = *b->host.img;
+    parallel_for(elems.size(), [&](size_t k) {
+      Slot& sl = slots[k];
+      try {
+        JVal v = json_parse(json + elems[k].first, elems[k].second);
+        const AdmissionRequest a = admission_request_from_json(v);
+        std::vector<EntityIn> ents;
+        RequestIn req;
+        sl.outcome = admission_to_cedar(a, ents, req, sl.err);
+        if (sl.outcome == ADM_EVAL) encode_request(img, ents, req, sl.e);
+      } catch (const CedarError& e) {
+        sl.err = e.what(); sl.rc = CG_E_PARSE;
+      } catch (const std::exception& e) {
+        sl.err = e.what(); sl.rc = CG_E_ARG;
+      }
+    });
+    for (auto& sl : slots)
+      if (sl.rc) { b->err = sl.err; return sl.rc; }
+    GUARD(b->err, {
+      for (auto& sl : slots) {
+        const uint32_t i = (uint32_t)b->items.size();
+        if (sl.outcome != ADM_EVAL) {
+          b->items.push_back({-1, sl.outcome});
+          if (sl.outcome == ADM_ERROR) b->fast_reason[i] = std::move(sl.err);
+          continue;
+        }
+        b->items.push_back({(int32_t)b->host.n(), -1});
+        b->host.append(sl.e);
+        sl.e = EncodedRequest();
+      }
+      return CG_OK;
+    })
+  }
   GUARD(b->err, {
     JVal v = json_parse(json, len);
     std::vector<EntityIn> ents;
