@@ -1311,8 +1311,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
 
   // the request row streams through once: non-temporal loads, header broadcast in the segment
   const uint32_t rw = (valid && sl < RW_HDR) ? __builtin_nontemporal_load(row + sl) : 0u;
+  // segments narrower than the header hold its upper words in a second register
+  const uint32_t rw_hi = (SEG < RW_HDR && valid && SEG + sl < RW_HDR) ? __builtin_nontemporal_load(row + SEG + sl) : 0u;
+  auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
   PCtx c;
-  c.blk = a.heap + sbcast(rw, RW_BLK);
+  c.blk = a.heap + hdr(RW_BLK);
   c.cpool = a.cpool;
   c.lh = wl.he[seg];  // atoms never address lane scratch (any valid pointer)
   c.gstr_off = a.gstr_off;
@@ -1321,12 +1324,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
   c.bstr_bytes = a.bstr_bytes;
   c.n_gstr = a.n_gstr;
   c.hotl = wl.hot[seg];
-  c.pt = sbcast(rw, RW_P); c.pi = sbcast(rw, RW_P + 1);
-  c.at = sbcast(rw, RW_A); c.ai = sbcast(rw, RW_A + 1);
-  c.rt = sbcast(rw, RW_R); c.ri = sbcast(rw, RW_R + 1);
-  c.p_anc = sbcast(rw, RW_PANC); c.p_nanc = sbcast(rw, RW_PN);
-  c.r_anc = sbcast(rw, RW_RANC); c.r_nanc = sbcast(rw, RW_RN);
-  c.a_anc = sbcast(rw, RW_AANC); c.a_nanc = sbcast(rw, RW_AN);
+  c.pt = hdr(RW_P); c.pi = hdr(RW_P + 1);
+  c.at = hdr(RW_A); c.ai = hdr(RW_A + 1);
+  c.rt = hdr(RW_R); c.ri = hdr(RW_R + 1);
+  c.p_anc = hdr(RW_PANC); c.p_nanc = hdr(RW_PN);
+  c.r_anc = hdr(RW_RANC); c.r_nanc = hdr(RW_RN);
+  c.a_anc = hdr(RW_AANC); c.a_nanc = hdr(RW_AN);
   for (uint32_t h = sl; h < a.n_hot; h += SEG)
     wl.hot[seg][h] = valid ? make_uint2(__builtin_nontemporal_load(row + RW_HDR + 2 * h),
                                         __builtin_nontemporal_load(row + RW_HDR + 2 * h + 1))
@@ -1853,7 +1856,7 @@ static uint32_t probe_seg() {
   static const uint32_t seg = [] {
     const char* e = std::getenv("CEDARGPU_PROBE_SEG");
     const uint32_t v = e ? (uint32_t)std::atoi(e) : 16u;
-    return (v == 32u || v == 64u) ? v : 16u;
+    return (v == 8u || v == 32u || v == 64u) ? v : 16u;
   }();
   return seg;
 }
@@ -1867,7 +1870,7 @@ static uint32_t probe_occ() {
   static const uint32_t occ = [] {
     const char* e = std::getenv("CEDARGPU_PROBE_OCC");
     const uint32_t v = e ? (uint32_t)std::atoi(e) : 4u;
-    return (v == 1u || v == 5u) ? v : 4u;
+    return (v == 1u || v == 3u || v == 5u) ? v : 4u;
   }();
   return occ;
 }
@@ -1917,6 +1920,8 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
   else if (seg == 16 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16 && occ == 5) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16) hipLaunchKernelGGL((cedar_probe_kernel<16, 64>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 8 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 8) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 32) hipLaunchKernelGGL((cedar_probe_kernel<32, 64>), grid, dim3(BLOCK), 0, s, k);
   else hipLaunchKernelGGL((cedar_probe_kernel<64, 64>), grid, dim3(BLOCK), 0, s, k);
 }
