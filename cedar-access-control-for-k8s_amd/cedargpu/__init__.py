@@ -10,4 +10,4 @@ is missing, and evaluation raises `DeviceError` when no GPU is present.
 """
 from ._lib import CedarGPUError, CompileError, DeviceError, lib, lib_path  # noqa: F401
 from .store import (AVPStore, Batch, Context, CRDStore, DirectoryStore, MemoryStore, PolicyStore,  # noqa: F401
-                    StaticStore, TieredPolicyStores, Authorizer, AdmissionHandler, admission_to_cedar_json, Queue, ALLOW_ALL_ADMISSION, build_image, image_stats, atomic_policies, device_count)
+                    StaticStore, TieredPolicyStores, Authorizer, AdmissionHandler, Compiler, admission_to_cedar_json, Queue, ALLOW_ALL_ADMISSION, build_image, image_stats, atomic_policies, device_count)

@@ -49,6 +49,8 @@ _SIGS = {
     "cg_compiler_destroy": (None, [P]),
     "cg_compiler_last_error": (cstr, [P]),
     "cg_compiler_add_tier": (ctypes.c_int, [P]),
+    "cg_compiler_clear": (ctypes.c_int, [P]),
+    "cg_compiler_cache_stats": (ctypes.c_int, [P, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     "cg_compiler_add_document": (ctypes.c_int, [P, cstr, cstr, sz, cstr, cstr]),
     "cg_compiler_add_policy": (ctypes.c_int, [P, cstr, cstr, cstr, sz, ctypes.c_int]),
     "cg_compiler_build": (ctypes.c_int, [P, u64, ctypes.POINTER(P), ctypes.POINTER(sz)]),

@@ -123,12 +123,29 @@ ALLOW_ALL_ADMISSION = StaticStore([(
     'k8s::admission::Action::"delete", k8s::admission::Action::"connect"], resource);')])
 
 
-def build_image(stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
-    """Compiles the tiers (one per store) into an image blob. Host only; no GPU needed."""
-    c = _P()
-    if lib.cg_compiler_create(ctypes.byref(c)):
-        raise CompileError(-1, "compiler create failed")
-    try:
+class Compiler:
+    """A policy compiler that keeps parsed documents across builds (cg_compiler_*): the incremental
+    rebuild a store change triggers parses only the new or changed documents."""
+
+    def __init__(self):
+        self._h = _P()
+        if lib.cg_compiler_create(ctypes.byref(self._h)):
+            raise CompileError(-1, "compiler create failed")
+
+    def close(self):
+        if self._h:
+            lib.cg_compiler_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def build(self, stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
+        c = self._h
+        lib.cg_compiler_clear(c)
         for st in stores:
             lib.cg_compiler_add_tier(c)
             for d in st.documents():
@@ -143,7 +160,7 @@ def build_image(stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
                 if rc:
                     raise _err(rc, lib.cg_compiler_last_error(c).decode())
         out = _P()
-        n = ctypes.c_size_t()
+        n = ctypes.c_size_t(0)
         rc = lib.cg_compiler_build(c, epoch, ctypes.byref(out), ctypes.byref(n))
         if rc:
             raise _err(rc, lib.cg_compiler_last_error(c).decode())
@@ -151,8 +168,20 @@ def build_image(stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
             return ctypes.string_at(out, n.value)
         finally:
             lib.cg_free(out)
+
+    def cache_stats(self) -> dict:
+        v = [ctypes.c_uint64() for _ in range(3)]
+        lib.cg_compiler_cache_stats(self._h, *[ctypes.byref(x) for x in v])
+        return dict(zip(("hits", "misses", "entries"), (x.value for x in v)))
+
+
+def build_image(stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
+    """Compiles the tiers (one per store) into an image blob. Host only; no GPU needed."""
+    c = Compiler()
+    try:
+        return c.build(stores, epoch)
     finally:
-        lib.cg_compiler_destroy(c)
+        c.close()
 
 
 def image_stats(image: bytes) -> dict:

@@ -16,6 +16,7 @@ using namespace cg;
 
 struct cg_compiler {
   std::vector<std::vector<DocSpec>> tiers;
+  ParseCache cache;  // parsed documents reused across builds
   std::string err;
 };
 
@@ -195,6 +196,24 @@ int cg_compiler_create(cg_compiler** out) {
 void cg_compiler_destroy(cg_compiler* c) { delete c; }
 const char* cg_compiler_last_error(cg_compiler* c) { return c ? c->err.c_str() : "null compiler"; }
 
+int cg_compiler_clear(cg_compiler* c) {
+  if (!c) return CG_E_ARG;
+  c->tiers.clear();
+  return CG_OK;
+}
+
+int cg_compiler_cache_stats(cg_compiler* c, uint64_t* hits, uint64_t* misses, uint64_t* entries) {
+  if (!c) return CG_E_ARG;
+  if (hits) *hits = c->cache.hits;
+  if (misses) *misses = c->cache.misses;
+  if (entries) {
+    uint64_t n = 0;
+    for (auto& kv : c->cache.map) n += kv.second.size();
+    *entries = n;
+  }
+  return CG_OK;
+}
+
 int cg_compiler_add_tier(cg_compiler* c) {
   if (!c) return CG_E_ARG;
   c->tiers.emplace_back();
@@ -237,7 +256,7 @@ int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* fi
 int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len) {
   if (!c || !image || !len) return CG_E_ARG;
   try {
-    auto img = compile_image(c->tiers, epoch);
+    auto img = compile_image(c->tiers, epoch, &c->cache);
     auto blob = img->serialize();
     uint8_t* p = (uint8_t*)std::malloc(blob.size());
     if (!p) { c->err = "out of host memory"; return CG_E_ARG; }

@@ -1920,7 +1920,6 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
   else if (seg == 16 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16 && occ == 5) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16) hipLaunchKernelGGL((cedar_probe_kernel<16, 64>), grid, dim3(BLOCK), 0, s, k);
-  else if (seg == 8 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 8) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 32) hipLaunchKernelGGL((cedar_probe_kernel<32, 64>), grid, dim3(BLOCK), 0, s, k);
   else hipLaunchKernelGGL((cedar_probe_kernel<64, 64>), grid, dim3(BLOCK), 0, s, k);

@@ -20,8 +20,13 @@
 // AVP `<id>.<i>` (verified_permissions.go:95), static `allow-all-admission` (main.go:112).
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <thread>
 
 #include "engine.h"
 
@@ -859,6 +864,14 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
     return;
   }
+  static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
+  auto t_mark = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!times) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "  index %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_mark).count());
+    t_mark = now;
+  };
   // stream record offset / length of every policy
   std::vector<uint32_t> rec_off(n), rec_len(n);
   for (size_t ch = 0; ch < img.chunks.size(); ch += 4) {
@@ -870,9 +883,13 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     }
   }
   // most specific level-1 keys of every policy: its scope's own entity / type / wildcard
-  std::map<L1, std::vector<uint32_t>> b1;
-  std::map<L2, std::vector<uint32_t>> b2;
-  std::map<L1, uint32_t> hmask;
+  // filings as flat (key, policy) records, sorted: each key's policies stay in policy order, and
+  // buckets are laid out in key order
+  constexpr uint32_t NO_POLICY = 0xFFFFFFFFu;  // a level-1 entry that only carries level-2 keys
+  std::vector<std::pair<L1, uint32_t>> r1;
+  std::vector<std::pair<L2, uint32_t>> r2;
+  r1.reserve(n);
+  r2.reserve(2 * (size_t)n);
   for (uint32_t p = 0; p < n; p++) {
     const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
     const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
@@ -900,17 +917,40 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
       const L1 k{combo, pt, pi, a.first, a.second, rt, ri};
       if ((pt != KW_ANY && pt >= (1u << 28)) || (rt != KW_ANY && rt >= (1u << 28))) throw CedarError("string table too large for the scope index");
       img.combo_mask |= 1u << combo;
-      if (!akeys[p].ok) { b1[k].push_back(p); continue; }
-      b1[k];  // the level-1 entry carries the hmask even when it has no unkeyed policies
-      hmask[k] |= 1u << akeys[p].h;
-      b2[L2(k, {akeys[p].h, akeys[p].v0, akeys[p].v1})].push_back(p);
-      if (!akeys[p].guarded) b2[L2(k, {akeys[p].h, MISSING_W0, 0u})].push_back(p);
+      if (!akeys[p].ok) { r1.emplace_back(k, p); continue; }
+      r1.emplace_back(k, NO_POLICY);  // the level-1 entry carries the hmask even without unkeyed policies
+      r2.emplace_back(L2(k, {akeys[p].h, akeys[p].v0, akeys[p].v1}), p);
+      if (!akeys[p].guarded) r2.emplace_back(L2(k, {akeys[p].h, MISSING_W0, 0u}), p);
     }
   }
+  std::sort(r1.begin(), r1.end());
+  std::sort(r2.begin(), r2.end());
+  r2.erase(std::unique(r2.begin(), r2.end()), r2.end());
+  // groups: [begin, end) ranges of one key; level-1 hmask from the level-2 keys under it
+  struct G { size_t b, e; uint32_t hmask = 0; };
+  std::vector<G> g1, g2;
+  for (size_t i = 0; i < r1.size();) {
+    size_t j = i;
+    while (j < r1.size() && r1[j].first == r1[i].first) j++;
+    g1.push_back({i, j});
+    i = j;
+  }
+  for (size_t i = 0; i < r2.size();) {
+    size_t j = i;
+    while (j < r2.size() && r2[j].first == r2[i].first) j++;
+    g2.push_back({i, j});
+    i = j;
+  }
+  for (size_t a = 0, k = 0; a < g2.size(); a++) {  // both sorted by level-1 key first
+    const L1& key = r2[g2[a].b].first.first;
+    while (k < g1.size() && r1[g1[k].b].first < key) k++;
+    if (k < g1.size() && r1[g1[k].b].first == key) g1[k].hmask |= 1u << r2[g2[a].b].first.second[0];
+  }
+  mark("buckets");
   // record heads (bucket order) then the ext area (one full record per policy)
   uint32_t n_heads = 0;
-  for (auto& kv : b1) n_heads += (uint32_t)kv.second.size();
-  for (auto& kv : b2) n_heads += (uint32_t)kv.second.size();
+  for (auto& x : r1) n_heads += x.second != NO_POLICY;
+  n_heads += (uint32_t)r2.size();
   std::vector<uint32_t> ext(n);
   uint64_t ext_end = (uint64_t)n_heads * HEAD_WORDS;
   for (uint32_t p = 0; p < n; p++) { ext[p] = (uint32_t)ext_end; ext_end += rec_len[p]; }
@@ -919,9 +959,11 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   for (uint32_t p = 0; p < n; p++)
     std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
   uint32_t head = 0;
-  auto put_heads = [&](const std::vector<uint32_t>& ps) {
+  auto put_heads = [&](auto begin, auto end) {
     const uint32_t first = head;
-    for (uint32_t p : ps) {
+    for (auto it = begin; it != end; ++it) {
+      const uint32_t p = it->second;
+      if (p == NO_POLICY) continue;
       uint32_t* hd = &img.bstream[(size_t)head * HEAD_WORDS];
       const uint32_t* src = &img.pstream[rec_off[p]];
       std::copy(src, src + std::min<uint32_t>(rec_len[p], HEAD_WORDS), hd);
@@ -930,7 +972,8 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     }
     return first;
   };
-  const size_t n_entries = b1.size() + b2.size();
+  mark("ext area");
+  const size_t n_entries = g1.size() + g2.size();
   uint32_t size = 16;
   while (size < 2 * n_entries) size <<= 1;
   img.btab.assign((size_t)size * BT_WORDS, 0);
@@ -951,54 +994,140 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
       img.bfilt[2 * blk + (b >> 5)] |= 1u << (b & 31);
     }
   };
-  for (auto& kv : b1) {
-    const L1& k = kv.first;
-    const uint32_t first = put_heads(kv.second);
+  mark("tables");
+  for (const G& g : g1) {
+    const L1& k = r1[g.b].first;
+    const uint32_t first = put_heads(r1.begin() + (long)g.b, r1.begin() + (long)g.e);
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], 0, 0, first,
-                                  (uint32_t)kv.second.size(), hmask.count(k) ? hmask[k] : 0u, 0, 0, 0, 0};
+                                  head - first, g.hmask, 0, 0, 0, 0};
     insert(l1_hash(k), e);
     filt_add(l1_hash(k));
   }
-  for (auto& kv : b2) {
-    const L1& k = kv.first.first;
-    const auto& x = kv.first.second;
-    const uint32_t first = put_heads(kv.second);
+  for (const G& g : g2) {
+    const L1& k = r2[g.b].first.first;
+    const auto& x = r2[g.b].first.second;
+    const uint32_t first = put_heads(r2.begin() + (long)g.b, r2.begin() + (long)g.e);
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16) | BT_L2 | x[0], k[1], k[2], k[3], k[4], k[5], k[6], x[1], x[2],
-                                  first, (uint32_t)kv.second.size(), 0, 0, 0, 0, 0};
+                                  first, head - first, 0, 0, 0, 0, 0};
     insert(bucket_hash2(l1_hash(k), x[0], x[1], x[2]), e);
     filt_add(bucket_hash2(l1_hash(k), x[0], x[1], x[2]));
   }
+  mark("heads+slots");
 }
 
-std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch) {
+// Parses every document of the tiers, through the cache when one is given (unseen documents on
+// worker threads).
+static std::vector<std::shared_ptr<const std::vector<Policy>>> parse_documents(
+    const std::vector<std::vector<DocSpec>>& tiers, ParseCache* cache) {
+  std::vector<const DocSpec*> docs;
+  for (auto& t : tiers)
+    for (auto& d : t) docs.push_back(&d);
+  std::vector<std::shared_ptr<const std::vector<Policy>>> out(docs.size());
+  auto key = [](const DocSpec& d) {
+    return std::hash<std::string>()(d.filename) * 0x9E3779B97F4A7C15ull ^ std::hash<std::string>()(d.text);
+  };
+  std::vector<size_t> todo;
+  if (cache) {
+    cache->generation++;
+    cache->hits = cache->misses = 0;
+    for (size_t i = 0; i < docs.size(); i++) {
+      auto it = cache->map.find(key(*docs[i]));
+      if (it != cache->map.end())
+        for (auto& e : it->second)
+          if (e.filename == docs[i]->filename && e.text == docs[i]->text) {
+            out[i] = e.policies;
+            e.used = cache->generation;
+            break;
+          }
+      if (out[i]) cache->hits++;
+      else { cache->misses++; todo.push_back(i); }
+    }
+  } else {
+    for (size_t i = 0; i < docs.size(); i++) todo.push_back(i);
+  }
+  // parse the rest; the first syntax error (in document order) is the one reported
+  std::vector<std::string> errs(docs.size());
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned nt = (unsigned)std::min<size_t>(hw, todo.size() / 8 + 1);
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t k; (k = next++) < todo.size();) {
+      const size_t i = todo[k];
+      try {
+        out[i] = std::make_shared<const std::vector<Policy>>(parse_policies(docs[i]->text, docs[i]->filename));
+      } catch (const CedarError& e) {
+        errs[i] = e.what();
+      }
+    }
+  };
+  if (nt <= 1) {
+    work();
+  } else {
+    std::vector<std::thread> ws;
+    for (unsigned t = 0; t < nt; t++) ws.emplace_back(work);
+    for (auto& w : ws) w.join();
+  }
+  for (size_t i = 0; i < docs.size(); i++)
+    if (!errs[i].empty()) throw CedarError(errs[i]);
+  if (cache) {
+    for (size_t i : todo)
+      cache->map[key(*docs[i])].push_back({docs[i]->filename, docs[i]->text, out[i], cache->generation});
+    for (auto it = cache->map.begin(); it != cache->map.end();) {  // drop what this build did not use
+      auto& v = it->second;
+      v.erase(std::remove_if(v.begin(), v.end(), [&](const ParseCache::Entry& e) { return e.used != cache->generation; }), v.end());
+      it = v.empty() ? cache->map.erase(it) : std::next(it);
+    }
+  }
+  return out;
+}
+
+std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch, ParseCache* cache) {
   if (tiers.empty()) throw CedarError("at least one policy tier is required");
   if (tiers.size() > 255) throw CedarError("too many tiers");
   auto img = std::make_shared<Image>();
   img->epoch = epoch;
   Compiler C(*img);
-  // parse every tier; PolicySet.Add semantics: a repeated ID replaces the earlier policy in place
-  std::vector<std::vector<Policy>> parsed(tiers.size());
+  // CEDARGPU_COMPILE_TIMES=1: phase times to stderr (profiling)
+  static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
+  auto t_mark = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!times) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "compile %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_mark).count());
+    t_mark = now;
+  };
+  const auto docs = parse_documents(tiers, cache);
+  mark("parse");
+  // PolicySet.Add semantics: a repeated ID replaces the earlier policy in place. The tiers refer
+  // to the parsed ASTs (owned by `docs` / the cache); only ID and position are per use.
+  struct PRef {
+    const Policy* p;
+    std::string id, filename;
+    Position pos;
+  };
+  std::vector<std::vector<PRef>> parsed(tiers.size());
+  size_t di = 0;
   for (size_t t = 0; t < tiers.size(); t++) {
     std::unordered_map<std::string, size_t> ids;
     for (auto& doc : tiers[t]) {
-      std::vector<Policy> ps = parse_policies(doc.text, doc.filename);
+      const std::vector<Policy>& ps = *docs[di++];
       if (!doc.explicit_id.empty() && ps.size() != 1)
         throw CedarError("document for policy " + doc.explicit_id + " must hold exactly one policy");
       for (size_t i = 0; i < ps.size(); i++) {
-        Policy& p = ps[i];
-        p.id = doc.explicit_id.empty() ? doc.id_prefix + std::to_string(i) + doc.id_suffix : doc.explicit_id;
-        if (doc.zero_position) { p.pos = Position{}; p.filename = ""; }
-        auto it = ids.find(p.id);
-        if (it != ids.end()) parsed[t][it->second] = std::move(p);
-        else { ids.emplace(p.id, parsed[t].size()); parsed[t].push_back(std::move(p)); }
+        PRef r{&ps[i], doc.explicit_id.empty() ? doc.id_prefix + std::to_string(i) + doc.id_suffix : doc.explicit_id,
+               doc.zero_position ? std::string() : ps[i].filename, doc.zero_position ? Position{} : ps[i].pos};
+        auto it = ids.find(r.id);
+        if (it != ids.end()) parsed[t][it->second] = std::move(r);
+        else { ids.emplace(r.id, parsed[t].size()); parsed[t].push_back(std::move(r)); }
       }
     }
   }
+  mark("assemble");
   // hot attribute paths over the whole image: the NHOT most used
   std::map<Compiler::Path, uint32_t> cnt;
   for (auto& tp : parsed)
-    for (auto& p : tp)
-      for (auto& c : p.conds) C.count_hot(*c.second, cnt);
+    for (auto& r : tp)
+      for (auto& c : r.p->conds) C.count_hot(*c.second, cnt);
   std::vector<std::pair<uint32_t, Compiler::Path>> order;
   for (auto& kv : cnt) order.emplace_back(kv.second, kv.first);
   std::sort(order.begin(), order.end(), [](auto& a, auto& b) { return a.first != b.first ? a.first > b.first : a.second < b.second; });
@@ -1011,17 +1140,19 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     for (uint32_t j = 0; j < MAX_PATH; j++) img->hot.push_back(j < path.second.size() ? path.second[j] : 0u);
   }
   for (auto& tp : parsed)
-    for (auto& p : tp) C.collect_actions(p.action);
+    for (auto& r : tp) C.collect_actions(r.p->action);
   img->amask_ok = img->act.size() / 2 <= MAX_ACT ? 1u : 0u;
   for (size_t t = 0; t < parsed.size(); t++) {
-    for (auto& p : parsed[t]) {
-      C.policy(p, (uint32_t)t);
+    for (auto& r : parsed[t]) {
+      C.policy(*r.p, (uint32_t)t);
       PolicyMeta m;
-      m.id = p.id; m.filename = p.filename; m.pos = p.pos; m.tier = (uint32_t)t; m.forbid = p.forbid;
+      m.id = std::move(r.id); m.filename = std::move(r.filename); m.pos = r.pos; m.tier = (uint32_t)t;
+      m.forbid = r.p->forbid;
       img->meta.push_back(std::move(m));
     }
     img->tier_end.push_back(img->n_pol());
   }
+  mark("lower");
   // device policy stream + chunk table
   {
     uint32_t p = 0;
@@ -1054,7 +1185,9 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     }
     if (img->pstream.empty()) img->pstream.resize(4, 0);
   }
+  mark("stream");
   build_scope_index(*img, C.akeys);
+  mark("scope index");
   // global string table
   img->gstr_off.clear();
   img->gstr_bytes.clear();
@@ -1067,6 +1200,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
   if (img->cpool.empty()) img->cpool.push_back(0);
   if (img->gstr_bytes.empty()) img->gstr_bytes.push_back(0);
   img->build_lookup();
+  mark("strings");
   return img;
 }
 

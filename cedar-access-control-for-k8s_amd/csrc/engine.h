@@ -97,7 +97,24 @@ struct DocSpec {
   bool zero_position = false;  // policies built from AST (e.g. allow-all-admission) carry Position{}
 };
 
-std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch);
+// Parsed documents kept across builds (the incremental compiler): a rebuild after a store change
+// parses only the documents whose (filename, text) it has not seen; the rest reuse their ASTs.
+// Entries a build does not use are dropped after it.
+struct ParseCache {
+  struct Entry {
+    std::string filename, text;
+    std::shared_ptr<const std::vector<Policy>> policies;
+    uint64_t used = 0;  // generation of the last build that used it
+  };
+  std::unordered_map<uint64_t, std::vector<Entry>> map;  // by hash of (filename, text)
+  uint64_t generation = 0;
+  uint64_t hits = 0, misses = 0;  // over the last build
+};
+
+// Compiles the tiers. With a cache, unseen documents are parsed on worker threads and reused
+// next time; the image is byte-identical to a build without the cache.
+std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch,
+                                     ParseCache* cache = nullptr);
 
 // Entity input for the encoder (already decoded from JSON or built by the k8s model).
 struct EntityIn {

@@ -59,7 +59,15 @@ int cg_compiler_add_document(cg_compiler* c, const char* filename, const char* t
  * AST (cedar.NewPolicyFromAST, e.g. allow-all-admission) whose Position is the zero value. */
 int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* filename, const char* text,
                            size_t len, int zero_position);
-/* Compiles all tiers into an image blob (free with cg_free). */
+/* Drops the tiers added so far but keeps the compiler's parse cache: the incremental rebuild after
+ * a store change (a CRD added / updated / removed, crd.go:45-118; a directory re-read,
+ * directory.go:41-82; an AVP sync, verified_permissions.go:58-100) re-adds every document and
+ * parses only those whose (filename, text) the previous build did not have. */
+int cg_compiler_clear(cg_compiler* c);
+/* Documents the last build took from the parse cache / parsed anew, and cache entries kept. */
+int cg_compiler_cache_stats(cg_compiler* c, uint64_t* hits, uint64_t* misses, uint64_t* entries);
+/* Compiles all tiers into an image blob (free with cg_free). Unseen documents parse on worker
+ * threads; the blob is byte-identical to a build by a fresh compiler. */
 int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len);
 /* Number of policies / tiers of a built image blob. */
 int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t* n_tiers, uint64_t* epoch);

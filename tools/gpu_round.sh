@@ -8,5 +8,5 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -3 gpurun_out/$TAG/pytest.log
 timeout -k 10 300 python -u bench.py ${BENCH_ARGS} > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || { echo "bench failed"; tail -30 gpurun_out/$TAG/bench.err; exit 1; }
 cat gpurun_out/$TAG/bench.json
-(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --latency-batches 0 --serve-threads 0 --no-reload ${BENCH_ARGS}) > gpurun_out/$TAG/rocprof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/$TAG/rocprof.log; exit 1; }
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --latency-batches 0 --serve-threads 0 --no-reload --configs-requests 0 ${BENCH_ARGS}) > gpurun_out/$TAG/rocprof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/$TAG/rocprof.log; exit 1; }
 find gpurun_out/$TAG/prof -name "*stats*"
