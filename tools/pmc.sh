@@ -6,7 +6,7 @@ TAG=${1:-pmc}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --latency-batches 0 --parity-sample 0 --no-reload ${BENCH_ARGS}"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --latency-batches 0 --parity-sample 0 --no-reload --serve-threads 0 --configs-requests 0 ${BENCH_ARGS}"
 run() {
   local name=$1; shift
   (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS) > $OUT/$name.log 2>&1 || { echo "pass $name failed"; tail -20 $OUT/$name.log; return 1; }
