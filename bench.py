@@ -150,6 +150,30 @@ def secondary_configs(ctx, n_req, threads, sample=512):
         ok, _, _, reasons = w
         return (ok, 200, reasons if not ok and reasons not in ("", "[]", "null") else "")
 
+    # C5: 100k policies over 1,000 tenants (one CRD document each): compile, incremental rebuild
+    # after one tenant changes, device load + activate, evaluation
+    tpop = synth.Population(seed=7, n_namespaces=1000)
+    docs = synth.multitenant_policies(100_000, seed=51, pop=tpop)
+    comp = cedargpu.Compiler()
+    t0 = time.perf_counter()
+    comp.build([cedargpu.CRDStore(docs)], epoch=200)
+    t_full = time.perf_counter() - t0
+    docs[500] = (docs[500][0], docs[500][1], docs[500][2].replace("permit", "forbid", 1))
+    t0 = time.perf_counter()
+    img5 = comp.build([cedargpu.CRDStore(docs)], epoch=201)
+    t_inc = time.perf_counter() - t0
+    comp.close()
+    t0 = time.perf_counter()
+    ctx.load(img5, 201)
+    t_load = time.perf_counter() - t0
+    tsars = synth.random_sars(n_req, seed=5000, pop=tpop)
+    items5, idx5 = oracle_items(tsars[:sample // 2])
+    run("c5_multitenant_100k", [cedargpu.CRDStore(docs)], synth.sars_json(tsars), lambda b, p: b.add_sar_json(p),
+        lambda b, i: b.authz(i), authz_want, items5, idx5,
+        "100k namespace-scoped policies over 1,000 tenant CRD documents x synthetic SubjectAccessReviews")
+    out["c5_multitenant_100k"].update({"compile_s": t_full, "incremental_rebuild_s": t_inc, "image_bytes": len(img5),
+                                       "load_activate_s": t_load})
+
     run("c4_admission_1k", [cedargpu.MemoryStore("adm.cedar", synth.admission_policies(1000, seed=3)),
                             cedargpu.ALLOW_ALL_ADMISSION],
         json.dumps(reviews, separators=(",", ":")), lambda b, p: b.add_admission_json(p), lambda b, i: b.admit(i),

@@ -327,3 +327,34 @@ def admission_policies(n: int, seed: int = 3) -> str:
                        f'when {{ resource has data && resource.data.contains({{"key": "key{int(rng.integers(0, 9))}", '
                        f'"value": "value{int(rng.integers(0, 100))}"}}) }};\n')
     return "\n".join(out)
+
+
+def multitenant_policies(n: int, seed: int = 51, pop: Optional[Population] = None) -> List[Tuple[str, str, str]]:
+    """C5: `n` policies across the population's namespaces as tenants, one Policy CRD document per
+    tenant ((name, uid, text) for CRDStore): group-scoped permits on the tenant's namespace and
+    resource, and production-name forbids."""
+    pop = pop or Population(seed=7, n_namespaces=1000)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    per = max(1, n // len(pop.namespaces))
+    gi = _zipf_idx(rng, len(pop.groups), n, s=0.9)
+    ri = rng.integers(len(RESOURCES), size=n)
+    u = rng.random((n, 2))
+    docs = []
+    k = 0
+    for t, ns in enumerate(pop.namespaces):
+        out = []
+        for i in range(per if t < len(pop.namespaces) - 1 else n - per * (len(pop.namespaces) - 1)):
+            g = pop.groups[int(gi[k])]
+            grp, ver, res = RESOURCES[int(ri[k])]
+            if u[k, 0] < 0.85:
+                verbs = ["get", "list", "watch"] if u[k, 1] < 0.6 else ["create", "update", "patch", "delete"]
+                out.append(f'permit (\n  principal in k8s::Group::{json.dumps(g)},\n  {_actions(verbs)},\n'
+                           f'  resource is k8s::Resource\n)\nwhen {{ resource has namespace && resource.namespace == '
+                           f'{json.dumps(ns)} && resource.resource == {json.dumps(res)} }};\n')
+            else:
+                out.append(f'forbid (\n  principal,\n  action in [k8s::Action::"delete", k8s::Action::"update"],\n'
+                           f'  resource is k8s::Resource\n)\nwhen {{ resource has namespace && resource.namespace == '
+                           f'{json.dumps(ns)} && resource has name && resource.name like "prod-*" }};\n')
+            k += 1
+        docs.append((f"tenant-{t:04d}", f"uid-{t:04d}", "\n".join(out)))
+    return docs
