@@ -1334,18 +1334,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
     wl.hot[seg][h] = valid ? make_uint2(__builtin_nontemporal_load(row + RW_HDR + 2 * h),
                                         __builtin_nontemporal_load(row + RW_HDR + 2 * h + 1))
                            : make_uint2(0u, 0u);
-  // action masks over the image action table (`==` and `in`), SEG actions per step
+  // action masks over the image action table (`==` and `in`), resolved by the encoder
   uint64_t am = 0, as = 0;
   if (a.amask_ok) {
-    for (uint32_t k0 = 0; k0 < a.n_act; k0 += SEG) {
-      const uint32_t k = k0 + sl;
-      const bool on = valid && k < a.n_act;
-      const uint32_t qt = on ? a.act[2 * k] : 0u, qi = on ? a.act[2 * k + 1] : 0u;
-      const bool self = on && c.at == qt && c.ai == qi;
-      const bool hit = self || (on && c.a_nanc && anc_scan(c.blk, c.a_anc, c.a_nanc, qt, qi));
-      am |= (sballot(hit) >> sbase) << k0;
-      as |= (sballot(self) >> sbase) << k0;
-    }
+    am = ((uint64_t)hdr(RW_AM1) << 32) | hdr(RW_AM0);
+    const uint32_t self = hdr(RW_ASELF);
+    as = (valid && self < 64u) ? (1ull << self) : 0ull;
   }
   wave_lds_sync();
 

@@ -189,6 +189,23 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   anc_into(blk[RH_PIDX], RW_PANC, RW_PN);
   anc_into(blk[RH_RIDX], RW_RANC, RW_RN);
   anc_into(blk[RH_AIDX], RW_AANC, RW_AN);
+  // action masks over the image action table, as the probe kernel tests scopes against them
+  row[RW_ASELF] = 0xFFFFFFFFu;
+  if (img.amask_ok) {
+    uint64_t am = 0;
+    const uint32_t n_act = (uint32_t)img.act.size() / 2;
+    const uint32_t aoff = row[RW_AANC], an = row[RW_AN];
+    for (uint32_t k = 0; k < n_act; k++) {
+      const uint32_t qt = img.act[2 * k], qi = img.act[2 * k + 1];
+      const bool self = au.first == qt && au.second == qi;
+      bool hit = self;
+      for (uint32_t j = 0; j < an && !hit; j++) hit = blk[aoff + 2 * j] == qt && blk[aoff + 2 * j + 1] == qi;
+      if (hit) am |= 1ull << k;
+      if (self) row[RW_ASELF] = k;
+    }
+    row[RW_AM0] = (uint32_t)am;
+    row[RW_AM1] = (uint32_t)(am >> 32);
+  }
   const uint32_t nh = img.n_hot();
   for (uint32_t h = 0; h < nh; h++) {
     const uint32_t* hp = &img.hot[(size_t)h * HOT_WORDS];

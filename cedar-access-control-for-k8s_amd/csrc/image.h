@@ -210,6 +210,9 @@ enum RowW : uint32_t {
   RW_RN = 10,
   RW_AN = 11,
   RW_BLK = 12,   // heap word offset of the request block
+  RW_AM0 = 13,   // action mask over the image action table (`in`: the action or an ancestor), low
+  RW_AM1 = 14,   //   ... high word (valid when the image's amask_ok)
+  RW_ASELF = 15, // index of the action itself in the action table (`==`), ~0u when absent
   RW_HDR = 16,   // hot slots follow: (w0, w1) per hot path
 };
 constexpr uint32_t MISSING_W0 = 0xFFFFFFFFu;  // level-2 index key of an absent hot value
