@@ -1280,13 +1280,15 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
 // [7] heads passing the scope re-check [8] atoms evaluated [9] hits [10] stage flushes
 // [11] candidate passes; cycles (s_memtime) in [12] row / hot / action loading [13] key probing
 // [14] candidate evaluation [15] merge and result writes
-template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false>
-__global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
+// PW: waves per block. Resources are granted per block, so a block's LDS and wave slots return
+// only when its slowest wave ends; smaller blocks let fast waves' slots be reused sooner.
+template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false, uint32_t PW = WAVES>
+__global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint64_t t_start = STATS ? clock64() : 0;
   using L = SegLds<SEG, HCAP>;
   static_assert(L::HC <= 4096 && L::XC <= 255, "hit slots are 12-bit sort payloads, error slots 8-bit");
   constexpr uint32_t NS = L::NS;
-  __shared__ L wl_all[WAVES];
+  __shared__ L wl_all[PW];
   const uint32_t lane = threadIdx.x & 63;
   L& wl = wl_all[threadIdx.x >> 6];
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
@@ -1304,7 +1306,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
     }
     return x;
   };
-  const uint32_t gid = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * NS + seg;
+  const uint32_t gid = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
   const bool valid = gid < a.n_req;
   const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0u;
   const uint32_t* row = a.rows + (size_t)r * a.row_words;
@@ -1589,7 +1591,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void cedar_probe_kernel(KArgs a) {
   if (STATS) {
     if (valid && sl == 0) st[0] = 1;
     const uint64_t t_end = clock64();
-    unsigned long long* w = a.stats + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * 16;
+    unsigned long long* w = a.stats + ((size_t)blockIdx.x * PW + (threadIdx.x >> 6)) * 16;
     for (uint32_t i = 0; i < 12; i++) {
       uint32_t x = valid ? st[i] : 0u;
       for (uint32_t o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, (int)o);
@@ -1876,8 +1878,22 @@ static bool probe_stats() {
   return on;
 }
 
+// Waves per block of the default probe kernel: 1 (one-wave blocks: a finished wave's slot is
+// reused at once; 4-wave blocks hold their resources until the slowest wave ends — 770M vs 626M
+// decisions/s, profiles/r01/ab_v9/wpb_*). CEDARGPU_PROBE_WPB = 2 / 4 for comparisons.
+static uint32_t probe_wpb() {
+  static const uint32_t w = [] {
+    const char* e = std::getenv("CEDARGPU_PROBE_WPB");
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : 1u;
+    return (v == 2u || v == 4u) ? v : 1u;
+  }();
+  return w;
+}
+
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
-  const uint32_t seg = big ? 64u : probe_seg(), per_block = WAVES * (64 / seg);
+  const uint32_t seg = big ? 64u : probe_seg();
+  const uint32_t wpb = (!big && seg == 16 && probe_occ() == 4 && !probe_stats()) ? probe_wpb() : WAVES;
+  const uint32_t per_block = wpb * (64 / seg);
   const dim3 grid((n + per_block - 1) / per_block);
   const uint32_t occ = probe_occ();
   if (!big && probe_stats()) {
@@ -1911,6 +1927,8 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     return;
   }
   if (big) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 16 && occ == 4 && wpb == 1) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, false, 1>), grid, dim3(64), 0, s, k);
+  else if (seg == 16 && occ == 4 && wpb == 2) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, false, 2>), grid, dim3(128), 0, s, k);
   else if (seg == 16 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16 && occ == 5) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16) hipLaunchKernelGGL((cedar_probe_kernel<16, 64>), grid, dim3(BLOCK), 0, s, k);
