@@ -1892,7 +1892,7 @@ static uint32_t probe_wpb() {
 
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
   const uint32_t seg = big ? 64u : probe_seg();
-  const uint32_t wpb = (!big && seg == 16 && probe_occ() == 4 && !probe_stats()) ? probe_wpb() : WAVES;
+  const uint32_t wpb = (!big && seg == 16 && (probe_occ() == 4 || probe_occ() == 5) && !probe_stats()) ? probe_wpb() : WAVES;
   const uint32_t per_block = wpb * (64 / seg);
   const dim3 grid((n + per_block - 1) / per_block);
   const uint32_t occ = probe_occ();
@@ -1930,6 +1930,7 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
   else if (seg == 16 && occ == 4 && wpb == 1) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, false, 1>), grid, dim3(64), 0, s, k);
   else if (seg == 16 && occ == 4 && wpb == 2) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, false, 2>), grid, dim3(128), 0, s, k);
   else if (seg == 16 && occ == 4) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 16 && occ == 5 && wpb == 1) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5, false, 1>), grid, dim3(64), 0, s, k);
   else if (seg == 16 && occ == 5) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16) hipLaunchKernelGGL((cedar_probe_kernel<16, 64>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 8) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3>), grid, dim3(BLOCK), 0, s, k);
