@@ -13,7 +13,7 @@ import csv, glob, sys, collections
 rows = []
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     rows += list(csv.DictReader(open(f)))
-rows = [r for r in rows if "cedar_probe_kernel<16u, 64u, 4u, false>" in r["Kernel_Name"]]
+rows = [r for r in rows if "cedar_probe_kernel<16u, 64u, 4u, false" in r["Kernel_Name"]]
 g = max(int(r["Grid_Size"]) for r in rows)
 acc = collections.defaultdict(float)
 disp = set()
