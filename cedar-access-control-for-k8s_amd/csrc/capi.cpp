@@ -686,6 +686,7 @@ int cg_batch_submit(cg_batch* b) {
   if (b->host.n() == 0) { b->submitted = b->done = true; return CG_OK; }
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   if (dev_eval(b->img->dev, b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  if (dev_download_async(b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   b->submitted = true;
   return CG_OK;
 }
@@ -695,7 +696,7 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   if (!b->submitted) { b->err = "batch not submitted"; return CG_E_STATE; }
   if (b->done) return CG_OK;
   (void)timeout_ns;  // stream sync is bounded by the kernel; the webhook deadline is enforced by the caller
-  if (dev_download(b->dev, b->host, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  if (dev_download_finish(b->dev, b->host)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   // Overflowed result lists: re-run just those requests. Capacity overflows of the probe kernel
   // re-run there with the exact capacities; requests it could not decide (RF_GENERAL) and any
   // stream-kernel overflow re-run on the stream kernel, which reports exact counts, so a second

@@ -1805,6 +1805,8 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.reasons_p = (uint32_t*)(o + o_rp);
   d.errs = (uint32_t*)(o + o_er);
   d.bytes = in_bytes + d.out_bytes;
+  d.stream = stream;
+  d.pending = true;
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
   HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
   HIPCHK(hipMemsetAsync(d.res, 0, n * 2 * 4, s), "memset res");
@@ -1813,10 +1815,20 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
 
 void dev_batch_free(DevBatch* d) {
   if (d->device < 0) return;
+  (void)hipSetDevice(d->device);
+  if (d->pending && d->stream) {
+    // work on the batch's blocks may still run (submitted, never waited): drain its stream first
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+      (void)hipEventRecord(e, (hipStream_t)d->stream);
+      (void)hipEventSynchronize(e);
+      (void)hipEventDestroy(e);
+    } else {
+      (void)hipDeviceSynchronize();
+    }
+  }
+  if (d->done) (void)hipEventDestroy((hipEvent_t)d->done);
   if (d->pool) {
-    // the stream may still be reading the staging block / writing results: wait before reuse
-    (void)hipSetDevice(d->device);
-    (void)hipDeviceSynchronize();
     pool_put(d->pool, false, d->in_blk, d->in_cls);
     pool_put(d->pool, false, d->out_blk, d->out_cls);
     pool_put(d->pool, true, d->stage, d->stage_cls);
@@ -2002,9 +2014,7 @@ int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx,
   return rc;
 }
 
-int dev_download(const DevBatch& b, Batch& host, void* stream) {
-  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
-  hipStream_t s = (hipStream_t)stream;
+static void copy_results(const DevBatch& b, Batch& host) {
   const size_t n = b.n;
   host.capr = b.capr;
   host.cape = b.cape;
@@ -2012,9 +2022,7 @@ int dev_download(const DevBatch& b, Batch& host, void* stream) {
   host.reasons_f.resize(n * b.capr);
   host.reasons_p.resize(n * b.capr);
   host.errs.resize(n * b.cape * ERR_WORDS);
-  if (n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
-  HIPCHK(hipStreamSynchronize(s), "sync download");
-  if (!n) return 0;
+  if (!n) return;
   const uint8_t* st = (const uint8_t*)b.stage;
   const uint8_t* base = (const uint8_t*)b.out_blk;
   auto cp = [&](std::vector<uint32_t>& v, const uint32_t* dev) {
@@ -2024,6 +2032,36 @@ int dev_download(const DevBatch& b, Batch& host, void* stream) {
   cp(host.reasons_f, b.reasons_f);
   cp(host.reasons_p, b.reasons_p);
   cp(host.errs, b.errs);
+}
+
+int dev_download(DevBatch& b, Batch& host, void* stream) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
+  HIPCHK(hipStreamSynchronize(s), "sync download");
+  b.pending = false;
+  copy_results(b, host);
+  return 0;
+}
+
+int dev_download_async(DevBatch& b, void* stream) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  if (!b.done) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    b.done = (void*)e;
+  }
+  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
+  HIPCHK(hipEventRecord((hipEvent_t)b.done, s), "event record");
+  return 0;
+}
+
+int dev_download_finish(DevBatch& b, Batch& host) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  if (b.done) HIPCHK(hipEventSynchronize((hipEvent_t)b.done), "event sync");
+  b.pending = false;
+  copy_results(b, host);
   return 0;
 }
 

@@ -36,6 +36,9 @@ struct DevBatch {
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)
   size_t in_cls = 0, out_cls = 0, stage_cls = 0, out_bytes = 0;
+  void* stream = nullptr;  // the stream the batch's work runs on
+  void* done = nullptr;    // event after the result download (dev_download_async)
+  bool pending = false;    // work enqueued on the batch's buffers not yet waited for
 };
 
 // All functions return 0 on success, or a negative CG_E_* code with dev_last_error() set.
@@ -58,7 +61,12 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream);
 int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
                     uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
                     std::vector<uint32_t>& rp, std::vector<uint32_t>& er);
-int dev_download(const DevBatch& b, Batch& host, void* stream);
+int dev_download(DevBatch& b, Batch& host, void* stream);
+// Enqueues the results' copy into the batch's pinned block right behind its evaluation and records
+// an event, so that the next batch's upload and launch queue behind it without a host round trip.
+int dev_download_async(DevBatch& b, void* stream);
+// Waits for that event and copies the results out of the pinned block.
+int dev_download_finish(DevBatch& b, Batch& host);
 int dev_stream_create(int device, void** stream);
 void dev_stream_destroy(void* stream);
 int dev_stream_sync(void* stream);

@@ -84,7 +84,7 @@ void cg_queue::run() {
     uint64_t seq = 0;
     Clock::time_point t;
   };
-  std::vector<InFlight> flight;  // at most one batch on the device while the next is built
+  std::vector<InFlight> flight;  // at most one batch on the device while the next is built / queued
   auto drain = [&] {
     for (auto& st : stripes) {
       {
@@ -111,8 +111,8 @@ void cg_queue::run() {
     drain();
     if (backlog.empty()) {
       if (!flight.empty()) {  // nothing to build: finish the batch on the device
-        finish(flight.back());
-        flight.clear();
+        finish(flight.front());
+        flight.erase(flight.begin());
         continue;
       }
       if (stop.load()) return;
@@ -152,10 +152,11 @@ void cg_queue::run() {
     const uint64_t n = qb->b->items.size();
     for (uint64_t m = max_seen.load(); n > m && !max_seen.compare_exchange_weak(m, n);) {
     }
-    // the previous batch finishes before this one is submitted (one stream; its download first)
+    // the batch on the device finishes (its callers released) before this one is submitted: in a
+    // closed loop of callers, releasing them early is worth more than the host time overlapped
     if (!flight.empty()) {
-      finish(flight.back());
-      flight.clear();
+      finish(flight.front());
+      flight.erase(flight.begin());
     }
     InFlight f{qb, my, Clock::now()};
     qb->rc = cg_batch_submit(qb->b);
