@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cctype>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -11,6 +12,29 @@
 #include "admission.h"
 #include "capi_internal.h"
 #include "sar.h"
+
+namespace {
+// CEDARGPU_TRACE_LAT=1: one stderr line per submit / wait with the microseconds of each phase
+// (diagnostic only; off by default).
+struct LatTrace {
+  static bool on() {
+    static const bool v = [] { const char* e = std::getenv("CEDARGPU_TRACE_LAT"); return e && *e == '1'; }();
+    return v;
+  }
+  const char* what;
+  std::chrono::steady_clock::time_point t;
+  std::string line;
+  explicit LatTrace(const char* w) : what(w) { if (on()) t = std::chrono::steady_clock::now(); }
+  void mark(const char* phase) {
+    if (!on()) return;
+    auto n = std::chrono::steady_clock::now();
+    line += " "; line += phase; line += "=";
+    line += std::to_string(std::chrono::duration<double, std::micro>(n - t).count());
+    t = n;
+  }
+  ~LatTrace() { if (on() && !line.empty()) std::fprintf(stderr, "LAT %s%s\n", what, line.c_str()); }
+};
+}  // namespace
 
 using namespace cg;
 
@@ -682,11 +706,16 @@ uint32_t cg_batch_size(cg_batch* b) { return b ? (uint32_t)b->items.size() : 0; 
 int cg_batch_submit(cg_batch* b) {
   if (!b) return CG_E_ARG;
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
+  LatTrace tr("submit");
   b->host.finalize_strings();
+  tr.mark("finalize");
   if (b->host.n() == 0) { b->submitted = b->done = true; return CG_OK; }
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  tr.mark("upload");
   if (dev_eval(b->img->dev, b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  tr.mark("launch");
   if (dev_download_async(b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  tr.mark("d2h_enqueue");
   b->submitted = true;
   return CG_OK;
 }
@@ -696,7 +725,9 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   if (!b->submitted) { b->err = "batch not submitted"; return CG_E_STATE; }
   if (b->done) return CG_OK;
   (void)timeout_ns;  // stream sync is bounded by the kernel; the webhook deadline is enforced by the caller
+  LatTrace tr("wait");
   if (dev_download_finish(b->dev, b->host)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  tr.mark("sync_copy");
   // Overflowed result lists: re-run just those requests. Capacity overflows of the probe kernel
   // re-run there with the exact capacities; requests it could not decide (RF_GENERAL) and any
   // stream-kernel overflow re-run on the stream kernel, which reports exact counts, so a second
@@ -716,12 +747,36 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       idx_probe.push_back(i); capr_p = std::max(capr_p, nr); cape_p = std::max(cape_p, ne);
     }
   }
-  // re-runs a subset (mode: 1 probe kernel, 2 its large-stage variant, 0 stream kernel); requests
-  // a probe re-run cannot decide move on to the next mode
+  // Folds one re-run's results (subset order) into the batch. Requests a probe re-run cannot decide
+  // move on to `next`; those whose lists overflowed again go to `again` with their exact counts.
+  auto apply = [&](const std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, int mode, const std::vector<uint32_t>& res,
+                   const std::vector<uint32_t>& rf, const std::vector<uint32_t>& rp, const std::vector<uint32_t>& er,
+                   std::vector<uint32_t>& again, uint32_t& capr2, uint32_t& cape2, std::vector<uint32_t>& next) {
+    for (size_t k = 0; k < idx.size(); k++) {
+      uint32_t i = idx[k];
+      uint32_t fl = res[2 * k] >> 16;
+      uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
+      if (mode && (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) { next.push_back(i); continue; }
+      if (fl & cgi::RF_OVERFLOW) {
+        again.push_back(i);
+        capr2 = std::max(capr2, nr);
+        cape2 = std::max(cape2, ne);
+        continue;
+      }
+      const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
+      b->host.res[2 * (size_t)i] = res[2 * k];
+      b->host.res[2 * (size_t)i + 1] = res[2 * k + 1];
+      b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
+      b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
+    }
+  };
+  auto clampr = [](uint32_t c, uint32_t lo) { return std::max(std::min(c, 4096u), lo); };
+  // re-runs a subset (mode: 1 probe kernel, 2 its large-stage variant, 0 stream kernel) until its
+  // lists fit, one round trip per pass
   auto rerun = [&](std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, int mode, std::vector<uint32_t>& next) -> int {
     for (int pass = 0; pass < 3 && !idx.empty(); pass++) {
-      capr = std::max(std::min(capr, 4096u), 8u);
-      cape = std::max(std::min(cape, 4096u), 4u);
+      capr = clampr(capr, 8u);
+      cape = clampr(cape, 4u);
       std::vector<uint32_t> res, rf, rp, er;
       if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->stream, res, rf, rp, er)) {
         b->err = dev_last_error();
@@ -729,23 +784,7 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       }
       std::vector<uint32_t> again;
       uint32_t capr2 = 0, cape2 = 0;
-      for (size_t k = 0; k < idx.size(); k++) {
-        uint32_t i = idx[k];
-        uint32_t fl = res[2 * k] >> 16;
-        uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
-        if (mode && (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) { next.push_back(i); continue; }
-        if (fl & cgi::RF_OVERFLOW) {
-          again.push_back(i);
-          capr2 = std::max(capr2, nr);
-          cape2 = std::max(cape2, ne);
-          continue;
-        }
-        const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
-        b->host.res[2 * (size_t)i] = res[2 * k];
-        b->host.res[2 * (size_t)i + 1] = res[2 * k + 1];
-        b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
-        b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
-      }
+      apply(idx, capr, cape, mode, res, rf, rp, er, again, capr2, cape2, next);
       idx.swap(again);
       capr = capr2;
       cape = cape2;
@@ -754,18 +793,48 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     return CG_OK;
   };
   int rc;
-  if (!idx_probe.empty() && (rc = rerun(idx_probe, capr_p, cape_p, 1, idx_big))) return rc;
-  if (!idx_big.empty()) {
-    capr_b = std::max(capr_b, 64u);
-    cape_b = std::max(cape_b, 16u);
-    if ((rc = rerun(idx_big, capr_b, cape_b, 2, idx_gen))) return rc;
+  tr.mark("scan");
+  // First round: the three subsets are known from the first pass's flags, so their re-runs are
+  // enqueued back to back and share one wait. Leftovers (rare: a probe re-run that found it needs
+  // the large stage or the stream kernel, or lists that overflowed again) finish sequentially.
+  {
+    struct Sub { std::vector<uint32_t>* idx; uint32_t capr, cape; int mode; DevSubset job; };
+    Sub subs[3] = {{&idx_probe, clampr(capr_p, 8u), clampr(cape_p, 4u), 1, {}},
+                   {&idx_big, clampr(capr_b, 64u), clampr(cape_b, 16u), 2, {}},
+                   {&idx_gen, clampr(capr_g, 64u), clampr(cape_g, 16u), 0, {}}};
+    int brc = 0;
+    for (auto& u : subs)
+      if (!brc && !u.idx->empty())
+        brc = dev_subset_begin(b->img->dev, b->dev, u.idx->data(), (uint32_t)u.idx->size(), u.capr, u.cape, u.mode, b->ctx->stream, &u.job);
+    std::vector<uint32_t> res[3], rf[3], rp[3], er[3];
+    for (int k = 0; k < 3; k++) {
+      const int erc = dev_subset_end(&subs[k].job, res[k], rf[k], rp[k], er[k]);
+      if (!brc) brc = erc;
+    }
+    if (brc) { b->err = dev_last_error(); return CG_E_DEVICE; }
+    std::vector<uint32_t> again[3], next_big, next_gen;
+    uint32_t capr2[3] = {0, 0, 0}, cape2[3] = {0, 0, 0};
+    std::vector<uint32_t>* nexts[3] = {&next_big, &next_gen, &next_gen};
+    for (int k = 0; k < 3; k++)
+      if (!subs[k].idx->empty())
+        apply(*subs[k].idx, subs[k].capr, subs[k].cape, subs[k].mode, res[k], rf[k], rp[k], er[k], again[k], capr2[k], cape2[k], *nexts[k]);
+    tr.mark("rerun_batched");
+    if (!again[0].empty() && (rc = rerun(again[0], capr2[0], cape2[0], 1, next_big))) return rc;
+    if (!next_big.empty()) {
+      // exact counts unknown for these: the large stage reports them, a second pass completes it
+      if ((rc = rerun(next_big, 64u, 16u, 2, next_gen))) return rc;
+    }
+    if (!again[1].empty() && (rc = rerun(again[1], capr2[1], cape2[1], 2, next_gen))) return rc;
+    if (!again[2].empty()) {
+      std::vector<uint32_t> none;
+      if ((rc = rerun(again[2], capr2[2], cape2[2], 0, none))) return rc;
+    }
+    if (!next_gen.empty()) {
+      std::vector<uint32_t> none;
+      if ((rc = rerun(next_gen, 64u, 16u, 0, none))) return rc;
+    }
   }
-  if (!idx_gen.empty()) {
-    capr_g = std::max(capr_g, 64u);
-    cape_g = std::max(cape_g, 16u);
-    std::vector<uint32_t> none;
-    if ((rc = rerun(idx_gen, capr_g, cape_g, 0, none))) return rc;
-  }
+  tr.mark("rerun_big_general");
   b->done = true;
   return CG_OK;
 }

@@ -1969,49 +1969,79 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
 }
 
 // Re-evaluates a subset of requests (overflowed result lists) with larger capacities; results are
-// compact in subset order and copied to host before returning.
-int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
-                    uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
-                    std::vector<uint32_t>& rp, std::vector<uint32_t>& er) {
+// compact in subset order. _begin enqueues (H2D of the indices, launch, D2H) on `stream` without
+// waiting, so several subsets share one host round trip; _end waits and copies the results out.
+int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
+                     uint32_t cape, int probe, void* stream, DevSubset* job) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
+  *job = DevSubset();
   if (n == 0) return 0;
   if (!b.pool) { g_err = "batch has no buffer pool"; return -4; }
   for (uint32_t i = 0; i < n; i++) if (idx[i] >= b.n) { g_err = "request index out of range"; return -2; }
   // one device block [idx | res | reasons_f | reasons_p | errs] and one pinned block, from the pool
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t o_idx = 0, o_res = al((size_t)n * 4), o_rf = o_res + al((size_t)n * 2 * 4),
-               o_rp = o_rf + al((size_t)n * capr * 4), o_er = o_rp + al((size_t)n * capr * 4),
-               total = o_er + al((size_t)n * cape * ERR_WORDS * 4);
-  void *dblk = nullptr, *hblk = nullptr;
-  size_t dcls = 0, hcls = 0;
+  DevSubset j;
+  j.pool = b.pool;
+  j.stream = stream;
+  j.n = n;
+  j.capr = capr;
+  j.cape = cape;
+  j.o_res = al((size_t)n * 4);
+  j.o_rf = j.o_res + al((size_t)n * 2 * 4);
+  j.o_rp = j.o_rf + al((size_t)n * capr * 4);
+  j.o_er = j.o_rp + al((size_t)n * capr * 4);
+  j.total = j.o_er + al((size_t)n * cape * ERR_WORDS * 4);
   int rc;
-  if ((rc = pool_get(b.pool, false, total, &dblk, &dcls))) return rc;
-  if ((rc = pool_get(b.pool, true, total, &hblk, &hcls))) { pool_put(b.pool, false, dblk, dcls); return rc; }
-  uint8_t* d8 = (uint8_t*)dblk;
-  uint8_t* h8 = (uint8_t*)hblk;
-  std::memcpy(h8 + o_idx, idx, (size_t)n * 4);
-  do {
-    hipError_t e;
-    if ((e = hipMemcpyAsync(d8 + o_idx, h8 + o_idx, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) { rc = fail(e, "H2D"); break; }
-    KArgs k = make_args(img, b, (uint32_t*)(d8 + o_idx), n, (uint32_t*)(d8 + o_res), (uint32_t*)(d8 + o_rf),
-                        (uint32_t*)(d8 + o_rp), (uint32_t*)(d8 + o_er), capr, cape);
-    if (probe && img.indexed)
-      launch_probe(k, n, s, probe == 2);
-    else
-      hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
-    if ((e = hipGetLastError()) != hipSuccess) { rc = fail(e, "launch"); break; }
-    if ((e = hipMemcpyAsync(h8 + o_res, d8 + o_res, total - o_res, hipMemcpyDeviceToHost, s)) != hipSuccess) { rc = fail(e, "D2H"); break; }
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) { rc = fail(e, "sync"); break; }
-    res.assign((const uint32_t*)(h8 + o_res), (const uint32_t*)(h8 + o_res) + (size_t)n * 2);
-    rf.assign((const uint32_t*)(h8 + o_rf), (const uint32_t*)(h8 + o_rf) + (size_t)n * capr);
-    rp.assign((const uint32_t*)(h8 + o_rp), (const uint32_t*)(h8 + o_rp) + (size_t)n * capr);
-    er.assign((const uint32_t*)(h8 + o_er), (const uint32_t*)(h8 + o_er) + (size_t)n * cape * ERR_WORDS);
-  } while (0);
-  if (rc) (void)hipStreamSynchronize(s);  // nothing of ours in flight before the blocks are reused
-  pool_put(b.pool, false, dblk, dcls);
-  pool_put(b.pool, true, hblk, hcls);
+  if ((rc = pool_get(b.pool, false, j.total, &j.dblk, &j.dcls))) return rc;
+  if ((rc = pool_get(b.pool, true, j.total, &j.hblk, &j.hcls))) { pool_put(b.pool, false, j.dblk, j.dcls); return rc; }
+  uint8_t* d8 = (uint8_t*)j.dblk;
+  uint8_t* h8 = (uint8_t*)j.hblk;
+  std::memcpy(h8, idx, (size_t)n * 4);
+  *job = j;  // blocks owned by the job from here on (returned by dev_subset_end)
+  hipError_t e;
+  if ((e = hipMemcpyAsync(d8, h8, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return fail(e, "H2D");
+  KArgs k = make_args(img, b, (uint32_t*)d8, n, (uint32_t*)(d8 + j.o_res), (uint32_t*)(d8 + j.o_rf),
+                      (uint32_t*)(d8 + j.o_rp), (uint32_t*)(d8 + j.o_er), capr, cape);
+  if (probe && img.indexed)
+    launch_probe(k, n, s, probe == 2);
+  else
+    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
+  if ((e = hipGetLastError()) != hipSuccess) return fail(e, "launch");
+  if ((e = hipMemcpyAsync(h8 + j.o_res, d8 + j.o_res, j.total - j.o_res, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e, "D2H");
+  return 0;
+}
+
+int dev_subset_end(DevSubset* job, std::vector<uint32_t>& res, std::vector<uint32_t>& rf, std::vector<uint32_t>& rp,
+                   std::vector<uint32_t>& er) {
+  if (!job->dblk) return 0;
+  // on success or failure nothing of ours is in flight once the stream drained
+  hipError_t e = hipStreamSynchronize((hipStream_t)job->stream);
+  int rc = 0;
+  if (e != hipSuccess) {
+    rc = fail(e, "sync");
+  } else {
+    const uint8_t* h8 = (const uint8_t*)job->hblk;
+    const size_t n = job->n;
+    res.assign((const uint32_t*)(h8 + job->o_res), (const uint32_t*)(h8 + job->o_res) + n * 2);
+    rf.assign((const uint32_t*)(h8 + job->o_rf), (const uint32_t*)(h8 + job->o_rf) + n * job->capr);
+    rp.assign((const uint32_t*)(h8 + job->o_rp), (const uint32_t*)(h8 + job->o_rp) + n * job->capr);
+    er.assign((const uint32_t*)(h8 + job->o_er), (const uint32_t*)(h8 + job->o_er) + n * job->cape * ERR_WORDS);
+  }
+  pool_put(job->pool, false, job->dblk, job->dcls);
+  pool_put(job->pool, true, job->hblk, job->hcls);
+  *job = DevSubset();
   return rc;
+}
+
+int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
+                    uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
+                    std::vector<uint32_t>& rp, std::vector<uint32_t>& er) {
+  DevSubset j;
+  int rc = dev_subset_begin(img, b, idx, n, capr, cape, probe, stream, &j);
+  std::vector<uint32_t> r2, f2, p2, e2;
+  int rc2 = rc ? dev_subset_end(&j, r2, f2, p2, e2) : dev_subset_end(&j, res, rf, rp, er);
+  return rc ? rc : rc2;
 }
 
 static void copy_results(const DevBatch& b, Batch& host) {

@@ -61,6 +61,20 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream);
 int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
                     uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
                     std::vector<uint32_t>& rp, std::vector<uint32_t>& er);
+// The same, split: _begin enqueues one subset's re-run on `stream`; _end waits for the stream and
+// copies its results (several subsets enqueued back to back share one wait).
+struct DevSubset {
+  DevPool* pool = nullptr;
+  void* stream = nullptr;
+  void *dblk = nullptr, *hblk = nullptr;
+  size_t dcls = 0, hcls = 0;
+  uint32_t n = 0, capr = 0, cape = 0;
+  size_t o_res = 0, o_rf = 0, o_rp = 0, o_er = 0, total = 0;
+};
+int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
+                     uint32_t cape, int probe, void* stream, DevSubset* job);
+int dev_subset_end(DevSubset* job, std::vector<uint32_t>& res, std::vector<uint32_t>& rf, std::vector<uint32_t>& rp,
+                   std::vector<uint32_t>& er);
 int dev_download(DevBatch& b, Batch& host, void* stream);
 // Enqueues the results' copy into the batch's pinned block right behind its evaluation and records
 // an event, so that the next batch's upload and launch queue behind it without a host round trip.

@@ -18,13 +18,13 @@ using namespace cgi;
 void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, const Image& img, EncodedRequest& e, uint32_t& w0,
                      uint32_t& w1);
 
-const std::string& Batch::str(uint32_t i, uint32_t id) const {
-  static const std::string empty;
+std::string Batch::str(uint32_t i, uint32_t id) const {
   const uint32_t ng = img->n_gstr();
   if (id < ng) return img->strings[id];
-  if (i >= req_base.size()) return empty;
+  if (i >= req_base.size()) return std::string();
   const size_t j = (size_t)heap[req_base[i] + RH_SBASE] + (id - ng);
-  return j < bstrings.size() ? bstrings[j] : empty;
+  if (j >= n_bstr()) return std::string();
+  return std::string((const char*)bstr_bytes.data() + bstr_off[j], bstr_off[j + 1] - bstr_off[j]);
 }
 
 namespace {
@@ -64,13 +64,19 @@ void Batch::append(EncodedRequest& e) {
   if (!row_words) row_words = img->row_words();
   if (e.row.size() != row_words || e.blk.size() < RH_WORDS) throw CedarError("request encoded for another image");
   if (heap.size() + e.blk.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
-  if (bstrings.size() + e.strs.size() > 0xFFFFFFFFull) throw CedarError("batch string table overflow");
-  e.blk[RH_SBASE] = (uint32_t)bstrings.size();
+  size_t sbytes = 0;
+  for (auto& s : e.strs) sbytes += s.size();
+  if (n_bstr() + e.strs.size() >= 0xFFFFFFFFull || bstr_bytes.size() + sbytes > 0xFFFFFFFFull)
+    throw CedarError("batch string table overflow");
+  e.blk[RH_SBASE] = n_bstr();
   e.row[RW_BLK] = (uint32_t)heap.size();
   req_base.push_back((uint32_t)heap.size());
   heap.insert(heap.end(), e.blk.begin(), e.blk.end());
   rows.insert(rows.end(), e.row.begin(), e.row.end());
-  for (auto& s : e.strs) bstrings.push_back(std::move(s));
+  for (auto& s : e.strs) {
+    bstr_bytes.insert(bstr_bytes.end(), s.begin(), s.end());
+    bstr_off.push_back((uint32_t)bstr_bytes.size());
+  }
 }
 
 void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
@@ -79,14 +85,8 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
   append(e);
 }
 
+// The string table is built as requests are appended; the device reads at least one byte and word.
 void Batch::finalize_strings() {
-  bstr_off.clear();
-  bstr_bytes.clear();
-  for (auto& s : bstrings) {
-    bstr_off.push_back((uint32_t)bstr_bytes.size());
-    bstr_bytes.insert(bstr_bytes.end(), s.begin(), s.end());
-  }
-  bstr_off.push_back((uint32_t)bstr_bytes.size());
   if (bstr_bytes.empty()) bstr_bytes.push_back(0);
   if (heap.empty()) heap.push_back(0);
 }

@@ -156,9 +156,11 @@ struct Batch {
   std::vector<uint32_t> heap, req_base;
   std::vector<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
   uint32_t row_words = 0;
-  std::vector<std::string> bstrings;  // request-local strings of every request, concatenated
-  std::vector<uint32_t> bstr_off;
+  // request-local strings of every request, appended as requests arrive: string j is
+  // bstr_bytes[bstr_off[j] .. bstr_off[j + 1]) (bstr_off keeps a trailing end offset)
+  std::vector<uint32_t> bstr_off{0};
   std::vector<uint8_t> bstr_bytes;
+  uint32_t n_bstr() const { return (uint32_t)bstr_off.size() - 1; }
   // results
   uint32_t capr = 8, cape = 4;
   std::vector<uint32_t> res, reasons_f, reasons_p, errs;
@@ -167,7 +169,7 @@ struct Batch {
 
   uint32_t n() const { return (uint32_t)req_base.size(); }
   // string `id` as request i sees it
-  const std::string& str(uint32_t i, uint32_t id) const;
+  std::string str(uint32_t i, uint32_t id) const;
   void add(const std::vector<EntityIn>& ents, const RequestIn& req);  // encode_request + append
   void append(EncodedRequest& e);                                     // moves e's strings
   void finalize_strings();
