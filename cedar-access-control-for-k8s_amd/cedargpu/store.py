@@ -362,6 +362,14 @@ class Batch:
             raise _err(rc, "reasons failed")
         return list(arr[:n.value]), ne.value
 
+    def reruns(self) -> int:
+        """Requests whose result lists overflowed the first pass and were re-run (cg_batch_reruns)."""
+        n = ctypes.c_uint32()
+        rc = lib.cg_batch_reruns(self._h, ctypes.byref(n))
+        if rc:
+            raise _err(rc, "reruns failed")
+        return n.value
+
     def time(self, iters: int) -> float:
         ms = ctypes.c_float()
         rc = lib.cg_batch_time(self._h, iters, ctypes.byref(ms))

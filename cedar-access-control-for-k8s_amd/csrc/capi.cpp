@@ -747,15 +747,15 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       idx_probe.push_back(i); capr_p = std::max(capr_p, nr); cape_p = std::max(cape_p, ne);
     }
   }
-  // Folds one re-run's results (subset order) into the batch. Requests a probe re-run cannot decide
-  // move on to `next`; those whose lists overflowed again go to `again` with their exact counts.
-  auto apply = [&](const std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, int mode, const std::vector<uint32_t>& res,
-                   const std::vector<uint32_t>& rf, const std::vector<uint32_t>& rp, const std::vector<uint32_t>& er,
+  // Folds one re-run's results (subset order, read in place from the job's pinned block) into the
+  // batch. Requests a probe re-run cannot decide move on to `next`; those whose lists overflowed
+  // again go to `again` with their exact counts.
+  auto apply = [&](const std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, int mode, const SubsetView& v,
                    std::vector<uint32_t>& again, uint32_t& capr2, uint32_t& cape2, std::vector<uint32_t>& next) {
     for (size_t k = 0; k < idx.size(); k++) {
       uint32_t i = idx[k];
-      uint32_t fl = res[2 * k] >> 16;
-      uint32_t nr = res[2 * k + 1] & 0xFFFF, ne = res[2 * k + 1] >> 16;
+      uint32_t fl = v.res[2 * k] >> 16;
+      uint32_t nr = v.res[2 * k + 1] & 0xFFFF, ne = v.res[2 * k + 1] >> 16;
       if (mode && (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) { next.push_back(i); continue; }
       if (fl & cgi::RF_OVERFLOW) {
         again.push_back(i);
@@ -763,11 +763,10 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
         cape2 = std::max(cape2, ne);
         continue;
       }
-      const auto& src = (fl & cgi::RF_FORBID) ? rf : rp;
-      b->host.res[2 * (size_t)i] = res[2 * k];
-      b->host.res[2 * (size_t)i + 1] = res[2 * k + 1];
-      b->host.big_reasons[i].assign(src.begin() + (long)(k * capr), src.begin() + (long)(k * capr + nr));
-      b->host.big_errs[i].assign(er.begin() + (long)(k * cape * cgi::ERR_WORDS), er.begin() + (long)((k * cape + ne) * cgi::ERR_WORDS));
+      const uint32_t* src = (fl & cgi::RF_FORBID) ? v.rf : v.rp;
+      b->host.res[2 * (size_t)i] = v.res[2 * k];
+      b->host.res[2 * (size_t)i + 1] = v.res[2 * k + 1];
+      b->host.set_big(i, src + k * capr, nr, v.er + k * cape * cgi::ERR_WORDS, ne * cgi::ERR_WORDS);
     }
   };
   auto clampr = [](uint32_t c, uint32_t lo) { return std::max(std::min(c, 4096u), lo); };
@@ -777,14 +776,25 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     for (int pass = 0; pass < 3 && !idx.empty(); pass++) {
       capr = clampr(capr, 8u);
       cape = clampr(cape, 4u);
-      std::vector<uint32_t> res, rf, rp, er;
-      if (dev_eval_subset(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->stream, res, rf, rp, er)) {
+      DevSubset job;
+      SubsetView v;
+      if (dev_subset_begin(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->stream, &job) ||
+          dev_subset_end(&job, &v)) {
         b->err = dev_last_error();
+        (void)dev_stream_sync(b->ctx->stream);
+        dev_subset_release(&job);
         return CG_E_DEVICE;
       }
       std::vector<uint32_t> again;
       uint32_t capr2 = 0, cape2 = 0;
-      apply(idx, capr, cape, mode, res, rf, rp, er, again, capr2, cape2, next);
+      try {
+        apply(idx, capr, cape, mode, v, again, capr2, cape2, next);
+      } catch (const std::exception& ex) {
+        b->err = ex.what();
+        dev_subset_release(&job);
+        return CG_E_RANGE;
+      }
+      b->held.push_back(job);  // the batch's lists point into its pinned block
       idx.swap(again);
       capr = capr2;
       cape = cape2;
@@ -792,32 +802,46 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     if (!idx.empty()) { b->err = "result lists exceed the device re-run capacity"; return CG_E_RANGE; }
     return CG_OK;
   };
+  b->n_rerun = (uint32_t)(idx_probe.size() + idx_big.size() + idx_gen.size());
   int rc;
   tr.mark("scan");
   // First round: the three subsets are known from the first pass's flags, so their re-runs are
   // enqueued back to back and share one wait. Leftovers (rare: a probe re-run that found it needs
   // the large stage or the stream kernel, or lists that overflowed again) finish sequentially.
   {
-    struct Sub { std::vector<uint32_t>* idx; uint32_t capr, cape; int mode; DevSubset job; };
-    Sub subs[3] = {{&idx_probe, clampr(capr_p, 8u), clampr(cape_p, 4u), 1, {}},
-                   {&idx_big, clampr(capr_b, 64u), clampr(cape_b, 16u), 2, {}},
-                   {&idx_gen, clampr(capr_g, 64u), clampr(cape_g, 16u), 0, {}}};
+    struct Sub { std::vector<uint32_t>* idx; uint32_t capr, cape; int mode; DevSubset job; SubsetView v; };
+    Sub subs[3] = {{&idx_probe, clampr(capr_p, 8u), clampr(cape_p, 4u), 1, {}, {}},
+                   {&idx_big, clampr(capr_b, 64u), clampr(cape_b, 16u), 2, {}, {}},
+                   {&idx_gen, clampr(capr_g, 64u), clampr(cape_g, 16u), 0, {}, {}}};
     int brc = 0;
     for (auto& u : subs)
       if (!brc && !u.idx->empty())
         brc = dev_subset_begin(b->img->dev, b->dev, u.idx->data(), (uint32_t)u.idx->size(), u.capr, u.cape, u.mode, b->ctx->stream, &u.job);
-    std::vector<uint32_t> res[3], rf[3], rp[3], er[3];
-    for (int k = 0; k < 3; k++) {
-      const int erc = dev_subset_end(&subs[k].job, res[k], rf[k], rp[k], er[k]);
-      if (!brc) brc = erc;
-    }
-    if (brc) { b->err = dev_last_error(); return CG_E_DEVICE; }
+    for (auto& u : subs)
+      if (!brc) brc = dev_subset_end(&u.job, &u.v);
     std::vector<uint32_t> again[3], next_big, next_gen;
     uint32_t capr2[3] = {0, 0, 0}, cape2[3] = {0, 0, 0};
     std::vector<uint32_t>* nexts[3] = {&next_big, &next_gen, &next_gen};
-    for (int k = 0; k < 3; k++)
-      if (!subs[k].idx->empty())
-        apply(*subs[k].idx, subs[k].capr, subs[k].cape, subs[k].mode, res[k], rf[k], rp[k], er[k], again[k], capr2[k], cape2[k], *nexts[k]);
+    int arc = CG_OK;
+    if (brc) {
+      b->err = dev_last_error();
+      (void)dev_stream_sync(b->ctx->stream);  // nothing in flight before the blocks go back
+      arc = CG_E_DEVICE;
+    } else {
+      try {
+        for (int k = 0; k < 3; k++)
+          if (!subs[k].idx->empty())
+            apply(*subs[k].idx, subs[k].capr, subs[k].cape, subs[k].mode, subs[k].v, again[k], capr2[k], cape2[k], *nexts[k]);
+      } catch (const std::exception& ex) {
+        b->err = ex.what();
+        arc = CG_E_RANGE;
+      }
+    }
+    for (auto& u : subs) {
+      if (arc) dev_subset_release(&u.job);
+      else if (u.job.dblk) b->held.push_back(u.job);  // the batch's lists point into its pinned block
+    }
+    if (arc) return arc;
     tr.mark("rerun_batched");
     if (!again[0].empty() && (rc = rerun(again[0], capr2[0], cape2[0], 1, next_big))) return rc;
     if (!next_big.empty()) {
@@ -836,6 +860,13 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   }
   tr.mark("rerun_big_general");
   b->done = true;
+  return CG_OK;
+}
+
+int cg_batch_reruns(cg_batch* b, uint32_t* n) {
+  if (!b || !n) return CG_E_ARG;
+  if (!b->done) return CG_E_STATE;
+  *n = b->n_rerun;
   return CG_OK;
 }
 

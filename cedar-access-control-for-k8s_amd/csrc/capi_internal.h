@@ -51,12 +51,17 @@ struct cg_batch {
   cg::Batch host;
   cg::DevBatch dev;
   bool submitted = false, done = false;
+  uint32_t n_rerun = 0;  // requests re-run by cg_batch_wait
   std::string err;
   // items: caller-visible entries; dev >= 0 is the device request index, else a fast-path result
   struct Item { int32_t dev; int32_t fast; };
   std::vector<Item> items;
   std::map<uint32_t, std::string> fast_reason;  // authz fast paths: the reason; admission: error text
-  ~cg_batch() { dev_batch_free(&dev); }
+  std::vector<cg::DevSubset> held;  // re-run result blocks the host lists point into (Batch::big)
+  ~cg_batch() {
+    for (auto& j : held) dev_subset_release(&j);
+    dev_batch_free(&dev);
+  }
   int32_t dev_of(uint32_t i) const { return i < items.size() ? items[i].dev : -1; }
 };
 

@@ -1970,7 +1970,8 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
 
 // Re-evaluates a subset of requests (overflowed result lists) with larger capacities; results are
 // compact in subset order. _begin enqueues (H2D of the indices, launch, D2H) on `stream` without
-// waiting, so several subsets share one host round trip; _end waits and copies the results out.
+// waiting, so several subsets share one host round trip; _end waits and points at the results in
+// the job's pinned block; _release returns the job's blocks to the pool.
 int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
                      uint32_t cape, int probe, void* stream, DevSubset* job) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
@@ -1998,7 +1999,7 @@ int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx
   uint8_t* d8 = (uint8_t*)j.dblk;
   uint8_t* h8 = (uint8_t*)j.hblk;
   std::memcpy(h8, idx, (size_t)n * 4);
-  *job = j;  // blocks owned by the job from here on (returned by dev_subset_end)
+  *job = j;  // blocks owned by the job from here on (returned by dev_subset_release)
   hipError_t e;
   if ((e = hipMemcpyAsync(d8, h8, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return fail(e, "H2D");
   KArgs k = make_args(img, b, (uint32_t*)d8, n, (uint32_t*)(d8 + j.o_res), (uint32_t*)(d8 + j.o_rf),
@@ -2012,36 +2013,30 @@ int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx
   return 0;
 }
 
-int dev_subset_end(DevSubset* job, std::vector<uint32_t>& res, std::vector<uint32_t>& rf, std::vector<uint32_t>& rp,
-                   std::vector<uint32_t>& er) {
+int dev_subset_end(DevSubset* job, SubsetView* v) {
+  *v = SubsetView();
   if (!job->dblk) return 0;
   // on success or failure nothing of ours is in flight once the stream drained
   hipError_t e = hipStreamSynchronize((hipStream_t)job->stream);
-  int rc = 0;
   if (e != hipSuccess) {
-    rc = fail(e, "sync");
-  } else {
-    const uint8_t* h8 = (const uint8_t*)job->hblk;
-    const size_t n = job->n;
-    res.assign((const uint32_t*)(h8 + job->o_res), (const uint32_t*)(h8 + job->o_res) + n * 2);
-    rf.assign((const uint32_t*)(h8 + job->o_rf), (const uint32_t*)(h8 + job->o_rf) + n * job->capr);
-    rp.assign((const uint32_t*)(h8 + job->o_rp), (const uint32_t*)(h8 + job->o_rp) + n * job->capr);
-    er.assign((const uint32_t*)(h8 + job->o_er), (const uint32_t*)(h8 + job->o_er) + n * job->cape * ERR_WORDS);
+    const int rc = fail(e, "sync");
+    dev_subset_release(job);
+    return rc;
   }
-  pool_put(job->pool, false, job->dblk, job->dcls);
-  pool_put(job->pool, true, job->hblk, job->hcls);
-  *job = DevSubset();
-  return rc;
+  const uint8_t* h8 = (const uint8_t*)job->hblk;
+  v->res = (const uint32_t*)(h8 + job->o_res);
+  v->rf = (const uint32_t*)(h8 + job->o_rf);
+  v->rp = (const uint32_t*)(h8 + job->o_rp);
+  v->er = (const uint32_t*)(h8 + job->o_er);
+  return 0;
 }
 
-int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
-                    uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
-                    std::vector<uint32_t>& rp, std::vector<uint32_t>& er) {
-  DevSubset j;
-  int rc = dev_subset_begin(img, b, idx, n, capr, cape, probe, stream, &j);
-  std::vector<uint32_t> r2, f2, p2, e2;
-  int rc2 = rc ? dev_subset_end(&j, r2, f2, p2, e2) : dev_subset_end(&j, res, rf, rp, er);
-  return rc ? rc : rc2;
+void dev_subset_release(DevSubset* job) {
+  if (job->pool) {
+    pool_put(job->pool, false, job->dblk, job->dcls);
+    pool_put(job->pool, true, job->hblk, job->hcls);
+  }
+  *job = DevSubset();
 }
 
 static void copy_results(const DevBatch& b, Batch& host) {

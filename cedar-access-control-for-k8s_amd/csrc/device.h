@@ -56,13 +56,10 @@ void dev_batch_free(DevBatch* d);  // returns the blocks to the batch's pool
 // Evaluates every request of the batch into the batch's device result buffers (async on stream).
 int dev_eval(const DevImage& img, DevBatch& b, void* stream);
 // Re-evaluates the subset idx[0..n) with larger result capacities (probe 1: on the probe kernel,
-// 2: on its large-stage variant, for an indexed image; 0: the stream kernel); synchronous,
-// results on host.
-int dev_eval_subset(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
-                    uint32_t cape, int probe, void* stream, std::vector<uint32_t>& res, std::vector<uint32_t>& rf,
-                    std::vector<uint32_t>& rp, std::vector<uint32_t>& er);
-// The same, split: _begin enqueues one subset's re-run on `stream`; _end waits for the stream and
-// copies its results (several subsets enqueued back to back share one wait).
+// 2: on its large-stage variant, for an indexed image; 0: the stream kernel). Results are compact
+// in subset order. _begin enqueues one subset's re-run on `stream` (several subsets enqueued back
+// to back share one wait); _end waits for the stream and points `v` at the results in the job's
+// pinned block, valid until dev_subset_release returns the job's blocks to the pool.
 struct DevSubset {
   DevPool* pool = nullptr;
   void* stream = nullptr;
@@ -71,10 +68,13 @@ struct DevSubset {
   uint32_t n = 0, capr = 0, cape = 0;
   size_t o_res = 0, o_rf = 0, o_rp = 0, o_er = 0, total = 0;
 };
+struct SubsetView {
+  const uint32_t *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
+};
 int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
                      uint32_t cape, int probe, void* stream, DevSubset* job);
-int dev_subset_end(DevSubset* job, std::vector<uint32_t>& res, std::vector<uint32_t>& rf, std::vector<uint32_t>& rp,
-                   std::vector<uint32_t>& er);
+int dev_subset_end(DevSubset* job, SubsetView* v);
+void dev_subset_release(DevSubset* job);
 int dev_download(DevBatch& b, Batch& host, void* stream);
 // Enqueues the results' copy into the batch's pinned block right behind its evaluation and records
 // an event, so that the next batch's upload and launch queue behind it without a host round trip.

@@ -165,7 +165,12 @@ struct Batch {
   uint32_t capr = 8, cape = 4;
   std::vector<uint32_t> res, reasons_f, reasons_p, errs;
   // per-request overflow re-run results (index -> reasons / errors)
-  std::unordered_map<uint32_t, std::vector<uint32_t>> big_reasons, big_errs;
+  // Re-run results: request i's reason / error list read in place from the re-run's pinned result
+  // block, which the owning cg_batch keeps until it is destroyed (big stays empty until a re-run
+  // fills one; ptr null = the first pass's lists).
+  struct BigRef { const uint32_t *r = nullptr, *e = nullptr; uint32_t nr = 0, ne_words = 0; };
+  std::vector<BigRef> big;
+  void set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words);
 
   uint32_t n() const { return (uint32_t)req_base.size(); }
   // string `id` as request i sees it

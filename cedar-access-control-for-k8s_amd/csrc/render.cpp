@@ -17,18 +17,27 @@ bool Batch::decision(uint32_t i) const { return (res[2 * (size_t)i] & 0xFF) == D
 void Batch::reason_ids(uint32_t i, std::vector<uint32_t>& out) const {
   out.clear();
   uint32_t n = res[2 * (size_t)i + 1] & 0xFFFF;
-  auto it = big_reasons.find(i);
-  if (it != big_reasons.end()) { out = it->second; return; }
+  if (!big.empty() && big[i].r) {
+    out.assign(big[i].r, big[i].r + big[i].nr);
+    return;
+  }
   uint32_t flags = res[2 * (size_t)i] >> 16;
   const std::vector<uint32_t>& src = (flags & RF_FORBID) ? reasons_f : reasons_p;
   for (uint32_t k = 0; k < n && k < capr; k++) out.push_back(src[(size_t)i * capr + k]);
 }
 
+void Batch::set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words) {
+  if (big.empty()) big.resize(n());
+  big[i] = BigRef{reasons, errs, nr, nerr_words};
+}
+
 void Batch::error_recs(uint32_t i, std::vector<uint32_t>& out) const {
   out.clear();
   uint32_t n = res[2 * (size_t)i + 1] >> 16;
-  auto it = big_errs.find(i);
-  if (it != big_errs.end()) { out = it->second; return; }
+  if (!big.empty() && big[i].r) {
+    out.assign(big[i].e, big[i].e + big[i].ne_words);
+    return;
+  }
   for (uint32_t k = 0; k < n && k < cape; k++)
     for (uint32_t w = 0; w < ERR_WORDS; w++) out.push_back(errs[((size_t)i * cape + k) * ERR_WORDS + w]);
 }

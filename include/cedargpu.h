@@ -132,6 +132,9 @@ int cg_batch_diagnostic(cg_batch* b, uint32_t i, int reasons_only, char* buf, si
 int cg_batch_reasons(cg_batch* b, uint32_t i, uint32_t* idx, uint32_t cap, uint32_t* n, uint32_t* n_errors);
 /* Re-launches evaluation of the resident batch `iters` times; device time via HIP events. */
 int cg_batch_time(cg_batch* b, uint32_t iters, float* ms_total);
+/* Requests of the batch whose result lists overflowed the first pass and were re-run by
+ * cg_batch_wait (diagnostic; valid once the batch is done). */
+int cg_batch_reruns(cg_batch* b, uint32_t* n);
 /* Device bytes of the batch (heap + results) and of its image. */
 int cg_batch_bytes(cg_batch* b, uint64_t* batch_bytes, uint64_t* image_bytes, uint64_t* heap_bytes);
 
