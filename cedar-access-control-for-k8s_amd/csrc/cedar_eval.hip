@@ -26,6 +26,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <algorithm>
 #include <vector>
 #include <string>
@@ -1792,7 +1793,28 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     return rc;
   }
   uint8_t* st = (uint8_t*)d.stage;
-  for (int k = 0; k < 5; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
+  // Large batches (admission objects run to ~600 B per request) are staged by several threads:
+  // one core's memcpy into pinned memory runs at ~10 GB/s.
+  size_t total_len = 0;
+  for (int k = 0; k < 5; k++) total_len += len[k];
+  const unsigned nt = total_len >= (8u << 20) ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
+  if (nt <= 1) {
+    for (int k = 0; k < 5; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
+  } else {
+    auto part = [&](unsigned t) {  // byte range [t, t+1) / nt of the concatenated sections
+      const size_t lo = total_len * t / nt, hi = total_len * (t + 1) / nt;
+      size_t pos = 0;
+      for (int k = 0; k < 5; k++) {
+        const size_t a = std::max(lo, pos), b = std::min(hi, pos + len[k]);
+        if (a < b) std::memcpy(st + off[k] + (a - pos), (const uint8_t*)src[k] + (a - pos), b - a);
+        pos += len[k];
+      }
+    };
+    std::vector<std::thread> ts;
+    for (unsigned t = 1; t < nt; t++) ts.emplace_back(part, t);
+    part(0);
+    for (auto& th : ts) th.join();
+  }
   uint8_t* in = (uint8_t*)d.in_blk;
   uint8_t* o = (uint8_t*)d.out_blk;
   d.heap = (uint32_t*)(in + off[0]);
@@ -2039,24 +2061,18 @@ void dev_subset_release(DevSubset* job) {
   *job = DevSubset();
 }
 
-static void copy_results(const DevBatch& b, Batch& host) {
-  const size_t n = b.n;
+// Points the host batch's result arrays into the pinned staging block the results were copied to
+// (the block stays with the batch until dev_batch_free).
+static void bind_results(const DevBatch& b, Batch& host) {
   host.capr = b.capr;
   host.cape = b.cape;
-  host.res.resize(n * 2);
-  host.reasons_f.resize(n * b.capr);
-  host.reasons_p.resize(n * b.capr);
-  host.errs.resize(n * b.cape * ERR_WORDS);
-  if (!n) return;
-  const uint8_t* st = (const uint8_t*)b.stage;
+  uint8_t* st = (uint8_t*)b.stage;
   const uint8_t* base = (const uint8_t*)b.out_blk;
-  auto cp = [&](std::vector<uint32_t>& v, const uint32_t* dev) {
-    if (!v.empty()) std::memcpy(v.data(), st + ((const uint8_t*)dev - base), v.size() * 4);
-  };
-  cp(host.res, b.res);
-  cp(host.reasons_f, b.reasons_f);
-  cp(host.reasons_p, b.reasons_p);
-  cp(host.errs, b.errs);
+  auto at = [&](const uint32_t* dev) { return (uint32_t*)(st + ((const uint8_t*)dev - base)); };
+  host.res = b.n ? at(b.res) : nullptr;
+  host.reasons_f = b.n ? at(b.reasons_f) : nullptr;
+  host.reasons_p = b.n ? at(b.reasons_p) : nullptr;
+  host.errs = b.n ? at(b.errs) : nullptr;
 }
 
 int dev_download(DevBatch& b, Batch& host, void* stream) {
@@ -2065,7 +2081,7 @@ int dev_download(DevBatch& b, Batch& host, void* stream) {
   if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
   HIPCHK(hipStreamSynchronize(s), "sync download");
   b.pending = false;
-  copy_results(b, host);
+  bind_results(b, host);
   return 0;
 }
 
@@ -2086,7 +2102,7 @@ int dev_download_finish(DevBatch& b, Batch& host) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   if (b.done) HIPCHK(hipEventSynchronize((hipEvent_t)b.done), "event sync");
   b.pending = false;
-  copy_results(b, host);
+  bind_results(b, host);
   return 0;
 }
 

@@ -163,7 +163,11 @@ struct Batch {
   uint32_t n_bstr() const { return (uint32_t)bstr_off.size() - 1; }
   // results
   uint32_t capr = 8, cape = 4;
-  std::vector<uint32_t> res, reasons_f, reasons_p, errs;
+  // first-pass results, read in place from the batch's pinned staging block (device.h DevBatch;
+  // valid while the batch lives): res[2i], [2i+1] per request, capr reasons of each effect, cape
+  // error records. res is written back by overflow re-runs.
+  uint32_t* res = nullptr;
+  const uint32_t *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
   // per-request overflow re-run results (index -> reasons / errors)
   // Re-run results: request i's reason / error list read in place from the re-run's pinned result
   // block, which the owning cg_batch keeps until it is destroyed (big stays empty until a re-run

@@ -22,7 +22,7 @@ void Batch::reason_ids(uint32_t i, std::vector<uint32_t>& out) const {
     return;
   }
   uint32_t flags = res[2 * (size_t)i] >> 16;
-  const std::vector<uint32_t>& src = (flags & RF_FORBID) ? reasons_f : reasons_p;
+  const uint32_t* src = (flags & RF_FORBID) ? reasons_f : reasons_p;
   for (uint32_t k = 0; k < n && k < capr; k++) out.push_back(src[(size_t)i * capr + k]);
 }
 
