@@ -710,6 +710,12 @@ int cg_batch_submit(cg_batch* b) {
   b->host.finalize_strings();
   tr.mark("finalize");
   if (b->host.n() == 0) { b->submitted = b->done = true; return CG_OK; }
+  // First-pass reason capacity: up to the probe kernel's 64-hit stage while the two reason arrays
+  // stay within 4 MB (small, latency-bound batches then need no re-run for 9..64 reasons); large
+  // throughput batches keep 8 per effect.
+  // CEDARGPU_FIRST_CAPR pins it (tests drive the 9..64-reason re-run path with small batches).
+  b->host.capr = std::max<uint32_t>(8u, std::min<uint32_t>(64u, (uint32_t)((4u << 20) / (8ull * b->host.n()))));
+  if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   tr.mark("upload");
   if (dev_eval(b->img->dev, b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
@@ -732,6 +738,25 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   // re-run there with the exact capacities; requests it could not decide (RF_GENERAL) and any
   // stream-kernel overflow re-run on the stream kernel, which reports exact counts, so a second
   // pass with those capacities completes it.
+  // Many-hit requests the on-device follow-up completed (large stage right behind the first pass,
+  // same results block): their lists are final, unless the follow-up itself overflowed.
+  if (b->host.fu.cap) {
+    const auto& fu = b->host.fu;
+    const uint32_t cnt = std::min(fu.wl[0], fu.cap);
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t i = fu.wl[1 + k];
+      if (i >= b->host.n()) { b->err = "follow-up worklist out of range"; return CG_E_DEVICE; }
+      const uint32_t fl = fu.res[2 * k] >> 16;
+      if (!(fl & cgi::RF_VALID) || (fl & (cgi::RF_OVERFLOW | cgi::RF_GENERAL | cgi::RF_BIG))) continue;
+      const uint32_t nr = fu.res[2 * k + 1] & 0xFFFF, ne = fu.res[2 * k + 1] >> 16;
+      b->host.res[2 * (size_t)i] = fu.res[2 * k];
+      b->host.res[2 * (size_t)i + 1] = fu.res[2 * k + 1];
+      GUARD(b->err, {
+        b->host.set_big(i, ((fl & cgi::RF_FORBID) ? fu.rf : fu.rp) + (size_t)k * fu.capr, nr,
+                        fu.er + (size_t)k * fu.cape * cgi::ERR_WORDS, ne * cgi::ERR_WORDS);
+      })
+    }
+  }
   std::vector<uint32_t> idx_probe, idx_big, idx_gen;
   uint32_t capr_p = 0, cape_p = 0, capr_b = 0, cape_b = 0, capr_g = 0, cape_g = 0;
   for (uint32_t i = 0; i < b->host.n(); i++) {

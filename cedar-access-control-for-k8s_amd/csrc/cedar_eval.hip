@@ -70,6 +70,9 @@ struct KArgs {
   const uint32_t* __restrict__ bstream;
   const uint32_t* __restrict__ rows;     // columnar request rows (row_words each)
   unsigned long long* stats;             // probe-kernel work counters (STATS variant only)
+  uint32_t* fu_wl;                       // first pass: RF_BIG worklist [count, ids] (null: none)
+  const uint32_t* n_dev;                 // follow-up pass: request count on the device (null: n_req)
+  uint32_t fu_cap;
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
 };
 
@@ -1308,7 +1311,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     return x;
   };
   const uint32_t gid = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
-  const bool valid = gid < a.n_req;
+  const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;
+  const bool valid = gid < n_req;
   const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0u;
   const uint32_t* row = a.rows + (size_t)r * a.row_words;
 
@@ -1534,6 +1538,10 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     const uint32_t why = (structural || L::HC >= 1024) ? RF_GENERAL : RF_BIG;
     a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | why) << 16);
     a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
+    if (why == RF_BIG && a.fu_wl) {  // hand it to the follow-up launch (first pass: gid == r)
+      const uint32_t k = atomicAdd(a.fu_wl, 1u);
+      if (k < a.fu_cap) a.fu_wl[1 + k] = gid;
+    }
   }
   const uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge
   // bitonic sort of (policy index << 8 | slot) over the wave's largest power of two >= nh
@@ -1783,7 +1791,15 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   for (int k = 0; k < 5; k++) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
   const size_t n = std::max<uint32_t>(b.n(), 1);
   const size_t o_res = 0, o_rf = al(n * 2 * 4), o_rp = o_rf + al(n * d.capr * 4), o_er = o_rp + al(n * d.capr * 4);
-  d.out_bytes = o_er + al(n * d.cape * ERR_WORDS * 4);
+  // on-device follow-up for batches up to 65,536 requests: n / 32 entries (4..64), 256 reasons
+  d.fu_cap = b.n() <= 65536u ? std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u)) : 0u;
+  if (const char* e = std::getenv("CEDARGPU_FOLLOWUP")) if (*e == '0') d.fu_cap = 0;
+  d.fu_capr = 256;
+  d.fu_cape = 16;
+  const size_t o_fwl = o_er + al(n * d.cape * ERR_WORDS * 4), o_fres = o_fwl + al((1 + (size_t)d.fu_cap) * 4),
+               o_frf = o_fres + al((size_t)d.fu_cap * 2 * 4), o_frp = o_frf + al((size_t)d.fu_cap * d.fu_capr * 4),
+               o_fer = o_frp + al((size_t)d.fu_cap * d.fu_capr * 4);
+  d.out_bytes = d.fu_cap ? o_fer + al((size_t)d.fu_cap * d.fu_cape * ERR_WORDS * 4) : o_fwl;
   int rc;
   if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) return rc;
   if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) { pool_put(pool, false, d.in_blk, d.in_cls); return rc; }
@@ -1826,12 +1842,20 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.reasons_f = (uint32_t*)(o + o_rf);
   d.reasons_p = (uint32_t*)(o + o_rp);
   d.errs = (uint32_t*)(o + o_er);
+  if (d.fu_cap) {
+    d.fu_wl = (uint32_t*)(o + o_fwl);
+    d.fu_res = (uint32_t*)(o + o_fres);
+    d.fu_rf = (uint32_t*)(o + o_frf);
+    d.fu_rp = (uint32_t*)(o + o_frp);
+    d.fu_er = (uint32_t*)(o + o_fer);
+  }
   d.bytes = in_bytes + d.out_bytes;
   d.stream = stream;
   d.pending = true;
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
   HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
   HIPCHK(hipMemsetAsync(d.res, 0, n * 2 * 4, s), "memset res");
+  if (d.fu_cap) HIPCHK(hipMemsetAsync(d.fu_wl, 0, 4, s), "memset worklist");
   return 0;
 }
 
@@ -1875,6 +1899,9 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.stats = nullptr;
+  k.fu_wl = nullptr;
+  k.n_dev = nullptr;
+  k.fu_cap = 0;
   return k;
 }
 
@@ -1985,8 +2012,19 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
   if (b.n == 0) return 0;
   if (img.device != b.device) { g_err = "image and batch live on different devices"; return -2; }
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
+  const bool fu = b.fu_cap && img.indexed;
+  if (fu) {
+    k.fu_wl = b.fu_wl;
+    k.fu_cap = b.fu_cap;
+  }
   launch_eval(img, k, b.n, (hipStream_t)stream);
   HIPCHK(hipGetLastError(), "launch");
+  if (fu) {  // the large-stage variant over the worklist the first pass filled (count read on device)
+    KArgs f = make_args(img, b, b.fu_wl + 1, b.fu_cap, b.fu_res, b.fu_rf, b.fu_rp, b.fu_er, b.fu_capr, b.fu_cape);
+    f.n_dev = b.fu_wl;
+    launch_probe(f, b.fu_cap, (hipStream_t)stream, true);
+    HIPCHK(hipGetLastError(), "launch follow-up");
+  }
   return 0;
 }
 
@@ -2073,6 +2111,17 @@ static void bind_results(const DevBatch& b, Batch& host) {
   host.reasons_f = b.n ? at(b.reasons_f) : nullptr;
   host.reasons_p = b.n ? at(b.reasons_p) : nullptr;
   host.errs = b.n ? at(b.errs) : nullptr;
+  host.fu = Batch::FollowUp();
+  if (b.n && b.fu_cap) {
+    host.fu.wl = at(b.fu_wl);
+    host.fu.res = at(b.fu_res);
+    host.fu.rf = at(b.fu_rf);
+    host.fu.rp = at(b.fu_rp);
+    host.fu.er = at(b.fu_er);
+    host.fu.cap = b.fu_cap;
+    host.fu.capr = b.fu_capr;
+    host.fu.cape = b.fu_cape;
+  }
 }
 
 int dev_download(DevBatch& b, Batch& host, void* stream) {

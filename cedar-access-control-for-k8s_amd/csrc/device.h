@@ -32,6 +32,12 @@ struct DevBatch {
   uint8_t* bstr_bytes = nullptr;
   // results: one device block (res | reasons_f | reasons_p | errs), one copy back
   uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
+  // on-device follow-up of many-hit requests (small batches): the first pass appends the requests
+  // it flags RF_BIG to fu_wl = [count, request ids (fu_cap)], and the large-stage kernel evaluates
+  // them right behind it into fu_res / fu_rf / fu_rp / fu_er (fu_capr reasons, fu_cape errors per
+  // entry), all inside the result block, so no host round trip (device-side count, fu_cap == 0: off)
+  uint32_t *fu_wl = nullptr, *fu_res = nullptr, *fu_rf = nullptr, *fu_rp = nullptr, *fu_er = nullptr;
+  uint32_t fu_cap = 0, fu_capr = 0, fu_cape = 0;
   uint32_t n = 0, capr = 0, cape = 0, row_words = 0;
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)

@@ -172,6 +172,11 @@ struct Batch {
   // Re-run results: request i's reason / error list read in place from the re-run's pinned result
   // block, which the owning cg_batch keeps until it is destroyed (big stays empty until a re-run
   // fills one; ptr null = the first pass's lists).
+  // the on-device follow-up of many-hit requests (device.h DevBatch::fu_*), in the pinned block
+  struct FollowUp {
+    const uint32_t *wl = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
+    uint32_t cap = 0, capr = 0, cape = 0;
+  } fu;
   struct BigRef { const uint32_t *r = nullptr, *e = nullptr; uint32_t nr = 0, ne_words = 0; };
   std::vector<BigRef> big;
   void set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words);

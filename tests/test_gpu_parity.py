@@ -100,8 +100,12 @@ def test_random_atomic_policies_vs_oracle(ctx, seed):
     check_items(ctx, stores, items)
 
 
-def test_random_overflowing_result_lists(ctx):
-    """300 policies: many requests exceed the inline reason/error capacity -> re-run path."""
+@pytest.mark.parametrize("first_capr", [None, "8", "1"])
+def test_random_overflowing_result_lists(ctx, first_capr, monkeypatch):
+    """300 policies: many requests exceed the inline reason/error capacity -> re-run path (with
+    the batch's adaptive first-pass capacity, and pinned to 8 and 1 reasons per effect)."""
+    if first_capr:
+        monkeypatch.setenv("CEDARGPU_FIRST_CAPR", first_capr)
     g = Gen(77)
     stores = [cedargpu.MemoryStore("big.cedar", g.policies(300))]
     items = [g.item() for _ in range(200)]
@@ -217,11 +221,14 @@ def test_hot_reload_epochs(ctx):
 
 
 # ---------------------------------------------------------------- scope-index kernel paths
+@pytest.mark.parametrize("first_capr", [None, "8"])
 @pytest.mark.parametrize("n", [40, 150, 1100])
-def test_index_kernel_hit_overflow_reruns(ctx, n):
+def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, monkeypatch):
     """Many satisfied policies: beyond the inline reason capacity (probe-kernel re-run with exact
     capacities), beyond the 64 hits the probe kernel stages per request (large-stage variant) and,
     at 1100, beyond its 1024 (stream-kernel re-run)."""
+    if first_capr:
+        monkeypatch.setenv("CEDARGPU_FIRST_CAPR", first_capr)
     pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
                      for i in range(n))
     pols += '\nforbid (principal, action == k8s::Action::"create", resource) when { principal has nick };'
