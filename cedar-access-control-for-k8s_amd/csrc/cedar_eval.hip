@@ -70,9 +70,7 @@ struct KArgs {
   const uint32_t* __restrict__ bstream;
   const uint32_t* __restrict__ rows;     // columnar request rows (row_words each)
   unsigned long long* stats;             // probe-kernel work counters (STATS variant only)
-  uint32_t* fu_wl;                       // first pass: RF_BIG worklist [count, ids] (null: none)
   const uint32_t* n_dev;                 // follow-up pass: request count on the device (null: n_req)
-  uint32_t fu_cap;
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
 };
 
@@ -1538,10 +1536,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     const uint32_t why = (structural || L::HC >= 1024) ? RF_GENERAL : RF_BIG;
     a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | why) << 16);
     a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
-    if (why == RF_BIG && a.fu_wl) {  // hand it to the follow-up launch (first pass: gid == r)
-      const uint32_t k = atomicAdd(a.fu_wl, 1u);
-      if (k < a.fu_cap) a.fu_wl[1 + k] = gid;
-    }
+
   }
   const uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge
   // bitonic sort of (policy index << 8 | slot) over the wave's largest power of two >= nh
@@ -1885,6 +1880,17 @@ void dev_batch_free(DevBatch* d) {
 
 static size_t lds_bytes(const DevImage& img) { return (size_t)std::max<uint32_t>(img.n_hot, 1) * BLOCK * sizeof(uint2); }
 
+// Worklist of the on-device follow-up: every request the first pass flagged RF_BIG (more hits
+// than its stage holds), in any order ([0] = count; entries past `cap` are left to the host).
+__global__ void __launch_bounds__(256) cedar_fu_gather(const uint32_t* __restrict__ res, uint32_t n, uint32_t* wl, uint32_t cap) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t fl = res[2 * (size_t)i] >> 16;
+  if ((fl & (RF_OVERFLOW | RF_BIG | RF_GENERAL)) != (RF_OVERFLOW | RF_BIG)) return;
+  const uint32_t k = atomicAdd(wl, 1u);
+  if (k < cap) wl[1 + k] = i;
+}
+
 static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* req_idx, uint32_t n, uint32_t* res,
                        uint32_t* rf, uint32_t* rp, uint32_t* er, uint32_t capr, uint32_t cape) {
   KArgs k;
@@ -1899,9 +1905,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.stats = nullptr;
-  k.fu_wl = nullptr;
   k.n_dev = nullptr;
-  k.fu_cap = 0;
   return k;
 }
 
@@ -2013,13 +2017,12 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
   if (img.device != b.device) { g_err = "image and batch live on different devices"; return -2; }
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
   const bool fu = b.fu_cap && img.indexed;
-  if (fu) {
-    k.fu_wl = b.fu_wl;
-    k.fu_cap = b.fu_cap;
-  }
   launch_eval(img, k, b.n, (hipStream_t)stream);
   HIPCHK(hipGetLastError(), "launch");
-  if (fu) {  // the large-stage variant over the worklist the first pass filled (count read on device)
+  if (fu) {
+    // the requests the first pass flagged RF_BIG, gathered into the worklist, then the
+    // large-stage variant over it (its count read on the device)
+    hipLaunchKernelGGL(cedar_fu_gather, dim3((b.n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b.res, b.n, b.fu_wl, b.fu_cap);
     KArgs f = make_args(img, b, b.fu_wl + 1, b.fu_cap, b.fu_res, b.fu_rf, b.fu_rp, b.fu_er, b.fu_capr, b.fu_cape);
     f.n_dev = b.fu_wl;
     launch_probe(f, b.fu_cap, (hipStream_t)stream, true);

@@ -221,14 +221,18 @@ def test_hot_reload_epochs(ctx):
 
 
 # ---------------------------------------------------------------- scope-index kernel paths
+@pytest.mark.parametrize("followup", [None, "0"])
 @pytest.mark.parametrize("first_capr", [None, "8"])
-@pytest.mark.parametrize("n", [40, 150, 1100])
-def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, monkeypatch):
+@pytest.mark.parametrize("n", [40, 150, 400, 1100])
+def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, monkeypatch):
     """Many satisfied policies: beyond the inline reason capacity (probe-kernel re-run with exact
     capacities), beyond the 64 hits the probe kernel stages per request (large-stage variant) and,
-    at 1100, beyond its 1024 (stream-kernel re-run)."""
+    at 1100, beyond its 1024 (stream-kernel re-run). 400 overflows the on-device follow-up's 256
+    reasons per request (host re-run of the large stage)."""
     if first_capr:
         monkeypatch.setenv("CEDARGPU_FIRST_CAPR", first_capr)
+    if followup:  # many-hit requests on the host re-run path instead of the on-device follow-up
+        monkeypatch.setenv("CEDARGPU_FOLLOWUP", followup)
     pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
                      for i in range(n))
     pols += '\nforbid (principal, action == k8s::Action::"create", resource) when { principal has nick };'
