@@ -278,7 +278,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--policies", type=int, default=10_000)
-    ap.add_argument("--batch", type=int, default=262_144, help="requests per GPU per step (one launch)")
+    ap.add_argument("--batch", type=int, default=1_048_576, help="requests per GPU per step (one launch)")
     ap.add_argument("--variant", default="full", help="policy-shape study: full | scope-only | no-group | atomic-only")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-sample", type=int, default=2048)
