@@ -279,6 +279,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--policies", type=int, default=10_000)
     ap.add_argument("--batch", type=int, default=1_048_576, help="requests per GPU per step (one launch)")
+    ap.add_argument("--order", default="random", choices=["random", "user"],
+                    help="request order within the batch (locality study; random is the benchmark)")
     ap.add_argument("--variant", default="full", help="policy-shape study: full | scope-only | no-group | atomic-only")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-sample", type=int, default=2048)
@@ -305,6 +307,8 @@ def main():
     pop = synth.Population(seed=7)
     policies = synth.abac_policies(args.policies, seed=31, pop=pop, variant=args.variant)
     sars = synth.random_sars(args.batch, seed=1000 + rank, pop=pop)
+    if args.order == "user":  # locality study: the batch grouped by caller
+        sars.sort(key=lambda s: s["spec"]["user"])
 
     baseline = None
     threads = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
