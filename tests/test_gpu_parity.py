@@ -84,7 +84,9 @@ def test_tier_reference_vectors_gpu(ctx, case):
 
 # ---------------------------------------------------------------- randomized differential
 @pytest.mark.parametrize("seed", range(12))
-def test_random_policies_vs_oracle(ctx, seed):
+def test_random_policies_vs_oracle(ctx, seed, monkeypatch):
+    if seed % 2:  # odd seeds: the batch grouped by principal before upload (results mapped back)
+        monkeypatch.setenv("CEDARGPU_GROUP", "1")
     g = Gen(1000 + seed)
     stores = [cedargpu.MemoryStore(f"t{t}.cedar", g.policies(g.r.randint(0, 12))) for t in range(g.r.randint(1, 3))]
     items = [g.item() for _ in range(300)]
@@ -92,8 +94,10 @@ def test_random_policies_vs_oracle(ctx, seed):
 
 
 @pytest.mark.parametrize("seed", range(8))
-def test_random_atomic_policies_vs_oracle(ctx, seed):
+def test_random_atomic_policies_vs_oracle(ctx, seed, monkeypatch):
     """Policies lowered to predicate atoms (incl. label-selector record templates)."""
+    if seed % 2:  # odd seeds: the batch grouped by principal before upload (results mapped back)
+        monkeypatch.setenv("CEDARGPU_GROUP", "1")
     g = Gen(5000 + seed)
     stores = [cedargpu.MemoryStore(f"a{t}.cedar", g.atomic_policies(g.r.randint(1, 40))) for t in range(g.r.randint(1, 2))]
     items = [g.item() for _ in range(400)]
@@ -141,8 +145,12 @@ def test_converter_corpus_vs_oracle(ctx):
     check_items(ctx, stores, _sar_items(2000, 9))
 
 
-def test_authorizer_sar_path_matches_oracle(ctx):
-    """Full Authorize() over SAR JSON (C++ model + GPU) vs oracle authorize()."""
+@pytest.mark.parametrize("group", [None, "1"])
+def test_authorizer_sar_path_matches_oracle(ctx, group, monkeypatch):
+    """Full Authorize() over SAR JSON (C++ model + GPU) vs oracle authorize() (also with the batch
+    grouped by principal; the SAR fast paths keep their item slots)."""
+    if group:
+        monkeypatch.setenv("CEDARGPU_GROUP", group)
     stores = [cedargpu.MemoryStore("demo.cedar", "\n".join(v for k, v in sorted(CORPUS["demo"].items())))]
     authz = cedargpu.Authorizer(stores, ctx=ctx)
     sars = synth.random_sars(2000, seed=17, pop=synth.Population(seed=17, n_users=1000, n_groups=100))
@@ -155,8 +163,12 @@ def test_authorizer_sar_path_matches_oracle(ctx):
         assert (dec, reason) == want, s
 
 
-def test_admission_policies_vs_oracle(ctx):
-    """C4 at test scale: admission demo policies + allow-all tier, ConfigMap/Secret objects."""
+@pytest.mark.parametrize("group", [None, "1"])
+def test_admission_policies_vs_oracle(ctx, group, monkeypatch):
+    """C4 at test scale: admission demo policies + allow-all tier, ConfigMap/Secret objects
+    (also with the batch grouped by principal before upload)."""
+    if group:
+        monkeypatch.setenv("CEDARGPU_GROUP", group)
     stores = [cedargpu.MemoryStore("adm.cedar", "\n".join(v for k, v in sorted(CORPUS["demo"].items()) if k.startswith("admission"))),
               cedargpu.ALLOW_ALL_ADMISSION]
     items = []
@@ -221,10 +233,11 @@ def test_hot_reload_epochs(ctx):
 
 
 # ---------------------------------------------------------------- scope-index kernel paths
+@pytest.mark.parametrize("group", [None, "1"])
 @pytest.mark.parametrize("followup", [None, "0"])
 @pytest.mark.parametrize("first_capr", [None, "8"])
 @pytest.mark.parametrize("n", [40, 150, 400, 1100])
-def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, monkeypatch):
+def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, group, monkeypatch):
     """Many satisfied policies: beyond the inline reason capacity (probe-kernel re-run with exact
     capacities), beyond the 64 hits the probe kernel stages per request (large-stage variant) and,
     at 1100, beyond its 1024 (stream-kernel re-run). 400 overflows the on-device follow-up's 256
@@ -233,6 +246,8 @@ def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, monkeypa
         monkeypatch.setenv("CEDARGPU_FIRST_CAPR", first_capr)
     if followup:  # many-hit requests on the host re-run path instead of the on-device follow-up
         monkeypatch.setenv("CEDARGPU_FOLLOWUP", followup)
+    if group:  # the batch grouped by principal before upload
+        monkeypatch.setenv("CEDARGPU_GROUP", group)
     pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
                      for i in range(n))
     pols += '\nforbid (principal, action == k8s::Action::"create", resource) when { principal has nick };'
