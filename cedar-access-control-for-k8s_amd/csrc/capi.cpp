@@ -110,45 +110,47 @@ void parallel_for(size_t n, F&& f) {
 // collective loops converge and neighbouring waves share image lines in L2: C3 1M-request
 // launches went from 870M to 1.15B decisions/s (profiles/r01/group_ab). Rows and request bases
 // move to their new slots and items map to the slots, so every result accessor reads its own
-// request. Throughput batches (>= 65,536 requests) only: the sort costs ~0.2 µs of host time per
-// request, which a latency-bound batch would pay in full. CEDARGPU_GROUP=1 / 0 forces it.
+// request. Throughput batches (>= 65,536 requests) only: a radix sort plus the row permutation
+// costs ~50 ns of host time per request (~2 ms at 32,768), more than a smaller batch's kernel
+// wins back (C4 at 32,768: kernel 1.32 -> 0.81 ms, submit -> results 7.4 -> 8.0 ms).
+// CEDARGPU_GROUP=1 / 0 forces it.
 void group_requests(cg_batch* b) {
   Batch& h = b->host;
   const uint32_t n = h.n(), rw = h.row_words;
   bool on = n >= 65536u;
   if (const char* e = std::getenv("CEDARGPU_GROUP")) on = *e == '1';
-  if (!on || n < 2 || !rw || h.rows.size() != (size_t)n * rw) return;
-  struct Key {
-    uint64_t ar, grp, hot;
-    uint32_t i;
-    bool operator<(const Key& o) const {
-      if (ar != o.ar) return ar < o.ar;
-      if (grp != o.grp) return grp < o.grp;
-      if (hot != o.hot) return hot < o.hot;
-      return i < o.i;  // stable
-    }
-  };
+  if (!on || n < 2 || n >= (1u << 24) || !rw || h.rows.size() != (size_t)n * rw) return;
   auto mix = [](uint64_t k, uint32_t w) {
     k ^= w;
     k *= 0xff51afd7ed558ccdull;
     return k ^ (k >> 29);
   };
-  std::vector<Key> key(n);
+  // one 64-bit key per request: 12 bits of (action, resource type) | 20 bits of the principal's
+  // type and groups | 8 bits of its hot values | 24 bits of its position (ties keep batch order).
+  // Hash fields group equal values; unequal values sharing a field only cost locality.
+  std::vector<uint64_t> key(n), tmp(n);
   parallel_for(n, [&](size_t i) {
     const uint32_t* row = h.rows.data() + i * rw;
-    // groups: the principal's ancestor (type, id) pairs; a request-local string id can collide
-    // across requests, which only costs locality
-    uint64_t g = 0x9E3779B97F4A7C15ull ^ row[cgi::RW_P];
+    const uint64_t ar = mix(mix(0x51ED27Fu, row[cgi::RW_A + 1]), row[cgi::RW_R]);
+    // groups: the principal's ancestor (type, id) pairs
+    uint64_t g = mix(0x9E3779B97F4A7C15ull, row[cgi::RW_P]);
     const size_t anc = (size_t)row[cgi::RW_BLK] + row[cgi::RW_PANC];
     for (uint32_t j = 0; j < 2 * row[cgi::RW_PN] && anc + j < h.heap.size(); j++) g = mix(g, h.heap[anc + j]);
     uint64_t hv = 0x2545F4914F6CDD1Dull;
     for (uint32_t j = cgi::RW_HDR; j < rw; j++) hv = mix(hv, row[j]);
-    key[i] = Key{((uint64_t)row[cgi::RW_A + 1] << 32) | row[cgi::RW_R], g, hv, (uint32_t)i};
+    key[i] = ((ar >> 52) << 52) | ((g >> 44) << 32) | ((hv >> 56) << 24) | (uint64_t)i;
   });
-  std::sort(key.begin(), key.end());
+  // LSD radix sort on bits 24..63 (4 passes of 10 bits)
+  for (uint32_t sh = 24; sh < 64; sh += 10) {
+    uint32_t cnt[1025] = {0};
+    for (uint32_t i = 0; i < n; i++) cnt[((key[i] >> sh) & 1023u) + 1]++;
+    for (uint32_t d = 0; d < 1024; d++) cnt[d + 1] += cnt[d];
+    for (uint32_t i = 0; i < n; i++) tmp[cnt[(key[i] >> sh) & 1023u]++] = key[i];
+    key.swap(tmp);
+  }
   std::vector<uint32_t> rows((size_t)n * rw), base(n), slot(n);
   parallel_for(n, [&](size_t s) {
-    const uint32_t o = key[s].i;
+    const uint32_t o = (uint32_t)(key[s] & 0xFFFFFFu);
     std::memcpy(rows.data() + s * rw, h.rows.data() + (size_t)o * rw, (size_t)rw * 4);
     base[s] = h.req_base[o];
     slot[o] = (uint32_t)s;
