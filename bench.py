@@ -419,6 +419,9 @@ def main():
                                    "resource/labelSelector/like conditions) x synthetic SARs",
                        "policies": args.policies, "requests_per_gpu": args.batch, "tiers": 1,
                        "variant": args.variant,
+                       "request_order": (f"{args.order}; the batching layer groups batches of >= 65,536 requests by "
+                                         "(action, resource type), principal groups, hot attributes at submit "
+                                         "(host radix sort, outside the timed launches)"),
                        "parallelism": f"request-sharded x{world}, image replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
