@@ -125,9 +125,15 @@ void group_requests(cg_batch* b) {
     k *= 0xff51afd7ed558ccdull;
     return k ^ (k >> 29);
   };
-  // one 64-bit key per request: 12 bits of (action, resource type) | 20 bits of the principal's
-  // type and groups | 8 bits of its hot values | 24 bits of its position (ties keep batch order).
+  // one 64-bit key per request: 12 bits of (action, resource type) | the principal's type and
+  // groups in the bits left over | 8 bits of its hot values | its position in ceil(log2 n) bits
+  // (ties keep batch order).
   // Hash fields group equal values; unequal values sharing a field only cost locality.
+  // position bits: just enough for n; the groups field takes the rest between the fixed fields
+  uint32_t ib = 1;
+  while ((1ull << ib) < n) ib++;
+  const uint64_t imask = (1ull << ib) - 1, hmask = 0xFFull << ib;
+  const uint64_t gmask = ((1ull << 52) - 1) & ~((1ull << (ib + 8)) - 1);
   std::vector<uint64_t> key(n), tmp(n);
   parallel_for(n, [&](size_t i) {
     const uint32_t* row = h.rows.data() + i * rw;
@@ -138,19 +144,19 @@ void group_requests(cg_batch* b) {
     for (uint32_t j = 0; j < 2 * row[cgi::RW_PN] && anc + j < h.heap.size(); j++) g = mix(g, h.heap[anc + j]);
     uint64_t hv = 0x2545F4914F6CDD1Dull;
     for (uint32_t j = cgi::RW_HDR; j < rw; j++) hv = mix(hv, row[j]);
-    key[i] = ((ar >> 52) << 52) | ((g >> 44) << 32) | ((hv >> 56) << 24) | (uint64_t)i;
+    key[i] = ((ar >> 52) << 52) | (((g >> 40) << (64 - 12 - 24)) & gmask) | (((hv >> 56) << ib) & hmask) | (uint64_t)i;
   });
-  // LSD radix sort on bits 24..63 (4 passes of 10 bits)
-  for (uint32_t sh = 24; sh < 64; sh += 10) {
-    uint32_t cnt[1025] = {0};
-    for (uint32_t i = 0; i < n; i++) cnt[((key[i] >> sh) & 1023u) + 1]++;
-    for (uint32_t d = 0; d < 1024; d++) cnt[d + 1] += cnt[d];
-    for (uint32_t i = 0; i < n; i++) tmp[cnt[(key[i] >> sh) & 1023u]++] = key[i];
+  // LSD radix sort on the key bits above the position (11-bit digits)
+  for (uint32_t sh = ib; sh < 64; sh += 11) {
+    std::vector<uint32_t> cnt(2049, 0);
+    for (uint32_t i = 0; i < n; i++) cnt[((key[i] >> sh) & 2047u) + 1]++;
+    for (uint32_t d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
+    for (uint32_t i = 0; i < n; i++) tmp[cnt[(key[i] >> sh) & 2047u]++] = key[i];
     key.swap(tmp);
   }
   std::vector<uint32_t> rows((size_t)n * rw), base(n), slot(n);
   parallel_for(n, [&](size_t s) {
-    const uint32_t o = (uint32_t)(key[s] & 0xFFFFFFu);
+    const uint32_t o = (uint32_t)(key[s] & imask);
     std::memcpy(rows.data() + s * rw, h.rows.data() + (size_t)o * rw, (size_t)rw * 4);
     base[s] = h.req_base[o];
     slot[o] = (uint32_t)s;
