@@ -779,6 +779,11 @@ int cg_batch_submit(cg_batch* b) {
   // CEDARGPU_FIRST_CAPR pins it (tests drive the 9..64-reason re-run path with small batches).
   b->host.capr = std::max<uint32_t>(8u, std::min<uint32_t>(64u, (uint32_t)((4u << 20) / (8ull * b->host.n()))));
   if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
+  // Follow-up sized for the many-hit share the last batch on this image saw (+1/8 and 32 spare),
+  // so images whose requests mostly collect > 64 reasons (C4) finish without a host round trip.
+  b->host.fu_hint = 0;
+  if (b->ctx->big_img.load() == b->img.get())
+    b->host.fu_hint = (uint32_t)std::min<uint64_t>(b->host.n(), (uint64_t)b->ctx->big_ppm.load() * b->host.n() / 1000000u * 9 / 8 + 32);
   GUARD(b->err, { group_requests(b); })
   tr.mark("group");
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
@@ -807,6 +812,8 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   // same results block): their lists are final, unless the follow-up itself overflowed.
   if (b->host.fu.cap) {
     const auto& fu = b->host.fu;
+    b->ctx->big_ppm.store((uint32_t)std::min<uint64_t>(1000000u, (uint64_t)fu.wl[0] * 1000000u / std::max<uint32_t>(1u, b->host.n())));
+    b->ctx->big_img.store(b->img.get());
     const uint32_t cnt = std::min(fu.wl[0], fu.cap);
     for (uint32_t k = 0; k < cnt; k++) {
       const uint32_t i = fu.wl[1 + k];

@@ -1,5 +1,6 @@
 // Internal state behind the C-ABI handles (include/cedargpu.h), shared by capi.cpp and queue.cpp.
 #pragma once
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -43,6 +44,10 @@ struct cg_ctx {
   std::map<uint64_t, std::shared_ptr<LoadedImage>> images;
   std::shared_ptr<LoadedImage> active;
   std::string err;
+  // many-hit share (RF_BIG requests per million) of the last batch that ran the on-device
+  // follow-up, and the image it ran on: the next batch on that image sizes its follow-up by it
+  std::atomic<uint32_t> big_ppm{0};
+  std::atomic<const LoadedImage*> big_img{nullptr};
 };
 
 struct cg_batch {

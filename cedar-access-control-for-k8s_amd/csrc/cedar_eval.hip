@@ -1787,7 +1787,8 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   const size_t n = std::max<uint32_t>(b.n(), 1);
   const size_t o_res = 0, o_rf = al(n * 2 * 4), o_rp = o_rf + al(n * d.capr * 4), o_er = o_rp + al(n * d.capr * 4);
   // on-device follow-up for batches up to 65,536 requests: n / 32 entries (4..64), 256 reasons
-  d.fu_cap = b.n() <= 65536u ? std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u)) : 0u;
+  // (or the caller's hint, from the many-hit share of the previous batch on this image)
+  d.fu_cap = b.n() <= 65536u ? std::max(std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u)), std::min(b.fu_hint, b.n())) : 0u;
   if (const char* e = std::getenv("CEDARGPU_FOLLOWUP")) if (*e == '0') d.fu_cap = 0;
   d.fu_capr = 256;
   d.fu_cape = 16;

@@ -261,6 +261,32 @@ def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, group, m
         check_items(ctx, stores, items)
 
 
+def test_followup_sized_by_previous_batch(ctx):
+    """Most requests collect > 64 reasons: the first batch on an image follows up at most 64 of
+    them on the device and re-runs the rest from the host; the next batch on that image sizes its
+    follow-up by the share the first one saw, so it re-runs none. Both agree with the oracle."""
+    pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 2}", action, resource);' for i in range(200))
+    stores = [cedargpu.MemoryStore("hits.cedar", pols)]
+    img = cedargpu.build_image(stores, epoch=951)
+    ctx.load(img, 951)
+    g = Gen(93)
+    items = [g.item() for _ in range(2048)]
+    runs = []
+    for _ in range(2):
+        b = ctx.batch()
+        for ents, req in items:
+            b.add(ents, req)
+        b.submit()
+        b.wait()
+        runs.append((b.reruns(), [b.decision(i) for i in range(len(b))], [b.diagnostic(i) for i in range(len(b))]))
+        b.close()
+    assert runs[0][0] > 64, "test needs more many-hit requests than the default follow-up holds"
+    assert runs[1][0] == 0
+    assert runs[0][1:] == runs[1][1:]
+    got = check_items(ctx, stores, items[:300])
+    assert [d for d, _ in got] == [d for d, _ in runs[1][1][:300]]
+
+
 def test_index_kernel_action_hierarchy_duplicates(ctx):
     """A policy filed under several actions of `action in [..]` is reached twice when the request
     action's ancestors include more than one of them; it must be reported once."""
