@@ -1882,12 +1882,13 @@ void dev_batch_free(DevBatch* d) {
 static size_t lds_bytes(const DevImage& img) { return (size_t)std::max<uint32_t>(img.n_hot, 1) * BLOCK * sizeof(uint2); }
 
 // Worklist of the on-device follow-up: every request the first pass flagged RF_BIG (more hits
-// than its stage holds), in any order ([0] = count; entries past `cap` are left to the host).
+// than its stage holds) or whose reason / error lists outgrew the first pass's capacities, in any
+// order ([0] = count; entries past `cap` are left to the host). RF_GENERAL requests go to the host.
 __global__ void __launch_bounds__(256) cedar_fu_gather(const uint32_t* __restrict__ res, uint32_t n, uint32_t* wl, uint32_t cap) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint32_t fl = res[2 * (size_t)i] >> 16;
-  if ((fl & (RF_OVERFLOW | RF_BIG | RF_GENERAL)) != (RF_OVERFLOW | RF_BIG)) return;
+  if ((fl & (RF_OVERFLOW | RF_GENERAL)) != RF_OVERFLOW) return;
   const uint32_t k = atomicAdd(wl, 1u);
   if (k < cap) wl[1 + k] = i;
 }
