@@ -781,9 +781,14 @@ int cg_batch_submit(cg_batch* b) {
   if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   // Follow-up sized for the many-hit share the last batch on this image saw (+1/8 and 32 spare),
   // so images whose requests mostly collect > 64 reasons (C4) finish without a host round trip.
-  b->host.fu_hint = 0;
-  if (b->ctx->big_img.load() == b->img.get())
+  // Its per-entry reason capacity follows the longest list the last follow-up produced (+1/8,
+  // rounded up to 32; 64..256), which trims the result block copied back.
+  b->host.fu_hint = b->host.fu_capr_hint = 0;
+  if (b->ctx->big_img.load() == b->img.get()) {
     b->host.fu_hint = (uint32_t)std::min<uint64_t>(b->host.n(), (uint64_t)b->ctx->big_ppm.load() * b->host.n() / 1000000u * 9 / 8 + 32);
+    const uint32_t mr = b->ctx->big_maxr.load();
+    if (mr) b->host.fu_capr_hint = (mr + mr / 8 + 8 + 31) & ~31u;
+  }
   GUARD(b->err, { group_requests(b); })
   tr.mark("group");
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
@@ -815,6 +820,9 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     b->ctx->big_ppm.store((uint32_t)std::min<uint64_t>(1000000u, (uint64_t)fu.wl[0] * 1000000u / std::max<uint32_t>(1u, b->host.n())));
     b->ctx->big_img.store(b->img.get());
     const uint32_t cnt = std::min(fu.wl[0], fu.cap);
+    uint32_t maxr = 0;
+    for (uint32_t k = 0; k < cnt; k++) maxr = std::max(maxr, fu.res[2 * k + 1] & 0xFFFF);
+    b->ctx->big_maxr.store(maxr);
     for (uint32_t k = 0; k < cnt; k++) {
       const uint32_t i = fu.wl[1 + k];
       if (i >= b->host.n()) { b->err = "follow-up worklist out of range"; return CG_E_DEVICE; }

@@ -46,7 +46,7 @@ struct cg_ctx {
   std::string err;
   // many-hit share (RF_BIG requests per million) of the last batch that ran the on-device
   // follow-up, and the image it ran on: the next batch on that image sizes its follow-up by it
-  std::atomic<uint32_t> big_ppm{0};
+  std::atomic<uint32_t> big_ppm{0}, big_maxr{0};  // share, and the most reasons one entry needed
   std::atomic<const LoadedImage*> big_img{nullptr};
 };
 

@@ -1790,7 +1790,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // (or the caller's hint, from the many-hit share of the previous batch on this image)
   d.fu_cap = b.n() <= 65536u ? std::max(std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u)), std::min(b.fu_hint, b.n())) : 0u;
   if (const char* e = std::getenv("CEDARGPU_FOLLOWUP")) if (*e == '0') d.fu_cap = 0;
-  d.fu_capr = 256;
+  d.fu_capr = b.fu_capr_hint ? std::min<uint32_t>(256u, std::max<uint32_t>(64u, b.fu_capr_hint)) : 256u;
   d.fu_cape = 16;
   const size_t o_fwl = o_er + al(n * d.cape * ERR_WORDS * 4), o_fres = o_fwl + al((1 + (size_t)d.fu_cap) * 4),
                o_frf = o_fres + al((size_t)d.fu_cap * 2 * 4), o_frp = o_frf + al((size_t)d.fu_cap * d.fu_capr * 4),

@@ -164,6 +164,7 @@ struct Batch {
   // results
   uint32_t capr = 8, cape = 4;
   uint32_t fu_hint = 0;  // on-device follow-up entries wanted (0: the default n / 32, at most 64)
+  uint32_t fu_capr_hint = 0;  // reasons per follow-up entry (0: 256)
   // first-pass results, read in place from the batch's pinned staging block (device.h DevBatch;
   // valid while the batch lives): res[2i], [2i+1] per request, capr reasons of each effect, cape
   // error records. res is written back by overflow re-runs.
