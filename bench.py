@@ -55,22 +55,64 @@ def oracle_items(sars):
     return items, idx
 
 
-def cpu_baseline(policies_text, items, seconds, threads):
+def host_cpus():
+    """The host cores this process may run on: the affinity mask, bounded by the cgroup CPU
+    quota (cgroup v2 cpu.max or v1 cfs_quota/period) when one is set; plus the CPU model."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    usable = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    # the GPU pool declares each box's host-core share in OMP_NUM_THREADS (16 per GPU); nproc there
+    # counts the whole machine, so the share bounds the worker count too
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        usable = min(usable, int(share))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, {"affinity_cpus": affinity, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(),
+                    "omp_num_threads": share, "cpu_model": model}
+
+
+def cpu_baseline(policies_text, items, seconds, threads, cpu_info, entities=None):
     """C++ oracle (`port`: oracle/cedar_ref.cpp, the restatement of cedar-go's per-request linear
-    scan with a tree-walking evaluator) on `threads` host threads over pre-built EntityMaps.
-    Runs before any GPU initialisation."""
+    scan with a tree-walking evaluator) on `threads` host threads (one per usable core, SURVEY
+    §8(d) GOMAXPROCS = nproc) over pre-built EntityMaps. Runs before any GPU initialisation."""
     from cedar_ref import RefPolicySet, items_json
     ref = RefPolicySet()
+    if entities:
+        ref.set_entities(json.dumps(entities))
     ref.add_tier()
     ref.add_document("c3.cedar", policies_text)
     ref.load_items(items_json(items))
     n, wall = ref.bench(threads, seconds)
     ref.close()
-    return {"value": n / wall, "unit": "decisions/s", "cores": threads, "kind": "port",
+    return {"value": n / wall, "unit": "decisions/s", "cores": threads, "kind": "port", **cpu_info,
             "sample": f"{n} decisions in {wall:.1f} s: {len(items)} pre-built (EntityMap, Request) items from the "
                       f"benchmark's SubjectAccessReviews x {policies_text.count(';')} policies through "
-                      f"oracle/cedar_ref.cpp (C++ restatement of cedar-go IsAuthorized, linear scan), "
-                      f"{threads} threads on {os.cpu_count()} visible CPUs"}
+                      f"oracle/cedar_ref.cpp (C++ restatement of cedar-go IsAuthorized, linear scan; not cedar-go), "
+                      f"{threads} threads = the usable host cores (affinity {cpu_info['affinity_cpus']}, cgroup "
+                      f"quota {cpu_info['cgroup_quota_cpus']}, declared share OMP_NUM_THREADS="
+                      f"{cpu_info['omp_num_threads']}) on {cpu_info['cpu_model'] or 'unknown CPU'}"}
 
 
 def parity_sample(policies_text, items, idx, gpu_batch, threads):
@@ -115,7 +157,6 @@ def secondary_configs(ctx, n_req, threads, sample=512):
         enc_s = time.perf_counter() - t0
         b.submit()
         b.wait()
-        ms = b.time(5) / 5
         n_req_b = len(b)
         ref = RefPolicySet.from_stores(stores)
         ref.load_items(items_json(items))
@@ -123,11 +164,12 @@ def secondary_configs(ctx, n_req, threads, sample=512):
         ref.close()
         bad = sum(1 for w, i in zip(want, idx) if result(b, i) != want_of(w))
         b.close()
-        # the same payload again on the warm buffer pool: submit -> results, with the H2D copy, the
-        # first pass, every overflow re-run (requests with more reasons than the first pass holds)
-        # and the D2H copies; best of 3
+        # the same payload again on the warm buffer pool (steady state: each batch's result
+        # capacities sized by the one before on the image): submit -> results, with the H2D copy,
+        # the first pass, the on-device follow-ups, any host re-run and the D2H copy; best of 3.
+        # The device step of the last one is timed (HIP events, 5 repeats).
         full_ms = None
-        for _ in range(3):
+        for k in range(3):
             b2 = ctx.batch()
             add(b2, payload)
             t0 = time.perf_counter()
@@ -135,11 +177,13 @@ def secondary_configs(ctx, n_req, threads, sample=512):
             b2.wait()
             t = (time.perf_counter() - t0) * 1e3
             full_ms = t if full_ms is None else min(full_ms, t)
-            n_big = b2.reruns()
+            n_big, fus = b2.reruns(), b2.followups()
+            if k == 2:
+                ms = b2.time(5) / 5  # complete step: first pass + gather + on-device follow-ups
             b2.close()
         out[name] = {"what": what, "requests": n_req_b, "kernel_ms": ms, "kernel_decisions_per_s": n_req_b / (ms * 1e-3),
                      "submit_to_results_ms": full_ms, "decisions_per_s": n_req_b / (full_ms * 1e-3),
-                     "rerun_requests": n_big,
+                     "rerun_requests": n_big, "device_followup_requests": fus,
                      "host_encode_per_s": n_req_b / enc_s,
                      "parity_sample": {"requests": len(items), "mismatches": bad, "oracle": "oracle/cedar_ref.cpp"}}
 
@@ -311,10 +355,11 @@ def main():
         sars.sort(key=lambda s: s["spec"]["user"])
 
     baseline = None
-    threads = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+    usable, cpu_info = host_cpus()
+    threads = args.cpu_workers or usable
     items, idx = oracle_items(sars[:args.parity_sample]) if rank == 0 else ([], [])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        baseline = cpu_baseline(policies, items, args.cpu_seconds, threads)
+        baseline = cpu_baseline(policies, items, args.cpu_seconds, threads, cpu_info)
 
     # torch is plumbing only: the cross-rank barrier / max-reduce of timings runs over gloo on CPU
     # tensors. torch's bundled HIP runtime is never initialised in this process (it would clash
@@ -330,16 +375,24 @@ def main():
         dist.init_process_group(backend="gloo")
     device = local
 
-    t_build = time.perf_counter()
     image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies)], epoch=1)
     ctx = cedargpu.Context(device)
     ctx.load(image, 1)
+    # steady state: the batch before the measured one on this image sizes its result capacities
+    # (the context's CapHint: first-pass reasons, on-device follow-up worklists)
+    sizing = ctx.batch()
+    sizing.add_sar_json(synth.sars_json(sars[:65536]))
+    sizing.submit()
+    sizing.wait()
+    sizing.close()
+    t_build = time.perf_counter()
     b = ctx.batch()
     b.add_sar_json(synth.sars_json(sars))
     t_enc = time.perf_counter()
     b.submit()
-    b.wait()  # correctness pass: results downloaded, overflow re-runs done
+    b.wait()  # correctness pass: results downloaded, follow-ups folded, host re-runs (if any) done
     t_first = time.perf_counter()
+    followups, host_reruns = b.followups(), b.reruns()
     n_reasons = [b.reasons(i)[0].__len__() for i in range(len(b))]
     alg_bytes = algorithmic_bytes(sars, n_reasons, has_like=True)
 
@@ -419,6 +472,10 @@ def main():
                                    "resource/labelSelector/like conditions) x synthetic SARs",
                        "policies": args.policies, "requests_per_gpu": args.batch, "tiers": 1,
                        "variant": args.variant,
+                       "step": "first pass + gather + on-device follow-up launches (every request decided, "
+                               "all reasons and errors listed, on the device)",
+                       "device_followup_requests": followups,
+                       "rerun_requests": host_reruns,
                        "request_order": (f"{args.order}; the batching layer groups batches of >= 65,536 requests by "
                                          "(action, resource type), principal groups, hot attributes at submit "
                                          "(host radix sort, outside the timed launches)"),

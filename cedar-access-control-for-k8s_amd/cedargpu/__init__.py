@@ -8,6 +8,8 @@ Mirrors the reference's store interface for the hot path:
 The product path has no CPU fallback: importing this package fails loudly when libcedargpu.so
 is missing, and evaluation raises `DeviceError` when no GPU is present.
 """
-from ._lib import CedarGPUError, CompileError, DeviceError, lib, lib_path  # noqa: F401
-from .store import (AVPStore, Batch, Context, CRDStore, DirectoryStore, MemoryStore, PolicyStore,  # noqa: F401
-                    StaticStore, TieredPolicyStores, Authorizer, AdmissionHandler, Compiler, admission_to_cedar_json, Queue, ALLOW_ALL_ADMISSION, build_image, image_stats, atomic_policies, device_count)
+from ._lib import CedarGPUError, CompileError, DeadlineError, DeviceError, lib, lib_path  # noqa: F401
+from .store import (ALLOW_ALL_ADMISSION, FAULT_DEVICE_ERROR, FAULT_NONE, FAULT_STALL, AdmissionHandler,  # noqa: F401
+                    Authorizer, AVPStore, Batch, Compiler, Context, CRDStore, DirectoryStore, MemoryStore, PolicyStore,
+                    Queue, StaticStore, TieredPolicyStores, admission_to_cedar_json, atomic_policies, build_image,
+                    device_count, image_stats)

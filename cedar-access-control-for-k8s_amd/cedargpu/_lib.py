@@ -30,11 +30,17 @@ class DeviceError(CedarGPUError):
     pass
 
 
+class DeadlineError(CedarGPUError):
+    """CG_E_TIMEOUT: the call's deadline passed (callers fail safe as on a webhook timeout)."""
+
+
 def _err(code, msg):
     if code in (CG_E_PARSE, CG_E_COMPILE):
         return CompileError(code, msg)
     if code == CG_E_DEVICE:
         return DeviceError(code, msg)
+    if code == CG_E_TIMEOUT:
+        return DeadlineError(code, msg)
     return CedarGPUError(code, msg)
 
 
@@ -63,6 +69,7 @@ _SIGS = {
     "cg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(P)]),
     "cg_ctx_destroy": (None, [P]),
     "cg_last_error": (cstr, [P]),
+    "cg_ctx_inject_fault": (ctypes.c_int, [P, ctypes.c_int, u64]),
     "cg_image_load": (ctypes.c_int, [P, P, sz, u64]),
     "cg_image_activate": (ctypes.c_int, [P, u64]),
     "cg_image_active": (ctypes.c_int, [P, ctypes.POINTER(u64)]),
@@ -83,6 +90,7 @@ _SIGS = {
     "cg_batch_reasons": (ctypes.c_int, [P, u32, ctypes.POINTER(u32), u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]),
     "cg_batch_time": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_float)]),
     "cg_batch_reruns": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
+    "cg_batch_followups": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
     "cg_batch_bytes": (ctypes.c_int, [P, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     "cg_batch_add_sar_json": (ctypes.c_int, [P, cstr, sz]),
     "cg_sar_to_cedar_json": (ctypes.c_int, [cstr, sz, P, sz, ctypes.POINTER(sz)]),
@@ -97,8 +105,9 @@ _SIGS = {
     "cg_queue_create": (ctypes.c_int, [P, u32, u32, ctypes.POINTER(P)]),
     "cg_queue_destroy": (None, [P]),
     "cg_queue_last_error": (cstr, []),
-    "cg_queue_authorize_sar": (ctypes.c_int, [P, cstr, sz, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
-    "cg_queue_is_authorized_json": (ctypes.c_int, [P, cstr, sz, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
+    "cg_queue_authorize_sar": (ctypes.c_int, [P, cstr, sz, i64, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
+    "cg_queue_is_authorized_json": (ctypes.c_int, [P, cstr, sz, i64, ctypes.POINTER(ctypes.c_int), P, sz,
+                                                   ctypes.POINTER(sz)]),
     "cg_queue_stats": (ctypes.c_int, [P] + [ctypes.POINTER(u64)] * 5),
     "cg_queue_loadgen": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), u32, u32, u64,
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u64),

@@ -16,7 +16,14 @@ import json
 import threading
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
-from ._lib import CG_E_RANGE, CompileError, DeviceError, _err, lib
+from ._lib import CG_E_RANGE, CompileError, DeadlineError, DeviceError, _err, lib
+
+FAULT_NONE, FAULT_DEVICE_ERROR, FAULT_STALL = 0, 1, 2
+
+
+def _timeout_ns(timeout: Optional[float]) -> int:
+    return -1 if timeout is None else max(0, int(timeout * 1e9))
+
 
 _P = ctypes.c_void_p
 
@@ -250,6 +257,13 @@ class Context:
     def batch(self) -> "Batch":
         return Batch(self)
 
+    def inject_fault(self, kind: int, arg: int = 0):
+        """Gameday fault injection (cg_ctx_inject_fault): FAULT_DEVICE_ERROR fails the next `arg`
+        submits, FAULT_STALL delays every batch by `arg` microseconds on the device."""
+        rc = lib.cg_ctx_inject_fault(self._h, kind, arg)
+        if rc:
+            raise _err(rc, "inject_fault failed")
+
 
 class Batch:
     def __init__(self, ctx: Context):
@@ -328,8 +342,9 @@ class Batch:
         if rc:
             raise _err(rc, "batch submit failed")
 
-    def wait(self):
-        rc = lib.cg_batch_wait(self._h, -1)
+    def wait(self, timeout: Optional[float] = None):
+        """cg_batch_wait; raises DeadlineError past `timeout` seconds (the batch stays in flight)."""
+        rc = lib.cg_batch_wait(self._h, _timeout_ns(timeout))
         if rc:
             raise _err(rc, "batch wait failed")
 
@@ -370,6 +385,14 @@ class Batch:
             raise _err(rc, "reruns failed")
         return n.value
 
+    def followups(self) -> dict:
+        """Requests finished by each on-device follow-up worklist (cg_batch_followups)."""
+        c = (ctypes.c_uint32 * 3)()
+        rc = lib.cg_batch_followups(self._h, c)
+        if rc:
+            raise _err(rc, "followups failed")
+        return {"big": c[0], "long_lists": c[1], "structural": c[2]}
+
     def time(self, iters: int) -> float:
         ms = ctypes.c_float()
         rc = lib.cg_batch_time(self._h, iters, ctypes.byref(ms))
@@ -407,26 +430,38 @@ class Queue:
         except Exception:
             pass
 
-    def _call(self, fn, payload: str) -> Tuple[int, str]:
+    def _call(self, fn, payload: str, timeout: Optional[float]) -> Tuple[int, str]:
         b = _b(payload)
         out = ctypes.c_int()
         need = ctypes.c_size_t(0)
         buf = ctypes.create_string_buffer(1024)
-        rc = fn(self._h, b, len(b), ctypes.byref(out), buf, 1024, ctypes.byref(need))
+        rc = fn(self._h, b, len(b), _timeout_ns(timeout), ctypes.byref(out), buf, 1024, ctypes.byref(need))
         if rc == CG_E_RANGE and need.value > 1024:
             buf = ctypes.create_string_buffer(need.value)
-            rc = fn(self._h, b, len(b), ctypes.byref(out), buf, need.value, ctypes.byref(need))
+            rc = fn(self._h, b, len(b), _timeout_ns(timeout), ctypes.byref(out), buf, need.value, ctypes.byref(need))
         if rc:
             raise _err(rc, lib.cg_queue_last_error().decode())
         return out.value, buf.value.decode("utf-8")
 
-    def authorize(self, sar: Union[dict, str]) -> Tuple[int, str]:
-        """(authorizer.Decision: 0 Deny / 1 Allow / 2 NoOpinion, reason)."""
-        return self._call(lib.cg_queue_authorize_sar, sar if isinstance(sar, str) else json.dumps(sar))
+    def authorize(self, sar: Union[dict, str], timeout: Optional[float] = None) -> Tuple[int, str]:
+        """(authorizer.Decision: 0 Deny / 1 Allow / 2 NoOpinion, reason). Raises DeadlineError past
+        `timeout` seconds and DeviceError on a device failure (see `authorize_failsafe`)."""
+        return self._call(lib.cg_queue_authorize_sar, sar if isinstance(sar, str) else json.dumps(sar), timeout)
 
-    def is_authorized(self, entities: list, request: dict) -> Tuple[bool, str]:
+    def authorize_failsafe(self, sar: Union[dict, str], timeout: Optional[float] = None) -> Tuple[int, str]:
+        """authorize() with the webhook's fail-safe: a deadline or device failure answers NoOpinion
+        with no reason, as the apiserver's failurePolicy NoOpinion would on a webhook timeout
+        (mount/authorization-config.yaml:11,16) and as Authorize does without an opinion
+        (authorizer.go:80-84)."""
+        try:
+            return self.authorize(sar, timeout)
+        except (DeadlineError, DeviceError):
+            return Authorizer.NO_OPINION, ""
+
+    def is_authorized(self, entities: list, request: dict, timeout: Optional[float] = None) -> Tuple[bool, str]:
         """(allow, json.Marshal(cedar.Diagnostic))."""
-        allow, diag = self._call(lib.cg_queue_is_authorized_json, json.dumps({"entities": entities, "request": request}))
+        allow, diag = self._call(lib.cg_queue_is_authorized_json, json.dumps({"entities": entities, "request": request}),
+                                 timeout)
         return bool(allow), diag
 
     def stats(self) -> dict:
@@ -502,22 +537,30 @@ class Authorizer:
 
     DENY, ALLOW, NO_OPINION = 0, 1, 2
 
-    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None):
+    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None,
+                 timeout: Optional[float] = None):
         self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx)
         self._loaded = False
+        self.timeout = timeout  # per batch, seconds (the apiserver allows 3 s: authorization-config.yaml:11)
 
     def authorize_batch(self, sars: Sequence[dict]) -> List[Tuple[int, str]]:
+        """Fail-safe: a device failure or a missed deadline answers NoOpinion for every request
+        that needed the device (fast-path answers stand), as the apiserver's failurePolicy would."""
         if not self._loaded:  # authorizer.go:58-66 (checked after the fast paths there; see below)
             if not self.tiers.ready():
                 return [_fast_or_noopinion(s) for s in sars]
             self._loaded = True
         b = self.tiers.ctx.batch()
-        b.add_sar_json(json.dumps(list(sars)))
-        b.submit()
-        b.wait()
-        out = [b.authz(i) for i in range(len(b))]
-        b.close()
-        return out
+        try:
+            b.add_sar_json(json.dumps(list(sars)))
+            try:
+                b.submit()
+                b.wait(self.timeout)
+            except (DeviceError, DeadlineError):
+                return [_fast_or_noopinion(s) for s in sars]
+            return [b.authz(i) for i in range(len(b))]
+        finally:
+            b.close()
 
     def authorize(self, sar: dict) -> Tuple[int, str]:
         return self.authorize_batch([sar])[0]
@@ -528,19 +571,27 @@ class AdmissionHandler:
     `ALLOW_ALL_ADMISSION` (main.go:111-116). `handle_batch` takes AdmissionReview dicts and returns
     [(allowed, HTTP status code, message)]."""
 
-    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None):
+    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None,
+                 timeout: Optional[float] = None):
         self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx)
+        self.timeout = timeout  # per batch, seconds (the webhook allows 30 s: admission-webhook.yaml:26)
 
     def handle_batch(self, reviews: Sequence[dict]) -> List[Tuple[bool, int, str]]:
+        """Fail-safe: a device failure or a missed deadline allows every review (allowOnError,
+        cmd/cedar-webhook/main.go:116; failurePolicy Ignore, manifests/admission-webhook.yaml:11)."""
         if not self.tiers.ready():  # handler.go:49-57: allow until every store has loaded
             return [(True, 200, "") for _ in reviews]
         b = self.tiers.ctx.batch()
-        b.add_admission_json(json.dumps(list(reviews)))
-        b.submit()
-        b.wait()
-        out = [b.admit(i) for i in range(len(b))]
-        b.close()
-        return out
+        try:
+            b.add_admission_json(json.dumps(list(reviews)))
+            try:
+                b.submit()
+                b.wait(self.timeout)
+            except (DeviceError, DeadlineError):
+                return [(True, 200, "") for _ in reviews]
+            return [b.admit(i) for i in range(len(b))]
+        finally:
+            b.close()
 
     def handle(self, review: dict) -> Tuple[bool, int, str]:
         return self.handle_batch([review])[0]

@@ -447,6 +447,16 @@ void cg_ctx_destroy(cg_ctx* ctx) {
 
 const char* cg_last_error(cg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg) {
+  if (!ctx) return CG_E_ARG;
+  switch (kind) {
+    case CG_FAULT_NONE: ctx->fault_errors = 0; ctx->fault_stall_us = 0; return CG_OK;
+    case CG_FAULT_DEVICE_ERROR: ctx->fault_errors = arg; return CG_OK;
+    case CG_FAULT_STALL: ctx->fault_stall_us = std::min<uint64_t>(arg, 2000000u); return CG_OK;
+    default: return CG_E_ARG;
+  }
+}
+
 int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch) {
   if (!ctx || !image) return CG_E_ARG;
   std::shared_ptr<Image> img;
@@ -461,6 +471,7 @@ int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch) {
   li->host = img;
   if (dev_image_upload(ctx->device, *img, &li->dev)) { ctx->err = dev_last_error(); return CG_E_DEVICE; }
   std::lock_guard<std::mutex> g(ctx->mu);
+  li->serial = ctx->next_serial++;
   ctx->images[epoch] = li;
   return CG_OK;
 }
@@ -777,22 +788,39 @@ int cg_batch_submit(cg_batch* b) {
   // stay within 4 MB (small, latency-bound batches then need no re-run for 9..64 reasons); large
   // throughput batches keep 8 per effect.
   // CEDARGPU_FIRST_CAPR pins it (tests drive the 9..64-reason re-run path with small batches).
-  b->host.capr = std::max<uint32_t>(8u, std::min<uint32_t>(64u, (uint32_t)((4u << 20) / (8ull * b->host.n()))));
-  if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
-  // Follow-up sized for the many-hit share the last batch on this image saw (+1/8 and 32 spare),
-  // so images whose requests mostly collect > 64 reasons (C4) finish without a host round trip.
-  // Its per-entry reason capacity follows the longest list the last follow-up produced (+1/8,
-  // rounded up to 32; 64..256), which trims the result block copied back.
-  b->host.fu_hint = b->host.fu_capr_hint = 0;
-  if (b->ctx->big_img.load() == b->img.get()) {
-    b->host.fu_hint = (uint32_t)std::min<uint64_t>(b->host.n(), (uint64_t)b->ctx->big_ppm.load() * b->host.n() / 1000000u * 9 / 8 + 32);
-    const uint32_t mr = b->ctx->big_maxr.load();
-    if (mr) b->host.fu_capr_hint = (mr + mr / 8 + 8 + 31) & ~31u;
+  const uint32_t n = b->host.n();
+  b->host.capr = std::max<uint32_t>(8u, std::min<uint32_t>(64u, (uint32_t)((4u << 20) / (8ull * n))));
+  // Sizing from the last batch on this image (CapHint): each follow-up worklist gets the share
+  // that batch needed (+1/4 and 64 spare), so images whose requests mostly collect many reasons
+  // (C4) finish on the device; FU_BIG's per-entry reason capacity follows the longest list it
+  // produced (+1/8, rounded up to 32; 64..256); the first pass holds the longest list it counted
+  // (up to 64) while its two reason arrays stay within 32 MB.
+  CapHint h;
+  {
+    std::lock_guard<std::mutex> g(b->ctx->mu);
+    h = b->ctx->hint;
   }
+  for (uint32_t k = 0; k < FU_KINDS; k++) b->host.fu_want[k] = 0;
+  b->host.fu_capr_hint = 0;
+  if (h.serial && h.serial == b->img->serial) {
+    for (uint32_t k = 0; k < FU_KINDS; k++)
+      if (h.ppm[k]) b->host.fu_want[k] = (uint32_t)std::min<uint64_t>(n, (uint64_t)h.ppm[k] * n / 1000000u * 5 / 4 + 64);
+    if (h.big_maxr) b->host.fu_capr_hint = (h.big_maxr + h.big_maxr / 8 + 8 + 31) & ~31u;
+    const uint32_t want_capr = std::min<uint32_t>(64u, (h.first_maxr + 7) & ~7u);
+    if (want_capr > b->host.capr && (uint64_t)n * want_capr * 8 <= (32ull << 20)) b->host.capr = want_capr;
+  }
+  if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   GUARD(b->err, { group_requests(b); })
   tr.mark("group");
+  for (uint64_t f = b->ctx->fault_errors.load(); f;)
+    if (b->ctx->fault_errors.compare_exchange_weak(f, f - 1)) {
+      b->err = "injected device error (cg_ctx_inject_fault CG_FAULT_DEVICE_ERROR)";
+      return CG_E_DEVICE;
+    }
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   tr.mark("upload");
+  if (const uint64_t us = b->ctx->fault_stall_us.load())
+    if (dev_stall(b->ctx->device, b->ctx->stream, us)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   if (dev_eval(b->img->dev, b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   tr.mark("launch");
   if (dev_download_async(b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
@@ -805,41 +833,61 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   if (!b) return CG_E_ARG;
   if (!b->submitted) { b->err = "batch not submitted"; return CG_E_STATE; }
   if (b->done) return CG_OK;
-  (void)timeout_ns;  // stream sync is bounded by the kernel; the webhook deadline is enforced by the caller
+  if (b->failed) return b->failed;
+  const int64_t deadline = timeout_ns < 0 ? -1 : dev_now_ns() + timeout_ns;
   LatTrace tr("wait");
-  if (dev_download_finish(b->dev, b->host)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  if (const int drc = dev_download_finish(b->dev, b->host, deadline)) {
+    b->err = dev_last_error();
+    return drc == DEV_TIMEOUT ? CG_E_TIMEOUT : CG_E_DEVICE;  // a timeout leaves the batch in flight
+  }
   tr.mark("sync_copy");
   // Overflowed result lists: re-run just those requests. Capacity overflows of the probe kernel
   // re-run there with the exact capacities; requests it could not decide (RF_GENERAL) and any
   // stream-kernel overflow re-run on the stream kernel, which reports exact counts, so a second
   // pass with those capacities completes it.
-  // Many-hit requests the on-device follow-up completed (large stage right behind the first pass,
-  // same results block): their lists are final, unless the follow-up itself overflowed.
-  if (b->host.fu.cap) {
-    const auto& fu = b->host.fu;
-    b->ctx->big_ppm.store((uint32_t)std::min<uint64_t>(1000000u, (uint64_t)fu.wl[0] * 1000000u / std::max<uint32_t>(1u, b->host.n())));
-    b->ctx->big_img.store(b->img.get());
-    const uint32_t cnt = std::min(fu.wl[0], fu.cap);
-    uint32_t maxr = 0;
-    for (uint32_t k = 0; k < cnt; k++) maxr = std::max(maxr, fu.res[2 * k + 1] & 0xFFFF);
-    b->ctx->big_maxr.store(maxr);
-    for (uint32_t k = 0; k < cnt; k++) {
-      const uint32_t i = fu.wl[1 + k];
-      if (i >= b->host.n()) { b->err = "follow-up worklist out of range"; return CG_E_DEVICE; }
-      const uint32_t fl = fu.res[2 * k] >> 16;
-      if (!(fl & cgi::RF_VALID) || (fl & (cgi::RF_OVERFLOW | cgi::RF_GENERAL | cgi::RF_BIG))) continue;
-      const uint32_t nr = fu.res[2 * k + 1] & 0xFFFF, ne = fu.res[2 * k + 1] >> 16;
-      b->host.res[2 * (size_t)i] = fu.res[2 * k];
-      b->host.res[2 * (size_t)i + 1] = fu.res[2 * k + 1];
-      GUARD(b->err, {
-        b->host.set_big(i, ((fl & cgi::RF_FORBID) ? fu.rf : fu.rp) + (size_t)k * fu.capr, nr,
-                        fu.er + (size_t)k * fu.cape * cgi::ERR_WORDS, ne * cgi::ERR_WORDS);
-      })
+  // Requests the on-device follow-up finished (worklists right behind the first pass, same
+  // results block): their lists are final, unless the follow-up itself overflowed (those keep the
+  // first pass's RF_OVERFLOW and go to the host re-run below). Their counts size the next batch.
+  CapHint h;
+  h.serial = b->img->serial;
+  const uint32_t n = b->host.n();
+  for (uint32_t i = 0; i < n; i++) {  // the first pass's exact list lengths (<= 64 hits)
+    const uint32_t fl = b->host.res[2 * (size_t)i] >> 16;
+    if ((fl & cgi::RF_VALID) && !(fl & (cgi::RF_GENERAL | cgi::RF_BIG)))
+      h.first_maxr = std::max(h.first_maxr, b->host.res[2 * (size_t)i + 1] & 0xFFFF);
+  }
+  if (b->host.fu_cnt) {
+    for (uint32_t q = 0; q < FU_KINDS; q++) {
+      const auto& fu = b->host.fu[q];
+      h.ppm[q] = (uint32_t)std::min<uint64_t>(1000000u, (uint64_t)b->host.fu_cnt[q] * 1000000u / std::max<uint32_t>(1u, n));
+      const uint32_t cnt = std::min(b->host.fu_cnt[q], fu.cap);
+      for (uint32_t k = 0; k < cnt; k++) {
+        const uint32_t i = fu.ids[k];
+        if (i >= n) { b->err = "follow-up worklist out of range"; return CG_E_DEVICE; }
+        const uint32_t fl = fu.res[2 * k] >> 16;
+        if (!(fl & cgi::RF_VALID) || (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) continue;
+        const uint32_t nr = fu.res[2 * k + 1] & 0xFFFF, ne = fu.res[2 * k + 1] >> 16;
+        if (q == FU_BIG) h.big_maxr = std::max(h.big_maxr, nr);  // exact, overflowed or not
+        if (fl & cgi::RF_OVERFLOW) continue;
+        b->host.res[2 * (size_t)i] = fu.res[2 * k];
+        b->host.res[2 * (size_t)i + 1] = fu.res[2 * k + 1];
+        b->n_fu[q]++;
+        GUARD(b->err, {
+          b->host.set_big(i, ((fl & cgi::RF_FORBID) ? fu.rf : fu.rp) + (size_t)k * fu.capr, nr,
+                          fu.er + (size_t)k * fu.cape * cgi::ERR_WORDS, ne * cgi::ERR_WORDS);
+        })
+      }
     }
+  }
+  {
+    std::lock_guard<std::mutex> g(b->ctx->mu);
+    // a batch without FU_BIG entries keeps the image's last known FU_BIG list length
+    if (!h.big_maxr && b->ctx->hint.serial == h.serial) h.big_maxr = b->ctx->hint.big_maxr;
+    b->ctx->hint = h;
   }
   std::vector<uint32_t> idx_probe, idx_big, idx_gen;
   uint32_t capr_p = 0, cape_p = 0, capr_b = 0, cape_b = 0, capr_g = 0, cape_g = 0;
-  for (uint32_t i = 0; i < b->host.n(); i++) {
+  for (uint32_t i = 0; i < n; i++) {
     uint32_t fl = b->host.res[2 * (size_t)i] >> 16;
     if (!(fl & cgi::RF_VALID)) { b->err = "request left unevaluated"; return CG_E_DEVICE; }
     if (!(fl & cgi::RF_OVERFLOW)) continue;
@@ -875,6 +923,16 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     }
   };
   auto clampr = [](uint32_t c, uint32_t lo) { return std::max(std::min(c, 4096u), lo); };
+  // a re-run that missed the deadline is still in flight: its blocks stay with the batch, whose
+  // destruction drains the stream first; the batch is failed
+  auto timed_out = [&](std::initializer_list<DevSubset*> jobs) {
+    b->err = "deadline exceeded during a host re-run";
+    for (DevSubset* j : jobs)
+      if (j->dblk) b->held.push_back(*j);
+    b->dev.pending = true;
+    b->failed = CG_E_TIMEOUT;
+    return CG_E_TIMEOUT;
+  };
   // re-runs a subset (mode: 1 probe kernel, 2 its large-stage variant, 0 stream kernel) until its
   // lists fit, one round trip per pass
   auto rerun = [&](std::vector<uint32_t>& idx, uint32_t capr, uint32_t cape, int mode, std::vector<uint32_t>& next) -> int {
@@ -883,8 +941,10 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       cape = clampr(cape, 4u);
       DevSubset job;
       SubsetView v;
-      if (dev_subset_begin(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->stream, &job) ||
-          dev_subset_end(&job, &v)) {
+      int src = dev_subset_begin(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->stream, &job);
+      if (!src) src = dev_subset_end(&job, &v, deadline);
+      if (src == DEV_TIMEOUT) return timed_out({&job});
+      if (src) {
         b->err = dev_last_error();
         (void)dev_stream_sync(b->ctx->stream);
         dev_subset_release(&job);
@@ -923,7 +983,8 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       if (!brc && !u.idx->empty())
         brc = dev_subset_begin(b->img->dev, b->dev, u.idx->data(), (uint32_t)u.idx->size(), u.capr, u.cape, u.mode, b->ctx->stream, &u.job);
     for (auto& u : subs)
-      if (!brc) brc = dev_subset_end(&u.job, &u.v);
+      if (!brc) brc = dev_subset_end(&u.job, &u.v, deadline);
+    if (brc == DEV_TIMEOUT) return timed_out({&subs[0].job, &subs[1].job, &subs[2].job});
     std::vector<uint32_t> again[3], next_big, next_gen;
     uint32_t capr2[3] = {0, 0, 0}, cape2[3] = {0, 0, 0};
     std::vector<uint32_t>* nexts[3] = {&next_big, &next_gen, &next_gen};
@@ -972,6 +1033,13 @@ int cg_batch_reruns(cg_batch* b, uint32_t* n) {
   if (!b || !n) return CG_E_ARG;
   if (!b->done) return CG_E_STATE;
   *n = b->n_rerun;
+  return CG_OK;
+}
+
+int cg_batch_followups(cg_batch* b, uint32_t* counts) {
+  if (!b || !counts) return CG_E_ARG;
+  if (!b->done) return CG_E_STATE;
+  for (uint32_t k = 0; k < FU_KINDS; k++) counts[k] = b->n_fu[k];
   return CG_OK;
 }
 

@@ -15,7 +15,18 @@ namespace cg {
 struct LoadedImage {
   std::shared_ptr<Image> host;
   DevImage dev;
+  uint64_t serial = 0;  // per-context load number (never reused, unlike the address or the epoch)
   ~LoadedImage() { dev_image_free(&dev); }
+};
+
+// Result-capacity sizing hint: what the last completed batch on an image needed. The next batch
+// on that image sizes its first-pass reason capacity and its follow-up worklists by it. A hint
+// only: results never depend on it (a short capacity falls back to the host re-run).
+struct CapHint {
+  uint64_t serial = 0;                   // LoadedImage::serial it describes (0: none)
+  uint32_t ppm[FU_KINDS] = {0, 0, 0};   // share of the batch each follow-up worklist took (per million)
+  uint32_t big_maxr = 0;                 // longest reason list a FU_BIG entry produced
+  uint32_t first_maxr = 0;               // longest reason list (<= 64) the first pass counted exactly
 };
 
 #define GUARD(errstr, body)                                       \
@@ -44,10 +55,10 @@ struct cg_ctx {
   std::map<uint64_t, std::shared_ptr<LoadedImage>> images;
   std::shared_ptr<LoadedImage> active;
   std::string err;
-  // many-hit share (RF_BIG requests per million) of the last batch that ran the on-device
-  // follow-up, and the image it ran on: the next batch on that image sizes its follow-up by it
-  std::atomic<uint32_t> big_ppm{0}, big_maxr{0};  // share, and the most reasons one entry needed
-  std::atomic<const LoadedImage*> big_img{nullptr};
+  uint64_t next_serial = 1;  // under mu
+  cg::CapHint hint;          // under mu
+  // cg_ctx_inject_fault: submits left to fail, and the device stall before each batch (us)
+  std::atomic<uint64_t> fault_errors{0}, fault_stall_us{0};
 };
 
 struct cg_batch {
@@ -56,7 +67,9 @@ struct cg_batch {
   cg::Batch host;
   cg::DevBatch dev;
   bool submitted = false, done = false;
+  int failed = 0;        // a host re-run missed its deadline: every later wait returns this
   uint32_t n_rerun = 0;  // requests re-run by cg_batch_wait
+  uint32_t n_fu[cg::FU_KINDS] = {0, 0, 0};  // requests finished by each on-device follow-up worklist
   std::string err;
   // items: caller-visible entries; dev >= 0 is the device request index, else a fast-path result
   struct Item { int32_t dev; int32_t fast; };
@@ -64,8 +77,8 @@ struct cg_batch {
   std::map<uint32_t, std::string> fast_reason;  // authz fast paths: the reason; admission: error text
   std::vector<cg::DevSubset> held;  // re-run result blocks the host lists point into (Batch::big)
   ~cg_batch() {
+    dev_batch_free(&dev);  // drains the batch's stream first when work on it may still run
     for (auto& j : held) dev_subset_release(&j);
-    dev_batch_free(&dev);
   }
   int32_t dev_of(uint32_t i) const { return i < items.size() ? items[i].dev : -1; }
 };

@@ -961,7 +961,8 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   __shared__ uint32_t rsn_lds[2 * CAPR_L * BLOCK];
   extern __shared__ uint2 hot_lds[];                                          // [n_hot][BLOCK]
   const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
-  const bool valid = gid < a.n_req;
+  const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;  // follow-up: count on the device
+  const bool valid = gid < n_req;
   const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0;
 
   uint32_t lane_scratch[LANE_WORDS];
@@ -1786,16 +1787,36 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   for (int k = 0; k < 5; k++) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
   const size_t n = std::max<uint32_t>(b.n(), 1);
   const size_t o_res = 0, o_rf = al(n * 2 * 4), o_rp = o_rf + al(n * d.capr * 4), o_er = o_rp + al(n * d.capr * 4);
-  // on-device follow-up for batches up to 65,536 requests: n / 32 entries (4..64), 256 reasons
-  // (or the caller's hint, from the many-hit share of the previous batch on this image)
-  d.fu_cap = b.n() <= 65536u ? std::max(std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u)), std::min(b.fu_hint, b.n())) : 0u;
-  if (const char* e = std::getenv("CEDARGPU_FOLLOWUP")) if (*e == '0') d.fu_cap = 0;
-  d.fu_capr = b.fu_capr_hint ? std::min<uint32_t>(256u, std::max<uint32_t>(64u, b.fu_capr_hint)) : 256u;
-  d.fu_cape = 16;
-  const size_t o_fwl = o_er + al(n * d.cape * ERR_WORDS * 4), o_fres = o_fwl + al((1 + (size_t)d.fu_cap) * 4),
-               o_frf = o_fres + al((size_t)d.fu_cap * 2 * 4), o_frp = o_frf + al((size_t)d.fu_cap * d.fu_capr * 4),
-               o_fer = o_frp + al((size_t)d.fu_cap * d.fu_capr * 4);
-  d.out_bytes = d.fu_cap ? o_fer + al((size_t)d.fu_cap * d.fu_cape * ERR_WORDS * 4) : o_fwl;
+  // On-device follow-up worklists. Entries: n / 32 (4..64) by default, or what the previous batch
+  // on this image needed (the caller's hint), within a byte budget per worklist; FU_BIG holds 256
+  // reasons per entry unless the hint says fewer suffice (64..256).
+  const bool fu_on = !(std::getenv("CEDARGPU_FOLLOWUP") && *std::getenv("CEDARGPU_FOLLOWUP") == '0');
+  const uint32_t fu_default = std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u));
+  const uint32_t capr_k[FU_KINDS] = {b.fu_capr_hint ? std::min<uint32_t>(256u, std::max<uint32_t>(64u, b.fu_capr_hint)) : 256u,
+                                     64u, 64u};
+  const size_t budget_k[FU_KINDS] = {std::min<size_t>(128u << 20, std::max<size_t>(16u << 20, (size_t)b.n() * 2048)),
+                                     std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024)),
+                                     std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024))};
+  size_t o_fu = o_er + al(n * d.cape * ERR_WORDS * 4);
+  const size_t o_cnt = o_fu;
+  o_fu += al(FU_KINDS * 4);
+  size_t o_k[FU_KINDS][5];
+  for (uint32_t k = 0; k < FU_KINDS; k++) {
+    auto& f = d.fu[k];
+    const bool probe_kind = k != FU_GEN;
+    f.capr = capr_k[k];
+    f.cape = 16;
+    const size_t entry = 4 * (1 + 2 + 2 * (size_t)f.capr + (size_t)f.cape * ERR_WORDS);
+    const uint32_t want = std::min<uint32_t>(b.n(), std::max(fu_default, b.fu_want[k]));
+    f.cap = (fu_on && b.n() && (!probe_kind || b.img->indexed)) ? (uint32_t)std::min<size_t>(want, budget_k[k] / entry) : 0u;
+    o_k[k][0] = o_fu;                                        // ids
+    o_k[k][1] = o_k[k][0] + al((size_t)f.cap * 4);           // res
+    o_k[k][2] = o_k[k][1] + al((size_t)f.cap * 2 * 4);       // reasons_f
+    o_k[k][3] = o_k[k][2] + al((size_t)f.cap * f.capr * 4);  // reasons_p
+    o_k[k][4] = o_k[k][3] + al((size_t)f.cap * f.capr * 4);  // errors
+    o_fu = o_k[k][4] + al((size_t)f.cap * f.cape * ERR_WORDS * 4);
+  }
+  d.out_bytes = o_fu;
   int rc;
   if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) return rc;
   if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) { pool_put(pool, false, d.in_blk, d.in_cls); return rc; }
@@ -1838,12 +1859,14 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.reasons_f = (uint32_t*)(o + o_rf);
   d.reasons_p = (uint32_t*)(o + o_rp);
   d.errs = (uint32_t*)(o + o_er);
-  if (d.fu_cap) {
-    d.fu_wl = (uint32_t*)(o + o_fwl);
-    d.fu_res = (uint32_t*)(o + o_fres);
-    d.fu_rf = (uint32_t*)(o + o_frf);
-    d.fu_rp = (uint32_t*)(o + o_frp);
-    d.fu_er = (uint32_t*)(o + o_fer);
+  d.fu_cnt = (uint32_t*)(o + o_cnt);
+  for (uint32_t k = 0; k < FU_KINDS; k++) {
+    auto& f = d.fu[k];
+    f.ids = (uint32_t*)(o + o_k[k][0]);
+    f.res = (uint32_t*)(o + o_k[k][1]);
+    f.rf = (uint32_t*)(o + o_k[k][2]);
+    f.rp = (uint32_t*)(o + o_k[k][3]);
+    f.er = (uint32_t*)(o + o_k[k][4]);
   }
   d.bytes = in_bytes + d.out_bytes;
   d.stream = stream;
@@ -1851,7 +1874,6 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
   HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
   HIPCHK(hipMemsetAsync(d.res, 0, n * 2 * 4, s), "memset res");
-  if (d.fu_cap) HIPCHK(hipMemsetAsync(d.fu_wl, 0, 4, s), "memset worklist");
   return 0;
 }
 
@@ -1881,16 +1903,55 @@ void dev_batch_free(DevBatch* d) {
 
 static size_t lds_bytes(const DevImage& img) { return (size_t)std::max<uint32_t>(img.n_hot, 1) * BLOCK * sizeof(uint2); }
 
-// Worklist of the on-device follow-up: every request the first pass flagged RF_BIG (more hits
-// than its stage holds) or whose reason / error lists outgrew the first pass's capacities, in any
-// order ([0] = count; entries past `cap` are left to the host). RF_GENERAL requests go to the host.
-__global__ void __launch_bounds__(256) cedar_fu_gather(const uint32_t* __restrict__ res, uint32_t n, uint32_t* wl, uint32_t cap) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t fl = res[2 * (size_t)i] >> 16;
-  if ((fl & (RF_OVERFLOW | RF_GENERAL)) != RF_OVERFLOW) return;
-  const uint32_t k = atomicAdd(wl, 1u);
-  if (k < cap) wl[1 + k] = i;
+// Worklists of the on-device follow-up (device.h FuKind): every request the first pass left
+// unfinished (RF_OVERFLOW), by what finishes it, in any order. cnt[k] counts them all; entries
+// past cap[k] are left to the host re-run.
+struct FuLists {
+  uint32_t* ids[FU_KINDS];
+  uint32_t cap[FU_KINDS];
+};
+// A block covers GATHER_ITEMS * 256 requests (coalesced strides of 256) in two passes over their
+// result words: count per worklist, block-wide exclusive scan in LDS, ONE atomicAdd per worklist
+// per block for its base, then write the ids. (One atomic per unfinished request serialised on
+// three L2 addresses: 153 us for the 14.7k of a 1M-request C3 batch.)
+constexpr uint32_t GATHER_ITEMS = 16;
+__device__ __forceinline__ uint32_t fu_kind(uint32_t fl, uint32_t indexed) {
+  if (!(fl & RF_OVERFLOW)) return FU_KINDS;
+  return ((fl & RF_GENERAL) || !indexed) ? FU_GEN : (fl & RF_BIG) ? FU_BIG : FU_OVF;
+}
+__global__ void __launch_bounds__(256) cedar_fu_gather(const uint32_t* __restrict__ res, uint32_t n, uint32_t indexed,
+                                                       uint32_t* __restrict__ cnt, FuLists wl) {
+  __shared__ uint32_t scan[FU_KINDS][256];
+  __shared__ uint32_t base[FU_KINDS];
+  const uint32_t t = threadIdx.x;
+  const size_t b0 = (size_t)blockIdx.x * GATHER_ITEMS * 256;
+  uint32_t c[FU_KINDS] = {0, 0, 0};
+  for (uint32_t k = 0; k < GATHER_ITEMS; k++) {
+    const size_t i = b0 + (size_t)k * 256 + t;
+    const uint32_t q = i < n ? fu_kind(res[2 * i] >> 16, indexed) : FU_KINDS;
+    if (q < FU_KINDS) c[q]++;
+  }
+  for (uint32_t q = 0; q < FU_KINDS; q++) scan[q][t] = c[q];
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan, three lists at once
+    uint32_t v[FU_KINDS];
+    for (uint32_t q = 0; q < FU_KINDS; q++) v[q] = t >= o ? scan[q][t - o] : 0u;
+    __syncthreads();
+    for (uint32_t q = 0; q < FU_KINDS; q++) scan[q][t] += v[q];
+    __syncthreads();
+  }
+  if (t < FU_KINDS) base[t] = scan[t][255] ? atomicAdd(cnt + t, scan[t][255]) : 0u;
+  __syncthreads();
+  uint32_t pos[FU_KINDS];
+  for (uint32_t q = 0; q < FU_KINDS; q++) pos[q] = base[q] + scan[q][t] - c[q];
+  for (uint32_t k = 0; k < GATHER_ITEMS; k++) {
+    const size_t i = b0 + (size_t)k * 256 + t;
+    const uint32_t q = i < n ? fu_kind(res[2 * i] >> 16, indexed) : FU_KINDS;
+    if (q < FU_KINDS) {
+      if (pos[q] < wl.cap[q]) wl.ids[q][pos[q]] = (uint32_t)i;
+      pos[q]++;
+    }
+  }
 }
 
 static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* req_idx, uint32_t n, uint32_t* res,
@@ -2013,24 +2074,42 @@ static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStre
                        dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
 }
 
+static void launch_stream(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK),
+                     dim3(BLOCK), lds_bytes(img), s, k);
+}
+
+// One complete evaluation step of a batch, stream-ordered with no host round trip: the first
+// pass over every request, then the gather of the requests it left unfinished and the three
+// follow-up launches over them (their counts read on the device). dev_eval enqueues it once;
+// dev_time_eval times it.
+static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
+  KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
+  launch_eval(img, k, b.n, s);
+  HIPCHK(hipGetLastError(), "launch");
+  if (!b.fu_cnt) return 0;
+  HIPCHK(hipMemsetAsync(b.fu_cnt, 0, FU_KINDS * 4, s), "memset worklists");
+  FuLists wl;
+  for (uint32_t q = 0; q < FU_KINDS; q++) { wl.ids[q] = b.fu[q].ids; wl.cap[q] = b.fu[q].cap; }
+  hipLaunchKernelGGL(cedar_fu_gather, dim3((b.n + GATHER_ITEMS * 256 - 1) / (GATHER_ITEMS * 256)), dim3(256), 0, s, b.res,
+                     b.n, img.indexed, b.fu_cnt, wl);
+  for (uint32_t q = 0; q < FU_KINDS; q++) {
+    const auto& f = b.fu[q];
+    if (!f.cap) continue;
+    KArgs fk = make_args(img, b, f.ids, f.cap, f.res, f.rf, f.rp, f.er, f.capr, f.cape);
+    fk.n_dev = b.fu_cnt + q;
+    if (q == FU_GEN) launch_stream(img, fk, f.cap, s);
+    else launch_probe(fk, f.cap, s, q == FU_BIG);
+  }
+  HIPCHK(hipGetLastError(), "launch follow-up");
+  return 0;
+}
+
 int dev_eval(const DevImage& img, DevBatch& b, void* stream) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   if (b.n == 0) return 0;
   if (img.device != b.device) { g_err = "image and batch live on different devices"; return -2; }
-  KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
-  const bool fu = b.fu_cap && img.indexed;
-  launch_eval(img, k, b.n, (hipStream_t)stream);
-  HIPCHK(hipGetLastError(), "launch");
-  if (fu) {
-    // the requests the first pass flagged RF_BIG, gathered into the worklist, then the
-    // large-stage variant over it (its count read on the device)
-    hipLaunchKernelGGL(cedar_fu_gather, dim3((b.n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b.res, b.n, b.fu_wl, b.fu_cap);
-    KArgs f = make_args(img, b, b.fu_wl + 1, b.fu_cap, b.fu_res, b.fu_rf, b.fu_rp, b.fu_er, b.fu_capr, b.fu_cape);
-    f.n_dev = b.fu_wl;
-    launch_probe(f, b.fu_cap, (hipStream_t)stream, true);
-    HIPCHK(hipGetLastError(), "launch follow-up");
-  }
-  return 0;
+  return enqueue_step(img, b, (hipStream_t)stream);
 }
 
 // Re-evaluates a subset of requests (overflowed result lists) with larger capacities; results are
@@ -2066,6 +2145,9 @@ int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx
   std::memcpy(h8, idx, (size_t)n * 4);
   *job = j;  // blocks owned by the job from here on (returned by dev_subset_release)
   hipError_t e;
+  hipEvent_t ev;
+  if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+  job->done = (void*)ev;
   if ((e = hipMemcpyAsync(d8, h8, (size_t)n * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return fail(e, "H2D");
   KArgs k = make_args(img, b, (uint32_t*)d8, n, (uint32_t*)(d8 + j.o_res), (uint32_t*)(d8 + j.o_rf),
                       (uint32_t*)(d8 + j.o_rp), (uint32_t*)(d8 + j.o_er), capr, cape);
@@ -2075,16 +2157,43 @@ int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx
     hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "launch");
   if ((e = hipMemcpyAsync(h8 + j.o_res, d8 + j.o_res, j.total - j.o_res, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e, "D2H");
+  if ((e = hipEventRecord(ev, s)) != hipSuccess) return fail(e, "event record");
   return 0;
 }
 
-int dev_subset_end(DevSubset* job, SubsetView* v) {
+int64_t dev_now_ns() {
+  return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Waits for `ev` until deadline_ns (< 0: none): spins with yields for the first ~50 us (results
+// of a latency-bound batch arrive within that), then sleeps 10 us between queries.
+static int wait_event(hipEvent_t ev, int64_t deadline_ns, const char* what) {
+  if (deadline_ns < 0) {
+    HIPCHK(hipEventSynchronize(ev), what);
+    return 0;
+  }
+  const int64_t t0 = dev_now_ns();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return fail(q, what);
+    const int64_t now = dev_now_ns();
+    if (now >= deadline_ns) {
+      g_err = std::string(what) + ": deadline exceeded";
+      return DEV_TIMEOUT;
+    }
+    if (now - t0 < 50000) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(10));
+  }
+}
+
+int dev_subset_end(DevSubset* job, SubsetView* v, int64_t deadline_ns) {
   *v = SubsetView();
   if (!job->dblk) return 0;
-  // on success or failure nothing of ours is in flight once the stream drained
-  hipError_t e = hipStreamSynchronize((hipStream_t)job->stream);
-  if (e != hipSuccess) {
-    const int rc = fail(e, "sync");
+  const int rc = wait_event((hipEvent_t)job->done, deadline_ns, "re-run");
+  if (rc == DEV_TIMEOUT) return rc;  // still in flight: the caller keeps the job until the stream drains
+  if (rc) {
+    (void)hipStreamSynchronize((hipStream_t)job->stream);  // nothing of ours in flight before release
     dev_subset_release(job);
     return rc;
   }
@@ -2097,6 +2206,7 @@ int dev_subset_end(DevSubset* job, SubsetView* v) {
 }
 
 void dev_subset_release(DevSubset* job) {
+  if (job->done) (void)hipEventDestroy((hipEvent_t)job->done);
   if (job->pool) {
     pool_put(job->pool, false, job->dblk, job->dcls);
     pool_put(job->pool, true, job->hblk, job->hcls);
@@ -2116,16 +2226,19 @@ static void bind_results(const DevBatch& b, Batch& host) {
   host.reasons_f = b.n ? at(b.reasons_f) : nullptr;
   host.reasons_p = b.n ? at(b.reasons_p) : nullptr;
   host.errs = b.n ? at(b.errs) : nullptr;
-  host.fu = Batch::FollowUp();
-  if (b.n && b.fu_cap) {
-    host.fu.wl = at(b.fu_wl);
-    host.fu.res = at(b.fu_res);
-    host.fu.rf = at(b.fu_rf);
-    host.fu.rp = at(b.fu_rp);
-    host.fu.er = at(b.fu_er);
-    host.fu.cap = b.fu_cap;
-    host.fu.capr = b.fu_capr;
-    host.fu.cape = b.fu_cape;
+  host.fu_cnt = (b.n && b.fu_cnt) ? at(b.fu_cnt) : nullptr;
+  for (uint32_t k = 0; k < FU_KINDS; k++) {
+    host.fu[k] = Batch::FollowUp();
+    const auto& f = b.fu[k];
+    if (!b.n || !f.cap) continue;
+    host.fu[k].ids = at(f.ids);
+    host.fu[k].res = at(f.res);
+    host.fu[k].rf = at(f.rf);
+    host.fu[k].rp = at(f.rp);
+    host.fu[k].er = at(f.er);
+    host.fu[k].cap = f.cap;
+    host.fu[k].capr = f.capr;
+    host.fu[k].cape = f.cape;
   }
 }
 
@@ -2152,11 +2265,31 @@ int dev_download_async(DevBatch& b, void* stream) {
   return 0;
 }
 
-int dev_download_finish(DevBatch& b, Batch& host) {
+int dev_download_finish(DevBatch& b, Batch& host, int64_t deadline_ns) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
-  if (b.done) HIPCHK(hipEventSynchronize((hipEvent_t)b.done), "event sync");
+  if (b.done) {
+    const int rc = wait_event((hipEvent_t)b.done, deadline_ns, "batch");
+    if (rc) return rc;  // DEV_TIMEOUT: still in flight (pending), wait again or destroy
+  }
   b.pending = false;
   bind_results(b, host);
+  return 0;
+}
+
+// A one-thread kernel that waits on the device wall clock (wall_clock64, constant rate `khz`).
+__global__ void __launch_bounds__(64) cedar_stall_kernel(uint64_t ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+int dev_stall(int device, void* stream, uint64_t us) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  int khz = 0;
+  HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
+  const uint64_t ticks = std::min<uint64_t>(us, 2000000u) * (uint64_t)std::max(khz, 1) / 1000u;
+  hipLaunchKernelGGL(cedar_stall_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ticks);
+  HIPCHK(hipGetLastError(), "launch stall");
   return 0;
 }
 
@@ -2166,11 +2299,11 @@ int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0), "event");
   HIPCHK(hipEventCreate(&e1), "event");
-  KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
   HIPCHK(hipEventRecord(e0, s), "event record");
-  for (uint32_t i = 0; i < iters; i++)
-    launch_eval(img, k, b.n, s);
-  HIPCHK(hipGetLastError(), "launch");
+  for (uint32_t i = 0; i < iters; i++) {
+    const int rc = enqueue_step(img, b, s);
+    if (rc) return rc;
+  }
   HIPCHK(hipEventRecord(e1, s), "event record");
   HIPCHK(hipEventSynchronize(e1), "event sync");
   HIPCHK(hipEventElapsedTime(ms_total, e0, e1), "elapsed");

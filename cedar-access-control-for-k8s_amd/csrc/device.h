@@ -10,6 +10,8 @@ namespace cg {
 struct Image;
 struct Batch;
 
+enum FuKind : uint32_t { FU_BIG = 0, FU_OVF = 1, FU_GEN = 2, FU_KINDS = 3 };
+
 struct DevImage {
   int device = -1;
   uint32_t *pstream = nullptr, *tier_cend = nullptr, *chunks = nullptr, *cpool = nullptr, *gstr_off = nullptr, *hot = nullptr;
@@ -32,12 +34,22 @@ struct DevBatch {
   uint8_t* bstr_bytes = nullptr;
   // results: one device block (res | reasons_f | reasons_p | errs), one copy back
   uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
-  // on-device follow-up of many-hit requests (small batches): the first pass appends the requests
-  // it flags RF_BIG to fu_wl = [count, request ids (fu_cap)], and the large-stage kernel evaluates
-  // them right behind it into fu_res / fu_rf / fu_rp / fu_er (fu_capr reasons, fu_cape errors per
-  // entry), all inside the result block, so no host round trip (device-side count, fu_cap == 0: off)
-  uint32_t *fu_wl = nullptr, *fu_res = nullptr, *fu_rf = nullptr, *fu_rp = nullptr, *fu_er = nullptr;
-  uint32_t fu_cap = 0, fu_capr = 0, fu_cape = 0;
+  // On-device follow-up (every batch size): right behind the first pass a gather kernel sorts the
+  // requests it left unfinished (RF_OVERFLOW) into three worklists, and each worklist is
+  // evaluated again on the device into its own results, all inside the result block, so one D2H
+  // copy brings back both passes and the timed step holds every launch that decides a request:
+  //   FU_BIG  more hits than the probe kernel stages (RF_BIG): its large-stage variant
+  //   FU_OVF  reason / error lists longer than the first pass holds (exact counts known, <= 64
+  //           hits): the probe kernel again with 64 reasons / 16 errors per entry
+  //   FU_GEN  structural comparisons (RF_GENERAL) or any overflow of a non-indexed image: the
+  //           policy-stream kernel
+  // fu_cnt[k] = requests the gather found for worklist k (device-side; entries past fu[k].cap are
+  // left to the host re-run). fu[k].cap == 0: worklist k off.
+  uint32_t* fu_cnt = nullptr;
+  struct FollowUp {
+    uint32_t *ids = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
+    uint32_t cap = 0, capr = 0, cape = 0;
+  } fu[3];
   uint32_t n = 0, capr = 0, cape = 0, row_words = 0;
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)
@@ -69,6 +81,7 @@ int dev_eval(const DevImage& img, DevBatch& b, void* stream);
 struct DevSubset {
   DevPool* pool = nullptr;
   void* stream = nullptr;
+  void* done = nullptr;  // event after the job's D2H copy
   void *dblk = nullptr, *hblk = nullptr;
   size_t dcls = 0, hcls = 0;
   uint32_t n = 0, capr = 0, cape = 0;
@@ -79,14 +92,22 @@ struct SubsetView {
 };
 int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx, uint32_t n, uint32_t capr,
                      uint32_t cape, int probe, void* stream, DevSubset* job);
-int dev_subset_end(DevSubset* job, SubsetView* v);
+// deadline_ns: steady-clock deadline (dev_now_ns() scale), < 0 none. Returns DEV_TIMEOUT past it
+// (the job stays in flight and keeps its blocks; release it only after its stream drained).
+int dev_subset_end(DevSubset* job, SubsetView* v, int64_t deadline_ns = -1);
 void dev_subset_release(DevSubset* job);
 int dev_download(DevBatch& b, Batch& host, void* stream);
 // Enqueues the results' copy into the batch's pinned block right behind its evaluation and records
 // an event, so that the next batch's upload and launch queue behind it without a host round trip.
 int dev_download_async(DevBatch& b, void* stream);
-// Waits for that event and copies the results out of the pinned block.
-int dev_download_finish(DevBatch& b, Batch& host);
+// Waits for that event (until deadline_ns, < 0 none: DEV_TIMEOUT past it, the batch stays in
+// flight) and points the host batch at the results in the pinned block.
+constexpr int DEV_TIMEOUT = -6;  // CG_E_TIMEOUT
+int64_t dev_now_ns();
+int dev_download_finish(DevBatch& b, Batch& host, int64_t deadline_ns = -1);
+// Fault injection (cg_ctx_inject_fault): enqueues a one-thread kernel that waits `us` microseconds
+// of device wall clock on `stream` (a slow GPU), at most 2 s.
+int dev_stall(int device, void* stream, uint64_t us);
 int dev_stream_create(int device, void** stream);
 void dev_stream_destroy(void* stream);
 int dev_stream_sync(void* stream);

@@ -163,8 +163,10 @@ struct Batch {
   uint32_t n_bstr() const { return (uint32_t)bstr_off.size() - 1; }
   // results
   uint32_t capr = 8, cape = 4;
-  uint32_t fu_hint = 0;  // on-device follow-up entries wanted (0: the default n / 32, at most 64)
-  uint32_t fu_capr_hint = 0;  // reasons per follow-up entry (0: 256)
+  // on-device follow-up sizing (device.h FuKind), from the previous batch on the same image:
+  // entries wanted per worklist (0: the default) and reasons per FU_BIG entry (0: 256)
+  uint32_t fu_want[3] = {0, 0, 0};
+  uint32_t fu_capr_hint = 0;
   // first-pass results, read in place from the batch's pinned staging block (device.h DevBatch;
   // valid while the batch lives): res[2i], [2i+1] per request, capr reasons of each effect, cape
   // error records. res is written back by overflow re-runs.
@@ -174,11 +176,12 @@ struct Batch {
   // Re-run results: request i's reason / error list read in place from the re-run's pinned result
   // block, which the owning cg_batch keeps until it is destroyed (big stays empty until a re-run
   // fills one; ptr null = the first pass's lists).
-  // the on-device follow-up of many-hit requests (device.h DevBatch::fu_*), in the pinned block
+  // the on-device follow-up worklists (device.h DevBatch::fu_*), read in the pinned block
   struct FollowUp {
-    const uint32_t *wl = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
+    const uint32_t *ids = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
     uint32_t cap = 0, capr = 0, cape = 0;
-  } fu;
+  } fu[3];
+  const uint32_t* fu_cnt = nullptr;  // requests each worklist's gather found (may exceed cap)
   struct BigRef { const uint32_t *r = nullptr, *e = nullptr; uint32_t nr = 0, ne_words = 0; };
   std::vector<BigRef> big;
   void set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words);

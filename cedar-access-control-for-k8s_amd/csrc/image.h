@@ -67,6 +67,24 @@ enum ReqHdr : uint32_t {
 enum EntRow : uint32_t { ER_TYPE = 0, ER_ID = 1, ER_ATTR0 = 2, ER_ATTR1 = 3, ER_ANC = 4, ER_PAD = 5, ENT_WORDS = 6 };
 constexpr uint32_t NO_ENT = 0xFFFFFFFFu;
 
+// ---- static entities (the image's entity hierarchy) -------------------------------------------
+// Entities compiled into the image (cg_compiler_set_entities): a group / namespace hierarchy the
+// requests' EntityMaps do not carry. Evaluation sees each request's EntityMap merged with them: a
+// static entity the request lacks is present; for a UID in both, the request's attributes and the
+// union of both parent lists. Device form: `srows` rows of ENT_WORDS laid out like the request
+// entity table, with ER_ATTR* a record and ER_ANC a reference into the constant pool
+// ([n, (type, id) x n]: the entity's transitive ancestors over the static edges, the compiled
+// `in`-closure row); `shash` an open-addressed table of SH_WORDS slots [type, id, row + 1, 0].
+// An entity index with ENT_STATIC set names static row (index & ~ENT_STATIC).
+constexpr uint32_t ENT_STATIC = 0x40000000u, SH_WORDS = 4;
+__host__ __device__ constexpr inline uint32_t uid_hash(uint32_t t, uint32_t i) {
+  uint32_t h = (t * 0x9E3779B1u) ^ (i * 0x85EBCA77u);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h;
+}
+
 // ---- policy descriptor ----------------------------------------------------------------------
 enum ScopeK : uint32_t { SK_ANY = 0, SK_EQ = 1, SK_IN = 2, SK_IS = 3, SK_ISIN = 4, SK_INSET = 5 };
 enum PolFlags : uint32_t { PF_FORBID = 1, PF_ATOMIC = 2 };
@@ -206,9 +224,9 @@ enum RowW : uint32_t {
   RW_PANC = 6,   // block-relative offset of the principal's ancestor (type, id) pairs
   RW_RANC = 7,
   RW_AANC = 8,
-  RW_PN = 9,     // ancestor counts
-  RW_RN = 10,
-  RW_AN = 11,
+  RW_PN = 9,     // ancestor counts (AN_COUNT); an indexed image's lists hold the ancestors that are
+  RW_RN = 10,    //   scope-index key entities first (AN_KEYS of them, AN_SELF: the UID itself is
+  RW_AN = 11,    //   one), so the probe kernel enumerates only keys that can exist
   RW_BLK = 12,   // heap word offset of the request block
   RW_AM0 = 13,   // action mask over the image action table (`in`: the action or an ancestor), low
   RW_AM1 = 14,   //   ... high word (valid when the image's amask_ok)
@@ -216,6 +234,8 @@ enum RowW : uint32_t {
   RW_HDR = 16,   // hot slots follow: (w0, w1) per hot path
 };
 constexpr uint32_t MISSING_W0 = 0xFFFFFFFFu;  // level-2 index key of an absent hot value
+// RW_PN / RW_RN / RW_AN fields
+constexpr uint32_t AN_COUNT = 0xFFFFu, AN_KEYS_SHIFT = 16, AN_KEYS = 0x7FFFu, AN_SELF = 0x80000000u;
 
 // ---- bytecode -------------------------------------------------------------------------------
 // word0 = op | d << 8 | a << 14 | b << 20 | c << 26 (6-bit slot fields); word1 = imm

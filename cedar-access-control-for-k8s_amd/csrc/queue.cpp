@@ -10,11 +10,17 @@
 // for that long after its first request), submits it, builds the next batch while the device runs
 // this one, then publishes the results with one futex wake for every waiting caller. Callers
 // render their own decision and reason in parallel. The batch size adapts to the offered load.
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <cstring>
+#include <ctime>
 #include <deque>
 #include <mutex>
 #include <thread>
@@ -34,7 +40,8 @@ struct QBatch {
   ~QBatch() { cg_batch_destroy(b); }
 };
 
-// One caller's request, on the caller's stack until its result is published.
+// One caller's request. Shared by the caller and the flusher: a caller whose deadline passes
+// returns while the flusher may still hold (and batch) its ticket.
 struct Ticket {
   std::shared_ptr<LoadedImage> img;  // the image the request was encoded against
   EncodedRequest e;
@@ -49,10 +56,25 @@ struct Ticket {
 
 constexpr uint32_t STRIPES = 16;
 
+using TicketP = std::shared_ptr<Ticket>;
+
 struct alignas(64) Stripe {
   std::mutex mu;
-  std::vector<Ticket*> q;
+  std::vector<TicketP> q;
 };
+
+// Futex on a 32-bit publication counter: callers sleep on it with an optional timeout (C++20
+// atomic wait has none), the flusher wakes them all once per published batch.
+void futex_wake_all(std::atomic<uint32_t>* w) {
+  (void)syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+}
+void futex_wait(std::atomic<uint32_t>* w, uint32_t seen, int64_t rel_ns) {
+  timespec ts{(time_t)(rel_ns / 1000000000), (long)(rel_ns % 1000000000)};
+  (void)syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, seen, rel_ns < 0 ? nullptr : &ts, nullptr, 0);
+}
+int64_t now_ns() {
+  return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
 
 }  // namespace
 
@@ -62,7 +84,8 @@ struct cg_queue {
   Clock::duration max_delay{};
   Stripe stripes[STRIPES];
   std::atomic<uint32_t> pending{0};     // tickets in the stripes (the flusher sleeps on it at 0)
-  std::atomic<uint64_t> done_seq{0};    // batches published (callers sleep on it)
+  std::atomic<uint64_t> done_seq{0};    // batches published
+  std::atomic<uint32_t> pub{0};         // bumped per publication (callers' futex word)
   std::atomic<uint32_t> next_stripe{0};
   std::atomic<bool> stop{false};
   std::thread flusher;
@@ -71,13 +94,14 @@ struct cg_queue {
   void run();
   void publish(uint64_t seq) {
     done_seq.store(seq, std::memory_order_release);
-    done_seq.notify_all();
+    pub.fetch_add(1, std::memory_order_release);
+    futex_wake_all(&pub);
   }
 };
 
 void cg_queue::run() {
-  std::deque<Ticket*> backlog;  // drained, not yet batched (over max_batch, or another image)
-  std::vector<Ticket*> grab;
+  std::deque<TicketP> backlog;  // drained, not yet batched (over max_batch, or another image)
+  std::vector<TicketP> grab;
   uint64_t seq = 0;
   struct InFlight {
     std::shared_ptr<QBatch> qb;
@@ -93,7 +117,7 @@ void cg_queue::run() {
         grab.swap(st.q);
       }
       pending.fetch_sub((uint32_t)grab.size(), std::memory_order_relaxed);
-      for (Ticket* t : grab) backlog.push_back(t);
+      for (TicketP& t : grab) backlog.push_back(std::move(t));
       grab.clear();
     }
   };
@@ -135,7 +159,7 @@ void cg_queue::run() {
     qb->b->host.img = img->host;
     const uint64_t my = ++seq;
     while (!backlog.empty() && qb->b->items.size() < max_batch && backlog.front()->img == img) {
-      Ticket* t = backlog.front();
+      TicketP t = std::move(backlog.front());
       backlog.pop_front();
       t->seq.store(my, std::memory_order_relaxed);
       try {
@@ -174,24 +198,34 @@ std::shared_ptr<LoadedImage> active_image(cg_ctx* ctx, std::string& err) {
 }
 
 thread_local uint32_t t_stripe = 0xFFFFFFFFu;
+thread_local std::string t_err;
 
-// Hands the ticket to the flusher and sleeps until its batch is published.
-int wait_ticket(cg_queue* q, Ticket& t, std::string& err) {
+// Hands the ticket to the flusher and sleeps until its batch is published, or until the deadline
+// (steady-clock ns, < 0 none) passes: CG_E_TIMEOUT, the ticket stays with the flusher.
+int wait_ticket(cg_queue* q, const TicketP& tp, int64_t deadline, std::string& err) {
   if (q->stop.load()) { err = "queue closed"; return CG_E_STATE; }
+  if (deadline >= 0 && now_ns() >= deadline) { err = "deadline exceeded before the request was queued"; return CG_E_TIMEOUT; }
   if (t_stripe == 0xFFFFFFFFu) t_stripe = q->next_stripe.fetch_add(1) % STRIPES;
+  Ticket& t = *tp;
   t.t = Clock::now();
   {
     Stripe& st = q->stripes[t_stripe];
     std::lock_guard<std::mutex> g(st.mu);
-    st.q.push_back(&t);
+    st.q.push_back(tp);
   }
   if (q->pending.fetch_add(1, std::memory_order_release) == 0) q->pending.notify_one();
   // the ticket's seq is written by the flusher before it publishes; read it only once published
   for (;;) {
+    const uint32_t w = q->pub.load(std::memory_order_acquire);
     const uint64_t d = q->done_seq.load(std::memory_order_acquire);
     const uint64_t my = t.seq.load(std::memory_order_relaxed);
     if (my && d >= my) break;
-    q->done_seq.wait(d, std::memory_order_acquire);
+    int64_t rel = -1;
+    if (deadline >= 0) {
+      rel = deadline - now_ns();
+      if (rel <= 0) { err = "deadline exceeded waiting for the device batch"; return CG_E_TIMEOUT; }
+    }
+    futex_wait(&q->pub, w, rel);
   }
   if (t.rc) { err = t.err; return t.rc; }
   if (t.qb->rc) { err = t.qb->err; return t.qb->rc; }
@@ -206,13 +240,13 @@ int put_string(const std::string& s, char* buf, size_t cap, size_t* need) {
   return CG_OK;
 }
 
-thread_local std::string t_err;
-
 // Queues the caller's encoded request, waits for its batch and renders the caller's result
 // (authz: cg_batch_authz's Decision + reason; else cg_batch_decision + diagnostic).
-int submit_ticket(cg_queue* q, Ticket& t, int* out, char* buf, size_t cap, size_t* need, bool authz) {
-  int rc = wait_ticket(q, t, t_err);
+int submit_ticket(cg_queue* q, const TicketP& tp, int64_t deadline, int* out, char* buf, size_t cap, size_t* need,
+                  bool authz) {
+  int rc = wait_ticket(q, tp, deadline, t_err);
   if (rc) return rc;
+  const Ticket& t = *tp;
   q->n_requests++;
   cg_batch* b = t.qb->b;
   if (authz) {
@@ -258,10 +292,12 @@ void cg_queue_destroy(cg_queue* q) {
 
 const char* cg_queue_last_error(void) { return t_err.c_str(); }
 
-int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* decision, char* reason, size_t cap,
-                           size_t* need) {
+int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout_ns, int* decision,
+                           char* reason, size_t cap, size_t* need) {
   if (!q || !sar_json || !decision) return CG_E_ARG;
-  Ticket t;
+  const int64_t deadline = timeout_ns < 0 ? -1 : now_ns() + timeout_ns;
+  TicketP tp = std::make_shared<Ticket>();
+  Ticket& t = *tp;
   t.img = active_image(q->ctx, t_err);
   if (!t.img) return CG_E_STATE;
   const std::shared_ptr<LoadedImage>& li = t.img;
@@ -293,23 +329,25 @@ int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* d
       })
     }
   }
-  return submit_ticket(q, t, decision, reason, cap, need, true);
+  return submit_ticket(q, tp, deadline, decision, reason, cap, need, true);
 }
 
-int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
-                                size_t* need) {
+int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int64_t timeout_ns, int* allow,
+                                char* diag, size_t cap, size_t* need) {
   if (!q || !item_json || !allow) return CG_E_ARG;
+  const int64_t deadline = timeout_ns < 0 ? -1 : now_ns() + timeout_ns;
   std::vector<EntityIn> ents;
   RequestIn req;
   GUARD(t_err, {
     JVal v = json_parse(item_json, len);
     decode_json_item(v, ents, req);
   })
-  Ticket t;
+  TicketP tp = std::make_shared<Ticket>();
+  Ticket& t = *tp;
   t.img = active_image(q->ctx, t_err);
   if (!t.img) return CG_E_STATE;
   GUARD(t_err, { encode_request(*t.img->host, ents, req, t.e); })
-  return submit_ticket(q, t, allow, diag, cap, need, false);
+  return submit_ticket(q, tp, deadline, allow, diag, cap, need, false);
 }
 
 int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,
@@ -344,10 +382,10 @@ int cg_queue_loadgen(cg_queue* q, const char* const* sars, const size_t* lens, u
       int d = 0;
       size_t need = 0;
       const auto t1 = Clock::now();
-      int rc = cg_queue_authorize_sar(q, sars[k], lens[k], &d, buf.data(), buf.size(), &need);
+      int rc = cg_queue_authorize_sar(q, sars[k], lens[k], -1, &d, buf.data(), buf.size(), &need);
       if (rc == CG_E_RANGE) {
         buf.resize(need);
-        rc = cg_queue_authorize_sar(q, sars[k], lens[k], &d, buf.data(), buf.size(), &need);
+        rc = cg_queue_authorize_sar(q, sars[k], lens[k], -1, &d, buf.data(), buf.size(), &need);
       }
       lat[t].push_back((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t1).count());
       if (rc) {

@@ -89,6 +89,16 @@ int cg_device_synchronize(int device);
 int cg_ctx_create(int device, cg_ctx** out);
 void cg_ctx_destroy(cg_ctx* ctx);
 const char* cg_last_error(cg_ctx* ctx);
+/* Gameday fault injection for the fail-safe path (the evaluator's counterpart of the reference's
+ * ErrorInjector, internal/server/error_injector.go:11-50, gated there by
+ * --confirm-non-prod-inject-errors; not for production). CG_FAULT_DEVICE_ERROR: the next `arg`
+ * batch submits on ctx fail with CG_E_DEVICE without touching the device. CG_FAULT_STALL: every
+ * batch submit first runs a device kernel that waits `arg` microseconds (at most 2 s), as a slow or
+ * stuck GPU would. CG_FAULT_NONE clears both. */
+#define CG_FAULT_NONE 0
+#define CG_FAULT_DEVICE_ERROR 1
+#define CG_FAULT_STALL 2
+int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg);
 /* Copies and uploads an image; the caller keeps ownership of `image`. Not active until activated. */
 int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch);
 /* Atomically makes `epoch` the image new batches bind to; in-flight batches keep theirs. */
@@ -121,7 +131,13 @@ int cg_batch_add_json(cg_batch* b, const char* json, size_t len);
 uint32_t cg_batch_size(cg_batch* b);
 /* Encodes strings, uploads the batch to the device and launches evaluation (asynchronous). */
 int cg_batch_submit(cg_batch* b);
-/* Waits for completion (timeout_ns < 0: forever), downloads results, re-runs overflowed requests. */
+/* Waits for completion, binds the results and re-runs from the host what the device could not fit.
+ * timeout_ns < 0: no deadline. Otherwise returns CG_E_TIMEOUT once timeout_ns has passed; a
+ * timeout in the first wait leaves the batch in flight (wait again, or destroy it, which drains
+ * its stream), a timeout during a host re-run fails the batch. Callers fail safe on CG_E_TIMEOUT
+ * and CG_E_DEVICE as on a webhook timeout (mount/authorization-config.yaml:11,16 failurePolicy
+ * NoOpinion; manifests/admission-webhook.yaml:11 failurePolicy Ignore): authz NoOpinion, admission
+ * allow (cmd/cedar-webhook/main.go:116 allowOnError). */
 int cg_batch_wait(cg_batch* b, int64_t timeout_ns);
 /* cedar.Decision for request i: *allow = 1 (Allow) / 0 (Deny); *tier = deciding tier index. */
 int cg_batch_decision(cg_batch* b, uint32_t i, int* allow, uint32_t* tier);
@@ -130,11 +146,17 @@ int cg_batch_decision(cg_batch* b, uint32_t i, int* allow, uint32_t* tier);
 int cg_batch_diagnostic(cg_batch* b, uint32_t i, int reasons_only, char* buf, size_t cap, size_t* need);
 /* Determining-policy indices (image order) and error count for request i. */
 int cg_batch_reasons(cg_batch* b, uint32_t i, uint32_t* idx, uint32_t cap, uint32_t* n, uint32_t* n_errors);
-/* Re-launches evaluation of the resident batch `iters` times; device time via HIP events. */
+/* Re-runs the complete evaluation step of the resident batch `iters` times (the first pass, the
+ * gather of unfinished requests and the on-device follow-up launches, exactly what
+ * cg_batch_submit enqueues); device time via HIP events on the batch's stream. */
 int cg_batch_time(cg_batch* b, uint32_t iters, float* ms_total);
-/* Requests of the batch whose result lists overflowed the first pass and were re-run by
- * cg_batch_wait (diagnostic; valid once the batch is done). */
+/* Requests of the batch whose result lists overflowed both the first pass and the on-device
+ * follow-up and were re-run from the host by cg_batch_wait (diagnostic; valid once done). */
 int cg_batch_reruns(cg_batch* b, uint32_t* n);
+/* Requests finished by each on-device follow-up worklist: counts[0] many-hit (large-stage probe
+ * kernel), [1] long reason / error lists (probe kernel), [2] structural comparisons (policy-stream
+ * kernel). Valid once the batch is done. */
+int cg_batch_followups(cg_batch* b, uint32_t* counts);
 /* Device bytes of the batch (heap + results) and of its image. */
 int cg_batch_bytes(cg_batch* b, uint64_t* batch_bytes, uint64_t* image_bytes, uint64_t* heap_bytes);
 
@@ -192,13 +214,17 @@ void cg_queue_destroy(cg_queue* q);
 /* Error text of the calling thread's last failed cg_queue_* call. */
 const char* cg_queue_last_error(void);
 /* authorizer.Decision (0 Deny, 1 Allow, 2 NoOpinion) and reason of one SubjectAccessReview, as
- * cg_batch_authz reports them. CG_E_RANGE: reason needs *need bytes (the decision is valid). */
-int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int* decision, char* reason, size_t cap,
-                           size_t* need);
+ * cg_batch_authz reports them. CG_E_RANGE: reason needs *need bytes (the decision is valid).
+ * timeout_ns (< 0: none) bounds the whole call, counted from its entry: past it the call returns
+ * CG_E_TIMEOUT (the request may still be evaluated; its result is dropped). On CG_E_TIMEOUT or
+ * CG_E_DEVICE the caller answers NoOpinion (authorizer.go:80-84; the apiserver's failurePolicy). */
+int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout_ns, int* decision,
+                           char* reason, size_t cap, size_t* need);
 /* TieredPolicyStores.IsAuthorized for one Cedar-JSON item (cg_batch_add_json's format) through
- * the queue: *allow and, when diag or need is given, json.Marshal(cedar.Diagnostic). */
-int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int* allow, char* diag, size_t cap,
-                                size_t* need);
+ * the queue: *allow and, when diag or need is given, json.Marshal(cedar.Diagnostic). timeout_ns as
+ * for cg_queue_authorize_sar; on CG_E_TIMEOUT / CG_E_DEVICE the admission caller allows. */
+int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int64_t timeout_ns, int* allow,
+                                char* diag, size_t cap, size_t* need);
 /* Counters: device batches run, requests through the device, fast-path requests, largest batch,
  * nanoseconds the flusher spent in submit + wait. Any pointer may be NULL. */
 int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,

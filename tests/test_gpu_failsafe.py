@@ -1,0 +1,131 @@
+"""§8(b) fail-safe contract through the C-ABI: deadlines (CG_E_TIMEOUT) and device errors
+(CG_E_DEVICE) on the batch and queue paths, driven by the gameday fault injector
+(cg_ctx_inject_fault). Authorization fails safe to NoOpinion (authorizer.go:80-84; the apiserver's
+failurePolicy NoOpinion, mount/authorization-config.yaml:11,16), admission to allow
+(cmd/cedar-webhook/main.go:116 allowOnError; manifests/admission-webhook.yaml:11 Ignore)."""
+import json
+import os
+import time
+
+import pytest
+
+import cedar_oracle as co
+import k8s_model as km
+from conftest import GOLDEN
+
+import cedargpu
+from cedargpu import synth
+
+pytestmark = pytest.mark.gpu
+
+CORPUS = json.load(open(os.path.join(GOLDEN, "reference_corpus.json")))
+DEMO_AUTHZ = "\n".join(v for k, v in sorted(CORPUS["demo"].items()) if k.startswith("authorization"))
+DEMO_ADM = "\n".join(v for k, v in sorted(CORPUS["demo"].items()) if k.startswith("admission"))
+
+
+@pytest.fixture()
+def ctx():
+    assert cedargpu.device_count() >= 1, "GPU tests need a GPU"
+    c = cedargpu.Context(0)
+    yield c
+    c.inject_fault(cedargpu.FAULT_NONE)
+    c.close()
+
+
+def _sars():
+    sars = synth.random_sars(200, seed=71, pop=synth.Population(seed=71, n_users=300, n_groups=30))
+    sars.append(synth.make_sar("system:authorizer:cedar-authorizer", "", [], "get", group="rbac.authorization.k8s.io",
+                               resource="roles"))  # self-allow fast path (authorizer.go:44-49)
+    sars.append(synth.make_sar("system:kube-scheduler", "", [], "get", resource="pods"))  # system: bypass
+    sars.append(synth.make_sar("test-user", "1", ["viewers"], "get", ns="default", resource="pods", name="p"))
+    return sars
+
+
+def _oracle(text, sars):
+    tiers = [co.PolicySet.from_bytes("demo.cedar", text)]
+    return [km.authorize(tiers, km.attributes_from_sar(s)) for s in sars]
+
+
+def test_device_error_authz_answers_noopinion(ctx):
+    authz = cedargpu.Authorizer([cedargpu.MemoryStore("demo.cedar", DEMO_AUTHZ)], ctx=ctx)
+    sars = _sars()
+    want = _oracle(DEMO_AUTHZ, sars)
+    ctx.inject_fault(cedargpu.FAULT_DEVICE_ERROR, 1)
+    got = authz.authorize_batch(sars)
+    for s, g, w in zip(sars, got, want):
+        name = s["spec"]["user"]
+        fast = name.startswith("system:") and not name.startswith(("system:serviceaccount:", "system:node:"))
+        fast = fast or (name == "system:authorizer:cedar-authorizer")
+        assert g == (w if fast else (cedargpu.Authorizer.NO_OPINION, "")), s
+    assert authz.authorize_batch(sars) == want  # the injected error was consumed
+
+
+def test_device_error_admission_allows(ctx):
+    handler = cedargpu.AdmissionHandler([cedargpu.MemoryStore("adm.cedar", DEMO_ADM), cedargpu.ALLOW_ALL_ADMISSION],
+                                        ctx=ctx)
+    reviews = synth.admission_reviews(64, seed=9)
+    normal = handler.handle_batch(reviews)
+    assert any(not ok for ok, _, _ in normal), "the workload must hold denials for the test to mean anything"
+    ctx.inject_fault(cedargpu.FAULT_DEVICE_ERROR, 1)
+    assert handler.handle_batch(reviews) == [(True, 200, "")] * len(reviews)
+    assert handler.handle_batch(reviews) == normal
+
+
+def test_batch_wait_deadline_then_completes(ctx):
+    tiers = cedargpu.TieredPolicyStores([cedargpu.MemoryStore("demo.cedar", DEMO_AUTHZ)], ctx=ctx)
+    assert tiers.ready()
+    sars = _sars()
+    ctx.inject_fault(cedargpu.FAULT_STALL, 300_000)
+    b = ctx.batch()
+    b.add_sar_json(json.dumps(sars))
+    b.submit()
+    t0 = time.perf_counter()
+    with pytest.raises(cedargpu.DeadlineError):
+        b.wait(timeout=0.02)
+    assert time.perf_counter() - t0 < 0.2
+    b.wait()  # the batch stayed in flight and completes
+    assert [b.authz(i) for i in range(len(b))] == _oracle(DEMO_AUTHZ, sars)
+    b.close()
+    # a timed-out batch destroyed while in flight: destroy drains its stream
+    b = ctx.batch()
+    b.add_sar_json(json.dumps(sars[:10]))
+    b.submit()
+    with pytest.raises(cedargpu.DeadlineError):
+        b.wait(timeout=0.01)
+    b.close()
+    ctx.inject_fault(cedargpu.FAULT_NONE)
+    b = ctx.batch()
+    b.add_sar_json(json.dumps(sars))
+    b.submit()
+    b.wait(timeout=5.0)
+    assert [b.authz(i) for i in range(len(b))] == _oracle(DEMO_AUTHZ, sars)
+    b.close()
+
+
+def test_queue_deadline_and_failsafe(ctx):
+    cedargpu.TieredPolicyStores([cedargpu.MemoryStore("demo.cedar", DEMO_AUTHZ)], ctx=ctx)
+    sars = _sars()
+    want = _oracle(DEMO_AUTHZ, sars)
+    q = cedargpu.Queue(ctx, max_batch=256, max_delay_us=0)
+    try:
+        ctx.inject_fault(cedargpu.FAULT_STALL, 400_000)
+        t0 = time.perf_counter()
+        with pytest.raises(cedargpu.DeadlineError):
+            q.authorize(sars[-1], timeout=0.05)
+        assert time.perf_counter() - t0 < 0.3
+        assert q.authorize_failsafe(sars[-1], timeout=0.05) == (cedargpu.Authorizer.NO_OPINION, "")
+        em, r = km.record_to_cedar_resource(km.attributes_from_sar(sars[-1]))
+        with pytest.raises(cedargpu.DeadlineError):
+            q.is_authorized(co.entities_to_json(em), co.request_to_json(r), timeout=0.05)
+        # fast paths answer on the caller's thread, inside any deadline
+        assert q.authorize(sars[-3], timeout=0.0) == want[-3]
+        ctx.inject_fault(cedargpu.FAULT_NONE)
+        time.sleep(0.5)  # the stalled batches drain
+        assert [q.authorize(s, timeout=5.0) for s in sars] == want
+        ctx.inject_fault(cedargpu.FAULT_DEVICE_ERROR, 1)
+        got = q.authorize_failsafe(sars[-1], timeout=5.0)
+        assert got == (cedargpu.Authorizer.NO_OPINION, "")
+        assert q.authorize(sars[-1], timeout=5.0) == want[-1]
+    finally:
+        ctx.inject_fault(cedargpu.FAULT_NONE)
+        q.close()

@@ -287,6 +287,65 @@ def test_followup_sized_by_previous_batch(ctx):
     assert [d for d, _ in got] == [d for d, _ in runs[1][1][:300]]
 
 
+def _level_items(levels, seed=0):
+    """Requests whose principal.level = L satisfy the L + 1 policies `principal.level >= i`."""
+    out = []
+    for k, lv in enumerate(levels):
+        ents = [{"uid": {"type": "k8s::User", "id": f"u{k}"}, "attrs": {"level": lv}, "parents": []}]
+        req = {"principal": {"type": "k8s::User", "id": f"u{k}"}, "action": {"type": "k8s::Action", "id": "get"},
+               "resource": {"type": "k8s::Resource", "id": f"/r/{k}"}, "context": {}}
+        out.append((ents, req))
+    return out
+
+
+def _run_batch(ctx, items):
+    b = ctx.batch()
+    b.add_json(json.dumps([{"entities": e, "request": r} for e, r in items]))
+    b.submit()
+    b.wait()
+    out = (b.reruns(), b.followups(), [b.diagnostic(i) for i in range(len(b))])
+    b.close()
+    return out
+
+
+def _oracle_diags(stores, items):
+    otiers = oracle_tiers(stores)
+    return [co.tiered_is_authorized(otiers, co.entities_from_json(e), co.request_from_json(r))[1].to_go_json()
+            for e, r in items]
+
+
+def test_capacity_hint_short_then_long_lists(ctx):
+    """one image, a batch of ~70-reason requests (FU_BIG capacity hint 96), then one of
+    ~200 (longer than the hint: the follow-up overflows and the host re-runs), then another of ~200
+    (the hint grew: no re-run). Every batch matches the oracle."""
+    pols = "\n".join(f"permit (principal, action, resource) when {{ principal.level >= {i} }};" for i in range(260))
+    stores = [cedargpu.MemoryStore("levels.cedar", pols)]
+    ctx.load(cedargpu.build_image(stores, epoch=961), 961)
+    short = _level_items([66 + k % 8 for k in range(256)])
+    long_ = _level_items([196 + k % 8 for k in range(256)])
+    runs = [_run_batch(ctx, it) for it in (short, long_, long_)]
+    assert runs[1][0] > 0, "the second batch outgrows the first batch's follow-up capacity"
+    assert runs[2][0] == 0 and runs[2][1]["big"] == 256
+    for (_, _, diags), it in zip(runs, (short, long_, long_)):
+        assert diags == _oracle_diags(stores, it)
+
+
+def test_first_pass_capacity_hint_65536(ctx):
+    """65,536 requests with ~16 reasons each. The first batch overflows the default
+    8-reason first pass; the next batch on the image sizes the first pass from it (no follow-up,
+    no re-run). Parity on a sample against the oracle."""
+    pols = "\n".join(f"permit (principal, action, resource) when {{ principal.level >= {i} }};" for i in range(24))
+    stores = [cedargpu.MemoryStore("levels16.cedar", pols)]
+    ctx.load(cedargpu.build_image(stores, epoch=962), 962)
+    items = _level_items([12 + k % 8 for k in range(65536)])
+    r1 = _run_batch(ctx, items)
+    r2 = _run_batch(ctx, items)
+    assert r2[0] == 0 and r2[1] == {"big": 0, "long_lists": 0, "structural": 0}
+    assert r1[2] == r2[2]
+    sample = list(range(0, 65536, 211))
+    assert [r2[2][i] for i in sample] == _oracle_diags(stores, [items[i] for i in sample])
+
+
 def test_index_kernel_action_hierarchy_duplicates(ctx):
     """A policy filed under several actions of `action in [..]` is reached twice when the request
     action's ancestors include more than one of them; it must be reported once."""
