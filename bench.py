@@ -115,11 +115,14 @@ def cpu_baseline(policies_text, items, seconds, threads, cpu_info, entities=None
                       f"{cpu_info['omp_num_threads']}) on {cpu_info['cpu_model'] or 'unknown CPU'}"}
 
 
-def parity_sample(policies_text, items, idx, gpu_batch, threads):
+def parity_sample(policies_text, items, idx, gpu_batch, threads, entities=None):
     """GPU authorizer answers vs the C++ oracle on a sample of the timed batch (decision + exact
-    reason string, authorizer.go:75-84 mapping)."""
+    reason string, authorizer.go:75-84 mapping; the static group hierarchy merged into every
+    EntityMap)."""
     from cedar_ref import RefPolicySet, items_json
     ref = RefPolicySet()
+    if entities:
+        ref.set_entities(json.dumps(entities))
     ref.add_tier()
     ref.add_document("c3.cedar", policies_text)
     ref.load_items(items_json(items))
@@ -244,7 +247,7 @@ def secondary_configs(ctx, n_req, threads, sample=512):
     return out
 
 
-def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=120.0):
+def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=120.0, entities=None):
     """Policy hot reload after the timed region: rank 0 compiles epoch 2 (the policies plus one
     forbid), one RCCL broadcast ships it to every GPU, each rank activates it and checks a request
     the new forbid decides. Runs in a daemon thread with a deadline so that a stuck collective
@@ -261,7 +264,8 @@ def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=120.0):
             uid = cdist.exchange_unique_id(rank) if dist_on else cdist.unique_id()
             comm = cdist.Comm(device, world, rank, uid)
             extra = 'forbid (principal, action == k8s::Action::"reload-check", resource);'
-            image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies + "\n" + extra)], epoch=2) if rank == 0 else None
+            image = (cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies + "\n" + extra)], epoch=2,
+                                          entities=entities) if rank == 0 else None)
             t0 = time.perf_counter()
             n = comm.broadcast_image(ctx, image, 2)
             dt = time.perf_counter() - t0
@@ -326,6 +330,9 @@ def main():
     ap.add_argument("--order", default="random", choices=["random", "user"],
                     help="request order within the batch (locality study; random is the benchmark)")
     ap.add_argument("--variant", default="full", help="policy-shape study: full | scope-only | no-group | atomic-only")
+    ap.add_argument("--hierarchy", default="dag", choices=["dag", "flat"],
+                    help="k8s::Group hierarchy: a static depth-12 DAG over the 5k groups (C3 as BASELINE.json "
+                         "states it) or none (groups without parents, round 1's workload)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--parity-sample", type=int, default=2048)
     ap.add_argument("--no-reload", dest="reload", action="store_false",
@@ -348,7 +355,8 @@ def main():
 
     from cedargpu import synth
 
-    pop = synth.Population(seed=7)
+    pop = synth.Population(seed=7, dag_depth=12 if args.hierarchy == "dag" else 0)
+    entities = pop.static_entities() or None  # the image's static group hierarchy
     policies = synth.abac_policies(args.policies, seed=31, pop=pop, variant=args.variant)
     sars = synth.random_sars(args.batch, seed=1000 + rank, pop=pop)
     if args.order == "user":  # locality study: the batch grouped by caller
@@ -359,7 +367,7 @@ def main():
     threads = args.cpu_workers or usable
     items, idx = oracle_items(sars[:args.parity_sample]) if rank == 0 else ([], [])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        baseline = cpu_baseline(policies, items, args.cpu_seconds, threads, cpu_info)
+        baseline = cpu_baseline(policies, items, args.cpu_seconds, threads, cpu_info, entities)
 
     # torch is plumbing only: the cross-rank barrier / max-reduce of timings runs over gloo on CPU
     # tensors. torch's bundled HIP runtime is never initialised in this process (it would clash
@@ -375,7 +383,7 @@ def main():
         dist.init_process_group(backend="gloo")
     device = local
 
-    image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies)], epoch=1)
+    image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies)], epoch=1, entities=entities)
     ctx = cedargpu.Context(device)
     ctx.load(image, 1)
     # steady state: the batch before the measured one on this image sizes its result capacities
@@ -436,10 +444,10 @@ def main():
     if rank == 0 and args.serve_threads and args.serve_requests:
         serving = serve(ctx, sars, args.serve_threads, args.serve_requests, args.serve_max_batch)
 
-    parity = parity_sample(policies, items, idx, b, threads) if rank == 0 and items else None
+    parity = parity_sample(policies, items, idx, b, threads, entities) if rank == 0 and items else None
     configs = (secondary_configs(ctx, args.configs_requests, threads)
                if rank == 0 and world == 1 and args.configs_requests else None)
-    reload = hot_reload(ctx, policies, rank, world, local, dist_on) if args.reload else None
+    reload = hot_reload(ctx, policies, rank, world, local, dist_on, entities=entities) if args.reload else None
 
     if rank == 0:
         ms_per_step = wall_s * 1e3 / args.steps
@@ -469,9 +477,12 @@ def main():
             "dtype": "u32",
             "data": "synthetic (seeded SubjectAccessReviews + generated ABAC policies; no dataset)",
             "config": {"workload": "C3 single-GPU shard: 10k ABAC policies (k8s::Group scope, namespace/apiGroup/"
-                                   "resource/labelSelector/like conditions) x synthetic SARs",
+                                   "resource/labelSelector/like conditions) x synthetic SARs"
+                                   + (", deep k8s::Group `in` hierarchy (static DAG over 5k groups, depth <= 12, "
+                                      "compiled in-closure rows)" if entities else ""),
                        "policies": args.policies, "requests_per_gpu": args.batch, "tiers": 1,
-                       "variant": args.variant,
+                       "variant": args.variant, "hierarchy": args.hierarchy,
+                       "static_entities": len(entities or []),
                        "step": "first pass + gather + on-device follow-up launches (every request decided, "
                                "all reasons and errors listed, on the device)",
                        "device_followup_requests": followups,

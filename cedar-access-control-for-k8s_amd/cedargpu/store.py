@@ -150,9 +150,15 @@ class Compiler:
         except Exception:
             pass
 
-    def build(self, stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
+    def build(self, stores: Sequence[PolicyStore], epoch: int = 1, entities: Optional[list] = None) -> bytes:
+        """Compiles the tiers. `entities`: the image's static entities (Cedar JSON entity list, e.g.
+        a group hierarchy), merged into every request's EntityMap (cg_compiler_set_entities)."""
         c = self._h
         lib.cg_compiler_clear(c)
+        eb = _b(json.dumps(entities)) if entities else b""
+        rc = lib.cg_compiler_set_entities(c, eb, len(eb))
+        if rc:
+            raise _err(rc, lib.cg_compiler_last_error(c).decode())
         for st in stores:
             lib.cg_compiler_add_tier(c)
             for d in st.documents():
@@ -182,11 +188,11 @@ class Compiler:
         return dict(zip(("hits", "misses", "entries"), (x.value for x in v)))
 
 
-def build_image(stores: Sequence[PolicyStore], epoch: int = 1) -> bytes:
-    """Compiles the tiers (one per store) into an image blob. Host only; no GPU needed."""
+def build_image(stores: Sequence[PolicyStore], epoch: int = 1, entities: Optional[list] = None) -> bytes:
+    """Compiles the tiers (one per store), and the static entities, into an image blob. Host only."""
     c = Compiler()
     try:
-        return c.build(stores, epoch)
+        return c.build(stores, epoch, entities)
     finally:
         c.close()
 
@@ -497,8 +503,10 @@ class TieredPolicyStores:
     _epoch_lock = threading.Lock()
     _next_epoch = 1
 
-    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None):
+    def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None,
+                 entities: Optional[list] = None):
         self.stores = list(stores)
+        self.entities = entities  # static entities merged into every EntityMap (a group hierarchy)
         self.ctx = ctx or Context(device)
         self.reload()
 
@@ -507,7 +515,7 @@ class TieredPolicyStores:
         with TieredPolicyStores._epoch_lock:
             epoch = TieredPolicyStores._next_epoch
             TieredPolicyStores._next_epoch += 1
-        self.image = build_image(self.stores, epoch)
+        self.image = build_image(self.stores, epoch, self.entities)
         self.ctx.load(self.image, epoch, activate=True)
         self.epoch = epoch
 
@@ -538,8 +546,8 @@ class Authorizer:
     DENY, ALLOW, NO_OPINION = 0, 1, 2
 
     def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None,
-                 timeout: Optional[float] = None):
-        self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx)
+                 timeout: Optional[float] = None, entities: Optional[list] = None):
+        self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx, entities=entities)
         self._loaded = False
         self.timeout = timeout  # per batch, seconds (the apiserver allows 3 s: authorization-config.yaml:11)
 
@@ -572,8 +580,8 @@ class AdmissionHandler:
     [(allowed, HTTP status code, message)]."""
 
     def __init__(self, stores: Sequence[PolicyStore], device: int = 0, ctx: Optional[Context] = None,
-                 timeout: Optional[float] = None):
-        self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx)
+                 timeout: Optional[float] = None, entities: Optional[list] = None):
+        self.tiers = TieredPolicyStores(stores, device=device, ctx=ctx, entities=entities)
         self.timeout = timeout  # per batch, seconds (the webhook allows 30 s: admission-webhook.yaml:26)
 
     def handle_batch(self, reviews: Sequence[dict]) -> List[Tuple[bool, int, str]]:

@@ -57,9 +57,18 @@ def _zipf_idx(rng, n: int, size: int, s: float = 1.1) -> np.ndarray:
 
 
 class Population:
-    """Users, service accounts, nodes and their group memberships."""
+    """Users, service accounts, nodes and their group memberships; with `dag_depth`, a static
+    k8s::Group hierarchy of at most that many levels (C3, SURVEY §8(d)).
 
-    def __init__(self, seed: int = 7, n_users: int = 50_000, n_groups: int = 5_000, n_namespaces: int = 200):
+    The hierarchy ranks groups by popularity (group-00000 is the most used, in memberships and in
+    policies) and puts the popular ones near the roots: level L holds ~8 * 1.8^L groups. A group at
+    level L > 0 has one parent on level L - 1 and, one time in four, a second one on level L - 1 or
+    L - 2, so a group's transitive ancestors number up to ~2L. The reference's SAR entities give
+    groups no parents (internal/server/entities/user.go:40-54): the hierarchy reaches evaluation as
+    the image's static entities (`static_entities()`, cg_compiler_set_entities)."""
+
+    def __init__(self, seed: int = 7, n_users: int = 50_000, n_groups: int = 5_000, n_namespaces: int = 200,
+                 dag_depth: int = 0):
         rng = np.random.Generator(np.random.PCG64(seed))
         self.n_users = n_users
         self.groups = [f"group-{i:05d}" for i in range(n_groups)]
@@ -84,6 +93,31 @@ class Population:
             if kind[i] == 1:
                 gs += ["system:serviceaccounts", f"system:serviceaccounts:{self.names[i].split(':')[2]}"]
             self.user_groups.append(list(dict.fromkeys(gs)))
+        self.group_parents: Dict[str, List[str]] = {}
+        if dag_depth > 0:
+            drng = np.random.Generator(np.random.PCG64(seed + 0x5A6))  # memberships above are unchanged
+            level = [min(dag_depth - 1, int(np.log1p(i / 8.0) / np.log(1.8))) for i in range(n_groups)]
+            by_level: Dict[int, List[int]] = {}
+            for i, lv in enumerate(level):
+                by_level.setdefault(lv, []).append(i)
+            for i, lv in enumerate(level):
+                if lv == 0:
+                    continue
+                up = by_level[lv - 1]
+                par = [up[int(drng.integers(len(up)))]]
+                if drng.random() < 0.25:
+                    alt = by_level[max(0, lv - 2)] if drng.random() < 0.5 else up
+                    par.append(alt[int(drng.integers(len(alt)))])
+                self.group_parents[self.groups[i]] = [self.groups[p] for p in dict.fromkeys(par)]
+
+    def static_entities(self) -> List[dict]:
+        """The group hierarchy as Cedar JSON entities, shaped like UserToCedarEntity's group
+        entities (entities/user.go:40-54: attrs {name}) plus their parents."""
+        if not self.group_parents:
+            return []
+        return [{"uid": {"type": "k8s::Group", "id": g}, "attrs": {"name": g},
+                 "parents": [{"type": "k8s::Group", "id": p} for p in self.group_parents.get(g, [])]}
+                for g in self.groups]
 
 
 def make_sar(user: str, uid: str, groups: List[str], verb: str, ns: str = "", group: str = "", version: str = "v1",

@@ -40,6 +40,7 @@ using namespace cg;
 
 struct cg_compiler {
   std::vector<std::vector<DocSpec>> tiers;
+  std::vector<EntityIn> statics;  // the image's static entities (cg_compiler_set_entities)
   ParseCache cache;  // parsed documents reused across builds
   std::string err;
 };
@@ -141,7 +142,7 @@ void group_requests(cg_batch* b) {
     // groups: the principal's ancestor (type, id) pairs
     uint64_t g = mix(0x9E3779B97F4A7C15ull, row[cgi::RW_P]);
     const size_t anc = (size_t)row[cgi::RW_BLK] + row[cgi::RW_PANC];
-    for (uint32_t j = 0; j < 2 * row[cgi::RW_PN] && anc + j < h.heap.size(); j++) g = mix(g, h.heap[anc + j]);
+    for (uint32_t j = 0; j < 2 * (row[cgi::RW_PN] & cgi::AN_COUNT) && anc + j < h.heap.size(); j++) g = mix(g, h.heap[anc + j]);
     uint64_t hv = 0x2545F4914F6CDD1Dull;
     for (uint32_t j = cgi::RW_HDR; j < rw; j++) hv = mix(hv, row[j]);
     key[i] = ((ar >> 52) << 52) | (((g >> 40) << (64 - 12 - 24)) & gmask) | (((hv >> 56) << ib) & hmask) | (uint64_t)i;
@@ -301,6 +302,16 @@ int cg_compiler_cache_stats(cg_compiler* c, uint64_t* hits, uint64_t* misses, ui
   return CG_OK;
 }
 
+int cg_compiler_set_entities(cg_compiler* c, const char* json, size_t len) {
+  if (!c || (!json && len)) return CG_E_ARG;
+  GUARD(c->err, {
+    std::vector<EntityIn> ents;
+    if (len) decode_json_entities(json_parse(json, len), ents);
+    c->statics = std::move(ents);
+    return CG_OK;
+  })
+}
+
 int cg_compiler_add_tier(cg_compiler* c) {
   if (!c) return CG_E_ARG;
   c->tiers.emplace_back();
@@ -343,7 +354,7 @@ int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* fi
 int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len) {
   if (!c || !image || !len) return CG_E_ARG;
   try {
-    auto img = compile_image(c->tiers, epoch, &c->cache);
+    auto img = compile_image(c->tiers, epoch, &c->cache, &c->statics);
     auto blob = img->serialize();
     uint8_t* p = (uint8_t*)std::malloc(blob.size());
     if (!p) { c->err = "out of host memory"; return CG_E_ARG; }

@@ -69,9 +69,12 @@ struct KArgs {
   const uint32_t* __restrict__ bfilt;    // key filter (image.h filt_*)
   const uint32_t* __restrict__ bstream;
   const uint32_t* __restrict__ rows;     // columnar request rows (row_words each)
+  const uint32_t* __restrict__ srows;    // static entities (image.h "static entities")
+  const uint4* __restrict__ shash;
   unsigned long long* stats;             // probe-kernel work counters (STATS variant only)
   const uint32_t* n_dev;                 // follow-up pass: request count on the device (null: n_req)
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
+  uint32_t n_static, smask;
 };
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
@@ -91,8 +94,13 @@ struct Ctx {
   uint32_t pt, pi, at, ai, rt, ri;
   uint32_t pidx, aidx, ridx;
   uint32_t nent;
-  uint32_t p_anc, p_nanc, r_anc, r_nanc;  // heap offsets of ancestor pair arrays, and counts
+  uint32_t p_anc, p_nanc, r_anc, r_nanc;  // offsets of ancestor pair arrays (in p_base / r_base), counts
+  const uint32_t* p_base;                 // the request block, or the constant pool for a static entity
+  const uint32_t* r_base;
   uint32_t a_anc, a_nanc;                 // action ancestors (probe kernel; stream kernel uses aidx)
+  const uint32_t* srows;                  // static entities: rows and UID hash (n_static == 0: none)
+  const uint4* shash;
+  uint32_t n_static, smask;
   // first 8 principal ancestors, for the exact `in` test in registers (named scalars: an array
   // here would keep the whole context out of registers)
   uint32_t t0, i0, t1, i1, t2, i2, t3, i3, t4, i4, t5, i5, t6, i6, t7, i7;
@@ -302,6 +310,16 @@ __device__ __forceinline__ bool rec_get_heap(const uint32_t* blk, uint32_t rw0, 
   return false;
 }
 
+// A UID the request's table lacks may be one of the image's static entities (merged EntityMap).
+__device__ __forceinline__ uint32_t static_find(const Ctx& c, uint32_t et, uint32_t ei) {
+  if (!c.n_static) return NO_ENT;
+  for (uint32_t h = uid_hash(et, ei) & c.smask;; h = (h + 1) & c.smask) {
+    const uint4 sl = c.shash[h];
+    if (sl.z == 0) return NO_ENT;
+    if (sl.x == et && sl.y == ei) return ENT_STATIC | (sl.z - 1);
+  }
+}
+
 __device__ __forceinline__ uint32_t find_ent(const Ctx& c, uint32_t et, uint32_t ei) {
   if (et == c.pt && ei == c.pi) return opq(c.pidx);
   if (et == c.rt && ei == c.ri) return opq(c.ridx);
@@ -310,7 +328,12 @@ __device__ __forceinline__ uint32_t find_ent(const Ctx& c, uint32_t et, uint32_t
     const uint32_t* row = c.blk + RH_WORDS + i * ENT_WORDS;
     if (row[ER_TYPE] == et && row[ER_ID] == ei) return i;
   }
-  return NO_ENT;
+  return static_find(c, et, ei);
+}
+
+// entity row of a table index or a static index
+__device__ __forceinline__ const uint32_t* ent_row(const Ctx& c, uint32_t idx) {
+  return (idx & ENT_STATIC) ? c.srows + (size_t)(idx & ~ENT_STATIC) * ENT_WORDS : c.blk + RH_WORDS + idx * ENT_WORDS;
 }
 
 // exact membership in a heap ancestor list: pairs at blk[off + 2k], independent loads, 4 per step
@@ -326,18 +349,22 @@ __device__ __forceinline__ bool anc_scan(const uint32_t* blk, uint32_t off, uint
   return f;
 }
 
-__device__ __forceinline__ void anc_of(const Ctx& c, uint32_t idx, uint32_t& off, uint32_t& n) {
-  off = 0; n = 0;
+// ancestor list of an entity: pairs at base[off + 2k] (a static entity's closure row lives in the
+// constant pool)
+__device__ __forceinline__ void anc_of(const Ctx& c, uint32_t idx, const uint32_t*& base, uint32_t& off, uint32_t& n) {
+  base = c.blk; off = 0; n = 0;
   if (idx == NO_ENT) return;
-  const uint32_t ref = c.blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;
-  n = c.blk[ref];
+  if (idx & ENT_STATIC) base = c.cpool;
+  const uint32_t ref = ent_row(c, idx)[ER_ANC] & OFF_MASK;
+  n = base[ref];
   off = ref + 1;
 }
 
 __device__ __forceinline__ bool anc_has(const Ctx& c, uint32_t idx, uint32_t qt, uint32_t qi) {
+  const uint32_t* base;
   uint32_t off, n;
-  anc_of(c, idx, off, n);
-  return anc_scan(c.blk, off, n, qt, qi);
+  anc_of(c, idx, base, off, n);
+  return anc_scan(base, off, n, qt, qi);
 }
 
 __device__ __forceinline__ bool ent_in(const Ctx& c, uint32_t et, uint32_t ei, uint32_t qt, uint32_t qi) {
@@ -365,13 +392,13 @@ __device__ __forceinline__ bool p_in(const Ctx& c, uint32_t et, uint32_t ei, uin
   bool f = ((c.t0 == et) & (c.i0 == ei)) | ((c.t1 == et) & (c.i1 == ei)) | ((c.t2 == et) & (c.i2 == ei)) |
            ((c.t3 == et) & (c.i3 == ei)) | ((c.t4 == et) & (c.i4 == ei)) | ((c.t5 == et) & (c.i5 == ei)) |
            ((c.t6 == et) & (c.i6 == ei)) | ((c.t7 == et) & (c.i7 == ei));
-  if (!f && c.p_nanc > 8) f = anc_scan(c.blk, c.p_anc + 16, c.p_nanc - 8, et, ei);
+  if (!f && c.p_nanc > 8) f = anc_scan(c.p_base, c.p_anc + 16, c.p_nanc - 8, et, ei);
   return f;
 }
 __device__ __forceinline__ bool r_in(const Ctx& c, uint32_t et, uint32_t ei, uint32_t bit) {
   if (c.rt == et && c.ri == ei) return true;
   if (!bloom_test(c.rb0, c.rb1, c.rb2, c.rb3, bit)) return false;
-  return anc_scan(c.blk, c.r_anc, c.r_nanc, et, ei);
+  return anc_scan(c.r_base, c.r_anc, c.r_nanc, et, ei);
 }
 
 // ---- strings / like -------------------------------------------------------------------------
@@ -728,7 +755,7 @@ __device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code,
               e.code = E_ENTITY_MISSING; e.et = et; e.ei = ei; err = true; wr = false;
               break;
             }
-            const uint32_t* row = c.blk + RH_WORDS + idx * ENT_WORDS;
+            const uint32_t* row = ent_row(c, idx);
             RV got;
             const bool f = rec_get(c, RV{row[ER_ATTR0], row[ER_ATTR1], 0}, imm, got);
             if (has) { out = mk_bool(f); break; }
@@ -978,9 +1005,14 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   c.n_gstr = a.n_gstr;
   c.hotl = hot_lds + threadIdx.x;
   c.hstride = BLOCK;
+  c.srows = a.srows;
+  c.shash = a.shash;
+  c.n_static = a.n_static;
+  c.smask = a.smask;
   c.pb0 = c.pb1 = c.pb2 = c.pb3 = 0;
   c.rb0 = c.rb1 = c.rb2 = c.rb3 = 0;
   c.p_anc = c.p_nanc = c.r_anc = c.r_nanc = 0;
+  c.p_base = c.r_base = c.blk;
   c.a_anc = c.a_nanc = 0;
   uint32_t am0 = 0, am1 = 0;  // action mask over the image action table: action in act[k]
   uint32_t as0 = 0, as1 = 0;  // action == act[k]
@@ -990,20 +1022,20 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
     c.at = c.blk[RH_A] & X_MASK; c.ai = c.blk[RH_A + 1];
     c.rt = c.blk[RH_R] & X_MASK; c.ri = c.blk[RH_R + 1];
     c.pidx = c.blk[RH_PIDX]; c.aidx = c.blk[RH_AIDX]; c.ridx = c.blk[RH_RIDX];
-    anc_of(c, c.pidx, c.p_anc, c.p_nanc);
+    anc_of(c, c.pidx, c.p_base, c.p_anc, c.p_nanc);
 #define CG_ANC(k) \
-    c.t##k = k < c.p_nanc ? c.blk[c.p_anc + 2 * k] : 0xFFFFFFFFu; \
-    c.i##k = k < c.p_nanc ? c.blk[c.p_anc + 2 * k + 1] : 0xFFFFFFFFu;
+    c.t##k = k < c.p_nanc ? c.p_base[c.p_anc + 2 * k] : 0xFFFFFFFFu; \
+    c.i##k = k < c.p_nanc ? c.p_base[c.p_anc + 2 * k + 1] : 0xFFFFFFFFu;
     CG_ANC(0) CG_ANC(1) CG_ANC(2) CG_ANC(3) CG_ANC(4) CG_ANC(5) CG_ANC(6) CG_ANC(7)
 #undef CG_ANC
-    anc_of(c, c.ridx, c.r_anc, c.r_nanc);
+    anc_of(c, c.ridx, c.r_base, c.r_anc, c.r_nanc);
     // ancestor-or-self Bloom filters of principal and resource
     bloom_add(c.pb0, c.pb1, c.pb2, c.pb3, uid_bloom_bit(c.pt, c.pi));
     for (uint32_t k = 0; k < c.p_nanc; k++)
-      bloom_add(c.pb0, c.pb1, c.pb2, c.pb3, uid_bloom_bit(c.blk[c.p_anc + 2 * k], c.blk[c.p_anc + 2 * k + 1]));
+      bloom_add(c.pb0, c.pb1, c.pb2, c.pb3, uid_bloom_bit(c.p_base[c.p_anc + 2 * k], c.p_base[c.p_anc + 2 * k + 1]));
     bloom_add(c.rb0, c.rb1, c.rb2, c.rb3, uid_bloom_bit(c.rt, c.ri));
     for (uint32_t k = 0; k < c.r_nanc; k++)
-      bloom_add(c.rb0, c.rb1, c.rb2, c.rb3, uid_bloom_bit(c.blk[c.r_anc + 2 * k], c.blk[c.r_anc + 2 * k + 1]));
+      bloom_add(c.rb0, c.rb1, c.rb2, c.rb3, uid_bloom_bit(c.r_base[c.r_anc + 2 * k], c.r_base[c.r_anc + 2 * k + 1]));
   } else {
     c.nent = 0; c.pt = c.pi = c.at = c.ai = c.rt = c.ri = 0xFFFFFFFFu;
     c.t0 = c.t1 = c.t2 = c.t3 = c.t4 = c.t5 = c.t6 = c.t7 = 0xFFFFFFFFu;
@@ -1012,12 +1044,13 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   }
   if (a.amask_ok) {
     uint32_t a_off = 0, a_n = 0;
-    if (valid) anc_of(c, c.aidx, a_off, a_n);
+    const uint32_t* a_base = c.blk;
+    if (valid) anc_of(c, c.aidx, a_base, a_off, a_n);
     const uint32_t n_act = a.n_act;
     for (uint32_t k = 0; k < n_act; k++) {
       const uint32_t qt = uni(a.act[2 * k]), qi = uni(a.act[2 * k + 1]);
       const bool self = valid && c.at == qt && c.ai == qi;
-      const bool hit = self || (valid && a_n && anc_scan(c.blk, a_off, a_n, qt, qi));
+      const bool hit = self || (valid && a_n && anc_scan(a_base, a_off, a_n, qt, qi));
       if (hit) { if (k < 32) am0 |= 1u << k; else am1 |= 1u << (k - 32); }
       if (self) { if (k < 32) as0 |= 1u << k; else as1 |= 1u << (k - 32); }
     }
@@ -1234,7 +1267,7 @@ __device__ __forceinline__ bool var_in(const PCtx& c, uint32_t h, uint32_t qt, u
 }
 
 // One (principal, action, resource) component: kind KC_*, list index j of the request's
-// ancestor-or-self list (j = 0: the UID itself)
+// ancestor-or-self list (j = 0: the UID itself, j > 0: ancestor j - 1)
 __device__ __forceinline__ uint2 key_comp(uint32_t kc, uint32_t j, uint32_t st, uint32_t si, const uint32_t* blk,
                                           uint32_t off) {
   if (kc == KC_WILD) return make_uint2(KW_ANY, KW_ANY);
@@ -1333,9 +1366,11 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   c.pt = hdr(RW_P); c.pi = hdr(RW_P + 1);
   c.at = hdr(RW_A); c.ai = hdr(RW_A + 1);
   c.rt = hdr(RW_R); c.ri = hdr(RW_R + 1);
-  c.p_anc = hdr(RW_PANC); c.p_nanc = hdr(RW_PN);
-  c.r_anc = hdr(RW_RANC); c.r_nanc = hdr(RW_RN);
-  c.a_anc = hdr(RW_AANC); c.a_nanc = hdr(RW_AN);
+  // ancestor counts, and how many of each list (key entities first) the key enumeration takes
+  const uint32_t pn = hdr(RW_PN), rn = hdr(RW_RN), an = hdr(RW_AN);
+  c.p_anc = hdr(RW_PANC); c.p_nanc = pn & AN_COUNT;
+  c.r_anc = hdr(RW_RANC); c.r_nanc = rn & AN_COUNT;
+  c.a_anc = hdr(RW_AANC); c.a_nanc = an & AN_COUNT;
   for (uint32_t h = sl; h < a.n_hot; h += SEG)
     wl.hot[seg][h] = valid ? make_uint2(__builtin_nontemporal_load(row + RW_HDR + 2 * h),
                                         __builtin_nontemporal_load(row + RW_HDR + 2 * h + 1))
@@ -1357,7 +1392,10 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   bool general = false;               // needs the stream kernel (structural equality)
 
   const uint32_t cm = a.combo_mask;
-  const uint32_t nP = 1 + c.p_nanc, nA = 1 + c.a_nanc, nR = 1 + c.r_nanc;
+  // entity components: the UID itself when it is a key entity (AN_SELF), then the key entities
+  // among its ancestors (listed first); none of the other ancestors can complete a key
+  const uint32_t nP = (pn >> 31) + ((pn >> AN_KEYS_SHIFT) & AN_KEYS), nA = (an >> 31) + ((an >> AN_KEYS_SHIFT) & AN_KEYS),
+                 nR = (rn >> 31) + ((rn >> AN_KEYS_SHIFT) & AN_KEYS);
   uint32_t n_keys = 0;
   if (valid)
     for (uint32_t m = cm; m; m &= m - 1) {
@@ -1402,9 +1440,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
             const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
             const uint32_t ip = j % np_, t2 = j / np_, ia = t2 % na_, ir = t2 / na_;
-            kp = key_comp(pkc, ip, c.pt, c.pi, c.blk, c.p_anc);
-            ka = key_comp(akc, ia, c.at, c.ai, c.blk, c.a_anc);
-            kr = key_comp(rkc, ir, c.rt, c.ri, c.blk, c.r_anc);
+            kp = key_comp(pkc, ip + 1 - (pn >> 31), c.pt, c.pi, c.blk, c.p_anc);
+            ka = key_comp(akc, ia + 1 - (an >> 31), c.at, c.ai, c.blk, c.a_anc);
+            kr = key_comp(rkc, ir + 1 - (rn >> 31), c.rt, c.ri, c.blk, c.r_anc);
             w0 = BT_USED | (combo << 16);
             h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
             if (filt_maybe(a.bfilt, a.fmask, h1)) e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5]);
@@ -1684,6 +1722,10 @@ int dev_image_upload(int device, const Image& img, DevImage* out) {
   if ((rc = up(&d.btab, img.btab, d.bytes, s))) return rc;
   if ((rc = up(&d.bfilt, img.bfilt, d.bytes, s))) return rc;
   if ((rc = up(&d.bstream, img.bstream, d.bytes, s))) return rc;
+  if ((rc = up(&d.srows, img.srows, d.bytes, s))) return rc;
+  if ((rc = up(&d.shash, img.shash, d.bytes, s))) return rc;
+  d.n_static = img.n_static();
+  d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
   d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
   d.fmask = (uint32_t)(img.bfilt.size() / 2) - 1;
   d.indexed = img.indexed;
@@ -1706,7 +1748,7 @@ void dev_image_free(DevImage* d) {
   (void)hipSetDevice(d->device);
   for (void* p : {(void*)d->pstream, (void*)d->tier_cend, (void*)d->chunks, (void*)d->cpool, (void*)d->gstr_off,
                   (void*)d->hot, (void*)d->act, (void*)d->gstr_bytes, (void*)d->btab, (void*)d->bfilt,
-                  (void*)d->bstream})
+                  (void*)d->bstream, (void*)d->srows, (void*)d->shash})
     if (p) (void)hipFree(p);
   *d = DevImage();
 }
@@ -1967,6 +2009,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
+  k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
   k.stats = nullptr;
   k.n_dev = nullptr;
   return k;

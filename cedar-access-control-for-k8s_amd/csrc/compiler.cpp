@@ -844,6 +844,85 @@ struct Compiler {
     akeys.push_back(key);
   }
   std::vector<AttrKey> akeys;  // per policy (global index)
+
+  // Static entities (image.h "static entities"): one row per UID (a repeated UID replaces the
+  // earlier entity, as in an EntityMap), attributes as constant-pool records, and per row the
+  // transitive ancestors over the static parent edges (the compiled `in`-closure row, sorted)
+  // and the direct parents, both as [n, (type, id) x n] lists in the constant pool.
+  void statics(const std::vector<EntityIn>& ents) {
+    std::unordered_map<uint64_t, uint32_t> row_of;
+    std::vector<const EntityIn*> src;
+    auto key = [](uint32_t t, uint32_t i) { return ((uint64_t)t << 32) | i; };
+    for (const EntityIn& e : ents) {
+      const uint64_t k = key(intern(e.type), intern(e.id));
+      auto it = row_of.find(k);
+      if (it != row_of.end()) { src[it->second] = &e; continue; }
+      row_of.emplace(k, (uint32_t)src.size());
+      src.push_back(&e);
+    }
+    const uint32_t n = (uint32_t)src.size();
+    if ((uint64_t)n >= ENT_STATIC) throw CedarError("too many static entities");
+    std::vector<uint64_t> uid(n);
+    std::vector<std::vector<uint64_t>> par(n);
+    for (uint32_t r = 0; r < n; r++) {
+      uid[r] = key(intern(src[r]->type), intern(src[r]->id));
+      for (auto& p : src[r]->parents) {
+        const uint64_t k = key(intern(p.first), intern(p.second));
+        if (std::find(par[r].begin(), par[r].end(), k) == par[r].end()) par[r].push_back(k);
+      }
+    }
+    auto put_list = [this](const std::vector<uint64_t>& l) {
+      const uint32_t off = (uint32_t)I.cpool.size();
+      I.cpool.push_back((uint32_t)l.size());
+      for (uint64_t x : l) { I.cpool.push_back((uint32_t)(x >> 32)); I.cpool.push_back((uint32_t)x); }
+      return off;
+    };
+    I.srows.assign((size_t)n * ENT_WORDS, 0);
+    std::vector<uint64_t> anc, stack;
+    std::vector<uint32_t> mark(n, 0xFFFFFFFFu);
+    for (uint32_t r = 0; r < n; r++) {
+      uint32_t w0 = mk_w0(T_REC, mk_ref(SP_CPOOL, 0)), w1 = 0;
+      value_words(src[r]->attrs, w0, w1);
+      anc.clear();
+      stack.assign(1, uid[r]);
+      while (!stack.empty()) {  // closure over the static edges (cycles tolerated: as a walk)
+        const uint64_t cur = stack.back();
+        stack.pop_back();
+        auto it = row_of.find(cur);
+        if (it == row_of.end()) continue;
+        for (uint64_t p : par[it->second]) {
+          auto pr = row_of.find(p);
+          if (pr != row_of.end()) {
+            if (mark[pr->second] == r) continue;
+            mark[pr->second] = r;
+          } else if (std::find(anc.begin(), anc.end(), p) != anc.end()) {
+            continue;
+          }
+          anc.push_back(p);
+          stack.push_back(p);
+        }
+      }
+      std::sort(anc.begin(), anc.end());
+      uint32_t* row = &I.srows[(size_t)r * ENT_WORDS];
+      row[ER_TYPE] = (uint32_t)(uid[r] >> 32);
+      row[ER_ID] = (uint32_t)uid[r];
+      row[ER_ATTR0] = w0;
+      row[ER_ATTR1] = w1;
+      row[ER_ANC] = mk_ref(SP_CPOOL, put_list(anc));
+      row[ER_PAD] = put_list(par[r]);
+    }
+    uint32_t size = 1;
+    while (size < 2 * n + 1) size <<= 1;
+    I.shash.assign((size_t)size * SH_WORDS, 0);
+    for (uint32_t r = 0; r < n; r++) {
+      const uint32_t t = (uint32_t)(uid[r] >> 32), i = (uint32_t)uid[r];
+      uint32_t h = uid_hash(t, i) & (size - 1);
+      while (I.shash[(size_t)h * SH_WORDS + 2]) h = (h + 1) & (size - 1);
+      I.shash[(size_t)h * SH_WORDS] = t;
+      I.shash[(size_t)h * SH_WORDS + 1] = i;
+      I.shash[(size_t)h * SH_WORDS + 2] = r + 1;
+    }
+  }
 };
 
 }  // namespace
@@ -888,6 +967,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   constexpr uint32_t NO_POLICY = 0xFFFFFFFFu;  // a level-1 entry that only carries level-2 keys
   std::vector<std::pair<L1, uint32_t>> r1;
   std::vector<std::pair<L2, uint32_t>> r2;
+  std::vector<uint64_t> kents;  // entity components of the level-1 keys
   r1.reserve(n);
   r2.reserve(2 * (size_t)n);
   for (uint32_t p = 0; p < n; p++) {
@@ -913,7 +993,10 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
       acts.emplace_back(KW_ANY, KW_ANY);
     }
     const uint32_t combo = key_combo(pkc, akc, rkc);
+    if (pkc == KC_ENT) kents.push_back(((uint64_t)pt << 32) | pi);
+    if (rkc == KC_ENT) kents.push_back(((uint64_t)rt << 32) | ri);
     for (auto& a : acts) {
+      if (akc == KC_ENT) kents.push_back(((uint64_t)a.first << 32) | a.second);
       const L1 k{combo, pt, pi, a.first, a.second, rt, ri};
       if ((pt != KW_ANY && pt >= (1u << 28)) || (rt != KW_ANY && rt >= (1u << 28))) throw CedarError("string table too large for the scope index");
       img.combo_mask |= 1u << combo;
@@ -926,6 +1009,9 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   std::sort(r1.begin(), r1.end());
   std::sort(r2.begin(), r2.end());
   r2.erase(std::unique(r2.begin(), r2.end()), r2.end());
+  std::sort(kents.begin(), kents.end());
+  kents.erase(std::unique(kents.begin(), kents.end()), kents.end());
+  img.key_ents = std::move(kents);
   // groups: [begin, end) ranges of one key; level-1 hmask from the level-2 keys under it
   struct G { size_t b, e; uint32_t hmask = 0; };
   std::vector<G> g1, g2;
@@ -1081,7 +1167,8 @@ static std::vector<std::shared_ptr<const std::vector<Policy>>> parse_documents(
   return out;
 }
 
-std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch, ParseCache* cache) {
+std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch, ParseCache* cache,
+                                     const std::vector<EntityIn>* statics) {
   if (tiers.empty()) throw CedarError("at least one policy tier is required");
   if (tiers.size() > 255) throw CedarError("too many tiers");
   auto img = std::make_shared<Image>();
@@ -1188,6 +1275,9 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
   mark("stream");
   build_scope_index(*img, C.akeys);
   mark("scope index");
+  if (statics && !statics->empty()) C.statics(*statics);
+  if (img->shash.empty()) img->shash.assign(SH_WORDS, 0);  // never empty buffers
+  mark("static entities");
   // global string table
   img->gstr_off.clear();
   img->gstr_bytes.clear();
@@ -1235,6 +1325,9 @@ std::vector<uint8_t> Image::serialize() const {
   w.vec(act); w.u32(amask_ok); w.u32(n_atomic);
   w.vec(pstream); w.vec(chunks); w.vec(tier_cend);
   w.vec(btab); w.vec(bfilt); w.vec(bstream); w.u32(indexed); w.u32(combo_mask);
+  w.vec(srows); w.vec(shash);
+  w.u32((uint32_t)key_ents.size());
+  for (uint64_t k : key_ents) w.u64(k);
   w.u32((uint32_t)strings.size());
   for (auto& s : strings) w.str(s);
   w.u32((uint32_t)meta.size());
@@ -1263,6 +1356,15 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     const size_t nb = img->btab.size() / BT_WORDS, nf = img->bfilt.size();
     if (!nb || (nb & (nb - 1)) || nf < 2 || (nf & (nf - 1))) throw CedarError("corrupt image (scope index)");
   }
+  img->srows = r.vec(); img->shash = r.vec();
+  {
+    const size_t ns = img->shash.size() / SH_WORDS;
+    if (!ns || (ns & (ns - 1)) || img->srows.size() % ENT_WORDS || ns <= img->n_static()) throw CedarError("corrupt image (static entities)");
+  }
+  const uint32_t nk = r.u32();
+  r.need((size_t)nk * 8);
+  img->key_ents.resize(nk);
+  for (auto& k : img->key_ents) k = r.u64();
   uint32_t ns = r.u32();
   for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }
   uint32_t nm = r.u32();
@@ -1320,6 +1422,18 @@ void Image::build_lookup() {
       h = (h + 1) & (cap - 1);
     }
     if (!lookup[h]) lookup[h] = ((hv >> 32) << 32) | (i + 1);
+  }
+  sindex.clear();
+  static_targets.clear();
+  for (uint32_t r = 0; r < n_static(); r++) {
+    sindex.emplace(((uint64_t)srows[(size_t)r * ENT_WORDS + ER_TYPE] << 32) | srows[(size_t)r * ENT_WORDS + ER_ID], r);
+    const uint32_t pl = srows[(size_t)r * ENT_WORDS + ER_PAD];  // direct parents [n, pairs]
+    for (uint32_t k = 0; k < cpool[pl]; k++) static_targets.insert(((uint64_t)cpool[pl + 1 + 2 * k] << 32) | cpool[pl + 2 + 2 * k]);
+  }
+  key_bloom.assign(std::max<size_t>(1, key_ents.size() / 4 + 1), 0);  // ~16 bits per key entity
+  for (uint64_t k : key_ents) {
+    const uint64_t h = (k * 0x9E3779B97F4A7C15ull) >> 40;
+    key_bloom[(h >> 6) % key_bloom.size()] |= 1ull << (h & 63);
   }
 }
 

@@ -17,7 +17,9 @@ struct DevImage {
   uint32_t *pstream = nullptr, *tier_cend = nullptr, *chunks = nullptr, *cpool = nullptr, *gstr_off = nullptr, *hot = nullptr;
   uint32_t* act = nullptr;
   uint32_t *btab = nullptr, *bfilt = nullptr, *bstream = nullptr;  // scope index
+  uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
   uint8_t* gstr_bytes = nullptr;
+  uint32_t n_static = 0, smask = 0;
   uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0, n_act = 0, amask_ok = 0, has_bytecode = 1, indexed = 0, bmask = 0, fmask = 0, combo_mask = 0;
   size_t bytes = 0;
 };

@@ -23,22 +23,43 @@ uint32_t request_sid(const Image& img, EncodedRequest& e, std::string_view s);
 namespace enc {
 using namespace cgi;
 
-// memory-form record lookup inside an emitted request block (the device's rec_get, on the host)
-inline bool blk_rec_get(const std::vector<uint32_t>& blk, uint32_t rw0, uint32_t n, uint32_t key, uint32_t& w0,
-                        uint32_t& w1) {
+// memory-form record lookup (the device's rec_get, on the host): the record lives in the emitted
+// request block or, for a static entity's attributes, in the image's constant pool
+inline bool blk_rec_get(const std::vector<uint32_t>& blk, const std::vector<uint32_t>& cpool, uint32_t rw0, uint32_t n,
+                        uint32_t key, uint32_t& w0, uint32_t& w1) {
   const uint32_t off = rw0 & OFF_MASK;
+  const std::vector<uint32_t>& m = ((rw0 & X_MASK) >> SPACE_SHIFT) == SP_CPOOL ? cpool : blk;
   uint32_t lo = 0, hi = n;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (blk[off + 1 + 3 * mid] < key) lo = mid + 1;
+    if (m[off + 1 + 3 * mid] < key) lo = mid + 1;
     else hi = mid;
   }
-  if (lo < n && blk[off + 1 + 3 * lo] == key) {
-    w0 = blk[off + 2 + 3 * lo];
-    w1 = blk[off + 3 + 3 * lo];
+  if (lo < n && m[off + 1 + 3 * lo] == key) {
+    w0 = m[off + 2 + 3 * lo];
+    w1 = m[off + 3 + 3 * lo];
     return true;
   }
   return false;
+}
+
+// [n, (type, id) x n] list at cpool[off] as UID keys
+inline void cpool_uids(const Image& img, uint32_t off, std::vector<uint64_t>& out) {
+  const uint32_t n = img.cpool[off];
+  for (uint32_t k = 0; k < n; k++) out.push_back(((uint64_t)img.cpool[off + 1 + 2 * k] << 32) | img.cpool[off + 2 + 2 * k]);
+}
+
+// Orders an ancestor list for the probe kernel (image.h RW_PN): scope-index key entities first,
+// each part sorted; returns how many lead.
+inline uint32_t order_ancestors(const Image& img, std::vector<uint64_t>& anc) {
+  if (!img.indexed) {
+    std::sort(anc.begin(), anc.end());
+    return 0;
+  }
+  auto mid = std::partition(anc.begin(), anc.end(), [&](uint64_t u) { return img.is_key_ent(u); });
+  std::sort(anc.begin(), mid);
+  std::sort(mid, anc.end());
+  return (uint32_t)(mid - anc.begin());
 }
 
 inline uint32_t mem_tname(uint32_t w0) {
@@ -106,12 +127,60 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     index.add(k);
     table.push_back(e);
   }
-  const uint32_t n = (uint32_t)table.size();
-  blk.resize(RH_WORDS + (size_t)n * ENT_WORDS, 0);
   auto uid_of = [&](const std::pair<std::string_view, std::string_view>& u) {
     const uint32_t t = sid(u.first);
     return std::make_pair(t, sid(u.second));
   };
+  // parent adjacency (ids of parents that exist in the map are followed; absent ones are leaves)
+  std::vector<std::vector<uint64_t>> parents(table.size());
+  for (uint32_t i = 0; i < table.size(); i++) {
+    const uint32_t np = src.n_parents(table[i]);
+    for (uint32_t k = 0; k < np; k++) {
+      const auto u = uid_of(src.parent(table[i], k));
+      const uint64_t key = uid_key(u.first, u.second);
+      if (std::find(parents[i].begin(), parents[i].end(), key) == parents[i].end()) parents[i].push_back(key);
+    }
+  }
+  // Static entities merged into the map (image.h "static entities"). A table entity that is also
+  // static gains the static parents. A static entity outside the table keeps its compiled closure
+  // row, which is its merged ancestry unless that row names a table entity with parents of its own
+  // (the request extends the hierarchy above it): such static entities join the table (rare: the
+  // SAR path gives only the principal parents, and no static edge names a principal).
+  const bool has_static = img.n_static() != 0;
+  constexpr uint32_t FROM_STATIC = 0x80000000u;  // table slot holding static row (slot & ~FROM_STATIC)
+  if (has_static) {
+    const uint32_t n0 = (uint32_t)table.size();
+    std::vector<uint64_t> extended;  // table entities with parents that some static edge names
+    for (uint32_t i = 0; i < n0; i++)
+      if (!parents[i].empty() && img.is_static_target(index.keys[i])) extended.push_back(index.keys[i]);
+    if (!extended.empty()) {
+      std::sort(extended.begin(), extended.end());
+      std::vector<uint64_t> cl;
+      for (uint32_t s = 0; s < img.n_static(); s++) {
+        const uint32_t* r = &img.srows[(size_t)s * ENT_WORDS];
+        const uint64_t k = uid_key(r[ER_TYPE], r[ER_ID]);
+        if (index.find(k) >= 0) continue;
+        cl.clear();
+        cpool_uids(img, r[ER_ANC] & OFF_MASK, cl);
+        bool hit = false;
+        for (size_t a = 0; a < cl.size() && !hit; a++) hit = std::binary_search(extended.begin(), extended.end(), cl[a]);
+        if (!hit) continue;
+        index.add(k);
+        table.push_back(FROM_STATIC | s);
+        parents.emplace_back();
+      }
+    }
+    for (uint32_t i = 0; i < table.size(); i++) {
+      const int32_t s = (table[i] & FROM_STATIC) ? (int32_t)(table[i] & ~FROM_STATIC) : img.static_row(index.keys[i]);
+      if (s < 0) continue;
+      std::vector<uint64_t> sp;
+      cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_PAD], sp);
+      for (const uint64_t p : sp)
+        if (std::find(parents[i].begin(), parents[i].end(), p) == parents[i].end()) parents[i].push_back(p);
+    }
+  }
+  const uint32_t n = (uint32_t)table.size();
+  blk.resize(RH_WORDS + (size_t)n * ENT_WORDS, 0);
   const auto pu = uid_of(src.principal()), au = uid_of(src.action()), ru = uid_of(src.resource());
   for (auto* u : {&pu, &au, &ru})
     if (u->first > X_MASK) throw CedarError("string table overflow");
@@ -119,9 +188,12 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   blk[RH_P] = mk_w0(T_ENT, pu.first); blk[RH_P + 1] = pu.second;
   blk[RH_A] = mk_w0(T_ENT, au.first); blk[RH_A + 1] = au.second;
   blk[RH_R] = mk_w0(T_ENT, ru.first); blk[RH_R + 1] = ru.second;
+  // entity index of a UID: the request's table, else the image's static entities (ENT_STATIC)
   auto idx_of = [&](const std::pair<uint32_t, uint32_t>& u) {
     const int32_t i = index.find(uid_key(u.first, u.second));
-    return i < 0 ? NO_ENT : (uint32_t)i;
+    if (i >= 0) return (uint32_t)i;
+    const int32_t s = has_static ? img.static_row(uid_key(u.first, u.second)) : -1;
+    return s < 0 ? NO_ENT : (ENT_STATIC | (uint32_t)s);
   };
   blk[RH_PIDX] = idx_of(pu);
   blk[RH_AIDX] = idx_of(au);
@@ -131,44 +203,53 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     src.emit_ctx(blk, img, E, w0, w1);
     blk[RH_CTX] = w0; blk[RH_CTX + 1] = w1;
   }
-  // parent adjacency (ids of parents that exist in the map are followed; absent ones are leaves)
-  std::vector<std::vector<uint64_t>> parents(n);
-  for (uint32_t i = 0; i < n; i++) {
-    const uint32_t np = src.n_parents(table[i]);
-    for (uint32_t k = 0; k < np; k++) {
-      const auto u = uid_of(src.parent(table[i], k));
-      const uint64_t key = uid_key(u.first, u.second);
-      if (std::find(parents[i].begin(), parents[i].end(), key) == parents[i].end()) parents[i].push_back(key);
-    }
-  }
-  std::vector<uint64_t> anc;
-  std::vector<uint32_t> stack;
+  std::vector<uint64_t> anc, nodes, cl;
+  std::vector<uint32_t> n_key(n, 0);
   std::unordered_set<uint64_t> seen_big;
   for (uint32_t i = 0; i < n; i++) {
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_TYPE] = (uint32_t)(index.keys[i] >> 32);
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ID] = (uint32_t)index.keys[i];
     uint32_t w0, w1;
-    src.emit_attrs(table[i], blk, img, E, w0, w1);
+    if (table[i] & FROM_STATIC) {  // the static entity's attributes (constant-pool record)
+      w0 = img.srows[(size_t)(table[i] & ~FROM_STATIC) * ENT_WORDS + ER_ATTR0];
+      w1 = img.srows[(size_t)(table[i] & ~FROM_STATIC) * ENT_WORDS + ER_ATTR1];
+    } else {
+      src.emit_attrs(table[i], blk, img, E, w0, w1);
+    }
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ATTR0] = w0;
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ATTR1] = w1;
-    // transitive ancestors (through the map; cycles tolerated)
+    // transitive ancestors (through the merged map; cycles tolerated)
     anc.clear();
     seen_big.clear();
-    stack.assign(1, i);
-    while (!stack.empty()) {
-      const uint32_t cur = stack.back();
-      stack.pop_back();
-      for (const uint64_t p : parents[cur]) {
-        const bool seen = anc.size() <= 64 ? std::find(anc.begin(), anc.end(), p) != anc.end() : seen_big.count(p) > 0;
-        if (seen) continue;
-        anc.push_back(p);
-        if (anc.size() == 65) seen_big.insert(anc.begin(), anc.end());  // switch to hashing
-        else if (anc.size() > 65) seen_big.insert(p);
-        const int32_t at = index.find(p);
-        if (at >= 0) stack.push_back((uint32_t)at);
+    auto seen = [&](uint64_t p) {
+      return anc.size() <= 64 ? std::find(anc.begin(), anc.end(), p) != anc.end() : seen_big.count(p) > 0;
+    };
+    auto add = [&](uint64_t p) {
+      anc.push_back(p);
+      if (anc.size() == 65) seen_big.insert(anc.begin(), anc.end());  // switch to hashing
+      else if (anc.size() > 65) seen_big.insert(p);
+    };
+    nodes.assign(1, index.keys[i]);  // table entities still to expand
+    while (!nodes.empty()) {
+      const int32_t at = index.find(nodes.back());
+      nodes.pop_back();
+      for (const uint64_t p : parents[(uint32_t)at]) {
+        if (seen(p)) continue;
+        add(p);
+        if (index.find(p) >= 0) { nodes.push_back(p); continue; }
+        const int32_t s = has_static ? img.static_row(p) : -1;
+        if (s < 0) continue;  // in neither map: no parents
+        // a static entity outside the table: its compiled closure row
+        cl.clear();
+        cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_ANC] & OFF_MASK, cl);
+        for (const uint64_t q : cl) {
+          if (seen(q)) continue;
+          add(q);
+          if (index.find(q) >= 0) nodes.push_back(q);  // a table entity a static edge names
+        }
       }
     }
-    std::sort(anc.begin(), anc.end());
+    n_key[i] = order_ancestors(img, anc);
     const uint32_t off = (uint32_t)blk.size();
     blk.push_back((uint32_t)anc.size());
     for (const uint64_t a : anc) { blk.push_back((uint32_t)(a >> 32)); blk.push_back((uint32_t)a); }
@@ -180,21 +261,36 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   row[RW_P] = pu.first; row[RW_P + 1] = pu.second;
   row[RW_A] = au.first; row[RW_A + 1] = au.second;
   row[RW_R] = ru.first; row[RW_R + 1] = ru.second;
-  auto anc_into = [&](uint32_t idx, uint32_t w_off, uint32_t w_n) {
-    if (idx == NO_ENT) return;
-    const uint32_t ref = blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;
-    row[w_off] = ref + 1;
-    row[w_n] = blk[ref];
+  // ancestor lists of P / A / R (a static entity outside the table: its closure row, copied into
+  // the block so the probe kernel reads every list block-relative), with the key counts
+  auto anc_into = [&](uint32_t idx, const std::pair<uint32_t, uint32_t>& self, uint32_t w_off, uint32_t w_n) {
+    uint32_t cnt = 0, keys = 0;
+    if (idx != NO_ENT && (idx & ENT_STATIC)) {
+      anc.clear();
+      cpool_uids(img, img.srows[(size_t)(idx & ~ENT_STATIC) * ENT_WORDS + ER_ANC] & OFF_MASK, anc);
+      keys = order_ancestors(img, anc);
+      row[w_off] = (uint32_t)blk.size() + 1;
+      blk.push_back((uint32_t)anc.size());
+      for (const uint64_t a : anc) { blk.push_back((uint32_t)(a >> 32)); blk.push_back((uint32_t)a); }
+      cnt = (uint32_t)anc.size();
+    } else if (idx != NO_ENT) {
+      const uint32_t ref = blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;
+      row[w_off] = ref + 1;
+      cnt = blk[ref];
+      keys = n_key[idx];
+    }
+    if (cnt > AN_COUNT || keys > AN_KEYS) throw CedarError("entity has too many ancestors for the device row format");
+    row[w_n] = cnt | (keys << AN_KEYS_SHIFT) | (img.is_key_ent(uid_key(self.first, self.second)) ? AN_SELF : 0u);
   };
-  anc_into(blk[RH_PIDX], RW_PANC, RW_PN);
-  anc_into(blk[RH_RIDX], RW_RANC, RW_RN);
-  anc_into(blk[RH_AIDX], RW_AANC, RW_AN);
+  anc_into(blk[RH_PIDX], pu, RW_PANC, RW_PN);
+  anc_into(blk[RH_RIDX], ru, RW_RANC, RW_RN);
+  anc_into(blk[RH_AIDX], au, RW_AANC, RW_AN);
   // action masks over the image action table, as the probe kernel tests scopes against them
   row[RW_ASELF] = 0xFFFFFFFFu;
   if (img.amask_ok) {
     uint64_t am = 0;
     const uint32_t n_act = (uint32_t)img.act.size() / 2;
-    const uint32_t aoff = row[RW_AANC], an = row[RW_AN];
+    const uint32_t aoff = row[RW_AANC], an = row[RW_AN] & AN_COUNT;
     for (uint32_t k = 0; k < n_act; k++) {
       const uint32_t qt = img.act[2 * k], qi = img.act[2 * k + 1];
       const bool self = au.first == qt && au.second == qi;
@@ -220,12 +316,14 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       const bool last = j + 1 == depth;
       if (tag == T_ENT) {
         const uint32_t t = w0 & X_MASK, id = w1;
-        const int32_t at = index.find(uid_key(t, id));
-        if (at < 0) { code = E_ENTITY_MISSING; et = t; ei = id; fin = last; break; }
-        const uint32_t* er = &blk[RH_WORDS + (size_t)at * ENT_WORDS];
-        if (!blk_rec_get(blk, er[ER_ATTR0], er[ER_ATTR1], key, w0, w1)) { code = E_ATTR_ENTITY; k = key; et = t; ei = id; fin = last; }
+        const uint32_t at = idx_of({t, id});
+        if (at == NO_ENT) { code = E_ENTITY_MISSING; et = t; ei = id; fin = last; break; }
+        const uint32_t* er = (at & ENT_STATIC) ? &img.srows[(size_t)(at & ~ENT_STATIC) * ENT_WORDS]
+                                               : &blk[RH_WORDS + (size_t)at * ENT_WORDS];
+        const uint32_t a0 = er[ER_ATTR0], a1 = er[ER_ATTR1];
+        if (!blk_rec_get(blk, img.cpool, a0, a1, key, w0, w1)) { code = E_ATTR_ENTITY; k = key; et = t; ei = id; fin = last; }
       } else if (tag == T_REC) {
-        if (!blk_rec_get(blk, w0, w1, key, w0, w1)) { code = E_ATTR_RECORD; k = key; fin = last; }
+        if (!blk_rec_get(blk, img.cpool, w0, w1, key, w0, w1)) { code = E_ATTR_RECORD; k = key; fin = last; }
       } else {
         code = E_TYPE;
         aux = TN_ENTITY_OR_RECORD | (mem_tname(w0) << 8);

@@ -97,28 +97,30 @@ static std::pair<std::string, std::string> uid_from_json(const JVal& j) {
   return {x.str_or("type"), x.str_or("id")};
 }
 
+void decode_json_entities(const JVal& es, std::vector<EntityIn>& ents) {
+  if (es.t != JVal::Arr) throw CedarError("\"entities\" must be an array");
+  for (auto& e : es.arr) {
+    EntityIn ei;
+    const JVal* uid = e.get("uid");
+    if (!uid) throw CedarError("entity without uid");
+    auto u = uid_from_json(*uid);
+    ei.type = u.first; ei.id = u.second;
+    const JVal* at = e.get("attrs");
+    if (at) ei.attrs = hval_from_json(*at);
+    else ei.attrs.k = VK::Rec;
+    if (ei.attrs.k != VK::Rec) throw CedarError("entity attrs must be an object");
+    const JVal* ps = e.get("parents");
+    if (ps) for (auto& p : ps->arr) ei.parents.push_back(uid_from_json(p));
+    ents.push_back(std::move(ei));
+  }
+}
+
 void decode_json_item(const JVal& item, std::vector<EntityIn>& ents, RequestIn& req) {
   const JVal* es = item.get("entities");
   const JVal* rq = item.get("request");
   if (!rq || rq->t != JVal::Obj) throw CedarError("item needs a \"request\" object");
   ents.clear();
-  if (es) {
-    if (es->t != JVal::Arr) throw CedarError("\"entities\" must be an array");
-    for (auto& e : es->arr) {
-      EntityIn ei;
-      const JVal* uid = e.get("uid");
-      if (!uid) throw CedarError("entity without uid");
-      auto u = uid_from_json(*uid);
-      ei.type = u.first; ei.id = u.second;
-      const JVal* at = e.get("attrs");
-      if (at) ei.attrs = hval_from_json(*at);
-      else ei.attrs.k = VK::Rec;
-      if (ei.attrs.k != VK::Rec) throw CedarError("entity attrs must be an object");
-      const JVal* ps = e.get("parents");
-      if (ps) for (auto& p : ps->arr) ei.parents.push_back(uid_from_json(p));
-      ents.push_back(std::move(ei));
-    }
-  }
+  if (es) decode_json_entities(*es, ents);
   const JVal* p = rq->get("principal");
   const JVal* a = rq->get("action");
   const JVal* r = rq->get("resource");

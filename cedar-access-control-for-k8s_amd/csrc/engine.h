@@ -1,5 +1,6 @@
 // Host engine: compiled image, batch encoder, result renderer, device bridge.
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <cstring>
@@ -8,6 +9,7 @@
 #include <string>
 #include <string_view>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "cedar.h"
@@ -39,6 +41,29 @@ struct Image {
   std::vector<uint32_t> btab, bfilt, bstream;  // bfilt: key filter, 2 words per block
   uint32_t indexed = 0;
   uint32_t combo_mask = 0;  // level-1 key combos in use (bit key_combo(..))
+  // entity components of the scope index's level-1 keys, (type sid << 32 | id sid), sorted: the
+  // encoder lists a request's ancestors that are among them first (image.h RW_PN)
+  std::vector<uint64_t> key_ents;
+  // static entities (image.h "static entities"): device rows and UID hash; closure rows and
+  // direct-parent lists in cpool ([n, (type, id) x n]; ER_ANC / ER_PAD offsets)
+  std::vector<uint32_t> srows, shash;
+  uint32_t n_static() const { return (uint32_t)srows.size() / cgi::ENT_WORDS; }
+  // host lookups, rebuilt by build_lookup
+  std::unordered_map<uint64_t, uint32_t> sindex;  // UID key -> static row
+  std::unordered_set<uint64_t> static_targets;    // UIDs some static entity names as a parent
+  std::vector<uint64_t> key_bloom;                // 1-bit-per-hash prefilter over key_ents
+  bool is_static_target(uint64_t uid) const { return !static_targets.empty() && static_targets.count(uid) > 0; }
+  int32_t static_row(uint64_t uid) const {
+    if (sindex.empty()) return -1;
+    auto it = sindex.find(uid);
+    return it == sindex.end() ? -1 : (int32_t)it->second;
+  }
+  bool is_key_ent(uint64_t uid) const {
+    if (key_ents.empty()) return false;
+    const uint64_t h = (uid * 0x9E3779B97F4A7C15ull) >> 40;
+    if (!((key_bloom[(h >> 6) % key_bloom.size()] >> (h & 63)) & 1)) return false;
+    return std::binary_search(key_ents.begin(), key_ents.end(), uid);
+  }
   std::vector<uint8_t> gstr_bytes;
   std::vector<PolicyMeta> meta;
   std::vector<std::string> strings;
@@ -111,17 +136,18 @@ struct ParseCache {
   uint64_t hits = 0, misses = 0;  // over the last build
 };
 
-// Compiles the tiers. With a cache, unseen documents are parsed on worker threads and reused
-// next time; the image is byte-identical to a build without the cache.
-std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch,
-                                     ParseCache* cache = nullptr);
-
 // Entity input for the encoder (already decoded from JSON or built by the k8s model).
 struct EntityIn {
   std::string type, id;
   HVal attrs;  // Record
   std::vector<std::pair<std::string, std::string>> parents;
 };
+
+// Compiles the tiers. With a cache, unseen documents are parsed on worker threads and reused
+// next time; the image is byte-identical to a build without the cache. `statics`: the image's
+// static entities (cg_compiler_set_entities).
+std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch,
+                                     ParseCache* cache = nullptr, const std::vector<EntityIn>* statics = nullptr);
 struct RequestIn {
   std::pair<std::string, std::string> principal, action, resource;
   HVal context;  // Record
@@ -202,5 +228,7 @@ struct Batch {
 
 // Parses a Cedar-JSON request item {"entities": [...], "request": {...}} into encoder input.
 void decode_json_item(const JVal& item, std::vector<EntityIn>& ents, RequestIn& req);
+// Parses a Cedar-JSON entity array.
+void decode_json_entities(const JVal& arr, std::vector<EntityIn>& ents);
 
 }  // namespace cg

@@ -318,6 +318,6 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 4;
+constexpr uint32_t IMG_VERSION = 5;
 
 }  // namespace cgi

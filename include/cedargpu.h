@@ -59,6 +59,15 @@ int cg_compiler_add_document(cg_compiler* c, const char* filename, const char* t
  * AST (cedar.NewPolicyFromAST, e.g. allow-all-admission) whose Position is the zero value. */
 int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* filename, const char* text,
                            size_t len, int zero_position);
+/* Sets the image's static entities: a JSON array of Cedar entities ({"uid":{"type","id"},
+ * "attrs":{...},"parents":[...]}) such as a group / namespace hierarchy that the requests' EntityMaps
+ * do not carry (the reference's SAR path gives groups no parents, internal/server/entities/
+ * user.go:40-54; a deeper hierarchy, like store_test.go:35-40's user -> group edge, needs a static
+ * source). Every evaluation then sees the request's EntityMap merged with them: a static entity the
+ * request lacks is present; for a UID in both, the request's attributes and the union of both parent
+ * lists. The compiler builds each static entity's transitive `in`-closure row into the image.
+ * Replaces any earlier set; an empty array (len 0) clears it. */
+int cg_compiler_set_entities(cg_compiler* c, const char* json, size_t len);
 /* Drops the tiers added so far but keeps the compiler's parse cache: the incremental rebuild after
  * a store change (a CRD added / updated / removed, crd.go:45-118; a directory re-read,
  * directory.go:41-82; an AVP sync, verified_permissions.go:58-100) re-adds every document and

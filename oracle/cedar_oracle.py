@@ -798,6 +798,25 @@ class Request:
     context: Record = field(default_factory=Record)
 
 
+def merge_static_entities(em: EntityMap, static: Optional[EntityMap]) -> EntityMap:
+    """The EntityMap a request is evaluated against when the policy image carries static entities
+    (a group / namespace hierarchy the request does not hold; cedargpu.h cg_compiler_set_entities).
+    This is what a maintainer merging a static entity source into the map built by
+    RecordToCedarResource (authorizer.go:89-111) before TieredPolicyStores.IsAuthorized
+    (store.go:25) would hand cedar-go: the request's entities, plus every static entity the request
+    lacks; for a UID in both, the request's attributes and the union of both parent lists."""
+    if not static:
+        return em
+    out = dict(em)
+    for uid, se in static.items():
+        e = out.get(uid)
+        if e is None:
+            out[uid] = se
+        else:
+            out[uid] = Entity(uid, e.attrs, tuple(dict.fromkeys(tuple(e.parents) + tuple(se.parents))))
+    return out
+
+
 def ancestors(em: EntityMap, uid: EntityUID) -> set:
     seen = set()
     stack = [uid]

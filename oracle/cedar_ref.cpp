@@ -1083,10 +1083,16 @@ bool like_match(const std::string& s, const std::vector<Piece>& pat, size_t si, 
 struct Evaluator {
   const Item& it;
   Arena& A;
+  const Item* st = nullptr;  // static entities of the image, merged into the map (may be null)
 
+  // The merged EntityMap (cedar_oracle.merge_static_entities): the request's entity, else the
+  // static one; a UID in both keeps the request's attributes and unites both parent lists.
   const Entity* find(const Val& u) const {
     auto f = it.ents.find(KV{*u.et, *u.s});
-    return f == it.ents.end() ? nullptr : &f->second;
+    if (f != it.ents.end()) return &f->second;
+    if (!st) return nullptr;
+    auto g = st->ents.find(KV{*u.et, *u.s});
+    return g == st->ents.end() ? nullptr : &g->second;
   }
   // X in E: X == E, or E is reachable through the entity map's parent edges (absent entities have
   // no parents). Early-exit depth-first walk with a visited list, as cedar-go's entityInOne.
@@ -1096,15 +1102,22 @@ struct Evaluator {
     todo.clear();
     known.clear();
     KV cur{*a.et, *a.s};
+    auto visit = [&](const std::vector<KV>& ps) {
+      for (auto& p : ps) {
+        if (std::find(known.begin(), known.end(), p) != known.end()) continue;
+        for (size_t k = 0; k < nt; k++) if (p == targets[k]) return true;
+        known.push_back(p);
+        todo.push_back(p);
+      }
+      return false;
+    };
     for (;;) {
       auto f = it.ents.find(cur);
-      if (f != it.ents.end())
-        for (auto& p : f->second.parents) {
-          if (std::find(known.begin(), known.end(), p) != known.end()) continue;
-          for (size_t k = 0; k < nt; k++) if (p == targets[k]) return true;
-          known.push_back(p);
-          todo.push_back(p);
-        }
+      if (f != it.ents.end() && visit(f->second.parents)) return true;
+      if (st) {
+        auto g = st->ents.find(cur);
+        if (g != st->ents.end() && visit(g->second.parents)) return true;
+      }
       if (todo.empty()) return false;
       cur = todo.back();
       todo.pop_back();
@@ -1391,8 +1404,8 @@ void is_authorized(const Tier& t, Evaluator& ev, Result& r) {
   else { r.allow = 0; r.reasons.clear(); }
 }
 
-void tiered(const std::vector<Tier>& tiers, const Item& it, Arena& A, Result& r) {
-  Evaluator ev{it, A};
+void tiered(const std::vector<Tier>& tiers, const Item& it, Arena& A, Result& r, const Item* statics) {
+  Evaluator ev{it, A, statics};
   r = Result();
   for (uint32_t t = 0; t < tiers.size(); t++) {
     A.clear();
@@ -1458,6 +1471,7 @@ struct Set {
   std::vector<Tier> tiers;
   std::string err;
   std::vector<std::unique_ptr<Item>> items;  // loaded items (bench / batch)
+  std::unique_ptr<Item> statics;             // static entities (cref_set_entities)
 };
 
 }  // namespace cref
@@ -1507,6 +1521,29 @@ int cref_add_policy(cref_set* s, const char* policy_id, const char* filename, co
   return add_doc(reinterpret_cast<Set*>(s), filename, text, len, nullptr, nullptr, policy_id, zero_position);
 }
 
+// Static entities (a JSON entity array) merged into every item's EntityMap; empty: none.
+int cref_set_entities(cref_set* s0, const char* json, size_t len) {
+  Set* s = reinterpret_cast<Set*>(s0);
+  try {
+    s->statics.reset();
+    if (!len) return 0;
+    std::string item = "{\"entities\":" + std::string(json, len) +
+                       ",\"request\":{\"principal\":{\"type\":\"_\",\"id\":\"\"},\"action\":{\"type\":\"_\",\"id\":\"\"},"
+                       "\"resource\":{\"type\":\"_\",\"id\":\"\"}}}";
+    J j = parse_json(item.data(), item.size());
+    std::unique_ptr<Item> it(new Item());
+    item_from_json(j, *it);
+    s->statics = std::move(it);
+  } catch (std::exception& e) {
+    s->err = e.what();
+    return -1;
+  } catch (EvalError& e) {
+    s->err = e.msg;
+    return -1;
+  }
+  return 0;
+}
+
 // Loads a JSON array of {"entities":[...],"request":{...}} items (replacing earlier ones).
 int cref_load_items(cref_set* s0, const char* json, size_t len, uint32_t* n) {
   Set* s = reinterpret_cast<Set*>(s0);
@@ -1544,7 +1581,7 @@ int cref_eval(cref_set* s0, int threads, char** out, size_t* out_len) {
     for (;;) {
       size_t k = next.fetch_add(1);
       if (k >= n) break;
-      tiered(s->tiers, *s->items[k], A, r);
+      tiered(s->tiers, *s->items[k], A, r, s->statics.get());
       std::string& o = lines[k];
       o = std::to_string(r.allow) + "\t" + std::to_string(r.tier) + "\t";
       diag_json(s->tiers[r.tier], r, false, o);
@@ -1588,7 +1625,7 @@ int cref_bench(cref_set* s0, int threads, double seconds, uint64_t* decisions, d
     size_t k = (size_t)w % n;
     while (std::chrono::steady_clock::now() < deadline) {
       for (int rep = 0; rep < 16; rep++) {
-        tiered(s->tiers, *s->items[k], A, r);
+        tiered(s->tiers, *s->items[k], A, r, s->statics.get());
         acc += (uint32_t)r.allow + (uint32_t)r.reasons.size();
         done++;
         k += (size_t)threads;

@@ -27,6 +27,7 @@ def lib():
         L.cref_add_tier.argtypes = [P]
         L.cref_add_document.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_char_p]
         L.cref_add_policy.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_int]
+        L.cref_set_entities.argtypes = [P, ctypes.c_char_p, sz]
         L.cref_load_items.argtypes = [P, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint32)]
         L.cref_eval.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.cref_bench.argtypes = [P, ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_uint64),
@@ -59,6 +60,11 @@ class RefPolicySet:
         if rc != 0:
             raise RefError(lib().cref_last_error(self.h).decode(errors="replace"))
 
+    def set_entities(self, entities_json: str):
+        """Static entities merged into every item's EntityMap (cedar_oracle.merge_static_entities)."""
+        b = entities_json.encode() if entities_json else b""
+        self._chk(lib().cref_set_entities(self.h, b, len(b)))
+
     def add_tier(self):
         self._chk(lib().cref_add_tier(self.h))
 
@@ -71,9 +77,12 @@ class RefPolicySet:
         self._chk(lib().cref_add_policy(self.h, policy_id.encode(), filename.encode(), b, len(b), int(zero_position)))
 
     @classmethod
-    def from_stores(cls, stores):
-        """From cedargpu store objects (their `documents()` lists), one tier per store."""
+    def from_stores(cls, stores, entities=None):
+        """From cedargpu store objects (their `documents()` lists), one tier per store; `entities`:
+        static entities (Cedar JSON list) merged into every EntityMap."""
         s = cls()
+        if entities:
+            s.set_entities(json.dumps(entities))
         for st in stores:
             s.add_tier()
             for d in st.documents():

@@ -18,6 +18,7 @@ import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
+import cedar_oracle as _co
 from cedar_oracle import (CSet, Diagnostic, Entity, EntityMap, EntityUID, IPAddr, Long, PolicySet, Record,
                           Request, parse_policies, tiered_is_authorized)
 
@@ -197,8 +198,9 @@ def diagnostic_to_reason(d: Diagnostic) -> str:
     return d.to_go_json()
 
 
-def authorize(tiers: List[PolicySet], a: Attributes, stores_loaded: bool = True) -> Tuple[int, str]:
-    """cedarWebhookAuthorizer.Authorize (authorizer.go:36-85). Returns (decision, reason)."""
+def authorize(tiers: List[PolicySet], a: Attributes, stores_loaded: bool = True, static=None) -> Tuple[int, str]:
+    """cedarWebhookAuthorizer.Authorize (authorizer.go:36-85). Returns (decision, reason).
+    `static`: an EntityMap of static entities merged into the request's (merge_static_entities)."""
     name = a.user.name
     if name == CEDAR_AUTHORIZER_IDENTITY and a.is_read_only() and a.api_group == "cedar.k8s.aws" and a.resource == "policies":
         return DECISION_ALLOW, "cedar authorizer is always allowed to access policies"
@@ -209,7 +211,7 @@ def authorize(tiers: List[PolicySet], a: Attributes, stores_loaded: bool = True)
     if not stores_loaded:
         return DECISION_NO_OPINION, ""
     em, req = record_to_cedar_resource(a)
-    ok, diag, _ = tiered_is_authorized(tiers, em, req)
+    ok, diag, _ = tiered_is_authorized(tiers, _co.merge_static_entities(em, static), req)
     if ok:
         return DECISION_ALLOW, diagnostic_to_reason(diag)
     if diag.reasons:

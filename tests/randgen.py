@@ -19,9 +19,15 @@ def q(s):
     return json.dumps(s)
 
 
+# groups only the image's static entities know (static mode)
+SGROUPS = [f"s{i}" for i in range(4)]
+
+
 class Gen:
-    def __init__(self, seed):
+    def __init__(self, seed, static=False):
         self.r = random.Random(seed)
+        self.static = static
+        self.groups = GROUPS + SGROUPS if static else GROUPS
 
     def pick(self, xs):
         return self.r.choice(xs)
@@ -45,7 +51,7 @@ class Gen:
     def ent_e(self, d=0):
         r = self.r
         return r.choice([lambda: "principal", lambda: "resource", lambda: "resource.owner", lambda: "action",
-                         lambda: f'k8s::Group::{q(r.choice(GROUPS))}', lambda: f'k8s::User::{q(r.choice(USERS))}'])()
+                         lambda: f'k8s::Group::{q(r.choice(self.groups))}', lambda: f'k8s::User::{q(r.choice(USERS))}'])()
 
     def set_e(self, d=0):
         r = self.r
@@ -53,7 +59,7 @@ class Gen:
                          lambda: "[" + ", ".join(q(x) for x in r.sample(TAGS, r.randint(0, 3))) + "]",
                          lambda: f"[{self.str_e(d + 1)}, {q(r.choice(TAGS))}]",
                          lambda: f"[{self.long_e(d + 1)}, 3]",
-                         lambda: "[" + ", ".join(f"k8s::Group::{q(g)}" for g in r.sample(GROUPS, 2)) + "]",
+                         lambda: "[" + ", ".join(f"k8s::Group::{q(g)}" for g in r.sample(self.groups, 2)) + "]",
                          lambda: f'[{{"key": {q(r.choice(["k0", "k1"]))}, "value": {self.str_e(d + 1)}}}]',
                          lambda: "principal.info.c"])()
 
@@ -65,10 +71,10 @@ class Gen:
         leaves = [
             lambda: "principal.active", lambda: "context.flag", lambda: r.choice(["true", "false"]),
             lambda: f"{r.choice(['principal', 'resource', 'context', 'principal.info'])} has {r.choice(['name', 'namespace', 'age', 'tags', 'a', 'x', 'info', 'owner'])}",
-            lambda: f"{self.ent_e(d)} in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: f"{self.ent_e(d)} in k8s::Group::{q(r.choice(self.groups))}",
             lambda: f"{self.ent_e(d)} in {self.set_e(d)}",
             lambda: f"{self.ent_e(d)} is {r.choice(['k8s::User', 'k8s::Group', 'k8s::Resource'])}",
-            lambda: f"principal is k8s::User in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: f"principal is k8s::User in k8s::Group::{q(r.choice(self.groups))}",
             lambda: f"{self.long_e(d)} {r.choice(['<', '<=', '>', '>='])} {self.long_e(d)}",
             lambda: f"{self.str_e(d)} {r.choice(['==', '!='])} {self.str_e(d)}",
             lambda: f"{self.any_e(d)} {r.choice(['==', '!='])} {self.any_e(d)}",
@@ -102,9 +108,9 @@ class Gen:
         if t < 0.55:
             return f"{var} is {r.choice(['k8s::User', 'k8s::Resource', 'k8s::Group'])}"
         if t < 0.7:
-            return f"{var} in k8s::Group::{q(r.choice(GROUPS))}"
+            return f"{var} in k8s::Group::{q(r.choice(self.groups))}"
         if t < 0.85:
-            return f"{var} is k8s::User in k8s::Group::{q(r.choice(GROUPS))}"
+            return f"{var} is k8s::User in k8s::Group::{q(r.choice(self.groups))}"
         if var == "principal":
             return f"principal == k8s::User::{q(r.choice(USERS))}"
         return f"resource == k8s::Resource::{q('r' + str(r.randint(0, 3)))}"
@@ -145,7 +151,7 @@ class Gen:
             lambda: f"principal.age {r.choice(['<', '<=', '>', '>='])} {r.randint(-5, 50)}",
             lambda: "resource.name == principal.name",
             lambda: f'{q(r.choice(USERS))} == principal.name',
-            lambda: f"principal in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: f"principal in k8s::Group::{q(r.choice(self.groups))}",
             lambda: f"principal is {r.choice(['k8s::User', 'k8s::Group'])}",
             lambda: "[" + ", ".join(q(x) for x in r.sample(TAGS + USERS, 3)) + "].contains(resource.name)",
             lambda: f"principal.tags.contains({q(r.choice(TAGS))})",
@@ -162,9 +168,9 @@ class Gen:
             lambda: f"context.x {r.choice(['<', '>'])} {r.randint(0, 40)}",
             lambda: "context.flag", lambda: "context has s && context.s == principal.name",
             # entity set membership, is-in, var == literal, constants
-            lambda: "resource in [" + ", ".join(f"k8s::Group::{q(g)}" for g in r.sample(GROUPS, 2)) + "]",
-            lambda: f"principal in [k8s::Group::{q(r.choice(GROUPS))}, k8s::User::{q(r.choice(USERS))}]",
-            lambda: f"principal is k8s::User in k8s::Group::{q(r.choice(GROUPS))}",
+            lambda: "resource in [" + ", ".join(f"k8s::Group::{q(g)}" for g in r.sample(self.groups, 2)) + "]",
+            lambda: f"principal in [k8s::Group::{q(r.choice(self.groups))}, k8s::User::{q(r.choice(USERS))}]",
+            lambda: f"principal is k8s::User in k8s::Group::{q(r.choice(self.groups))}",
             lambda: f'resource == k8s::Resource::{q("r" + str(r.randint(0, 3)))}',
             lambda: f'principal == k8s::User::{q(r.choice(USERS))}',
             lambda: r.choice(["true", "false"]),
@@ -237,17 +243,45 @@ class Gen:
             a["nick"] = r.choice(USERS[:3] + TAGS[:2])
         return a
 
+    def static_entities(self):
+        """A static hierarchy for the image (cg_compiler_set_entities): groups g*/s* with parents
+        among later groups (a DAG, sometimes a cycle), static-only users u4/u5 in groups, and a
+        static resource r3 with attributes."""
+        r = self.r
+        out = []
+        allg = GROUPS + SGROUPS
+        for i, g in enumerate(allg):
+            later = allg[i + 1:]
+            par = r.sample(later, min(len(later), r.choice([0, 1, 1, 2]))) if later else []
+            if r.random() < 0.05:
+                par.append(r.choice(allg[:i + 1]))  # a cycle now and then
+            out.append({"uid": {"type": "k8s::Group", "id": g}, "attrs": {"name": g, "level": i},
+                        "parents": [{"type": "k8s::Group", "id": p} for p in par]})
+        for u in ("u4", "u5"):
+            out.append({"uid": {"type": "k8s::User", "id": u}, "attrs": self.value_attrs_user(),
+                        "parents": [{"type": "k8s::Group", "id": g} for g in r.sample(allg, 2)]})
+        out.append({"uid": {"type": "k8s::Resource", "id": "r3"}, "attrs": {"name": "r3", "size": 7, "namespace": "ns1"},
+                    "parents": [{"type": "k8s::Group", "id": r.choice(SGROUPS)}]})
+        return out
+
     def item(self):
         r = self.r
         ents = []
         groups = r.sample(GROUPS, r.randint(0, 3))
         puid = {"type": "k8s::User", "id": r.choice(USERS)}
-        ents.append({"uid": puid, "attrs": self.value_attrs_user(), "parents": [{"type": "k8s::Group", "id": g} for g in groups]})
-        # group hierarchy g_i -> g_{i+1}
+        if self.static and puid["id"] in ("u4", "u5") and r.random() < 0.7:
+            pass  # the principal is only a static entity
+        else:
+            ents.append({"uid": puid, "attrs": self.value_attrs_user(),
+                         "parents": [{"type": "k8s::Group", "id": g} for g in groups]})
+        # group hierarchy g_i -> g_{i+1} (static mode: mostly parentless group entities, as the SAR
+        # path builds them, which the static hierarchy then re-parents; sometimes a request edge of
+        # its own on a static group)
         for g in GROUPS:
             if r.random() < 0.7:
                 i = int(g[1:])
-                par = [{"type": "k8s::Group", "id": f"g{i + 1}"}] if i + 1 < len(GROUPS) and r.random() < 0.6 else []
+                chance = 0.1 if self.static else 0.6
+                par = [{"type": "k8s::Group", "id": f"g{i + 1}"}] if i + 1 < len(GROUPS) and r.random() < chance else []
                 ents.append({"uid": {"type": "k8s::Group", "id": g}, "attrs": {"name": g}, "parents": par})
         ruid = {"type": "k8s::Resource", "id": f"r{r.randint(0, 3)}"}
         ra = {"name": r.choice(TAGS + USERS), "size": r.randint(-10, 100)}
@@ -264,7 +298,7 @@ class Gen:
         if r.random() < 0.75:
             ra["sel"] = self.sel_value()
         if r.random() < 0.9:
-            ents.append({"uid": ruid, "attrs": ra, "parents": [{"type": "k8s::Group", "id": r.choice(GROUPS)}] if r.random() < 0.3 else []})
+            ents.append({"uid": ruid, "attrs": ra, "parents": [{"type": "k8s::Group", "id": r.choice(self.groups)}] if r.random() < 0.3 else []})
         act = {"type": "k8s::Action", "id": r.choice(["get", "list", "watch", "create"])}
         ctx = {}
         if r.random() < 0.8:

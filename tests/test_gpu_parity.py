@@ -48,13 +48,15 @@ def oracle_tiers(stores):
     return out
 
 
-def check_items(ctx, stores, items):
-    """items: list of (entities_json, request_json). Compares GPU and oracle for every item."""
-    tiers = cedargpu.TieredPolicyStores(stores, ctx=ctx)
+def check_items(ctx, stores, items, entities=None):
+    """items: list of (entities_json, request_json). Compares GPU and oracle for every item
+    (`entities`: the image's static entities, merged into every EntityMap)."""
+    tiers = cedargpu.TieredPolicyStores(stores, ctx=ctx, entities=entities)
     got = tiers.is_authorized_batch(items)
     otiers = oracle_tiers(stores)
+    sem = co.entities_from_json(entities) if entities else None
     for (ents, req), (ok, diag) in zip(items, got):
-        em, r = co.entities_from_json(ents), co.request_from_json(req)
+        em, r = co.merge_static_entities(co.entities_from_json(ents), sem), co.request_from_json(req)
         want_ok, want_diag, _ = co.tiered_is_authorized(otiers, em, r)
         assert ok == want_ok, (req, diag, want_diag.to_go_json())
         assert diag == want_diag.to_go_json(), (req,)
@@ -403,14 +405,14 @@ def _atomic_only(stores_texts):
     raise AssertionError("could not reduce to an all-atomic image")
 
 
-def check_items_ref(ctx, stores, items, want_indexed=None):
+def check_items_ref(ctx, stores, items, want_indexed=None, entities=None):
     """GPU vs the C++ oracle (oracle/cedar_ref.cpp) for larger item counts."""
     from cedar_ref import RefPolicySet, items_json
     if want_indexed is not None:
         assert cedargpu.image_stats(cedargpu.build_image(stores))["indexed"] == want_indexed
-    tiers = cedargpu.TieredPolicyStores(stores, ctx=ctx)
+    tiers = cedargpu.TieredPolicyStores(stores, ctx=ctx, entities=entities)
     got = tiers.is_authorized_batch(items)
-    ref = RefPolicySet.from_stores(stores)
+    ref = RefPolicySet.from_stores(stores, entities)
     ref.load_items(items_json(items))
     want = ref.evaluate(8)
     ref.close()
@@ -440,6 +442,70 @@ def test_probe_kernel_abac_synth(ctx):
         em, r = km.record_to_cedar_resource(a)
         items.append((co.entities_to_json(em), co.request_to_json(r)))
     check_items_ref(ctx, stores, items, want_indexed=True)
+
+
+def _dag_items(pop, n, seed):
+    items = []
+    for s in synth.random_sars(n, seed=seed, pop=pop):
+        a = km.attributes_from_sar(s)
+        nm = a.user.name
+        if nm.startswith("system:") and not nm.startswith(("system:serviceaccount:", "system:node:")):
+            continue
+        em, r = km.record_to_cedar_resource(a)
+        items.append((co.entities_to_json(em), co.request_to_json(r)))
+    return items
+
+
+def test_probe_kernel_abac_deep_group_dag(ctx):
+    """C3 as BASELINE.json states it: ABAC policies over a static k8s::Group DAG (depth <= 12)
+    compiled into the image's in-closure rows; >= 1k policies, >= 3k SARs, vs the C++ oracle on the
+    merged EntityMaps."""
+    pop = synth.Population(seed=5, n_users=3000, n_groups=800, dag_depth=12)
+    ents = pop.static_entities()
+    stores = [cedargpu.MemoryStore("c3.cedar", synth.abac_policies(1500, seed=5, pop=pop))]
+    items = _dag_items(pop, 3200, 6)
+    assert len(items) >= 3000
+    check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_static_entities_random_general(ctx, seed):
+    """Random general policies (policy-stream kernel, bytecode) with an image-level static
+    hierarchy: static-only principals and resources, literal static entities' attributes and
+    ancestors, request entities re-parented on top of static ones."""
+    g = Gen(11000 + seed, static=True)
+    statics = g.static_entities()
+    stores = [cedargpu.MemoryStore(f"s{t}.cedar", g.policies(g.r.randint(1, 14))) for t in range(g.r.randint(1, 2))]
+    items = [g.item() for _ in range(300)]
+    check_items(ctx, stores, items, entities=statics)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_static_entities_random_atomic(ctx, seed):
+    """The same through the probe kernel: key enumeration over the merged ancestors, key entities
+    first."""
+    g = Gen(12000 + seed, static=True)
+    statics = g.static_entities()
+    texts = [(f"p{t}.cedar", g.atomic_policies(g.r.randint(1, 50))) for t in range(g.r.randint(1, 2))]
+    stores = _atomic_only(texts)
+    items = [g.item() for _ in range(500)]
+    check_items_ref(ctx, stores, items, want_indexed=True, entities=statics)
+    check_items(ctx, stores, items[:150], entities=statics)
+
+
+def test_static_entities_sar_path(ctx):
+    """Authorize() over SAR JSON with the static hierarchy (C++ SAR model, direct encoder) vs the
+    oracle's authorize on the merged map."""
+    pop = synth.Population(seed=9, n_users=500, n_groups=120, dag_depth=12)
+    ents = pop.static_entities()
+    stores = [cedargpu.MemoryStore("c3.cedar", synth.abac_policies(400, seed=9, pop=pop))]
+    authz = cedargpu.Authorizer(stores, ctx=ctx, entities=ents)
+    sars = synth.random_sars(1500, seed=19, pop=pop)
+    got = authz.authorize_batch(sars)
+    otiers = oracle_tiers(stores)
+    sem = co.entities_from_json(ents)
+    for s, g_ in zip(sars, got):
+        assert g_ == km.authorize(otiers, km.attributes_from_sar(s), static=sem), s
 
 
 def test_probe_kernel_rbac_synth(ctx):

@@ -30,8 +30,10 @@ def _py_tiers(docs_per_tier):
     return out
 
 
-def _ref(docs_per_tier):
+def _ref(docs_per_tier, statics=None):
     r = RefPolicySet()
+    if statics:
+        r.set_entities(json.dumps(statics))
     for docs in docs_per_tier:
         r.add_tier()
         for fname, text in docs:
@@ -39,13 +41,15 @@ def _ref(docs_per_tier):
     return r
 
 
-def _compare(docs_per_tier, items, threads=4):
+def _compare(docs_per_tier, items, threads=4, statics=None):
     py = _py_tiers(docs_per_tier)
-    ref = _ref(docs_per_tier)
+    ref = _ref(docs_per_tier, statics)
+    sem = co.entities_from_json(statics) if statics else None
     assert ref.load_items(items_json(items)) == len(items)
     got = ref.evaluate(threads)
     for (ents, req), (ok, tier, diag, reasons) in zip(items, got):
-        want_ok, want_diag, want_tier = co.tiered_is_authorized(py, co.entities_from_json(ents), co.request_from_json(req))
+        em = co.merge_static_entities(co.entities_from_json(ents), sem)
+        want_ok, want_diag, want_tier = co.tiered_is_authorized(py, em, co.request_from_json(req))
         assert (ok, tier) == (want_ok, want_tier), req
         assert diag == want_diag.to_go_json(), req
         assert reasons == want_diag.reasons_json(), req
@@ -94,6 +98,30 @@ def test_cxx_random_atomic_policies(seed):
     tiers = [[("a%d.cedar" % t, g.atomic_policies(50))] for t in range(1 + seed % 2)]
     items = [g.item() for _ in range(60)]
     _compare(tiers, items)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_cxx_static_entities(seed):
+    """Static entities (an image-level hierarchy) merged into every EntityMap: the C++ oracle's
+    lookup fallback against the Python oracle's merge_static_entities."""
+    g = Gen(300 + seed, static=True)
+    statics = g.static_entities()
+    tiers = [[("s%d.cedar" % t, g.policies(40) if seed % 2 else g.atomic_policies(50))] for t in range(1 + seed % 2)]
+    items = [g.item() for _ in range(80)]
+    _compare(tiers, items, statics=statics)
+
+
+def test_merge_static_entities_semantics():
+    """A UID in both maps keeps the request's attributes and unites the parents; a UID only in the
+    static map is added; the request's other entities are untouched."""
+    req = co.entities_from_json([{"uid": {"type": "G", "id": "a"}, "attrs": {"n": 1}, "parents": [{"type": "G", "id": "x"}]},
+                                 {"uid": {"type": "U", "id": "u"}, "attrs": {}, "parents": [{"type": "G", "id": "a"}]}])
+    st = co.entities_from_json([{"uid": {"type": "G", "id": "a"}, "attrs": {"n": 2}, "parents": [{"type": "G", "id": "b"}]},
+                                {"uid": {"type": "G", "id": "b"}, "attrs": {}, "parents": [{"type": "G", "id": "c"}]}])
+    m = co.merge_static_entities(req, st)
+    a = m[co.EntityUID("G", "a")]
+    assert a.attrs == co.Record({"n": co.Long(1)}) and set(a.parents) == {co.EntityUID("G", "x"), co.EntityUID("G", "b")}
+    assert co.EntityUID("G", "b") in m and co.entity_in(m, co.EntityUID("U", "u"), co.EntityUID("G", "c"))
 
 
 def test_cxx_demo_and_converter_corpus():

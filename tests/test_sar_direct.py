@@ -48,6 +48,18 @@ def test_synthetic_sars_take_the_direct_path_and_match():
         assert nd == n  # plain bodies never need the general path
 
 
+def test_static_hierarchy_image_encodes_alike():
+    """An image with a static group DAG: both paths merge the hierarchy into the request the same
+    way (closure rows, key-entity-first ancestor order)."""
+    pop = synth.Population(seed=8, n_users=3000, n_groups=400, dag_depth=12)
+    image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", synth.abac_policies(600, seed=3, pop=pop))],
+                                 entities=pop.static_entities())
+    sars = synth.random_sars(3000, seed=12, pop=pop)
+    n, nd, nm, first = check(image, json.dumps(sars))
+    assert n == len(sars) and nd == n
+    assert nm == 0, sars[first]
+
+
 def _variants(rng: random.Random):
     """SubjectAccessReview bodies around every branch of GetAuthorizerAttributes and
     RecordToCedarResource, plus shapes the direct path must hand to the general path."""
