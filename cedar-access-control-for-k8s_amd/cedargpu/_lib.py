@@ -60,6 +60,8 @@ _SIGS = {
     "cg_compiler_add_document": (ctypes.c_int, [P, cstr, cstr, sz, cstr, cstr]),
     "cg_compiler_add_policy": (ctypes.c_int, [P, cstr, cstr, cstr, sz, ctypes.c_int]),
     "cg_compiler_set_entities": (ctypes.c_int, [P, cstr, sz]),
+    "cg_compiler_add_document_ex": (ctypes.c_int, [P, cstr, cstr, sz, cstr, cstr, ctypes.c_int]),
+    "cg_compiler_doc_errors": (ctypes.c_int, [P, P, sz, ctypes.POINTER(sz)]),
     "cg_compiler_build": (ctypes.c_int, [P, u64, ctypes.POINTER(P), ctypes.POINTER(sz)]),
     "cg_image_info": (ctypes.c_int, [P, sz, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u64)]),
     "cg_image_stats": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u32)] * 4),

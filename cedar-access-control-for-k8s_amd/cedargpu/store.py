@@ -19,6 +19,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple, Union
 from ._lib import CG_E_RANGE, CompileError, DeadlineError, DeviceError, _err, lib
 
 FAULT_NONE, FAULT_DEVICE_ERROR, FAULT_STALL = 0, 1, 2
+DOC_SKIP_INVALID = 1
 
 
 def _timeout_ns(timeout: Optional[float]) -> int:
@@ -49,6 +50,7 @@ class PolicyStore:
 
     name = "PolicyStore"
     load_complete = True
+    skip_invalid = False  # a document that does not parse fails the build (memory.go:17-22)
 
     def documents(self):
         raise NotImplementedError
@@ -78,6 +80,8 @@ class DirectoryStore(PolicyStore):
     def __init__(self, files: dict):
         self.files = dict(files)
 
+    skip_invalid = True  # a file that does not parse is logged and skipped (directory.go:69-73)
+
     def documents(self):
         for fname in sorted(self.files):  # os.ReadDir returns entries sorted by filename
             if not fname.endswith(".cedar"):
@@ -89,6 +93,7 @@ class CRDStore(PolicyStore):
     """Policy CRD snapshot: list of (metadata.name, metadata.uid, spec.content) (crd.go:45-118)."""
 
     name = "CRDPolicyStore"
+    skip_invalid = True  # a CRD that does not parse contributes nothing (crd.go:51-55, 83-95)
 
     def __init__(self, policies: Sequence[Tuple[str, str, str]]):
         self.policies = list(policies)
@@ -102,6 +107,7 @@ class AVPStore(PolicyStore):
     """Amazon Verified Permissions snapshot: list of (policyId, statement) (verified_permissions.go:58-100)."""
 
     name = "VerifiedPermissionsPolicyStore"
+    skip_invalid = True  # a statement that does not parse is skipped (verified_permissions.go:89-93)
 
     def __init__(self, policies: Sequence[Tuple[str, str]]):
         self.policies = list(policies)
@@ -165,7 +171,8 @@ class Compiler:
                 if d[0] == "doc":
                     _, fname, text, pre, suf = d
                     tb = _b(text)
-                    rc = lib.cg_compiler_add_document(c, _b(fname), tb, len(tb), _b(pre), _b(suf))
+                    rc = lib.cg_compiler_add_document_ex(c, _b(fname), tb, len(tb), _b(pre), _b(suf),
+                                                         DOC_SKIP_INVALID if st.skip_invalid else 0)
                 else:
                     _, pid, fname, text, zero = d
                     tb = _b(text)
@@ -181,6 +188,16 @@ class Compiler:
             return ctypes.string_at(out, n.value)
         finally:
             lib.cg_free(out)
+
+    def doc_errors(self) -> List[dict]:
+        """[{"filename", "error"}] of the documents the last build left out (skip_invalid stores)."""
+        need = ctypes.c_size_t(0)
+        lib.cg_compiler_doc_errors(self._h, None, 0, ctypes.byref(need))
+        buf = ctypes.create_string_buffer(max(need.value, 3))
+        rc = lib.cg_compiler_doc_errors(self._h, buf, len(buf), ctypes.byref(need))
+        if rc:
+            raise _err(rc, "doc_errors failed")
+        return json.loads(buf.value.decode("utf-8"))
 
     def cache_stats(self) -> dict:
         v = [ctypes.c_uint64() for _ in range(3)]

@@ -41,6 +41,7 @@ using namespace cg;
 struct cg_compiler {
   std::vector<std::vector<DocSpec>> tiers;
   std::vector<EntityIn> statics;  // the image's static entities (cg_compiler_set_entities)
+  std::vector<DocError> skipped;  // documents the last build left out (CG_DOC_SKIP_INVALID)
   ParseCache cache;  // parsed documents reused across builds
   std::string err;
 };
@@ -318,20 +319,25 @@ int cg_compiler_add_tier(cg_compiler* c) {
   return CG_OK;
 }
 
-int cg_compiler_add_document(cg_compiler* c, const char* filename, const char* text, size_t len, const char* id_prefix,
-                             const char* id_suffix) {
-  if (!c || (!text && len)) return CG_E_ARG;
+int cg_compiler_add_document_ex(cg_compiler* c, const char* filename, const char* text, size_t len, const char* id_prefix,
+                                const char* id_suffix, int flags) {
+  if (!c || (!text && len) || (flags & ~CG_DOC_SKIP_INVALID)) return CG_E_ARG;
   GUARD(c->err, {
     DocSpec d;
     d.filename = filename ? filename : "";
     d.text.assign(text ? text : "", len);
     d.id_prefix = id_prefix ? id_prefix : "policy";
     d.id_suffix = id_suffix ? id_suffix : "";
-    (void)parse_policies(d.text, d.filename);  // fail at add time like cedar.NewPolicySetFromBytes
-    if (c->tiers.empty()) c->tiers.emplace_back();
+    d.skip_invalid = (flags & CG_DOC_SKIP_INVALID) != 0;
+    if (c->tiers.empty()) c->tiers.emplace_back();  // parsed by the build (on workers, cached)
     c->tiers.back().push_back(std::move(d));
     return CG_OK;
   })
+}
+
+int cg_compiler_add_document(cg_compiler* c, const char* filename, const char* text, size_t len, const char* id_prefix,
+                             const char* id_suffix) {
+  return cg_compiler_add_document_ex(c, filename, text, len, id_prefix, id_suffix, 0);
 }
 
 int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* filename, const char* text, size_t len,
@@ -343,18 +349,35 @@ int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* fi
     d.text.assign(text ? text : "", len);
     d.explicit_id = policy_id;
     d.zero_position = zero_position != 0;
-    auto ps = parse_policies(d.text, d.filename);
-    if (ps.size() != 1) { c->err = "expected exactly one policy"; return CG_E_PARSE; }
-    if (c->tiers.empty()) c->tiers.emplace_back();
+    if (c->tiers.empty()) c->tiers.emplace_back();  // the build checks it holds exactly one policy
     c->tiers.back().push_back(std::move(d));
     return CG_OK;
   })
 }
 
+int cg_compiler_doc_errors(cg_compiler* c, char* buf, size_t cap, size_t* need) {
+  if (!c) return CG_E_ARG;
+  std::string s = "[";
+  for (size_t k = 0; k < c->skipped.size(); k++) {
+    if (k) s += ",";
+    s += "{\"filename\":";
+    go_json_string(s, c->skipped[k].filename);
+    s += ",\"error\":";
+    go_json_string(s, c->skipped[k].error);
+    s += "}";
+  }
+  s += "]";
+  if (need) *need = s.size() + 1;
+  if (!buf || cap < s.size() + 1) return buf ? CG_E_RANGE : CG_OK;
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return CG_OK;
+}
+
 int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len) {
   if (!c || !image || !len) return CG_E_ARG;
   try {
-    auto img = compile_image(c->tiers, epoch, &c->cache, &c->statics);
+    c->skipped.clear();
+    auto img = compile_image(c->tiers, epoch, &c->cache, &c->statics, &c->skipped);
     auto blob = img->serialize();
     uint8_t* p = (uint8_t*)std::malloc(blob.size());
     if (!p) { c->err = "out of host memory"; return CG_E_ARG; }
@@ -812,11 +835,12 @@ int cg_batch_submit(cg_batch* b) {
     h = b->ctx->hint;
   }
   for (uint32_t k = 0; k < FU_KINDS; k++) b->host.fu_want[k] = 0;
-  b->host.fu_capr_hint = 0;
+  b->host.fu_capr_hint = b->host.fu_capr_gen_hint = 0;
   if (h.serial && h.serial == b->img->serial) {
     for (uint32_t k = 0; k < FU_KINDS; k++)
       if (h.ppm[k]) b->host.fu_want[k] = (uint32_t)std::min<uint64_t>(n, (uint64_t)h.ppm[k] * n / 1000000u * 5 / 4 + 64);
     if (h.big_maxr) b->host.fu_capr_hint = (h.big_maxr + h.big_maxr / 8 + 8 + 31) & ~31u;
+    if (h.gen_maxr) b->host.fu_capr_gen_hint = (h.gen_maxr + h.gen_maxr / 8 + 8 + 31) & ~31u;
     const uint32_t want_capr = std::min<uint32_t>(64u, (h.first_maxr + 7) & ~7u);
     if (want_capr > b->host.capr && (uint64_t)n * want_capr * 8 <= (32ull << 20)) b->host.capr = want_capr;
   }
@@ -879,6 +903,7 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
         if (!(fl & cgi::RF_VALID) || (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) continue;
         const uint32_t nr = fu.res[2 * k + 1] & 0xFFFF, ne = fu.res[2 * k + 1] >> 16;
         if (q == FU_BIG) h.big_maxr = std::max(h.big_maxr, nr);  // exact, overflowed or not
+        if (q == FU_GEN) h.gen_maxr = std::max(h.gen_maxr, nr);
         if (fl & cgi::RF_OVERFLOW) continue;
         b->host.res[2 * (size_t)i] = fu.res[2 * k];
         b->host.res[2 * (size_t)i + 1] = fu.res[2 * k + 1];
@@ -892,8 +917,9 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   }
   {
     std::lock_guard<std::mutex> g(b->ctx->mu);
-    // a batch without FU_BIG entries keeps the image's last known FU_BIG list length
+    // a batch without FU_BIG / FU_GEN entries keeps the image's last known list lengths
     if (!h.big_maxr && b->ctx->hint.serial == h.serial) h.big_maxr = b->ctx->hint.big_maxr;
+    if (!h.gen_maxr && b->ctx->hint.serial == h.serial) h.gen_maxr = b->ctx->hint.gen_maxr;
     b->ctx->hint = h;
   }
   std::vector<uint32_t> idx_probe, idx_big, idx_gen;

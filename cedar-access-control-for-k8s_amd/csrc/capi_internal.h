@@ -26,6 +26,7 @@ struct CapHint {
   uint64_t serial = 0;                   // LoadedImage::serial it describes (0: none)
   uint32_t ppm[FU_KINDS] = {0, 0, 0};   // share of the batch each follow-up worklist took (per million)
   uint32_t big_maxr = 0;                 // longest reason list a FU_BIG entry produced
+  uint32_t gen_maxr = 0;                 // longest reason list a FU_GEN entry produced
   uint32_t first_maxr = 0;               // longest reason list (<= 64) the first pass counted exactly
 };
 

@@ -69,12 +69,13 @@ struct KArgs {
   const uint32_t* __restrict__ bfilt;    // key filter (image.h filt_*)
   const uint32_t* __restrict__ bstream;
   const uint32_t* __restrict__ rows;     // columnar request rows (row_words each)
+  uint32_t* __restrict__ lane;           // global lane area (GLANE stream kernel), lane_stride words per request
   const uint32_t* __restrict__ srows;    // static entities (image.h "static entities")
   const uint4* __restrict__ shash;
   unsigned long long* stats;             // probe-kernel work counters (STATS variant only)
   const uint32_t* n_dev;                 // follow-up pass: request count on the device (null: n_req)
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
-  uint32_t n_static, smask;
+  uint32_t n_static, smask, lane_stride;
 };
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
@@ -666,7 +667,8 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
 // Runs one policy program for the lanes with `run` set. On return run = satisfied, err = error.
 // `code` points into the LDS-staged record.
 // Register file of the bytecode machine: 24 local scalars a0..c7 (never address-taken, so
-// they stay in VGPRs) selected by wave-uniform operands through macro-expanded switches.
+// they stay in VGPRs) selected by wave-uniform operands through macro-expanded switches; slots 8..
+// (deep expressions) spill to the policy's lane scratch at sb (image.h MAX_SLOTS).
 #define CG_SLOT_GET(i, out) \
   do { \
     switch (i) { \
@@ -677,7 +679,8 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
       case 4: (out) = RV{a4, b4, c4}; break; \
       case 5: (out) = RV{a5, b5, c5}; break; \
       case 6: (out) = RV{a6, b6, c6}; break; \
-      default: (out) = RV{a7, b7, c7}; break; \
+      case 7: (out) = RV{a7, b7, c7}; break; \
+      default: { const uint32_t* sp_ = c.lh + sb + 3 * ((i) - 8); (out) = RV{sp_[0], sp_[1], sp_[2]}; } break; \
     } \
   } while (0)
 #define CG_SLOT_SET(i, v) \
@@ -690,13 +693,146 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
       case 4: a4 = (v).w0; b4 = (v).w1; c4 = (v).w2; break; \
       case 5: a5 = (v).w0; b5 = (v).w1; c5 = (v).w2; break; \
       case 6: a6 = (v).w0; b6 = (v).w1; c6 = (v).w2; break; \
-      default: a7 = (v).w0; b7 = (v).w1; c7 = (v).w2; break; \
+      case 7: a7 = (v).w0; b7 = (v).w1; c7 = (v).w2; break; \
+      default: { uint32_t* sp_ = c.lh + sb + 3 * ((i) - 8); sp_[0] = (v).w0; sp_[1] = (v).w1; sp_[2] = (v).w2; } break; \
     } \
   } while (0)
-static_assert(NSLOT == 8, "CG_SLOT_GET/SET enumerate 8 slots");
+static_assert(NSLOT == 8, "CG_SLOT_GET/SET enumerate 8 register slots");
 
-__device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code, uint32_t n_ins, bool& run, bool& err,
-                                             Err& e) {
+// ip(s) / decimal(s) of a runtime string, as the host parser (parser.cpp parse_ip / parse_decimal)
+__device__ __forceinline__ bool dev_digit(uint32_t ch) { return ch - '0' < 10u; }
+__device__ __forceinline__ int dev_hex(uint32_t ch) {
+  if (ch - '0' < 10u) return (int)(ch - '0');
+  if (ch - 'a' < 6u) return (int)(ch - 'a' + 10);
+  if (ch - 'A' < 6u) return (int)(ch - 'A' + 10);
+  return -1;
+}
+__device__ bool dev_parse_decimal(const uint8_t* s, uint32_t n, int64_t& out) {
+  uint32_t i = 0;
+  const bool neg = n > 0 && s[0] == '-';
+  if (neg) i = 1;
+  uint32_t dot = i;
+  while (dot < n && s[dot] != '.') dot++;
+  if (dot == n || dot == i) return false;
+  const uint32_t fl = n - dot - 1;
+  if (fl == 0 || fl > 4) return false;
+  uint64_t ip = 0;
+  bool big = false;
+  for (uint32_t k = i; k < dot; k++) {
+    if (!dev_digit(s[k])) return false;
+    if (ip > (~0ull - 9) / 10) big = true;  // beyond 2^64: out of range whatever follows
+    else ip = ip * 10 + (s[k] - '0');
+  }
+  uint64_t fp = 0;
+  for (uint32_t k = dot + 1; k < n; k++) {
+    if (!dev_digit(s[k])) return false;
+    fp = fp * 10 + (s[k] - '0');
+  }
+  for (uint32_t k = fl; k < 4; k++) fp *= 10;
+  const uint64_t lim = neg ? (1ull << 63) : (1ull << 63) - 1;
+  if (big || ip > (lim - fp) / 10000) return false;
+  const uint64_t mag = ip * 10000 + fp;
+  if (mag > lim) return false;
+  out = neg ? (int64_t)(0 - mag) : (int64_t)mag;
+  return true;
+}
+__device__ bool dev_parse_ipv4(const uint8_t* s, uint32_t n, uint32_t& a) {
+  uint32_t i = 0;
+  a = 0;
+  for (uint32_t part = 0; part < 4; part++) {
+    if (i >= n || !dev_digit(s[i])) return false;
+    uint32_t v = 0;
+    const uint32_t st = i;
+    while (i < n && dev_digit(s[i])) {
+      v = v * 10 + (s[i] - '0');
+      i++;
+      if (v > 255) return false;
+    }
+    if (i - st > 1 && s[st] == '0') return false;  // no leading zeros
+    a = (a << 8) | v;
+    if (part < 3) {
+      if (i >= n || s[i] != '.') return false;
+      i++;
+    }
+  }
+  return i == n;
+}
+__device__ bool dev_parse_ipv6(const uint8_t* s, uint32_t n, uint32_t* w4) {
+  uint32_t head[8], tail[8], nh = 0, nt = 0;
+  bool dbl = false, v4tail = false, in_tail = false;
+  uint32_t v4 = 0, i = 0;
+  if (n >= 2 && s[0] == ':' && s[1] == ':') { dbl = true; in_tail = true; i = 2; }
+  while (i < n) {
+    uint32_t j = i;
+    bool dot = false;
+    while (j < n && s[j] != ':') { dot = dot || s[j] == '.'; j++; }
+    if (dot) {
+      if (j != n || !dev_parse_ipv4(s + i, j - i, v4)) return false;
+      v4tail = true;
+      i = j;
+      break;
+    }
+    if (j == i || j - i > 4) return false;
+    uint32_t g = 0;
+    for (uint32_t k = i; k < j; k++) {
+      const int h = dev_hex(s[k]);
+      if (h < 0) return false;
+      g = (g << 4) | (uint32_t)h;
+    }
+    if (in_tail) { if (nt >= 8) return false; tail[nt++] = g; }
+    else { if (nh >= 8) return false; head[nh++] = g; }
+    if (j == n) { i = j; break; }
+    if (j + 1 < n && s[j + 1] == ':') {
+      if (dbl) return false;
+      dbl = true;
+      in_tail = true;
+      i = j + 2;
+      if (i == n) break;
+    } else {
+      i = j + 1;
+      if (i == n) return false;
+    }
+  }
+  const uint32_t groups = nh + nt + (v4tail ? 2u : 0u);
+  if (groups > 8 || (!dbl && groups != 8) || (dbl && groups == 8)) return false;
+  uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t k = 0; k < nh; k++) w[k] = head[k];
+  const uint32_t ts = 8 - nt - (v4tail ? 2u : 0u);
+  for (uint32_t k = 0; k < nt; k++) w[ts + k] = tail[k];
+  if (v4tail) { w[6] = v4 >> 16; w[7] = v4 & 0xFFFFu; }
+  for (uint32_t k = 0; k < 4; k++) w4[k] = (w[2 * k] << 16) | w[2 * k + 1];
+  return true;
+}
+// [v6 | prefix << 8, a0..a3] (image.h T_IP)
+__device__ bool dev_parse_ip(const uint8_t* s, uint32_t n, uint32_t* out) {
+  uint32_t sl = 0;
+  while (sl < n && s[sl] != '/') sl++;
+  int prefix = -1;
+  if (sl < n) {
+    const uint32_t pl = n - sl - 1;
+    if (pl == 0 || pl > 3) return false;
+    if (pl > 1 && s[sl + 1] == '0') return false;
+    prefix = 0;
+    for (uint32_t k = sl + 1; k < n; k++) {
+      if (!dev_digit(s[k])) return false;
+      prefix = prefix * 10 + (int)(s[k] - '0');
+    }
+  }
+  bool v6 = false;
+  for (uint32_t k = 0; k < sl; k++) v6 = v6 || s[k] == ':';
+  uint32_t a[4] = {0, 0, 0, 0};
+  if (v6) {
+    if (!dev_parse_ipv6(s, sl, a) || prefix > 128) return false;
+  } else {
+    if (!dev_parse_ipv4(s, sl, a[0]) || prefix > 32) return false;
+  }
+  out[0] = (v6 ? 1u : 0u) | ((uint32_t)(prefix < 0 ? (v6 ? 128 : 32) : prefix) << 8);
+  for (uint32_t k = 0; k < 4; k++) out[1 + k] = a[k];
+  return true;
+}
+
+__device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code, uint32_t n_ins, uint32_t sb, bool& run,
+                                             bool& err, Err& e) {
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
   uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
@@ -714,9 +850,9 @@ __device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code,
     const uint32_t imm = uni(ins.y);
     const uint32_t op = w0 & 0xFF, D = (w0 >> 8) & 63, A = (w0 >> 14) & 63, B = (w0 >> 20) & 63, C = w0 >> 26;
     if (on) {
-      RV va, vb;
+      RV va, vb{0, 0, 0};
       CG_SLOT_GET(A, va);
-      CG_SLOT_GET(B, vb);
+      if (op != OP_RECPUT) CG_SLOT_GET(B, vb);  // RECPUT keeps a position in b
       RV out = va;
       bool wr = true;
       switch (op) {
@@ -862,6 +998,24 @@ __device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code,
           break;
         }
         case OP_CALL: {
+          if (C == CO_PARSE_IP || C == CO_PARSE_DEC) {  // ip(x) / decimal(x) into lane scratch at imm
+            const uint32_t which = C == CO_PARSE_DEC ? 1u : 0u;
+            if (tag_of(va) != T_STR) { e.code = E_EXT_ARG; e.aux = which; err = true; wr = false; break; }
+            const uint8_t* sp;
+            uint32_t sn;
+            str_span(c, va.w1, sp, sn);
+            bool ok;
+            if (which) {
+              int64_t x = 0;
+              ok = dev_parse_decimal(sp, sn, x);
+              if (ok) { c.lh[imm] = (uint32_t)((uint64_t)x & 0xFFFFFFFFu); c.lh[imm + 1] = (uint32_t)((uint64_t)x >> 32); }
+            } else {
+              ok = dev_parse_ip(sp, sn, c.lh + imm);
+            }
+            if (!ok) { e.code = E_EXT_PARSE; e.aux = which; e.k = va.w1; err = true; wr = false; break; }
+            out = RV{mk_w0(which ? T_DEC : T_IP, mk_ref(SP_LANE, imm)), 0, 0};
+            break;
+          }
           if (C == CO_CONTAINS_ALL || C == CO_CONTAINS_ANY || C == CO_IS_EMPTY) {
             if (tag_of(va) != T_SET) { type_err(e, TN_SET, va); err = true; wr = false; break; }
             if (C == CO_IS_EMPTY) { out = mk_bool(va.w1 == 0); break; }
@@ -928,27 +1082,29 @@ __device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code,
         }
         case OP_SETNEW:
         case OP_RECNEW: {
-          const uint32_t off = imm & 0xFFFF, n = imm >> 16;
+          const uint32_t off = imm & 0xFFFFFu, n = imm >> 20;
           c.lh[off] = n;
           out = RV{mk_w0(op == OP_SETNEW ? T_SET : T_REC, mk_ref(SP_LANE, off)), n, 0};
           break;
         }
         case OP_SETPUT:
         case OP_RECPUT: {
-          // store slot A (register form) into the container in slot D at position C
+          // store slot A (register form) into the container in slot D at position pos (SETPUT:
+          // imm; RECPUT: c | b << 6, imm = key)
           wr = false;
           RV cont;
           CG_SLOT_GET(D, cont);
           const uint32_t base = cont.w0 & OFF_MASK, n = cont.w1;
           const bool isrec = op == OP_RECPUT;
           const uint32_t stride = isrec ? 3u : 2u;
-          uint32_t* slotp = c.lh + base + 1 + stride * C;
+          const uint32_t pos = isrec ? (C | (B << 6)) : imm;
+          uint32_t* slotp = c.lh + base + 1 + stride * pos;
           if (isrec) *slotp++ = imm;
           if (tag_of(va) == T_LONG) {
             const int64_t x = as_i64(va);
             if (x >= INT32_MIN && x <= INT32_MAX) { slotp[0] = mk_w0(T_LONG, 0); slotp[1] = va.w1; }
             else {
-              const uint32_t sp = base + 1 + stride * n + 2 * C;
+              const uint32_t sp = base + 1 + stride * n + 2 * pos;
               c.lh[sp] = va.w1; c.lh[sp + 1] = va.w2;
               slotp[0] = mk_w0(T_LONGREF, mk_ref(SP_LANE, sp)); slotp[1] = 0;
             }
@@ -980,7 +1136,9 @@ __device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code,
 // ---- the kernel -----------------------------------------------------------------------------
 constexpr uint32_t CAPR_L = 8;  // reasons per lane staged in LDS before spilling to global
 
-template <bool BYTECODE>
+// GLANE: lane scratch in the batch's global lane area (a.lane, lane_stride words per request)
+// instead of a private array, for images whose bytecode needs more than LANE_WORDS.
+template <bool BYTECODE, bool GLANE = false>
 __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t chunk_lds[CHUNK_WORDS];  // staged policy records
   // per-lane reason lists of the current tier ([forbid|permit][slot][lane]); global stores inside
@@ -992,11 +1150,11 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   const bool valid = gid < n_req;
   const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0;
 
-  uint32_t lane_scratch[LANE_WORDS];
+  uint32_t lane_scratch[GLANE ? 1 : LANE_WORDS];
   Ctx c;
   c.blk = a.heap + (valid ? a.req_base[r] : 0);
   c.cpool = a.cpool;
-  c.lh = lane_scratch;
+  c.lh = GLANE ? a.lane + (size_t)(valid ? gid : 0) * a.lane_stride : lane_scratch;
   c.hot = a.hot;
   c.gstr_off = a.gstr_off;
   c.gstr_bytes = a.gstr_bytes;
@@ -1069,27 +1227,32 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
     const uint32_t cend = uni(a.tier_cend[t]);
     uint32_t nf = 0, np = 0, ne = 0;
     for (uint32_t ch = cbeg; ch < cend; ch++) {
-      // stage the chunk's policy records in LDS (block-cooperative, coalesced 16-byte loads)
+      // stage the chunk's policy records in LDS (block-cooperative, coalesced 16-byte loads); a
+      // record too large for LDS has a chunk of its own and is read in place (CHUNK_GLOBAL)
       const uint32_t c_off = uni(a.chunks[4 * ch]), c_nw = uni(a.chunks[4 * ch + 1]);
       const uint32_t c_p0 = uni(a.chunks[4 * ch + 2]), c_p1 = uni(a.chunks[4 * ch + 3]);
+      const bool glob = (c_nw & CHUNK_GLOBAL) != 0;
       if (!__syncthreads_or(!decided)) break;  // whole block decided: later chunks/tiers are moot
-      {
+      if (!glob) {
         const uint4* src = reinterpret_cast<const uint4*>(a.pstream + c_off);
         uint4* dst = reinterpret_cast<uint4*>(chunk_lds);
         for (uint32_t k = threadIdx.x; k < (c_nw >> 2); k += BLOCK) dst[k] = src[k];
       }
       __syncthreads();
       if (__ballot(!decided) == 0) continue;  // this wave is done; keep joining the barriers
+      // the chunk's policies; `base` is the LDS copy or, for CHUNK_GLOBAL, the stream itself (two
+      // inlined copies, each with its own address space)
+      auto run_chunk = [&](const uint32_t* base) {
       uint32_t rw = 0;                         // record offset inside the chunk (words)
       for (uint32_t p = c_p0; p < c_p1; p++) {
-        const uint32_t* rec = chunk_lds + rw;
+        const uint32_t* rec = base + rw;
         const uint4* d4 = reinterpret_cast<const uint4*>(rec);
         const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
         const uint32_t flags = uni(q0.x), kinds = uni(q0.y);
         const uint32_t p_ty = uni(q0.z), p_et = uni(q0.w), p_ei = uni(q1.x);
         const uint32_t a_et = uni(q1.y), a_ei = uni(q1.z);
         const uint32_t r_ty = uni(q1.w), r_et = uni(q2.x), r_ei = uni(q2.y);
-        const uint32_t n_code = uni(q2.w), n_atom = uni(q3.x);
+        const uint32_t n_code = uni(q2.w), n_atom = uni(q3.x), n_lane = uni(q3.y);
         const uint32_t am0p = uni(q3.z), am1p = uni(q3.w);
         rw += (POL_WORDS + n_code + 3) & ~3u;
         const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
@@ -1142,7 +1305,9 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
           }
           run = pc == AT_SAT;
         } else if constexpr (BYTECODE) {
-          run_bytecode(c, rec + POL_WORDS, n_code >> 1, run, err, e);
+          // spilled registers (slots 8..) sit at the end of the policy's lane area
+          const uint32_t sb = n_atom > NSLOT ? n_lane - 3 * (n_atom - NSLOT) : 0u;
+          run_bytecode(c, rec + POL_WORDS, n_code >> 1, sb, run, err, e);
         }
         // ---- record outcome ----
         if (ok) {
@@ -1165,6 +1330,9 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
           }
         }
       }
+      };
+      if (glob) run_chunk(a.pstream + c_off);
+      else run_chunk(chunk_lds);
     }
     if (!decided) {
       if (t + 1 == n_tiers || nf || np || ne) {
@@ -1599,20 +1767,31 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       wave_lds_sync();
     }
   }
-  // deciding-tier hits, duplicates (adjacent after the sort) dropped; ranks by prefix counts
-  uint32_t nf = 0, np = 0, nerr = 0;
-  for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
-    const uint32_t i = c0 + sl;
+  // deciding-tier hits, duplicates (adjacent after the sort) dropped; ranks by prefix counts.
+  // Only the deciding list is written, into reasons_f (the host passes reasons_p == reasons_f):
+  // a first sweep learns whether any forbid decides.
+  auto deciding = [&](uint32_t i, uint32_t& pj, uint32_t& mj) {
     const bool have = i < nhm;
     const uint32_t key = have ? wl.hs[seg][i] : 0xFFFFFFFFu;
-    const uint32_t slot = key & 0xFFF, pj = key >> 12;
-    const uint32_t mj = have ? wl.hm[seg][slot] : 0u;
+    pj = key >> 12;
+    mj = have ? wl.hm[seg][key & 0xFFF] : 0u;
+    return have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.hs[seg][i - 1] >> 12) != pj);
+  };
+  bool deny = false;
+  for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
+    uint32_t pj, mj;
+    const bool el = deciding(c0 + sl, pj, mj);
+    deny = deny || sballot(el && (mj & 0xFF) == 1) != 0;
+  }
+  uint32_t nf = 0, np = 0, nerr = 0;
+  for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
+    uint32_t pj, mj;
+    const bool el = deciding(c0 + sl, pj, mj);
     const uint32_t kind = mj & 0xFF;
-    const bool el = have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.hs[seg][i - 1] >> 12) != pj);
     const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
     const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
-    if (el && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rf);
-    if (el && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_p + (size_t)gid * a.capr + rp);
+    if (el && deny && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rf);
+    if (el && !deny && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rp);
     if (el && kind == 2 && re < a.cape) {
       const uint32_t xs = mj >> 16;
       uint32_t* er = a.errs + ((size_t)gid * a.cape + re) * ERR_WORDS;
@@ -1725,6 +1904,7 @@ int dev_image_upload(int device, const Image& img, DevImage* out) {
   if ((rc = up(&d.srows, img.srows, d.bytes, s))) return rc;
   if ((rc = up(&d.shash, img.shash, d.bytes, s))) return rc;
   d.n_static = img.n_static();
+  d.lane_need = img.lane_need;
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
   d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
   d.fmask = (uint32_t)(img.bfilt.size() / 2) - 1;
@@ -1828,14 +2008,19 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   size_t off[5], in_bytes = 0;
   for (int k = 0; k < 5; k++) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
   const size_t n = std::max<uint32_t>(b.n(), 1);
-  const size_t o_res = 0, o_rf = al(n * 2 * 4), o_rp = o_rf + al(n * d.capr * 4), o_er = o_rp + al(n * d.capr * 4);
+  // The probe kernel writes only the deciding reason list (into reasons_f; reasons_p aliases it),
+  // the policy-stream kernel both lists: an indexed image's first pass needs one array.
+  const bool one_list = b.img->indexed != 0;
+  const size_t o_res = 0, o_rf = al(n * 2 * 4), o_rp = one_list ? o_rf : o_rf + al(n * d.capr * 4),
+               o_er = o_rp + al(n * d.capr * 4);
   // On-device follow-up worklists. Entries: n / 32 (4..64) by default, or what the previous batch
-  // on this image needed (the caller's hint), within a byte budget per worklist; FU_BIG holds 256
-  // reasons per entry unless the hint says fewer suffice (64..256).
+  // on this image needed (the caller's hint), within a byte budget per worklist. Reasons per entry:
+  // FU_BIG 256 unless the hint says otherwise (64..1024, the large stage's hit capacity), FU_OVF 64
+  // (the probe kernel's), FU_GEN 64 unless hinted (..4096).
   const bool fu_on = !(std::getenv("CEDARGPU_FOLLOWUP") && *std::getenv("CEDARGPU_FOLLOWUP") == '0');
   const uint32_t fu_default = std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u));
-  const uint32_t capr_k[FU_KINDS] = {b.fu_capr_hint ? std::min<uint32_t>(256u, std::max<uint32_t>(64u, b.fu_capr_hint)) : 256u,
-                                     64u, 64u};
+  const uint32_t capr_k[FU_KINDS] = {b.fu_capr_hint ? std::min<uint32_t>(1024u, std::max<uint32_t>(64u, b.fu_capr_hint)) : 256u,
+                                     64u, std::min<uint32_t>(4096u, std::max<uint32_t>(64u, b.fu_capr_gen_hint))};
   const size_t budget_k[FU_KINDS] = {std::min<size_t>(128u << 20, std::max<size_t>(16u << 20, (size_t)b.n() * 2048)),
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024)),
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024))};
@@ -1848,23 +2033,38 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     const bool probe_kind = k != FU_GEN;
     f.capr = capr_k[k];
     f.cape = 16;
-    const size_t entry = 4 * (1 + 2 + 2 * (size_t)f.capr + (size_t)f.cape * ERR_WORDS);
+    const size_t lists = probe_kind ? 1 : 2;
+    const size_t entry = 4 * (1 + 2 + lists * (size_t)f.capr + (size_t)f.cape * ERR_WORDS);
     const uint32_t want = std::min<uint32_t>(b.n(), std::max(fu_default, b.fu_want[k]));
     f.cap = (fu_on && b.n() && (!probe_kind || b.img->indexed)) ? (uint32_t)std::min<size_t>(want, budget_k[k] / entry) : 0u;
     o_k[k][0] = o_fu;                                        // ids
     o_k[k][1] = o_k[k][0] + al((size_t)f.cap * 4);           // res
     o_k[k][2] = o_k[k][1] + al((size_t)f.cap * 2 * 4);       // reasons_f
-    o_k[k][3] = o_k[k][2] + al((size_t)f.cap * f.capr * 4);  // reasons_p
+    o_k[k][3] = probe_kind ? o_k[k][2] : o_k[k][2] + al((size_t)f.cap * f.capr * 4);  // reasons_p
     o_k[k][4] = o_k[k][3] + al((size_t)f.cap * f.capr * 4);  // errors
     o_fu = o_k[k][4] + al((size_t)f.cap * f.cape * ERR_WORDS * 4);
   }
   d.out_bytes = o_fu;
   int rc;
-  if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) return rc;
-  if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) { pool_put(pool, false, d.in_blk, d.in_cls); return rc; }
+  if (b.img->lane_need > LANE_WORDS) {  // per-request lane scratch of the GLANE stream kernel
+    const size_t lane_bytes = (size_t)n * b.img->lane_need * 4;
+    if (lane_bytes > (8ull << 30)) {
+      g_err = "batch needs " + std::to_string(lane_bytes >> 20) + " MB of lane scratch for this image's policies; submit smaller batches";
+      return -7;  // CG_E_RANGE
+    }
+    if ((rc = pool_get(pool, false, lane_bytes, &d.lane_blk, &d.lane_cls))) return rc;
+    d.lane = (uint32_t*)d.lane_blk;
+  }
+  if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) { pool_put(pool, false, d.lane_blk, d.lane_cls); return rc; }
+  if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) {
+    pool_put(pool, false, d.in_blk, d.in_cls);
+    pool_put(pool, false, d.lane_blk, d.lane_cls);
+    return rc;
+  }
   if ((rc = pool_get(pool, true, std::max(in_bytes, d.out_bytes), &d.stage, &d.stage_cls))) {
     pool_put(pool, false, d.in_blk, d.in_cls);
     pool_put(pool, false, d.out_blk, d.out_cls);
+    pool_put(pool, false, d.lane_blk, d.lane_cls);
     return rc;
   }
   uint8_t* st = (uint8_t*)d.stage;
@@ -1938,6 +2138,7 @@ void dev_batch_free(DevBatch* d) {
     pool_put(d->pool, false, d->in_blk, d->in_cls);
     pool_put(d->pool, false, d->out_blk, d->out_cls);
     pool_put(d->pool, true, d->stage, d->stage_cls);
+    pool_put(d->pool, false, d->lane_blk, d->lane_cls);
   }
   if (d->req_idx) (void)hipFree(d->req_idx);
   *d = DevBatch();
@@ -2010,6 +2211,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
+  k.lane = b.lane; k.lane_stride = img.lane_need;
   k.stats = nullptr;
   k.n_dev = nullptr;
   return k;
@@ -2109,17 +2311,20 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
   else hipLaunchKernelGGL((cedar_probe_kernel<64, 64>), grid, dim3(BLOCK), 0, s, k);
 }
 
+// the policy-stream kernel for n requests: without bytecode, with it, or with it on the global
+// lane area (an image whose bytecode needs more lane scratch than the private array holds)
+static void launch_stream(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
+  auto kern = img.lane_need > LANE_WORDS ? cedar_eval_kernel<true, true>
+              : img.has_bytecode          ? cedar_eval_kernel<true>
+                                          : cedar_eval_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
+}
+
 static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
   if (img.indexed)
     launch_probe(k, n, s);
   else
-    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>,
-                       dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
-}
-
-static void launch_stream(const DevImage& img, const KArgs& k, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK),
-                     dim3(BLOCK), lds_bytes(img), s, k);
+    launch_stream(img, k, n, s);
 }
 
 // One complete evaluation step of a batch, stream-ordered with no host round trip: the first
@@ -2167,6 +2372,7 @@ int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx
   if (n == 0) return 0;
   if (!b.pool) { g_err = "batch has no buffer pool"; return -4; }
   for (uint32_t i = 0; i < n; i++) if (idx[i] >= b.n) { g_err = "request index out of range"; return -2; }
+  if (n > b.n && img.lane_need > LANE_WORDS) { g_err = "subset larger than its batch's lane area"; return -2; }
   // one device block [idx | res | reasons_f | reasons_p | errs] and one pinned block, from the pool
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   DevSubset j;
@@ -2177,7 +2383,8 @@ int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx
   j.cape = cape;
   j.o_res = al((size_t)n * 4);
   j.o_rf = j.o_res + al((size_t)n * 2 * 4);
-  j.o_rp = j.o_rf + al((size_t)n * capr * 4);
+  const bool one_list = probe && img.indexed;  // the probe kernel writes only the deciding list
+  j.o_rp = one_list ? j.o_rf : j.o_rf + al((size_t)n * capr * 4);
   j.o_er = j.o_rp + al((size_t)n * capr * 4);
   j.total = j.o_er + al((size_t)n * cape * ERR_WORDS * 4);
   int rc;
@@ -2197,7 +2404,7 @@ int dev_subset_begin(const DevImage& img, const DevBatch& b, const uint32_t* idx
   if (probe && img.indexed)
     launch_probe(k, n, s, probe == 2);
   else
-    hipLaunchKernelGGL(img.has_bytecode ? cedar_eval_kernel<true> : cedar_eval_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds_bytes(img), s, k);
+    launch_stream(img, k, n, s);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "launch");
   if ((e = hipMemcpyAsync(h8 + j.o_res, d8 + j.o_res, j.total - j.o_res, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e, "D2H");
   if ((e = hipEventRecord(ev, s)) != hipSuccess) return fail(e, "event record");

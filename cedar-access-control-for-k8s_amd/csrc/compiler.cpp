@@ -148,9 +148,15 @@ struct Compiler {
   uint32_t here() const { return (uint32_t)(I.code.size() - code0) / 2; }
   void patch(uint32_t idx, uint32_t imm) { I.code[code0 + 2 * idx + 1] = imm; }
 
-  void slot(uint32_t d) {
-    if (d >= NSLOT) throw CedarError("expression too deep for the device register file");
+  void slot(uint32_t d) {  // slots NSLOT.. spill to lane scratch (image.h MAX_SLOTS)
+    if (d >= MAX_SLOTS) throw CedarError("expression nesting beyond the device evaluator's 64 registers is not supported by the device compiler");
     max_slot = std::max(max_slot, d + 1);
+  }
+  uint32_t lane(uint32_t words) {  // a region of the policy's lane scratch
+    const uint32_t off = lane_off;
+    lane_off += words;
+    if (lane_off > LANE_MAX) throw CedarError("policy needs more lane scratch than the device provides (not supported by the device compiler)");
+    return off;
   }
 
   static int var_index(const std::string& n) {
@@ -313,7 +319,12 @@ struct Compiler {
           emit(OP_ERR, 0, 0, 0, E_EXT, ext_msg("error parsing " + std::string(e.name == "ip" ? "ip" : "decimal") + " value: " + a.s));
           return;
         }
-        throw CedarError("extension call " + e.name + "() with a non-constant argument is not supported by the device compiler");
+        if (e.kids.size() != 1 || (e.name != "decimal" && e.name != "ip")) throw CedarError("unknown extension function " + e.name);
+        // ip(x) / decimal(x) over a runtime value: parsed on the device into lane scratch
+        compile(*e.kids[0], d);
+        const bool ip = e.name == "ip";
+        emit(OP_CALL, d, d, 0, ip ? CO_PARSE_IP : CO_PARSE_DEC, lane(ip ? 5u : 2u));
+        return;
       }
       case EK::Method: {
         const std::string& m = e.name;
@@ -343,33 +354,29 @@ struct Compiler {
       }
       case EK::Set: {
         uint32_t n = (uint32_t)e.kids.size();
-        if (n >= 64) throw CedarError("non-constant set literal too large for the device");
-        uint32_t off = lane_off;
-        lane_off += 1 + 4 * n;  // [n, (w0,w1)*n, (lo,hi)*n spare for 64-bit longs]
-        if (lane_off > LANE_WORDS) throw CedarError("policy needs more lane scratch than the device provides");
-        emit(OP_SETNEW, d, 0, 0, 0, off | (n << 16));
+        if (n >= MAX_LITERAL) throw CedarError("non-constant set literal of 4096 or more elements is not supported by the device compiler");
+        const uint32_t off = lane(1 + 4 * n);  // [n, (w0,w1)*n, (lo,hi)*n spare for 64-bit longs]
+        emit(OP_SETNEW, d, 0, 0, 0, off | (n << 20));  // lane offset < 2^20, n < 2^12
         for (uint32_t i = 0; i < n; i++) {
           compile(*e.kids[i], d + 1);
-          emit(OP_SETPUT, d, d + 1, 0, i, 0);
+          emit(OP_SETPUT, d, d + 1, 0, 0, i);
         }
         return;
       }
       case EK::Rec: {
         uint32_t n = (uint32_t)e.kids.size();
-        if (n >= 64) throw CedarError("non-constant record literal too large for the device");
-        uint32_t off = lane_off;
-        lane_off += 1 + 5 * n;  // [n, (key,w0,w1)*n, (lo,hi)*n spare]
-        if (lane_off > LANE_WORDS) throw CedarError("policy needs more lane scratch than the device provides");
+        if (n >= MAX_LITERAL) throw CedarError("non-constant record literal of 4096 or more fields is not supported by the device compiler");
+        const uint32_t off = lane(1 + 5 * n);  // [n, (key,w0,w1)*n, (lo,hi)*n spare]
         std::vector<std::pair<uint32_t, uint32_t>> order;  // (key sid, source index)
         for (uint32_t i = 0; i < n; i++) order.emplace_back(intern(e.keys[i]), i);
         std::vector<uint32_t> pos(n);
         auto sorted = order;
         std::sort(sorted.begin(), sorted.end());
         for (uint32_t k = 0; k < n; k++) pos[sorted[k].second] = k;
-        emit(OP_RECNEW, d, 0, 0, 0, off | (n << 16));
+        emit(OP_RECNEW, d, 0, 0, 0, off | (n << 20));
         for (uint32_t i = 0; i < n; i++) {
           compile(*e.kids[i], d + 1);
-          emit(OP_RECPUT, d, d + 1, 0, pos[i], order[i].first);
+          emit(OP_RECPUT, d, d + 1, pos[i] >> 6, pos[i] & 63, order[i].first);  // position c | b << 6
         }
         return;
       }
@@ -838,7 +845,11 @@ struct Compiler {
     }
     w[PW_CODE] = code0;
     w[PW_CODE_N] = (uint32_t)I.code.size() - code0;
-    if (!(w[PW_FLAGS] & PF_ATOMIC)) w[PW_SLOTS] = max_slot;
+    if (!(w[PW_FLAGS] & PF_ATOMIC)) {
+      w[PW_SLOTS] = max_slot;
+      if (max_slot > NSLOT) (void)lane(3 * (max_slot - NSLOT));  // spilled registers: the lane area's end
+      I.lane_need = std::max(I.lane_need, lane_off);
+    }
     w[PW_LANE] = lane_off;
     I.pol.insert(I.pol.end(), w, w + POL_WORDS);
     akeys.push_back(key);
@@ -1104,7 +1115,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
 // Parses every document of the tiers, through the cache when one is given (unseen documents on
 // worker threads).
 static std::vector<std::shared_ptr<const std::vector<Policy>>> parse_documents(
-    const std::vector<std::vector<DocSpec>>& tiers, ParseCache* cache) {
+    const std::vector<std::vector<DocSpec>>& tiers, ParseCache* cache, std::vector<DocError>* skipped) {
   std::vector<const DocSpec*> docs;
   for (auto& t : tiers)
     for (auto& d : t) docs.push_back(&d);
@@ -1153,11 +1164,18 @@ static std::vector<std::shared_ptr<const std::vector<Policy>>> parse_documents(
     for (unsigned t = 0; t < nt; t++) ws.emplace_back(work);
     for (auto& w : ws) w.join();
   }
-  for (size_t i = 0; i < docs.size(); i++)
-    if (!errs[i].empty()) throw CedarError(errs[i]);
+  // a document that does not parse fails the build, unless its store skips such documents: then
+  // it contributes no policies and is reported (the first error, in document order, either way)
+  static const auto empty = std::make_shared<const std::vector<Policy>>();
+  for (size_t i = 0; i < docs.size(); i++) {
+    if (errs[i].empty()) continue;
+    if (!docs[i]->skip_invalid) throw CedarError(errs[i]);
+    if (skipped) skipped->push_back({docs[i]->filename, errs[i]});
+    out[i] = empty;
+  }
   if (cache) {
     for (size_t i : todo)
-      cache->map[key(*docs[i])].push_back({docs[i]->filename, docs[i]->text, out[i], cache->generation});
+      if (errs[i].empty()) cache->map[key(*docs[i])].push_back({docs[i]->filename, docs[i]->text, out[i], cache->generation});
     for (auto it = cache->map.begin(); it != cache->map.end();) {  // drop what this build did not use
       auto& v = it->second;
       v.erase(std::remove_if(v.begin(), v.end(), [&](const ParseCache::Entry& e) { return e.used != cache->generation; }), v.end());
@@ -1168,7 +1186,7 @@ static std::vector<std::shared_ptr<const std::vector<Policy>>> parse_documents(
 }
 
 std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch, ParseCache* cache,
-                                     const std::vector<EntityIn>* statics) {
+                                     const std::vector<EntityIn>* statics, std::vector<DocError>* skipped) {
   if (tiers.empty()) throw CedarError("at least one policy tier is required");
   if (tiers.size() > 255) throw CedarError("too many tiers");
   auto img = std::make_shared<Image>();
@@ -1183,7 +1201,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     std::fprintf(stderr, "compile %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_mark).count());
     t_mark = now;
   };
-  const auto docs = parse_documents(tiers, cache);
+  const auto docs = parse_documents(tiers, cache, skipped);
   mark("parse");
   // PolicySet.Add semantics: a repeated ID replaces the earlier policy in place. The tiers refer
   // to the parsed ASTs (owned by `docs` / the cache); only ID and position are per use.
@@ -1246,28 +1264,31 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     for (uint32_t t = 0; t < img->n_tiers(); t++) {
       uint32_t pend = img->tier_end[t];
       uint32_t c_off = (uint32_t)img->pstream.size(), c_p0 = p;
-      auto close = [&]() {
+      auto close = [&](uint32_t flag) {
         uint32_t nw = (uint32_t)img->pstream.size() - c_off;
         if (p > c_p0) {
-          img->chunks.push_back(c_off); img->chunks.push_back(nw);
+          img->chunks.push_back(c_off); img->chunks.push_back(nw | flag);
           img->chunks.push_back(c_p0); img->chunks.push_back(p);
         }
         c_off = (uint32_t)img->pstream.size();
         c_p0 = p;
       };
-      for (; p < pend; p++) {
+      for (; p < pend;) {
         const uint32_t* d = &img->pol[(size_t)p * POL_WORDS];
         uint32_t ncode = d[PW_CODE_N];
         uint32_t rec = (POL_WORDS + ncode + 3) & ~3u;
-        if (rec > CHUNK_WORDS) throw CedarError("policy " + img->meta[p].id + " is too large for the device policy stream");
-        if ((uint32_t)img->pstream.size() - c_off + rec > CHUNK_WORDS) close();
+        // a record larger than an LDS chunk gets a chunk of its own, read in place (CHUNK_GLOBAL)
+        const bool big = rec > CHUNK_WORDS;
+        if (big || (uint32_t)img->pstream.size() - c_off + rec > CHUNK_WORDS) close(0);
         size_t base = img->pstream.size();
         img->pstream.insert(img->pstream.end(), d, d + POL_WORDS);
         img->pstream[base + PW_CODE] = p;
         img->pstream.insert(img->pstream.end(), img->code.begin() + d[PW_CODE], img->code.begin() + d[PW_CODE] + ncode);
         while ((img->pstream.size() - base) % 4) img->pstream.push_back(0);
+        p++;
+        if (big) close(CHUNK_GLOBAL);
       }
-      close();
+      close(0);
       img->tier_cend.push_back((uint32_t)img->chunks.size() / 4);
     }
     if (img->pstream.empty()) img->pstream.resize(4, 0);
@@ -1325,7 +1346,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.vec(act); w.u32(amask_ok); w.u32(n_atomic);
   w.vec(pstream); w.vec(chunks); w.vec(tier_cend);
   w.vec(btab); w.vec(bfilt); w.vec(bstream); w.u32(indexed); w.u32(combo_mask);
-  w.vec(srows); w.vec(shash);
+  w.vec(srows); w.vec(shash); w.u32(lane_need);
   w.u32((uint32_t)key_ents.size());
   for (uint64_t k : key_ents) w.u64(k);
   w.u32((uint32_t)strings.size());
@@ -1356,7 +1377,8 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     const size_t nb = img->btab.size() / BT_WORDS, nf = img->bfilt.size();
     if (!nb || (nb & (nb - 1)) || nf < 2 || (nf & (nf - 1))) throw CedarError("corrupt image (scope index)");
   }
-  img->srows = r.vec(); img->shash = r.vec();
+  img->srows = r.vec(); img->shash = r.vec(); img->lane_need = r.u32();
+  if (img->lane_need > LANE_MAX) throw CedarError("corrupt image (lane scratch)");
   {
     const size_t ns = img->shash.size() / SH_WORDS;
     if (!ns || (ns & (ns - 1)) || img->srows.size() % ENT_WORDS || ns <= img->n_static()) throw CedarError("corrupt image (static entities)");

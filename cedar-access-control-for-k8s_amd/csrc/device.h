@@ -20,6 +20,7 @@ struct DevImage {
   uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
   uint8_t* gstr_bytes = nullptr;
   uint32_t n_static = 0, smask = 0;
+  uint32_t lane_need = 0;  // lane-scratch words per request (> LANE_WORDS: the GLANE stream kernel)
   uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0, n_act = 0, amask_ok = 0, has_bytecode = 1, indexed = 0, bmask = 0, fmask = 0, combo_mask = 0;
   size_t bytes = 0;
 };
@@ -52,6 +53,9 @@ struct DevBatch {
     uint32_t *ids = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
     uint32_t cap = 0, capr = 0, cape = 0;
   } fu[3];
+  uint32_t* lane = nullptr;  // per-request lane scratch (images with lane_need > LANE_WORDS)
+  void* lane_blk = nullptr;
+  size_t lane_cls = 0;
   uint32_t n = 0, capr = 0, cape = 0, row_words = 0;
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)

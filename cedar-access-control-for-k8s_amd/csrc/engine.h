@@ -37,6 +37,7 @@ struct Image {
   std::vector<uint32_t> act;  // action table: (type sid, id sid) pairs of every action entity in scopes
   uint32_t amask_ok = 0;      // 1 when act has <= MAX_ACT entries (PW_AMASK* valid)
   uint32_t n_atomic = 0;      // policies compiled to atoms (statistics)
+  uint32_t lane_need = 0;     // most lane-scratch words a bytecode policy uses (image.h LANE_MAX)
   // scope index over atomic policies (image.h "scope index"); indexed = every policy is atomic
   std::vector<uint32_t> btab, bfilt, bstream;  // bfilt: key filter, 2 words per block
   uint32_t indexed = 0;
@@ -120,6 +121,13 @@ struct DocSpec {
   std::string filename, text, id_prefix, id_suffix;
   std::string explicit_id;  // when set: the document holds exactly one policy with this ID
   bool zero_position = false;  // policies built from AST (e.g. allow-all-admission) carry Position{}
+  // a document that does not parse is left out of the build and reported (the directory / CRD /
+  // AVP stores log and skip it: directory.go:69-73, crd.go:51-55,91-95,
+  // verified_permissions.go:89-93); else it fails the build (cedar.NewPolicySetFromBytes, memory.go:18)
+  bool skip_invalid = false;
+};
+struct DocError {
+  std::string filename, error;
 };
 
 // Parsed documents kept across builds (the incremental compiler): a rebuild after a store change
@@ -147,7 +155,8 @@ struct EntityIn {
 // next time; the image is byte-identical to a build without the cache. `statics`: the image's
 // static entities (cg_compiler_set_entities).
 std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch,
-                                     ParseCache* cache = nullptr, const std::vector<EntityIn>* statics = nullptr);
+                                     ParseCache* cache = nullptr, const std::vector<EntityIn>* statics = nullptr,
+                                     std::vector<DocError>* skipped = nullptr);
 struct RequestIn {
   std::pair<std::string, std::string> principal, action, resource;
   HVal context;  // Record
@@ -192,7 +201,7 @@ struct Batch {
   // on-device follow-up sizing (device.h FuKind), from the previous batch on the same image:
   // entries wanted per worklist (0: the default) and reasons per FU_BIG entry (0: 256)
   uint32_t fu_want[3] = {0, 0, 0};
-  uint32_t fu_capr_hint = 0;
+  uint32_t fu_capr_hint = 0, fu_capr_gen_hint = 0;  // reasons per FU_BIG / FU_GEN entry (0: default)
   // first-pass results, read in place from the batch's pinned staging block (device.h DevBatch;
   // valid while the batch lives): res[2i], [2i+1] per request, capr reasons of each effect, cape
   // error records. res is written back by overflow re-runs.

@@ -284,7 +284,20 @@ enum CallOp : uint32_t {
   CO_CONTAINS_ALL = 0, CO_CONTAINS_ANY, CO_IS_EMPTY,
   CO_DEC_LT, CO_DEC_LE, CO_DEC_GT, CO_DEC_GE,
   CO_IP_V4, CO_IP_V6, CO_IP_LOOPBACK, CO_IP_MULTICAST, CO_IP_IN_RANGE,
+  CO_PARSE_IP, CO_PARSE_DEC,  // ip(a) / decimal(a) over a runtime string: value into lane scratch at imm
 };
+// Register slots: 0..NSLOT-1 live in registers; deeper expressions spill slots NSLOT.. into the
+// policy's lane scratch, 3 words each, at the end of its lane area (PW_LANE - 3 * (PW_SLOTS - NSLOT)).
+constexpr uint32_t MAX_SLOTS = 64;  // 6-bit slot fields
+// SETPUT / RECPUT element position: c | b << 6 (12 bits)
+constexpr uint32_t MAX_LITERAL = 4096;
+// Lane scratch: a private array of LANE_WORDS per lane; an image with a policy that needs more
+// (big runtime literals, spilled slots) runs the stream kernel on a per-request global lane area of
+// the image's lane_need words (DevBatch::lane).
+constexpr uint32_t LANE_MAX = 1u << 20;
+// chunk table: words field with CHUNK_GLOBAL set = one policy record too large for the LDS chunk,
+// read from the policy stream in place
+constexpr uint32_t CHUNK_GLOBAL = 0x80000000u;
 
 __host__ __device__ constexpr inline uint32_t mk_ins(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
   return op | (d << 8) | (a << 14) | (b << 20) | (c << 26);
@@ -310,6 +323,8 @@ enum ErrCode : uint32_t {
   E_EXT = 6,             // aux = message index in image (compile-time message)
   E_DEPTH = 7,           // value nesting beyond VAL_DEPTH (device limit)
   E_LANE = 8,            // lane scratch exhausted (device limit)
+  E_EXT_ARG = 9,         // aux = 0 ip / 1 decimal: the argument is not a string
+  E_EXT_PARSE = 10,      // aux = 0 ip / 1 decimal, k = the string that does not parse
 };
 enum TypeName : uint32_t {
   TN_BOOL = 0, TN_LONG, TN_STRING, TN_ENTITY, TN_SET, TN_RECORD, TN_DECIMAL, TN_IP,

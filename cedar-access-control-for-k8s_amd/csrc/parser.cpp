@@ -388,6 +388,17 @@ struct Parser {
     }
     return e;
   }
+  // The extension functions and methods Cedar defines (ip/decimal plus the set, decimal and ipaddr
+  // methods): anything else, or another argument count, is a parse error, so a document that
+  // names one is rejected (or skipped by the stores that skip bad documents) as a whole.
+  static int method_arity(const std::string& m) {
+    static const char* one[] = {"contains", "containsAll", "containsAny", "lessThan", "lessThanOrEqual",
+                                "greaterThan", "greaterThanOrEqual", "isInRange"};
+    static const char* zero[] = {"isEmpty", "isIpv4", "isIpv6", "isLoopback", "isMulticast"};
+    for (const char* x : one) if (m == x) return 1;
+    for (const char* x : zero) if (m == x) return 0;
+    return -1;
+  }
   ExprP member() { return member_tail(primary()); }
   ExprP member_tail(ExprP e) {
     for (;;) {
@@ -401,6 +412,9 @@ struct Parser {
           m->name = nm.text;
           m->kids.push_back(e);
           auto args = expr_list(")");
+          const int want = method_arity(nm.text);
+          if (want < 0) fail("`" + nm.text + "` is not a method");
+          if ((int)args.size() != want) fail(nm.text + " expects " + std::to_string(want) + " argument(s)");
           m->kids.insert(m->kids.end(), args.begin(), args.end());
           e = m;
         } else {
@@ -476,8 +490,10 @@ struct Parser {
       if (is_op("(", j)) {
         auto c = mk(EK::Call);
         c->name = path();
+        if (c->name != "ip" && c->name != "decimal") fail("`" + c->name + "` is not a function");
         expect("(");
         c->kids = expr_list(")");
+        if (c->kids.size() != 1) fail(c->name + " expects 1 argument");
         return c;
       }
       fail("unexpected identifier '" + x.text + "'");

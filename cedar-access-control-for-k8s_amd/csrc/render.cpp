@@ -88,6 +88,8 @@ std::string Batch::error_message(uint32_t i, const uint32_t* rec) const {
     case E_ATTR_RECORD: body = "record does not have the attribute `" + str(i, rec[2]) + "`"; break;
     case E_OVERFLOW: body = "integer overflow"; break;
     case E_EXT: body = aux < img->ext_msgs.size() ? img->ext_msgs[aux] : "extension error"; break;
+    case E_EXT_ARG: body = std::string(aux ? "decimal" : "ip") + " takes one string argument"; break;
+    case E_EXT_PARSE: body = std::string("error parsing ") + (aux ? "decimal" : "ip") + " value: " + str(i, rec[2]); break;
     case E_DEPTH: body = "value nesting exceeds the device evaluator limit"; break;
     case E_LANE: body = "device lane scratch exhausted"; break;
     default: body = "unknown evaluation error"; break;

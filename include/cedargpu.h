@@ -52,9 +52,22 @@ const char* cg_compiler_last_error(cg_compiler* c);
 int cg_compiler_add_tier(cg_compiler* c);
 /* Adds every policy of a Cedar document to the current tier with IDs id_prefix + i + id_suffix:
  * memory store: ("policy", ""), directory: ("<file>.policy", ""), CRD: ("<name>", "-<uid>"),
- * AVP: ("<id>.", ""). `filename` becomes Position.filename. */
+ * AVP: ("<id>.", ""). `filename` becomes Position.filename. Documents are parsed by
+ * cg_compiler_build; one that does not parse fails the build with CG_E_PARSE, as
+ * cedar.NewPolicySetFromBytes fails NewMemoryStore (store/memory.go:17-22). */
 int cg_compiler_add_document(cg_compiler* c, const char* filename, const char* text, size_t len,
                              const char* id_prefix, const char* id_suffix);
+/* As cg_compiler_add_document; with CG_DOC_SKIP_INVALID a document that does not parse is left out
+ * of the build (no policies) and listed by cg_compiler_doc_errors, while the build succeeds: the
+ * directory, CRD and AVP stores log such a document and load the rest (store/directory.go:69-73,
+ * crd.go:51-55 and 91-95 -- an update that breaks a CRD drops its old policies --,
+ * verified_permissions.go:89-93). */
+#define CG_DOC_SKIP_INVALID 1
+int cg_compiler_add_document_ex(cg_compiler* c, const char* filename, const char* text, size_t len,
+                                const char* id_prefix, const char* id_suffix, int flags);
+/* The documents the last cg_compiler_build left out: JSON [{"filename":..,"error":..}, ...].
+ * Writes at most cap bytes incl. NUL; *need = required size. */
+int cg_compiler_doc_errors(cg_compiler* c, char* buf, size_t cap, size_t* need);
 /* Adds exactly one policy with an explicit ID. zero_position=1 reproduces policies built from an
  * AST (cedar.NewPolicyFromAST, e.g. allow-all-admission) whose Position is the zero value. */
 int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* filename, const char* text,

@@ -36,6 +36,7 @@ style and compared only where both sides are ours.
 from __future__ import annotations
 
 import ipaddress
+import re
 import json
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
@@ -645,6 +646,11 @@ class Parser:
                 if self.is_op("("):
                     self.next()
                     args = self.expr_list(")")
+                    want = _METHOD_ARITY.get(name.text)
+                    if want is None:
+                        raise ParseError(f"`{name.text}` is not a method")
+                    if len(args) != want:
+                        raise ParseError(f"{name.text} expects {want} argument(s)")
                     e = ("method", e, name.text, args)
                 else:
                     e = ("attr", e, name.text)
@@ -733,11 +739,23 @@ class Parser:
                 return ("lit", self.entity_ref())
             if self.is_op("(", j):
                 name = self.path()
+                if name not in ("ip", "decimal"):
+                    raise ParseError(f"`{name}` is not a function")
                 self.expect("(")
                 args = self.expr_list(")")
+                if len(args) != 1:
+                    raise ParseError(f"{name} expects 1 argument")
                 return ("call", name, args)
             raise ParseError(f"{self.filename}:{t.line}:{t.col}: unexpected identifier {t.text!r}")
         raise ParseError(f"{self.filename}:{t.line}:{t.col}: unexpected token {t.text!r}")
+
+
+# Cedar's extension functions are ip/decimal (one argument each); its methods and their argument
+# counts are below. Other names or counts are parse errors (the device compiler's parser.cpp
+# rejects them the same way), so the whole document is rejected or skipped.
+_METHOD_ARITY = {"contains": 1, "containsAll": 1, "containsAny": 1, "lessThan": 1, "lessThanOrEqual": 1,
+                 "greaterThan": 1, "greaterThanOrEqual": 1, "isInRange": 1,
+                 "isEmpty": 0, "isIpv4": 0, "isIpv6": 0, "isLoopback": 0, "isMulticast": 0}
 
 
 def parse_policies(src: str, filename: str = "") -> List[Policy]:
@@ -754,7 +772,7 @@ def parse_decimal(s: str) -> Decimal:
     if "." not in body:
         raise EvalError("extension", f"error parsing decimal value: {s}")
     ip, fp = body.split(".", 1)
-    if not ip.isdigit() or not fp.isdigit() or len(fp) > 4 or len(fp) == 0:
+    if not (ip.isascii() and ip.isdigit() and fp.isascii() and fp.isdigit()) or len(fp) > 4:
         raise EvalError("extension", f"error parsing decimal value: {s}")
     v = int(ip) * 10000 + int(fp.ljust(4, "0"))
     if neg:
@@ -765,6 +783,11 @@ def parse_decimal(s: str) -> Decimal:
 
 
 def parse_ip(s: str) -> IPAddr:
+    # netip.ParsePrefix / ParseAddr rules where Python's ipaddress is looser: the prefix length is
+    # decimal digits without a leading zero (no netmask form), and IPv6 zones are not addresses
+    addr, slash, bits = s.partition("/")
+    if "%" in addr or (slash and not re.fullmatch(r"0|[1-9][0-9]{0,2}", bits)):
+        raise EvalError("extension", f"error parsing ip value: {s}")
     try:
         if "/" in s:
             net = ipaddress.ip_network(s, strict=False)

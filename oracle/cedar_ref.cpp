@@ -246,7 +246,7 @@ IPv parse_ip(const std::string& s) {
   }
   const int maxp = r.v6 ? 128 : 32;
   if (slash != std::string::npos) {
-    if (!all_digits(pre) || pre.size() > 3) throw bad();
+    if (pre.empty() || !all_digits(pre) || pre.size() > 3 || (pre.size() > 1 && pre[0] == '0')) throw bad();
     int p = std::stoi(pre);
     if (p > maxp) throw bad();
     r.prefix = (uint8_t)p;

@@ -88,7 +88,13 @@ class RefPolicySet:
             for d in st.documents():
                 if d[0] == "doc":
                     _, fname, text, pre, suf = d
-                    s.add_document(fname, text, pre, suf)
+                    try:
+                        s.add_document(fname, text, pre, suf)
+                    except RefError:
+                        # directory / CRD / AVP stores log and skip such a document (directory.go:69-73,
+                        # crd.go:51-55,91-95, verified_permissions.go:89-93)
+                        if not getattr(st, "skip_invalid", False):
+                            raise
                 else:
                     _, pid, fname, text, zero = d
                     s.add_policy(pid, fname, text, zero)

@@ -35,7 +35,13 @@ def oracle_tiers(stores):
         for d in s.documents():
             if d[0] == "doc":
                 _, fname, text, pre, suf = d
-                for i, p in enumerate(co.parse_policies(text, fname)):
+                try:
+                    parsed = co.parse_policies(text, fname)
+                except co.ParseError:
+                    if not s.skip_invalid:  # directory / CRD / AVP stores skip it (directory.go:69-73)
+                        raise
+                    continue
+                for i, p in enumerate(parsed):
                     ps.add(f"{pre}{i}{suf}", p)
             else:
                 _, pid, fname, text, zero = d
@@ -214,6 +220,28 @@ def test_empty_tiers_and_no_entities(ctx):
     stores = [cedargpu.MemoryStore("empty.cedar", ""), cedargpu.MemoryStore("e2.cedar", "// only a comment\n")]
     req = {"principal": {"type": "U", "id": "a"}, "action": {"type": "A", "id": "b"}, "resource": {"type": "R", "id": "c"}}
     check_items(ctx, stores, [([], req)])
+
+
+def test_broken_crd_reload_keeps_other_edits(ctx):
+    """Reload parity for bad documents (crd.go:51-55, 83-95): CRD a is edited, CRD b breaks, CRD c
+    is edited; after the reload a's and c's edits decide requests, b contributes nothing (its old
+    policies are gone), all against the oracle's skip-the-document stores."""
+    g = Gen(4242)
+    crds = [("a", "u-a", g.atomic_policies(6)), ("b", "u-b", g.policies(6)), ("c", "u-c", g.atomic_policies(6))]
+    items = [g.item() for _ in range(300)]
+    tiers = cedargpu.TieredPolicyStores([cedargpu.CRDStore(crds)], ctx=ctx)
+    check_items(ctx, [cedargpu.CRDStore(crds)], items)
+    edited = [("a", "u-a", crds[0][2] + "\nforbid (principal, action == k8s::Action::\"get\", resource);"),
+              ("b", "u-b", "permit (principal, action, resource) when { principal.active ;"),
+              ("c", "u-c", "permit (principal, action, resource);")]
+    tiers.stores = [cedargpu.CRDStore(edited)]
+    tiers.reload()
+    got = tiers.is_authorized_batch(items)
+    otiers = oracle_tiers(tiers.stores)
+    assert len(otiers[0].policies) == len(co.parse_policies(edited[0][2])) + 1
+    for (ents, req), (ok, diag) in zip(items, got):
+        want_ok, want_diag, _ = co.tiered_is_authorized(otiers, co.entities_from_json(ents), co.request_from_json(req))
+        assert (ok, diag) == (want_ok, want_diag.to_go_json()), req
 
 
 def test_hot_reload_epochs(ctx):
@@ -557,3 +585,17 @@ def test_rccl_broadcast_reload(ctx):
         b.wait()
     assert old.decision(0)[0] is True and new.decision(0)[0] is False
     comm.close()
+
+
+# ---------------------------------------------------------------- shapes lowered in round 2
+@pytest.mark.parametrize("name", ["ext_runtime", "deep_nesting", "big_literal", "big_record"])
+def test_lowered_shapes_vs_oracle(ctx, name):
+    """Runtime ip()/decimal(), spilled register slots, set/record literals on the global lane area
+    (GLANE kernel) and policy records read from the stream in place (CHUNK_GLOBAL), vs the Python
+    oracle; then a larger batch vs the C++ oracle."""
+    from lowering_cases import CASES
+    docs, items = CASES[name]()
+    stores = [cedargpu.MemoryStore(f, t) for f, t in docs]
+    check_items(ctx, stores, items)
+    _, many = CASES[name](n=5000, seed=1)
+    check_items_ref(ctx, stores, many)

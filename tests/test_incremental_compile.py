@@ -51,14 +51,44 @@ def test_rebuild_with_tiers_and_static_policy():
 
 
 def test_syntax_error_reports_and_keeps_cache_usable():
+    """A memory store's document that does not parse fails the build (memory.go:17-22); the
+    compiler's cache stays usable."""
     docs = _tenants(5, 5, seed=4)
+    text = "\n".join(d[2] for d in docs)
     comp = cedargpu.Compiler()
-    comp.build([cedargpu.CRDStore(docs)], epoch=1)
-    bad = list(docs) + [("broken", "u", "permit (principal, action, resource) when { ;")]
+    comp.build([cedargpu.MemoryStore("m.cedar", text)], epoch=1)
     try:
-        comp.build([cedargpu.CRDStore(bad)], epoch=2)
+        comp.build([cedargpu.MemoryStore("m.cedar", text + "\npermit (principal, action, resource) when { ;")], epoch=2)
         raise AssertionError("expected a compile error")
     except cedargpu.CompileError:
         pass
-    assert comp.build([cedargpu.CRDStore(docs)], epoch=1) == _fresh([cedargpu.CRDStore(docs)], 1)
+    assert comp.build([cedargpu.MemoryStore("m.cedar", text)], epoch=1) == _fresh([cedargpu.MemoryStore("m.cedar", text)], 1)
+    comp.close()
+
+
+def test_broken_crd_is_skipped_and_other_edits_apply():
+    """crd.go:51-55 / 83-95: a CRD whose content does not parse is logged and contributes no
+    policies -- an update that breaks it drops its old ones -- while every other CRD loads and
+    later edits to them take effect. The same holds for directory files (directory.go:69-73) and
+    AVP statements (verified_permissions.go:89-93)."""
+    docs = _tenants(6, 5, seed=6)
+    comp = cedargpu.Compiler()
+    img1 = comp.build([cedargpu.CRDStore(docs)], epoch=1)
+    assert comp.doc_errors() == []
+    broken = list(docs)
+    broken[2] = (broken[2][0], broken[2][1], "permit (principal, action, resource) when { ;")
+    broken[4] = (broken[4][0], broken[4][1], broken[4][2].replace("permit", "forbid", 1))  # another CRD's edit
+    img2 = comp.build([cedargpu.CRDStore(broken)], epoch=2)
+    errs = comp.doc_errors()
+    assert [e["filename"] for e in errs] == [docs[2][0]] and errs[0]["error"]
+    without = [d for k, d in enumerate(broken) if k != 2]
+    assert img2 == _fresh([cedargpu.CRDStore(without)], 2)
+    assert cedargpu.image_stats(img2)["policies"] == cedargpu.image_stats(img1)["policies"] - 5
+    # directory and AVP stores skip the same way; a memory store does not
+    files = {"a.cedar": docs[0][2], "b.cedar": "forbid (principal,", "c.cedar": docs[1][2]}
+    img3 = comp.build([cedargpu.DirectoryStore(files)], epoch=3)
+    assert [e["filename"] for e in comp.doc_errors()] == ["b.cedar"]
+    assert img3 == _fresh([cedargpu.DirectoryStore({k: v for k, v in files.items() if k != "b.cedar"})], 3)
+    img4 = comp.build([cedargpu.AVPStore([("p1", docs[0][2]), ("p2", "permit (")])], epoch=4)
+    assert img4 == _fresh([cedargpu.AVPStore([("p1", docs[0][2])])], 4)
     comp.close()

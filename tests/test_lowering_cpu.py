@@ -1,0 +1,46 @@
+"""The shapes of tests/lowering_cases.py compile to device images (no CG_E_COMPILE for valid Cedar
+within the documented limits) and the two oracles agree on them; GPU parity is in
+tests/test_gpu_parity.py (test_lowered_shapes_vs_oracle)."""
+import pytest
+
+import cedar_oracle as co
+import cedargpu
+from lowering_cases import CASES
+from test_oracle_cxx import _compare
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_lowered_shapes_compile(name):
+    docs, _ = CASES[name]()
+    for fname, text in docs:
+        img = cedargpu.build_image([cedargpu.MemoryStore(fname, text)])
+        st = cedargpu.image_stats(img)
+        assert st["policies"] == len(co.parse_policies(text, fname)), st
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_lowered_shapes_oracles_agree(name):
+    docs, items = CASES[name](n=120)
+    _compare([docs], items)
+
+
+def test_unknown_functions_and_methods_are_parse_errors():
+    """Both parsers reject names Cedar does not define, so the whole document is rejected (or
+    skipped by the stores that skip bad documents) instead of failing one policy at run time."""
+    for src in ['permit (principal, action, resource) when { foo("x") };',
+                'permit (principal, action, resource) when { ip("1.2.3.4", "x") == ip("1.2.3.4") };',
+                'permit (principal, action, resource) when { context.s.frobnicate() };',
+                'permit (principal, action, resource) when { context.s.contains() };',
+                'permit (principal, action, resource) when { ip("::1").isIpv4(1) };']:
+        with pytest.raises(co.ParseError):
+            co.parse_policies(src, "x.cedar")
+        with pytest.raises(cedargpu.CompileError):
+            cedargpu.build_image([cedargpu.MemoryStore("x.cedar", src)])
+
+
+def test_nesting_beyond_64_slots_is_a_named_limit():
+    deep = "context.a"
+    for _ in range(70):
+        deep = f"1 + ({deep})"
+    with pytest.raises(cedargpu.CompileError, match="64 registers"):
+        cedargpu.build_image([cedargpu.MemoryStore("x.cedar", f"permit (principal, action, resource) when {{ {deep} > 0 }};")])
