@@ -1457,9 +1457,10 @@ __device__ __forceinline__ bool filt_maybe(const uint32_t* bfilt, uint32_t fmask
 }
 
 // probe: (first, count, hmask) of the slot matching key words w0..w6 (+ v0, v1 for level 2)
+// (level-1 probes also return the entry's level-2 bloom in *bloom)
 template <bool ST = false>
 __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uint32_t hash, uint32_t w0, uint2 p, uint2 q,
-                                       uint2 r, uint32_t v0, uint32_t v1, uint32_t& steps) {
+                                       uint2 r, uint32_t v0, uint32_t v1, uint32_t& steps, uint4* bloom = nullptr) {
   uint32_t h = hash & bmask;
   for (;;) {
     if (ST) steps++;
@@ -1468,13 +1469,25 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
     if (x.x == 0) return make_uint3(0, 0, 0);
     if (x.x == w0 && x.y == p.x && x.z == p.y && x.w == q.x) {
       const uint4 y = sl[1], z = sl[2];
-      if (y.x == q.y && y.y == r.x && y.z == r.y && (!(w0 & BT_L2) || (y.w == v0 && z.x == v1)))
+      if (y.x == q.y && y.y == r.x && y.z == r.y && (!(w0 & BT_L2) || (y.w == v0 && z.x == v1))) {
+        if (bloom) *bloom = sl[3];
         return make_uint3(z.y, z.z, z.w);
+      }
     }
     h = (h + 1) & bmask;
   }
 }
-
+// level-2 key hash h2 possibly under the level-1 entry whose bloom is b
+__device__ __forceinline__ bool l2_bloom_maybe(uint4 b, uint32_t h2) {
+  const uint32_t bits = l2_bloom_bits(h2);
+  bool ok = true;
+  for (uint32_t j = 0; j < 3; j++) {
+    const uint32_t x = (bits >> (7 * j)) & 127u;
+    const uint32_t w = x < 64 ? (x < 32 ? b.x : b.y) : (x < 96 ? b.z : b.w);
+    ok = ok && ((w >> (x & 31)) & 1u);
+  }
+  return ok;
+}
 // SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
 // (row -> level-1 probe -> level-2 probe -> head -> atom data) overlap. Collectives (ballot, scan,
 // min, broadcast) are segment-local; loops run while any segment of the wave has work.
@@ -1572,6 +1585,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     }
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
+  uint4 blm = make_uint4(0, 0, 0, 0);  // level-2 bloom of this lane's level-1 entry
   uint32_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // STATS only (per lane)
   for (;;) {
     const bool l2 = sballot(hm != 0) != 0;
@@ -1587,9 +1601,11 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             const uint2 v = wl.hot[seg][h];
             const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
             const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
-            if (filt_maybe(a.bfilt, a.fmask, h2))
-              e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, st[5]);
-            if (STATS) { st[3]++; st[4] += e.y != 0; }
+            if (l2_bloom_maybe(blm, h2)) {
+              if (filt_maybe(a.bfilt, a.fmask, h2))
+                e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, st[5]);
+              if (STATS) { st[3]++; st[4] += e.y != 0; }
+            }
           }
         } else {
           const uint32_t k = kb + sl;
@@ -1613,9 +1629,10 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             kr = key_comp(rkc, ir + 1 - (rn >> 31), c.rt, c.ri, c.blk, c.r_anc);
             w0 = BT_USED | (combo << 16);
             h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
-            if (filt_maybe(a.bfilt, a.fmask, h1)) e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5]);
+            if (filt_maybe(a.bfilt, a.fmask, h1)) e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5], &blm);
             hm = e.z;
-            if (STATS) { st[1]++; st[2] += e.y != 0; }
+            if (STATS) st[1]++;
+            if (STATS) st[2] += e.y != 0;
           }
         }
       }

@@ -948,6 +948,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   using L2 = std::pair<L1, std::array<uint32_t, 3>>;    // (+ h, v0, v1)
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
+  img.key_ents.clear();
   img.combo_mask = 0;
   img.indexed = (n > 0 && img.n_atomic == n) ? 1u : 0u;
   if (!img.indexed) {
@@ -1024,7 +1025,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   kents.erase(std::unique(kents.begin(), kents.end()), kents.end());
   img.key_ents = std::move(kents);
   // groups: [begin, end) ranges of one key; level-1 hmask from the level-2 keys under it
-  struct G { size_t b, e; uint32_t hmask = 0; };
+  struct G { size_t b, e; uint32_t hmask = 0; uint32_t bloom[4] = {0, 0, 0, 0}; };
   std::vector<G> g1, g2;
   for (size_t i = 0; i < r1.size();) {
     size_t j = i;
@@ -1041,7 +1042,15 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   for (size_t a = 0, k = 0; a < g2.size(); a++) {  // both sorted by level-1 key first
     const L1& key = r2[g2[a].b].first.first;
     while (k < g1.size() && r1[g1[k].b].first < key) k++;
-    if (k < g1.size() && r1[g1[k].b].first == key) g1[k].hmask |= 1u << r2[g2[a].b].first.second[0];
+    if (k < g1.size() && r1[g1[k].b].first == key) {
+      const auto& x = r2[g2[a].b].first.second;
+      g1[k].hmask |= 1u << x[0];
+      const uint32_t bits = l2_bloom_bits(bucket_hash2(key_hash(key[0], key[1], key[2], key[3], key[4], key[5], key[6]), x[0], x[1], x[2]));
+      for (uint32_t j = 0; j < 3; j++) {
+        const uint32_t b = (bits >> (7 * j)) & 127u;
+        g1[k].bloom[b >> 5] |= 1u << (b & 31);
+      }
+    }
   }
   mark("buckets");
   // record heads (bucket order) then the ext area (one full record per policy)
@@ -1096,7 +1105,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     const L1& k = r1[g.b].first;
     const uint32_t first = put_heads(r1.begin() + (long)g.b, r1.begin() + (long)g.e);
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], 0, 0, first,
-                                  head - first, g.hmask, 0, 0, 0, 0};
+                                  head - first, g.hmask, g.bloom[0], g.bloom[1], g.bloom[2], g.bloom[3]};
     insert(l1_hash(k), e);
     filt_add(l1_hash(k));
   }

@@ -126,7 +126,9 @@ constexpr uint32_t PW_EXT = PW_LANE;
 // the entry's hmask, with its own value of that slot (or MISSING_W0).
 // btab: open addressing, linear probing, power-of-two slots of BT_WORDS:
 //   [BT_USED | combo << 16 | (BT_L2 | h for level 2), p type, p id, a type, a id, r type, r id,
-//    value w0, value w1, first, count, hmask (level 1), 0, 0, 0, 0]; empty slot: word0 == 0.
+//    value w0, value w1, first, count, hmask (level 1), l2 bloom x 4 (level 1)]; empty: word0 == 0.
+//   The level-1 entry's 128-bit bloom (l2_bloom_bits) holds its level-2 keys: a request probes
+//   level 2 only for (h, value) pairs it admits.
 // Records: bstream[first * HEAD_WORDS ...] fixed heads (descriptor + the first 4 atoms) in bucket
 // order; the head's PW_EXT is the absolute bstream offset of the full variable-length record
 // (descriptor, atoms, atom data) in the ext area, which record-relative offsets address.
@@ -153,6 +155,10 @@ __host__ __device__ constexpr inline uint32_t bucket_hash2(uint32_t l1, uint32_t
   return h;
 }
 
+__host__ __device__ constexpr inline uint32_t l2_bloom_bits(uint32_t h2) {  // three 7-bit positions
+  const uint32_t y = (h2 ^ (h2 >> 13)) * 0x5BD1E995u;
+  return (y >> 11) & 0x1FFFFFu;
+}
 // Key filter of the scope index (bfilt): a blocked Bloom filter over the level-1 and level-2 key
 // hashes, 3 bits in one 64-bit block (two words) per key, about 16 bits per entry. Most probes
 // miss (a request enumerates ~11 level-1 keys and finds ~0.3), and a miss then costs one small,
@@ -333,6 +339,6 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 5;
+constexpr uint32_t IMG_VERSION = 6;
 
 }  // namespace cgi

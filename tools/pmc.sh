@@ -15,4 +15,5 @@ run fetch FETCH_SIZE && \
 run write WRITE_SIZE && \
 run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD && \
 run tcc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE && \
+run tcp TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum && \
 python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $OUT > $OUT/summary.json && cat $OUT/summary.json
