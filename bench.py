@@ -459,7 +459,8 @@ def main():
         if os.path.exists(pmc):
             try:
                 pj = json.load(open(pmc))
-                if pj.get("policies") == args.policies and pj.get("batch") == args.batch:
+                if (pj.get("policies") == args.policies and pj.get("batch") == args.batch
+                        and pj.get("hierarchy", "flat") == args.hierarchy):
                     traffic = pj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None

@@ -4,6 +4,11 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.path.join(_HERE, "libcedargpu.so")
+# Host sanitizer runs only (tools/sanitize.sh): the ASan build of the host engine over the
+# host-memory device stand-in (csrc/device_stub.cpp), for the CPU tests. It has no GPU path.
+SANITIZER_BUILD = bool(os.environ.get("CEDARGPU_SANITIZER_LIB"))
+if SANITIZER_BUILD:
+    lib_path = os.environ["CEDARGPU_SANITIZER_LIB"]
 
 if not os.path.exists(lib_path):
     raise ImportError(f"cedargpu: native library not built ({lib_path}); run `make -C cedar-access-control-for-k8s_amd/csrc`"

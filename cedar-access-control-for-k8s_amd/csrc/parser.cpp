@@ -298,12 +298,12 @@ struct Parser {
   }
   ExprP or_() {
     ExprP l = and_();
-    while (is_op("||")) { next(); auto e = mk(EK::Or); e->kids = {l, and_()}; l = e; }
+    while (is_op("||")) { next(); auto e = mk(EK::Or); { ExprP rhs = and_(); e->kids = {l, rhs}; } l = e; }
     return l;
   }
   ExprP and_() {
     ExprP l = relation();
-    while (is_op("&&")) { next(); auto e = mk(EK::And); e->kids = {l, relation()}; l = e; }
+    while (is_op("&&")) { next(); auto e = mk(EK::And); { ExprP rhs = relation(); e->kids = {l, rhs}; } l = e; }
     return l;
   }
   ExprP relation() {
@@ -315,12 +315,12 @@ struct Parser {
       for (auto& r : rel) {
         if (x.text == r.first) {
           next();
-          auto e = mk(EK::Bin); e->op = r.second; e->kids = {l, add()};
+          auto e = mk(EK::Bin); e->op = r.second; { ExprP rhs = add(); e->kids = {l, rhs}; }
           return e;
         }
       }
     }
-    if (is_kw("in")) { next(); auto e = mk(EK::Bin); e->op = BinOp::In; e->kids = {l, add()}; return e; }
+    if (is_kw("in")) { next(); auto e = mk(EK::Bin); e->op = BinOp::In; { ExprP rhs = add(); e->kids = {l, rhs}; } return e; }
     if (is_kw("has")) {
       next();
       const Tok& k = next();
@@ -354,13 +354,13 @@ struct Parser {
     ExprP l = mult();
     while (is_op("+") || is_op("-")) {
       bool plus = next().text == "+";
-      auto e = mk(EK::Bin); e->op = plus ? BinOp::Add : BinOp::Sub; e->kids = {l, mult()}; l = e;
+      auto e = mk(EK::Bin); e->op = plus ? BinOp::Add : BinOp::Sub; { ExprP rhs = mult(); e->kids = {l, rhs}; } l = e;
     }
     return l;
   }
   ExprP mult() {
     ExprP l = unary();
-    while (is_op("*")) { next(); auto e = mk(EK::Bin); e->op = BinOp::Mul; e->kids = {l, unary()}; l = e; }
+    while (is_op("*")) { next(); auto e = mk(EK::Bin); e->op = BinOp::Mul; { ExprP rhs = unary(); e->kids = {l, rhs}; } l = e; }
     return l;
   }
   ExprP unary() {

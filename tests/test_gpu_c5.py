@@ -1,0 +1,123 @@
+"""C5 under -m gpu: the 100k-policy multi-tenant image (1,000 tenant Policy CRDs) and a hot reload
+while a batch bound to the old epoch is still in flight (crd.go:45-118 mutates the
+policy set per CRD event while requests keep being served).
+
+The reload's new epoch carries three CRD events at once: one tenant's permits turned into forbids
+(update), one tenant's CRD replaced by text that does not parse (skipped, crd.go:51-55,91-95 — its
+old policies are removed, the others' edits still apply) and one tenant deleted. The in-flight
+batch must finish on the epoch it was submitted against; the next batch must see every edit. Both
+are checked against the C++ oracle (oracle/cedar_ref.cpp) built from the matching store snapshot."""
+import json
+import random
+import re
+
+import pytest
+
+import cedargpu
+from cedargpu import synth
+from cedar_ref import RefPolicySet, items_json
+import cedar_oracle as co
+import k8s_model as km
+
+pytestmark = pytest.mark.gpu
+
+N_REQ = 600
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    assert cedargpu.device_count() >= 1, "GPU tests need a GPU"
+    c = cedargpu.Context(0)
+    yield c
+    c.close()
+
+
+def _items(sars):
+    out = []
+    for s in sars:
+        a = km.attributes_from_sar(s)
+        em, req = km.record_to_cedar_resource(a)
+        out.append((co.entities_to_json(em), co.request_to_json(req)))
+    return out
+
+
+_PERMIT = re.compile(r'principal in k8s::Group::"([^"]+)",\s*action in \[([^\]]*)\],.*?resource\.namespace == "([^"]+)" '
+                     r'&& resource\.resource == "([^"]+)"', re.S)
+
+
+def _targeted(docs, tenants, n_each, seed):
+    """SARs that a tenant's permits (and, for delete / update of prod-* names, its forbids) decide."""
+    r = random.Random(seed)
+    api = {res: (grp, ver) for grp, ver, res in synth.RESOURCES}
+    out = []
+    for t in tenants:
+        pols = _PERMIT.findall(docs[t][2])
+        for k in range(n_each):
+            g, acts, ns, res = r.choice(pols)
+            verb = r.choice(re.findall(r'"([^"]+)"', acts))
+            grp, ver = api[res]
+            name = r.choice(["", "web-1", "prod-db"])
+            out.append(synth.make_sar(f"user-{t}-{k}", f"uid-{k}", [g, "system:authenticated"], verb, ns=ns, group=grp,
+                                      version=ver, resource=res, name=name))
+    return out
+
+
+def _want(docs, items):
+    ref = RefPolicySet.from_stores([cedargpu.CRDStore(docs)])
+    ref.load_items(items_json(items))
+    got = ref.evaluate(16)
+    ref.close()
+    return [(ok, diag) for ok, _, diag, _ in got]
+
+
+def _batch(ctx, items):
+    b = ctx.batch()
+    b.add_json(json.dumps([{"entities": e, "request": r} for e, r in items]))
+    return b
+
+
+def _results(b):
+    return [(b.decision(i)[0], b.diagnostic(i)) for i in range(len(b))]
+
+
+def test_c5_100k_reload_with_batch_in_flight(ctx):
+    pop = synth.Population(seed=7, n_namespaces=1000)
+    docs = synth.multitenant_policies(100_000, seed=51, pop=pop)
+    # requests aimed at a few tenants, the edited ones among them, plus random traffic
+    sars = synth.random_sars(N_REQ // 2, seed=5001, pop=pop) + _targeted(docs, (3, 500, 501, 502, 777), N_REQ // 10, 9)
+    items = _items(sars)
+
+    comp = cedargpu.Compiler()
+    img1 = comp.build([cedargpu.CRDStore(docs)], epoch=1)
+    assert cedargpu.image_stats(img1)["policies"] == 100_000
+    ctx.load(img1, 1)
+
+    docs2 = list(docs)
+    name, uid, text = docs2[500]
+    docs2[500] = (name, uid, text.replace("permit", "forbid"))                  # update
+    docs2[501] = (docs2[501][0], docs2[501][1], "permit (principal, action, resource) when { 1 + };")  # broken
+    del docs2[502]                                                              # delete
+
+    # batch A is submitted against epoch 1; epoch 2 is compiled and activated while A runs
+    a = _batch(ctx, items)
+    a.submit()
+    img2 = comp.build([cedargpu.CRDStore(docs2)], epoch=2)
+    errs = comp.doc_errors()
+    assert [e["filename"] for e in errs] == [docs2[501][0]], errs
+    st = comp.cache_stats()
+    assert st["hits"] >= 997, st  # only the edited documents were parsed again
+    comp.close()
+    ctx.load(img2, 2)
+    b = _batch(ctx, items)
+    b.submit()
+    a.wait()
+    b.wait()
+    got_a, got_b = _results(a), _results(b)
+    a.close()
+    b.close()
+
+    want_a, want_b = _want(docs, items), _want(docs2, items)
+    assert got_a == want_a
+    assert got_b == want_b
+    # the edits are visible: some decision changed between the epochs
+    assert sum(1 for x, y in zip(want_a, want_b) if x != y) > 0
