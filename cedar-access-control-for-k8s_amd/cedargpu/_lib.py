@@ -79,6 +79,8 @@ _SIGS = {
     "cg_last_error": (cstr, [P]),
     "cg_ctx_inject_fault": (ctypes.c_int, [P, ctypes.c_int, u64]),
     "cg_image_load": (ctypes.c_int, [P, P, sz, u64]),
+    "cg_image_load_device": (ctypes.c_int, [P, P, sz, u64, P]),
+    "cg_image_load_peer": (ctypes.c_int, [P, P, u64]),
     "cg_image_activate": (ctypes.c_int, [P, u64]),
     "cg_image_active": (ctypes.c_int, [P, ctypes.POINTER(u64)]),
     "cg_image_unload": (ctypes.c_int, [P, u64]),
@@ -110,6 +112,8 @@ _SIGS = {
     "cg_batch_admit": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), P, sz,
                                       ctypes.POINTER(sz)]),
     "cg_admission_to_cedar_json": (ctypes.c_int, [cstr, sz, P, sz, ctypes.POINTER(sz)]),
+    "cg_queue_create_multi": (ctypes.c_int, [ctypes.POINTER(P), u32, u32, u32, ctypes.POINTER(P)]),
+    "cg_queue_gpu_stats": (ctypes.c_int, [P, u32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     "cg_queue_create": (ctypes.c_int, [P, u32, u32, ctypes.POINTER(P)]),
     "cg_queue_destroy": (None, [P]),
     "cg_queue_last_error": (cstr, []),

@@ -272,6 +272,14 @@ class Context:
             if rc:
                 raise _err(rc, self.last_error())
 
+    def load_peer(self, src: "Context", epoch: int, activate: bool = True):
+        """cg_image_load_peer: `src`'s image for `epoch`, host tables shared, device copy GPU to GPU."""
+        rc = lib.cg_image_load_peer(self._h, src._h, epoch)
+        if rc:
+            raise _err(rc, self.last_error())
+        if activate:
+            self.activate(epoch)
+
     def activate(self, epoch: int):
         rc = lib.cg_image_activate(self._h, epoch)
         if rc:
@@ -435,12 +443,26 @@ class Queue:
     SubjectAccessReview; `is_authorized` is TieredPolicyStores.IsAuthorized for one Cedar-JSON item.
     ctypes releases the GIL for the duration of each call, so Python threads batch together."""
 
-    def __init__(self, ctx: Context, max_batch: int = 4096, max_delay_us: int = 0):
-        self.ctx = ctx
+    def __init__(self, ctx: Union[Context, Sequence[Context]], max_batch: int = 4096, max_delay_us: int = 0):
+        """`ctx`: one context, or one per GPU (cg_queue_create_multi: batches dealt to the least
+        loaded GPU; requests encode against the first context's active image)."""
+        ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx]
+        self.ctx = ctxs[0]
+        self.ctxs = ctxs
         self._h = _P()
-        rc = lib.cg_queue_create(ctx._h, max_batch, max_delay_us, ctypes.byref(self._h))
+        arr = (_P * len(ctxs))(*[c._h for c in ctxs])
+        rc = lib.cg_queue_create_multi(arr, len(ctxs), max_batch, max_delay_us, ctypes.byref(self._h))
         if rc:
             raise _err(rc, "queue create failed")
+
+    def gpu_stats(self) -> List[dict]:
+        """Per context: batches and requests it ran."""
+        out = []
+        for k in range(len(self.ctxs)):
+            b, r = ctypes.c_uint64(), ctypes.c_uint64()
+            lib.cg_queue_gpu_stats(self._h, k, ctypes.byref(b), ctypes.byref(r))
+            out.append({"batches": b.value, "requests": r.value})
+        return out
 
     def close(self):
         if self._h:

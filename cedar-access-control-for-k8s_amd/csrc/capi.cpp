@@ -503,10 +503,58 @@ int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch) {
   img->epoch = epoch;
   auto li = std::make_shared<LoadedImage>();
   li->host = img;
-  if (dev_image_upload(ctx->device, *img, &li->dev)) { ctx->err = dev_last_error(); return CG_E_DEVICE; }
+  if (dev_image_upload(ctx->device, *img, (const uint8_t*)image, &li->dev)) { ctx->err = dev_last_error(); return CG_E_DEVICE; }
   std::lock_guard<std::mutex> g(ctx->mu);
   li->serial = ctx->next_serial++;
   ctx->images[epoch] = li;
+  return CG_OK;
+}
+
+int cg_image_load_device(cg_ctx* ctx, void* dev_blob, size_t len, uint64_t epoch, const void* host_blob) {
+  if (!ctx || !dev_blob) return CG_E_ARG;
+  std::vector<uint8_t> copy;
+  if (!host_blob) {  // the host side of the image (encoder tables, reasons' metadata) from the device blob
+    try {
+      copy.resize(len);
+    } catch (const std::exception& e) {
+      ctx->err = e.what();
+      return CG_E_ARG;
+    }
+    if (dev_to_host(ctx->device, dev_blob, len, copy.data())) { ctx->err = dev_last_error(); return CG_E_DEVICE; }
+    host_blob = copy.data();
+  }
+  std::shared_ptr<Image> img;
+  try {
+    img = Image::deserialize((const uint8_t*)host_blob, len);
+  } catch (const std::exception& e) {
+    ctx->err = e.what();
+    return CG_E_ARG;
+  }
+  img->epoch = epoch;
+  auto li = std::make_shared<LoadedImage>();
+  li->host = img;
+  if (dev_image_adopt(ctx->device, *img, dev_blob, &li->dev)) { ctx->err = dev_last_error(); return CG_E_DEVICE; }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  li->serial = ctx->next_serial++;
+  ctx->images[epoch] = li;
+  return CG_OK;
+}
+
+int cg_image_load_peer(cg_ctx* dst, cg_ctx* src, uint64_t epoch) {
+  if (!dst || !src) return CG_E_ARG;
+  std::shared_ptr<LoadedImage> from;
+  {
+    std::lock_guard<std::mutex> g(src->mu);
+    auto it = src->images.find(epoch);
+    if (it == src->images.end()) { dst->err = "no image loaded for epoch on the source context"; return CG_E_STATE; }
+    from = it->second;
+  }
+  auto li = std::make_shared<LoadedImage>();
+  li->host = from->host;  // one host image (encoder tables, metadata) shared by both contexts
+  if (dev_image_copy(dst->device, *from->host, from->dev, &li->dev)) { dst->err = dev_last_error(); return CG_E_DEVICE; }
+  std::lock_guard<std::mutex> g(dst->mu);
+  li->serial = dst->next_serial++;
+  dst->images[epoch] = li;
   return CG_OK;
 }
 

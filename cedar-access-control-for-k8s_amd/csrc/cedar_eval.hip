@@ -1902,24 +1902,19 @@ int dev_stream_sync(void* stream) {
   return 0;
 }
 
-int dev_image_upload(int device, const Image& img, DevImage* out) {
-  HIPCHK(hipSetDevice(device), "hipSetDevice");
-  DevImage d;
+// scalars and array pointers of a device image whose region sits at `base` (blob offset `origin`)
+static void image_fields(const Image& img, int device, void* base, uint64_t origin, DevImage& d) {
   d.device = device;
-  hipStream_t s = nullptr;
-  int rc;
-  if ((rc = up(&d.pstream, img.pstream, d.bytes, s))) return rc;
-  if ((rc = up(&d.tier_cend, img.tier_cend, d.bytes, s))) return rc;
-  if ((rc = up(&d.chunks, img.chunks, d.bytes, s))) return rc;
-  if ((rc = up(&d.cpool, img.cpool, d.bytes, s))) return rc;
-  if ((rc = up(&d.gstr_off, img.gstr_off, d.bytes, s))) return rc;
-  if ((rc = up(&d.hot, img.hot, d.bytes, s))) return rc;
-  if ((rc = up(&d.act, img.act, d.bytes, s))) return rc;
-  if ((rc = up(&d.btab, img.btab, d.bytes, s))) return rc;
-  if ((rc = up(&d.bfilt, img.bfilt, d.bytes, s))) return rc;
-  if ((rc = up(&d.bstream, img.bstream, d.bytes, s))) return rc;
-  if ((rc = up(&d.srows, img.srows, d.bytes, s))) return rc;
-  if ((rc = up(&d.shash, img.shash, d.bytes, s))) return rc;
+  d.base = base;
+  d.origin = origin;
+  d.region = img.dev_end - img.dev_begin;
+  d.bytes = d.region;
+  auto at = [&](uint32_t k) { return (uint8_t*)base + (img.dev_off[k] - origin); };
+  d.pstream = (uint32_t*)at(DS_PSTREAM); d.tier_cend = (uint32_t*)at(DS_TIER_CEND); d.chunks = (uint32_t*)at(DS_CHUNKS);
+  d.cpool = (uint32_t*)at(DS_CPOOL); d.gstr_off = (uint32_t*)at(DS_GSTR_OFF); d.hot = (uint32_t*)at(DS_HOT);
+  d.act = (uint32_t*)at(DS_ACT); d.btab = (uint32_t*)at(DS_BTAB); d.bfilt = (uint32_t*)at(DS_BFILT);
+  d.bstream = (uint32_t*)at(DS_BSTREAM); d.srows = (uint32_t*)at(DS_SROWS); d.shash = (uint32_t*)at(DS_SHASH);
+  d.gstr_bytes = at(DS_GSTR_BYTES);
   d.n_static = img.n_static();
   d.lane_need = img.lane_need;
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
@@ -1930,23 +1925,63 @@ int dev_image_upload(int device, const Image& img, DevImage* out) {
   d.n_act = (uint32_t)img.act.size() / 2;
   d.has_bytecode = img.n_atomic < img.n_pol() ? 1u : 0u;
   d.amask_ok = img.amask_ok;
-  if ((rc = up(&d.gstr_bytes, img.gstr_bytes, d.bytes, s))) return rc;
-  HIPCHK(hipStreamSynchronize(s), "sync image upload");
   d.n_pol = img.n_pol();
   d.n_tiers = img.n_tiers();
   d.n_gstr = img.n_gstr();
   d.n_hot = (uint32_t)img.hot.size() / HOT_WORDS;
+}
+
+int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage* out) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  const size_t n = img.dev_end - img.dev_begin;
+  void* base = nullptr;
+  HIPCHK(hipMalloc(&base, std::max<size_t>(n, DS_ALIGN)), "hipMalloc image");
+  if (hipMemcpy(base, blob + img.dev_begin, n, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(base);
+    g_err = "H2D image";
+    return -5;
+  }
+  DevImage d;
+  image_fields(img, device, base, img.dev_begin, d);
   *out = d;
+  return 0;
+}
+
+int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* out) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  const size_t n = img.dev_end - img.dev_begin;
+  void* base = nullptr;
+  HIPCHK(hipMalloc(&base, std::max<size_t>(n, DS_ALIGN)), "hipMalloc image");
+  const uint8_t* from = (const uint8_t*)src.base + (img.dev_begin - src.origin);
+  const hipError_t e = device == src.device ? hipMemcpy(base, from, n, hipMemcpyDeviceToDevice)
+                                            : hipMemcpyPeer(base, device, from, src.device, n);
+  if (e != hipSuccess) {
+    (void)hipFree(base);
+    return fail(e, "peer copy of the image");
+  }
+  DevImage d;
+  image_fields(img, device, base, img.dev_begin, d);
+  *out = d;
+  return 0;
+}
+
+int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out) {
+  DevImage d;
+  image_fields(img, device, dev_blob, 0, d);
+  *out = d;
+  return 0;
+}
+
+int dev_to_host(int device, const void* src, size_t n, void* dst) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost), "D2H");
   return 0;
 }
 
 void dev_image_free(DevImage* d) {
   if (d->device < 0) return;
   (void)hipSetDevice(d->device);
-  for (void* p : {(void*)d->pstream, (void*)d->tier_cend, (void*)d->chunks, (void*)d->cpool, (void*)d->gstr_off,
-                  (void*)d->hot, (void*)d->act, (void*)d->gstr_bytes, (void*)d->btab, (void*)d->bfilt,
-                  (void*)d->bstream, (void*)d->srows, (void*)d->shash})
-    if (p) (void)hipFree(p);
+  if (d->base) (void)hipFree(d->base);
   *d = DevImage();
 }
 

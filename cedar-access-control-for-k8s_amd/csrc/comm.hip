@@ -4,7 +4,7 @@
 // replica of the compiled image. On a reload (the reference swaps the *cedar.PolicySet at
 // internal/server/store/directory.go:81 and verified_permissions.go:99, and mutates it in place
 // at crd.go:62,85,102,114), rank `root` compiles the new image once and one ncclBroadcast ships the
-// serialized blob to every GPU; each rank then loads and activates it as the new epoch.
+// serialized blob straight into each GPU's image storage; each rank activates it as the new epoch.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -69,40 +69,62 @@ void cg_comm_destroy(cg_comm* c) {
 const char* cg_comm_last_error(cg_comm* c) { return c ? c->err.c_str() : g_comm_err.c_str(); }
 
 // Collective: every rank calls it. On `root`, image/len are the compiled blob; elsewhere they are
-// ignored. The blob goes through one device buffer per rank; every rank then loads it into ctx as
-// `epoch` (and activates it when activate != 0). *out_len (optional) receives the blob size.
+// ignored. The blob goes to device memory once on the root (one H2D copy) and one ncclBroadcast
+// writes it into a device buffer on every other rank (xGMI, RCCL's own pipelining, no per-piece
+// host sync); each rank's buffer then becomes its image's device storage as is
+// (cg_image_load_device: no re-upload), loaded as `epoch` and activated when activate != 0.
+// Every rank but the root copies the blob back once for its host-side tables. *out_len
+// (optional) receives the blob size. A failure leaves a rank's active image as it was: a rank that
+// cannot allocate makes every rank fail before the blob moves (an all-reduce of readiness), and a
+// decode error after the broadcast is local to its rank; no rank is left waiting in a collective.
 int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, size_t len, uint64_t epoch, int activate,
                        size_t* out_len) {
   if (!ctx || !c || root < 0 || root >= c->nranks) return CG_E_ARG;
-  if (c->rank == root && !image) return CG_E_ARG;
   auto fail = [&](const std::string& m) { c->err = m; return CG_E_DEVICE; };
   if (hipSetDevice(c->device) != hipSuccess) return fail("hipSetDevice failed");
-  uint64_t n = c->rank == root ? (uint64_t)len : 0;
-  void* d = nullptr;
-  const size_t cap = 1 << 20;
-  if (hipMalloc(&d, cap) != hipSuccess) return fail("hipMalloc failed");
-  std::vector<uint8_t> blob;
-  int rc = CG_OK;
-  do {
-    // length first (8 bytes), then the blob in device-buffer-sized pieces
-    if (hipMemcpy(d, &n, 8, hipMemcpyHostToDevice) != hipSuccess) { rc = fail("H2D failed"); break; }
-    ncclResult_t r = ncclBroadcast(d, d, 8, ncclUint8, root, c->nccl, c->stream);
-    if (r != ncclSuccess || hipStreamSynchronize(c->stream) != hipSuccess) { rc = fail(std::string("ncclBroadcast: ") + ncclGetErrorString(r)); break; }
-    if (hipMemcpy(&n, d, 8, hipMemcpyDeviceToHost) != hipSuccess) { rc = fail("D2H failed"); break; }
-    if (c->rank != root) blob.resize((size_t)n);
-    const uint8_t* src = c->rank == root ? (const uint8_t*)image : nullptr;
-    for (uint64_t off = 0; off < n && rc == CG_OK; off += cap) {
-      const size_t piece = (size_t)std::min<uint64_t>(cap, n - off);
-      if (c->rank == root && hipMemcpy(d, src + off, piece, hipMemcpyHostToDevice) != hipSuccess) { rc = fail("H2D failed"); break; }
-      r = ncclBroadcast(d, d, piece, ncclUint8, root, c->nccl, c->stream);
-      if (r != ncclSuccess || hipStreamSynchronize(c->stream) != hipSuccess) { rc = fail(std::string("ncclBroadcast: ") + ncclGetErrorString(r)); break; }
-      if (c->rank != root && hipMemcpy(blob.data() + off, d, piece, hipMemcpyDeviceToHost) != hipSuccess) { rc = fail("D2H failed"); break; }
-    }
-  } while (0);
-  (void)hipFree(d);
-  if (rc) return rc;
-  const void* img = c->rank == root ? image : (const void*)blob.data();
-  if ((rc = cg_image_load(ctx, img, (size_t)n, epoch))) { c->err = cg_last_error(ctx); return rc; }
+  // the root's length, or 0 when it has no blob: every rank then stops after this first collective
+  uint64_t n = (c->rank == root && image) ? (uint64_t)len : 0;
+  uint64_t* dn = nullptr;
+  if (hipMalloc((void**)&dn, 8) != hipSuccess) return fail("hipMalloc failed");
+  ncclResult_t r = ncclSuccess;
+  bool ok = hipMemcpy(dn, &n, 8, hipMemcpyHostToDevice) == hipSuccess &&
+            (r = ncclBroadcast(dn, dn, 8, ncclUint8, root, c->nccl, c->stream)) == ncclSuccess &&
+            hipStreamSynchronize(c->stream) == hipSuccess && hipMemcpy(&n, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
+  if (!ok) {
+    (void)hipFree(dn);
+    return fail(std::string("length broadcast: ") + ncclGetErrorString(r));
+  }
+  if (n == 0) {
+    (void)hipFree(dn);
+    c->err = "the root has no image to broadcast";
+    return CG_E_ARG;
+  }
+  // every rank allocates its receive buffer (the root also stages the blob into it), then all agree
+  // (min over ranks) before the blob moves: a rank whose allocation failed makes every rank return
+  // CG_E_DEVICE instead of leaving the others inside a broadcast it never joins
+  void* buf = nullptr;
+  uint64_t ready = hipMalloc(&buf, (size_t)n) == hipSuccess ? 1u : 0u;
+  if (ready && c->rank == root && hipMemcpy(buf, image, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) ready = 0;
+  ok = hipMemcpy(dn, &ready, 8, hipMemcpyHostToDevice) == hipSuccess &&
+       (r = ncclAllReduce(dn, dn, 1, ncclUint64, ncclMin, c->nccl, c->stream)) == ncclSuccess &&
+       hipStreamSynchronize(c->stream) == hipSuccess && hipMemcpy(&ready, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipFree(dn);
+  if (!ok || !ready) {
+    if (buf) (void)hipFree(buf);
+    return fail(!ok ? std::string("readiness all-reduce: ") + ncclGetErrorString(r)
+                    : std::string("a rank could not allocate or stage the image buffer"));
+  }
+  r = ncclBroadcast(buf, buf, (size_t)n, ncclUint8, root, c->nccl, c->stream);
+  if (r != ncclSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+    (void)hipFree(buf);
+    return fail(std::string("image broadcast: ") + ncclGetErrorString(r));
+  }
+  int rc = cg_image_load_device(ctx, buf, (size_t)n, epoch, c->rank == root ? image : nullptr);
+  if (rc) {
+    (void)hipFree(buf);
+    c->err = cg_last_error(ctx);
+    return rc;
+  }
   if (activate && (rc = cg_image_activate(ctx, epoch))) { c->err = cg_last_error(ctx); return rc; }
   if (out_len) *out_len = (size_t)n;
   return CG_OK;

@@ -1326,16 +1326,21 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
 
 // ---------------------------------------------------------------------------------------------
 // Serialization: a versioned little-endian blob (what a Go-side compiler would hand to
-// cg_image_load). Sections are u32-length-prefixed.
+// cg_image_load): header, the device-region section table, the device region (image.h
+// DevSection: raw arrays at 256-byte-aligned offsets), then the host-only part (u32-length-
+// prefixed sections).
 // ---------------------------------------------------------------------------------------------
 namespace {
 struct W {
   std::vector<uint8_t> b;
   void u32(uint32_t v) { for (int k = 0; k < 4; k++) b.push_back((uint8_t)(v >> (8 * k))); }
   void u64(uint64_t v) { u32((uint32_t)v); u32((uint32_t)(v >> 32)); }
+  void put64(size_t at, uint64_t v) { for (int k = 0; k < 8; k++) b[at + k] = (uint8_t)(v >> (8 * k)); }
   void vec(const std::vector<uint32_t>& v) { u32((uint32_t)v.size()); for (auto x : v) u32(x); }
   void bytes(const std::vector<uint8_t>& v) { u32((uint32_t)v.size()); b.insert(b.end(), v.begin(), v.end()); }
   void str(const std::string& s) { u32((uint32_t)s.size()); b.insert(b.end(), s.begin(), s.end()); }
+  void align(size_t a) { b.resize((b.size() + a - 1) / a * a, 0); }
+  void raw(const void* p, size_t n) { b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + n); }
 };
 struct R {
   const uint8_t* p; const uint8_t* e;
@@ -1351,11 +1356,27 @@ struct R {
 std::vector<uint8_t> Image::serialize() const {
   W w;
   w.u32(IMG_MAGIC); w.u32(IMG_VERSION); w.u64(epoch);
-  w.vec(pol); w.vec(tier_end); w.vec(code); w.vec(cpool); w.vec(gstr_off); w.vec(hot); w.bytes(gstr_bytes);
-  w.vec(act); w.u32(amask_ok); w.u32(n_atomic);
-  w.vec(pstream); w.vec(chunks); w.vec(tier_cend);
-  w.vec(btab); w.vec(bfilt); w.vec(bstream); w.u32(indexed); w.u32(combo_mask);
-  w.vec(srows); w.vec(shash); w.u32(lane_need);
+  const size_t table = w.b.size();
+  for (uint32_t k = 0; k < 2 * DS_COUNT + 2; k++) w.u64(0);  // (offset, bytes) per section, begin, end
+  auto words = [](const std::vector<uint32_t>& v) { return std::make_pair((const void*)v.data(), v.size() * 4); };
+  const std::pair<const void*, size_t> sec[DS_COUNT] = {
+      words(pstream), words(tier_cend), words(chunks), words(cpool), words(gstr_off), words(hot), words(act),
+      words(btab), words(bfilt), words(bstream), words(srows), words(shash),
+      std::make_pair((const void*)gstr_bytes.data(), gstr_bytes.size())};
+  w.align(DS_ALIGN);
+  const size_t begin = w.b.size();
+  for (uint32_t k = 0; k < DS_COUNT; k++) {
+    w.align(DS_ALIGN);
+    w.put64(table + 16 * k, w.b.size());
+    w.put64(table + 16 * k + 8, sec[k].second);
+    w.raw(sec[k].first, sec[k].second);
+  }
+  w.raw("\0\0\0\0", 4);  // no section ends the region: a kernel may read one word of an empty one
+  w.align(DS_ALIGN);
+  w.put64(table + 16 * DS_COUNT, begin);
+  w.put64(table + 16 * DS_COUNT + 8, w.b.size());
+  w.vec(pol); w.vec(tier_end); w.vec(code);
+  w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need);
   w.u32((uint32_t)key_ents.size());
   for (uint64_t k : key_ents) w.u64(k);
   w.u32((uint32_t)strings.size());
@@ -1377,16 +1398,35 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   if (r.u32() != IMG_VERSION) throw CedarError("unsupported image version");
   auto img = std::make_shared<Image>();
   img->epoch = r.u64();
-  img->pol = r.vec(); img->tier_end = r.vec(); img->code = r.vec(); img->cpool = r.vec();
-  img->gstr_off = r.vec(); img->hot = r.vec(); img->gstr_bytes = r.bytes();
-  img->act = r.vec(); img->amask_ok = r.u32(); img->n_atomic = r.u32();
-  img->pstream = r.vec(); img->chunks = r.vec(); img->tier_cend = r.vec();
-  img->btab = r.vec(); img->bfilt = r.vec(); img->bstream = r.vec(); img->indexed = r.u32(); img->combo_mask = r.u32();
+  for (uint32_t k = 0; k < DS_COUNT; k++) { img->dev_off[k] = r.u64(); img->dev_len[k] = r.u64(); }
+  img->dev_begin = r.u64();
+  img->dev_end = r.u64();
+  if (img->dev_begin % DS_ALIGN || img->dev_end % DS_ALIGN || img->dev_begin > img->dev_end || img->dev_end > n ||
+      img->dev_begin < (size_t)(r.p - p))
+    throw CedarError("corrupt image (device region)");
+  auto sec_words = [&](uint32_t k, std::vector<uint32_t>& v) {
+    const uint64_t off = img->dev_off[k], len = img->dev_len[k];
+    if (off % DS_ALIGN || off < img->dev_begin || len % 4 || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
+    v.resize(len / 4);
+    std::memcpy(v.data(), p + off, len);
+  };
+  sec_words(DS_PSTREAM, img->pstream); sec_words(DS_TIER_CEND, img->tier_cend); sec_words(DS_CHUNKS, img->chunks);
+  sec_words(DS_CPOOL, img->cpool); sec_words(DS_GSTR_OFF, img->gstr_off); sec_words(DS_HOT, img->hot);
+  sec_words(DS_ACT, img->act); sec_words(DS_BTAB, img->btab); sec_words(DS_BFILT, img->bfilt);
+  sec_words(DS_BSTREAM, img->bstream); sec_words(DS_SROWS, img->srows); sec_words(DS_SHASH, img->shash);
+  {
+    const uint64_t off = img->dev_off[DS_GSTR_BYTES], len = img->dev_len[DS_GSTR_BYTES];
+    if (off % DS_ALIGN || off < img->dev_begin || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
+    img->gstr_bytes.assign(p + off, p + off + len);
+  }
+  r.p = p + img->dev_end;
+  img->pol = r.vec(); img->tier_end = r.vec(); img->code = r.vec();
+  img->amask_ok = r.u32(); img->n_atomic = r.u32(); img->indexed = r.u32(); img->combo_mask = r.u32();
+  img->lane_need = r.u32();
   {
     const size_t nb = img->btab.size() / BT_WORDS, nf = img->bfilt.size();
     if (!nb || (nb & (nb - 1)) || nf < 2 || (nf & (nf - 1))) throw CedarError("corrupt image (scope index)");
   }
-  img->srows = r.vec(); img->shash = r.vec(); img->lane_need = r.u32();
   if (img->lane_need > LANE_MAX) throw CedarError("corrupt image (lane scratch)");
   {
     const size_t ns = img->shash.size() / SH_WORDS;

@@ -19,6 +19,10 @@ struct DevImage {
   uint32_t *btab = nullptr, *bfilt = nullptr, *bstream = nullptr;  // scope index
   uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
   uint8_t* gstr_bytes = nullptr;
+  // the one device allocation holding the image's device region (image.h DevSection); the arrays
+  // above point into it at (blob offset - origin)
+  void* base = nullptr;
+  uint64_t origin = 0, region = 0;  // blob offset of base[0]; region bytes (dev_end - dev_begin)
   uint32_t n_static = 0, smask = 0;
   uint32_t lane_need = 0;  // lane-scratch words per request (> LANE_WORDS: the GLANE stream kernel)
   uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0, n_act = 0, amask_ok = 0, has_bytecode = 1, indexed = 0, bmask = 0, fmask = 0, combo_mask = 0;
@@ -70,7 +74,17 @@ const char* dev_last_error();
 int dev_count(int* n);
 int dev_select(int device);
 int dev_synchronize(int device);
-int dev_image_upload(int device, const Image& img, DevImage* out);
+// Device copy of an image read from `blob` (Image::deserialize): its device region in one
+// allocation and one H2D copy.
+int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage* out);
+// Device copy on `device` of an image already on another (or the same) device: one peer copy of
+// the region (xGMI between GPUs).
+int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* out);
+// Adopts `dev_blob`, the whole serialized blob already in device memory on `device` (hipMalloc'd,
+// e.g. the buffer a broadcast wrote): the arrays point into it, and dev_image_free frees it.
+int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out);
+// Copies n bytes of device memory on `device` to host memory (pinned staging, one copy).
+int dev_to_host(int device, const void* src, size_t n, void* dst);
 void dev_image_free(DevImage* d);
 int dev_pool_create(int device, DevPool** out);
 void dev_pool_destroy(DevPool* p);

@@ -44,22 +44,56 @@ struct DevPool {
 };
 
 const char* dev_last_error() { return g_err.c_str(); }
-int dev_count(int* n) { *n = 1; return 0; }
+int dev_count(int* n) { *n = 8; return 0; }  // contexts 0..7 (multi-context queue tests)
 int dev_select(int) { return 0; }
 int dev_synchronize(int) { return 0; }
 
-int dev_image_upload(int device, const Image& img, DevImage* out) {
-  DevImage d;
+static void stub_image(int device, const Image& img, DevImage& d) {
   d.device = device;
   d.n_pol = img.n_pol();
   d.n_tiers = img.n_tiers();
   d.indexed = img.indexed;
   d.lane_need = img.lane_need;
-  d.bytes = img.pstream.size() * 4 + img.cpool.size() * 4 + img.btab.size() * 4 + img.bstream.size() * 4;
+  d.region = img.dev_end - img.dev_begin;
+  d.bytes = d.region;
+}
+int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage* out) {
+  DevImage d;
+  stub_image(device, img, d);
+  d.base = std::malloc(std::max<size_t>(d.region, 1));
+  if (!d.base) { g_err = "out of memory"; return -5; }
+  std::memcpy(d.base, blob + img.dev_begin, d.region);  // the H2D copy of the device region
+  d.origin = img.dev_begin;
   *out = d;
   return 0;
 }
-void dev_image_free(DevImage* d) { *d = DevImage(); }
+int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* out) {
+  DevImage d;
+  stub_image(device, img, d);
+  d.base = std::malloc(std::max<size_t>(d.region, 1));
+  if (!d.base) { g_err = "out of memory"; return -5; }
+  std::memcpy(d.base, (const uint8_t*)src.base + (img.dev_begin - src.origin), d.region);
+  d.origin = img.dev_begin;
+  *out = d;
+  return 0;
+}
+// the stub's "device memory" is host malloc memory (cg_image_load_device callers of the stub pass it)
+int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out) {
+  DevImage d;
+  stub_image(device, img, d);
+  d.base = dev_blob;
+  d.origin = 0;
+  *out = d;
+  return 0;
+}
+int dev_to_host(int, const void* src, size_t n, void* dst) {
+  std::memcpy(dst, src, n);
+  return 0;
+}
+void dev_image_free(DevImage* d) {
+  std::free(d->base);
+  *d = DevImage();
+}
 
 int dev_pool_create(int device, DevPool** out) {
   *out = new DevPool();

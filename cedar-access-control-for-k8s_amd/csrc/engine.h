@@ -113,6 +113,10 @@ struct Image {
     return h ^ (h >> 33);
   }
   std::vector<uint8_t> serialize() const;
+  // device region of the blob this image was read from (image.h DevSection): section offsets and
+  // byte sizes, and the region's bounds (blob offsets)
+  uint64_t dev_off[cgi::DS_COUNT] = {}, dev_len[cgi::DS_COUNT] = {};
+  uint64_t dev_begin = 0, dev_end = 0;
   static std::shared_ptr<Image> deserialize(const uint8_t* p, size_t n);
 };
 

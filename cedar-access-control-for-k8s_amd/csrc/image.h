@@ -339,6 +339,15 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 6;
+constexpr uint32_t IMG_VERSION = 7;
+// The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
+// in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
+// copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob
+// itself when a collective delivered it to device memory), with each array at its blob offset.
+enum DevSection : uint32_t {
+  DS_PSTREAM, DS_TIER_CEND, DS_CHUNKS, DS_CPOOL, DS_GSTR_OFF, DS_HOT, DS_ACT, DS_BTAB, DS_BFILT, DS_BSTREAM,
+  DS_SROWS, DS_SHASH, DS_GSTR_BYTES, DS_COUNT
+};
+constexpr uint32_t DS_ALIGN = 256;
 
 }  // namespace cgi

@@ -1,15 +1,21 @@
 // Serving queue (include/cedargpu.h "serving queue"): turns concurrent, blocking per-request calls
-// into device batches.
+// into device batches, over one GPU or several in one process.
 //
 // The reference's webhook answers each SubjectAccessReview in its own goroutine with one
-// PolicySet.IsAuthorized call (internal/server/authorizer/authorizer.go:36-86). Here every caller
-// thread parses, converts and encodes its own request (SAR -> attributes -> fast path -> entities
-// -> position-independent request block) with no lock held, hands the block to one of 16 stripes
-// (a mutex held for one pointer push) and sleeps. One flusher thread drains the stripes into a
-// device batch (at most `max_batch` requests; with `max_delay_us` > 0 it first lets the batch fill
-// for that long after its first request), submits it, builds the next batch while the device runs
-// this one, then publishes the results with one futex wake for every waiting caller. Callers
-// render their own decision and reason in parallel. The batch size adapts to the offered load.
+// PolicySet.IsAuthorized call (internal/server/authorizer/authorizer.go:36-86, server.go:67-117).
+// Here every caller thread parses, converts and encodes its own request (SAR -> attributes -> fast
+// path -> entities -> position-independent request block) with no lock held, hands the block to one
+// of 16 stripes (a mutex held for one pointer push) and sleeps. One flusher thread drains the
+// stripes into device batches (at most `max_batch` requests; with `max_delay_us` > 0 it first lets
+// a batch fill for that long after its first request) and deals each closed batch to the least
+// loaded GPU: one submitter thread per context runs its batches (submit, wait) and publishes the
+// results with one futex wake for every waiting caller. While every GPU is busy with a batch and
+// has the next one queued, the flusher keeps draining into a larger batch, so the batch size adapts
+// to the offered load. Callers render their own decision and reason in parallel.
+//
+// Requests are encoded against the first context's active image; a batch dealt to another context
+// runs on that context's image of the same epoch (loaded with cg_image_load_peer, or the same blob),
+// or goes to the first context while another has not loaded that epoch yet.
 #include <linux/futex.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -19,6 +25,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <condition_variable>
 #include <cstring>
 #include <ctime>
 #include <deque>
@@ -33,23 +40,26 @@ using Clock = std::chrono::steady_clock;
 
 namespace {
 
+struct Ticket;
+
 struct QBatch {
   cg_batch* b = nullptr;
   int rc = CG_OK;
   std::string err;
+  std::vector<std::shared_ptr<Ticket>> tickets;  // released (cleared) when the batch is published
   ~QBatch() { cg_batch_destroy(b); }
 };
 
-// One caller's request. Shared by the caller and the flusher: a caller whose deadline passes
-// returns while the flusher may still hold (and batch) its ticket.
+// One caller's request. Shared by the caller and the flusher / submitter: a caller whose deadline
+// passes returns while the queue may still hold (and batch) its ticket.
 struct Ticket {
-  std::shared_ptr<LoadedImage> img;  // the image the request was encoded against
+  std::shared_ptr<LoadedImage> img;  // the image the request was encoded against (first context)
   EncodedRequest e;
   Clock::time_point t;
-  // set by the flusher
+  // set by the flusher before the batch is dealt; read by the caller once `ready`
   std::shared_ptr<QBatch> qb;
   uint32_t idx = 0;
-  std::atomic<uint64_t> seq{0};  // the request's batch is published when done_seq reaches seq
+  std::atomic<uint32_t> ready{0};  // the request's batch is published
   int rc = CG_OK;    // a request the batch could not take (error set, no batch)
   std::string err;
 };
@@ -78,37 +88,79 @@ int64_t now_ns() {
 
 }  // namespace
 
-struct cg_queue {
+// one GPU's submitter: runs the batches dealt to its context, in order
+struct QWorker {
   cg_ctx* ctx = nullptr;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::shared_ptr<QBatch>> q;
+  std::atomic<uint32_t> load{0};  // batches queued or running
+  bool stop = false;              // under mu
+  std::atomic<uint64_t> n_batches{0}, n_requests{0};
+};
+
+struct cg_queue {
+  std::vector<cg_ctx*> ctxs;  // ctxs[0] encodes (its active image)
   uint32_t max_batch = 4096;
   Clock::duration max_delay{};
   Stripe stripes[STRIPES];
   std::atomic<uint32_t> pending{0};     // tickets in the stripes (the flusher sleeps on it at 0)
-  std::atomic<uint64_t> done_seq{0};    // batches published
   std::atomic<uint32_t> pub{0};         // bumped per publication (callers' futex word)
   std::atomic<uint32_t> next_stripe{0};
   std::atomic<bool> stop{false};
   std::thread flusher;
+  std::vector<std::unique_ptr<QWorker>> workers;
+  std::mutex slot_mu;  // the flusher waits here for a submitter with room
+  std::condition_variable slot_cv;
   std::atomic<uint64_t> n_batches{0}, n_requests{0}, n_fast{0}, max_seen{0}, device_ns{0};
 
+  static constexpr uint32_t DEPTH = 2;  // batches per submitter: one running, the next queued
+
   void run();
-  void publish(uint64_t seq) {
-    done_seq.store(seq, std::memory_order_release);
+  void work(QWorker& w);
+  void publish(QBatch& qb) {
+    for (auto& t : qb.tickets) t->ready.store(1, std::memory_order_release);
+    qb.tickets.clear();  // breaks the ticket <-> batch reference cycle
     pub.fetch_add(1, std::memory_order_release);
     futex_wake_all(&pub);
   }
 };
 
-void cg_queue::run() {
-  std::deque<TicketP> backlog;  // drained, not yet batched (over max_batch, or another image)
-  std::vector<TicketP> grab;
-  uint64_t seq = 0;
-  struct InFlight {
+void cg_queue::work(QWorker& w) {
+  for (;;) {
     std::shared_ptr<QBatch> qb;
-    uint64_t seq = 0;
-    Clock::time_point t;
-  };
-  std::vector<InFlight> flight;  // at most one batch on the device while the next is built / queued
+    {
+      std::unique_lock<std::mutex> g(w.mu);
+      w.cv.wait(g, [&] { return w.stop || !w.q.empty(); });
+      if (w.q.empty()) return;  // stopped and drained
+      qb = std::move(w.q.front());
+      w.q.pop_front();
+    }
+    const auto t0 = Clock::now();
+    if (!qb->rc) {
+      int rc = cg_batch_submit(qb->b);
+      if (!rc) rc = cg_batch_wait(qb->b, -1);
+      if (rc) {
+        qb->rc = rc;
+        qb->err = qb->b->err;
+      }
+    }
+    device_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+    w.n_batches++;
+    w.n_requests += qb->b->items.size();
+    publish(*qb);
+    {
+      std::lock_guard<std::mutex> g(slot_mu);
+      w.load.fetch_sub(1);
+    }
+    slot_cv.notify_one();
+  }
+}
+
+void cg_queue::run() {
+  std::deque<std::shared_ptr<Ticket>> backlog;  // drained, not yet batched (over max_batch, or another image)
+  std::vector<std::shared_ptr<Ticket>> grab;
   auto drain = [&] {
     for (auto& st : stripes) {
       {
@@ -117,28 +169,23 @@ void cg_queue::run() {
         grab.swap(st.q);
       }
       pending.fetch_sub((uint32_t)grab.size(), std::memory_order_relaxed);
-      for (TicketP& t : grab) backlog.push_back(std::move(t));
+      for (auto& t : grab) backlog.push_back(std::move(t));
       grab.clear();
     }
   };
-  auto finish = [&](InFlight& f) {
-    int rc = f.qb->rc;
-    if (!rc) rc = cg_batch_wait(f.qb->b, -1);
-    device_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - f.t).count();
-    if (rc) {
-      f.qb->rc = rc;
-      f.qb->err = f.qb->b->err;
+  uint32_t rr = 0;  // round-robin start: ties (idle GPUs) take turns
+  auto least = [&]() -> QWorker* {
+    const uint32_t n = (uint32_t)workers.size();
+    QWorker* best = workers[rr % n].get();
+    for (uint32_t k = 1; k < n; k++) {
+      QWorker* w = workers[(rr + k) % n].get();
+      if (w->load.load() < best->load.load()) best = w;
     }
-    publish(f.seq);
+    return best;
   };
   for (;;) {
     drain();
     if (backlog.empty()) {
-      if (!flight.empty()) {  // nothing to build: finish the batch on the device
-        finish(flight.front());
-        flight.erase(flight.begin());
-        continue;
-      }
       if (stop.load()) return;
       pending.wait(0, std::memory_order_acquire);
       continue;
@@ -150,18 +197,37 @@ void cg_queue::run() {
         drain();
       }
     }
-    // build the next batch from the backlog (one image per batch)
+    // a submitter with room; while every one has a batch running and one queued, keep draining
+    // (the next batch grows)
+    QWorker* w = least();
+    while (w->load.load() >= DEPTH) {
+      {
+        std::unique_lock<std::mutex> g(slot_mu);
+        // every submitter notifies when it frees a slot; the timeout only bounds a missed wake
+        // (system_clock: pthread_cond_timedwait, which the thread sanitizer models)
+        slot_cv.wait_until(g, std::chrono::system_clock::now() + std::chrono::microseconds(50),
+                           [&] { return least()->load.load() < DEPTH; });
+      }
+      drain();
+      w = least();
+    }
+    // the batch's image on that context: the encoding image's epoch (else the first context)
+    const std::shared_ptr<LoadedImage> enc = backlog.front()->img;
+    std::shared_ptr<LoadedImage> img = enc;
+    if (w->ctx != ctxs[0]) {
+      std::lock_guard<std::mutex> g(w->ctx->mu);
+      auto it = w->ctx->images.find(enc->host->epoch);
+      if (it != w->ctx->images.end()) img = it->second;
+    }
+    if (img == enc && w->ctx != ctxs[0]) w = workers[0].get();
     auto qb = std::make_shared<QBatch>();
-    const std::shared_ptr<LoadedImage> img = backlog.front()->img;
     qb->b = new cg_batch();
-    qb->b->ctx = ctx;
+    qb->b->ctx = w->ctx;
     qb->b->img = img;
     qb->b->host.img = img->host;
-    const uint64_t my = ++seq;
-    while (!backlog.empty() && qb->b->items.size() < max_batch && backlog.front()->img == img) {
-      TicketP t = std::move(backlog.front());
+    while (!backlog.empty() && qb->b->items.size() < max_batch && backlog.front()->img == enc) {
+      std::shared_ptr<Ticket> t = std::move(backlog.front());
       backlog.pop_front();
-      t->seq.store(my, std::memory_order_relaxed);
       try {
         qb->b->host.append(t->e);
         qb->b->items.push_back({(int32_t)qb->b->host.n() - 1, -1});
@@ -171,21 +237,19 @@ void cg_queue::run() {
         t->rc = CG_E_ARG;
         t->err = ex.what();
       }
+      qb->tickets.push_back(std::move(t));
     }
     n_batches++;
     const uint64_t n = qb->b->items.size();
     for (uint64_t m = max_seen.load(); n > m && !max_seen.compare_exchange_weak(m, n);) {
     }
-    // the batch on the device finishes (its callers released) before this one is submitted: in a
-    // closed loop of callers, releasing them early is worth more than the host time overlapped
-    if (!flight.empty()) {
-      finish(flight.front());
-      flight.erase(flight.begin());
+    rr++;
+    w->load.fetch_add(1);
+    {
+      std::lock_guard<std::mutex> g(w->mu);
+      w->q.push_back(std::move(qb));
     }
-    InFlight f{qb, my, Clock::now()};
-    qb->rc = cg_batch_submit(qb->b);
-    if (qb->rc) qb->err = qb->b->err;
-    flight.push_back(std::move(f));
+    w->cv.notify_one();
   }
 }
 
@@ -214,12 +278,9 @@ int wait_ticket(cg_queue* q, const TicketP& tp, int64_t deadline, std::string& e
     st.q.push_back(tp);
   }
   if (q->pending.fetch_add(1, std::memory_order_release) == 0) q->pending.notify_one();
-  // the ticket's seq is written by the flusher before it publishes; read it only once published
   for (;;) {
     const uint32_t w = q->pub.load(std::memory_order_acquire);
-    const uint64_t d = q->done_seq.load(std::memory_order_acquire);
-    const uint64_t my = t.seq.load(std::memory_order_relaxed);
-    if (my && d >= my) break;
+    if (t.ready.load(std::memory_order_acquire)) break;
     int64_t rel = -1;
     if (deadline >= 0) {
       rel = deadline - now_ns();
@@ -263,17 +324,32 @@ int submit_ticket(cg_queue* q, const TicketP& tp, int64_t deadline, int* out, ch
 
 extern "C" {
 
-int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_queue** out) {
-  if (!ctx || !out || max_batch == 0) return CG_E_ARG;
+int cg_queue_create_multi(cg_ctx* const* ctxs, uint32_t n_ctx, uint32_t max_batch, uint32_t max_delay_us, cg_queue** out) {
+  if (!ctxs || !n_ctx || !out || max_batch == 0) return CG_E_ARG;
+  for (uint32_t k = 0; k < n_ctx; k++)
+    if (!ctxs[k]) return CG_E_ARG;
   *out = nullptr;
   auto* q = new (std::nothrow) cg_queue();
   if (!q) return CG_E_ARG;
-  q->ctx = ctx;
+  q->ctxs.assign(ctxs, ctxs + n_ctx);
   q->max_batch = max_batch;
   q->max_delay = std::chrono::microseconds(max_delay_us);
   try {
+    for (uint32_t k = 0; k < n_ctx; k++) {
+      q->workers.push_back(std::make_unique<QWorker>());
+      q->workers.back()->ctx = ctxs[k];
+    }
+    for (auto& w : q->workers) {
+      QWorker* wp = w.get();
+      w->th = std::thread([q, wp] { q->work(*wp); });
+    }
     q->flusher = std::thread([q] { q->run(); });
   } catch (...) {
+    for (auto& w : q->workers) {
+      { std::lock_guard<std::mutex> g(w->mu); w->stop = true; }
+      w->cv.notify_one();
+      if (w->th.joinable()) w->th.join();
+    }
     delete q;
     return CG_E_ARG;
   }
@@ -281,13 +357,29 @@ int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_q
   return CG_OK;
 }
 
+int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_queue** out) {
+  return cg_queue_create_multi(&ctx, ctx ? 1u : 0u, max_batch, max_delay_us, out);
+}
+
 void cg_queue_destroy(cg_queue* q) {
   if (!q) return;
   q->stop.store(true);
-  q->pending.fetch_add(1);  // wakes the flusher, which finishes what it holds and returns
+  q->pending.fetch_add(1);  // wakes the flusher, which deals what it holds and returns
   q->pending.notify_one();
   if (q->flusher.joinable()) q->flusher.join();
+  for (auto& w : q->workers) {  // each submitter runs what it was dealt, then returns
+    { std::lock_guard<std::mutex> g(w->mu); w->stop = true; }
+    w->cv.notify_one();
+    if (w->th.joinable()) w->th.join();
+  }
   delete q;
+}
+
+int cg_queue_gpu_stats(cg_queue* q, uint32_t k, uint64_t* batches, uint64_t* requests) {
+  if (!q || k >= q->workers.size()) return CG_E_ARG;
+  if (batches) *batches = q->workers[k]->n_batches.load();
+  if (requests) *requests = q->workers[k]->n_requests.load();
+  return CG_OK;
 }
 
 const char* cg_queue_last_error(void) { return t_err.c_str(); }
@@ -298,7 +390,7 @@ int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_
   const int64_t deadline = timeout_ns < 0 ? -1 : now_ns() + timeout_ns;
   TicketP tp = std::make_shared<Ticket>();
   Ticket& t = *tp;
-  t.img = active_image(q->ctx, t_err);
+  t.img = active_image(q->ctxs[0], t_err);
   if (!t.img) return CG_E_STATE;
   const std::shared_ptr<LoadedImage>& li = t.img;
   EncodedRequest& e = t.e;
@@ -344,7 +436,7 @@ int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, 
   })
   TicketP tp = std::make_shared<Ticket>();
   Ticket& t = *tp;
-  t.img = active_image(q->ctx, t_err);
+  t.img = active_image(q->ctxs[0], t_err);
   if (!t.img) return CG_E_STATE;
   GUARD(t_err, { encode_request(*t.img->host, ents, req, t.e); })
   return submit_ticket(q, tp, deadline, allow, diag, cap, need, false);

@@ -123,6 +123,17 @@ const char* cg_last_error(cg_ctx* ctx);
 int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg);
 /* Copies and uploads an image; the caller keeps ownership of `image`. Not active until activated. */
 int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch);
+/* Loads an image whose serialized blob is already in device memory on ctx's device, e.g. the
+ * buffer a collective delivered it to (cg_broadcast_image): the blob's device region is used in
+ * place (no copy); `host_blob` is the same bytes in host memory, or NULL to copy them back for the
+ * host-side tables. dev_blob must come from hipMalloc on ctx's device; on success the library owns
+ * it (hipFree when the image is dropped). The reference swaps its whole policy set on a reload
+ * (directory.go:81, verified_permissions.go:99; crd.go:62-114 per CRD event). */
+int cg_image_load_device(cg_ctx* ctx, void* dev_blob, size_t len, uint64_t epoch, const void* host_blob);
+/* Loads onto `dst` the image `src` holds for `epoch`: the host tables are shared, the device region
+ * is copied GPU to GPU (xGMI peer copy; a device copy when both contexts use the same GPU). The
+ * in-process multi-GPU reload: compile once, cg_image_load on one context, this on the others. */
+int cg_image_load_peer(cg_ctx* dst, cg_ctx* src, uint64_t epoch);
 /* Atomically makes `epoch` the image new batches bind to; in-flight batches keep theirs. */
 int cg_image_activate(cg_ctx* ctx, uint64_t epoch);
 int cg_image_active(cg_ctx* ctx, uint64_t* epoch);
@@ -231,6 +242,14 @@ int cg_is_authorized_json(cg_ctx* ctx, const char* item_json, size_t len, int* a
  * its first request has waited max_delay_us (0: as soon as the device is idle). */
 typedef struct cg_queue cg_queue;
 int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_queue** out);
+/* The same queue over n_ctx contexts (one per GPU, §8(e)): one flusher builds the batches and deals
+ * each to the least loaded GPU, whose submitter thread runs it. Requests are encoded against
+ * ctxs[0]'s active image; a batch runs on the other context's image of that epoch (load it there
+ * with cg_image_load_peer or the same blob), or on ctxs[0] while that context lacks the epoch. */
+int cg_queue_create_multi(cg_ctx* const* ctxs, uint32_t n_ctx, uint32_t max_batch, uint32_t max_delay_us,
+                          cg_queue** out);
+/* Batches and requests the queue's k-th context (ctxs[k]) has run. */
+int cg_queue_gpu_stats(cg_queue* q, uint32_t k, uint64_t* batches, uint64_t* requests);
 /* Drains pending batches, then stops the flusher. No call may be in flight on q. */
 void cg_queue_destroy(cg_queue* q);
 /* Error text of the calling thread's last failed cg_queue_* call. */

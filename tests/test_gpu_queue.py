@@ -139,3 +139,62 @@ def test_queue_errors(ctx):
     dec, _ = q.authorize(synth.make_sar("alice", "", ["viewers"], "get", resource="pods", ns="default"))
     assert dec in (0, 1, 2)
     q.close()
+
+
+def test_multi_context_queue_peer_reload_matches_oracle(ctx):
+    """cg_queue_create_multi over two contexts (here both on GPU 0; one per GPU in production):
+    the image reaches the second context by cg_image_load_peer (device-to-device copy, host tables
+    shared), batches are dealt to both, and a reload (load + activate on the first context, peer
+    load on the second) while callers run changes no result against the oracle of the epoch each
+    request was encoded against."""
+    text = _demo()
+    extra = '\nforbid (principal, action == k8s::Action::"get", resource) when { resource has namespace && ' \
+            'resource.namespace == "kube-system" };'
+    c2 = cedargpu.Context(0)
+    try:
+        _load(ctx, [cedargpu.MemoryStore("demo.cedar", text)], 301)
+        c2.load_peer(ctx, 301)
+        q = cedargpu.Queue([ctx, c2], max_batch=48, max_delay_us=100)
+        pop = synth.Population(seed=29, n_users=600, n_groups=60)
+        sars = synth.random_sars(3000, seed=29, pop=pop)
+        for k in range(0, len(sars), 5):
+            ra = sars[k]["spec"].get("resourceAttributes")
+            if ra is not None:
+                ra["namespace"], ra["verb"] = "kube-system", "get"
+        want1 = [km.authorize(_oracle_tiers(text), km.attributes_from_sar(s)) for s in sars]
+        want2 = [km.authorize(_oracle_tiers(text + extra), km.attributes_from_sar(s)) for s in sars]
+        assert want1 != want2
+        got = [None] * len(sars)
+        errors = []
+        half, reloaded = threading.Barrier(17), threading.Barrier(17)
+
+        def work(t):
+            try:
+                for n, i in enumerate(range(t, len(sars), 16)):
+                    if n == 20:
+                        half.wait(60)      # every caller has had 20 answers on epoch 301
+                        reloaded.wait(60)  # and continues once epoch 302 is active
+                    got[i] = q.authorize(sars[i])
+            except Exception as e:  # surfaced below
+                errors.append(e)
+
+        ws = [threading.Thread(target=work, args=(t,)) for t in range(16)]
+        for w in ws:
+            w.start()
+        half.wait(60)
+        _load(ctx, [cedargpu.MemoryStore("demo.cedar", text + extra)], 302)
+        c2.load_peer(ctx, 302)
+        reloaded.wait(60)
+        for w in ws:
+            w.join(120)
+        per_gpu = q.gpu_stats()
+        q.close()
+        assert not errors, errors[0]
+        for s, g, w1, w2 in zip(sars, got, want1, want2):
+            assert g in (w1, w2), s  # either epoch, depending on when the request was encoded
+        # requests issued after the reload see the new epoch
+        late = [i for t in range(16) for n, i in enumerate(range(t, len(sars), 16)) if n >= 20]
+        assert all(got[i] == want2[i] for i in late)
+        assert all(p["batches"] > 0 for p in per_gpu), per_gpu
+    finally:
+        c2.close()

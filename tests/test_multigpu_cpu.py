@@ -65,3 +65,92 @@ def test_two_ranks_gloo():
     assert got[0][0] == got[1][0]                      # identical compiled image on both ranks
     assert got[0][1] == got[1][1] == bytes(range(128))  # the id reached rank 1
     assert got[0][2] == (0, 500) and got[1][2] == (500, 1000)
+
+
+# ------------------------------------------------ multi-context queue + reload (device stand-in)
+STUB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "san", "libcedargpu_stub.so")
+
+
+def _queue_worker(rank, world, port, out):
+    """One rank = one process with two contexts (GPUs) behind one serving queue. Rank 0 compiles,
+    the blob travels over the collective (gloo here, RCCL on GPUs), every rank loads it on its first
+    context and peer-copies it to the second; a reload then happens while callers keep calling."""
+    import threading
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import cedargpu as cg
+        assert cg._lib.SANITIZER_BUILD  # the host engine over the device stand-in
+        pop = synth.Population(seed=3, n_users=200, n_groups=20)
+        text = synth.abac_policies(300, seed=3, pop=pop)
+
+        def reload(epoch, extra=""):
+            blob = [cg.build_image([cg.MemoryStore("c3.cedar", text + extra)], epoch=epoch) if rank == 0 else None]
+            dist.broadcast_object_list(blob, src=0)
+            ctxs[0].load(blob[0], epoch)       # new requests encode against it from here on
+            ctxs[1].load_peer(ctxs[0], epoch)  # the second GPU follows (its batches fall back meanwhile)
+
+        ctxs = [cg.Context(2 * rank), cg.Context(2 * rank + 1)]
+        reload(1)
+        q = cg.Queue(ctxs, max_batch=64, max_delay_us=50)
+        sars = synth.random_sars(2000, seed=40 + rank, pop=pop)
+        errors = []
+
+        def caller(k):
+            for s in sars[k::8]:
+                try:
+                    d, _ = q.authorize(s)
+                    assert d in (0, 1, 2)
+                except Exception as e:  # noqa: BLE001 (reported to the parent)
+                    errors.append(repr(e))
+
+        th = [threading.Thread(target=caller, args=(k,)) for k in range(8)]
+        for t in th:
+            t.start()
+        reload(2, '\nforbid (principal, action == k8s::Action::"reload-check", resource);')
+        for t in th:
+            t.join()
+        stats = q.gpu_stats()
+        q.close()
+        active = []
+        for c in ctxs:
+            e = cg._lib.u64()
+            cg.lib.cg_image_active(c._h, cg._lib.ctypes.byref(e))
+            active.append(e.value)
+            c.close()
+        got = [None] * world
+        dist.all_gather_object(got, (errors, stats, active))
+        if rank == 0:
+            out.put(got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_multi_context_queue_with_reload():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(os.path.dirname(STUB), "..", "..", "cedar-access-control-for-k8s_amd",
+                                                      "csrc"), "stub"], check=True, capture_output=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    old = os.environ.get("CEDARGPU_SANITIZER_LIB")
+    os.environ["CEDARGPU_SANITIZER_LIB"] = STUB  # inherited by the spawned ranks only
+    try:
+        procs = [ctx.Process(target=_queue_worker, args=(r, 2, port, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+    finally:
+        if old is None:
+            del os.environ["CEDARGPU_SANITIZER_LIB"]
+        else:
+            os.environ["CEDARGPU_SANITIZER_LIB"] = old
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for errors, stats, active in got:
+        assert errors == []
+        assert sum(s["requests"] for s in stats) > 0
+        assert all(s["batches"] > 0 for s in stats), stats  # both contexts of the rank ran batches
+        assert active == [2, 2]                               # the reload reached both contexts

@@ -275,6 +275,64 @@ static void phase_queue(cg_ctx* ctx, cg_compiler* comp, std::mt19937& r0) {
   cg_queue_destroy(q);
 }
 
+// four contexts behind one queue: images reach the others by cg_image_load_peer, later than the
+// first context's activation (batches fall back to the first context meanwhile)
+static void phase_multi(cg_compiler* comp) {
+  std::mt19937 r(77);
+  cg_ctx* ctxs[4] = {};
+  for (int k = 0; k < 4; k++) CHECK(cg_ctx_create(k, &ctxs[k]) == 0, "ctx %d", k);
+  auto img = build(comp, 500, 120, r, false);
+  CHECK(cg_image_load(ctxs[0], img.data(), img.size(), 500) == 0, "load");
+  CHECK(cg_image_activate(ctxs[0], 500) == 0, "activate");
+  for (int k = 1; k < 4; k++) CHECK(cg_image_load_peer(ctxs[k], ctxs[0], 500) == 0, "peer load %d", k);
+  cg_queue* q = nullptr;
+  CHECK(cg_queue_create_multi(ctxs, 4, 32, 20, &q) == 0, "queue multi");
+  std::atomic<bool> stop{false};
+  std::thread reloader([&] {
+    std::mt19937 rr(5);
+    for (uint64_t epoch = 501; !stop.load(); epoch++) {
+      auto im = build(comp, epoch, 60 + (int)(rr() % 60), rr, false);
+      CHECK(cg_image_load(ctxs[0], im.data(), im.size(), epoch) == 0, "load");
+      CHECK(cg_image_activate(ctxs[0], epoch) == 0, "activate");
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      for (int k = 1; k < 4; k++) {
+        CHECK(cg_image_load_peer(ctxs[k], ctxs[0], epoch) == 0, "peer load");
+        cg_image_unload(ctxs[k], epoch - 1);
+      }
+      cg_image_unload(ctxs[0], epoch - 1);
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+  });
+  std::atomic<uint64_t> ok{0};
+  std::vector<std::thread> callers;
+  for (int t = 0; t < 16; t++)
+    callers.emplace_back([&, t] {
+      std::mt19937 rt(300 + t);
+      char reason[8192];
+      for (int k = 0; k < 300; k++) {
+        const std::string s = sar_json(rt);
+        int dec = -1;
+        size_t need = 0;
+        const int rc = cg_queue_authorize_sar(q, s.data(), s.size(), -1, &dec, reason, sizeof reason, &need);
+        CHECK(rc == CG_OK, "multi queue rc %d: %s", rc, cg_queue_last_error());
+        if (rc == CG_OK) ok++;
+      }
+    });
+  for (auto& x : callers) x.join();
+  stop = true;
+  reloader.join();
+  uint64_t used = 0;
+  for (uint32_t k = 0; k < 4; k++) {
+    uint64_t b = 0, n = 0;
+    cg_queue_gpu_stats(q, k, &b, &n);
+    std::printf("  context %u: %llu batches, %llu requests\n", k, (unsigned long long)b, (unsigned long long)n);
+    used += b > 0;
+  }
+  CHECK(used >= 2, "batches went to %llu contexts only", (unsigned long long)used);
+  cg_queue_destroy(q);
+  for (auto* c : ctxs) cg_ctx_destroy(c);
+}
+
 int main() {
   std::mt19937 r(1);
   cg_compiler* comp = nullptr;
@@ -292,6 +350,8 @@ int main() {
   std::printf("batches ok\n");
   phase_queue(ctx, comp, r);
   std::printf("queue ok\n");
+  phase_multi(comp);
+  std::printf("multi-context queue ok\n");
   cg_ctx_destroy(ctx);
   cg_compiler_destroy(comp);
   std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "PASSED", g_fail);
