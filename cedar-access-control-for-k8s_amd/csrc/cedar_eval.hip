@@ -75,6 +75,7 @@ struct KArgs {
   unsigned long long* stats;             // probe-kernel work counters (STATS variant only)
   const uint32_t* n_dev;                 // follow-up pass: request count on the device (null: n_req)
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
+  uint32_t hlists;  // rows carry element-hash lists (image.h "set-membership keys")
   uint32_t n_static, smask, lane_stride;
 };
 
@@ -107,6 +108,7 @@ struct Ctx {
   uint32_t t0, i0, t1, i1, t2, i2, t3, i3, t4, i4, t5, i5, t6, i6, t7, i7;
   uint32_t pb0, pb1, pb2, pb3;            // principal ancestor-or-self Bloom
   uint32_t rb0, rb1, rb2, rb3;            // resource ancestor-or-self Bloom
+  const uint32_t* rowx;                   // the row's element-hash list offsets per hot slot, or null
 };
 
 // Makes a value opaque to the optimizer. Used on context fields that feed a select: otherwise
@@ -624,6 +626,14 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
     case AK_CONTAINS: {
       if (tag_of(v) != T_SET) { type_err(e, TN_SET, v); return 2u; }
       const uint32_t ref = v.w0 & X_MASK, n = v.w1;
+      const uint32_t hl = c.rowx ? c.rowx[h] : 0xFFFFFFFFu;
+      uint32_t th;
+      if (hl != 0xFFFFFFFFu && reg_chash(w1, w2, w3, th)) {  // element hashes first, values on a match
+        bool f = false;
+        for (uint32_t k = 0; k < n && !f; k++)
+          if (c.blk[hl + 1 + k] == th) f = prim_eq(load_val(c, rd(c, ref, 1 + 2 * k), rd(c, ref, 2 + 2 * k)), w1, w2, w3);
+        return f ? 1u : 0u;
+      }
       bool f = false;
       for (uint32_t k = 0; k < n && !f; k++) f = prim_eq(load_val(c, rd(c, ref, 1 + 2 * k), rd(c, ref, 2 + 2 * k)), w1, w2, w3);
       return f ? 1u : 0u;
@@ -641,6 +651,37 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
       if (tag_of(v) != T_SET) { type_err(e, TN_SET, v); return 2u; }
       const uint32_t ref = v.w0 & X_MASK, n = v.w1;
       bool f = false, deep = false;
+      const uint32_t hl = c.rowx ? c.rowx[h] : 0xFFFFFFFFu;
+      if (hl != 0xFFFFFFFFu) {  // templates of primitives (constants, primitive holes): hashes first
+        bool hashable = true;
+        const uint32_t* t = d + 1 + nh;
+        for (uint32_t j = 0; j < w2 && !f && hashable; j++) {
+          const uint32_t nk = t[0];
+          uint32_t th = chash_mix(CHASH_REC, nk);
+          for (uint32_t q = 0; q < nk && hashable; q++) {
+            const uint32_t* fl = t + 1 + RS_FIELD_WORDS * q;
+            uint32_t fh = 0;
+            if (fl[1] == RF_CONST) {
+              hashable = reg_chash(fl[2], fl[3], fl[4], fh);
+            } else if (fl[1] == RF_HOLE) {
+              const uint2 hv3 = hot_get(c, fl[2]);
+              const RV hx = load_val(c, hv3.x, hv3.y);
+              hashable = reg_chash(hx.w0, hx.w1, hx.w2, fh);
+            } else {
+              hashable = false;
+            }
+            th = chash_mix(chash_mix(th, fl[0]), fh);
+          }
+          for (uint32_t i = 0; i < n && !f && hashable; i++)
+            if (c.blk[hl + 1 + i] == th) f = rs_rec_eq<STRUCT>(c, rec, load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i)), t, deep);
+          t += 1 + RS_FIELD_WORDS * nk;
+        }
+        if (hashable) {
+          if (deep) { if (!STRUCT) return 3u; e.code = E_DEPTH; return 2u; }
+          return f ? 1u : 0u;
+        }
+        f = deep = false;  // a template the hashes do not cover: the element-by-element path
+      }
       for (uint32_t i = 0; i < n && !f; i++) {
         const RV x = load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i));
         if (tag_of(x) != T_REC) continue;
@@ -1218,6 +1259,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
     const uint32_t* row = a.rows + (size_t)r * a.row_words;
     for (uint32_t h = 0; h < a.n_hot; h++)
       c.hotl[h * c.hstride] = valid ? make_uint2(row[RW_HDR + 2 * h], row[RW_HDR + 2 * h + 1]) : make_uint2(0u, 0u);
+    c.rowx = (valid && a.hlists) ? row + RW_HDR + 2 * a.n_hot : nullptr;
   }
 
   bool decided = !valid;
@@ -1421,6 +1463,7 @@ struct PCtx {
   static constexpr uint32_t hstride = 1;
   uint32_t pt, pi, at, ai, rt, ri;
   uint32_t p_anc, p_nanc, r_anc, r_nanc, a_anc, a_nanc;
+  const uint32_t* rowx;  // the row's element-hash list offsets per hot slot, or null
 };
 
 // X in (qt, qi) for X with UID (st, si) and ancestor pairs at blk[off + 2k]
@@ -1457,10 +1500,11 @@ __device__ __forceinline__ bool filt_maybe(const uint32_t* bfilt, uint32_t fmask
 }
 
 // probe: (first, count, hmask) of the slot matching key words w0..w6 (+ v0, v1 for level 2)
-// (level-1 probes also return the entry's level-2 bloom in *bloom)
+// (level-1 probes also return the entry's level-2 bloom in *bloom and its cmask in *cmask)
 template <bool ST = false>
 __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uint32_t hash, uint32_t w0, uint2 p, uint2 q,
-                                       uint2 r, uint32_t v0, uint32_t v1, uint32_t& steps, uint4* bloom = nullptr) {
+                                       uint2 r, uint32_t v0, uint32_t v1, uint32_t& steps, uint4* bloom = nullptr,
+                                       uint32_t* cmask = nullptr) {
   uint32_t h = hash & bmask;
   for (;;) {
     if (ST) steps++;
@@ -1471,6 +1515,7 @@ __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uin
       const uint4 y = sl[1], z = sl[2];
       if (y.x == q.y && y.y == r.x && y.z == r.y && (!(w0 & BT_L2) || (y.w == v0 && z.x == v1))) {
         if (bloom) *bloom = sl[3];
+        if (cmask) *cmask = y.w;
         return make_uint3(z.y, z.z, z.w);
       }
     }
@@ -1536,6 +1581,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
   PCtx c;
   c.blk = a.heap + hdr(RW_BLK);
+  c.rowx = (valid && a.hlists) ? row + RW_HDR + 2 * a.n_hot : nullptr;
   c.cpool = a.cpool;
   c.lh = wl.he[seg];  // atoms never address lane scratch (any valid pointer)
   c.gstr_off = a.gstr_off;
@@ -1586,9 +1632,12 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);  // level-2 bloom of this lane's level-1 entry
+  // set-membership slots of the entry still to probe (image.h BT_CKEY), the current one's element
+  // hash list in the request block and the next element
+  uint32_t csl = 0, ch = 0, cl = 0, ck = 0, cn = 0;
   uint32_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // STATS only (per lane)
   for (;;) {
-    const bool l2 = sballot(hm != 0) != 0;
+    const bool l2 = sballot(hm != 0 || csl != 0 || ck < cn) != 0;
     const bool done = !l2 && kb >= n_keys;
     const bool all_done = __ballot(!done) == 0;
     if (!all_done) {
@@ -1605,6 +1654,38 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
               if (filt_maybe(a.bfilt, a.fmask, h2))
                 e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, st[5]);
               if (STATS) { st[3]++; st[4] += e.y != 0; }
+            }
+          } else if (csl || ck < cn) {
+            uint32_t v0 = 0, v1 = 0;
+            bool go = false;
+            if (ck >= cn) {  // the next set-membership slot: its list header
+              ch = __builtin_ctz(csl);
+              csl &= csl - 1;
+              const uint32_t lo = row[RW_HDR + 2 * a.n_hot + ch];
+              const uint32_t hd = c.blk[lo];
+              ck = cn = 0;
+              if (hd & 0x80000000u) {
+                v0 = hd == CL_MISSING ? MISSING_W0 : NOTSET_W0;
+                go = true;
+              } else {
+                cl = lo + 1;
+                cn = hd;
+              }
+            }
+            if (!go && ck < cn) {
+              v0 = c.blk[cl + ck];
+              v1 = 1;
+              ck++;
+              go = true;
+            }
+            if (go) {
+              const uint32_t hs = ch | BT_CKEY;
+              const uint32_t h2 = bucket_hash2(h1, hs, v0, v1);
+              if (l2_bloom_maybe(blm, h2)) {
+                if (filt_maybe(a.bfilt, a.fmask, h2))
+                  e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | hs, kp, ka, kr, v0, v1, st[5]);
+                if (STATS) { st[3]++; st[4] += e.y != 0; }
+              }
             }
           }
         } else {
@@ -1629,8 +1710,10 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             kr = key_comp(rkc, ir + 1 - (rn >> 31), c.rt, c.ri, c.blk, c.r_anc);
             w0 = BT_USED | (combo << 16);
             h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
-            if (filt_maybe(a.bfilt, a.fmask, h1)) e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5], &blm);
+            uint32_t cmv = 0;
+            if (filt_maybe(a.bfilt, a.fmask, h1)) e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5], &blm, &cmv);
             hm = e.z;
+            csl = cmv;
             if (STATS) st[1]++;
             if (STATS) st[2] += e.y != 0;
           }
@@ -1722,17 +1805,36 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
           }
         }
-        // record hits (segment-local slots)
+        // record hits (segment-local slots): a duplicate class (head word PW_CODE_N, image.h) hits
+        // for every member, all sharing the head's error detail
         const bool hit = ok && (err || pc == AT_SAT);
-        if (STATS) st[9] += hit;
-        const uint64_t hmask = sballot(hit), xmask = sballot(hit && err);
+        const uint32_t mlist = q2.w;
+        const uint32_t nmem = hit ? (mlist ? a.bstream[mlist] : 1u) : 0u;
+        if (STATS) st[9] += nmem;
+        const uint32_t mincl = sscan(nmem);
+        const uint64_t xmask = sballot(hit && err);
+        const uint32_t xpos = nx + mbcnt64(xmask);
+        const uint32_t hmv = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8) | (min(xpos, 0xFFu) << 16);
+        const uint32_t pos0 = nh + mincl - nmem;
+        if (hit && !mlist && pos0 < L::HC) {
+          wl.hp[seg][pos0] = q2.z;  // PW_CODE: global policy index
+          wl.hm[seg][pos0] = hmv;
+        }
+        // class members: the segment copies each hitting class's list together (coalesced)
+        for (uint64_t cls = sballot(hit && mlist != 0); __ballot(cls != 0);) {
+          const bool act = cls != 0;  // this segment still has a class to copy
+          const uint32_t src = act ? (uint32_t)__builtin_ctzll(cls) : lane;
+          cls &= act ? cls - 1 : 0ull;
+          const uint32_t p0 = (uint32_t)__shfl((int)pos0, (int)src), nm = (uint32_t)__shfl((int)nmem, (int)src);
+          const uint32_t mls = (uint32_t)__shfl((int)mlist, (int)src), hv = (uint32_t)__shfl((int)hmv, (int)src);
+          const uint32_t ml = act ? mls : 0u;
+          if (ml)
+            for (uint32_t j = sl; j < nm && p0 + j < L::HC; j += SEG) {
+              wl.hp[seg][p0 + j] = a.bstream[ml + 1 + j];
+              wl.hm[seg][p0 + j] = hv;
+            }
+        }
         if (hit) {
-          const uint32_t pos = nh + mbcnt64(hmask);
-          const uint32_t xpos = nx + mbcnt64(xmask);
-          if (pos < L::HC) {
-            wl.hp[seg][pos] = q2.z;  // PW_CODE: global policy index
-            wl.hm[seg][pos] = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8) | (min(xpos, 0xFFu) << 16);
-          }
           if (err && xpos < L::XC) {
             wl.he[seg][4 * xpos] = e.code | (e.aux << 8);
             wl.he[seg][4 * xpos + 1] = e.k;
@@ -1740,7 +1842,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             wl.he[seg][4 * xpos + 3] = e.ei;
           }
         }
-        nh += popc64(hmask);
+        nh += sbcast(mincl, SEG - 1);
         nx += popc64(xmask);
         min_tier = min(min_tier, smin(hit ? tier : 0xFFu));
       }
@@ -1917,6 +2019,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.gstr_bytes = at(DS_GSTR_BYTES);
   d.n_static = img.n_static();
   d.lane_need = img.lane_need;
+  d.cslot_mask = img.cslot_mask;
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
   d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
   d.fmask = (uint32_t)(img.bfilt.size() / 2) - 1;
@@ -2264,6 +2367,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
   k.lane = b.lane; k.lane_stride = img.lane_need;
+  k.hlists = img.cslot_mask ? 1u : 0u;
   k.stats = nullptr;
   k.n_dev = nullptr;
   return k;

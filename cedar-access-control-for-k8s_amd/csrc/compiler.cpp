@@ -436,6 +436,8 @@ struct Compiler {
     *patch = false;
     auto put = [&](uint32_t kind, uint32_t h) {
       w[0] = kind | (h << 8);
+      // set-membership atoms read the slot's element hashes (image.h "set-membership keys")
+      if (kind == AK_CONTAINS || kind == AK_RECSET) I.cslot_mask |= 1u << h;
       return true;
     };
     HVal c;
@@ -728,8 +730,10 @@ struct Compiler {
   // false edge is UNSAT and whose constant has a canonical memory form.
   struct AttrKey {
     bool ok = false, guarded = false;
+    bool contains = false;  // a set-membership key (image.h BT_CKEY): v0 = element hash, v1 = 1
     uint32_t h = 0, v0 = 0, v1 = 0;
   };
+
   AttrKey attr_key(const std::vector<uint32_t>& at, uint32_t n_atom_words) const {
     AttrKey k;
     const uint32_t n = n_atom_words / ATOM_WORDS;
@@ -746,6 +750,37 @@ struct Compiler {
           k.h = h;
           k.v0 = tag == T_LONG ? mk_w0(T_LONG, 0) : a[1];
           k.v1 = a[2];
+          k.guarded = std::find(present.begin(), present.end(), h) != present.end();
+        }
+        return k;
+      }
+      // hot(h).contains(primitive) / hot(h).contains({k: primitive, ..}) on the spine: a
+      // set-membership key (image.h BT_CKEY)
+      if ((kind == AK_CONTAINS || (kind == AK_RECSET && a[3] == 1 && a[2] == 1)) && f == AT_UNSAT && t != AT_UNSAT) {
+        uint32_t hv = 0;
+        bool keyable = false;
+        if (kind == AK_CONTAINS) {
+          keyable = reg_chash(a[1], a[2], a[3], hv);
+        } else {
+          const uint32_t* d = &at[a[1] - POL_WORDS];  // [n_holes, holes.., n_keys, (key, kind, a, b, c)..]
+          if (d[0] == 0) {
+            const uint32_t nk = d[1];
+            keyable = true;
+            hv = chash_mix(CHASH_REC, nk);
+            for (uint32_t j = 0; j < nk && keyable; j++) {
+              const uint32_t* fld = &d[2 + RS_FIELD_WORDS * j];
+              uint32_t fh = 0;
+              keyable = fld[1] == RF_CONST && reg_chash(fld[2], fld[3], fld[4], fh);
+              hv = chash_mix(chash_mix(hv, fld[0]), fh);
+            }
+          }
+        }
+        if (keyable) {
+          k.ok = true;
+          k.contains = true;
+          k.h = h;
+          k.v0 = hv;
+          k.v1 = 1;
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
         }
         return k;
@@ -976,6 +1011,38 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   // most specific level-1 keys of every policy: its scope's own entity / type / wildcard
   // filings as flat (key, policy) records, sorted: each key's policies stay in policy order, and
   // buckets are laid out in key order
+  // duplicate classes: policies whose records agree word for word (the global index aside, an
+  // action list by content) decide alike for every request; only the lowest-index member is filed,
+  // and its head lists the class (head word PW_CODE_N: bstream offset of [n, member indices...]),
+  // so the probe kernel evaluates the class once and records every member
+  std::vector<uint32_t> rep(n);
+  std::vector<std::vector<uint32_t>> members(n);
+  {
+    static const bool off = std::getenv("CEDARGPU_NO_CLASSES") != nullptr;  // A/B studies
+    auto key_of = [&](uint32_t q) {
+      std::vector<uint32_t> k(img.pstream.begin() + rec_off[q], img.pstream.begin() + rec_off[q] + rec_len[q]);
+      k[PW_CODE] = 0;
+      const uint32_t* d = &img.pol[(size_t)q * POL_WORDS];
+      if (((d[PW_KINDS] >> 8) & 0xFF) == SK_INSET) {
+        k[PW_A_EI] = 0;
+        k.insert(k.end(), img.cpool.begin() + d[PW_A_EI], img.cpool.begin() + d[PW_A_EI] + 2 * d[PW_A_ET]);
+      }
+      return k;
+    };
+    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;  // key hash -> representatives
+    for (uint32_t q = 0; q < n; q++) {
+      rep[q] = q;
+      if (off) continue;
+      const std::vector<uint32_t> k = key_of(q);
+      uint64_t h = 1469598103934665603ull;
+      for (uint32_t x : k) h = (h ^ x) * 1099511628211ull;
+      auto& cands = by_hash[h];
+      for (uint32_t c : cands)
+        if (key_of(c) == k) { rep[q] = c; break; }
+      if (rep[q] == q) cands.push_back(q);
+      members[rep[q]].push_back(q);
+    }
+  }
   constexpr uint32_t NO_POLICY = 0xFFFFFFFFu;  // a level-1 entry that only carries level-2 keys
   std::vector<std::pair<L1, uint32_t>> r1;
   std::vector<std::pair<L2, uint32_t>> r2;
@@ -983,6 +1050,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   r1.reserve(n);
   r2.reserve(2 * (size_t)n);
   for (uint32_t p = 0; p < n; p++) {
+    if (rep[p] != p) continue;  // filed through its class representative
     const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
     const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
     auto comp = [](uint32_t kind, uint32_t ty, uint32_t et, uint32_t ei, uint32_t& kc, uint32_t& t, uint32_t& i) {
@@ -1014,8 +1082,13 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
       img.combo_mask |= 1u << combo;
       if (!akeys[p].ok) { r1.emplace_back(k, p); continue; }
       r1.emplace_back(k, NO_POLICY);  // the level-1 entry carries the hmask even without unkeyed policies
-      r2.emplace_back(L2(k, {akeys[p].h, akeys[p].v0, akeys[p].v1}), p);
-      if (!akeys[p].guarded) r2.emplace_back(L2(k, {akeys[p].h, MISSING_W0, 0u}), p);
+      const uint32_t hk = akeys[p].h | (akeys[p].contains ? BT_CKEY : 0u);
+      r2.emplace_back(L2(k, {hk, akeys[p].v0, akeys[p].v1}), p);
+      if (!akeys[p].guarded) r2.emplace_back(L2(k, {hk, MISSING_W0, 0u}), p);
+      if (akeys[p].contains) {
+        r2.emplace_back(L2(k, {hk, NOTSET_W0, 0u}), p);  // contains on a non-set raises
+        img.cslot_mask |= 1u << akeys[p].h;
+      }
     }
   }
   std::sort(r1.begin(), r1.end());
@@ -1025,7 +1098,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   kents.erase(std::unique(kents.begin(), kents.end()), kents.end());
   img.key_ents = std::move(kents);
   // groups: [begin, end) ranges of one key; level-1 hmask from the level-2 keys under it
-  struct G { size_t b, e; uint32_t hmask = 0; uint32_t bloom[4] = {0, 0, 0, 0}; };
+  struct G { size_t b, e; uint32_t hmask = 0, cmask = 0; uint32_t bloom[4] = {0, 0, 0, 0}; };
   std::vector<G> g1, g2;
   for (size_t i = 0; i < r1.size();) {
     size_t j = i;
@@ -1044,7 +1117,8 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
     while (k < g1.size() && r1[g1[k].b].first < key) k++;
     if (k < g1.size() && r1[g1[k].b].first == key) {
       const auto& x = r2[g2[a].b].first.second;
-      g1[k].hmask |= 1u << x[0];
+      if (x[0] & BT_CKEY) g1[k].cmask |= 1u << (x[0] & ~BT_CKEY);
+      else g1[k].hmask |= 1u << x[0];
       const uint32_t bits = l2_bloom_bits(bucket_hash2(key_hash(key[0], key[1], key[2], key[3], key[4], key[5], key[6]), x[0], x[1], x[2]));
       for (uint32_t j = 0; j < 3; j++) {
         const uint32_t b = (bits >> (7 * j)) & 127u;
@@ -1057,13 +1131,20 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   uint32_t n_heads = 0;
   for (auto& x : r1) n_heads += x.second != NO_POLICY;
   n_heads += (uint32_t)r2.size();
-  std::vector<uint32_t> ext(n);
+  std::vector<uint32_t> ext(n), mlist(n, 0);
   uint64_t ext_end = (uint64_t)n_heads * HEAD_WORDS;
   for (uint32_t p = 0; p < n; p++) { ext[p] = (uint32_t)ext_end; ext_end += rec_len[p]; }
+  for (uint32_t p = 0; p < n; p++)
+    if (members[p].size() > 1) { mlist[p] = (uint32_t)ext_end; ext_end += 1 + members[p].size(); }
   if (ext_end >= (1ull << 32)) throw CedarError("scope index exceeds 16 GiB");
   img.bstream.assign(std::max<uint64_t>(ext_end, HEAD_WORDS), 0);
-  for (uint32_t p = 0; p < n; p++)
+  for (uint32_t p = 0; p < n; p++) {
     std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
+    if (mlist[p]) {
+      img.bstream[mlist[p]] = (uint32_t)members[p].size();
+      std::copy(members[p].begin(), members[p].end(), img.bstream.begin() + mlist[p] + 1);  // ascending
+    }
+  }
   uint32_t head = 0;
   auto put_heads = [&](auto begin, auto end) {
     const uint32_t first = head;
@@ -1074,6 +1155,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
       const uint32_t* src = &img.pstream[rec_off[p]];
       std::copy(src, src + std::min<uint32_t>(rec_len[p], HEAD_WORDS), hd);
       hd[PW_EXT] = ext[p];
+      hd[PW_CODE_N] = mlist[p];  // heads: the duplicate class's member list (0: the policy alone)
       head++;
     }
     return first;
@@ -1104,7 +1186,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
   for (const G& g : g1) {
     const L1& k = r1[g.b].first;
     const uint32_t first = put_heads(r1.begin() + (long)g.b, r1.begin() + (long)g.e);
-    const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], 0, 0, first,
+    const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], g.cmask, 0, first,
                                   head - first, g.hmask, g.bloom[0], g.bloom[1], g.bloom[2], g.bloom[3]};
     insert(l1_hash(k), e);
     filt_add(l1_hash(k));
@@ -1376,7 +1458,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.put64(table + 16 * DS_COUNT, begin);
   w.put64(table + 16 * DS_COUNT + 8, w.b.size());
   w.vec(pol); w.vec(tier_end); w.vec(code);
-  w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need);
+  w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
   w.u32((uint32_t)key_ents.size());
   for (uint64_t k : key_ents) w.u64(k);
   w.u32((uint32_t)strings.size());
@@ -1423,6 +1505,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->pol = r.vec(); img->tier_end = r.vec(); img->code = r.vec();
   img->amask_ok = r.u32(); img->n_atomic = r.u32(); img->indexed = r.u32(); img->combo_mask = r.u32();
   img->lane_need = r.u32();
+  img->cslot_mask = r.u32();
   {
     const size_t nb = img->btab.size() / BT_WORDS, nf = img->bfilt.size();
     if (!nb || (nb & (nb - 1)) || nf < 2 || (nf & (nf - 1))) throw CedarError("corrupt image (scope index)");

@@ -43,6 +43,32 @@ inline bool blk_rec_get(const std::vector<uint32_t>& blk, const std::vector<uint
   return false;
 }
 
+// element hash (image.h chash_*) of a memory-form value held in the block or the constant pool:
+// primitives canonically, records over (key sid, primitive field hash) in key order; anything else
+// by its tag (no set-membership key has such an element)
+inline uint32_t mem_chash(const std::vector<uint32_t>& blk, const std::vector<uint32_t>& cpool, uint32_t w0, uint32_t w1,
+                          bool nested = false) {
+  auto mem = [&](uint32_t x) -> const uint32_t* {
+    return ((x >> SPACE_SHIFT) == SP_CPOOL ? cpool.data() : blk.data()) + (x & OFF_MASK);
+  };
+  const uint32_t tag = w0 >> TAG_SHIFT;
+  switch (tag) {
+    case T_BOOL: case T_STR: return chash_prim(tag, w1, 0);
+    case T_LONG: return chash_prim(T_LONG, w1, (int32_t)w1 < 0 ? 0xFFFFFFFFu : 0u);
+    case T_LONGREF: { const uint32_t* q = mem(w0 & X_MASK); return chash_prim(T_LONG, q[0], q[1]); }
+    case T_ENT: return chash_prim(T_ENT, w0 & X_MASK, w1);
+    case T_REC: {
+      if (nested) break;
+      const uint32_t* q = mem(w0 & X_MASK);
+      uint32_t h = chash_mix(CHASH_REC, q[0]);
+      for (uint32_t j = 0; j < q[0]; j++) h = chash_mix(chash_mix(h, q[1 + 3 * j]), mem_chash(blk, cpool, q[2 + 3 * j], q[3 + 3 * j], true));
+      return h;
+    }
+    default: break;
+  }
+  return chash_prim(tag, 0, 0);
+}
+
 // [n, (type, id) x n] list at cpool[off] as UID keys
 inline void cpool_uids(const Image& img, uint32_t off, std::vector<uint64_t>& out) {
   const uint32_t n = img.cpool[off];
@@ -337,6 +363,27 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       blk.push_back(code | (aux << 8)); blk.push_back(k); blk.push_back(et); blk.push_back(ei);
       row[RW_HDR + 2 * h] = mk_w0(T_NONE, code | (fin ? HS_FINAL : 0u));
       row[RW_HDR + 2 * h + 1] = off;
+    }
+  }
+  // set-membership keys (image.h BT_CKEY): each such slot's element hashes, after the hot slots
+  if (img.cslot_mask) {
+    for (uint32_t h = 0; h < nh; h++) row[RW_HDR + 2 * nh + h] = 0xFFFFFFFFu;  // no list
+    std::vector<uint32_t> hs;
+    for (uint32_t m = img.cslot_mask; m; m &= m - 1) {
+      const uint32_t h = (uint32_t)__builtin_ctz(m);
+      const uint32_t w0 = row[RW_HDR + 2 * h], w1 = row[RW_HDR + 2 * h + 1], tag = w0 >> TAG_SHIFT;
+      hs.clear();
+      uint32_t head = tag == T_NONE ? CL_MISSING : tag != T_SET ? CL_NOTSET : 0u;
+      if (tag == T_SET) {
+        const uint32_t x = w0 & X_MASK;
+        const std::vector<uint32_t>& mm = (x >> SPACE_SHIFT) == SP_CPOOL ? img.cpool : blk;
+        const uint32_t off = x & OFF_MASK, n = mm[off];
+        head = n;
+        for (uint32_t k = 0; k < n; k++) hs.push_back(mem_chash(blk, img.cpool, mm[off + 1 + 2 * k], mm[off + 2 + 2 * k]));
+      }
+      row[RW_HDR + 2 * nh + h] = (uint32_t)blk.size();
+      blk.push_back(head);
+      blk.insert(blk.end(), hs.begin(), hs.end());
     }
   }
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");

@@ -126,12 +126,16 @@ constexpr uint32_t PW_EXT = PW_LANE;
 // the entry's hmask, with its own value of that slot (or MISSING_W0).
 // btab: open addressing, linear probing, power-of-two slots of BT_WORDS:
 //   [BT_USED | combo << 16 | (BT_L2 | h for level 2), p type, p id, a type, a id, r type, r id,
-//    value w0, value w1, first, count, hmask (level 1), l2 bloom x 4 (level 1)]; empty: word0 == 0.
+//    value w0 (level 1: cmask), value w1, first, count, hmask (level 1), l2 bloom x 4 (level 1)];
+//   empty: word0 == 0.
 //   The level-1 entry's 128-bit bloom (l2_bloom_bits) holds its level-2 keys: a request probes
 //   level 2 only for (h, value) pairs it admits.
 // Records: bstream[first * HEAD_WORDS ...] fixed heads (descriptor + the first 4 atoms) in bucket
 // order; the head's PW_EXT is the absolute bstream offset of the full variable-length record
 // (descriptor, atoms, atom data) in the ext area, which record-relative offsets address.
+// Duplicate classes: policies whose records agree word for word (global index aside) are filed
+// once, under the lowest-index member; its head's PW_CODE_N holds the bstream offset of the class
+// list [n, member global indices ascending] (0: a policy alone), and a hit records every member.
 constexpr uint32_t KC_WILD = 0, KC_ENT = 1, KC_TYPE = 2;  // component kinds
 __host__ __device__ constexpr inline uint32_t key_combo(uint32_t pk, uint32_t ak, uint32_t rk) { return pk | (ak << 2) | (rk << 3); }
 constexpr uint32_t KW_ANY = 0xFFFFFFFFu;  // id of a type-only component; both words of a wildcard
@@ -240,6 +244,38 @@ enum RowW : uint32_t {
   RW_HDR = 16,   // hot slots follow: (w0, w1) per hot path
 };
 constexpr uint32_t MISSING_W0 = 0xFFFFFFFFu;  // level-2 index key of an absent hot value
+// Set-membership level-2 keys: a policy whose satisfying evaluations all pass `hot(h).contains(c)`
+// (c a primitive, or a record template of primitive constants) is filed under (h | BT_CKEY,
+// element hash of c, 1), and also under (h | BT_CKEY, NOTSET_W0, 0) (a value that is no set makes
+// contains raise) and, unguarded, (h | BT_CKEY, MISSING_W0, 0). A level-1 entry's word 7 (cmask)
+// lists such slots. The request row then carries, after the hot slots, one word per hot slot:
+// for a slot of the image's cslot_mask (every slot a contains / containsAny atom reads) the block
+// offset of [n | CL_*, element hash x n], else ~0. The probe kernel probes each element of the
+// request's set; contains atoms compare element hashes first and the values only on a match
+// (image.h chash_*: equal values hash alike on both sides; a collision costs one exact compare).
+constexpr uint32_t BT_CKEY = 0x40, NOTSET_W0 = 0xFFFFFFFEu;
+constexpr uint32_t CL_MISSING = 0x80000000u, CL_NOTSET = 0x80000001u;
+__host__ __device__ constexpr inline uint32_t chash_mix(uint32_t h, uint32_t x) {
+  h ^= x;
+  h *= 0x01000193u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  return h;
+}
+// canonical primitive (tag, a, b): bool (T_BOOL, v, 0), long (T_LONG, lo, hi), string (T_STR,
+// sid, 0), entity (T_ENT, type sid, id sid); any other value hashes its tag alone
+__host__ __device__ constexpr inline uint32_t chash_prim(uint32_t tag, uint32_t a, uint32_t b) {
+  return chash_mix(chash_mix(chash_mix(0x811C9DC5u, tag), a), b);
+}
+constexpr uint32_t CHASH_REC = 0x9747B28Cu;  // record: mix(CHASH_REC, n), then (key sid, value hash) by key
+// element hash of a register-form primitive (tag word, y, z); false for other values
+__host__ __device__ constexpr inline bool reg_chash(uint32_t a, uint32_t b, uint32_t c, uint32_t& out) {
+  const uint32_t tag = a >> TAG_SHIFT;
+  if (tag == T_BOOL || tag == T_STR) { out = chash_prim(tag, b, 0); return true; }
+  if (tag == T_LONG) { out = chash_prim(T_LONG, b, c); return true; }
+  if (tag == T_ENT) { out = chash_prim(T_ENT, a & X_MASK, b); return true; }
+  return false;
+}
 // RW_PN / RW_RN / RW_AN fields
 constexpr uint32_t AN_COUNT = 0xFFFFu, AN_KEYS_SHIFT = 16, AN_KEYS = 0x7FFFu, AN_SELF = 0x80000000u;
 

@@ -599,3 +599,46 @@ def test_lowered_shapes_vs_oracle(ctx, name):
     check_items(ctx, stores, items)
     _, many = CASES[name](n=5000, seed=1)
     check_items_ref(ctx, stores, many)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_probe_kernel_duplicate_classes(ctx, seed):
+    """Duplicate policies (identical text under other IDs, the same condition with other action
+    lists, across tiers and effects, erroring ones included) are filed once as a class and hit for
+    every member: reasons, errors and their order vs the oracle, through the first pass and the
+    large stage (classes of up to ~100 members)."""
+    import random
+    g = Gen(12000 + seed)
+    r = random.Random(seed)
+    texts = [(f"p{t}.cedar", g.atomic_policies(g.r.randint(4, 30))) for t in range(g.r.randint(1, 3))]
+    stores = _atomic_only(texts)
+    dup = []
+    for st in stores:
+        _, name, text, _, _ = next(iter(st.documents()))
+        ps = co.parse_policies(text, name)
+        b = text.encode()
+        offs = [p.offset for p in ps] + [len(b)]
+        parts = [b[offs[i]:offs[i + 1]].decode() for i in range(len(ps))]
+        out = []
+        for part in parts:
+            out.append(part)
+            for _ in range(r.choice([0, 0, 1, 3, 40 if r.random() < 0.2 else 2])):
+                out.insert(r.randrange(len(out) + 1), part)
+        dup.append(cedargpu.MemoryStore(name, "\n".join(out)))
+    img = cedargpu.build_image(dup)
+    assert cedargpu.image_stats(img)["indexed"]
+    items = [g.item() for _ in range(600)]
+    check_items_ref(ctx, dup, items)
+    check_items(ctx, dup, items[:150])
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_probe_kernel_set_membership_keys(ctx, seed):
+    """contains() of primitives / constant record templates filed under element hashes (image.h
+    BT_CKEY): sets with extra-key / nested records, large longs, entities, non-set values, missing
+    attributes, duplicates, guarded and unguarded, vs both oracles."""
+    import contains_cases as cc
+    stores = [cedargpu.MemoryStore("c.cedar", cc.POLICIES)]
+    items = cc.items(1500, seed=seed)
+    check_items_ref(ctx, stores, items, want_indexed=True)
+    check_items(ctx, stores, items[:200])

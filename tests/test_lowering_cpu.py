@@ -44,3 +44,11 @@ def test_nesting_beyond_64_slots_is_a_named_limit():
         deep = f"1 + ({deep})"
     with pytest.raises(cedargpu.CompileError, match="64 registers"):
         cedargpu.build_image([cedargpu.MemoryStore("x.cedar", f"permit (principal, action, resource) when {{ {deep} > 0 }};")])
+
+
+def test_contains_shapes_index_and_oracles_agree():
+    import contains_cases as cc
+    img = cedargpu.build_image([cedargpu.MemoryStore("c.cedar", cc.POLICIES)])
+    st = cedargpu.image_stats(img)
+    assert st["indexed"] and st["policies"] == st["atomic"] == 12, st
+    _compare([[("c.cedar", cc.POLICIES)]], cc.items(300))
