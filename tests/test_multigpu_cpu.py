@@ -129,8 +129,10 @@ def _queue_worker(rank, world, port, out):
 
 def test_two_ranks_multi_context_queue_with_reload():
     import subprocess
-    subprocess.run(["make", "-s", "-C", os.path.join(os.path.dirname(STUB), "..", "..", "cedar-access-control-for-k8s_amd",
-                                                      "csrc"), "stub"], check=True, capture_output=True)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # a fresh checkout has no build/san yet: name csrc from the repo root, not through build/san/..
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "cedar-access-control-for-k8s_amd", "csrc"), "stub"],
+                   check=True, capture_output=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
