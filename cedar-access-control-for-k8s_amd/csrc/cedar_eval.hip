@@ -2022,7 +2022,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.gstr_bytes = at(DS_GSTR_BYTES);
   d.n_static = img.n_static();
   d.lane_need = img.lane_need;
-  d.cslot_mask = img.cslot_mask;
+  d.cslot_mask = img.list_mask();
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
   d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
   d.fmask = (uint32_t)(img.bfilt.size() / 2) - 1;
@@ -2380,27 +2380,31 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
 
 // Launches the evaluation of n requests: the request-per-wave kernel over the scope index when the
 // image is fully indexed, else the request-per-lane policy-stream kernel.
-// Probe-kernel segment width (lanes per request): 16 by default; CEDARGPU_PROBE_SEG=32 / 64 for
-// comparisons.
+// Probe-kernel segment width (lanes per request): 8 by default, 8 requests per wave (on the C3
+// group-DAG workload 2.94e8 decisions/s against 2.21e8 with 16 lanes: a request's ~60 level-1
+// probes are dependent-latency chains, and more requests in flight per wave hide them;
+// profiles/r02/ab_seg8); CEDARGPU_PROBE_SEG=16 / 32 / 64 for comparisons.
 static uint32_t probe_seg() {
   static const uint32_t seg = [] {
     const char* e = std::getenv("CEDARGPU_PROBE_SEG");
-    const uint32_t v = e ? (uint32_t)std::atoi(e) : 16u;
-    return (v == 8u || v == 32u || v == 64u) ? v : 16u;
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : 8u;
+    return (v == 16u || v == 32u || v == 64u) ? v : 8u;
   }();
   return seg;
 }
 
 // big: the re-run variant for requests with more hits than the default stage (one request per
 // wave, 1024 hits staged)
-// Minimum waves per SIMD the 16-lane kernel is register-allocated for: 4 (128 VGPRs, a few spilled
-// dwords) measured +15 % over the unconstrained allocation (3 waves) and ahead of 5;
-// CEDARGPU_PROBE_OCC=1 / 5 select the others for comparisons.
+// Minimum waves per SIMD the probe kernel is register-allocated for. 16 lanes: 4 (128 VGPRs, a few
+// spilled dwords) measured +15 % over the unconstrained allocation (3 waves) and ahead of 5.
+// 8 lanes: 3 (168 VGPRs, no spills; the 8-request LDS region allows no more) measured 2.94e8
+// against 2.44e8 when forced to 4; CEDARGPU_PROBE_OCC selects the others for comparisons.
 static uint32_t probe_occ() {
   static const uint32_t occ = [] {
     const char* e = std::getenv("CEDARGPU_PROBE_OCC");
-    const uint32_t v = e ? (uint32_t)std::atoi(e) : 4u;
-    return (v == 1u || v == 3u || v == 5u) ? v : 4u;
+    const uint32_t d = probe_seg() == 8 ? 3u : 4u;
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : d;
+    return (v == 1u || v == 3u || v == 4u || v == 5u) ? v : d;
   }();
   return occ;
 }
@@ -2426,7 +2430,8 @@ static uint32_t probe_wpb() {
 
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
   const uint32_t seg = big ? 64u : probe_seg();
-  const uint32_t wpb = (!big && seg == 16 && (probe_occ() == 4 || probe_occ() == 5) && !probe_stats()) ? probe_wpb() : WAVES;
+  const bool w1 = (seg == 16 && (probe_occ() == 4 || probe_occ() == 5)) || (seg == 8 && (probe_occ() == 3 || probe_occ() == 4));
+  const uint32_t wpb = (!big && w1 && !probe_stats()) ? probe_wpb() : WAVES;
   const uint32_t per_block = wpb * (64 / seg);
   const dim3 grid((n + per_block - 1) / per_block);
   const uint32_t occ = probe_occ();
@@ -2438,7 +2443,8 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     ks.stats = dstats;
     std::vector<unsigned long long> h(nw * 16);
     (void)hipMemsetAsync(dstats, 0, h.size() * sizeof(unsigned long long), s);
-    hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, true>), grid, dim3(BLOCK), 0, s, ks);
+    if (seg == 8) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3, true>), grid, dim3(BLOCK), 0, s, ks);
+    else hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 4, true>), grid, dim3(BLOCK), 0, s, ks);
     (void)hipMemcpyAsync(h.data(), dstats, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
     (void)hipFree(dstats);
@@ -2467,6 +2473,8 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
   else if (seg == 16 && occ == 5 && wpb == 1) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5, false, 1>), grid, dim3(64), 0, s, k);
   else if (seg == 16 && occ == 5) hipLaunchKernelGGL((cedar_probe_kernel<16, 64, 5>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 16) hipLaunchKernelGGL((cedar_probe_kernel<16, 64>), grid, dim3(BLOCK), 0, s, k);
+  else if (seg == 8 && occ == 3 && wpb == 1) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3, false, 1>), grid, dim3(64), 0, s, k);
+  else if (seg == 8 && occ == 4 && wpb == 1) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, false, 1>), grid, dim3(64), 0, s, k);
   else if (seg == 8) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3>), grid, dim3(BLOCK), 0, s, k);
   else if (seg == 32) hipLaunchKernelGGL((cedar_probe_kernel<32, 64>), grid, dim3(BLOCK), 0, s, k);
   else hipLaunchKernelGGL((cedar_probe_kernel<64, 64>), grid, dim3(BLOCK), 0, s, k);

@@ -731,6 +731,7 @@ struct Compiler {
   struct AttrKey {
     bool ok = false, guarded = false;
     bool contains = false;  // a set-membership key (image.h BT_CKEY): v0 = element hash, v1 = 1
+    uint32_t plen = 0;      // a prefix key (image.h "prefix level-2 keys"): prefix bytes hashed into v0
     uint32_t h = 0, v0 = 0, v1 = 0;
   };
 
@@ -780,6 +781,24 @@ struct Compiler {
           k.contains = true;
           k.h = h;
           k.v0 = hv;
+          k.v1 = 1;
+          k.guarded = std::find(present.begin(), present.end(), h) != present.end();
+        }
+        return k;
+      }
+      // hot(h) like "lit*..." on the spine: a prefix key on the pattern's opening literal (a
+      // pattern without a star is its whole literal, which is also a prefix of every match)
+      if (kind == AK_LIKE && f == AT_UNSAT && t != AT_UNSAT) {
+        const uint32_t* pw = &at[a[1] - POL_WORDS];  // [flags, prefix len, prefix bytes ...]
+        const uint32_t len = std::min(pw[1], PFX_MAX);
+        if (len > 0) {
+          uint8_t bytes[PFX_MAX];
+          for (uint32_t j = 0; j < len; j++) bytes[j] = (uint8_t)(pw[2 + (j >> 2)] >> (8 * (j & 3)));
+          k.ok = true;
+          k.contains = true;
+          k.plen = len;
+          k.h = h;
+          k.v0 = pfx_hash(bytes, len);
           k.v1 = 1;
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
         }
@@ -978,13 +997,40 @@ struct Compiler {
 // when it has one), then lay out fixed record heads bucket by bucket and the full records in the
 // ext area.
 template <class AK>
-static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
+static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   using L1 = std::array<uint32_t, 7>;                   // (combo, pt, pi, at, ai, rt, ri)
   using L2 = std::pair<L1, std::array<uint32_t, 3>>;    // (+ h, v0, v1)
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
   img.key_ents.clear();
   img.combo_mask = 0;
+  img.pslot_mask = 0;
+  img.pfx.assign((size_t)img.n_hot() * PFX_LENS, 0);
+  // prefix keys (image.h "prefix level-2 keys"): per slot the PFX_LENS most used prefix lengths;
+  // a policy whose length is not among them, or whose slot a contains atom reads, stays unkeyed
+  std::vector<AK> akeys = akeys_in;
+  {
+    static const bool off = std::getenv("CEDARGPU_NO_PREFIX_KEYS") != nullptr;  // A/B studies
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> uses;  // (slot, length) -> policies
+    for (auto& k : akeys)
+      if (k.ok && k.plen) {
+        if (off || ((img.cslot_mask >> k.h) & 1)) k.ok = false;
+        else uses[{k.h, k.plen}]++;
+      }
+    for (uint32_t h = 0; h < img.n_hot(); h++) {
+      std::vector<std::pair<uint32_t, uint32_t>> ls;  // (-uses, length)
+      for (auto it = uses.lower_bound({h, 0}); it != uses.end() && it->first.first == h; ++it)
+        ls.emplace_back(0u - it->second, it->first.second);
+      std::sort(ls.begin(), ls.end());
+      for (size_t j = 0; j < ls.size() && j < PFX_LENS; j++) img.pfx[(size_t)h * PFX_LENS + j] = ls[j].second;
+    }
+    for (auto& k : akeys)
+      if (k.ok && k.plen) {
+        const uint32_t* l = &img.pfx[(size_t)k.h * PFX_LENS];
+        if (std::find(l, l + PFX_LENS, k.plen) == l + PFX_LENS) k.ok = false;
+        else img.pslot_mask |= 1u << k.h;
+      }
+  }
   img.indexed = (n > 0 && img.n_atomic == n) ? 1u : 0u;
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
@@ -1086,8 +1132,8 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys) {
       r2.emplace_back(L2(k, {hk, akeys[p].v0, akeys[p].v1}), p);
       if (!akeys[p].guarded) r2.emplace_back(L2(k, {hk, MISSING_W0, 0u}), p);
       if (akeys[p].contains) {
-        r2.emplace_back(L2(k, {hk, NOTSET_W0, 0u}), p);  // contains on a non-set raises
-        img.cslot_mask |= 1u << akeys[p].h;
+        r2.emplace_back(L2(k, {hk, NOTSET_W0, 0u}), p);  // contains on a non-set (like on a non-string) raises
+        if (!akeys[p].plen) img.cslot_mask |= 1u << akeys[p].h;
       }
     }
   }
@@ -1459,6 +1505,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.put64(table + 16 * DS_COUNT + 8, w.b.size());
   w.vec(pol); w.vec(tier_end); w.vec(code);
   w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
+  w.u32(pslot_mask); w.vec(pfx);
   w.u32((uint32_t)key_ents.size());
   for (uint64_t k : key_ents) w.u64(k);
   w.u32((uint32_t)strings.size());
@@ -1506,6 +1553,10 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->amask_ok = r.u32(); img->n_atomic = r.u32(); img->indexed = r.u32(); img->combo_mask = r.u32();
   img->lane_need = r.u32();
   img->cslot_mask = r.u32();
+  img->pslot_mask = r.u32();
+  img->pfx = r.vec();
+  if (img->pfx.size() != (size_t)img->n_hot() * PFX_LENS && !(img->pfx.empty() && !img->pslot_mask))
+    throw CedarError("corrupt image (prefix lengths)");
   {
     const size_t nb = img->btab.size() / BT_WORDS, nf = img->bfilt.size();
     if (!nb || (nb & (nb - 1)) || nf < 2 || (nf & (nf - 1))) throw CedarError("corrupt image (scope index)");

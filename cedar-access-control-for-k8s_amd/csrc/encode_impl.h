@@ -365,16 +365,26 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       row[RW_HDR + 2 * h + 1] = off;
     }
   }
-  // set-membership keys (image.h BT_CKEY): each such slot's element hashes, after the hot slots
-  if (img.cslot_mask) {
+  // set-membership keys (image.h BT_CKEY): each such slot's element hashes, after the hot slots;
+  // prefix keys (image.h "prefix level-2 keys"): a string's prefix hashes at the slot's lengths
+  if (img.list_mask()) {
     for (uint32_t h = 0; h < nh; h++) row[RW_HDR + 2 * nh + h] = 0xFFFFFFFFu;  // no list
     std::vector<uint32_t> hs;
-    for (uint32_t m = img.cslot_mask; m; m &= m - 1) {
+    for (uint32_t m = img.list_mask(); m; m &= m - 1) {
       const uint32_t h = (uint32_t)__builtin_ctz(m);
       const uint32_t w0 = row[RW_HDR + 2 * h], w1 = row[RW_HDR + 2 * h + 1], tag = w0 >> TAG_SHIFT;
       hs.clear();
-      uint32_t head = tag == T_NONE ? CL_MISSING : tag != T_SET ? CL_NOTSET : 0u;
-      if (tag == T_SET) {
+      const bool pfx = (img.pslot_mask >> h) & 1;
+      const uint32_t want = pfx ? T_STR : T_SET;
+      uint32_t head = tag == T_NONE ? CL_MISSING : tag != want ? CL_NOTSET : 0u;
+      if (pfx && tag == T_STR) {
+        const std::string_view sv = w1 < img.n_gstr() ? std::string_view(img.strings[w1]) : std::string_view(E.strs[w1 - img.n_gstr()]);
+        for (uint32_t j = 0; j < PFX_LENS; j++) {
+          const uint32_t len = img.pfx[(size_t)h * PFX_LENS + j];
+          if (len && len <= sv.size()) hs.push_back(pfx_hash(reinterpret_cast<const uint8_t*>(sv.data()), len));
+        }
+        head = (uint32_t)hs.size();
+      } else if (!pfx && tag == T_SET) {
         const uint32_t x = w0 & X_MASK;
         const std::vector<uint32_t>& mm = (x >> SPACE_SHIFT) == SP_CPOOL ? img.cpool : blk;
         const uint32_t off = x & OFF_MASK, n = mm[off];

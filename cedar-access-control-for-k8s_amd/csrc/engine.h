@@ -76,7 +76,12 @@ struct Image {
   uint32_t n_hot() const { return (uint32_t)hot.size() / cgi::HOT_WORDS; }
   // hot slots with set-membership level-2 keys (image.h BT_CKEY): rows then carry n_hot more words
   uint32_t cslot_mask = 0;
-  uint32_t row_words() const { return (cgi::RW_HDR + 2 * n_hot() + (cslot_mask ? n_hot() : 0u) + 3) & ~3u; }
+  // hot slots with prefix level-2 keys (image.h "prefix level-2 keys") and their prefix lengths,
+  // PFX_LENS per hot slot (0 = unused)
+  uint32_t pslot_mask = 0;
+  std::vector<uint32_t> pfx;
+  uint32_t list_mask() const { return cslot_mask | pslot_mask; }
+  uint32_t row_words() const { return (cgi::RW_HDR + 2 * n_hot() + (list_mask() ? n_hot() : 0u) + 3) & ~3u; }
   // string -> id over a string_view: open addressing, entries (hash high 32 bits << 32 | id + 1),
   // 0 = empty; size is a power of two. Built by build_lookup once the table is final.
   std::vector<uint64_t> lookup;

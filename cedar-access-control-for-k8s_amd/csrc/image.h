@@ -276,6 +276,22 @@ __host__ __device__ constexpr inline bool reg_chash(uint32_t a, uint32_t b, uint
   if (tag == T_ENT) { out = chash_prim(T_ENT, a & X_MASK, b); return true; }
   return false;
 }
+// Prefix level-2 keys: a policy whose satisfying evaluations all pass `hot(h) like "lit*..."`
+// (a pattern that opens with a literal) is filed in the same BT_CKEY namespace under
+// (h | BT_CKEY, pfx_hash(first L literal bytes), 1), L = min(literal length, PFX_MAX); also under
+// NOTSET_W0 (a value that is no string makes `like` raise) and, unguarded, MISSING_W0. The image
+// keeps per slot up to PFX_LENS such lengths (Image::pfx, 0 = unused; pslot_mask lists the slots).
+// For a slot of pslot_mask the request block's list holds, instead of element hashes, the value's
+// prefix hashes at each of the slot's lengths it is long enough for. A slot read by any contains
+// atom (cslot_mask) is never prefix-keyed, so one list per slot serves both kinds. Host-side only:
+// the device probes the list's words as it probes element hashes.
+constexpr uint32_t PFX_LENS = 4, PFX_MAX = 16;
+constexpr uint32_t CHASH_PFX = 0x3C6EF372u;
+inline uint32_t pfx_hash(const uint8_t* s, uint32_t len) {
+  uint32_t h = chash_mix(CHASH_PFX, len);
+  for (uint32_t k = 0; k < len; k++) h = chash_mix(h, s[k]);
+  return h;
+}
 // RW_PN / RW_RN / RW_AN fields
 constexpr uint32_t AN_COUNT = 0xFFFFu, AN_KEYS_SHIFT = 16, AN_KEYS = 0x7FFFu, AN_SELF = 0x80000000u;
 
@@ -375,7 +391,7 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 7;
+constexpr uint32_t IMG_VERSION = 8;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob
