@@ -77,8 +77,15 @@ struct KArgs {
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
   uint32_t hlists;  // rows carry element-hash lists (image.h "set-membership keys")
   uint32_t l1filt;  // level-1 probes consult the key filter first (CEDARGPU_L1_FILTER=0: off, A/B)
+  uint32_t l2filt;  // level-2 probes too, after the level-1 entry's own bloom (CEDARGPU_L2_FILTER)
   uint32_t n_static, smask, lane_stride;
+  // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
+  // count at scan[i] (SCAN_OVF: more than SCAN_CAP), its (first head, count | combo) pairs at
+  // scan + scan_n + i * 2 * SCAN_CAP
+  uint32_t* scan;
+  uint32_t scan_n;
 };
+constexpr uint32_t SCAN_CAP = 24, SCAN_OVF = 0xFFFFFFFFu, SCAN_COUNT = (1u << 27) - 1, SCAN_COMBO_SHIFT = 27;
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
 // registers; the only non-inlined function (structural equality) takes plain pointers.
@@ -1439,13 +1446,19 @@ struct SegLds {
   static constexpr uint32_t NS = 64 / SEG;     // requests per wave
   static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : 32;  // staged buckets per request (>= 2 stages)
   static constexpr uint32_t HC = HCAP;         // hits per request (more: RF_BIG / RF_GENERAL re-run)
-  static constexpr uint32_t XC = HCAP >= 256 ? 64 : 16;  // error details per request
-  uint32_t efirst[NS][EC];   // found bucket: first head index
-  uint32_t epre[NS][EC + 1]; // candidate counts, then their exclusive prefix
-  uint32_t ecombo[NS][EC];   // key combo of the bucket's level-1 key
+  // error details per request (more: the on-device follow-up, which holds 64)
+  static constexpr uint32_t XC = HCAP >= 256 ? 64 : 8;
+  // the staged buckets live until the key loop ends, the merge's sort keys only after it: one region
+  union {
+    struct {
+      uint32_t efirst[NS][EC];   // found bucket: first head index
+      uint32_t epre[NS][EC];     // candidate counts, then their exclusive prefix
+      uint32_t ecombo[NS][EC];   // key combo of the bucket's level-1 key
+    } b;
+    uint32_t hs[NS][HC];         // merge: sort keys (policy index << 12 | hit slot)
+  } u;
   uint32_t hp[NS][HC];       // hit: global policy index
   uint32_t hm[NS][HC];       // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
-  uint32_t hs[NS][HC];       // merge: sort keys (policy index << 8 | hit slot)
   uint32_t he[NS][XC * 4];   // error details: code | aux << 8, k, et, ei
   uint2 hot[NS][NHOT];
 };
@@ -1535,6 +1548,134 @@ __device__ __forceinline__ bool l2_bloom_maybe(uint4 b, uint32_t h2) {
   }
   return ok;
 }
+
+// ---- split first pass: the index scan ---------------------------------------------------------
+// SEG lanes per request enumerate its level-1 keys as the probe kernel does (every used combo's
+// product of candidate components, SEG keys a step) and probe each found entry's level-2 keys
+// (hot slots in its hmask, set-membership / prefix list elements in its cmask), segment by
+// segment alternating the two; found buckets that hold candidate heads go straight to a.scan. No
+// LDS and no candidate evaluation: far fewer registers than the probe kernel, so more requests are
+// in flight per CU; the probe kernel's SPLIT variant then evaluates the buckets' heads.
+template <uint32_t SEG, uint32_t MINW = 1>
+__global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
+  const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
+  auto sballot = [&](bool p) -> uint64_t { return __ballot(p) & smask; };
+  auto sbcast = [&](uint32_t x, uint32_t k) -> uint32_t { return (uint32_t)__shfl((int)x, (int)(sbase + k)); };
+  const uint32_t gid = blockIdx.x * (64 / SEG) + seg;
+  const bool valid = gid < a.n_req;
+  const uint32_t* row = a.rows + (size_t)(valid ? gid : 0u) * a.row_words;
+  const uint32_t rw = (valid && sl < RW_HDR) ? row[sl] : 0u;
+  const uint32_t rw_hi = (SEG < RW_HDR && valid && SEG + sl < RW_HDR) ? row[SEG + sl] : 0u;
+  auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
+  const uint32_t* blk = a.heap + hdr(RW_BLK);
+  const uint32_t pt = hdr(RW_P), pi = hdr(RW_P + 1), at = hdr(RW_A), ai = hdr(RW_A + 1), rt = hdr(RW_R), ri = hdr(RW_R + 1);
+  const uint32_t pn = hdr(RW_PN), rn = hdr(RW_RN), an = hdr(RW_AN);
+  const uint32_t p_anc = hdr(RW_PANC), r_anc = hdr(RW_RANC), a_anc = hdr(RW_AANC);
+  const uint32_t cm = a.combo_mask;
+  const uint32_t nP = (pn >> 31) + ((pn >> AN_KEYS_SHIFT) & AN_KEYS), nA = (an >> 31) + ((an >> AN_KEYS_SHIFT) & AN_KEYS),
+                 nR = (rn >> 31) + ((rn >> AN_KEYS_SHIFT) & AN_KEYS);
+  uint32_t n_keys = 0;
+  if (valid)
+    for (uint32_t m = cm; m; m &= m - 1) {
+      const uint32_t cb = __builtin_ctz(m);
+      n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+    }
+  uint32_t* pairs = a.scan + a.scan_n + (size_t)gid * (2 * SCAN_CAP);
+  uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0;
+  uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
+  uint4 blm = make_uint4(0, 0, 0, 0);
+  uint32_t csl = 0, ch = 0, cl = 0, ck = 0, cn = 0;
+  for (;;) {
+    const bool l2 = sballot(hm != 0 || csl != 0 || ck < cn) != 0;
+    const bool done = !l2 && kb >= n_keys;
+    if (__ballot(!done) == 0) break;
+    uint3 e = make_uint3(0, 0, 0);
+    if (!done) {
+      if (l2) {
+        if (hm) {
+          const uint32_t h = __builtin_ctz(hm);
+          hm &= hm - 1;
+          const uint2 v = *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h);
+          const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
+          const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
+          if (l2_bloom_maybe(blm, h2) && (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2)))
+            e = probe(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, unused);
+        } else if (csl || ck < cn) {
+          uint32_t v0 = 0, v1 = 0;
+          bool go = false;
+          if (ck >= cn) {
+            ch = __builtin_ctz(csl);
+            csl &= csl - 1;
+            const uint32_t lo = row[RW_HDR + 2 * a.n_hot + ch];
+            const uint32_t hd = blk[lo];
+            ck = cn = 0;
+            if (hd & 0x80000000u) {
+              v0 = hd == CL_MISSING ? MISSING_W0 : NOTSET_W0;
+              go = true;
+            } else {
+              cl = lo + 1;
+              cn = hd;
+            }
+          }
+          if (!go && ck < cn) {
+            v0 = blk[cl + ck];
+            v1 = 1;
+            ck++;
+            go = true;
+          }
+          if (go) {
+            const uint32_t hs = ch | BT_CKEY;
+            const uint32_t h2 = bucket_hash2(h1, hs, v0, v1);
+            if (l2_bloom_maybe(blm, h2) && (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2)))
+              e = probe(a.btab, a.bmask, h2, w0 | BT_L2 | hs, kp, ka, kr, v0, v1, unused);
+          }
+        }
+      } else {
+        const uint32_t k = kb + sl;
+        kb += SEG;
+        uint32_t j = k;
+        bool found = false;
+        for (uint32_t m = cm; m; m &= m - 1) {
+          const uint32_t cb = __builtin_ctz(m);
+          const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+          if (!found) {
+            if (j < cnt) { combo = cb; found = true; }
+            else j -= cnt;
+          }
+        }
+        if (k < n_keys) {
+          const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
+          const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
+          uint32_t ip = j, ia = 0, ir = 0;
+          if (na_ != 1u || (rkc == KC_ENT && nR != 1u)) {
+            const uint32_t t2 = j / np_;
+            ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
+          }
+          kp = key_comp(pkc, ip + 1 - (pn >> 31), pt, pi, blk, p_anc);
+          ka = key_comp(akc, ia + 1 - (an >> 31), at, ai, blk, a_anc);
+          kr = key_comp(rkc, ir + 1 - (rn >> 31), rt, ri, blk, r_anc);
+          w0 = BT_USED | (combo << 16);
+          h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
+          uint32_t cmv = 0;
+          if (!a.l1filt || filt_maybe(a.bfilt, a.fmask, h1))
+            e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, &blm, &cmv);
+          hm = e.z;
+          csl = cmv;
+        }
+      }
+    }
+    // found buckets go to the request's list in segment order
+    const uint64_t m = sballot(e.y != 0);
+    const uint32_t pos = nb + mbcnt64(m);
+    if (e.y && pos < SCAN_CAP)
+      *reinterpret_cast<uint2*>(pairs + 2 * pos) = make_uint2(e.x, min(e.y, SCAN_COUNT) | (combo << SCAN_COMBO_SHIFT));
+    nb += popc64(m);
+  }
+  if (valid && sl == 0) a.scan[gid] = nb <= SCAN_CAP ? nb : SCAN_OVF;
+}
+
 // SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
 // (row -> level-1 probe -> level-2 probe -> head -> atom data) overlap. Collectives (ballot, scan,
 // min, broadcast) are segment-local; loops run while any segment of the wave has work.
@@ -1546,7 +1687,7 @@ __device__ __forceinline__ bool l2_bloom_maybe(uint4 b, uint32_t h2) {
 // [14] candidate evaluation [15] merge and result writes
 // PW: waves per block. Resources are granted per block, so a block's LDS and wave slots return
 // only when its slowest wave ends; smaller blocks let fast waves' slots be reused sooner.
-template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false, uint32_t PW = WAVES>
+template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false, uint32_t PW = WAVES, bool SPLIT = false>
 __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint64_t t_start = STATS ? clock64() : 0;
   using L = SegLds<SEG, HCAP>;
@@ -1631,13 +1772,155 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t cb = __builtin_ctz(m);
       n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
     }
+  uint32_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // STATS only (per lane)
+  // runs every segment's staged buckets (ne of them, in LDS): candidate heads, scope re-check,
+  // atom graph, hits recorded
+  auto flush = [&]() {
+    const uint64_t t_c0 = STATS ? clock64() : 0;
+    // ---- run every segment's staged buckets ----
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; __ballot(b0 < ne); b0 += SEG) {
+      const uint32_t b = b0 + sl;
+      const uint32_t cnt = b < ne ? wl.u.b.epre[seg][b] : 0u;
+      const uint32_t inc = sscan(cnt);
+      wave_lds_sync();
+      if (b < ne) wl.u.b.epre[seg][b] = carry + inc - cnt;
+      carry += sbcast(inc, SEG - 1);
+      wave_lds_sync();
+    }
+    const uint32_t total = carry;
+    for (uint32_t base = 0; __ballot(base < total); base += SEG) {
+      const uint32_t idx = base + sl;
+      bool ok = idx < total;
+      uint32_t lo = 0, hi = ne;  // bucket of candidate idx: last b with epre[b] <= idx
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (wl.u.b.epre[seg][mid] <= idx) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t hidx = ok ? wl.u.b.efirst[seg][lo] + (idx - wl.u.b.epre[seg][lo]) : 0u;
+      const uint32_t bcombo = ok ? wl.u.b.ecombo[seg][lo] : 0u;
+      const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
+      const uint4* d4 = reinterpret_cast<const uint4*>(head);
+      const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+      const uint32_t flags = q0.x, kinds = q0.y;
+      const uint32_t tier = (flags >> 8) & 0xFF;
+      ok = ok && tier <= min_tier;
+      const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
+      // scope re-check; an `in` / `is in` entity matched by the bucket key's entity component
+      // holds already (the request enumerated that key from its ancestor-or-self list)
+      if (ak != SK_ANY) {
+        if (a.amask_ok) {
+          const uint64_t pm = ((uint64_t)q3.w << 32) | q3.z;
+          ok = ok && (((ak == SK_EQ ? as : am) & pm) != 0);
+        } else if (ak == SK_EQ) {
+          ok = ok && c.at == q1.y && c.ai == q1.z;
+        } else if (ak == SK_IN) {
+          ok = ok && anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, q1.y, q1.z);
+        } else if (((bcombo >> 2) & 1) != KC_ENT) {
+          bool any = false;
+          for (uint32_t x = 0; ok && x < q1.y && !any; x++)
+            any = anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, a.cpool[q1.z + 2 * x], a.cpool[q1.z + 2 * x + 1]);
+          ok = ok && any;
+        }
+      }
+      if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
+      if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
+      else if ((pk == SK_IN || pk == SK_ISIN) && (bcombo & 3) != KC_ENT)
+        ok = ok && anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, q0.w, q1.x);
+      if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
+      if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
+      else if ((rk == SK_IN || rk == SK_ISIN) && (bcombo >> 3) != KC_ENT)
+        ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
+      // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
+      // atom data in the policy's full record at PW_EXT)
+      const uint32_t na = q3.x / ATOM_WORDS;
+      const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
+      uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
+      if (STATS) { st[6] += idx < total; st[7] += ok; st[11] += sl == 0; }
+      bool err = false;
+      Err e{0, 0, 0, 0, 0};
+      while (__ballot(pc < na)) {
+        if (pc < na) {
+          const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
+          const uint32_t rr = eval_atom<false>(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
+          if (STATS) st[8]++;
+          if (rr == 3u) { general = true; pc = AT_UNSAT; }
+          else if (rr == 2u) { err = true; pc = AT_UNSAT; }
+          else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
+        }
+      }
+      // record hits (segment-local slots): a duplicate class (head word PW_CODE_N, image.h) hits
+      // for every member, all sharing the head's error detail
+      const bool hit = ok && (err || pc == AT_SAT);
+      const uint32_t mlist = q2.w;
+      const uint32_t nmem = hit ? (mlist ? a.bstream[mlist] : 1u) : 0u;
+      if (STATS) st[9] += nmem;
+      const uint32_t mincl = sscan(nmem);
+      const uint64_t xmask = sballot(hit && err);
+      const uint32_t xpos = nx + mbcnt64(xmask);
+      const uint32_t hmv = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8) | (min(xpos, 0xFFu) << 16);
+      const uint32_t pos0 = nh + mincl - nmem;
+      if (hit && !mlist && pos0 < L::HC) {
+        wl.hp[seg][pos0] = q2.z;  // PW_CODE: global policy index
+        wl.hm[seg][pos0] = hmv;
+      }
+      // class members: the segment copies each hitting class's list together (coalesced)
+      for (uint64_t cls = sballot(hit && mlist != 0); __ballot(cls != 0);) {
+        const bool act = cls != 0;  // this segment still has a class to copy
+        const uint32_t src = act ? (uint32_t)__builtin_ctzll(cls) : lane;
+        cls &= act ? cls - 1 : 0ull;
+        const uint32_t p0 = (uint32_t)__shfl((int)pos0, (int)src), nm = (uint32_t)__shfl((int)nmem, (int)src);
+        const uint32_t mls = (uint32_t)__shfl((int)mlist, (int)src), hv = (uint32_t)__shfl((int)hmv, (int)src);
+        const uint32_t ml = act ? mls : 0u;
+        if (ml)
+          for (uint32_t j = sl; j < nm && p0 + j < L::HC; j += SEG) {
+            wl.hp[seg][p0 + j] = a.bstream[ml + 1 + j];
+            wl.hm[seg][p0 + j] = hv;
+          }
+      }
+      if (hit) {
+        if (err && xpos < L::XC) {
+          wl.he[seg][4 * xpos] = e.code | (e.aux << 8);
+          wl.he[seg][4 * xpos + 1] = e.k;
+          wl.he[seg][4 * xpos + 2] = e.et;
+          wl.he[seg][4 * xpos + 3] = e.ei;
+        }
+      }
+      nh += sbcast(mincl, SEG - 1);
+      nx += popc64(xmask);
+      min_tier = min(min_tier, smin(hit ? tier : 0xFFu));
+    }
+    ne = 0;
+    if (STATS && sl == 0) st[10]++;
+    wave_lds_sync();
+    if (STATS) t_cand += clock64() - t_c0;
+  };
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);  // level-2 bloom of this lane's level-1 entry
   // set-membership slots of the entry still to probe (image.h BT_CKEY), the current one's element
   // hash list in the request block and the next element
   uint32_t csl = 0, ch = 0, cl = 0, ck = 0, cn = 0;
-  uint32_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // STATS only (per lane)
+  if constexpr (SPLIT) {
+    // the scan kernel found this request's buckets (cedar_scan_kernel): stage them EC at a time
+    const uint32_t nb = valid ? a.scan[gid] : 0u;
+    const uint32_t nbk = nb == SCAN_OVF ? 0u : nb;
+    if (nb == SCAN_OVF) nh = L::HC + 1;  // more buckets than the scan holds: the large-stage follow-up
+    const uint32_t* pairs = a.scan + a.scan_n + (size_t)gid * (2 * SCAN_CAP);
+    for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
+      for (uint32_t i = sl; i < L::EC; i += SEG)
+        if (b0 + i < nbk) {
+          const uint2 q = *reinterpret_cast<const uint2*>(pairs + 2 * (b0 + i));
+          wl.u.b.efirst[seg][i] = q.x;
+          wl.u.b.epre[seg][i] = q.y & SCAN_COUNT;
+          wl.u.b.ecombo[seg][i] = q.y >> SCAN_COMBO_SHIFT;
+        }
+      ne = b0 < nbk ? min(L::EC, nbk - b0) : 0u;
+      wave_lds_sync();
+      flush();
+    }
+  } else
   for (;;) {
     const bool l2 = sballot(hm != 0 || csl != 0 || ck < cn) != 0;
     const bool done = !l2 && kb >= n_keys;
@@ -1653,7 +1936,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
             const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
             if (l2_bloom_maybe(blm, h2)) {
-              if (filt_maybe(a.bfilt, a.fmask, h2))
+              if (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2))
                 e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, st[5]);
               if (STATS) { st[3]++; st[4] += e.y != 0; }
             }
@@ -1684,13 +1967,15 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
               const uint32_t hs = ch | BT_CKEY;
               const uint32_t h2 = bucket_hash2(h1, hs, v0, v1);
               if (l2_bloom_maybe(blm, h2)) {
-                if (filt_maybe(a.bfilt, a.fmask, h2))
+                if (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2))
                   e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | hs, kp, ka, kr, v0, v1, st[5]);
                 if (STATS) { st[3]++; st[4] += e.y != 0; }
               }
             }
           }
         } else {
+          // (a variant where each lane took its own next level-1 key while others probed level 2
+          // was 15 % slower: the two paths then run divergently in every step; profiles/r02/ab_mix)
           const uint32_t k = kb + sl;
           kb += SEG;
           uint32_t j = k;
@@ -1706,7 +1991,11 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
           if (k < n_keys) {
             const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
             const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
-            const uint32_t ip = j % np_, t2 = j / np_, ia = t2 % na_, ir = t2 / na_;
+            uint32_t ip = j, ia = 0, ir = 0;
+            if (na_ != 1u || (rkc == KC_ENT && nR != 1u)) {  // only the principal varies: no division
+              const uint32_t t2 = j / np_;
+              ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
+            }
             kp = key_comp(pkc, ip + 1 - (pn >> 31), c.pt, c.pi, c.blk, c.p_anc);
             ka = key_comp(akc, ia + 1 - (an >> 31), c.at, c.ai, c.blk, c.a_anc);
             kr = key_comp(rkc, ir + 1 - (rn >> 31), c.rt, c.ri, c.blk, c.r_anc);
@@ -1726,134 +2015,14 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint64_t m = sballot(e.y != 0);
       if (e.y) {
         const uint32_t pos = ne + mbcnt64(m);
-        wl.efirst[seg][pos] = e.x;
-        wl.epre[seg][pos] = e.y;
-        wl.ecombo[seg][pos] = combo;
+        wl.u.b.efirst[seg][pos] = e.x;
+        wl.u.b.epre[seg][pos] = e.y;
+        wl.u.b.ecombo[seg][pos] = combo;
       }
       ne += popc64(m);
       wave_lds_sync();
     }
-    if (all_done || __ballot(ne + SEG > L::EC)) {
-      const uint64_t t_c0 = STATS ? clock64() : 0;
-      // ---- run every segment's staged buckets ----
-      uint32_t carry = 0;
-      for (uint32_t b0 = 0; __ballot(b0 < ne); b0 += SEG) {
-        const uint32_t b = b0 + sl;
-        const uint32_t cnt = b < ne ? wl.epre[seg][b] : 0u;
-        const uint32_t inc = sscan(cnt);
-        wave_lds_sync();
-        if (b < ne) wl.epre[seg][b] = carry + inc - cnt;
-        carry += sbcast(inc, SEG - 1);
-        wave_lds_sync();
-      }
-      const uint32_t total = carry;
-      for (uint32_t base = 0; __ballot(base < total); base += SEG) {
-        const uint32_t idx = base + sl;
-        bool ok = idx < total;
-        uint32_t lo = 0, hi = ne;  // bucket of candidate idx: last b with epre[b] <= idx
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (wl.epre[seg][mid] <= idx) lo = mid;
-          else hi = mid;
-        }
-        const uint32_t hidx = ok ? wl.efirst[seg][lo] + (idx - wl.epre[seg][lo]) : 0u;
-        const uint32_t bcombo = ok ? wl.ecombo[seg][lo] : 0u;
-        const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
-        const uint4* d4 = reinterpret_cast<const uint4*>(head);
-        const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
-        const uint32_t flags = q0.x, kinds = q0.y;
-        const uint32_t tier = (flags >> 8) & 0xFF;
-        ok = ok && tier <= min_tier;
-        const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
-        // scope re-check; an `in` / `is in` entity matched by the bucket key's entity component
-        // holds already (the request enumerated that key from its ancestor-or-self list)
-        if (ak != SK_ANY) {
-          if (a.amask_ok) {
-            const uint64_t pm = ((uint64_t)q3.w << 32) | q3.z;
-            ok = ok && (((ak == SK_EQ ? as : am) & pm) != 0);
-          } else if (ak == SK_EQ) {
-            ok = ok && c.at == q1.y && c.ai == q1.z;
-          } else if (ak == SK_IN) {
-            ok = ok && anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, q1.y, q1.z);
-          } else if (((bcombo >> 2) & 1) != KC_ENT) {
-            bool any = false;
-            for (uint32_t x = 0; ok && x < q1.y && !any; x++)
-              any = anc_in(c.blk, c.a_anc, c.a_nanc, c.at, c.ai, a.cpool[q1.z + 2 * x], a.cpool[q1.z + 2 * x + 1]);
-            ok = ok && any;
-          }
-        }
-        if (pk == SK_IS || pk == SK_ISIN) ok = ok && c.pt == q0.z;
-        if (pk == SK_EQ) ok = ok && c.pt == q0.w && c.pi == q1.x;
-        else if ((pk == SK_IN || pk == SK_ISIN) && (bcombo & 3) != KC_ENT)
-          ok = ok && anc_in(c.blk, c.p_anc, c.p_nanc, c.pt, c.pi, q0.w, q1.x);
-        if (rk == SK_IS || rk == SK_ISIN) ok = ok && c.rt == q1.w;
-        if (rk == SK_EQ) ok = ok && c.rt == q2.x && c.ri == q2.y;
-        else if ((rk == SK_IN || rk == SK_ISIN) && (bcombo >> 3) != KC_ENT)
-          ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
-        // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
-        // atom data in the policy's full record at PW_EXT)
-        const uint32_t na = q3.x / ATOM_WORDS;
-        const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
-        uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
-        if (STATS) { st[6] += idx < total; st[7] += ok; st[11] += sl == 0; }
-        bool err = false;
-        Err e{0, 0, 0, 0, 0};
-        while (__ballot(pc < na)) {
-          if (pc < na) {
-            const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
-            const uint32_t rr = eval_atom<false>(c, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
-            if (STATS) st[8]++;
-            if (rr == 3u) { general = true; pc = AT_UNSAT; }
-            else if (rr == 2u) { err = true; pc = AT_UNSAT; }
-            else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
-          }
-        }
-        // record hits (segment-local slots): a duplicate class (head word PW_CODE_N, image.h) hits
-        // for every member, all sharing the head's error detail
-        const bool hit = ok && (err || pc == AT_SAT);
-        const uint32_t mlist = q2.w;
-        const uint32_t nmem = hit ? (mlist ? a.bstream[mlist] : 1u) : 0u;
-        if (STATS) st[9] += nmem;
-        const uint32_t mincl = sscan(nmem);
-        const uint64_t xmask = sballot(hit && err);
-        const uint32_t xpos = nx + mbcnt64(xmask);
-        const uint32_t hmv = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8) | (min(xpos, 0xFFu) << 16);
-        const uint32_t pos0 = nh + mincl - nmem;
-        if (hit && !mlist && pos0 < L::HC) {
-          wl.hp[seg][pos0] = q2.z;  // PW_CODE: global policy index
-          wl.hm[seg][pos0] = hmv;
-        }
-        // class members: the segment copies each hitting class's list together (coalesced)
-        for (uint64_t cls = sballot(hit && mlist != 0); __ballot(cls != 0);) {
-          const bool act = cls != 0;  // this segment still has a class to copy
-          const uint32_t src = act ? (uint32_t)__builtin_ctzll(cls) : lane;
-          cls &= act ? cls - 1 : 0ull;
-          const uint32_t p0 = (uint32_t)__shfl((int)pos0, (int)src), nm = (uint32_t)__shfl((int)nmem, (int)src);
-          const uint32_t mls = (uint32_t)__shfl((int)mlist, (int)src), hv = (uint32_t)__shfl((int)hmv, (int)src);
-          const uint32_t ml = act ? mls : 0u;
-          if (ml)
-            for (uint32_t j = sl; j < nm && p0 + j < L::HC; j += SEG) {
-              wl.hp[seg][p0 + j] = a.bstream[ml + 1 + j];
-              wl.hm[seg][p0 + j] = hv;
-            }
-        }
-        if (hit) {
-          if (err && xpos < L::XC) {
-            wl.he[seg][4 * xpos] = e.code | (e.aux << 8);
-            wl.he[seg][4 * xpos + 1] = e.k;
-            wl.he[seg][4 * xpos + 2] = e.et;
-            wl.he[seg][4 * xpos + 3] = e.ei;
-          }
-        }
-        nh += sbcast(mincl, SEG - 1);
-        nx += popc64(xmask);
-        min_tier = min(min_tier, smin(hit ? tier : 0xFFu));
-      }
-      ne = 0;
-      if (STATS && sl == 0) st[10]++;
-      wave_lds_sync();
-      if (STATS) t_cand += clock64() - t_c0;
-    }
+    if (all_done || __ballot(ne + SEG > L::EC)) flush();
     if (all_done) break;
   }
   const uint64_t t_loop = STATS ? clock64() : 0;
@@ -1873,7 +2042,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   while (mloc < nhm) mloc <<= 1;
   uint32_t m = mloc;
   for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
-  for (uint32_t i = sl; i < m; i += SEG) wl.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
+  for (uint32_t i = sl; i < m; i += SEG) wl.u.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
   wave_lds_sync();
   for (uint32_t k = 2; k <= m; k <<= 1) {
     for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
@@ -1881,9 +2050,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         const uint32_t q = i0 + sl;  // compare-exchange pair q
         if (q < (m >> 1)) {
           const uint32_t lo = ((q / jj) * 2 * jj) + (q % jj), hi = lo + jj;
-          const uint32_t x = wl.hs[seg][lo], y = wl.hs[seg][hi];
+          const uint32_t x = wl.u.hs[seg][lo], y = wl.u.hs[seg][hi];
           const bool up = (lo & k) == 0;
-          if ((x > y) == up) { wl.hs[seg][lo] = y; wl.hs[seg][hi] = x; }
+          if ((x > y) == up) { wl.u.hs[seg][lo] = y; wl.u.hs[seg][hi] = x; }
         }
       }
       wave_lds_sync();
@@ -1894,10 +2063,10 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   // a first sweep learns whether any forbid decides.
   auto deciding = [&](uint32_t i, uint32_t& pj, uint32_t& mj) {
     const bool have = i < nhm;
-    const uint32_t key = have ? wl.hs[seg][i] : 0xFFFFFFFFu;
+    const uint32_t key = have ? wl.u.hs[seg][i] : 0xFFFFFFFFu;
     pj = key >> 12;
     mj = have ? wl.hm[seg][key & 0xFFF] : 0u;
-    return have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.hs[seg][i - 1] >> 12) != pj);
+    return have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.u.hs[seg][i - 1] >> 12) != pj);
   };
   bool deny = false;
   for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
@@ -2147,6 +2316,8 @@ void dev_pool_destroy(DevPool* p) {
   delete p;
 }
 
+static bool split_on();
+
 // One pinned staging block and one device block for the inputs (256-B aligned sections), one for
 // the results; a batch costs two copies and a memset, and no allocation once the pool is warm.
 int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, DevPool* pool) {
@@ -2213,16 +2384,29 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     if ((rc = pool_get(pool, false, lane_bytes, &d.lane_blk, &d.lane_cls))) return rc;
     d.lane = (uint32_t*)d.lane_blk;
   }
-  if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) { pool_put(pool, false, d.lane_blk, d.lane_cls); return rc; }
+  if (b.img->indexed && split_on() && b.n()) {  // the index scan's bucket lists
+    if ((rc = pool_get(pool, false, (size_t)b.n() * (1 + 2 * SCAN_CAP) * 4, &d.scan_blk, &d.scan_cls))) {
+      pool_put(pool, false, d.lane_blk, d.lane_cls);
+      return rc;
+    }
+    d.scan = (uint32_t*)d.scan_blk;
+  }
+  if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) {
+    pool_put(pool, false, d.lane_blk, d.lane_cls);
+    pool_put(pool, false, d.scan_blk, d.scan_cls);
+    return rc;
+  }
   if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) {
     pool_put(pool, false, d.in_blk, d.in_cls);
     pool_put(pool, false, d.lane_blk, d.lane_cls);
+    pool_put(pool, false, d.scan_blk, d.scan_cls);
     return rc;
   }
   if ((rc = pool_get(pool, true, std::max(in_bytes, d.out_bytes), &d.stage, &d.stage_cls))) {
     pool_put(pool, false, d.in_blk, d.in_cls);
     pool_put(pool, false, d.out_blk, d.out_cls);
     pool_put(pool, false, d.lane_blk, d.lane_cls);
+    pool_put(pool, false, d.scan_blk, d.scan_cls);
     return rc;
   }
   uint8_t* st = (uint8_t*)d.stage;
@@ -2297,6 +2481,7 @@ void dev_batch_free(DevBatch* d) {
     pool_put(d->pool, false, d->out_blk, d->out_cls);
     pool_put(d->pool, true, d->stage, d->stage_cls);
     pool_put(d->pool, false, d->lane_blk, d->lane_cls);
+    pool_put(d->pool, false, d->scan_blk, d->scan_cls);
   }
   if (d->req_idx) (void)hipFree(d->req_idx);
   *d = DevBatch();
@@ -2373,8 +2558,13 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.hlists = img.cslot_mask ? 1u : 0u;
   static const uint32_t l1filt = [] { const char* e = std::getenv("CEDARGPU_L1_FILTER"); return (e && *e == '0') ? 0u : 1u; }();
   k.l1filt = l1filt;
+  // off by default: the level-1 entry's bloom already passes only likely keys (+2 %, profiles/r02/ab_mix)
+  static const uint32_t l2filt = [] { const char* e = std::getenv("CEDARGPU_L2_FILTER"); return (e && *e == '1') ? 1u : 0u; }();
+  k.l2filt = l2filt;
   k.stats = nullptr;
   k.n_dev = nullptr;
+  k.scan = nullptr;
+  k.scan_n = 0;
   return k;
 }
 
@@ -2384,6 +2574,10 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
 // group-DAG workload 2.94e8 decisions/s against 2.21e8 with 16 lanes: a request's ~60 level-1
 // probes are dependent-latency chains, and more requests in flight per wave hide them;
 // profiles/r02/ab_seg8); CEDARGPU_PROBE_SEG=16 / 32 / 64 for comparisons.
+static bool split_on() {
+  static const bool on = !(std::getenv("CEDARGPU_SPLIT") && *std::getenv("CEDARGPU_SPLIT") == '0');
+  return on;
+}
 static uint32_t probe_seg() {
   static const uint32_t seg = [] {
     const char* e = std::getenv("CEDARGPU_PROBE_SEG");
@@ -2428,7 +2622,22 @@ static uint32_t probe_wpb() {
   return w;
 }
 
+// The first pass of an indexed image runs split (cedar_scan_kernel, then the probe kernel's SPLIT
+// variant over the buckets it found); CEDARGPU_SPLIT=0 runs the fused probe kernel instead.
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
+  if (!big && k.scan && !probe_stats() && probe_seg() == 8 && probe_occ() == 3) {
+    // register targets: the scan at 8 waves per SIMD (64 VGPRs), the candidate pass at 4 (128)
+    // measured 3.62e8 decisions/s on C3 against 3.42e8 unconstrained (profiles/r02/ab_split2)
+    static const uint32_t socc = [] { const char* e = std::getenv("CEDARGPU_SCAN_OCC"); return e ? (uint32_t)std::atoi(e) : 8u; }();
+    static const uint32_t cocc = [] { const char* e = std::getenv("CEDARGPU_CAND_OCC"); return e ? (uint32_t)std::atoi(e) : 4u; }();
+    const dim3 sg((n + 7) / 8), sb(64);
+    if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8>), sg, sb, 0, s, k);
+    else if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6>), sg, sb, 0, s, k);
+    else hipLaunchKernelGGL((cedar_scan_kernel<8>), sg, sb, 0, s, k);
+    if (cocc == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
+    else hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
+    return;
+  }
   const uint32_t seg = big ? 64u : probe_seg();
   const bool w1 = (seg == 16 && (probe_occ() == 4 || probe_occ() == 5)) || (seg == 8 && (probe_occ() == 3 || probe_occ() == 4));
   const uint32_t wpb = (!big && w1 && !probe_stats()) ? probe_wpb() : WAVES;
@@ -2502,6 +2711,8 @@ static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStre
 // dev_time_eval times it.
 static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
+  k.scan = b.scan;
+  k.scan_n = b.n;
   launch_eval(img, k, b.n, s);
   HIPCHK(hipGetLastError(), "launch");
   if (!b.fu_cnt) return 0;

@@ -58,6 +58,10 @@ struct DevBatch {
     uint32_t *ids = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
     uint32_t cap = 0, capr = 0, cape = 0;
   } fu[3];
+  // split first pass: the index scan's bucket lists (cedar_eval.hip SCAN_*), device only
+  uint32_t* scan = nullptr;
+  void* scan_blk = nullptr;
+  size_t scan_cls = 0;
   uint32_t* lane = nullptr;  // per-request lane scratch (images with lane_need > LANE_WORDS)
   void* lane_blk = nullptr;
   size_t lane_cls = 0;
