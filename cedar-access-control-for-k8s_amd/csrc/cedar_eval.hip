@@ -1902,12 +1902,16 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   // set-membership slots of the entry still to probe (image.h BT_CKEY), the current one's element
   // hash list in the request block and the next element
   uint32_t csl = 0, ch = 0, cl = 0, ck = 0, cn = 0;
+  bool probe_loop = !SPLIT;
   if constexpr (SPLIT) {
-    // the scan kernel found this request's buckets (cedar_scan_kernel): stage them EC at a time
-    const uint32_t nb = valid ? a.scan[gid] : 0u;
+    // the scan kernel found this request's buckets (cedar_scan_kernel): stage them EC at a time.
+    // More buckets than the scan holds: the one-request-per-wave variant probes the index itself,
+    // narrower segments hand the request to that variant (the large-stage follow-up).
+    const uint32_t nb = valid ? a.scan[r] : 0u;
+    if (SEG == 64 && nb == SCAN_OVF) probe_loop = true;
     const uint32_t nbk = nb == SCAN_OVF ? 0u : nb;
-    if (nb == SCAN_OVF) nh = L::HC + 1;  // more buckets than the scan holds: the large-stage follow-up
-    const uint32_t* pairs = a.scan + a.scan_n + (size_t)gid * (2 * SCAN_CAP);
+    if (SEG < 64 && nb == SCAN_OVF) nh = L::HC + 1;
+    const uint32_t* pairs = a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP);
     for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
       for (uint32_t i = sl; i < L::EC; i += SEG)
         if (b0 + i < nbk) {
@@ -1920,7 +1924,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       wave_lds_sync();
       flush();
     }
-  } else
+  }
+  if (probe_loop)
   for (;;) {
     const bool l2 = sballot(hm != 0 || csl != 0 || ck < cn) != 0;
     const bool done = !l2 && kb >= n_keys;
@@ -2625,13 +2630,20 @@ static uint32_t probe_wpb() {
 // The first pass of an indexed image runs split (cedar_scan_kernel, then the probe kernel's SPLIT
 // variant over the buckets it found); CEDARGPU_SPLIT=0 runs the fused probe kernel instead.
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
+  if (big && k.scan) {  // the large stage over the scan's buckets (probing only past SCAN_CAP)
+    static const uint32_t bw = [] { const char* e = std::getenv("CEDARGPU_BIG_WPB"); return e ? (uint32_t)std::atoi(e) : 4u; }();
+    if (bw == 1) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, 1, false, 1, true>), dim3(n), dim3(64), 0, s, k);
+    else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, 1, false, WAVES, true>), dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
+    return;
+  }
   if (!big && k.scan && !probe_stats() && probe_seg() == 8 && probe_occ() == 3) {
     // register targets: the scan at 8 waves per SIMD (64 VGPRs), the candidate pass at 4 (128)
     // measured 3.62e8 decisions/s on C3 against 3.42e8 unconstrained (profiles/r02/ab_split2)
     static const uint32_t socc = [] { const char* e = std::getenv("CEDARGPU_SCAN_OCC"); return e ? (uint32_t)std::atoi(e) : 8u; }();
     static const uint32_t cocc = [] { const char* e = std::getenv("CEDARGPU_CAND_OCC"); return e ? (uint32_t)std::atoi(e) : 4u; }();
     const dim3 sg((n + 7) / 8), sb(64);
-    if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8>), sg, sb, 0, s, k);
+    if (k.req_idx) {  // a follow-up over the first pass's requests: their buckets are scanned
+    } else if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8>), sg, sb, 0, s, k);
     else if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6>), sg, sb, 0, s, k);
     else hipLaunchKernelGGL((cedar_scan_kernel<8>), sg, sb, 0, s, k);
     if (cocc == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
@@ -2726,6 +2738,8 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
     if (!f.cap) continue;
     KArgs fk = make_args(img, b, f.ids, f.cap, f.res, f.rf, f.rp, f.er, f.capr, f.cape);
     fk.n_dev = b.fu_cnt + q;
+    fk.scan = b.scan;  // the probe-kernel follow-ups read the first pass's buckets
+    fk.scan_n = b.n;
     if (q == FU_GEN) launch_stream(img, fk, f.cap, s);
     else launch_probe(fk, f.cap, s, q == FU_BIG);
   }
