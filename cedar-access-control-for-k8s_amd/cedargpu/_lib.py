@@ -9,6 +9,11 @@ lib_path = os.path.join(_HERE, "libcedargpu.so")
 SANITIZER_BUILD = bool(os.environ.get("CEDARGPU_SANITIZER_LIB"))
 if SANITIZER_BUILD:
     lib_path = os.environ["CEDARGPU_SANITIZER_LIB"]
+# A/B studies only (tools/ab_lib.sh): another build of this library, e.g. an earlier commit's, run
+# by the same bench in the same GPU session; symbols it predates are left unbound.
+AB_BUILD = bool(os.environ.get("CEDARGPU_AB_LIB"))
+if AB_BUILD:
+    lib_path = os.environ["CEDARGPU_AB_LIB"]
 
 if not os.path.exists(lib_path):
     raise ImportError(f"cedargpu: native library not built ({lib_path}); run `make -C cedar-access-control-for-k8s_amd/csrc`"
@@ -127,6 +132,8 @@ _SIGS = {
 }
 
 for _name, (_res, _args) in _SIGS.items():
+    if AB_BUILD and not hasattr(lib, _name):
+        continue
     _f = getattr(lib, _name)  # AttributeError here = the library does not export a declared symbol
     _f.restype = _res
     _f.argtypes = _args

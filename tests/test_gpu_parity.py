@@ -496,6 +496,45 @@ def test_probe_kernel_abac_deep_group_dag(ctx):
     check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
 
 
+def test_static_dag_handmade(ctx):
+    """A small static group DAG: principals in several groups with overlapping ancestor sets, a
+    static group the request re-parents (its request parent joins the merged ancestry), a direct
+    group outside the static set, `==` on a group, group-scoped keys at every DAG level,
+    wildcard-action keys and level-2 keys (namespace, resource, name prefix)."""
+    G = lambda g: {"type": "k8s::Group", "id": g}
+    ents = [{"uid": G(g), "attrs": {"name": g}, "parents": [G(p) for p in ps]} for g, ps in [
+        ("root1", []), ("root2", []), ("mid1", ["root1"]), ("mid2", ["root1", "root2"]), ("mid3", ["root2"]),
+        ("leafA", ["mid1", "mid2"]), ("leafB", ["mid2", "mid3"]), ("leafC", ["mid3"]), ("leafD", ["leafA"])]]
+    pols = []
+    for i, g in enumerate(["root1", "root2", "mid1", "mid2", "mid3", "leafA", "leafB", "leafC", "leafD"]):
+        pols.append(f'permit (principal in k8s::Group::"{g}", action == k8s::Action::"get", resource is k8s::Resource) '
+                    f'when {{ resource.namespace == "ns{i % 3}" }};')
+        pols.append(f'permit (principal in k8s::Group::"{g}", action, resource is k8s::Resource) '
+                    f'when {{ resource.resource == "pods" }};')
+        pols.append(f'forbid (principal in k8s::Group::"{g}", action in [k8s::Action::"delete"], resource is k8s::Resource) '
+                    f'when {{ resource has name && resource.name like "prod-{i}*" }};')
+    pols.append('permit (principal == k8s::Group::"mid2", action, resource);')
+    pols.append('permit (principal in k8s::Group::"extra", action == k8s::Action::"list", resource);')
+    stores = [cedargpu.MemoryStore("h.cedar", "\n".join(pols))]
+    items = []
+    combos = [["leafA", "leafB"], ["leafD", "leafC"], ["leafA", "leafD"], ["mid2", "leafC", "extra"], ["leafB"],
+              ["root1", "leafC"], ["extra"], ["leafA", "leafB", "leafC", "leafD", "extra"]]
+    k = 0
+    for groups in combos:
+        for verb in ("get", "list", "delete", "patch"):
+            for ns, res, name in (("ns0", "pods", "prod-5x"), ("ns1", "secrets", ""), ("ns2", "pods", "prod-0a")):
+                a = km.Attributes(user=km.UserInfo(name=f"u{k}", uid=f"id{k}", groups=groups), verb=verb,
+                                  namespace=ns, api_group="", api_version="v1", resource=res, name=name,
+                                  resource_request=True)
+                em, r = km.record_to_cedar_resource(a)
+                ej = co.entities_to_json(em)
+                if k % 5 == 0:  # a request-provided static group with a parent of its own
+                    ej = ej + [{"uid": G("leafA"), "attrs": {"name": "leafA"}, "parents": [G("extra")]}]
+                items.append((ej, co.request_to_json(r)))
+                k += 1
+    check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_static_entities_random_general(ctx, seed):
     """Random general policies (policy-stream kernel, bytecode) with an image-level static

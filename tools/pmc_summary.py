@@ -10,7 +10,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "cedar_probe_kernel"
+KERNEL = os.environ.get("PMC_KERNEL", "cedar_probe_kernel")  # substring of the kernel name
 
 
 def load(d):
