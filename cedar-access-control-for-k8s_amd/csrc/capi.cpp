@@ -1110,6 +1110,14 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     }
   }
   tr.mark("rerun_big_general");
+  if (!idx_big.empty()) {
+    // their exact list lengths join the image's sizing hint: the worklist the large stage ran on
+    // the device may have held only some of this batch's many-hit requests
+    uint32_t mx = 0;
+    for (const uint32_t i : idx_big) mx = std::max(mx, b->host.res[2 * (size_t)i + 1] & 0xFFFFu);
+    std::lock_guard<std::mutex> g(b->ctx->mu);
+    if (b->ctx->hint.serial == b->img->serial) b->ctx->hint.big_maxr = std::max(b->ctx->hint.big_maxr, mx);
+  }
   b->done = true;
   return CG_OK;
 }

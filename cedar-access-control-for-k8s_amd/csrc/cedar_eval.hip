@@ -2355,7 +2355,9 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   const uint32_t fu_default = std::min<uint32_t>(64u, std::max<uint32_t>(4u, b.n() / 32u));
   const uint32_t capr_k[FU_KINDS] = {b.fu_capr_hint ? std::min<uint32_t>(1024u, std::max<uint32_t>(64u, b.fu_capr_hint)) : 256u,
                                      64u, std::min<uint32_t>(4096u, std::max<uint32_t>(64u, b.fu_capr_gen_hint))};
-  const size_t budget_k[FU_KINDS] = {std::min<size_t>(128u << 20, std::max<size_t>(16u << 20, (size_t)b.n() * 2048)),
+  // (FU_BIG: up to 256 MB, room for C3's 1M-request batches: ~43k many-hit requests of up to ~700
+  // reasons each)
+  const size_t budget_k[FU_KINDS] = {std::min<size_t>(256u << 20, std::max<size_t>(16u << 20, (size_t)b.n() * 2048)),
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024)),
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024))};
   size_t o_fu = o_er + al(n * d.cape * ERR_WORDS * 4);

@@ -1208,8 +1208,10 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   };
   mark("ext area");
   const size_t n_entries = g1.size() + g2.size();
+  // slots: the power of two >= 2x the entries (CEDARGPU_BTAB_SLACK=k: >= k/4 x, A/B studies)
+  static const size_t slack = [] { const char* e = std::getenv("CEDARGPU_BTAB_SLACK"); return e ? (size_t)std::max(4, std::atoi(e)) : 8u; }();
   uint32_t size = 16;
-  while (size < 2 * n_entries) size <<= 1;
+  while (size * 4 < slack * n_entries) size <<= 1;
   img.btab.assign((size_t)size * BT_WORDS, 0);
   auto insert = [&](uint32_t hash, const uint32_t* e) {
     uint32_t h = hash & (size - 1);
