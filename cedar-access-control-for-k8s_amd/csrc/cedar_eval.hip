@@ -76,8 +76,9 @@ struct KArgs {
   const uint32_t* n_dev;                 // follow-up pass: request count on the device (null: n_req)
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
   uint32_t hlists;  // rows carry element-hash lists (image.h "set-membership keys")
-  uint32_t l1filt;  // level-1 probes consult the key filter first (CEDARGPU_L1_FILTER=0: off, A/B)
+  uint32_t l1filt;  // level-1 probes consult the key filter first (CEDARGPU_L1_FILTER=1: on, A/B)
   uint32_t l2filt;  // level-2 probes too, after the level-1 entry's own bloom (CEDARGPU_L2_FILTER)
+  uint32_t slot_split;  // probes load a slot's first 16 B, the rest only on a key match (CEDARGPU_SLOT_SPLIT)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
   // count at scan[i] (SCAN_OVF: more than SCAN_CAP), its (first head, count | combo) pairs at
@@ -1518,11 +1519,25 @@ __device__ __forceinline__ bool filt_maybe(const uint32_t* bfilt, uint32_t fmask
 template <bool ST = false>
 __device__ __forceinline__ uint3 probe(const uint32_t* btab, uint32_t bmask, uint32_t hash, uint32_t w0, uint2 p, uint2 q,
                                        uint2 r, uint32_t v0, uint32_t v1, uint32_t& steps, uint4* bloom = nullptr,
-                                       uint32_t* cmask = nullptr) {
+                                       uint32_t* cmask = nullptr, uint32_t split = 0) {
   uint32_t h = hash & bmask;
   for (;;) {
     if (ST) steps++;
     const uint4* sl = reinterpret_cast<const uint4*>(btab + (size_t)h * BT_WORDS);
+    if (split) {  // an empty or foreign slot costs one 16-byte load
+      const uint4 x = sl[0];
+      if (x.x == 0) return make_uint3(0, 0, 0);
+      if (x.x == w0 && x.y == p.x && x.z == p.y && x.w == q.x) {
+        const uint4 y = sl[1], z = sl[2];
+        if (y.x == q.y && y.y == r.x && y.z == r.y && (!(w0 & BT_L2) || (y.w == v0 && z.x == v1))) {
+          if (bloom) *bloom = sl[3];
+          if (cmask) *cmask = y.w;
+          return make_uint3(z.y, z.z, z.w);
+        }
+      }
+      h = (h + 1) & bmask;
+      continue;
+    }
     // the whole 64-byte slot in one round trip, compared once every word arrives (7 % faster on
     // C3 than loading the key's first words and the rest on a match: profiles/r02/ab_whole_slot)
     const uint4 x = sl[0], y = sl[1], z = sl[2];
@@ -1601,7 +1616,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
           const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
           if (l2_bloom_maybe(blm, h2) && (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2)))
-            e = probe(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, unused);
+            e = probe(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, unused, nullptr, nullptr, a.slot_split);
         } else if (csl || ck < cn) {
           uint32_t v0 = 0, v1 = 0;
           bool go = false;
@@ -1629,7 +1644,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
             const uint32_t hs = ch | BT_CKEY;
             const uint32_t h2 = bucket_hash2(h1, hs, v0, v1);
             if (l2_bloom_maybe(blm, h2) && (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2)))
-              e = probe(a.btab, a.bmask, h2, w0 | BT_L2 | hs, kp, ka, kr, v0, v1, unused);
+              e = probe(a.btab, a.bmask, h2, w0 | BT_L2 | hs, kp, ka, kr, v0, v1, unused, nullptr, nullptr, a.slot_split);
           }
         }
       } else {
@@ -1660,7 +1675,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
           uint32_t cmv = 0;
           if (!a.l1filt || filt_maybe(a.bfilt, a.fmask, h1))
-            e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, &blm, &cmv);
+            e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, &blm, &cmv, a.slot_split);
           hm = e.z;
           csl = cmv;
         }
@@ -1942,7 +1957,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
             if (l2_bloom_maybe(blm, h2)) {
               if (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2))
-                e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, st[5]);
+                e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | h, kp, ka, kr, v0, v1, st[5], nullptr, nullptr, a.slot_split);
               if (STATS) { st[3]++; st[4] += e.y != 0; }
             }
           } else if (csl || ck < cn) {
@@ -1973,7 +1988,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
               const uint32_t h2 = bucket_hash2(h1, hs, v0, v1);
               if (l2_bloom_maybe(blm, h2)) {
                 if (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2))
-                  e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | hs, kp, ka, kr, v0, v1, st[5]);
+                  e = probe<STATS>(a.btab, a.bmask, h2, w0 | BT_L2 | hs, kp, ka, kr, v0, v1, st[5], nullptr, nullptr, a.slot_split);
                 if (STATS) { st[3]++; st[4] += e.y != 0; }
               }
             }
@@ -2008,7 +2023,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
             uint32_t cmv = 0;
             if (!a.l1filt || filt_maybe(a.bfilt, a.fmask, h1))
-              e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5], &blm, &cmv);
+              e = probe<STATS>(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, st[5], &blm, &cmv, a.slot_split);
             hm = e.z;
             csl = cmv;
             if (STATS) st[1]++;
@@ -2563,11 +2578,15 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
   k.lane = b.lane; k.lane_stride = img.lane_need;
   k.hlists = img.cslot_mask ? 1u : 0u;
-  static const uint32_t l1filt = [] { const char* e = std::getenv("CEDARGPU_L1_FILTER"); return (e && *e == '0') ? 0u : 1u; }();
+  // off by default: the scope table is sized for ~1.06-slot chains, where a miss costs one slot load
+  // and the filter only adds a round trip in front of every hit (profiles/r02/ab_slack)
+  static const uint32_t l1filt = [] { const char* e = std::getenv("CEDARGPU_L1_FILTER"); return (e && *e == '1') ? 1u : 0u; }();
   k.l1filt = l1filt;
   // off by default: the level-1 entry's bloom already passes only likely keys (+2 %, profiles/r02/ab_mix)
   static const uint32_t l2filt = [] { const char* e = std::getenv("CEDARGPU_L2_FILTER"); return (e && *e == '1') ? 1u : 0u; }();
   k.l2filt = l2filt;
+  static const uint32_t slot_split = [] { const char* e = std::getenv("CEDARGPU_SLOT_SPLIT"); return (e && *e == '1') ? 1u : 0u; }();
+  k.slot_split = slot_split;
   k.stats = nullptr;
   k.n_dev = nullptr;
   k.scan = nullptr;
