@@ -1447,8 +1447,9 @@ struct SegLds {
   static constexpr uint32_t NS = 64 / SEG;     // requests per wave
   static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : 32;  // staged buckets per request (>= 2 stages)
   static constexpr uint32_t HC = HCAP;         // hits per request (more: RF_BIG / RF_GENERAL re-run)
-  // error details per request (more: the on-device follow-up, which holds 64)
-  static constexpr uint32_t XC = HCAP >= 256 ? 64 : 8;
+  // error details per request (more: the on-device follow-up, which holds 32; more still: the
+  // stream kernel). 32 keeps the large stage's 4-wave block under 53 KB: 3 blocks per CU
+  static constexpr uint32_t XC = HCAP >= 256 ? 32 : 8;
   // the staged buckets live until the key loop ends, the merge's sort keys only after it: one region
   union {
     struct {
@@ -2650,11 +2651,14 @@ static uint32_t probe_wpb() {
 
 // The first pass of an indexed image runs split (cedar_scan_kernel, then the probe kernel's SPLIT
 // variant over the buckets it found); CEDARGPU_SPLIT=0 runs the fused probe kernel instead.
+// the large stage's register target: 3 waves per SIMD (168 VGPRs), which its LDS (3 four-wave
+// blocks per CU) also allows
+constexpr uint32_t BIG_MINW = 3;
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
   if (big && k.scan) {  // the large stage over the scan's buckets (probing only past SCAN_CAP)
     static const uint32_t bw = [] { const char* e = std::getenv("CEDARGPU_BIG_WPB"); return e ? (uint32_t)std::atoi(e) : 4u; }();
-    if (bw == 1) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, 1, false, 1, true>), dim3(n), dim3(64), 0, s, k);
-    else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, 1, false, WAVES, true>), dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
+    if (bw == 1) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, 1, true>), dim3(n), dim3(64), 0, s, k);
+    else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, WAVES, true>), dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
     return;
   }
   if (!big && k.scan && !probe_stats() && probe_seg() == 8 && probe_occ() == 3) {
