@@ -79,6 +79,7 @@ struct KArgs {
   uint32_t l1filt;  // level-1 probes consult the key filter first (CEDARGPU_L1_FILTER=1: on, A/B)
   uint32_t l2filt;  // level-2 probes too, after the level-1 entry's own bloom (CEDARGPU_L2_FILTER)
   uint32_t slot_split;  // probes load a slot's first 16 B, the rest only on a key match (CEDARGPU_SLOT_SPLIT)
+  uint32_t scan_lds;    // the scan stages key ancestors and hot values in LDS up front (CEDARGPU_SCAN_LDS)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
   // count at scan[i] (SCAN_OVF: more than SCAN_CAP), its (first head, count | combo) pairs at
@@ -1572,8 +1573,15 @@ __device__ __forceinline__ bool l2_bloom_maybe(uint4 b, uint32_t h2) {
 // segment alternating the two; found buckets that hold candidate heads go straight to a.scan. No
 // LDS and no candidate evaluation: far fewer registers than the probe kernel, so more requests are
 // in flight per CU; the probe kernel's SPLIT variant then evaluates the buckets' heads.
+// principal key ancestors the scan stages in LDS per request (more: read from the request block)
+constexpr uint32_t SCAN_ANC = 40;
 template <uint32_t SEG, uint32_t MINW = 1>
 __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
+  // per request: its first SCAN_ANC key ancestors and its hot values, loaded in one round trip
+  // before the key loop (the request block and row are cold: each key step would otherwise start
+  // with a dependent HBM load)
+  __shared__ uint2 s_anc[64 / SEG][SCAN_ANC];
+  __shared__ uint2 s_hot[64 / SEG][NHOT];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
@@ -1599,6 +1607,15 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
     }
   uint32_t* pairs = a.scan + a.scan_n + (size_t)gid * (2 * SCAN_CAP);
+  const bool stl = a.scan_lds != 0;
+  if (stl) {
+    const uint32_t n_st = valid ? min((pn >> AN_KEYS_SHIFT) & AN_KEYS, SCAN_ANC) : 0u;
+    for (uint32_t j = sl; j < n_st; j += SEG)
+      s_anc[seg][j] = make_uint2(__builtin_nontemporal_load(blk + p_anc + 2 * j), __builtin_nontemporal_load(blk + p_anc + 2 * j + 1));
+    for (uint32_t h = sl; h < a.n_hot; h += SEG)
+      s_hot[seg][h] = valid ? *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h) : make_uint2(0u, 0u);
+    wave_lds_sync();
+  }
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);
@@ -1613,7 +1630,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         if (hm) {
           const uint32_t h = __builtin_ctz(hm);
           hm &= hm - 1;
-          const uint2 v = *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h);
+          const uint2 v = stl ? s_hot[seg][h] : *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h);
           const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
           const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
           if (l2_bloom_maybe(blm, h2) && (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2)))
@@ -1669,7 +1686,8 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
             const uint32_t t2 = j / np_;
             ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
           }
-          kp = key_comp(pkc, ip + 1 - (pn >> 31), pt, pi, blk, p_anc);
+          const uint32_t jp = ip + 1 - (pn >> 31);  // 0: the principal itself, j: ancestor j - 1
+          kp = (stl && pkc == KC_ENT && jp && jp <= SCAN_ANC) ? s_anc[seg][jp - 1] : key_comp(pkc, jp, pt, pi, blk, p_anc);
           ka = key_comp(akc, ia + 1 - (an >> 31), at, ai, blk, a_anc);
           kr = key_comp(rkc, ir + 1 - (rn >> 31), rt, ri, blk, r_anc);
           w0 = BT_USED | (combo << 16);
@@ -2588,6 +2606,8 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.l2filt = l2filt;
   static const uint32_t slot_split = [] { const char* e = std::getenv("CEDARGPU_SLOT_SPLIT"); return (e && *e == '1') ? 1u : 0u; }();
   k.slot_split = slot_split;
+  static const uint32_t scan_lds = [] { const char* e = std::getenv("CEDARGPU_SCAN_LDS"); return (e && *e == '0') ? 0u : 1u; }();
+  k.scan_lds = scan_lds;
   k.stats = nullptr;
   k.n_dev = nullptr;
   k.scan = nullptr;
