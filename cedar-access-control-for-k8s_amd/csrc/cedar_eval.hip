@@ -2682,9 +2682,12 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     return;
   }
   if (!big && k.scan && !probe_stats() && probe_seg() == 8 && probe_occ() == 3) {
-    // register targets: the scan at 8 waves per SIMD (64 VGPRs), the candidate pass at 4 (128)
-    // measured 3.62e8 decisions/s on C3 against 3.42e8 unconstrained (profiles/r02/ab_split2)
-    static const uint32_t socc = [] { const char* e = std::getenv("CEDARGPU_SCAN_OCC"); return e ? (uint32_t)std::atoi(e) : 8u; }();
+    // register targets: the candidate pass at 4 waves per SIMD (128 VGPRs; split at 8 + 4 measured
+    // 3.62e8 decisions/s on C3 against 3.42e8 unconstrained, profiles/r02/ab_split2); the scan at
+    // 6 (80 VGPRs): as fast as at 8 with its LDS staging (4.61e8 vs 4.62e8, profiles/r02/ab_scan_lds)
+    // and no register spills, whose scratch writes were 0.5 GB of the step's 2.2 GB L2-miss
+    // traffic at 8 (profiles/r02/pmc_s3e)
+    static const uint32_t socc = [] { const char* e = std::getenv("CEDARGPU_SCAN_OCC"); return e ? (uint32_t)std::atoi(e) : 6u; }();
     static const uint32_t cocc = [] { const char* e = std::getenv("CEDARGPU_CAND_OCC"); return e ? (uint32_t)std::atoi(e) : 4u; }();
     const dim3 sg((n + 7) / 8), sb(64);
     if (k.req_idx) {  // a follow-up over the first pass's requests: their buckets are scanned
