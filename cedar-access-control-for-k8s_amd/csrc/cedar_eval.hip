@@ -80,6 +80,7 @@ struct KArgs {
   uint32_t l2filt;  // level-2 probes too, after the level-1 entry's own bloom (CEDARGPU_L2_FILTER)
   uint32_t slot_split;  // probes load a slot's first 16 B, the rest only on a key match (CEDARGPU_SLOT_SPLIT)
   uint32_t scan_lds;    // the scan stages key ancestors and hot values in LDS up front (CEDARGPU_SCAN_LDS)
+  uint32_t scan_big;    // more scanned buckets than this: straight to the large stage (CEDARGPU_SCAN_BIG)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
   // count at scan[i] (SCAN_OVF: more than SCAN_CAP), its (first head, count | combo) pairs at
@@ -87,7 +88,10 @@ struct KArgs {
   uint32_t* scan;
   uint32_t scan_n;
 };
-constexpr uint32_t SCAN_CAP = 24, SCAN_OVF = 0xFFFFFFFFu, SCAN_COUNT = (1u << 27) - 1, SCAN_COMBO_SHIFT = 27;
+// SCAN_CAP: bucket pairs a request's list holds (more: SCAN_OVF, the large stage probes the index
+// itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
+// the large stage, which reads the list when it holds them all
+constexpr uint32_t SCAN_CAP = 96, SCAN_OVF = 0xFFFFFFFFu, SCAN_COUNT = (1u << 27) - 1, SCAN_COMBO_SHIFT = 27;
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
 // registers; the only non-inlined function (structural equality) takes plain pointers.
@@ -1943,8 +1947,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     // narrower segments hand the request to that variant (the large-stage follow-up).
     const uint32_t nb = valid ? a.scan[r] : 0u;
     if (SEG == 64 && nb == SCAN_OVF) probe_loop = true;
-    const uint32_t nbk = nb == SCAN_OVF ? 0u : nb;
-    if (SEG < 64 && nb == SCAN_OVF) nh = L::HC + 1;
+    uint32_t nbk = nb == SCAN_OVF ? 0u : nb;
+    if (SEG < 64 && nb != SCAN_OVF && nb > a.scan_big && !a.req_idx) nbk = 0;
+    if (SEG < 64 && (nb == SCAN_OVF || (nb > a.scan_big && !a.req_idx))) nh = L::HC + 1;
     const uint32_t* pairs = a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP);
     for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
       for (uint32_t i = sl; i < L::EC; i += SEG)
@@ -2608,6 +2613,10 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.slot_split = slot_split;
   static const uint32_t scan_lds = [] { const char* e = std::getenv("CEDARGPU_SCAN_LDS"); return (e && *e == '0') ? 0u : 1u; }();
   k.scan_lds = scan_lds;
+  // 48: C3 DAG 4.91e8 decisions/s at 32..96 alike; a list of 24 that sent every longer one to the
+  // large stage measured 4.58e8 (43,485 large-stage requests instead of 25,005; profiles/r02/ab_scan_cap)
+  static const uint32_t scan_big = [] { const char* e = std::getenv("CEDARGPU_SCAN_BIG"); return e ? (uint32_t)std::atoi(e) : 48u; }();
+  k.scan_big = scan_big;
   k.stats = nullptr;
   k.n_dev = nullptr;
   k.scan = nullptr;
