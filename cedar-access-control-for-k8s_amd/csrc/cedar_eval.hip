@@ -2685,7 +2685,9 @@ static uint32_t probe_wpb() {
 constexpr uint32_t BIG_MINW = 3;
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
   if (big && k.scan) {  // the large stage over the scan's buckets (probing only past SCAN_CAP)
-    static const uint32_t bw = [] { const char* e = std::getenv("CEDARGPU_BIG_WPB"); return e ? (uint32_t)std::atoi(e) : 4u; }();
+    // one-wave blocks: a finished request's wave slot and LDS return at once (C3 DAG 4.996e8 vs
+    // 4.919e8 with 4-wave blocks, profiles/r02/ab_big_occ)
+    static const uint32_t bw = [] { const char* e = std::getenv("CEDARGPU_BIG_WPB"); return e ? (uint32_t)std::atoi(e) : 1u; }();
     if (bw == 1) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, 1, true>), dim3(n), dim3(64), 0, s, k);
     else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, WAVES, true>), dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
     return;
