@@ -1543,7 +1543,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     const uint64_t off = img->dev_off[k], len = img->dev_len[k];
     if (off % DS_ALIGN || off < img->dev_begin || len % 4 || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
     v.resize(len / 4);
-    std::memcpy(v.data(), p + off, len);
+    if (len) std::memcpy(v.data(), p + off, len);  // an empty section (no static entities) has no storage
   };
   sec_words(DS_PSTREAM, img->pstream); sec_words(DS_TIER_CEND, img->tier_cend); sec_words(DS_CHUNKS, img->chunks);
   sec_words(DS_CPOOL, img->cpool); sec_words(DS_GSTR_OFF, img->gstr_off); sec_words(DS_HOT, img->hot);

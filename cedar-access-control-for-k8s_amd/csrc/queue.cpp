@@ -8,8 +8,9 @@
 // of 16 stripes (a mutex held for one pointer push) and sleeps. One flusher thread drains the
 // stripes into device batches (at most `max_batch` requests; with `max_delay_us` > 0 it first lets
 // a batch fill for that long after its first request) and deals each closed batch to the least
-// loaded GPU: one submitter thread per context runs its batches (submit, wait) and publishes the
-// results with one futex wake for every waiting caller. While every GPU is busy with a batch and
+// loaded GPU: one submitter thread per context runs its batches (submit, wait; the next batch is
+// submitted before the previous one is waited for) and publishes the results with one futex wake
+// for every waiting caller. While every GPU is busy with a batch and
 // has the next one queued, the flusher keeps draining into a larger batch, so the batch size adapts
 // to the offered load. Callers render their own decision and reason in parallel.
 //
@@ -128,25 +129,22 @@ struct cg_queue {
 };
 
 void cg_queue::work(QWorker& w) {
-  for (;;) {
-    std::shared_ptr<QBatch> qb;
-    {
-      std::unique_lock<std::mutex> g(w.mu);
-      w.cv.wait(g, [&] { return w.stop || !w.q.empty(); });
-      if (w.q.empty()) return;  // stopped and drained
-      qb = std::move(w.q.front());
-      w.q.pop_front();
-    }
-    const auto t0 = Clock::now();
+  // Pipelined: a batch dealt while the previous one runs is submitted before that one is waited
+  // for, so its host side (string table, pinned staging, launch) overlaps the device work and its
+  // upload queues right behind the previous batch's results on the context's stream.
+  std::shared_ptr<QBatch> inflight;  // submitted, not yet waited for
+  Clock::time_point busy_since{};    // device-busy accounting: the union of in-flight intervals
+  auto finish = [&](std::shared_ptr<QBatch>& qb) {
     if (!qb->rc) {
-      int rc = cg_batch_submit(qb->b);
-      if (!rc) rc = cg_batch_wait(qb->b, -1);
+      const int rc = cg_batch_wait(qb->b, -1);
       if (rc) {
         qb->rc = rc;
         qb->err = qb->b->err;
       }
     }
-    device_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+    const auto now = Clock::now();
+    device_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - busy_since).count();
+    busy_since = now;
     w.n_batches++;
     w.n_requests += qb->b->items.size();
     publish(*qb);
@@ -155,6 +153,36 @@ void cg_queue::work(QWorker& w) {
       w.load.fetch_sub(1);
     }
     slot_cv.notify_one();
+    qb.reset();
+  };
+  for (;;) {
+    std::shared_ptr<QBatch> qb;
+    {
+      std::unique_lock<std::mutex> g(w.mu);
+      if (!inflight) {
+        w.cv.wait(g, [&] { return w.stop || !w.q.empty(); });
+        if (w.q.empty()) return;  // stopped and drained
+      }
+      if (!w.q.empty()) {
+        qb = std::move(w.q.front());
+        w.q.pop_front();
+      }
+    }
+    if (qb) {
+      if (!inflight) busy_since = Clock::now();
+      if (!qb->rc) {
+        const int rc = cg_batch_submit(qb->b);
+        if (rc) {
+          qb->rc = rc;
+          qb->err = qb->b->err;
+        }
+      }
+    }
+    if (inflight) finish(inflight);  // the previous batch's results, while the next one runs
+    if (qb) {
+      if (qb->rc) finish(qb);  // not submitted: its callers get the error now
+      else inflight = std::move(qb);
+    }
   }
 }
 
