@@ -496,6 +496,40 @@ def test_probe_kernel_abac_deep_group_dag(ctx):
     check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
 
 
+@pytest.mark.parametrize("chain", [20, 40, 70, 130])
+def test_scan_list_thresholds(ctx, chain):
+    """A static group chain whose every level carries permits / forbids: a principal at the bottom
+    finds one bucket per level. 20: the candidate pass; 40: over the large stage's hand-off (48)
+    only with both effects; 70: the large stage reads the scan list (<= 96 buckets); 130: the list
+    overflows and the large stage probes the index itself. Hits past 64 / 1,024 and long reason
+    lists included; vs the C++ oracle."""
+    G = lambda g: {"type": "k8s::Group", "id": g}
+    ents = [{"uid": G(f"c{k}"), "attrs": {"name": f"c{k}"}, "parents": [G(f"c{k + 1}")] if k + 1 < chain else []}
+            for k in range(chain)]
+    pols = []
+    for k in range(chain):
+        pols.append(f'permit (principal in k8s::Group::"c{k}", action == k8s::Action::"get", resource is k8s::Resource) '
+                    f'when {{ resource.namespace == "ns{k % 3}" }};')
+        pols.append(f'permit (principal in k8s::Group::"c{k}", action, resource is k8s::Resource) '
+                    f'when {{ resource.resource == "pods" }};')
+        if k % 2 == 0:
+            pols.append(f'forbid (principal in k8s::Group::"c{k}", action in [k8s::Action::"delete"], resource is k8s::Resource) '
+                        f'when {{ resource has name && resource.name like "prod-*" }};')
+    stores = [cedargpu.MemoryStore("chain.cedar", "\n".join(pols))]
+    items = []
+    for i in range(96):
+        start = (i * 7) % chain
+        groups = [f"c{start}"] + ([f"c{(start + 5) % chain}"] if i % 3 == 0 else [])
+        verb = ["get", "list", "delete", "get"][i % 4]
+        a = km.Attributes(user=km.UserInfo(name=f"u{i}", uid=f"id{i}", groups=groups), verb=verb,
+                          namespace=f"ns{i % 4}", api_group="", api_version="v1",
+                          resource=["pods", "secrets"][i % 2], name=["prod-x", "dev-y", ""][i % 3],
+                          resource_request=True)
+        em, r = km.record_to_cedar_resource(a)
+        items.append((co.entities_to_json(em), co.request_to_json(r)))
+    check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
+
+
 def test_static_dag_handmade(ctx):
     """A small static group DAG: principals in several groups with overlapping ancestor sets, a
     static group the request re-parents (its request parent joins the merged ancestry), a direct
