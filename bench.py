@@ -494,7 +494,11 @@ def main():
                        "parallelism": f"request-sharded x{world}, image replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg_bytes},
+                         "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg_bytes,
+                         "launch": "one complete step on one stream: cedar_scan_kernel, the SPLIT candidate pass, "
+                                   "cedar_fu_gather and the follow-up launches (rocprofv3 split in profiles/r02/)",
+                         "traffic_source": "PMC FETCH_SIZE x2 + WRITE_SIZE summed over one step's dispatches "
+                                           "(tools/pmc_kernels.sh, profiles/pmc_latest.json)" if traffic else None},
             "cpu_baseline": baseline,
             "parity_sample": parity,
             "reload": reload,
