@@ -889,8 +889,12 @@ int cg_batch_submit(cg_batch* b) {
       if (h.ppm[k]) b->host.fu_want[k] = (uint32_t)std::min<uint64_t>(n, (uint64_t)h.ppm[k] * n / 1000000u * 5 / 4 + 64);
     if (h.big_maxr) b->host.fu_capr_hint = (h.big_maxr + h.big_maxr / 8 + 8 + 31) & ~31u;
     if (h.gen_maxr) b->host.fu_capr_gen_hint = (h.gen_maxr + h.gen_maxr / 8 + 8 + 31) & ~31u;
+    // the longest list the last first pass counted (<= 64), as far as the two reason arrays stay
+    // within the budget (CEDARGPU_FIRST_BUDGET_MB, default 32)
+    static const uint64_t budget = [] { const char* e = std::getenv("CEDARGPU_FIRST_BUDGET_MB"); return (uint64_t)(e ? std::max(1, std::atoi(e)) : 32) << 20; }();
     const uint32_t want_capr = std::min<uint32_t>(64u, (h.first_maxr + 7) & ~7u);
-    if (want_capr > b->host.capr && (uint64_t)n * want_capr * 8 <= (32ull << 20)) b->host.capr = want_capr;
+    const uint32_t fit = (uint32_t)std::min<uint64_t>(64u, budget / (8ull * std::max<uint32_t>(1u, n))) & ~7u;
+    if (std::min(want_capr, fit) > b->host.capr) b->host.capr = std::min(want_capr, fit);
   }
   if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   GUARD(b->err, { group_requests(b); })
