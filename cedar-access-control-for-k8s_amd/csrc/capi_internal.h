@@ -78,8 +78,7 @@ struct cg_batch {
   std::map<uint32_t, std::string> fast_reason;  // authz fast paths: the reason; admission: error text
   std::vector<cg::DevSubset> held;  // re-run result blocks the host lists point into (Batch::big)
   ~cg_batch() {
-    dev_batch_free(&dev);  // drains the batch's stream first when work on it may still run
-    for (auto& j : held) dev_subset_release(&j);
+    dev_batch_retire(&dev, held);  // never waits: blocks still in use return once the stream drains
   }
   int32_t dev_of(uint32_t i) const { return i < items.size() ? items[i].dev : -1; }
 };

@@ -28,6 +28,7 @@
 #include <mutex>
 #include <thread>
 #include <algorithm>
+#include <atomic>
 #include <vector>
 #include <string>
 
@@ -80,6 +81,7 @@ struct KArgs {
   uint32_t l2filt;  // level-2 probes too, after the level-1 entry's own bloom (CEDARGPU_L2_FILTER)
   uint32_t slot_split;  // probes load a slot's first 16 B, the rest only on a key match (CEDARGPU_SLOT_SPLIT)
   uint32_t scan_lds;    // the scan stages key ancestors and hot values in LDS up front (CEDARGPU_SCAN_LDS)
+  uint32_t scan_filt;   // the scan tests every level-1 key against the key filter first (CEDARGPU_SCAN_FILT)
   uint32_t scan_big;    // more scanned buckets than this: straight to the large stage (CEDARGPU_SCAN_BIG)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
@@ -1579,6 +1581,9 @@ __device__ __forceinline__ bool l2_bloom_maybe(uint4 b, uint32_t h2) {
 // in flight per CU; the probe kernel's SPLIT variant then evaluates the buckets' heads.
 // principal key ancestors the scan stages in LDS per request (more: read from the request block)
 constexpr uint32_t SCAN_ANC = 40;
+// key-filter pass: keys per lane per round (independent loads in flight), and the filter-passing
+// keys a request lists in LDS (more: it probes every key, as with the filter off)
+constexpr uint32_t SCAN_PU = 8, SCAN_POS = 64;
 template <uint32_t SEG, uint32_t MINW = 1>
 __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // per request: its first SCAN_ANC key ancestors and its hot values, loaded in one round trip
@@ -1586,6 +1591,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // with a dependent HBM load)
   __shared__ uint2 s_anc[64 / SEG][SCAN_ANC];
   __shared__ uint2 s_hot[64 / SEG][NHOT];
+  __shared__ uint16_t s_pos[64 / SEG][SCAN_POS];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
@@ -1620,13 +1626,110 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       s_hot[seg][h] = valid ? *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h) : make_uint2(0u, 0u);
     wave_lds_sync();
   }
+  // level-1 key k of the request: its combo and (principal, action, resource) components
+  auto key_at = [&](uint32_t k, uint32_t& cbo, uint2& p, uint2& q, uint2& r) {
+    uint32_t j = k, combo = 0;
+    bool found = false;
+    for (uint32_t m = cm; m; m &= m - 1) {
+      const uint32_t cb = __builtin_ctz(m);
+      const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+      if (!found) {
+        if (j < cnt) { combo = cb; found = true; }
+        else j -= cnt;
+      }
+    }
+    const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
+    const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
+    uint32_t ip = j, ia = 0, ir = 0;
+    if (na_ != 1u || (rkc == KC_ENT && nR != 1u)) {
+      const uint32_t t2 = j / np_;
+      ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
+    }
+    const uint32_t jp = ip + 1 - (pn >> 31);  // 0: the principal itself, j: ancestor j - 1
+    p = (stl && pkc == KC_ENT && jp && jp <= SCAN_ANC) ? s_anc[seg][jp - 1] : key_comp(pkc, jp, pt, pi, blk, p_anc);
+    q = key_comp(akc, ia + 1 - (an >> 31), at, ai, blk, a_anc);
+    r = key_comp(rkc, ir + 1 - (rn >> 31), rt, ri, blk, r_anc);
+    cbo = combo;
+  };
+  // the same from registers and LDS only; false (components not set) when a component is an
+  // ancestor that lives in the request block (the filter pass then lets the key through unread:
+  // a global load there would make every filter load before it wait)
+  auto key_at_reg = [&](uint32_t k, uint32_t& cbo, uint2& p, uint2& q, uint2& r) -> bool {
+    uint32_t j = k, combo = 0;
+    bool found = false;
+    for (uint32_t m = cm; m; m &= m - 1) {
+      const uint32_t cb = __builtin_ctz(m);
+      const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+      if (!found) {
+        if (j < cnt) { combo = cb; found = true; }
+        else j -= cnt;
+      }
+    }
+    const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
+    const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
+    uint32_t ip = j, ia = 0, ir = 0;
+    if (na_ != 1u || (rkc == KC_ENT && nR != 1u)) {
+      const uint32_t t2 = j / np_;
+      ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
+    }
+    const uint32_t jp = ip + 1 - (pn >> 31), ja = ia + 1 - (an >> 31), jr = ir + 1 - (rn >> 31);
+    if ((pkc == KC_ENT && jp && !(stl && jp <= SCAN_ANC)) || (akc == KC_ENT && ja) || (rkc == KC_ENT && jr)) return false;
+    p = (pkc == KC_ENT && jp) ? s_anc[seg][jp - 1] : key_comp(pkc, 0, pt, pi, blk, p_anc);
+    q = key_comp(akc, 0, at, ai, blk, a_anc);
+    r = key_comp(rkc, 0, rt, ri, blk, r_anc);
+    cbo = combo;
+    return true;
+  };
+  // Key-filter pass: every level-1 key's filter block is loaded up front (SCAN_PU independent
+  // small loads per lane in flight, from a table of ~16 bits per index entry that stays in L2),
+  // and only the keys the filter passes are probed below. The scope table's 64-byte slots are
+  // then touched ~once per found key instead of once per enumerated key (~62 on C3's group DAG,
+  // of which ~6 exist), and those probes leave in one step instead of one per SEG keys.
+  uint32_t npos = 0;
+  if (a.scan_filt) {
+    for (uint32_t rb = 0; __ballot(valid && rb < n_keys) != 0; rb += SEG * SCAN_PU) {
+      uint2 fw[SCAN_PU];
+      uint32_t fy[SCAN_PU];
+#pragma unroll
+      for (uint32_t u = 0; u < SCAN_PU; u++) {
+        const uint32_t k = rb + u * SEG + sl;
+        fw[u] = make_uint2(~0u, ~0u);  // keys not tested pass
+        fy[u] = 0;
+        uint32_t cb;
+        uint2 p, q, r;
+        if (valid && k < n_keys && key_at_reg(k, cb, p, q, r)) {
+          const uint32_t y = filt_mix(key_hash(cb, p.x, p.y, q.x, q.y, r.x, r.y));
+          fy[u] = y;
+          fw[u] = *reinterpret_cast<const uint2*>(a.bfilt + 2 * (size_t)(y & a.fmask));
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < SCAN_PU; u++) {
+        const uint32_t k = rb + u * SEG + sl;
+        const uint32_t bits = filt_bits(fy[u]);
+        const uint64_t w = ((uint64_t)fw[u].y << 32) | fw[u].x;  // (a select between the words
+        // would index the array dynamically and put it in scratch)
+        const uint64_t need = (1ull << (bits & 63u)) | (1ull << ((bits >> 6) & 63u)) | (1ull << ((bits >> 12) & 63u));
+        const bool ok = valid && k < n_keys && (w & need) == need;
+        const uint64_t m = sballot(ok);
+        const uint32_t at_ = npos + mbcnt64(m);
+        if (ok && at_ < SCAN_POS) s_pos[seg][at_] = (uint16_t)k;
+        npos += popc64(m);
+      }
+    }
+    wave_lds_sync();
+  }
+  // a request with more filter-passing keys than the list holds (or keys past its 16-bit
+  // indices) enumerates them all
+  const bool flt = a.scan_filt && npos <= SCAN_POS && n_keys <= 0x10000u;
+  const uint32_t n_l1 = flt ? npos : n_keys;
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);
   uint32_t csl = 0, ch = 0, cl = 0, ck = 0, cn = 0;
   for (;;) {
     const bool l2 = sballot(hm != 0 || csl != 0 || ck < cn) != 0;
-    const bool done = !l2 && kb >= n_keys;
+    const bool done = !l2 && kb >= n_l1;
     if (__ballot(!done) == 0) break;
     uint3 e = make_uint3(0, 0, 0);
     if (!done) {
@@ -1670,34 +1773,14 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           }
         }
       } else {
-        const uint32_t k = kb + sl;
+        const uint32_t kk = kb + sl;
         kb += SEG;
-        uint32_t j = k;
-        bool found = false;
-        for (uint32_t m = cm; m; m &= m - 1) {
-          const uint32_t cb = __builtin_ctz(m);
-          const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
-          if (!found) {
-            if (j < cnt) { combo = cb; found = true; }
-            else j -= cnt;
-          }
-        }
-        if (k < n_keys) {
-          const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
-          const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
-          uint32_t ip = j, ia = 0, ir = 0;
-          if (na_ != 1u || (rkc == KC_ENT && nR != 1u)) {
-            const uint32_t t2 = j / np_;
-            ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
-          }
-          const uint32_t jp = ip + 1 - (pn >> 31);  // 0: the principal itself, j: ancestor j - 1
-          kp = (stl && pkc == KC_ENT && jp && jp <= SCAN_ANC) ? s_anc[seg][jp - 1] : key_comp(pkc, jp, pt, pi, blk, p_anc);
-          ka = key_comp(akc, ia + 1 - (an >> 31), at, ai, blk, a_anc);
-          kr = key_comp(rkc, ir + 1 - (rn >> 31), rt, ri, blk, r_anc);
+        if (kk < n_l1) {
+          key_at(flt ? s_pos[seg][kk] : kk, combo, kp, ka, kr);
           w0 = BT_USED | (combo << 16);
           h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
           uint32_t cmv = 0;
-          if (!a.l1filt || filt_maybe(a.bfilt, a.fmask, h1))
+          if (flt || !a.l1filt || filt_maybe(a.bfilt, a.fmask, h1))
             e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, &blm, &cmv, a.slot_split);
           hm = e.z;
           csl = cmv;
@@ -2304,12 +2387,21 @@ void dev_image_free(DevImage* d) {
   *d = DevImage();
 }
 
+// A batch retired while its work may still run (dev_batch_retire): its blocks wait here until a
+// host callback behind that work on its stream marks it drained; pool users then reap it.
+struct Retired {
+  DevBatch d;
+  std::vector<DevSubset> held;
+  std::atomic<bool> drained{false};
+};
 struct DevPool {
   int device = -1;
   std::mutex mu;
   std::multimap<size_t, void*> dev_free, host_free;  // size class -> idle block
   std::vector<std::pair<void*, bool>> owned;         // (block, pinned host)
+  std::vector<Retired*> retired;                     // under mu
 };
+static void pool_reap(DevPool* p);
 
 static size_t size_class(size_t n) {
   size_t c = (size_t)1 << 16;
@@ -2319,6 +2411,7 @@ static size_t size_class(size_t n) {
 
 static int pool_get(DevPool* p, bool host, size_t n, void** out, size_t* cls) {
   *cls = size_class(n);
+  pool_reap(p);
   {
     std::lock_guard<std::mutex> g(p->mu);
     auto& fl = host ? p->host_free : p->dev_free;
@@ -2353,6 +2446,8 @@ void dev_pool_destroy(DevPool* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   (void)hipDeviceSynchronize();
+  pool_reap(p);
+  for (Retired* r : p->retired) delete r;  // (only on a device that never drained them)
   for (auto& o : p->owned) {
     if (o.second) (void)hipHostFree(o.first);
     else (void)hipFree(o.first);
@@ -2533,6 +2628,62 @@ void dev_batch_free(DevBatch* d) {
   *d = DevBatch();
 }
 
+// host callback behind a retired batch's work: no HIP calls here (HIP forbids them in callbacks)
+static void retired_drained(void* r) { static_cast<Retired*>(r)->drained.store(true, std::memory_order_release); }
+
+static void pool_reap(DevPool* p) {
+  std::vector<Retired*> done;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    if (p->retired.empty()) return;
+    auto keep = p->retired.begin();
+    for (Retired* r : p->retired) {
+      if (r->drained.load(std::memory_order_acquire)) done.push_back(r);
+      else *keep++ = r;
+    }
+    p->retired.erase(keep, p->retired.end());
+  }
+  for (Retired* r : done) {
+    r->d.pending = false;  // its stream passed the callback: nothing of it runs any more
+    dev_batch_free(&r->d);
+    for (auto& j : r->held) dev_subset_release(&j);
+    delete r;
+  }
+}
+
+void dev_batch_retire(DevBatch* d, std::vector<DevSubset>& held) {
+  bool busy = d->pending && d->stream;
+  for (auto& j : held)
+    if (j.done && hipEventQuery((hipEvent_t)j.done) == hipErrorNotReady) busy = true;
+  DevPool* pool = d->pool;
+  if (!busy || !pool || d->device < 0) {
+    dev_batch_free(d);
+    for (auto& j : held) dev_subset_release(&j);
+    held.clear();
+    return;
+  }
+  (void)hipSetDevice(d->device);
+  Retired* r = new (std::nothrow) Retired();
+  if (r) {
+    r->d = *d;
+    r->held.swap(held);
+    // the re-run jobs run on the batch's stream too (dev_subset_begin), so one callback covers all
+    if (hipLaunchHostFunc((hipStream_t)d->stream, retired_drained, r) == hipSuccess) {
+      {
+        std::lock_guard<std::mutex> g(pool->mu);
+        pool->retired.push_back(r);
+      }
+      *d = DevBatch();
+      return;
+    }
+    held.swap(r->held);
+    delete r;
+  }
+  dev_batch_free(d);  // no callback could be enqueued: fall back to draining the stream here
+  for (auto& j : held) dev_subset_release(&j);
+  held.clear();
+}
+
 static size_t lds_bytes(const DevImage& img) { return (size_t)std::max<uint32_t>(img.n_hot, 1) * BLOCK * sizeof(uint2); }
 
 // Worklists of the on-device follow-up (device.h FuKind): every request the first pass left
@@ -2613,6 +2764,8 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.slot_split = slot_split;
   static const uint32_t scan_lds = [] { const char* e = std::getenv("CEDARGPU_SCAN_LDS"); return (e && *e == '0') ? 0u : 1u; }();
   k.scan_lds = scan_lds;
+  static const uint32_t scan_filt = [] { const char* e = std::getenv("CEDARGPU_SCAN_FILT"); return (e && *e == '0') ? 0u : 1u; }();
+  k.scan_filt = scan_filt;
   // 48: C3 DAG 4.91e8 decisions/s at 32..96 alike; a list of 24 that sent every longer one to the
   // large stage measured 4.58e8 (43,485 large-stage requests instead of 25,005; profiles/r02/ab_scan_cap)
   static const uint32_t scan_big = [] { const char* e = std::getenv("CEDARGPU_SCAN_BIG"); return e ? (uint32_t)std::atoi(e) : 48u; }();

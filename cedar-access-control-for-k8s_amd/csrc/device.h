@@ -96,6 +96,12 @@ void dev_pool_destroy(DevPool* p);
 // Uploads the batch's inputs (staged through a pinned block, one H2D copy) and zeroes its results.
 int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, DevPool* pool);
 void dev_batch_free(DevBatch* d);  // returns the blocks to the batch's pool
+struct DevSubset;
+// The same without waiting, for a batch (and the re-run jobs it holds) that a caller gives up on
+// while its work may still run (a missed deadline, a hung device): the blocks return to the pool
+// once the batch's stream has passed a host callback enqueued behind that work, and never while
+// it may still write them. No wait at all, so a caller's deadline holds even on a hung GPU.
+void dev_batch_retire(DevBatch* d, std::vector<DevSubset>& held);
 // Evaluates every request of the batch into the batch's device result buffers (async on stream).
 int dev_eval(const DevImage& img, DevBatch& b, void* stream);
 // Re-evaluates the subset idx[0..n) with larger result capacities (probe 1: on the probe kernel,

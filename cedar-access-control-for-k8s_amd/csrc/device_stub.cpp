@@ -168,6 +168,11 @@ int dev_subset_begin(const DevImage&, const DevBatch&, const uint32_t*, uint32_t
 }
 int dev_subset_end(DevSubset*, SubsetView* v, int64_t) { *v = SubsetView(); return 0; }
 void dev_subset_release(DevSubset* job) { *job = DevSubset(); }
+void dev_batch_retire(DevBatch* d, std::vector<DevSubset>& held) {
+  dev_batch_free(d);  // the stand-in's work is synchronous: nothing of the batch's can still run
+  for (auto& j : held) dev_subset_release(&j);
+  held.clear();
+}
 
 static void bind(const DevBatch& b, Batch& host) {
   host.capr = b.capr;

@@ -86,13 +86,16 @@ def test_batch_wait_deadline_then_completes(ctx):
     b.wait()  # the batch stayed in flight and completes
     assert [b.authz(i) for i in range(len(b))] == _oracle(DEMO_AUTHZ, sars)
     b.close()
-    # a timed-out batch destroyed while in flight: destroy drains its stream
+    # a timed-out batch destroyed while in flight: destroy returns at once (its blocks go back to
+    # the pool once the stream has passed them, dev_batch_retire)
     b = ctx.batch()
     b.add_sar_json(json.dumps(sars[:10]))
     b.submit()
     with pytest.raises(cedargpu.DeadlineError):
         b.wait(timeout=0.01)
+    t0 = time.perf_counter()
     b.close()
+    assert time.perf_counter() - t0 < 0.1
     ctx.inject_fault(cedargpu.FAULT_NONE)
     b = ctx.batch()
     b.add_sar_json(json.dumps(sars))
@@ -129,3 +132,31 @@ def test_queue_deadline_and_failsafe(ctx):
     finally:
         ctx.inject_fault(cedargpu.FAULT_NONE)
         q.close()
+
+
+def test_authorizer_deadline_under_stall(ctx):
+    """Authorizer(timeout=...) answers NoOpinion within its deadline while the device stalls: the
+    timed-out batch is retired without waiting for the stream (close() used to drain it)."""
+    authz = cedargpu.Authorizer([cedargpu.MemoryStore("demo.cedar", DEMO_AUTHZ)], ctx=ctx, timeout=0.05)
+    sars = _sars()
+    want = _oracle(DEMO_AUTHZ, sars)
+    assert authz.authorize_batch(sars) == want
+    handler = cedargpu.AdmissionHandler([cedargpu.MemoryStore("adm.cedar", DEMO_ADM), cedargpu.ALLOW_ALL_ADMISSION],
+                                        ctx=ctx, timeout=0.05)
+    reviews = synth.admission_reviews(16, seed=9)
+    ctx.inject_fault(cedargpu.FAULT_STALL, 400_000)
+    t0 = time.perf_counter()
+    got = authz.authorize_batch(sars)
+    assert time.perf_counter() - t0 < 0.2
+    for s, g, w in zip(sars, got, want):
+        name = s["spec"]["user"]
+        fast = name.startswith("system:") and not name.startswith(("system:serviceaccount:", "system:node:"))
+        assert g == (w if fast else (cedargpu.Authorizer.NO_OPINION, "")), s
+    ctx.inject_fault(cedargpu.FAULT_STALL, 400_000)
+    t0 = time.perf_counter()
+    assert handler.handle_batch(reviews) == [(True, 200, "")] * len(reviews)
+    assert time.perf_counter() - t0 < 0.2
+    ctx.inject_fault(cedargpu.FAULT_NONE)
+    time.sleep(1.0)  # the stalled batches drain; their blocks are reaped by the next batch
+    authz.timeout = 5.0
+    assert authz.authorize_batch(sars) == want

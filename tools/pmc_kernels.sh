@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes over a short C3 bench run, reduced per kernel of the complete step (scan, candidate
-# pass, large stage): vL1D accesses, L2 requests, instruction mix, wave cycles, HBM fetch.
+# pass, large stage): vL1D accesses, L2 requests, instruction mix, wave cycles, LDS bank conflicts
+# (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE: conflict cycles over LDS-active cycles), HBM fetch.
 # Usage: tools/pmc_kernels.sh TAG   (extra env, e.g. CEDARGPU_NO_CLOSURE=1, applies to every pass)
 set -o pipefail
 TAG=${1:-pmck}
@@ -14,6 +15,7 @@ run() {
 }
 run tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum && \
 run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_ANY && \
+run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE && \
 run fetch FETCH_SIZE && \
 run write WRITE_SIZE && \
 for K in cedar_scan_kernel "cedar_probe_kernel<8u, 64u" "cedar_probe_kernel<64u, 1024u"; do

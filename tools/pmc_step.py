@@ -48,7 +48,7 @@ def short(n):
 def main(out, policies, batch, hierarchy):
     res = {"policies": policies, "batch": batch, "hierarchy": hierarchy, "kernels": {}}
     tot = defaultdict(float)
-    for sub in ("fetch", "write", "tcp", "sq"):
+    for sub in ("fetch", "write", "tcp", "sq", "lds"):
         d = os.path.join(out, sub)
         if not os.path.isdir(d):
             continue
@@ -68,6 +68,9 @@ def main(out, policies, batch, hierarchy):
         res["hbm_write_bytes_per_launch"] = res["WRITE_SIZE"] * 1024
         res["hbm_bytes_per_launch"] = res["hbm_read_bytes_per_launch"] + res["hbm_write_bytes_per_launch"]
         res["what"] = "one complete step (scan + candidate pass + gather + follow-ups), per 1M-request launch"
+    for k in res["kernels"].values():  # share of LDS-active cycles lost to bank conflicts
+        if k.get("SQ_LDS_IDX_ACTIVE"):
+            k["lds_bank_conflict_frac"] = k.get("SQ_LDS_BANK_CONFLICT", 0.0) / k["SQ_LDS_IDX_ACTIVE"]
     print(json.dumps(res, indent=1))
 
 
