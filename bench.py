@@ -393,10 +393,12 @@ def main():
     sizing.submit()
     sizing.wait()
     sizing.close()
+    payload = synth.sars_json(sars)  # the SAR bodies as the webhook receives them (not timed)
     t_build = time.perf_counter()
     b = ctx.batch()
-    b.add_sar_json(synth.sars_json(sars))
+    b.add_sar_json(payload)  # cg_batch_add_sar_json: SAR conversion + columnar encode, host threads
     t_enc = time.perf_counter()
+    del payload
     b.submit()
     b.wait()  # correctness pass: results downloaded, follow-ups folded, host re-runs (if any) done
     t_first = time.perf_counter()
@@ -418,6 +420,11 @@ def main():
         t = torch.tensor([wall_s, kernel_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall_s, kernel_ms = float(t[0]), float(t[1])
+
+    # per-phase split of the same step (HIP events at each phase boundary; outside the timed region)
+    split_steps = max(1, min(args.steps, 5))
+    phases, split_total = b.time_split(split_steps)
+    phases = {k: v / split_steps for k, v in phases.items()}
 
     # submit -> results-visible latency on small batches (includes H2D, launch, D2H)
     lat = []
@@ -488,14 +495,18 @@ def main():
                                "all reasons and errors listed, on the device)",
                        "device_followup_requests": followups,
                        "rerun_requests": host_reruns,
-                       "request_order": (f"{args.order}; the batching layer groups batches of >= 65,536 requests by "
-                                         "(action, resource type), principal groups, hot attributes at submit "
-                                         "(host radix sort, outside the timed launches)"),
+                       "request_order": (f"{args.order} as uploaded; batches of >= 65,536 requests are grouped on the "
+                                         "device inside every timed step (grouping-key kernel + rocPRIM radix sort of "
+                                         "(action, resource type), principal key ancestors, hot values; the kernels read "
+                                         "requests in that order)" if os.environ.get("CEDARGPU_GROUP_DEV", "1") != "0"
+                                         else f"{args.order}; host radix sort at submit, outside the timed step (A/B)"),
                        "parallelism": f"request-sharded x{world}, image replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg_bytes,
-                         "launch": "one complete step on one stream: cedar_scan_kernel, the SPLIT candidate pass, "
+                         "phases_ms": phases, "phases_total_ms": split_total / split_steps,
+                         "dominant_phase": max(phases, key=phases.get),
+                         "launch": "one complete step on one stream: the device grouping (key kernel + rocPRIM sort), cedar_scan_kernel, the SPLIT candidate pass, "
                                    "cedar_fu_gather and the follow-up launches (rocprofv3 split in profiles/r02/)",
                          "traffic_source": "PMC FETCH_SIZE x2 + WRITE_SIZE summed over one step's dispatches "
                                            "(tools/pmc_kernels.sh, profiles/pmc_latest.json)" if traffic else None},

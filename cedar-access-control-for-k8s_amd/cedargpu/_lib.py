@@ -104,6 +104,7 @@ _SIGS = {
     "cg_batch_diagnostic": (ctypes.c_int, [P, u32, ctypes.c_int, P, sz, ctypes.POINTER(sz)]),
     "cg_batch_reasons": (ctypes.c_int, [P, u32, ctypes.POINTER(u32), u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]),
     "cg_batch_time": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_float)]),
+    "cg_batch_time_split": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "cg_batch_reruns": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
     "cg_batch_followups": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
     "cg_batch_bytes": (ctypes.c_int, [P, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),

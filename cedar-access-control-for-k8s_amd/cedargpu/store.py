@@ -431,6 +431,18 @@ class Batch:
             raise _err(rc, "timing failed")
         return ms.value
 
+    PHASES = ("group", "scan", "candidates", "gather", "fu_big", "fu_long_lists", "fu_structural")
+
+    def time_split(self, iters: int):
+        """(per-phase device ms summed over `iters` steps, total ms): HIP events at each phase boundary
+        of the complete step (cg_batch_time_split)."""
+        ph = (ctypes.c_float * len(self.PHASES))()
+        tot = ctypes.c_float()
+        rc = lib.cg_batch_time_split(self._h, iters, ph, ctypes.byref(tot))
+        if rc:
+            raise _err(rc, "timing failed")
+        return dict(zip(self.PHASES, list(ph))), tot.value
+
     def bytes(self):
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         lib.cg_batch_bytes(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))

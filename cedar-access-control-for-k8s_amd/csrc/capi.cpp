@@ -116,12 +116,19 @@ void parallel_for(size_t n, F&& f) {
 // costs ~50 ns of host time per request (~2 ms at 32,768), more than a smaller batch's kernel
 // wins back (C4 at 32,768: kernel 1.32 -> 0.81 ms, submit -> results 7.4 -> 8.0 ms).
 // CEDARGPU_GROUP=1 / 0 forces it.
+// Round 3: the order is computed on the device inside every evaluation step (group.hip: a grouping
+// key per request and a rocPRIM radix sort; the kernels read requests in that order), so a batch
+// costs no host sort and the timed step includes its ordering. CEDARGPU_GROUP_DEV=0 keeps the host
+// sort below (A/B).
 void group_requests(cg_batch* b) {
   Batch& h = b->host;
   const uint32_t n = h.n(), rw = h.row_words;
   bool on = n >= 65536u;
   if (const char* e = std::getenv("CEDARGPU_GROUP")) on = *e == '1';
+  static const bool dev = !(std::getenv("CEDARGPU_GROUP_DEV") && *std::getenv("CEDARGPU_GROUP_DEV") == '0');
+  h.dev_group = false;
   if (!on || n < 2 || n >= (1u << 24) || !rw || h.rows.size() != (size_t)n * rw) return;
+  if (dev) { h.dev_group = true; return; }
   auto mix = [](uint64_t k, uint32_t w) {
     k ^= w;
     k *= 0xff51afd7ed558ccdull;
@@ -1184,6 +1191,13 @@ int cg_batch_time(cg_batch* b, uint32_t iters, float* ms_total) {
   if (!b || !ms_total) return CG_E_ARG;
   if (!b->submitted) return CG_E_STATE;
   if (dev_time_eval(b->img->dev, b->dev, iters, b->ctx->stream, ms_total)) { b->err = dev_last_error(); return CG_E_DEVICE; }
+  return CG_OK;
+}
+
+int cg_batch_time_split(cg_batch* b, uint32_t iters, float* ms_phase, float* ms_total) {
+  if (!b || !ms_phase || !ms_total) return CG_E_ARG;
+  if (!b->submitted) return CG_E_STATE;
+  if (dev_time_split(b->img->dev, b->dev, iters, b->ctx->stream, ms_phase, ms_total)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   return CG_OK;
 }
 

@@ -75,6 +75,9 @@ struct KArgs {
   const uint4* __restrict__ shash;
   unsigned long long* stats;             // probe-kernel work counters (STATS variant only)
   const uint32_t* n_dev;                 // follow-up pass: request count on the device (null: n_req)
+  // first pass of a grouped batch: launch position -> request (the device sort's order, so that the
+  // requests of a wave share scope-index buckets); results stay at the request's own index
+  const uint32_t* ord;
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
   uint32_t hlists;  // rows carry element-hash lists (image.h "set-membership keys")
   uint32_t l1filt;  // level-1 probes consult the key filter first (CEDARGPU_L1_FILTER=1: on, A/B)
@@ -1205,7 +1208,8 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;  // follow-up: count on the device
   const bool valid = gid < n_req;
-  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0;
+  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0;
+  const uint32_t wo = a.req_idx ? gid : r;  // result slot: the worklist entry, or the request itself
 
   uint32_t lane_scratch[GLANE ? 1 : LANE_WORDS];
   Ctx c;
@@ -1371,18 +1375,18 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
         if (ok) {
           if (err) {
             if (ne < a.cape) {
-              uint32_t* er = a.errs + ((size_t)gid * a.cape + ne) * ERR_WORDS;
+              uint32_t* er = a.errs + ((size_t)wo * a.cape + ne) * ERR_WORDS;
               er[0] = p; er[1] = e.code | (e.aux << 8); er[2] = e.k; er[3] = e.et; er[4] = e.ei; er[5] = 0;
             }
             ne++;
           } else if (run) {
             if (flags & PF_FORBID) {
               if (nf < CAPR_L) rsn_lds[nf * BLOCK + threadIdx.x] = p;
-              else if (nf < a.capr) a.reasons_f[(size_t)gid * a.capr + nf] = p;
+              else if (nf < a.capr) a.reasons_f[(size_t)wo * a.capr + nf] = p;
               nf++;
             } else {
               if (np < CAPR_L) rsn_lds[(CAPR_L + np) * BLOCK + threadIdx.x] = p;
-              else if (np < a.capr) a.reasons_p[(size_t)gid * a.capr + np] = p;
+              else if (np < a.capr) a.reasons_p[(size_t)wo * a.capr + np] = p;
               np++;
             }
           }
@@ -1400,11 +1404,11 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
         if (nr > a.capr || ne > a.cape) fl |= RF_OVERFLOW;
         // flush the LDS-staged reasons of the deciding list
         const uint32_t nflush = min(min(nr, a.capr), CAPR_L);
-        uint32_t* dst = (nf ? a.reasons_f : a.reasons_p) + (size_t)gid * a.capr;
+        uint32_t* dst = (nf ? a.reasons_f : a.reasons_p) + (size_t)wo * a.capr;
         const uint32_t lbase = nf ? 0u : CAPR_L;
         for (uint32_t k = 0; k < nflush; k++) dst[k] = rsn_lds[(lbase + k) * BLOCK + threadIdx.x];
-        a.res[2 * (size_t)gid] = dec | (t << 8) | (fl << 16);
-        a.res[2 * (size_t)gid + 1] = min(nr, 0xFFFFu) | (min(ne, 0xFFFFu) << 16);
+        a.res[2 * (size_t)wo] = dec | (t << 8) | (fl << 16);
+        a.res[2 * (size_t)wo + 1] = min(nr, 0xFFFFu) | (min(ne, 0xFFFFu) << 16);
         decided = true;
       }
     }
@@ -1597,9 +1601,10 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
   auto sballot = [&](bool p) -> uint64_t { return __ballot(p) & smask; };
   auto sbcast = [&](uint32_t x, uint32_t k) -> uint32_t { return (uint32_t)__shfl((int)x, (int)(sbase + k)); };
-  const uint32_t gid = blockIdx.x * (64 / SEG) + seg;
-  const bool valid = gid < a.n_req;
-  const uint32_t* row = a.rows + (size_t)(valid ? gid : 0u) * a.row_words;
+  const uint32_t gid_ = blockIdx.x * (64 / SEG) + seg;
+  const bool valid = gid_ < a.n_req;
+  const uint32_t gid = valid ? (a.ord ? a.ord[gid_] : gid_) : 0u;  // the request (its list and row)
+  const uint32_t* row = a.rows + (size_t)gid * a.row_words;
   const uint32_t rw = (valid && sl < RW_HDR) ? row[sl] : 0u;
   const uint32_t rw_hi = (SEG < RW_HDR && valid && SEG + sl < RW_HDR) ? row[SEG + sl] : 0u;
   auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
@@ -1835,7 +1840,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint32_t gid = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;
   const bool valid = gid < n_req;
-  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0u;
+  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0u;
+  const uint32_t wo = a.req_idx ? gid : r;  // result slot: the worklist entry, or the request itself
   const uint32_t* row = a.rows + (size_t)r * a.row_words;
 
   // the request row streams through once: non-temporal loads, header broadcast in the segment
@@ -2159,8 +2165,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const bool undecided = nh > L::HC || nx > L::XC || structural;
   if (valid && undecided && sl == 0) {
     const uint32_t why = (structural || L::HC >= 1024) ? RF_GENERAL : RF_BIG;
-    a.res[2 * (size_t)gid] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | why) << 16);
-    a.res[2 * (size_t)gid + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
+    a.res[2 * (size_t)wo] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | why) << 16);
+    a.res[2 * (size_t)wo + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
 
   }
   const uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge
@@ -2208,11 +2214,11 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     const uint32_t kind = mj & 0xFF;
     const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
     const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
-    if (el && deny && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rf);
-    if (el && !deny && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)gid * a.capr + rp);
+    if (el && deny && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rf);
+    if (el && !deny && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rp);
     if (el && kind == 2 && re < a.cape) {
       const uint32_t xs = mj >> 16;
-      uint32_t* er = a.errs + ((size_t)gid * a.cape + re) * ERR_WORDS;
+      uint32_t* er = a.errs + ((size_t)wo * a.cape + re) * ERR_WORDS;
       er[0] = pj; er[1] = wl.he[seg][4 * xs]; er[2] = wl.he[seg][4 * xs + 1]; er[3] = wl.he[seg][4 * xs + 2];
       er[4] = wl.he[seg][4 * xs + 3]; er[5] = 0;
     }
@@ -2225,8 +2231,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     const uint32_t nr = nf ? nf : np;
     uint32_t fl = RF_VALID | (nf ? RF_FORBID : 0u);
     if (nr > a.capr || nerr > a.cape) fl |= RF_OVERFLOW;
-    a.res[2 * (size_t)gid] = dec | (t << 8) | (fl << 16);
-    a.res[2 * (size_t)gid + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
+    a.res[2 * (size_t)wo] = dec | (t << 8) | (fl << 16);
+    a.res[2 * (size_t)wo + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
   }
   if (STATS) {
     if (valid && sl == 0) st[0] = 1;
@@ -2532,15 +2538,34 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     }
     d.scan = (uint32_t*)d.scan_blk;
   }
+  if (b.dev_group && b.n() >= 2) {  // the device grouping's order, keys, values and sort storage
+    const size_t tb = group_temp_bytes(b.n());
+    const size_t q = ((size_t)b.n() * 4 + 255) & ~(size_t)255;
+    if (!tb) { g_err = "rocPRIM radix sort: no temporary storage size"; pool_put(pool, false, d.lane_blk, d.lane_cls); pool_put(pool, false, d.scan_blk, d.scan_cls); return -4; }
+    if ((rc = pool_get(pool, false, 4 * q + tb, &d.grp_blk, &d.grp_cls))) {
+      pool_put(pool, false, d.lane_blk, d.lane_cls);
+      pool_put(pool, false, d.scan_blk, d.scan_cls);
+      return rc;
+    }
+    uint8_t* g8 = (uint8_t*)d.grp_blk;
+    d.ord = (uint32_t*)g8;
+    d.gkeys = (uint32_t*)(g8 + q);
+    d.gkeys2 = (uint32_t*)(g8 + 2 * q);
+    d.gvals = (uint32_t*)(g8 + 3 * q);
+    d.grp_temp = g8 + 4 * q;
+    d.grp_temp_bytes = tb;
+  }
   if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) {
     pool_put(pool, false, d.lane_blk, d.lane_cls);
     pool_put(pool, false, d.scan_blk, d.scan_cls);
+    pool_put(pool, false, d.grp_blk, d.grp_cls);
     return rc;
   }
   if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) {
     pool_put(pool, false, d.in_blk, d.in_cls);
     pool_put(pool, false, d.lane_blk, d.lane_cls);
     pool_put(pool, false, d.scan_blk, d.scan_cls);
+    pool_put(pool, false, d.grp_blk, d.grp_cls);
     return rc;
   }
   if ((rc = pool_get(pool, true, std::max(in_bytes, d.out_bytes), &d.stage, &d.stage_cls))) {
@@ -2548,6 +2573,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     pool_put(pool, false, d.out_blk, d.out_cls);
     pool_put(pool, false, d.lane_blk, d.lane_cls);
     pool_put(pool, false, d.scan_blk, d.scan_cls);
+    pool_put(pool, false, d.grp_blk, d.grp_cls);
     return rc;
   }
   uint8_t* st = (uint8_t*)d.stage;
@@ -2623,6 +2649,7 @@ void dev_batch_free(DevBatch* d) {
     pool_put(d->pool, true, d->stage, d->stage_cls);
     pool_put(d->pool, false, d->lane_blk, d->lane_cls);
     pool_put(d->pool, false, d->scan_blk, d->scan_cls);
+    pool_put(d->pool, false, d->grp_blk, d->grp_cls);
   }
   if (d->req_idx) (void)hipFree(d->req_idx);
   *d = DevBatch();
@@ -2772,6 +2799,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.scan_big = scan_big;
   k.stats = nullptr;
   k.n_dev = nullptr;
+  k.ord = nullptr;
   k.scan = nullptr;
   k.scan_n = 0;
   return k;
@@ -2783,6 +2811,13 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
 // group-DAG workload 2.94e8 decisions/s against 2.21e8 with 16 lanes: a request's ~60 level-1
 // probes are dependent-latency chains, and more requests in flight per wave hide them;
 // profiles/r02/ab_seg8); CEDARGPU_PROBE_SEG=16 / 32 / 64 for comparisons.
+// Per-phase timing of a step (dev_time_split): while set, the step records an event at the end of
+// each phase (device.h STEP_PHASES) on its stream.
+static thread_local hipEvent_t* t_marks = nullptr;
+static void mark(uint32_t phase, hipStream_t s) {
+  if (t_marks) (void)hipEventRecord(t_marks[phase + 1], s);
+}
+
 static bool split_on() {
   static const bool on = !(std::getenv("CEDARGPU_SPLIT") && *std::getenv("CEDARGPU_SPLIT") == '0');
   return on;
@@ -2858,6 +2893,7 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     } else if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8>), sg, sb, 0, s, k);
     else if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6>), sg, sb, 0, s, k);
     else hipLaunchKernelGGL((cedar_scan_kernel<8>), sg, sb, 0, s, k);
+    if (!k.req_idx) mark(PH_SCAN, s);
     if (cocc == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
     else hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
     return;
@@ -2937,23 +2973,41 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
   k.scan = b.scan;
   k.scan_n = b.n;
+  if (b.ord) {  // grouped batch: this step's order, from the rows as uploaded (group.hip)
+    if (group_enqueue(b.rows, b.heap, b.n, b.row_words, img.n_hot, b.gkeys, b.gkeys2, b.gvals, b.ord, b.grp_temp,
+                      b.grp_temp_bytes, s)) {
+      g_err = "request grouping (rocPRIM radix sort) failed";
+      return -4;
+    }
+    k.ord = b.ord;
+  }
+  mark(PH_GROUP, s);
+  const bool two = img.indexed && split_on() && !probe_stats() && probe_seg() == 8 && probe_occ() == 3;
   launch_eval(img, k, b.n, s);
   HIPCHK(hipGetLastError(), "launch");
-  if (!b.fu_cnt) return 0;
+  if (!two) mark(PH_SCAN, s);  // a one-kernel first pass: all of it in the scan phase
+  mark(PH_CAND, s);
+  if (!b.fu_cnt) {
+    for (uint32_t p = PH_GATHER; p < STEP_PHASES; p++) mark(p, s);
+    return 0;
+  }
   HIPCHK(hipMemsetAsync(b.fu_cnt, 0, FU_KINDS * 4, s), "memset worklists");
   FuLists wl;
   for (uint32_t q = 0; q < FU_KINDS; q++) { wl.ids[q] = b.fu[q].ids; wl.cap[q] = b.fu[q].cap; }
   hipLaunchKernelGGL(cedar_fu_gather, dim3((b.n + GATHER_ITEMS * 256 - 1) / (GATHER_ITEMS * 256)), dim3(256), 0, s, b.res,
                      b.n, img.indexed, b.fu_cnt, wl);
+  mark(PH_GATHER, s);
   for (uint32_t q = 0; q < FU_KINDS; q++) {
     const auto& f = b.fu[q];
-    if (!f.cap) continue;
-    KArgs fk = make_args(img, b, f.ids, f.cap, f.res, f.rf, f.rp, f.er, f.capr, f.cape);
-    fk.n_dev = b.fu_cnt + q;
-    fk.scan = b.scan;  // the probe-kernel follow-ups read the first pass's buckets
-    fk.scan_n = b.n;
-    if (q == FU_GEN) launch_stream(img, fk, f.cap, s);
-    else launch_probe(fk, f.cap, s, q == FU_BIG);
+    if (f.cap) {
+      KArgs fk = make_args(img, b, f.ids, f.cap, f.res, f.rf, f.rp, f.er, f.capr, f.cape);
+      fk.n_dev = b.fu_cnt + q;
+      fk.scan = b.scan;  // the probe-kernel follow-ups read the first pass's buckets
+      fk.scan_n = b.n;
+      if (q == FU_GEN) launch_stream(img, fk, f.cap, s);
+      else launch_probe(fk, f.cap, s, q == FU_BIG);
+    }
+    mark(PH_FU_BIG + q, s);
   }
   HIPCHK(hipGetLastError(), "launch follow-up");
   return 0;
@@ -3147,6 +3201,34 @@ int dev_stall(int device, void* stream, uint64_t us) {
   hipLaunchKernelGGL(cedar_stall_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ticks);
   HIPCHK(hipGetLastError(), "launch stall");
   return 0;
+}
+
+int dev_time_split(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_phase, float* ms_total) {
+  HIPCHK(hipSetDevice(b.device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<hipEvent_t> ev((size_t)iters * (STEP_PHASES + 1));
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e), "event");
+  int rc = 0;
+  for (uint32_t i = 0; i < iters && !rc; i++) {
+    t_marks = &ev[(size_t)i * (STEP_PHASES + 1)];
+    (void)hipEventRecord(t_marks[0], s);
+    rc = enqueue_step(img, b, s);
+    t_marks = nullptr;
+  }
+  if (!rc) HIPCHK(hipEventSynchronize(ev.back()), "event sync");
+  for (uint32_t p = 0; p < STEP_PHASES; p++) ms_phase[p] = 0.f;
+  *ms_total = 0.f;
+  for (uint32_t i = 0; i < iters && !rc; i++) {
+    const hipEvent_t* m = &ev[(size_t)i * (STEP_PHASES + 1)];
+    for (uint32_t p = 0; p < STEP_PHASES; p++) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, m[p], m[p + 1]) == hipSuccess) ms_phase[p] += t;
+    }
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, m[0], m[STEP_PHASES]) == hipSuccess) *ms_total += t;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return rc;
 }
 
 int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_total) {

@@ -62,6 +62,11 @@ struct DevBatch {
   uint32_t* scan = nullptr;
   void* scan_blk = nullptr;
   size_t scan_cls = 0;
+  // grouped batch (Batch::dev_group): the step's first pass runs in the order ord (group.hip), sorted
+  // on the device from keys / keys2 / vals and the sort's temp storage, all in one pool block
+  uint32_t *ord = nullptr, *gkeys = nullptr, *gkeys2 = nullptr, *gvals = nullptr;
+  void *grp_blk = nullptr, *grp_temp = nullptr;
+  size_t grp_cls = 0, grp_temp_bytes = 0;
   uint32_t* lane = nullptr;  // per-request lane scratch (images with lane_need > LANE_WORDS)
   void* lane_blk = nullptr;
   size_t lane_cls = 0;
@@ -144,5 +149,15 @@ void dev_stream_destroy(void* stream);
 int dev_stream_sync(void* stream);
 // bench support: times `iters` launches of the evaluation kernel on `stream` with HIP events
 int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_total);
+// The same with an event at each phase boundary of every step: ms_phase[STEP_PHASES] (summed over
+// the iterations) and the steps' total. Phases: device grouping, index scan (the whole first pass
+// when it is one kernel), candidate pass, follow-up gather, and the three follow-up worklists.
+enum StepPhase : uint32_t { PH_GROUP = 0, PH_SCAN, PH_CAND, PH_GATHER, PH_FU_BIG, PH_FU_OVF, PH_FU_GEN, STEP_PHASES };
+int dev_time_split(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_phase, float* ms_total);
+// group.hip: the device grouping of a batch (rocPRIM radix sort of 32-bit grouping keys)
+size_t group_temp_bytes(uint32_t n);
+int group_enqueue(const uint32_t* rows, const uint32_t* heap, uint32_t n, uint32_t row_words, uint32_t n_hot,
+                  uint32_t* keys, uint32_t* keys2, uint32_t* vals, uint32_t* ord, void* temp, size_t temp_bytes,
+                  void* stream);
 
 }  // namespace cg

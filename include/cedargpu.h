@@ -183,6 +183,12 @@ int cg_batch_reasons(cg_batch* b, uint32_t i, uint32_t* idx, uint32_t cap, uint3
  * gather of unfinished requests and the on-device follow-up launches, exactly what
  * cg_batch_submit enqueues); device time via HIP events on the batch's stream. */
 int cg_batch_time(cg_batch* b, uint32_t iters, float* ms_total);
+/* The same with a HIP event at every phase boundary: ms_phase[7] receives each phase's device time
+ * summed over the iterations (0 device grouping, 1 index scan or the whole one-kernel first pass,
+ * 2 candidate pass, 3 follow-up gather, 4-6 the many-hit / long-list / structural follow-ups) and
+ * ms_total the steps' total. */
+#define CG_STEP_PHASES 7
+int cg_batch_time_split(cg_batch* b, uint32_t iters, float* ms_phase, float* ms_total);
 /* Requests of the batch whose result lists overflowed both the first pass and the on-device
  * follow-up and were re-run from the host by cg_batch_wait (diagnostic; valid once done). */
 int cg_batch_reruns(cg_batch* b, uint32_t* n);

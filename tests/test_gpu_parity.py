@@ -442,7 +442,7 @@ def check_items_ref(ctx, stores, items, want_indexed=None, entities=None):
     got = tiers.is_authorized_batch(items)
     ref = RefPolicySet.from_stores(stores, entities)
     ref.load_items(items_json(items))
-    want = ref.evaluate(8)
+    want = ref.evaluate(min(16, os.cpu_count() or 8))
     ref.close()
     for k, ((ok, diag), (wok, _, wdiag, _)) in enumerate(zip(got, want)):
         assert (ok, diag) == (wok, wdiag), (k, items[k][1], diag, wdiag)
@@ -494,6 +494,34 @@ def test_probe_kernel_abac_deep_group_dag(ctx):
     items = _dag_items(pop, 3200, 6)
     assert len(items) >= 3000
     check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
+
+
+def test_c3_full_size_dag(ctx):
+    """C3 at its stated size: 10k ABAC policies over the bench's 5k-group static DAG (depth <= 12,
+    synth.Population(seed=7, dag_depth=12), the population bench.py times) x >= 3k SARs vs the C++
+    oracle on decision and the full diagnostic. The user -> group edge of store_test.go:35-40 is
+    the one level of it the reference's own tests pin."""
+    pop = synth.Population(seed=7, dag_depth=12)
+    assert len(pop.groups) >= 5000
+    ents = pop.static_entities()
+    stores = [cedargpu.MemoryStore("c3.cedar", synth.abac_policies(10_000, seed=31, pop=pop))]
+    items = _dag_items(pop, 3300, 1000)
+    assert len(items) >= 3000
+    check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
+
+
+def test_c2_full_size_rbac(ctx):
+    """C2 at its stated size: 1k RBAC-converted policies plus the demo tier x 4k SARs vs the C++
+    oracle."""
+    pop = synth.Population(seed=8)
+    stores = [cedargpu.MemoryStore("c2.cedar", synth.rbac_policies(1000, seed=8, pop=pop)),
+              cedargpu.MemoryStore("demo.cedar", "\n".join(v for k, v in sorted(CORPUS["demo"].items())
+                                                           if k.startswith("authorization")))]
+    items = []
+    for s in synth.random_sars(4000, seed=9, pop=pop):
+        em, r = km.record_to_cedar_resource(km.attributes_from_sar(s))
+        items.append((co.entities_to_json(em), co.request_to_json(r)))
+    check_items_ref(ctx, stores, items, want_indexed=True)
 
 
 @pytest.mark.parametrize("chain", [20, 40, 70, 130])
