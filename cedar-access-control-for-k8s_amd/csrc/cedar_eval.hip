@@ -2326,7 +2326,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.lane_need = img.lane_need;
   d.cslot_mask = img.list_mask();
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
-  d.bmask = (uint32_t)(img.btab.size() / BT_WORDS) - 1;
+  d.bmask = img.btab_slots - 1;
   d.fmask = (uint32_t)(img.bfilt.size() / 2) - 1;
   d.indexed = img.indexed;
   d.combo_mask = img.combo_mask;
@@ -2337,6 +2337,52 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.n_tiers = img.n_tiers();
   d.n_gstr = img.n_gstr();
   d.n_hot = (uint32_t)img.hot.size() / HOT_WORDS;
+}
+
+// One thread per scope-index entry: claims the first free slot of its key's linear-probe chain
+// (compare-and-swap of the slot's first word, never 0 in a used slot) and writes the rest. Keys
+// are distinct, so any insertion order yields a table every probe (probe()) resolves alike.
+__global__ void __launch_bounds__(256) cedar_btab_build(const uint32_t* __restrict__ ent, uint32_t n,
+                                                        uint32_t* __restrict__ tab, uint32_t mask) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint4* e = reinterpret_cast<const uint4*>(ent + (size_t)i * BT_WORDS);
+  const uint4 a = e[0], b = e[1], c = e[2], d = e[3];
+  if (a.x == 0) return;  // the placeholder of an image without entries
+  const uint32_t combo = (a.x & ~BT_USED) >> 16;
+  uint32_t h = key_hash(combo, a.y, a.z, a.w, b.x, b.y, b.z);
+  if (a.x & BT_L2) h = bucket_hash2(h, a.x & 0xFFu & ~BT_L2, b.w, c.x);
+  for (h &= mask;; h = (h + 1) & mask)
+    if (atomicCAS(tab + (size_t)h * BT_WORDS, 0u, a.x) == 0u) break;
+  uint4* t = reinterpret_cast<uint4*>(tab + (size_t)h * BT_WORDS);
+  t[0] = make_uint4(a.x, a.y, a.z, a.w);
+  t[1] = b;
+  t[2] = c;
+  t[3] = d;
+}
+
+// Builds the image's slot table from its entry list (d.btab points at the list in the region).
+static int build_btab(const Image& img, DevImage& d) {
+  const size_t bytes = (size_t)img.btab_slots * BT_WORDS * 4;
+  const uint32_t n = (uint32_t)(img.btab.size() / BT_WORDS);
+  hipStream_t s;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  hipError_t e = hipMalloc(&d.btab_mem, bytes);
+  if (e == hipSuccess) e = hipMemsetAsync(d.btab_mem, 0, bytes, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(cedar_btab_build, dim3((n + 255) / 256), dim3(256), 0, s, d.btab, n, (uint32_t*)d.btab_mem, d.bmask);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+  if (e != hipSuccess) {
+    if (d.btab_mem) (void)hipFree(d.btab_mem);
+    d.btab_mem = nullptr;
+    return fail(e, "scope table build");
+  }
+  d.btab = (uint32_t*)d.btab_mem;
+  d.bytes += bytes;
+  return 0;
 }
 
 int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage* out) {
@@ -2351,6 +2397,7 @@ int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage
   }
   DevImage d;
   image_fields(img, device, base, img.dev_begin, d);
+  if (const int rc = build_btab(img, d)) { (void)hipFree(base); return rc; }
   *out = d;
   return 0;
 }
@@ -2369,13 +2416,16 @@ int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* 
   }
   DevImage d;
   image_fields(img, device, base, img.dev_begin, d);
+  if (const int rc = build_btab(img, d)) { (void)hipFree(base); return rc; }
   *out = d;
   return 0;
 }
 
 int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
   DevImage d;
   image_fields(img, device, dev_blob, 0, d);
+  if (const int rc = build_btab(img, d)) return rc;  // the caller still owns dev_blob on failure
   *out = d;
   return 0;
 }
@@ -2390,6 +2440,7 @@ void dev_image_free(DevImage* d) {
   if (d->device < 0) return;
   (void)hipSetDevice(d->device);
   if (d->base) (void)hipFree(d->base);
+  if (d->btab_mem) (void)hipFree(d->btab_mem);
   *d = DevImage();
 }
 

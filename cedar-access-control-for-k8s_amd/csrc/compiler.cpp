@@ -1034,6 +1034,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   img.indexed = (n > 0 && img.n_atomic == n) ? 1u : 0u;
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
+    img.btab_slots = 2;
     return;
   }
   static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
@@ -1216,12 +1217,11 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   uint32_t size = 16;
   while (size * 4 < 8 * n_entries) size <<= 1;
   while (size * 4 < slack * n_entries && (size_t)size * 2 * BT_WORDS * 4 <= (64u << 20)) size <<= 1;
-  img.btab.assign((size_t)size * BT_WORDS, 0);
-  auto insert = [&](uint32_t hash, const uint32_t* e) {
-    uint32_t h = hash & (size - 1);
-    while (img.btab[(size_t)h * BT_WORDS] != 0) h = (h + 1) & (size - 1);
-    std::copy(e, e + BT_WORDS, &img.btab[(size_t)h * BT_WORDS]);
-  };
+  // the entries only: the device inserts them into `size` slots at load (cedar_btab_build)
+  img.btab_slots = size;
+  img.btab.clear();
+  img.btab.reserve(std::max<size_t>(n_entries, 1) * BT_WORDS);
+  auto insert = [&](uint32_t, const uint32_t* e) { img.btab.insert(img.btab.end(), e, e + BT_WORDS); };
   auto l1_hash = [](const L1& k) { return key_hash(k[0], k[1], k[2], k[3], k[4], k[5], k[6]); };
   size_t blocks = 16;
   while (blocks * 4 < n_entries) blocks <<= 1;  // >= 16 bits per entry
@@ -1252,6 +1252,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     insert(bucket_hash2(l1_hash(k), x[0], x[1], x[2]), e);
     filt_add(bucket_hash2(l1_hash(k), x[0], x[1], x[2]));
   }
+  if (img.btab.empty()) img.btab.assign(BT_WORDS, 0);  // never empty buffers
   mark("heads+slots");
 }
 
@@ -1511,7 +1512,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.put64(table + 16 * DS_COUNT + 8, w.b.size());
   w.vec(pol); w.vec(tier_end); w.vec(code);
   w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
-  w.u32(pslot_mask); w.vec(pfx);
+  w.u32(pslot_mask); w.vec(pfx); w.u32(btab_slots);
   w.u32((uint32_t)key_ents.size());
   for (uint64_t k : key_ents) w.u64(k);
   w.u32((uint32_t)strings.size());
@@ -1561,11 +1562,14 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->cslot_mask = r.u32();
   img->pslot_mask = r.u32();
   img->pfx = r.vec();
+  img->btab_slots = r.u32();
   if (img->pfx.size() != (size_t)img->n_hot() * PFX_LENS && !(img->pfx.empty() && !img->pslot_mask))
     throw CedarError("corrupt image (prefix lengths)");
   {
-    const size_t nb = img->btab.size() / BT_WORDS, nf = img->bfilt.size();
-    if (!nb || (nb & (nb - 1)) || nf < 2 || (nf & (nf - 1))) throw CedarError("corrupt image (scope index)");
+    // entries < slots: every insertion finds a free slot and every probe chain ends at one
+    const size_t ne = img->btab.size() / BT_WORDS, nb = img->btab_slots, nf = img->bfilt.size();
+    if (!ne || img->btab.size() % BT_WORDS || nb < 2 || (nb & (nb - 1)) || ne >= nb || nf < 2 || (nf & (nf - 1)))
+      throw CedarError("corrupt image (scope index)");
   }
   if (img->lane_need > LANE_MAX) throw CedarError("corrupt image (lane scratch)");
   {

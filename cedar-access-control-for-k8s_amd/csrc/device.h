@@ -17,6 +17,7 @@ struct DevImage {
   uint32_t *pstream = nullptr, *tier_cend = nullptr, *chunks = nullptr, *cpool = nullptr, *gstr_off = nullptr, *hot = nullptr;
   uint32_t* act = nullptr;
   uint32_t *btab = nullptr, *bfilt = nullptr, *bstream = nullptr;  // scope index
+  void* btab_mem = nullptr;  // the slot table btab points to (built at load from the entry list)
   uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
   uint8_t* gstr_bytes = nullptr;
   // the one device allocation holding the image's device region (image.h DevSection); the arrays

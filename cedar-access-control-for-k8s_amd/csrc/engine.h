@@ -39,7 +39,11 @@ struct Image {
   uint32_t n_atomic = 0;      // policies compiled to atoms (statistics)
   uint32_t lane_need = 0;     // most lane-scratch words a bytecode policy uses (image.h LANE_MAX)
   // scope index over atomic policies (image.h "scope index"); indexed = every policy is atomic
+  // btab: the scope index's entries, BT_WORDS each (one all-zero entry when it has none). The
+  // open-addressed table of btab_slots slots (image.h "scope index") is built on the device from
+  // them at load (cedar_btab_build), so blobs and reload broadcasts carry no empty slots.
   std::vector<uint32_t> btab, bfilt, bstream;  // bfilt: key filter, 2 words per block
+  uint32_t btab_slots = 1;
   uint32_t indexed = 0;
   uint32_t combo_mask = 0;  // level-1 key combos in use (bit key_combo(..))
   // entity components of the scope index's level-1 keys, (type sid << 32 | id sid), sorted: the

@@ -124,7 +124,9 @@ constexpr uint32_t PW_EXT = PW_LANE;
 //            `has h` guard before it).
 // A request probes level 1 for its keys, then level 2 under each found key for every hot slot in
 // the entry's hmask, with its own value of that slot (or MISSING_W0).
-// btab: open addressing, linear probing, power-of-two slots of BT_WORDS:
+// btab (device): open addressing, linear probing, power-of-two slots of BT_WORDS, built at load
+// from the blob's compact entry list (Image::btab, Image::btab_slots) by inserting each entry at
+// its key's hash (l1: key_hash; l2: bucket_hash2 of it); slot layout:
 //   [BT_USED | combo << 16 | (BT_L2 | h for level 2), p type, p id, a type, a id, r type, r id,
 //    value w0 (level 1: cmask), value w1, first, count, hmask (level 1), l2 bloom x 4 (level 1)];
 //   empty: word0 == 0.
@@ -391,7 +393,7 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 8;
+constexpr uint32_t IMG_VERSION = 9;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob

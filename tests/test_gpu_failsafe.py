@@ -135,15 +135,13 @@ def test_queue_deadline_and_failsafe(ctx):
 
 
 def test_authorizer_deadline_under_stall(ctx):
-    """Authorizer(timeout=...) answers NoOpinion within its deadline while the device stalls: the
-    timed-out batch is retired without waiting for the stream (close() used to drain it)."""
+    """Authorizer(timeout=...) answers NoOpinion within its deadline while the device stalls, and
+    AdmissionHandler allows: the timed-out batch is retired without waiting for the stream (ADVICE
+    r02: close() used to drain it). Blocks of the retired batches return to the pool afterwards."""
     authz = cedargpu.Authorizer([cedargpu.MemoryStore("demo.cedar", DEMO_AUTHZ)], ctx=ctx, timeout=0.05)
     sars = _sars()
     want = _oracle(DEMO_AUTHZ, sars)
     assert authz.authorize_batch(sars) == want
-    handler = cedargpu.AdmissionHandler([cedargpu.MemoryStore("adm.cedar", DEMO_ADM), cedargpu.ALLOW_ALL_ADMISSION],
-                                        ctx=ctx, timeout=0.05)
-    reviews = synth.admission_reviews(16, seed=9)
     ctx.inject_fault(cedargpu.FAULT_STALL, 400_000)
     t0 = time.perf_counter()
     got = authz.authorize_batch(sars)
@@ -152,11 +150,25 @@ def test_authorizer_deadline_under_stall(ctx):
         name = s["spec"]["user"]
         fast = name.startswith("system:") and not name.startswith(("system:serviceaccount:", "system:node:"))
         assert g == (w if fast else (cedargpu.Authorizer.NO_OPINION, "")), s
-    ctx.inject_fault(cedargpu.FAULT_STALL, 400_000)
-    t0 = time.perf_counter()
-    assert handler.handle_batch(reviews) == [(True, 200, "")] * len(reviews)
-    assert time.perf_counter() - t0 < 0.2
     ctx.inject_fault(cedargpu.FAULT_NONE)
-    time.sleep(1.0)  # the stalled batches drain; their blocks are reaped by the next batch
+    time.sleep(0.6)  # the stalled batch drains; its blocks are reaped by the next batch
     authz.timeout = 5.0
     assert authz.authorize_batch(sars) == want
+    # admission on its own context (a handler's tiers activate their image on the context they use)
+    actx = cedargpu.Context(0)
+    try:
+        handler = cedargpu.AdmissionHandler([cedargpu.MemoryStore("adm.cedar", DEMO_ADM), cedargpu.ALLOW_ALL_ADMISSION],
+                                            ctx=actx, timeout=0.05)
+        reviews = synth.admission_reviews(16, seed=9)
+        normal = handler.handle_batch(reviews)
+        actx.inject_fault(cedargpu.FAULT_STALL, 400_000)
+        t0 = time.perf_counter()
+        assert handler.handle_batch(reviews) == [(True, 200, "")] * len(reviews)
+        assert time.perf_counter() - t0 < 0.2
+        actx.inject_fault(cedargpu.FAULT_NONE)
+        time.sleep(0.6)
+        handler.timeout = 5.0
+        assert handler.handle_batch(reviews) == normal
+    finally:
+        actx.inject_fault(cedargpu.FAULT_NONE)
+        actx.close()
