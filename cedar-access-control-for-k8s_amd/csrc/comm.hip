@@ -8,8 +8,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/cedargpu.h"
@@ -19,9 +22,39 @@ struct cg_comm {
   ncclComm_t nccl = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
+  bool aborted = false;  // a collective failed or timed out here: the communicator was aborted
 };
 
 static thread_local std::string g_comm_err;
+
+// Waits for the comm stream's collectives with a deadline, polling RCCL's asynchronous error. On
+// an error or past the deadline this rank aborts its communicator (ncclCommAbort): its own pending
+// collective ends and its resources are released, instead of a rank blocking forever inside a
+// broadcast a failed peer never joins. The communicator is unusable afterwards (recreate it).
+static bool comm_wait(cg_comm* c, int64_t timeout_ms, std::string& why) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(c->stream);
+    if (q == hipSuccess) return true;
+    ncclResult_t ae = ncclSuccess;
+    (void)ncclCommGetAsyncError(c->nccl, &ae);
+    const bool late = std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms);
+    if (q != hipErrorNotReady || (ae != ncclSuccess && ae != ncclInProgress) || late) {
+      why = q != hipErrorNotReady ? std::string("stream: ") + hipGetErrorString(q)
+            : late                ? std::string("collective timed out")
+                                  : std::string("RCCL: ") + ncclGetErrorString(ae);
+      (void)ncclCommAbort(c->nccl);
+      c->nccl = nullptr;
+      c->aborted = true;
+      return false;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+static int64_t comm_timeout_ms() {
+  static const int64_t t = [] { const char* e = std::getenv("CEDARGPU_COMM_TIMEOUT_MS"); return e ? (int64_t)std::atoll(e) : 60000; }();
+  return t;
+}
 
 extern "C" {
 
@@ -61,7 +94,7 @@ int cg_comm_create(int device, int nranks, int rank, const uint8_t* id, size_t l
 void cg_comm_destroy(cg_comm* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  if (c->nccl) (void)ncclCommDestroy(c->nccl);  // (an aborted communicator is already released)
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -80,7 +113,9 @@ const char* cg_comm_last_error(cg_comm* c) { return c ? c->err.c_str() : g_comm_
 int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, size_t len, uint64_t epoch, int activate,
                        size_t* out_len) {
   if (!ctx || !c || root < 0 || root >= c->nranks) return CG_E_ARG;
+  if (c->aborted || !c->nccl) { c->err = "communicator aborted by an earlier failure; recreate it"; return CG_E_STATE; }
   auto fail = [&](const std::string& m) { c->err = m; return CG_E_DEVICE; };
+  std::string why;
   if (hipSetDevice(c->device) != hipSuccess) return fail("hipSetDevice failed");
   // the root's length, or 0 when it has no blob: every rank then stops after this first collective
   uint64_t n = (c->rank == root && image) ? (uint64_t)len : 0;
@@ -89,10 +124,10 @@ int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, siz
   ncclResult_t r = ncclSuccess;
   bool ok = hipMemcpy(dn, &n, 8, hipMemcpyHostToDevice) == hipSuccess &&
             (r = ncclBroadcast(dn, dn, 8, ncclUint8, root, c->nccl, c->stream)) == ncclSuccess &&
-            hipStreamSynchronize(c->stream) == hipSuccess && hipMemcpy(&n, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
+            comm_wait(c, comm_timeout_ms(), why) && hipMemcpy(&n, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
   if (!ok) {
     (void)hipFree(dn);
-    return fail(std::string("length broadcast: ") + ncclGetErrorString(r));
+    return fail(std::string("length broadcast: ") + (why.empty() ? ncclGetErrorString(r) : why.c_str()));
   }
   if (n == 0) {
     (void)hipFree(dn);
@@ -107,17 +142,19 @@ int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, siz
   if (ready && c->rank == root && hipMemcpy(buf, image, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) ready = 0;
   ok = hipMemcpy(dn, &ready, 8, hipMemcpyHostToDevice) == hipSuccess &&
        (r = ncclAllReduce(dn, dn, 1, ncclUint64, ncclMin, c->nccl, c->stream)) == ncclSuccess &&
-       hipStreamSynchronize(c->stream) == hipSuccess && hipMemcpy(&ready, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
+       comm_wait(c, comm_timeout_ms(), why) && hipMemcpy(&ready, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
   (void)hipFree(dn);
   if (!ok || !ready) {
     if (buf) (void)hipFree(buf);
-    return fail(!ok ? std::string("readiness all-reduce: ") + ncclGetErrorString(r)
+    return fail(!ok ? std::string("readiness all-reduce: ") + (why.empty() ? ncclGetErrorString(r) : why.c_str())
                     : std::string("a rank could not allocate or stage the image buffer"));
   }
+  // a failure from here on (RCCL error, dead peer, timeout) aborts this rank's communicator
   r = ncclBroadcast(buf, buf, (size_t)n, ncclUint8, root, c->nccl, c->stream);
-  if (r != ncclSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+  if (r != ncclSuccess || !comm_wait(c, comm_timeout_ms(), why)) {
+    if (r != ncclSuccess && !c->aborted) { (void)ncclCommAbort(c->nccl); c->nccl = nullptr; c->aborted = true; }
     (void)hipFree(buf);
-    return fail(std::string("image broadcast: ") + ncclGetErrorString(r));
+    return fail(std::string("image broadcast: ") + (why.empty() ? ncclGetErrorString(r) : why.c_str()));
   }
   int rc = cg_image_load_device(ctx, buf, (size_t)n, epoch, c->rank == root ? image : nullptr);
   if (rc) {

@@ -150,7 +150,11 @@ int cg_comm_create(int device, int nranks, int rank, const uint8_t* id, size_t l
 void cg_comm_destroy(cg_comm* comm);
 const char* cg_comm_last_error(cg_comm* comm);
 /* Collective over comm: root's image (len bytes) is broadcast; every rank loads it into ctx as
- * `epoch` and activates it when activate != 0. *out_len (may be NULL) receives the blob size. */
+ * `epoch` and activates it when activate != 0. *out_len (may be NULL) receives the blob size.
+ * Failure keeps each rank's active image. A rank that cannot allocate makes every rank fail before
+ * the blob moves; an RCCL error, a dead peer or a collective past CEDARGPU_COMM_TIMEOUT_MS (60 s)
+ * aborts this rank's communicator (ncclCommAbort) and returns CG_E_DEVICE; later calls on it
+ * return CG_E_STATE until it is recreated. */
 int cg_broadcast_image(cg_ctx* ctx, cg_comm* comm, int root, const void* image, size_t len, uint64_t epoch,
                        int activate, size_t* out_len);
 
