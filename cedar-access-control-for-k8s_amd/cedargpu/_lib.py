@@ -126,6 +126,7 @@ _SIGS = {
     "cg_queue_authorize_sar": (ctypes.c_int, [P, cstr, sz, i64, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
     "cg_queue_is_authorized_json": (ctypes.c_int, [P, cstr, sz, i64, ctypes.POINTER(ctypes.c_int), P, sz,
                                                    ctypes.POINTER(sz)]),
+    "cg_queue_dropped": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
     "cg_queue_stats": (ctypes.c_int, [P] + [ctypes.POINTER(u64)] * 5),
     "cg_queue_loadgen": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), u32, u32, u64,
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u64),

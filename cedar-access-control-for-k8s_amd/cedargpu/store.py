@@ -526,7 +526,11 @@ class Queue:
         rc = lib.cg_queue_stats(self._h, *[ctypes.byref(x) for x in v])
         if rc:
             raise _err(rc, "queue stats failed")
-        return dict(zip(("batches", "requests", "fast", "max_batch", "device_ns"), (x.value for x in v)))
+        out = dict(zip(("batches", "requests", "fast", "max_batch", "device_ns"), (x.value for x in v)))
+        d = ctypes.c_uint64()
+        if lib.cg_queue_dropped(self._h, ctypes.byref(d)) == 0:
+            out["dropped"] = d.value
+        return out
 
     def loadgen(self, sars_json: Sequence[str], threads: int, total: int) -> dict:
         """Bench support: `threads` native threads issue `total` blocking authorize calls."""

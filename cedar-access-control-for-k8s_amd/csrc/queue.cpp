@@ -61,9 +61,14 @@ struct Ticket {
   std::shared_ptr<QBatch> qb;
   uint32_t idx = 0;
   std::atomic<uint32_t> ready{0};  // the request's batch is published
+  // T_QUEUED until the flusher takes the ticket into a batch (T_TAKEN), or the caller gives up
+  // first (T_ABANDONED: its deadline passed while it was still queued; the flusher drops it, so
+  // a stalled GPU's backlog is not evaluated for callers that already failed safe)
+  std::atomic<uint32_t> state{0};
   int rc = CG_OK;    // a request the batch could not take (error set, no batch)
   std::string err;
 };
+constexpr uint32_t T_QUEUED = 0, T_TAKEN = 1, T_ABANDONED = 2;
 
 constexpr uint32_t STRIPES = 16;
 
@@ -114,9 +119,19 @@ struct cg_queue {
   std::vector<std::unique_ptr<QWorker>> workers;
   std::mutex slot_mu;  // the flusher waits here for a submitter with room
   std::condition_variable slot_cv;
-  std::atomic<uint64_t> n_batches{0}, n_requests{0}, n_fast{0}, max_seen{0}, device_ns{0};
+  std::atomic<uint64_t> n_batches{0}, n_requests{0}, n_fast{0}, max_seen{0}, device_ns{0}, n_abandoned{0};
+  std::atomic<int64_t> stop_ns{0};  // when cg_queue_destroy began (steady clock)
 
   static constexpr uint32_t DEPTH = 2;  // batches per submitter: one running, the next queued
+
+  // cg_queue_destroy waits this long for the device to drain what was dealt, then fails the rest
+  // (CEDARGPU_QUEUE_STOP_GRACE_MS, default 2000): a hung GPU cannot block shutdown forever
+  static int64_t stop_grace_ns() {
+    static const int64_t g = [] { const char* e = std::getenv("CEDARGPU_QUEUE_STOP_GRACE_MS"); return (int64_t)(e ? std::atoll(e) : 2000) * 1000000; }();
+    return g;
+  }
+  bool stopping_too_long() const;
+  void fail_backlog(std::deque<std::shared_ptr<Ticket>>& backlog);
 
   void run();
   void work(QWorker& w);
@@ -128,6 +143,23 @@ struct cg_queue {
   }
 };
 
+bool cg_queue::stopping_too_long() const {
+  const int64_t t = stop_ns.load();
+  return t && now_ns() - t > stop_grace_ns();
+}
+
+void cg_queue::fail_backlog(std::deque<std::shared_ptr<Ticket>>& backlog) {
+  auto qb = std::make_shared<QBatch>();
+  qb->rc = CG_E_STATE;
+  qb->err = "queue closed before the request reached a device";
+  for (auto& t : backlog) {
+    uint32_t st = T_QUEUED;
+    if (t->state.compare_exchange_strong(st, T_TAKEN)) { t->qb = qb; qb->tickets.push_back(t); }
+  }
+  backlog.clear();
+  publish(*qb);
+}
+
 void cg_queue::work(QWorker& w) {
   // Pipelined: a batch dealt while the previous one runs is submitted before that one is waited
   // for, so its host side (string table, pinned staging, launch) overlaps the device work and its
@@ -136,10 +168,14 @@ void cg_queue::work(QWorker& w) {
   Clock::time_point busy_since{};    // device-busy accounting: the union of in-flight intervals
   auto finish = [&](std::shared_ptr<QBatch>& qb) {
     if (!qb->rc) {
-      const int rc = cg_batch_wait(qb->b, -1);
+      // no deadline while the queue runs; once it is closing, at most its grace (a hung device
+      // then fails the batch's callers and cg_queue_destroy returns)
+      int rc;
+      while ((rc = cg_batch_wait(qb->b, stop_ns.load() ? 10000000 : -1)) == CG_E_TIMEOUT && !stopping_too_long()) {
+      }
       if (rc) {
         qb->rc = rc;
-        qb->err = qb->b->err;
+        qb->err = rc == CG_E_TIMEOUT ? std::string("queue closed while the device had not finished the batch") : qb->b->err;
       }
     }
     const auto now = Clock::now();
@@ -228,7 +264,7 @@ void cg_queue::run() {
     // a submitter with room; while every one has a batch running and one queued, keep draining
     // (the next batch grows)
     QWorker* w = least();
-    while (w->load.load() >= DEPTH) {
+    while (w->load.load() >= DEPTH && !stopping_too_long()) {
       {
         std::unique_lock<std::mutex> g(slot_mu);
         // every submitter notifies when it frees a slot; the timeout only bounds a missed wake
@@ -248,6 +284,10 @@ void cg_queue::run() {
       if (it != w->ctx->images.end()) img = it->second;
     }
     if (img == enc && w->ctx != ctxs[0]) w = workers[0].get();
+    if (stopping_too_long()) {  // closing over a device that does not drain: fail what is left
+      fail_backlog(backlog);
+      return;
+    }
     auto qb = std::make_shared<QBatch>();
     qb->b = new cg_batch();
     qb->b->ctx = w->ctx;
@@ -256,6 +296,11 @@ void cg_queue::run() {
     while (!backlog.empty() && qb->b->items.size() < max_batch && backlog.front()->img == enc) {
       std::shared_ptr<Ticket> t = std::move(backlog.front());
       backlog.pop_front();
+      uint32_t st = T_QUEUED;
+      if (!t->state.compare_exchange_strong(st, T_TAKEN)) {  // its caller already returned
+        n_abandoned++;
+        continue;
+      }
       try {
         qb->b->host.append(t->e);
         qb->b->items.push_back({(int32_t)qb->b->host.n() - 1, -1});
@@ -312,7 +357,12 @@ int wait_ticket(cg_queue* q, const TicketP& tp, int64_t deadline, std::string& e
     int64_t rel = -1;
     if (deadline >= 0) {
       rel = deadline - now_ns();
-      if (rel <= 0) { err = "deadline exceeded waiting for the device batch"; return CG_E_TIMEOUT; }
+      if (rel <= 0) {
+        uint32_t st = T_QUEUED;  // still queued: the flusher will drop it rather than batch it
+        (void)t.state.compare_exchange_strong(st, T_ABANDONED);
+        err = "deadline exceeded waiting for the device batch";
+        return CG_E_TIMEOUT;
+      }
     }
     futex_wait(&q->pub, w, rel);
   }
@@ -391,6 +441,7 @@ int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_q
 
 void cg_queue_destroy(cg_queue* q) {
   if (!q) return;
+  q->stop_ns.store(now_ns());
   q->stop.store(true);
   q->pending.fetch_add(1);  // wakes the flusher, which deals what it holds and returns
   q->pending.notify_one();
@@ -478,6 +529,12 @@ int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t*
   if (fast) *fast = q->n_fast.load();
   if (max_batch) *max_batch = q->max_seen.load();
   if (device_ns) *device_ns = q->device_ns.load();
+  return CG_OK;
+}
+
+int cg_queue_dropped(cg_queue* q, uint64_t* abandoned) {
+  if (!q || !abandoned) return CG_E_ARG;
+  *abandoned = q->n_abandoned.load();
   return CG_OK;
 }
 

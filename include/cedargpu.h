@@ -280,6 +280,9 @@ int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, 
  * nanoseconds the flusher spent in submit + wait. Any pointer may be NULL. */
 int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,
                    uint64_t* device_ns);
+/* Requests the queue dropped unevaluated because their callers' deadlines passed while they still
+ * waited for a batch (the callers already returned CG_E_TIMEOUT and failed safe). */
+int cg_queue_dropped(cg_queue* q, uint64_t* abandoned);
 /* Bench support: `threads` threads issue `total` blocking cg_queue_authorize_sar calls cycling
  * over sars[0..n); wall seconds, per-call latency p50/p99/max (ns) and decision counts
  * counts[0..3) = (Deny, Allow, NoOpinion). */

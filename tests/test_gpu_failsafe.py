@@ -122,9 +122,16 @@ def test_queue_deadline_and_failsafe(ctx):
             q.is_authorized(co.entities_to_json(em), co.request_to_json(r), timeout=0.05)
         # fast paths answer on the caller's thread, inside any deadline
         assert q.authorize(sars[-3], timeout=0.0) == want[-3]
+        # two batches now hold the stalled device (one running, one queued); requests behind them
+        # wait in the backlog, time out there and are dropped unevaluated (Ticket T_ABANDONED)
+        slow = [s for s in sars if not s["spec"]["user"].startswith("system:")][:6]
+        for s in slow:
+            with pytest.raises(cedargpu.DeadlineError):
+                q.authorize(s, timeout=0.02)
         ctx.inject_fault(cedargpu.FAULT_NONE)
-        time.sleep(0.5)  # the stalled batches drain
+        time.sleep(1.5)  # the stalled batches drain
         assert [q.authorize(s, timeout=5.0) for s in sars] == want
+        assert q.stats()["dropped"] >= 1
         ctx.inject_fault(cedargpu.FAULT_DEVICE_ERROR, 1)
         got = q.authorize_failsafe(sars[-1], timeout=5.0)
         assert got == (cedargpu.Authorizer.NO_OPINION, "")
