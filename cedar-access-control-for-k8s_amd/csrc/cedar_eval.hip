@@ -1516,14 +1516,9 @@ __device__ __forceinline__ uint2 key_comp(uint32_t kc, uint32_t j, uint32_t st, 
 
 // key filter: false = the key is certainly absent from the scope index
 __device__ __forceinline__ bool filt_maybe(const uint32_t* bfilt, uint32_t fmask, uint32_t hash) {
-  const uint32_t y = filt_mix(hash), bits = filt_bits(y);
-  const uint2 w = *reinterpret_cast<const uint2*>(bfilt + 2 * (size_t)(y & fmask));
-  bool ok = true;
-  for (uint32_t j = 0; j < 3; j++) {
-    const uint32_t b = (bits >> (6 * j)) & 63u;
-    ok = ok && (((b < 32 ? w.x : w.y) >> (b & 31)) & 1u);
-  }
-  return ok;
+  const uint2 w = *reinterpret_cast<const uint2*>(bfilt + 2 * (size_t)(hash & fmask));
+  const uint64_t need = filt_need(hash);
+  return ((((uint64_t)w.y << 32) | w.x) & need) == need;
 }
 
 // probe: (first, count, hmask) of the slot matching key words w0..w6 (+ v0, v1 for level 2)
@@ -1587,7 +1582,15 @@ __device__ __forceinline__ bool l2_bloom_maybe(uint4 b, uint32_t h2) {
 constexpr uint32_t SCAN_ANC = 40;
 // key-filter pass: keys per lane per round (independent loads in flight), and the filter-passing
 // keys a request lists in LDS (more: it probes every key, as with the filter off)
-constexpr uint32_t SCAN_PU = 8, SCAN_POS = 64;
+constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
+// combos whose action / resource component keys on the entity (image.h key_combo)
+constexpr uint32_t combo_mask_of(uint32_t k, uint32_t shift, uint32_t mask) {
+  uint32_t m = 0;
+  for (uint32_t cb = 0; cb < 32; cb++)
+    if (((cb >> shift) & mask) == k) m |= 1u << cb;
+  return m;
+}
+constexpr uint32_t COMBO_AENT = combo_mask_of(KC_ENT, 2, 1), COMBO_RENT = combo_mask_of(KC_ENT, 3, 3);
 template <uint32_t SEG, uint32_t MINW = 1>
 __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // per request: its first SCAN_ANC key ancestors and its hot values, loaded in one round trip
@@ -1595,7 +1598,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // with a dependent HBM load)
   __shared__ uint2 s_anc[64 / SEG][SCAN_ANC];
   __shared__ uint2 s_hot[64 / SEG][NHOT];
-  __shared__ uint16_t s_pos[64 / SEG][SCAN_POS];
+  __shared__ uint32_t s_pos[64 / SEG][SCAN_POS];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
@@ -1656,77 +1659,75 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     r = key_comp(rkc, ir + 1 - (rn >> 31), rt, ri, blk, r_anc);
     cbo = combo;
   };
-  // the same from registers and LDS only; false (components not set) when a component is an
-  // ancestor that lives in the request block (the filter pass then lets the key through unread:
-  // a global load there would make every filter load before it wait)
-  auto key_at_reg = [&](uint32_t k, uint32_t& cbo, uint2& p, uint2& q, uint2& r) -> bool {
-    uint32_t j = k, combo = 0;
-    bool found = false;
-    for (uint32_t m = cm; m; m &= m - 1) {
-      const uint32_t cb = __builtin_ctz(m);
-      const uint32_t cnt = ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
-      if (!found) {
-        if (j < cnt) { combo = cb; found = true; }
-        else j -= cnt;
-      }
-    }
-    const uint32_t pkc = combo & 3, akc = (combo >> 2) & 1, rkc = combo >> 3;
-    const uint32_t np_ = pkc == KC_ENT ? nP : 1u, na_ = akc == KC_ENT ? nA : 1u;
-    uint32_t ip = j, ia = 0, ir = 0;
-    if (na_ != 1u || (rkc == KC_ENT && nR != 1u)) {
-      const uint32_t t2 = j / np_;
-      ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
-    }
-    const uint32_t jp = ip + 1 - (pn >> 31), ja = ia + 1 - (an >> 31), jr = ir + 1 - (rn >> 31);
-    if ((pkc == KC_ENT && jp && !(stl && jp <= SCAN_ANC)) || (akc == KC_ENT && ja) || (rkc == KC_ENT && jr)) return false;
-    p = (pkc == KC_ENT && jp) ? s_anc[seg][jp - 1] : key_comp(pkc, 0, pt, pi, blk, p_anc);
-    q = key_comp(akc, 0, at, ai, blk, a_anc);
-    r = key_comp(rkc, 0, rt, ri, blk, r_anc);
-    cbo = combo;
+  // Key-filter pass. When every used combo's action / resource component is the request's own UID,
+  // its one key ancestor, its type or a wildcard (nA, nR <= 1: the k8s SAR shape), a combo's keys
+  // are its principal components alone: the (combo, action, resource) prefix of the key hash is
+  // computed once per combo, each principal key ancestor (staged in LDS) costs two multiply steps
+  // and a finalizer, and SEG * SCAN_PU filter blocks (a few hundred KB that stay in L2) are in
+  // flight per round. Keys the filter passes are listed as (combo << 16 | principal index) and
+  // only they probe the scope table's 64-byte slots below (~6 of ~62 on C3's group DAG).
+  const uint32_t simple = valid && (!(cm & COMBO_AENT) || nA <= 1u) && (!(cm & COMBO_RENT) || nR <= 1u) && nP <= 0xFFFFu;
+  // the request's action / resource key component for combos that key on the entity (one of them)
+  const uint2 ka1 = (simple && nA == 1u) ? key_comp(KC_ENT, 1u - (an >> 31), at, ai, blk, a_anc) : make_uint2(KW_ANY, KW_ANY);
+  const uint2 kr1 = (simple && nR == 1u) ? key_comp(KC_ENT, 1u - (rn >> 31), rt, ri, blk, r_anc) : make_uint2(KW_ANY, KW_ANY);
+  auto comb_q = [&](uint32_t cb) { return ((cb >> 2) & 1) == KC_ENT ? ka1 : make_uint2(KW_ANY, KW_ANY); };
+  auto comb_r = [&](uint32_t cb) {
+    const uint32_t rkc = cb >> 3;
+    return rkc == KC_ENT ? kr1 : (rkc == KC_TYPE ? make_uint2(rt, KW_ANY) : make_uint2(KW_ANY, KW_ANY));
+  };
+  // keys of combo cb for this request, and its principal component ip (false: not in LDS)
+  auto comb_cnt = [&](uint32_t cb) -> uint32_t {
+    return ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
+  };
+  auto comb_p_lds = [&](uint32_t cb, uint32_t ip, uint2& p) -> bool {
+    const uint32_t pkc = cb & 3;
+    if (pkc != KC_ENT) { p = key_comp(pkc, 0u, pt, pi, blk, p_anc); return true; }
+    const uint32_t jp = ip + 1 - (pn >> 31);  // 0: the principal itself, j: ancestor j - 1
+    if (!jp) { p = make_uint2(pt, pi); return true; }
+    if (!stl || jp > SCAN_ANC) return false;
+    p = s_anc[seg][jp - 1];
     return true;
   };
-  // Key-filter pass: every level-1 key's filter block is loaded up front (SCAN_PU independent
-  // small loads per lane in flight, from a table of ~16 bits per index entry that stays in L2),
-  // and only the keys the filter passes are probed below. The scope table's 64-byte slots are
-  // then touched ~once per found key instead of once per enumerated key (~62 on C3's group DAG,
-  // of which ~6 exist), and those probes leave in one step instead of one per SEG keys.
   uint32_t npos = 0;
   if (a.scan_filt) {
-    for (uint32_t rb = 0; __ballot(valid && rb < n_keys) != 0; rb += SEG * SCAN_PU) {
-      uint2 fw[SCAN_PU];
-      uint32_t fy[SCAN_PU];
+    for (uint32_t m = cm; m; m &= m - 1) {  // wave-uniform: the image's combos
+      const uint32_t cb = __builtin_ctz(m);
+      const uint32_t cnt = simple ? comb_cnt(cb) : 0u;
+      if (__ballot(cnt != 0) == 0) continue;
+      const uint2 q = comb_q(cb), r = comb_r(cb);
+      const uint32_t pre = key_pre(cb, q.x, q.y, r.x, r.y);
+      for (uint32_t rb = 0; __ballot(rb < cnt) != 0; rb += SEG * SCAN_PU) {
+        uint2 fw[SCAN_PU];
+        uint32_t fh[SCAN_PU];
 #pragma unroll
-      for (uint32_t u = 0; u < SCAN_PU; u++) {
-        const uint32_t k = rb + u * SEG + sl;
-        fw[u] = make_uint2(~0u, ~0u);  // keys not tested pass
-        fy[u] = 0;
-        uint32_t cb;
-        uint2 p, q, r;
-        if (valid && k < n_keys && key_at_reg(k, cb, p, q, r)) {
-          const uint32_t y = filt_mix(key_hash(cb, p.x, p.y, q.x, q.y, r.x, r.y));
-          fy[u] = y;
-          fw[u] = *reinterpret_cast<const uint2*>(a.bfilt + 2 * (size_t)(y & a.fmask));
+        for (uint32_t u = 0; u < SCAN_PU; u++) {
+          const uint32_t ip = rb + u * SEG + sl;
+          fw[u] = make_uint2(~0u, ~0u);  // a key not tested (its component is not in LDS) passes
+          fh[u] = 0;
+          uint2 p;
+          if (ip < cnt && comb_p_lds(cb, ip, p)) {
+            const uint32_t h = key_fin(pre, p.x, p.y);
+            fh[u] = h;
+            fw[u] = *reinterpret_cast<const uint2*>(a.bfilt + 2 * (size_t)(h & a.fmask));
+          }
         }
-      }
 #pragma unroll
-      for (uint32_t u = 0; u < SCAN_PU; u++) {
-        const uint32_t k = rb + u * SEG + sl;
-        const uint32_t bits = filt_bits(fy[u]);
-        const uint64_t w = ((uint64_t)fw[u].y << 32) | fw[u].x;  // (a select between the words
-        // would index the array dynamically and put it in scratch)
-        const uint64_t need = (1ull << (bits & 63u)) | (1ull << ((bits >> 6) & 63u)) | (1ull << ((bits >> 12) & 63u));
-        const bool ok = valid && k < n_keys && (w & need) == need;
-        const uint64_t m = sballot(ok);
-        const uint32_t at_ = npos + mbcnt64(m);
-        if (ok && at_ < SCAN_POS) s_pos[seg][at_] = (uint16_t)k;
-        npos += popc64(m);
+        for (uint32_t u = 0; u < SCAN_PU; u++) {
+          const uint32_t ip = rb + u * SEG + sl;
+          const uint64_t need = filt_need(fh[u]);
+          const bool ok = ip < cnt && ((((uint64_t)fw[u].y << 32) | fw[u].x) & need) == need;
+          const uint64_t mk = sballot(ok);
+          const uint32_t at_ = npos + mbcnt64(mk);
+          if (ok && at_ < SCAN_POS) s_pos[seg][at_] = (cb << 16) | ip;
+          npos += popc64(mk);
+        }
       }
     }
     wave_lds_sync();
   }
-  // a request with more filter-passing keys than the list holds (or keys past its 16-bit
-  // indices) enumerates them all
-  const bool flt = a.scan_filt && npos <= SCAN_POS && n_keys <= 0x10000u;
+  // a request off the simple shape, or with more filter-passing keys than the list holds,
+  // enumerates every key instead
+  const bool flt = a.scan_filt && simple && npos <= SCAN_POS;
   const uint32_t n_l1 = flt ? npos : n_keys;
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
@@ -1781,7 +1782,15 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         const uint32_t kk = kb + sl;
         kb += SEG;
         if (kk < n_l1) {
-          key_at(flt ? s_pos[seg][kk] : kk, combo, kp, ka, kr);
+          if (flt) {
+            const uint32_t x = s_pos[seg][kk];
+            combo = x >> 16;
+            if (!comb_p_lds(combo, x & 0xFFFFu, kp)) kp = key_comp(KC_ENT, (x & 0xFFFFu) + 1 - (pn >> 31), pt, pi, blk, p_anc);
+            ka = comb_q(combo);
+            kr = comb_r(combo);
+          } else {
+            key_at(kk, combo, kp, ka, kr);
+          }
           w0 = BT_USED | (combo << 16);
           h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
           uint32_t cmv = 0;

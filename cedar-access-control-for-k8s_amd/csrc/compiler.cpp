@@ -1227,12 +1227,10 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   while (blocks * 4 < n_entries) blocks <<= 1;  // >= 16 bits per entry
   img.bfilt.assign(2 * blocks, 0);
   auto filt_add = [&](uint32_t hash) {
-    const uint32_t y = filt_mix(hash), bits = filt_bits(y);
-    const size_t blk = y & (blocks - 1);
-    for (uint32_t j = 0; j < 3; j++) {
-      const uint32_t b = (bits >> (6 * j)) & 63u;
-      img.bfilt[2 * blk + (b >> 5)] |= 1u << (b & 31);
-    }
+    const uint64_t need = filt_need(hash);
+    const size_t blk = hash & (blocks - 1);
+    img.bfilt[2 * blk] |= (uint32_t)need;
+    img.bfilt[2 * blk + 1] |= (uint32_t)(need >> 32);
   };
   mark("tables");
   for (const G& g : g1) {

@@ -142,16 +142,26 @@ constexpr uint32_t KC_WILD = 0, KC_ENT = 1, KC_TYPE = 2;  // component kinds
 __host__ __device__ constexpr inline uint32_t key_combo(uint32_t pk, uint32_t ak, uint32_t rk) { return pk | (ak << 2) | (rk << 3); }
 constexpr uint32_t KW_ANY = 0xFFFFFFFFu;  // id of a type-only component; both words of a wildcard
 constexpr uint32_t BT_WORDS = 16, BT_USED = 0x80000000u, BT_L2 = 0x100, HEAD_WORDS = 32, HEAD_ATOMS = 4;
-__host__ __device__ constexpr inline uint32_t key_hash(uint32_t combo, uint32_t pt, uint32_t pi, uint32_t at, uint32_t ai,
-                                                       uint32_t rt, uint32_t ri) {
-  uint32_t h = combo * 0x9E3779B1u;
-  h = (h ^ pt) * 0x85EBCA77u; h = (h ^ pi) * 0xC2B2AE3Du;
-  h = (h ^ at) * 0x27D4EB2Fu; h = (h ^ ai) * 0x165667B1u;
-  h = (h ^ rt) * 0xD3A2646Cu; h = (h ^ ri) * 0xFD7046C5u;
+// key_hash = key_fin(key_pre(combo, action, resource), principal): the principal component is
+// mixed last, so a request hashes the (combo, action, resource) prefix once per combo and each of
+// its ~30 principal key ancestors in two multiply steps and a finalizer (cedar_scan_kernel).
+__host__ __device__ constexpr inline uint32_t key_pre(uint32_t combo, uint32_t at, uint32_t ai, uint32_t rt, uint32_t ri) {
+  uint32_t h = (combo + 1) * 0x9E3779B1u;
+  h = (h ^ at) * 0x85EBCA77u; h = (h ^ ai) * 0xC2B2AE3Du;
+  h = (h ^ rt) * 0x27D4EB2Fu; h = (h ^ ri) * 0x165667B1u;
+  return h;
+}
+__host__ __device__ constexpr inline uint32_t key_fin(uint32_t pre, uint32_t pt, uint32_t pi) {
+  uint32_t h = (pre ^ pt) * 0xD3A2646Du;
+  h = (h ^ pi) * 0xFD7046C5u;
   h ^= h >> 16;
   h *= 0x7FEB352Du;
   h ^= h >> 15;
   return h;
+}
+__host__ __device__ constexpr inline uint32_t key_hash(uint32_t combo, uint32_t pt, uint32_t pi, uint32_t at, uint32_t ai,
+                                                       uint32_t rt, uint32_t ri) {
+  return key_fin(key_pre(combo, at, ai, rt, ri), pt, pi);
 }
 __host__ __device__ constexpr inline uint32_t bucket_hash2(uint32_t l1, uint32_t hslot, uint32_t v0, uint32_t v1) {
   uint32_t h = l1 ^ ((hslot + 1) * 0x27D4EB2Fu) ^ (v0 * 0x165667B1u) ^ (v1 * 0xD3A2646Cu);
@@ -166,17 +176,16 @@ __host__ __device__ constexpr inline uint32_t l2_bloom_bits(uint32_t h2) {  // t
   return (y >> 11) & 0x1FFFFFu;
 }
 // Key filter of the scope index (bfilt): a blocked Bloom filter over the level-1 and level-2 key
-// hashes, 3 bits in one 64-bit block (two words) per key, about 16 bits per entry. Most probes
-// miss (a request enumerates ~11 level-1 keys and finds ~0.3), and a miss then costs one small,
-// cache-resident load instead of a walk over 64-byte table slots.
-__host__ __device__ constexpr inline uint32_t filt_mix(uint32_t x) {
-  x ^= 0x5BD1E995u;
-  x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
-  return x;
+// hashes, 3 bits in one 64-bit block (two words) per key, about 16 bits per entry: a few hundred KB
+// that stay in L2. The block is the hash's low bits (h & fmask); the bit positions come from the
+// top of h * φ, so a test costs one multiply beyond the key hash.
+__host__ __device__ constexpr inline uint32_t filt_bits(uint32_t h) {  // b0 | b1 << 6 | b2 << 12
+  const uint32_t y = h * 0x9E3779B1u;
+  return (y >> 26) | (((y >> 20) & 63u) << 6) | (((y >> 14) & 63u) << 12);
 }
-// bits (b0 | b1 << 6 | b2 << 12) of hash x's 64-bit block
-__host__ __device__ constexpr inline uint32_t filt_bits(uint32_t y) {
-  return ((y >> 14) & 63u) | (((y >> 20) & 63u) << 6) | (((y * 0x9E3779B1u) >> 26) << 12);
+__host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 bits as a 64-bit mask
+  const uint32_t b = filt_bits(h);
+  return (1ull << (b & 63u)) | (1ull << ((b >> 6) & 63u)) | (1ull << ((b >> 12) & 63u));
 }
 
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
