@@ -1461,19 +1461,24 @@ struct SegLds {
   // error details per request (more: the on-device follow-up, which holds 32; more still: the
   // stream kernel). 32 keeps the large stage's 4-wave block under 53 KB: 3 blocks per CU
   static constexpr uint32_t XC = HCAP >= 256 ? 32 : 8;
+  // Rows are not padded off the 64 LDS banks: the segments of a wave that touch element j of their
+  // rows in lockstep conflict (SQ_LDS_BANK_CONFLICT is ~1/3 of SQ_LDS_IDX_ACTIVE here), but those
+  // cycles are ~0.3 % of the kernel's wave cycles, and one padding word per row would take the
+  // 4-wave SPLIT candidate pass from 10,240 to 10,496 B per block, past 16 blocks per CU.
+  static constexpr uint32_t PAD = 0;
   // the staged buckets live until the key loop ends, the merge's sort keys only after it: one region
   union {
     struct {
-      uint32_t efirst[NS][EC];   // found bucket: first head index
-      uint32_t epre[NS][EC];     // candidate counts, then their exclusive prefix
-      uint32_t ecombo[NS][EC];   // key combo of the bucket's level-1 key
+      uint32_t efirst[NS][EC + PAD];   // found bucket: first head index
+      uint32_t epre[NS][EC + PAD];     // candidate counts, then their exclusive prefix
+      uint32_t ecombo[NS][EC + PAD];   // key combo of the bucket's level-1 key
     } b;
-    uint32_t hs[NS][HC];         // merge: sort keys (policy index << 12 | hit slot)
+    uint32_t hs[NS][HC + PAD];         // merge: sort keys (policy index << 12 | hit slot)
   } u;
-  uint32_t hp[NS][HC];       // hit: global policy index
-  uint32_t hm[NS][HC];       // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
-  uint32_t he[NS][XC * 4];   // error details: code | aux << 8, k, et, ei
-  uint2 hot[NS][NHOT];
+  uint32_t hp[NS][HC + PAD];       // hit: global policy index
+  uint32_t hm[NS][HC + PAD];       // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
+  uint32_t he[NS][XC * 4 + PAD];   // error details: code | aux << 8, k, et, ei
+  uint2 hot[NS][NHOT + PAD];
 };
 
 // Slim per-request context of the probe kernel (everything wave-uniform but the pointers' data).
@@ -1596,9 +1601,10 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // per request: its first SCAN_ANC key ancestors and its hot values, loaded in one round trip
   // before the key loop (the request block and row are cold: each key step would otherwise start
   // with a dependent HBM load)
-  __shared__ uint2 s_anc[64 / SEG][SCAN_ANC];
-  __shared__ uint2 s_hot[64 / SEG][NHOT];
-  __shared__ uint32_t s_pos[64 / SEG][SCAN_POS];
+  // rows padded off a multiple of the 64 LDS banks: the segments of a wave index them in lockstep
+  __shared__ uint2 s_anc[64 / SEG][SCAN_ANC + 1];
+  __shared__ uint2 s_hot[64 / SEG][NHOT + 1];
+  __shared__ uint32_t s_pos[64 / SEG][SCAN_POS + 1];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
