@@ -84,7 +84,10 @@ struct KArgs {
   uint32_t l2filt;  // level-2 probes too, after the level-1 entry's own bloom (CEDARGPU_L2_FILTER)
   uint32_t slot_split;  // probes load a slot's first 16 B, the rest only on a key match (CEDARGPU_SLOT_SPLIT)
   uint32_t scan_lds;    // the scan stages key ancestors and hot values in LDS up front (CEDARGPU_SCAN_LDS)
-  uint32_t scan_filt;   // the scan tests every level-1 key against the key filter first (CEDARGPU_SCAN_FILT)
+  uint32_t scan_filt;   // the scan tests principal keys against the scope bitsets first (CEDARGPU_SCAN_FILT)
+  const uint32_t* __restrict__ sctx;   // scope bitsets (image.h): context table, rows
+  const uint32_t* __restrict__ sbits;
+  uint32_t sctx_mask, sbits_words;     // sbits_words 0: the image has none
   uint32_t scan_big;    // more scanned buckets than this: straight to the large stage (CEDARGPU_SCAN_BIG)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
@@ -1602,9 +1605,14 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // before the key loop (the request block and row are cold: each key step would otherwise start
   // with a dependent HBM load)
   // rows padded off a multiple of the 64 LDS banks: the segments of a wave index them in lockstep
-  __shared__ uint2 s_anc[64 / SEG][SCAN_ANC + 1];
+  // (an image with scope bitsets stages the ancestors' key-entity indices instead of their UIDs)
+  __shared__ union {
+    uint2 anc[64 / SEG][SCAN_ANC + 1];
+    uint32_t kid[64 / SEG][SCAN_ANC + 2];  // [0]: the principal itself, [j]: key ancestor j - 1
+  } s_st;
+  auto& s_anc = s_st.anc;
   __shared__ uint2 s_hot[64 / SEG][NHOT + 1];
-  __shared__ uint32_t s_pos[64 / SEG][SCAN_POS + 1];
+  __shared__ uint16_t s_pos[64 / SEG][SCAN_POS + 2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
@@ -1631,11 +1639,21 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
     }
   uint32_t* pairs = a.scan + a.scan_n + (size_t)gid * (2 * SCAN_CAP);
-  const bool stl = a.scan_lds != 0;
-  if (stl) {
-    const uint32_t n_st = valid ? min((pn >> AN_KEYS_SHIFT) & AN_KEYS, SCAN_ANC) : 0u;
-    for (uint32_t j = sl; j < n_st; j += SEG)
-      s_anc[seg][j] = make_uint2(__builtin_nontemporal_load(blk + p_anc + 2 * j), __builtin_nontemporal_load(blk + p_anc + 2 * j + 1));
+  // scope-bitset pass (image.h "scope bitsets"): the principal's list carries the kidx of its owner
+  // and key ancestors after its pairs (p_anc == 0: the principal has no entity, no list)
+  const bool kbits = a.scan_filt && a.sbits_words != 0;
+  const bool klist = kbits && valid && p_anc != 0;
+  const bool stl = a.scan_lds != 0 && !kbits;  // UIDs in LDS (no bitsets) for the key loop
+  {
+    const uint32_t nk = (pn >> AN_KEYS_SHIFT) & AN_KEYS;
+    if (stl) {
+      const uint32_t n_st = valid ? min(nk, SCAN_ANC) : 0u;
+      for (uint32_t j = sl; j < n_st; j += SEG)
+        s_anc[seg][j] = make_uint2(__builtin_nontemporal_load(blk + p_anc + 2 * j), __builtin_nontemporal_load(blk + p_anc + 2 * j + 1));
+    } else if (klist) {
+      const uint32_t* kl = blk + p_anc + 2 * (pn & AN_COUNT);
+      for (uint32_t j = sl; j <= min(nk, SCAN_ANC); j += SEG) s_st.kid[seg][j] = __builtin_nontemporal_load(kl + j);
+    }
     for (uint32_t h = sl; h < a.n_hot; h += SEG)
       s_hot[seg][h] = valid ? *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h) : make_uint2(0u, 0u);
     wave_lds_sync();
@@ -1665,15 +1683,15 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     r = key_comp(rkc, ir + 1 - (rn >> 31), rt, ri, blk, r_anc);
     cbo = combo;
   };
-  // Key-filter pass. When every used combo's action / resource component is the request's own UID,
-  // its one key ancestor, its type or a wildcard (nA, nR <= 1: the k8s SAR shape), a combo's keys
-  // are its principal components alone: the (combo, action, resource) prefix of the key hash is
-  // computed once per combo, each principal key ancestor (staged in LDS) costs two multiply steps
-  // and a finalizer, and SEG * SCAN_PU filter blocks (a few hundred KB that stay in L2) are in
-  // flight per round. Keys the filter passes are listed as (combo << 16 | principal index) and
-  // only they probe the scope table's 64-byte slots below (~6 of ~62 on C3's group DAG).
-  const uint32_t simple = valid && (!(cm & COMBO_AENT) || nA <= 1u) && (!(cm & COMBO_RENT) || nR <= 1u) && nP <= 0xFFFFu;
-  // the request's action / resource key component for combos that key on the entity (one of them)
+  // Scope-bitset pass. When every used combo's action / resource component is the request's own
+  // UID, its one key ancestor, its type or a wildcard (nA, nR <= 1: the k8s SAR shape), a combo
+  // whose principal component is an entity has one context (combo, action, resource): one lookup in
+  // the small context table gives its bitset row, and each of the principal's key ancestors costs
+  // one bit test in that row (kidx staged in LDS; the grouped requests of a wave share the row).
+  // Only keys whose bit is set, and the single keys of the other combos, are listed (as
+  // combo << 11 | principal index) and probe the scope table's 64-byte slots below: ~6 of ~62 per
+  // request on C3's group DAG instead of all of them.
+  const uint32_t simple = valid && (!(cm & COMBO_AENT) || nA <= 1u) && (!(cm & COMBO_RENT) || nR <= 1u) && nP < 2048u;
   const uint2 ka1 = (simple && nA == 1u) ? key_comp(KC_ENT, 1u - (an >> 31), at, ai, blk, a_anc) : make_uint2(KW_ANY, KW_ANY);
   const uint2 kr1 = (simple && nR == 1u) ? key_comp(KC_ENT, 1u - (rn >> 31), rt, ri, blk, r_anc) : make_uint2(KW_ANY, KW_ANY);
   auto comb_q = [&](uint32_t cb) { return ((cb >> 2) & 1) == KC_ENT ? ka1 : make_uint2(KW_ANY, KW_ANY); };
@@ -1681,59 +1699,70 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     const uint32_t rkc = cb >> 3;
     return rkc == KC_ENT ? kr1 : (rkc == KC_TYPE ? make_uint2(rt, KW_ANY) : make_uint2(KW_ANY, KW_ANY));
   };
-  // keys of combo cb for this request, and its principal component ip (false: not in LDS)
   auto comb_cnt = [&](uint32_t cb) -> uint32_t {
     return ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
   };
-  auto comb_p_lds = [&](uint32_t cb, uint32_t ip, uint2& p) -> bool {
+  // principal component ip of a combo's keys (0: the UID itself when it is a key entity)
+  auto comb_p = [&](uint32_t cb, uint32_t ip) -> uint2 {
     const uint32_t pkc = cb & 3;
-    if (pkc != KC_ENT) { p = key_comp(pkc, 0u, pt, pi, blk, p_anc); return true; }
-    const uint32_t jp = ip + 1 - (pn >> 31);  // 0: the principal itself, j: ancestor j - 1
-    if (!jp) { p = make_uint2(pt, pi); return true; }
-    if (!stl || jp > SCAN_ANC) return false;
-    p = s_anc[seg][jp - 1];
-    return true;
+    if (pkc != KC_ENT) return key_comp(pkc, 0u, pt, pi, blk, p_anc);
+    return key_comp(KC_ENT, ip + 1 - (pn >> 31), pt, pi, blk, p_anc);
   };
   uint32_t npos = 0;
-  if (a.scan_filt) {
+  if (kbits && __ballot(klist && simple) != 0) {
+    const bool on = klist && simple;
     for (uint32_t m = cm; m; m &= m - 1) {  // wave-uniform: the image's combos
       const uint32_t cb = __builtin_ctz(m);
-      const uint32_t cnt = simple ? comb_cnt(cb) : 0u;
+      const uint32_t cnt = on ? comb_cnt(cb) : 0u;
       if (__ballot(cnt != 0) == 0) continue;
+      if ((cb & 3) != KC_ENT) {  // one key (principal type or wildcard): listed as is
+        if (cnt && sl == 0 && npos < SCAN_POS) s_pos[seg][npos] = (uint16_t)(cb << 11);
+        npos += cnt != 0;
+        continue;
+      }
+      // the context's bitset row: one probe chain in the context table (segment-uniform)
       const uint2 q = comb_q(cb), r = comb_r(cb);
-      const uint32_t pre = key_pre(cb, q.x, q.y, r.x, r.y);
-      for (uint32_t rb = 0; __ballot(rb < cnt) != 0; rb += SEG * SCAN_PU) {
-        uint2 fw[SCAN_PU];
-        uint32_t fh[SCAN_PU];
+      uint32_t row_ = KIDX_NONE;
+      if (cnt)
+        for (uint32_t h = ctx_hash(key_pre(cb, q.x, q.y, r.x, r.y)) & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
+          const uint4 x = *reinterpret_cast<const uint4*>(a.sctx + (size_t)h * SCTX_WORDS);
+          if (x.x == 0) break;
+          const uint2 y = *reinterpret_cast<const uint2*>(a.sctx + (size_t)h * SCTX_WORDS + 4);
+          if (x.x == (SCTX_USED | cb) && x.y == q.x && x.z == q.y && x.w == r.x && y.x == r.y) { row_ = y.y; break; }
+        }
+      const uint32_t* rowb = a.sbits + (size_t)(row_ == KIDX_NONE ? 0u : row_) * a.sbits_words;
+      const uint32_t lim = row_ == KIDX_NONE ? 0u : cnt;
+      const uint32_t self = pn >> 31;
+      for (uint32_t rb = 0; __ballot(rb < lim) != 0; rb += SEG * SCAN_PU) {
+        uint32_t fw[SCAN_PU], fk[SCAN_PU];
 #pragma unroll
         for (uint32_t u = 0; u < SCAN_PU; u++) {
           const uint32_t ip = rb + u * SEG + sl;
-          fw[u] = make_uint2(~0u, ~0u);  // a key not tested (its component is not in LDS) passes
-          fh[u] = 0;
-          uint2 p;
-          if (ip < cnt && comb_p_lds(cb, ip, p)) {
-            const uint32_t h = key_fin(pre, p.x, p.y);
-            fh[u] = h;
-            fw[u] = *reinterpret_cast<const uint2*>(a.bfilt + 2 * (size_t)(h & a.fmask));
+          const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
+          fw[u] = 0xFFFFFFFFu;  // a key whose kidx is not staged passes untested
+          fk[u] = 0;
+          if (ip < lim && jk <= SCAN_ANC) {
+            const uint32_t kid = s_st.kid[seg][jk];
+            fk[u] = kid;
+            fw[u] = kid == KIDX_NONE ? 0u : rowb[kid >> 5];
           }
         }
 #pragma unroll
         for (uint32_t u = 0; u < SCAN_PU; u++) {
           const uint32_t ip = rb + u * SEG + sl;
-          const uint64_t need = filt_need(fh[u]);
-          const bool ok = ip < cnt && ((((uint64_t)fw[u].y << 32) | fw[u].x) & need) == need;
+          const bool ok = ip < lim && ((fw[u] >> (fk[u] & 31)) & 1u);
           const uint64_t mk = sballot(ok);
           const uint32_t at_ = npos + mbcnt64(mk);
-          if (ok && at_ < SCAN_POS) s_pos[seg][at_] = (cb << 16) | ip;
+          if (ok && at_ < SCAN_POS) s_pos[seg][at_] = (uint16_t)((cb << 11) | ip);
           npos += popc64(mk);
         }
       }
     }
     wave_lds_sync();
   }
-  // a request off the simple shape, or with more filter-passing keys than the list holds,
-  // enumerates every key instead
-  const bool flt = a.scan_filt && simple && npos <= SCAN_POS;
+  // a request off the simple shape, or with more listed keys than the list holds, enumerates every
+  // key instead
+  const bool flt = klist && simple && npos <= SCAN_POS;
   const uint32_t n_l1 = flt ? npos : n_keys;
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
@@ -1790,8 +1819,8 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         if (kk < n_l1) {
           if (flt) {
             const uint32_t x = s_pos[seg][kk];
-            combo = x >> 16;
-            if (!comb_p_lds(combo, x & 0xFFFFu, kp)) kp = key_comp(KC_ENT, (x & 0xFFFFu) + 1 - (pn >> 31), pt, pi, blk, p_anc);
+            combo = x >> 11;
+            kp = comb_p(combo, x & 0x7FFu);
             ka = comb_q(combo);
             kr = comb_r(combo);
           } else {
@@ -2336,6 +2365,9 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.cpool = (uint32_t*)at(DS_CPOOL); d.gstr_off = (uint32_t*)at(DS_GSTR_OFF); d.hot = (uint32_t*)at(DS_HOT);
   d.act = (uint32_t*)at(DS_ACT); d.btab = (uint32_t*)at(DS_BTAB); d.bfilt = (uint32_t*)at(DS_BFILT);
   d.bstream = (uint32_t*)at(DS_BSTREAM); d.srows = (uint32_t*)at(DS_SROWS); d.shash = (uint32_t*)at(DS_SHASH);
+  d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS);
+  d.sctx_mask = (uint32_t)(img.sctx.size() / SCTX_WORDS) - 1;
+  d.sbits_words = img.sbits_words;
   d.gstr_bytes = at(DS_GSTR_BYTES);
   d.n_static = img.n_static();
   d.lane_need = img.lane_need;
@@ -2842,6 +2874,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.act = img.act; k.n_act = img.n_act; k.amask_ok = img.amask_ok;
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
+  k.sctx = img.sctx; k.sbits = img.sbits; k.sctx_mask = img.sctx_mask; k.sbits_words = img.sbits_words;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
   k.lane = b.lane; k.lane_stride = img.lane_need;

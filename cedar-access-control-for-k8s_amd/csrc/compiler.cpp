@@ -1003,6 +1003,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
   img.key_ents.clear();
+  img.sctx.assign(SCTX_WORDS, 0); img.sbits.assign(1, 0); img.sbits_words = 0;
   img.combo_mask = 0;
   img.pslot_mask = 0;
   img.pfx.assign((size_t)img.n_hot() * PFX_LENS, 0);
@@ -1035,6 +1036,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
     img.btab_slots = 2;
+    img.sctx.assign(SCTX_WORDS, 0); img.sbits.assign(1, 0); img.sbits_words = 0;
     return;
   }
   static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
@@ -1174,6 +1176,40 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     }
   }
   mark("buckets");
+  // scope bitsets (image.h): a row per (combo, action, resource) context of the level-1 keys whose
+  // principal component is an entity, a bit per key entity
+  {
+    std::map<std::array<uint32_t, 5>, uint32_t> ctx;
+    std::vector<std::pair<uint32_t, uint32_t>> bits;  // (row, kidx)
+    for (const G& g : g1) {
+      const L1& k = r1[g.b].first;
+      if ((k[0] & 3) != KC_ENT) continue;
+      const uint32_t row = ctx.emplace(std::array<uint32_t, 5>{k[0], k[3], k[4], k[5], k[6]}, (uint32_t)ctx.size()).first->second;
+      const uint64_t u = ((uint64_t)k[1] << 32) | k[2];
+      bits.emplace_back(row, (uint32_t)(std::lower_bound(img.key_ents.begin(), img.key_ents.end(), u) - img.key_ents.begin()));
+    }
+    const uint64_t words = (img.key_ents.size() + 31) / 32;
+    if (!ctx.empty() && words && (uint64_t)ctx.size() * words * 4 <= SBITS_MAX_BYTES) {
+      img.sbits_words = (uint32_t)words;
+      img.sbits.assign((size_t)ctx.size() * words, 0);
+      for (auto& b : bits) img.sbits[(size_t)b.first * words + (b.second >> 5)] |= 1u << (b.second & 31);
+      uint32_t slots = 2;
+      while (slots < 2 * ctx.size()) slots <<= 1;
+      img.sctx.assign((size_t)slots * SCTX_WORDS, 0);
+      for (auto& c : ctx) {
+        const auto& x = c.first;
+        uint32_t h = ctx_hash(key_pre(x[0], x[1], x[2], x[3], x[4])) & (slots - 1);
+        while (img.sctx[(size_t)h * SCTX_WORDS]) h = (h + 1) & (slots - 1);
+        uint32_t* e = &img.sctx[(size_t)h * SCTX_WORDS];
+        e[0] = SCTX_USED | x[0]; e[1] = x[1]; e[2] = x[2]; e[3] = x[3]; e[4] = x[4]; e[5] = c.second;
+      }
+    }
+    static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
+    if (times)
+      std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities): %.1f MB%s\n", ctx.size(),
+                   (unsigned long long)words, img.key_ents.size(), ctx.size() * words * 4 / 1e6,
+                   img.sbits_words ? "" : " (over the cap: none)");
+  }
   // record heads (bucket order) then the ext area (one full record per policy)
   uint32_t n_heads = 0;
   for (auto& x : r1) n_heads += x.second != NO_POLICY;
@@ -1494,7 +1530,7 @@ std::vector<uint8_t> Image::serialize() const {
   auto words = [](const std::vector<uint32_t>& v) { return std::make_pair((const void*)v.data(), v.size() * 4); };
   const std::pair<const void*, size_t> sec[DS_COUNT] = {
       words(pstream), words(tier_cend), words(chunks), words(cpool), words(gstr_off), words(hot), words(act),
-      words(btab), words(bfilt), words(bstream), words(srows), words(shash),
+      words(btab), words(bfilt), words(bstream), words(srows), words(shash), words(sctx), words(sbits),
       std::make_pair((const void*)gstr_bytes.data(), gstr_bytes.size())};
   w.align(DS_ALIGN);
   const size_t begin = w.b.size();
@@ -1510,7 +1546,7 @@ std::vector<uint8_t> Image::serialize() const {
   w.put64(table + 16 * DS_COUNT + 8, w.b.size());
   w.vec(pol); w.vec(tier_end); w.vec(code);
   w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
-  w.u32(pslot_mask); w.vec(pfx); w.u32(btab_slots);
+  w.u32(pslot_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words);
   w.u32((uint32_t)key_ents.size());
   for (uint64_t k : key_ents) w.u64(k);
   w.u32((uint32_t)strings.size());
@@ -1548,6 +1584,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   sec_words(DS_CPOOL, img->cpool); sec_words(DS_GSTR_OFF, img->gstr_off); sec_words(DS_HOT, img->hot);
   sec_words(DS_ACT, img->act); sec_words(DS_BTAB, img->btab); sec_words(DS_BFILT, img->bfilt);
   sec_words(DS_BSTREAM, img->bstream); sec_words(DS_SROWS, img->srows); sec_words(DS_SHASH, img->shash);
+  sec_words(DS_SCTX, img->sctx); sec_words(DS_SBITS, img->sbits);
   {
     const uint64_t off = img->dev_off[DS_GSTR_BYTES], len = img->dev_len[DS_GSTR_BYTES];
     if (off % DS_ALIGN || off < img->dev_begin || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
@@ -1561,6 +1598,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->pslot_mask = r.u32();
   img->pfx = r.vec();
   img->btab_slots = r.u32();
+  img->sbits_words = r.u32();
   if (img->pfx.size() != (size_t)img->n_hot() * PFX_LENS && !(img->pfx.empty() && !img->pslot_mask))
     throw CedarError("corrupt image (prefix lengths)");
   {
@@ -1571,6 +1609,21 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   }
   if (img->lane_need > LANE_MAX) throw CedarError("corrupt image (lane scratch)");
   {
+    const size_t nc = img->sctx.size() / SCTX_WORDS;
+    if (!nc || (nc & (nc - 1)) || img->sctx.size() % SCTX_WORDS ||
+        (img->sbits_words && img->sbits.size() % img->sbits_words))
+      throw CedarError("corrupt image (scope bitsets)");
+    // every context row in range, and a free slot that ends every probe chain
+    size_t used = 0;
+    const size_t rows = img->sbits_words ? img->sbits.size() / img->sbits_words : 0;
+    for (size_t k = 0; k < nc; k++)
+      if (img->sctx[k * SCTX_WORDS]) {
+        used++;
+        if (img->sctx[k * SCTX_WORDS + 5] >= rows) throw CedarError("corrupt image (scope bitsets)");
+      }
+    if (used >= nc) throw CedarError("corrupt image (scope bitsets)");
+  }
+  {
     const size_t ns = img->shash.size() / SH_WORDS;
     if (!ns || (ns & (ns - 1)) || img->srows.size() % ENT_WORDS || ns <= img->n_static()) throw CedarError("corrupt image (static entities)");
   }
@@ -1578,6 +1631,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   r.need((size_t)nk * 8);
   img->key_ents.resize(nk);
   for (auto& k : img->key_ents) k = r.u64();
+  if (img->sbits_words && img->sbits_words != (img->key_ents.size() + 31) / 32) throw CedarError("corrupt image (scope bitsets)");
   uint32_t ns = r.u32();
   for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }
   uint32_t nm = r.u32();

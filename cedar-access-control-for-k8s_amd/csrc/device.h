@@ -19,6 +19,8 @@ struct DevImage {
   uint32_t *btab = nullptr, *bfilt = nullptr, *bstream = nullptr;  // scope index
   void* btab_mem = nullptr;  // the slot table btab points to (built at load from the entry list)
   uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
+  uint32_t *sctx = nullptr, *sbits = nullptr;                        // scope bitsets
+  uint32_t sctx_mask = 0, sbits_words = 0;
   uint8_t* gstr_bytes = nullptr;
   // the one device allocation holding the image's device region (image.h DevSection); the arrays
   // above point into it at (blob offset - origin)

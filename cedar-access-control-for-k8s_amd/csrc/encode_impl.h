@@ -232,6 +232,13 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   std::vector<uint64_t> anc, nodes, cl;
   std::vector<uint32_t> n_key(n, 0);
   std::unordered_set<uint64_t> seen_big;
+  // image with scope bitsets: after an ancestor list's pairs, the key-entity index of its owner and
+  // of each of its `keys` leading (key-entity) ancestors (image.h "scope bitsets")
+  auto push_kidx = [&](uint64_t owner, uint32_t keys) {
+    if (!img.sbits_words) return;
+    blk.push_back(img.key_index(owner));
+    for (uint32_t j = 0; j < keys; j++) blk.push_back(img.key_index(anc[j]));
+  };
   for (uint32_t i = 0; i < n; i++) {
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_TYPE] = (uint32_t)(index.keys[i] >> 32);
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ID] = (uint32_t)index.keys[i];
@@ -279,6 +286,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     const uint32_t off = (uint32_t)blk.size();
     blk.push_back((uint32_t)anc.size());
     for (const uint64_t a : anc) { blk.push_back((uint32_t)(a >> 32)); blk.push_back((uint32_t)a); }
+    push_kidx(index.keys[i], n_key[i]);
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = mk_ref(SP_HEAP, off);
   }
   // ---- columnar row: UIDs, ancestor lists, hot paths resolved as attribute access would ----
@@ -298,6 +306,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       row[w_off] = (uint32_t)blk.size() + 1;
       blk.push_back((uint32_t)anc.size());
       for (const uint64_t a : anc) { blk.push_back((uint32_t)(a >> 32)); blk.push_back((uint32_t)a); }
+      push_kidx(uid_key(self.first, self.second), keys);
       cnt = (uint32_t)anc.size();
     } else if (idx != NO_ENT) {
       const uint32_t ref = blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;

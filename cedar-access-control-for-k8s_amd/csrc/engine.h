@@ -49,6 +49,14 @@ struct Image {
   // entity components of the scope index's level-1 keys, (type sid << 32 | id sid), sorted: the
   // encoder lists a request's ancestors that are among them first (image.h RW_PN)
   std::vector<uint64_t> key_ents;
+  // scope bitsets (image.h "scope bitsets"): context table and one row of sbits_words per context
+  std::vector<uint32_t> sctx, sbits;
+  uint32_t sbits_words = 0;
+  // index of `uid` in key_ents, KIDX_NONE when it is no key entity
+  uint32_t key_index(uint64_t uid) const {
+    if (!is_key_ent(uid)) return cgi::KIDX_NONE;
+    return (uint32_t)(std::lower_bound(key_ents.begin(), key_ents.end(), uid) - key_ents.begin());
+  }
   // static entities (image.h "static entities"): device rows and UID hash; closure rows and
   // direct-parent lists in cpool ([n, (type, id) x n]; ER_ANC / ER_PAD offsets)
   std::vector<uint32_t> srows, shash;

@@ -188,6 +188,26 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
   return (1ull << (b & 63u)) | (1ull << ((b >> 6) & 63u)) | (1ull << ((b >> 12) & 63u));
 }
 
+// Scope bitsets: an exact membership test for the level-1 keys whose principal component is an
+// entity (combo with pkc == KC_ENT). A key splits into its context (combo, action component,
+// resource component) and its principal key entity. Each context in use has a row of sbits_words
+// words, one bit per key entity (index into Image::key_ents, "kidx"); the bit is set when the
+// level-1 key exists. sctx: open-addressed table of SCTX_WORDS slots
+// [SCTX_USED | combo, at, ai, rt, ri, row, 0, 0] at ctx_hash(key_pre(combo, at, ai, rt, ri)).
+// A request looks its context up once per combo and tests one bit per principal key ancestor (the
+// encoder lists their kidx after the ancestor pairs: [n, (type, id) x n, kidx(self), kidx x keys],
+// kidx ~0 for a UID that is no key entity); only keys whose bit is set probe the scope table. The
+// requests of a wave (grouped) share the context row, so the test reads a few shared lines.
+// Images whose bitsets would exceed SBITS_MAX_BYTES have none (sbits_words == 0).
+constexpr uint32_t SCTX_WORDS = 8, SCTX_USED = 0x80000000u, KIDX_NONE = 0xFFFFFFFFu;
+constexpr uint64_t SBITS_MAX_BYTES = 64ull << 20;
+__host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {
+  pre ^= pre >> 16;
+  pre *= 0x7FEB352Du;
+  pre ^= pre >> 15;
+  return pre;
+}
+
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
 __host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_t ei) {
   return ((et * 0x9E3779B1u) ^ (ei * 0x85EBCA77u) ^ ((ei >> 16) * 0xC2B2AE3Du)) >> 25;
@@ -402,14 +422,14 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 9;
+constexpr uint32_t IMG_VERSION = 10;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob
 // itself when a collective delivered it to device memory), with each array at its blob offset.
 enum DevSection : uint32_t {
   DS_PSTREAM, DS_TIER_CEND, DS_CHUNKS, DS_CPOOL, DS_GSTR_OFF, DS_HOT, DS_ACT, DS_BTAB, DS_BFILT, DS_BSTREAM,
-  DS_SROWS, DS_SHASH, DS_GSTR_BYTES, DS_COUNT
+  DS_SROWS, DS_SHASH, DS_SCTX, DS_SBITS, DS_GSTR_BYTES, DS_COUNT
 };
 constexpr uint32_t DS_ALIGN = 256;
 
