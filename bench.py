@@ -423,8 +423,11 @@ def main():
 
     # per-phase split of the same step (HIP events at each phase boundary; outside the timed region)
     split_steps = max(1, min(args.steps, 5))
-    phases, split_total = b.time_split(split_steps)
-    phases = {k: v / split_steps for k, v in phases.items()}
+    try:
+        phases, split_total = b.time_split(split_steps)
+        phases = {k: v / split_steps for k, v in phases.items()}
+    except AttributeError:  # an A/B build (CEDARGPU_AB_LIB) that predates cg_batch_time_split
+        phases, split_total = {"total": kernel_ms / args.steps * split_steps}, kernel_ms / args.steps * split_steps
 
     # submit -> results-visible latency on small batches (includes H2D, launch, D2H)
     lat = []
