@@ -70,6 +70,9 @@ _SIGS = {
     "cg_compiler_add_document": (ctypes.c_int, [P, cstr, cstr, sz, cstr, cstr]),
     "cg_compiler_add_policy": (ctypes.c_int, [P, cstr, cstr, cstr, sz, ctypes.c_int]),
     "cg_compiler_set_entities": (ctypes.c_int, [P, cstr, sz]),
+    "cg_compiler_set_incremental": (ctypes.c_int, [P, ctypes.c_int]),
+    "cg_compiler_last_build": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                              ctypes.POINTER(ctypes.c_char_p)]),
     "cg_compiler_add_document_ex": (ctypes.c_int, [P, cstr, cstr, sz, cstr, cstr, ctypes.c_int]),
     "cg_compiler_doc_errors": (ctypes.c_int, [P, P, sz, ctypes.POINTER(sz)]),
     "cg_compiler_build": (ctypes.c_int, [P, u64, ctypes.POINTER(P), ctypes.POINTER(sz)]),

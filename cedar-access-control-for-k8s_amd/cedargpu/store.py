@@ -137,13 +137,26 @@ ALLOW_ALL_ADMISSION = StaticStore([(
 
 
 class Compiler:
-    """A policy compiler that keeps parsed documents across builds (cg_compiler_*): the incremental
-    rebuild a store change triggers parses only the new or changed documents."""
+    """A policy compiler that keeps parsed and lowered documents across builds (cg_compiler_*): the
+    incremental rebuild a store change triggers parses and lowers only the new or changed
+    documents (`incremental=False`: every build a full one, byte-identical to a fresh compiler's)."""
 
-    def __init__(self):
+    def __init__(self, incremental: bool = True):
         self._h = _P()
         if lib.cg_compiler_create(ctypes.byref(self._h)):
             raise CompileError(-1, "compiler create failed")
+        if not incremental:
+            lib.cg_compiler_set_incremental(self._h, 0)
+
+    def last_build(self) -> dict:
+        """{"incremental", "lowered", "reused", "why_full"} of the last build (cg_compiler_last_build)."""
+        inc, lo, re = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        why = ctypes.c_char_p()
+        rc = lib.cg_compiler_last_build(self._h, ctypes.byref(inc), ctypes.byref(lo), ctypes.byref(re), ctypes.byref(why))
+        if rc:
+            raise _err(rc, "last_build failed")
+        return {"incremental": bool(inc.value), "lowered": lo.value, "reused": re.value,
+                "why_full": (why.value or b"").decode()}
 
     def close(self):
         if self._h:

@@ -43,6 +43,11 @@ struct cg_compiler {
   std::vector<EntityIn> statics;  // the image's static entities (cg_compiler_set_entities)
   std::vector<DocError> skipped;  // documents the last build left out (CG_DOC_SKIP_INVALID)
   ParseCache cache;  // parsed documents reused across builds
+  std::unique_ptr<LowerState, LowerDeleter> lower = make_lower_state();  // lowered documents (incremental builds)
+  bool incremental = true;
+  uint64_t statics_gen = 0;  // bumped by every cg_compiler_set_entities that changes them
+  std::string statics_json;
+  BuildInfo last;
   std::string err;
 };
 
@@ -310,12 +315,31 @@ int cg_compiler_cache_stats(cg_compiler* c, uint64_t* hits, uint64_t* misses, ui
   return CG_OK;
 }
 
+int cg_compiler_set_incremental(cg_compiler* c, int on) {
+  if (!c) return CG_E_ARG;
+  c->incremental = on != 0;
+  if (!on) c->lower = make_lower_state();  // drop the arenas
+  return CG_OK;
+}
+
+int cg_compiler_last_build(cg_compiler* c, int* incremental, uint64_t* lowered, uint64_t* reused, const char** why_full) {
+  if (!c) return CG_E_ARG;
+  if (incremental) *incremental = c->last.incremental ? 1 : 0;
+  if (lowered) *lowered = c->last.lowered;
+  if (reused) *reused = c->last.reused;
+  if (why_full) *why_full = c->last.why_full;
+  return CG_OK;
+}
+
 int cg_compiler_set_entities(cg_compiler* c, const char* json, size_t len) {
   if (!c || (!json && len)) return CG_E_ARG;
   GUARD(c->err, {
+    if (c->statics_json.size() == len && (!len || std::memcmp(c->statics_json.data(), json, len) == 0)) return CG_OK;
     std::vector<EntityIn> ents;
     if (len) decode_json_entities(json_parse(json, len), ents);
     c->statics = std::move(ents);
+    c->statics_json.assign(json ? json : "", len);
+    c->statics_gen++;
     return CG_OK;
   })
 }
@@ -384,13 +408,13 @@ int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* l
   if (!c || !image || !len) return CG_E_ARG;
   try {
     c->skipped.clear();
-    auto img = compile_image(c->tiers, epoch, &c->cache, &c->statics, &c->skipped);
-    auto blob = img->serialize();
-    uint8_t* p = (uint8_t*)std::malloc(blob.size());
+    auto img = compile_image(c->tiers, epoch, &c->cache, &c->statics, &c->skipped, c->incremental ? c->lower.get() : nullptr,
+                             c->statics_gen, &c->last);
+    size_t n = 0;
+    uint8_t* p = img->serialize_malloc(&n);
     if (!p) { c->err = "out of host memory"; return CG_E_ARG; }
-    std::memcpy(p, blob.data(), blob.size());
     *image = p;
-    *len = blob.size();
+    *len = n;
     return CG_OK;
   } catch (const CedarError& e) {
     c->err = e.what();

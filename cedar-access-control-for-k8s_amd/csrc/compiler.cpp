@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <thread>
 
@@ -992,6 +993,26 @@ struct Compiler {
 
 }  // namespace
 
+// fn(i) for i in [0, n) on up to 16 threads (chunks of 4,096)
+static void parallel_range(size_t n, const std::function<void(size_t)>& fn) {
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t chunk = 4096;
+  const unsigned nt = (unsigned)std::min<size_t>(hw, (n + chunk - 1) / chunk);
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t b; (b = next.fetch_add(chunk)) < n;)
+      for (size_t i = b; i < std::min(n, b + chunk); i++) fn(i);
+  };
+  std::vector<std::thread> ts;
+  for (unsigned t = 1; t < nt; t++) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+}
+
 // Scope index (image.h "scope index"): file each policy of an all-atomic image under the key set
 // with the fewest competing policies (a level-1 scope key, refined by the policy's attribute key
 // when it has one), then lay out fixed record heads bucket by bucket and the full records in the
@@ -1064,40 +1085,61 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   // action list by content) decide alike for every request; only the lowest-index member is filed,
   // and its head lists the class (head word PW_CODE_N: bstream offset of [n, member indices...]),
   // so the probe kernel evaluates the class once and records every member
-  std::vector<uint32_t> rep(n);
-  std::vector<std::vector<uint32_t>> members(n);
+  // (key: the record with PW_CODE and an action list's offset zeroed, then that list's pairs;
+  // hashed on worker threads, classes found among equal hashes)
+  std::vector<uint32_t> rep(n), mcnt(n, 0), moff(n + 1, 0), mflat(n);
   {
     static const bool off = std::getenv("CEDARGPU_NO_CLASSES") != nullptr;  // A/B studies
-    auto key_of = [&](uint32_t q) {
-      std::vector<uint32_t> k(img.pstream.begin() + rec_off[q], img.pstream.begin() + rec_off[q] + rec_len[q]);
-      k[PW_CODE] = 0;
-      const uint32_t* d = &img.pol[(size_t)q * POL_WORDS];
-      if (((d[PW_KINDS] >> 8) & 0xFF) == SK_INSET) {
-        k[PW_A_EI] = 0;
-        k.insert(k.end(), img.cpool.begin() + d[PW_A_EI], img.cpool.begin() + d[PW_A_EI] + 2 * d[PW_A_ET]);
-      }
-      return k;
+    auto inset = [&](uint32_t q) { return ((img.pol[(size_t)q * POL_WORDS + PW_KINDS] >> 8) & 0xFF) == SK_INSET; };
+    auto klen = [&](uint32_t q) { return rec_len[q] + (inset(q) ? 2 * img.pol[(size_t)q * POL_WORDS + PW_A_ET] : 0u); };
+    auto kword = [&](uint32_t q, uint32_t j) -> uint32_t {
+      if (j < rec_len[q]) return (j == PW_CODE || (j == PW_A_EI && inset(q))) ? 0u : img.pstream[rec_off[q] + j];
+      return img.cpool[img.pol[(size_t)q * POL_WORDS + PW_A_EI] + (j - rec_len[q])];
     };
-    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;  // key hash -> representatives
-    for (uint32_t q = 0; q < n; q++) {
-      rep[q] = q;
-      if (off) continue;
-      const std::vector<uint32_t> k = key_of(q);
+    std::vector<std::pair<uint64_t, uint32_t>> hq(n);
+    parallel_range(off ? 0 : n, [&](size_t q) {
       uint64_t h = 1469598103934665603ull;
-      for (uint32_t x : k) h = (h ^ x) * 1099511628211ull;
-      auto& cands = by_hash[h];
-      for (uint32_t c : cands)
-        if (key_of(c) == k) { rep[q] = c; break; }
-      if (rep[q] == q) cands.push_back(q);
-      members[rep[q]].push_back(q);
+      const uint32_t L = klen((uint32_t)q);
+      for (uint32_t j = 0; j < L; j++) h = (h ^ kword((uint32_t)q, j)) * 1099511628211ull;
+      hq[q] = {h, (uint32_t)q};
+    });
+    for (uint32_t q = 0; q < n; q++) rep[q] = q;
+    if (!off) {
+      std::sort(hq.begin(), hq.end());
+      auto same = [&](uint32_t x, uint32_t y) {
+        const uint32_t L = klen(x);
+        if (klen(y) != L) return false;
+        for (uint32_t j = 0; j < L; j++)
+          if (kword(x, j) != kword(y, j)) return false;
+        return true;
+      };
+      std::vector<uint32_t> reps;  // distinct keys of one hash run, lowest member first
+      for (size_t i = 0; i < n;) {
+        size_t j = i;
+        while (j < n && hq[j].first == hq[i].first) j++;
+        reps.clear();
+        for (size_t k = i; k < j; k++) {  // ascending policy index within the run
+          const uint32_t q = hq[k].second;
+          for (uint32_t r : reps)
+            if (same(r, q)) { rep[q] = r; break; }
+          if (rep[q] == q) reps.push_back(q);
+        }
+        i = j;
+      }
     }
+    for (uint32_t q = 0; q < n; q++) mcnt[rep[q]]++;
+    for (uint32_t q = 0; q < n; q++) moff[q + 1] = moff[q] + mcnt[q];
+    std::vector<uint32_t> fill(moff.begin(), moff.end() - 1);
+    for (uint32_t q = 0; q < n; q++) mflat[fill[rep[q]]++] = q;  // ascending per class
   }
+  mark("classes");
   constexpr uint32_t NO_POLICY = 0xFFFFFFFFu;  // a level-1 entry that only carries level-2 keys
   std::vector<std::pair<L1, uint32_t>> r1;
   std::vector<std::pair<L2, uint32_t>> r2;
   std::vector<uint64_t> kents;  // entity components of the level-1 keys
   r1.reserve(n);
   r2.reserve(2 * (size_t)n);
+  std::vector<std::pair<uint32_t, uint32_t>> acts;  // a policy's action components
   for (uint32_t p = 0; p < n; p++) {
     if (rep[p] != p) continue;  // filed through its class representative
     const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
@@ -1110,7 +1152,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     uint32_t pkc, pt, pi, rkc, rt, ri;
     comp(pk, d[PW_P_TYPE], d[PW_P_ET], d[PW_P_EI], pkc, pt, pi);
     comp(rk, d[PW_R_TYPE], d[PW_R_ET], d[PW_R_EI], rkc, rt, ri);
-    std::vector<std::pair<uint32_t, uint32_t>> acts;  // action components
+    acts.clear();
     uint32_t akc = KC_ENT;
     if (ak == SK_EQ || ak == SK_IN) acts.emplace_back(d[PW_A_ET], d[PW_A_EI]);
     else if (ak == SK_INSET) {
@@ -1140,10 +1182,67 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       }
     }
   }
-  std::sort(r1.begin(), r1.end());
-  std::sort(r2.begin(), r2.end());
+  if (times) std::fprintf(stderr, "  index filings: r1 %zu r2 %zu kents %zu\n", r1.size(), r2.size(), kents.size());
+  mark("filings");
+  // Records ordered by (level-1 key hash, level-1 key[, level-2 part], policy): equal keys side by
+  // side in policy order, and r1 / r2 in the same level-1 order (merged below). The hash decides
+  // almost every comparison, so index records sort instead of the wide ones, on three threads.
+  auto l1_hash = [](const L1& k) { return key_hash(k[0], k[1], k[2], k[3], k[4], k[5], k[6]); };
+  auto l1_less = [&](const L1& a, uint32_t ha, const L1& b, uint32_t hb) { return ha != hb ? ha < hb : a < b; };
+  {
+    // 64-bit sort keys: r1 (hash, policy), r2 (hash, level-2 hash) then policy; a run of equal
+    // hashes over different keys (a collision) is put in key order afterwards
+    auto x_hash = [](const std::array<uint32_t, 3>& x) { return key_hash(x[0], x[1], x[2], 0, 0, 0, 0); };
+    struct K1 { uint64_t k; uint32_t i; bool operator<(const K1& o) const { return k != o.k ? k < o.k : i < o.i; } };
+    struct K2 { uint64_t k; uint32_t p, i; bool operator<(const K2& o) const { return k != o.k ? k < o.k : (p != o.p ? p < o.p : i < o.i); } };
+    std::vector<K1> i1(r1.size());
+    std::vector<K2> i2(r2.size());
+    std::vector<uint32_t> h1s(r1.size()), h2s(r2.size());  // level-1 hash by record
+    parallel_range(r1.size(), [&](size_t i) { h1s[i] = l1_hash(r1[i].first); i1[i] = {((uint64_t)h1s[i] << 32) | r1[i].second, (uint32_t)i}; });
+    parallel_range(r2.size(), [&](size_t i) {
+      h2s[i] = l1_hash(r2[i].first.first);
+      i2[i] = {((uint64_t)h2s[i] << 32) | x_hash(r2[i].first.second), r2[i].second, (uint32_t)i};
+    });
+    mark("sort keys");
+    std::thread t1([&] { std::sort(i1.begin(), i1.end()); });
+    std::thread t2([&] { std::sort(kents.begin(), kents.end()); });
+    std::sort(i2.begin(), i2.end());
+    t1.join();
+    t2.join();
+    mark("sort core");
+    // gathered in hash order, then each run of equal hashes checked (in order, cache-friendly)
+    std::vector<std::pair<L1, uint32_t>> s1(r1.size());
+    std::vector<std::pair<L2, uint32_t>> s2(r2.size());
+    std::vector<uint64_t> k2(r2.size());
+    parallel_range(r1.size(), [&](size_t i) { s1[i] = r1[i1[i].i]; });
+    parallel_range(r2.size(), [&](size_t i) { s2[i] = r2[i2[i].i]; k2[i] = i2[i].k; });
+    for (size_t b0 = 0; b0 < s1.size();) {  // collisions of the level-1 hash
+      size_t e = b0 + 1;
+      bool mixed = false;
+      while (e < s1.size() && (i1[e].k >> 32) == (i1[b0].k >> 32)) mixed |= s1[e++].first != s1[b0].first;
+      if (mixed) std::stable_sort(s1.begin() + (long)b0, s1.begin() + (long)e);
+      b0 = e;
+    }
+    for (size_t b0 = 0; b0 < s2.size();) {
+      size_t e = b0 + 1;
+      bool mixed = false;
+      while (e < s2.size() && (k2[e] >> 32) == (k2[b0] >> 32)) {
+        mixed |= s2[e].first.first != s2[b0].first.first;
+        e++;
+      }
+      for (size_t c = b0; !mixed && c < e;) {  // equal level-1 keys: level-2 hash collisions
+        size_t f = c + 1;
+        while (f < e && k2[f] == k2[c]) mixed |= s2[f++].first.second != s2[c].first.second;
+        c = f;
+      }
+      if (mixed) std::stable_sort(s2.begin() + (long)b0, s2.begin() + (long)e);
+      b0 = e;
+    }
+    r1.swap(s1);
+    r2.swap(s2);
+  }
   r2.erase(std::unique(r2.begin(), r2.end()), r2.end());
-  std::sort(kents.begin(), kents.end());
+  mark("sort");
   kents.erase(std::unique(kents.begin(), kents.end()), kents.end());
   img.key_ents = std::move(kents);
   // groups: [begin, end) ranges of one key; level-1 hmask from the level-2 keys under it
@@ -1161,9 +1260,10 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     g2.push_back({i, j});
     i = j;
   }
-  for (size_t a = 0, k = 0; a < g2.size(); a++) {  // both sorted by level-1 key first
+  for (size_t a = 0, k = 0; a < g2.size(); a++) {  // both in the same level-1 order
     const L1& key = r2[g2[a].b].first.first;
-    while (k < g1.size() && r1[g1[k].b].first < key) k++;
+    const uint32_t hk = l1_hash(key);
+    while (k < g1.size() && l1_less(r1[g1[k].b].first, l1_hash(r1[g1[k].b].first), key, hk)) k++;
     if (k < g1.size() && r1[g1[k].b].first == key) {
       const auto& x = r2[g2[a].b].first.second;
       if (x[0] & BT_CKEY) g1[k].cmask |= 1u << (x[0] & ~BT_CKEY);
@@ -1218,14 +1318,14 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   uint64_t ext_end = (uint64_t)n_heads * HEAD_WORDS;
   for (uint32_t p = 0; p < n; p++) { ext[p] = (uint32_t)ext_end; ext_end += rec_len[p]; }
   for (uint32_t p = 0; p < n; p++)
-    if (members[p].size() > 1) { mlist[p] = (uint32_t)ext_end; ext_end += 1 + members[p].size(); }
+    if (mcnt[p] > 1) { mlist[p] = (uint32_t)ext_end; ext_end += 1 + mcnt[p]; }
   if (ext_end >= (1ull << 32)) throw CedarError("scope index exceeds 16 GiB");
   img.bstream.assign(std::max<uint64_t>(ext_end, HEAD_WORDS), 0);
   for (uint32_t p = 0; p < n; p++) {
     std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
     if (mlist[p]) {
-      img.bstream[mlist[p]] = (uint32_t)members[p].size();
-      std::copy(members[p].begin(), members[p].end(), img.bstream.begin() + mlist[p] + 1);  // ascending
+      img.bstream[mlist[p]] = mcnt[p];
+      std::copy(mflat.begin() + moff[p], mflat.begin() + moff[p + 1], img.bstream.begin() + mlist[p] + 1);  // ascending
     }
   }
   uint32_t head = 0;
@@ -1258,7 +1358,6 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   img.btab.clear();
   img.btab.reserve(std::max<size_t>(n_entries, 1) * BT_WORDS);
   auto insert = [&](uint32_t, const uint32_t* e) { img.btab.insert(img.btab.end(), e, e + BT_WORDS); };
-  auto l1_hash = [](const L1& k) { return key_hash(k[0], k[1], k[2], k[3], k[4], k[5], k[6]); };
   size_t blocks = 16;
   while (blocks * 4 < n_entries) blocks <<= 1;  // >= 16 bits per entry
   img.bfilt.assign(2 * blocks, 0);
@@ -1363,133 +1462,409 @@ static std::vector<std::shared_ptr<const std::vector<Policy>>> parse_documents(
   return out;
 }
 
-std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch, ParseCache* cache,
-                                     const std::vector<EntityIn>* statics, std::vector<DocError>* skipped) {
-  if (tiers.empty()) throw CedarError("at least one policy tier is required");
-  if (tiers.size() > 255) throw CedarError("too many tiers");
+// Incremental lowering state (engine.h LowerState): the persistent arenas a full build leaves, the
+// compiler's image-wide choices over them, and every document's lowered policies (descriptor with
+// the tier bits clear, index key, hot-path uses).
+struct LowerState {
+  Image arena;  // strings, sid, code, cpool, ext_msgs, act, hot, amask_ok
+  Compiler C{arena};
+  struct Pol {
+    std::array<uint32_t, POL_WORDS> w{};
+    Compiler::AttrKey key;
+    std::vector<std::pair<Compiler::Path, uint32_t>> uses;  // hot-path candidates it reads
+  };
+  struct Doc {
+    std::shared_ptr<const std::vector<Policy>> keep;  // holds the address the map is keyed by
+    std::vector<Pol> pols;
+    std::map<Compiler::Path, uint32_t> sum;  // uses over all its policies
+    size_t words = 0;                        // arena code + cpool words its lowering appended
+    uint64_t used = 0;
+  };
+  std::unordered_map<const void*, Doc> docs;
+  std::vector<uint32_t> srows, shash;  // the static entities as the last full build lowered them
+  uint64_t statics_gen = 0, gen = 0;
+  size_t base_words = 0, full_strings = 0;  // arena words owned by no document; strings then
+  bool valid = false;
+  void reset() {  // before a full build (gen carries on)
+    arena = Image();
+    C.hot.clear(); C.hot_depth.clear(); C.act_index.clear(); C.akeys.clear();
+    docs.clear(); srows.clear(); shash.clear();
+    statics_gen = 0; base_words = full_strings = 0;
+    valid = false;
+  }
+};
+void LowerDeleter::operator()(LowerState* s) const { delete s; }
+std::unique_ptr<LowerState, LowerDeleter> make_lower_state() { return std::unique_ptr<LowerState, LowerDeleter>(new LowerState()); }
+
+namespace {
+// PolicySet.Add semantics: a repeated ID replaces the earlier policy in place. The tiers refer to
+// the parsed ASTs (owned by the parse results / the cache); only ID and position are per use.
+struct PRef {
+  const Policy* p;
+  std::string id;
+  const std::string* filename;  // empty for zero-position documents
+  Position pos;
+  uint32_t doc, idx;  // parsed document (tier order) and the policy's index in it
+};
+const std::string k_empty_name;
+
+// the NHOT most used paths (ties: path order) -> slot
+std::map<Compiler::Path, uint32_t> hot_slots(const std::map<Compiler::Path, uint32_t>& cnt) {
+  std::vector<std::pair<uint32_t, const Compiler::Path*>> order;
+  for (auto& kv : cnt) order.emplace_back(kv.second, &kv.first);
+  std::sort(order.begin(), order.end(), [](auto& a, auto& b) { return a.first != b.first ? a.first > b.first : *a.second < *b.second; });
+  std::map<Compiler::Path, uint32_t> out;
+  for (size_t k = 0; k < order.size() && k < NHOT; k++) out.emplace(*order[k].second, (uint32_t)k);
+  return out;
+}
+}  // namespace
+
+// The image's policy stream, scope index, static entities and string table from its lowered
+// policies (shared by the full and the incremental build).
+template <class AK>
+static void finish_image(Image& img, const std::vector<AK>& akeys, const std::function<void()>& statics,
+                         const std::function<void(const char*)>& mark) {
+  // device policy stream + chunk table
+  {
+    uint32_t p = 0;
+    for (uint32_t t = 0; t < img.n_tiers(); t++) {
+      uint32_t pend = img.tier_end[t];
+      uint32_t c_off = (uint32_t)img.pstream.size(), c_p0 = p;
+      auto close = [&](uint32_t flag) {
+        uint32_t nw = (uint32_t)img.pstream.size() - c_off;
+        if (p > c_p0) {
+          img.chunks.push_back(c_off); img.chunks.push_back(nw | flag);
+          img.chunks.push_back(c_p0); img.chunks.push_back(p);
+        }
+        c_off = (uint32_t)img.pstream.size();
+        c_p0 = p;
+      };
+      for (; p < pend;) {
+        const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
+        uint32_t ncode = d[PW_CODE_N];
+        uint32_t rec = (POL_WORDS + ncode + 3) & ~3u;
+        // a record larger than an LDS chunk gets a chunk of its own, read in place (CHUNK_GLOBAL)
+        const bool big = rec > CHUNK_WORDS;
+        if (big || (uint32_t)img.pstream.size() - c_off + rec > CHUNK_WORDS) close(0);
+        size_t base = img.pstream.size();
+        img.pstream.insert(img.pstream.end(), d, d + POL_WORDS);
+        img.pstream[base + PW_CODE] = p;
+        img.pstream.insert(img.pstream.end(), img.code.begin() + d[PW_CODE], img.code.begin() + d[PW_CODE] + ncode);
+        while ((img.pstream.size() - base) % 4) img.pstream.push_back(0);
+        p++;
+        if (big) close(CHUNK_GLOBAL);
+      }
+      close(0);
+      img.tier_cend.push_back((uint32_t)img.chunks.size() / 4);
+    }
+    if (img.pstream.empty()) img.pstream.resize(4, 0);
+  }
+  mark("stream");
+  build_scope_index(img, akeys);
+  mark("scope index");
+  statics();
+  if (img.shash.empty()) img.shash.assign(SH_WORDS, 0);  // never empty buffers
+  mark("static entities");
+  // global string table
+  img.gstr_off.clear();
+  img.gstr_bytes.clear();
+  for (auto& s : img.strings) {
+    img.gstr_off.push_back((uint32_t)img.gstr_bytes.size());
+    img.gstr_bytes.insert(img.gstr_bytes.end(), s.begin(), s.end());
+  }
+  img.gstr_off.push_back((uint32_t)img.gstr_bytes.size());
+  if (img.code.empty()) img.code.push_back(0), img.code.push_back(0);  // never empty buffers
+  if (img.cpool.empty()) img.cpool.push_back(0);
+  if (img.gstr_bytes.empty()) img.gstr_bytes.push_back(0);
+  img.build_lookup();
+  mark("strings");
+}
+
+// The incremental build (engine.h LowerState): null when the cached lowering cannot serve this
+// build (`why` says why), which then runs in full.
+static std::shared_ptr<Image> compile_incremental(LowerState& S, const std::vector<std::shared_ptr<const std::vector<Policy>>>& docs,
+                                                  const std::vector<std::vector<PRef>>& parsed, uint64_t epoch,
+                                                  BuildInfo* info, const char** why, const std::function<void(const char*)>& mark) {
+  Compiler& C = S.C;
+  Image& A = S.arena;
+  S.gen++;
+  const size_t nd = docs.size();
+  std::vector<LowerState::Doc*> dref(nd, nullptr);
+  std::vector<uint32_t> fresh;  // documents to lower
+  for (size_t d = 0; d < nd; d++) {
+    auto it = S.docs.find(docs[d].get());
+    if (it != S.docs.end() && it->second.keep == docs[d]) dref[d] = &it->second;
+    else fresh.push_back((uint32_t)d);
+  }
+  // hot-path uses of the new documents (interned into the arena) and the image-wide totals over
+  // the policies that stay (a repeated ID drops the earlier policy)
+  std::vector<LowerState::Doc> lowered(fresh.size());
+  for (size_t f = 0; f < fresh.size(); f++) {
+    const auto& ps = *docs[fresh[f]];
+    lowered[f].keep = docs[fresh[f]];
+    lowered[f].pols.resize(ps.size());
+    for (size_t i = 0; i < ps.size(); i++) {
+      std::map<Compiler::Path, uint32_t> c;
+      for (auto& cond : ps[i].conds) C.count_hot(*cond.second, c);
+      for (auto& kv : c) lowered[f].sum[kv.first] += kv.second;
+      lowered[f].pols[i].uses.assign(c.begin(), c.end());
+    }
+  }
+  std::vector<uint32_t> fresh_at(nd, 0xFFFFFFFFu);
+  for (size_t f = 0; f < fresh.size(); f++) fresh_at[fresh[f]] = (uint32_t)f;
+  auto doc_of = [&](uint32_t d) -> LowerState::Doc& { return dref[d] ? *dref[d] : lowered[fresh_at[d]]; };
+  std::vector<uint32_t> kept(nd, 0);
+  for (auto& tp : parsed)
+    for (auto& r : tp) kept[r.doc]++;
+  std::map<Compiler::Path, uint32_t> cnt;
+  for (size_t d = 0; d < nd; d++) {
+    LowerState::Doc& D = doc_of((uint32_t)d);
+    for (auto& kv : D.sum) cnt[kv.first] += kv.second;
+  }
+  for (size_t d = 0; d < nd; d++) {  // a document with replaced policies: take theirs back out
+    LowerState::Doc& D = doc_of((uint32_t)d);
+    if (kept[d] == D.pols.size()) continue;
+    std::vector<char> live(D.pols.size(), 0);
+    for (auto& tp : parsed)
+      for (auto& r : tp)
+        if (r.doc == d) live[r.idx] = 1;
+    for (size_t i = 0; i < D.pols.size(); i++)
+      if (!live[i])
+        for (auto& u : D.pols[i].uses) {
+          auto it = cnt.find(u.first);
+          if ((it->second -= u.second) == 0) cnt.erase(it);
+        }
+  }
+  // the hot slots stay as they are while the paths a fresh build would make hot are among them
+  // (a slot whose path fell out of use only costs the encoder a column)
+  for (auto& kv : hot_slots(cnt))
+    if (!C.hot.count(kv.first)) { *why = "hot attribute paths changed"; return nullptr; }
+  for (uint32_t d : fresh)
+    for (auto& p : *docs[d]) C.collect_actions(p.action);
+  if (A.amask_ok && A.act.size() / 2 > MAX_ACT) { *why = "action table outgrew the action masks"; return nullptr; }
+  mark("incremental check");
+  // lower the new documents into the arenas
+  uint64_t n_lowered = 0;
+  for (size_t f = 0; f < fresh.size(); f++) {
+    const auto& ps = *docs[fresh[f]];
+    for (size_t i = 0; i < ps.size(); i++) {
+      const size_t w0 = A.code.size() + A.cpool.size();
+      C.policy(ps[i], 0);
+      auto& P = lowered[f].pols[i];
+      std::copy(A.pol.end() - POL_WORDS, A.pol.end(), P.w.begin());
+      P.key = C.akeys.back();
+      A.pol.clear();
+      C.akeys.clear();
+      lowered[f].words += A.code.size() + A.cpool.size() - w0;
+      n_lowered++;
+    }
+  }
+  for (size_t f = 0; f < fresh.size(); f++) {
+    const void* k = docs[fresh[f]].get();
+    S.docs.erase(k);
+    dref[fresh[f]] = &(S.docs[k] = std::move(lowered[f]));
+  }
+  mark("lower");
   auto img = std::make_shared<Image>();
   img->epoch = epoch;
-  Compiler C(*img);
+  img->strings = A.strings;
+  img->sid = A.sid;
+  img->code = A.code;
+  img->cpool = A.cpool;
+  img->ext_msgs = A.ext_msgs;
+  img->act = A.act;
+  img->hot = A.hot;
+  img->amask_ok = A.amask_ok;
+  std::vector<Compiler::AttrKey> akeys;
+  size_t total = 0;
+  for (auto& tp : parsed) total += tp.size();
+  img->pol.reserve(total * POL_WORDS);
+  img->meta.reserve(total);
+  akeys.reserve(total);
+  for (size_t t = 0; t < parsed.size(); t++) {
+    for (auto& r : parsed[t]) {
+      LowerState::Doc& D = *dref[r.doc];
+      D.used = S.gen;
+      const LowerState::Pol& P = D.pols[r.idx];
+      const size_t at = img->pol.size();
+      img->pol.insert(img->pol.end(), P.w.begin(), P.w.end());
+      img->pol[at + PW_FLAGS] |= (uint32_t)t << 8;
+      if (P.w[PW_FLAGS] & PF_ATOMIC) img->n_atomic++;
+      else img->lane_need = std::max(img->lane_need, P.w[PW_LANE]);
+      akeys.push_back(P.key);
+      PolicyMeta m;
+      m.id = r.id; m.filename = *r.filename; m.pos = r.pos; m.tier = (uint32_t)t;
+      m.forbid = r.p->forbid;
+      img->meta.push_back(std::move(m));
+    }
+    img->tier_end.push_back(img->n_pol());
+  }
+  // documents this build did not use leave the cache; their words stay in the arenas as garbage
+  size_t live = S.base_words;
+  for (auto it = S.docs.begin(); it != S.docs.end();) {
+    if (it->second.used != S.gen) it = S.docs.erase(it);
+    else { live += it->second.words; ++it; }
+  }
+  if (A.code.size() + A.cpool.size() > 2 * live + 1024 || A.strings.size() > 2 * S.full_strings + 256)
+    S.valid = false;  // the next build compacts (a full one)
+  mark("assemble");
+  finish_image(*img, akeys, [&] { img->srows = S.srows; img->shash = S.shash; }, mark);
+  if (info) {
+    info->incremental = true;
+    info->lowered = n_lowered;
+    info->reused = total - std::min<uint64_t>(total, n_lowered);
+  }
+  return img;
+}
+
+std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch, ParseCache* cache,
+                                     const std::vector<EntityIn>* statics, std::vector<DocError>* skipped,
+                                     LowerState* inc, uint64_t statics_gen, BuildInfo* info) {
+  if (tiers.empty()) throw CedarError("at least one policy tier is required");
+  if (tiers.size() > 255) throw CedarError("too many tiers");
   // CEDARGPU_COMPILE_TIMES=1: phase times to stderr (profiling)
   static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
   auto t_mark = std::chrono::steady_clock::now();
-  auto mark = [&](const char* what) {
+  std::function<void(const char*)> mark = [&](const char* what) {
     if (!times) return;
     const auto now = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "compile %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_mark).count());
+    std::fprintf(stderr, "compile %-18s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_mark).count());
     t_mark = now;
   };
+  if (info) *info = BuildInfo();
   const auto docs = parse_documents(tiers, cache, skipped);
   mark("parse");
-  // PolicySet.Add semantics: a repeated ID replaces the earlier policy in place. The tiers refer
-  // to the parsed ASTs (owned by `docs` / the cache); only ID and position are per use.
-  struct PRef {
-    const Policy* p;
-    std::string id, filename;
-    Position pos;
-  };
   std::vector<std::vector<PRef>> parsed(tiers.size());
-  size_t di = 0;
-  for (size_t t = 0; t < tiers.size(); t++) {
-    std::unordered_map<std::string, size_t> ids;
-    for (auto& doc : tiers[t]) {
-      const std::vector<Policy>& ps = *docs[di++];
-      if (!doc.explicit_id.empty() && ps.size() != 1)
-        throw CedarError("document for policy " + doc.explicit_id + " must hold exactly one policy");
-      for (size_t i = 0; i < ps.size(); i++) {
-        PRef r{&ps[i], doc.explicit_id.empty() ? doc.id_prefix + std::to_string(i) + doc.id_suffix : doc.explicit_id,
-               doc.zero_position ? std::string() : ps[i].filename, doc.zero_position ? Position{} : ps[i].pos};
-        auto it = ids.find(r.id);
-        if (it != ids.end()) parsed[t][it->second] = std::move(r);
-        else { ids.emplace(r.id, parsed[t].size()); parsed[t].push_back(std::move(r)); }
+  {
+    size_t di = 0;
+    for (size_t t = 0; t < tiers.size(); t++) {
+      size_t n = 0;
+      for (size_t k = 0; k < tiers[t].size(); k++) n += docs[di + k]->size();
+      parsed[t].reserve(n);
+      std::unordered_map<std::string, size_t> ids;
+      ids.reserve(n);
+      for (auto& doc : tiers[t]) {
+        const std::vector<Policy>& ps = *docs[di];
+        if (!doc.explicit_id.empty() && ps.size() != 1)
+          throw CedarError("document for policy " + doc.explicit_id + " must hold exactly one policy");
+        for (size_t i = 0; i < ps.size(); i++) {
+          PRef r{&ps[i], doc.explicit_id.empty() ? doc.id_prefix + std::to_string(i) + doc.id_suffix : doc.explicit_id,
+                 doc.zero_position ? &k_empty_name : &ps[i].filename, doc.zero_position ? Position{} : ps[i].pos,
+                 (uint32_t)di, (uint32_t)i};
+          auto it = ids.find(r.id);
+          if (it != ids.end()) parsed[t][it->second] = std::move(r);
+          else { ids.emplace(r.id, parsed[t].size()); parsed[t].push_back(std::move(r)); }
+        }
+        di++;
       }
     }
   }
   mark("assemble");
+  const char* why_full = "first build";
+  if (inc && inc->valid && inc->statics_gen == statics_gen) {
+    const char* why = "";
+    if (auto img = compile_incremental(*inc, docs, parsed, epoch, info, &why, mark)) return img;
+    why_full = why;
+  } else if (inc && inc->valid) {
+    why_full = "static entities changed";
+  } else if (inc && inc->gen) {
+    why_full = "compaction";
+  }
+  if (inc) inc->reset();  // a full build records afresh
+
+  auto img = std::make_shared<Image>();
+  img->epoch = epoch;
+  Compiler C(*img);
   // hot attribute paths over the whole image: the NHOT most used
   std::map<Compiler::Path, uint32_t> cnt;
+  std::vector<std::vector<std::pair<Compiler::Path, uint32_t>>> uses;  // per policy (incremental state)
+  if (inc) {
+    size_t total = 0;
+    for (auto& tp : parsed) total += tp.size();
+    uses.reserve(total);
+  }
   for (auto& tp : parsed)
-    for (auto& r : tp)
-      for (auto& c : r.p->conds) C.count_hot(*c.second, cnt);
-  std::vector<std::pair<uint32_t, Compiler::Path>> order;
-  for (auto& kv : cnt) order.emplace_back(kv.second, kv.first);
-  std::sort(order.begin(), order.end(), [](auto& a, auto& b) { return a.first != b.first ? a.first > b.first : a.second < b.second; });
-  for (size_t k = 0; k < order.size() && k < NHOT; k++) {
-    const Compiler::Path& path = order[k].second;
-    C.hot[path] = (uint32_t)k;
-    C.hot_depth.push_back((uint32_t)path.second.size());
-    img->hot.push_back(path.first);
-    img->hot.push_back((uint32_t)path.second.size());
-    for (uint32_t j = 0; j < MAX_PATH; j++) img->hot.push_back(j < path.second.size() ? path.second[j] : 0u);
+    for (auto& r : tp) {
+      if (!inc) {
+        for (auto& c : r.p->conds) C.count_hot(*c.second, cnt);
+        continue;
+      }
+      std::map<Compiler::Path, uint32_t> c1;
+      for (auto& c : r.p->conds) C.count_hot(*c.second, c1);
+      for (auto& kv : c1) cnt[kv.first] += kv.second;
+      uses.emplace_back(c1.begin(), c1.end());
+    }
+  C.hot = hot_slots(cnt);
+  C.hot_depth.assign(C.hot.size(), 0);
+  img->hot.assign(C.hot.size() * HOT_WORDS, 0);
+  for (auto& kv : C.hot) {
+    const Compiler::Path& path = kv.first;
+    C.hot_depth[kv.second] = (uint32_t)path.second.size();
+    uint32_t* h = &img->hot[(size_t)kv.second * HOT_WORDS];
+    h[0] = path.first;
+    h[1] = (uint32_t)path.second.size();
+    for (uint32_t j = 0; j < MAX_PATH; j++) h[2 + j] = j < path.second.size() ? path.second[j] : 0u;
   }
   for (auto& tp : parsed)
     for (auto& r : tp) C.collect_actions(r.p->action);
   img->amask_ok = img->act.size() / 2 <= MAX_ACT ? 1u : 0u;
+  std::vector<size_t> words;  // per policy: arena words its lowering appended (incremental state)
   for (size_t t = 0; t < parsed.size(); t++) {
     for (auto& r : parsed[t]) {
+      const size_t w0 = img->code.size() + img->cpool.size();
       C.policy(*r.p, (uint32_t)t);
+      if (inc) words.push_back(img->code.size() + img->cpool.size() - w0);
       PolicyMeta m;
-      m.id = std::move(r.id); m.filename = std::move(r.filename); m.pos = r.pos; m.tier = (uint32_t)t;
+      m.id = std::move(r.id); m.filename = *r.filename; m.pos = r.pos; m.tier = (uint32_t)t;
       m.forbid = r.p->forbid;
       img->meta.push_back(std::move(m));
     }
     img->tier_end.push_back(img->n_pol());
   }
   mark("lower");
-  // device policy stream + chunk table
-  {
-    uint32_t p = 0;
-    for (uint32_t t = 0; t < img->n_tiers(); t++) {
-      uint32_t pend = img->tier_end[t];
-      uint32_t c_off = (uint32_t)img->pstream.size(), c_p0 = p;
-      auto close = [&](uint32_t flag) {
-        uint32_t nw = (uint32_t)img->pstream.size() - c_off;
-        if (p > c_p0) {
-          img->chunks.push_back(c_off); img->chunks.push_back(nw | flag);
-          img->chunks.push_back(c_p0); img->chunks.push_back(p);
+  finish_image(*img, C.akeys, [&] { if (statics && !statics->empty()) C.statics(*statics); }, mark);
+  if (inc) {  // the arenas (the static entities' lists included) and every document whose policies all stayed
+    LowerState& S = *inc;
+    Image& A = S.arena;
+    A.strings = img->strings; A.sid = img->sid; A.code = img->code; A.cpool = img->cpool;
+    A.ext_msgs = img->ext_msgs; A.act = img->act; A.hot = img->hot; A.amask_ok = img->amask_ok;
+    S.C.hot = C.hot; S.C.hot_depth = C.hot_depth; S.C.act_index = C.act_index;
+    S.gen++;
+    std::vector<uint32_t> kept(docs.size(), 0);
+    for (auto& tp : parsed)
+      for (auto& r : tp) kept[r.doc]++;
+    std::unordered_map<const void*, uint32_t> owner;  // a document parsed once but listed twice: its first listing
+    size_t p = 0, owned = 0;
+    for (size_t t = 0; t < parsed.size(); t++)
+      for (auto& r : parsed[t]) {
+        const auto& keep = docs[r.doc];
+        if (kept[r.doc] == keep->size() && owner.emplace(keep.get(), r.doc).first->second == r.doc) {
+          LowerState::Doc& D = S.docs[keep.get()];
+          if (!D.keep) { D.keep = keep; D.pols.resize(keep->size()); D.used = S.gen; }
+          LowerState::Pol& P = D.pols[r.idx];
+          std::copy(&img->pol[p * POL_WORDS], &img->pol[p * POL_WORDS] + POL_WORDS, P.w.begin());
+          P.w[PW_FLAGS] &= ~(0xFFu << 8);  // the tier is the build's
+          P.key = C.akeys[p];
+          P.uses = std::move(uses[p]);
+          for (auto& u : P.uses) D.sum[u.first] += u.second;
+          D.words += words[p];
+          owned += words[p];
         }
-        c_off = (uint32_t)img->pstream.size();
-        c_p0 = p;
-      };
-      for (; p < pend;) {
-        const uint32_t* d = &img->pol[(size_t)p * POL_WORDS];
-        uint32_t ncode = d[PW_CODE_N];
-        uint32_t rec = (POL_WORDS + ncode + 3) & ~3u;
-        // a record larger than an LDS chunk gets a chunk of its own, read in place (CHUNK_GLOBAL)
-        const bool big = rec > CHUNK_WORDS;
-        if (big || (uint32_t)img->pstream.size() - c_off + rec > CHUNK_WORDS) close(0);
-        size_t base = img->pstream.size();
-        img->pstream.insert(img->pstream.end(), d, d + POL_WORDS);
-        img->pstream[base + PW_CODE] = p;
-        img->pstream.insert(img->pstream.end(), img->code.begin() + d[PW_CODE], img->code.begin() + d[PW_CODE] + ncode);
-        while ((img->pstream.size() - base) % 4) img->pstream.push_back(0);
         p++;
-        if (big) close(CHUNK_GLOBAL);
       }
-      close(0);
-      img->tier_cend.push_back((uint32_t)img->chunks.size() / 4);
-    }
-    if (img->pstream.empty()) img->pstream.resize(4, 0);
+    S.srows = img->srows;
+    S.shash = img->shash;
+    S.statics_gen = statics_gen;
+    S.base_words = A.code.size() + A.cpool.size() - owned;
+    S.full_strings = A.strings.size();
+    S.valid = true;
+    mark("record");
   }
-  mark("stream");
-  build_scope_index(*img, C.akeys);
-  mark("scope index");
-  if (statics && !statics->empty()) C.statics(*statics);
-  if (img->shash.empty()) img->shash.assign(SH_WORDS, 0);  // never empty buffers
-  mark("static entities");
-  // global string table
-  img->gstr_off.clear();
-  img->gstr_bytes.clear();
-  for (auto& s : img->strings) {
-    img->gstr_off.push_back((uint32_t)img->gstr_bytes.size());
-    img->gstr_bytes.insert(img->gstr_bytes.end(), s.begin(), s.end());
+  if (info) {
+    info->incremental = false;
+    info->lowered = img->n_pol();
+    info->why_full = why_full;
   }
-  img->gstr_off.push_back((uint32_t)img->gstr_bytes.size());
-  if (img->code.empty()) img->code.push_back(0), img->code.push_back(0);  // never empty buffers
-  if (img->cpool.empty()) img->cpool.push_back(0);
-  if (img->gstr_bytes.empty()) img->gstr_bytes.push_back(0);
-  img->build_lookup();
-  mark("strings");
   return img;
 }
 
@@ -1500,32 +1875,38 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
 // prefixed sections).
 // ---------------------------------------------------------------------------------------------
 namespace {
+static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "the blob's word arrays are copied as little-endian memory");
+// Two passes over one writer: with no buffer it only counts bytes, then it fills an exact one.
 struct W {
-  std::vector<uint8_t> b;
-  void u32(uint32_t v) { for (int k = 0; k < 4; k++) b.push_back((uint8_t)(v >> (8 * k))); }
-  void u64(uint64_t v) { u32((uint32_t)v); u32((uint32_t)(v >> 32)); }
-  void put64(size_t at, uint64_t v) { for (int k = 0; k < 8; k++) b[at + k] = (uint8_t)(v >> (8 * k)); }
-  void vec(const std::vector<uint32_t>& v) { u32((uint32_t)v.size()); for (auto x : v) u32(x); }
-  void bytes(const std::vector<uint8_t>& v) { u32((uint32_t)v.size()); b.insert(b.end(), v.begin(), v.end()); }
-  void str(const std::string& s) { u32((uint32_t)s.size()); b.insert(b.end(), s.begin(), s.end()); }
-  void align(size_t a) { b.resize((b.size() + a - 1) / a * a, 0); }
-  void raw(const void* p, size_t n) { b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + n); }
+  uint8_t* b = nullptr;
+  size_t n = 0;
+  void raw(const void* p, size_t k) { if (b && k) std::memcpy(b + n, p, k); n += k; }
+  void u32(uint32_t v) { raw(&v, 4); }
+  void u64(uint64_t v) { raw(&v, 8); }
+  void put64(size_t at, uint64_t v) { if (b) std::memcpy(b + at, &v, 8); }
+  void vec(const std::vector<uint32_t>& v) { u32((uint32_t)v.size()); raw(v.data(), v.size() * 4); }
+  void str(const std::string& s) { u32((uint32_t)s.size()); raw(s.data(), s.size()); }
+  void align(size_t a) {
+    const size_t m = (n + a - 1) / a * a;
+    if (b) std::memset(b + n, 0, m - n);
+    n = m;
+  }
 };
 struct R {
   const uint8_t* p; const uint8_t* e;
   void need(size_t n) { if ((size_t)(e - p) < n) throw CedarError("truncated image"); }
-  uint32_t u32() { need(4); uint32_t v = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); p += 4; return v; }
+  uint32_t u32() { need(4); uint32_t v; std::memcpy(&v, p, 4); p += 4; return v; }
   uint64_t u64() { uint64_t lo = u32(); return lo | ((uint64_t)u32() << 32); }
-  std::vector<uint32_t> vec() { uint32_t n = u32(); need((size_t)n * 4); std::vector<uint32_t> v(n); for (auto& x : v) x = u32(); return v; }
+  std::vector<uint32_t> vec() { uint32_t n = u32(); need((size_t)n * 4); std::vector<uint32_t> v(n); if (n) std::memcpy(v.data(), p, (size_t)n * 4); p += (size_t)n * 4; return v; }
   std::vector<uint8_t> bytes() { uint32_t n = u32(); need(n); std::vector<uint8_t> v(p, p + n); p += n; return v; }
   std::string str() { uint32_t n = u32(); need(n); std::string s((const char*)p, n); p += n; return s; }
 };
 }  // namespace
 
-std::vector<uint8_t> Image::serialize() const {
-  W w;
+void Image::write_blob(void* wp) const {
+  W& w = *static_cast<W*>(wp);
   w.u32(IMG_MAGIC); w.u32(IMG_VERSION); w.u64(epoch);
-  const size_t table = w.b.size();
+  const size_t table = w.n;
   for (uint32_t k = 0; k < 2 * DS_COUNT + 2; k++) w.u64(0);  // (offset, bytes) per section, begin, end
   auto words = [](const std::vector<uint32_t>& v) { return std::make_pair((const void*)v.data(), v.size() * 4); };
   const std::pair<const void*, size_t> sec[DS_COUNT] = {
@@ -1533,22 +1914,22 @@ std::vector<uint8_t> Image::serialize() const {
       words(btab), words(bfilt), words(bstream), words(srows), words(shash), words(sctx), words(sbits),
       std::make_pair((const void*)gstr_bytes.data(), gstr_bytes.size())};
   w.align(DS_ALIGN);
-  const size_t begin = w.b.size();
+  const size_t begin = w.n;
   for (uint32_t k = 0; k < DS_COUNT; k++) {
     w.align(DS_ALIGN);
-    w.put64(table + 16 * k, w.b.size());
+    w.put64(table + 16 * k, w.n);
     w.put64(table + 16 * k + 8, sec[k].second);
     w.raw(sec[k].first, sec[k].second);
   }
   w.raw("\0\0\0\0", 4);  // no section ends the region: a kernel may read one word of an empty one
   w.align(DS_ALIGN);
   w.put64(table + 16 * DS_COUNT, begin);
-  w.put64(table + 16 * DS_COUNT + 8, w.b.size());
+  w.put64(table + 16 * DS_COUNT + 8, w.n);
   w.vec(pol); w.vec(tier_end); w.vec(code);
   w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
   w.u32(pslot_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words);
   w.u32((uint32_t)key_ents.size());
-  for (uint64_t k : key_ents) w.u64(k);
+  w.raw(key_ents.data(), key_ents.size() * 8);
   w.u32((uint32_t)strings.size());
   for (auto& s : strings) w.str(s);
   w.u32((uint32_t)meta.size());
@@ -1559,7 +1940,26 @@ std::vector<uint8_t> Image::serialize() const {
   }
   w.u32((uint32_t)ext_msgs.size());
   for (auto& s : ext_msgs) w.str(s);
-  return w.b;
+}
+
+std::vector<uint8_t> Image::serialize() const {
+  W c;
+  write_blob(&c);
+  std::vector<uint8_t> out(c.n);
+  W w{out.data(), 0};
+  write_blob(&w);
+  return out;
+}
+
+uint8_t* Image::serialize_malloc(size_t* len) const {
+  W c;
+  write_blob(&c);
+  uint8_t* p = (uint8_t*)std::malloc(std::max<size_t>(c.n, 1));
+  if (!p) return nullptr;
+  W w{p, 0};
+  write_blob(&w);
+  *len = c.n;
+  return p;
 }
 
 std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
@@ -1630,7 +2030,9 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   const uint32_t nk = r.u32();
   r.need((size_t)nk * 8);
   img->key_ents.resize(nk);
-  for (auto& k : img->key_ents) k = r.u64();
+  r.need(img->key_ents.size() * 8);
+  if (!img->key_ents.empty()) std::memcpy(img->key_ents.data(), r.p, img->key_ents.size() * 8);
+  r.p += img->key_ents.size() * 8;
   if (img->sbits_words && img->sbits_words != (img->key_ents.size() + 31) / 32) throw CedarError("corrupt image (scope bitsets)");
   uint32_t ns = r.u32();
   for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }

@@ -132,6 +132,8 @@ struct Image {
     return h ^ (h >> 33);
   }
   std::vector<uint8_t> serialize() const;
+  uint8_t* serialize_malloc(size_t* len) const;  // the blob in one malloc'd buffer (cg_free)
+  void write_blob(void* writer) const;
   // device region of the blob this image was read from (image.h DevSection): section offsets and
   // byte sizes, and the region's bounds (blob offsets)
   uint64_t dev_off[cgi::DS_COUNT] = {}, dev_len[cgi::DS_COUNT] = {};
@@ -174,12 +176,32 @@ struct EntityIn {
   std::vector<std::pair<std::string, std::string>> parents;
 };
 
+// Lowered documents kept across builds (the incremental compiler, compiler.cpp): a full build
+// records every document's lowered policies against persistent arenas (string table, code,
+// constant pool, action table); a later build lowers only the documents it has not seen and
+// copies the rest, as long as the image-wide choices it made stay valid (the hot attribute paths,
+// the action table within MAX_ACT, the static entities). Otherwise, or once the arenas hold more
+// garbage than live words, the build is a full one again.
+struct LowerState;
+struct LowerDeleter { void operator()(LowerState* s) const; };
+std::unique_ptr<LowerState, LowerDeleter> make_lower_state();
+struct BuildInfo {
+  bool incremental = false;      // the last build copied cached documents' lowered policies
+  uint64_t lowered = 0;          // policies it lowered
+  uint64_t reused = 0;           // policies it copied from the cache
+  const char* why_full = "";     // a full build's reason (first build, hot paths, actions, ...)
+};
+
 // Compiles the tiers. With a cache, unseen documents are parsed on worker threads and reused
-// next time; the image is byte-identical to a build without the cache. `statics`: the image's
-// static entities (cg_compiler_set_entities).
+// next time; without `inc` the image is byte-identical to a build without the cache. `statics`:
+// the image's static entities (cg_compiler_set_entities), `statics_gen` their version. With `inc`
+// a build after a document change lowers only the changed documents: its image decides every
+// request as a fresh build would, but its arenas keep the removed documents' words (not byte-
+// identical to a fresh build).
 std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& tiers, uint64_t epoch,
                                      ParseCache* cache = nullptr, const std::vector<EntityIn>* statics = nullptr,
-                                     std::vector<DocError>* skipped = nullptr);
+                                     std::vector<DocError>* skipped = nullptr, LowerState* inc = nullptr,
+                                     uint64_t statics_gen = 0, BuildInfo* info = nullptr);
 struct RequestIn {
   std::pair<std::string, std::string> principal, action, resource;
   HVal context;  // Record

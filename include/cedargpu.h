@@ -89,8 +89,20 @@ int cg_compiler_clear(cg_compiler* c);
 /* Documents the last build took from the parse cache / parsed anew, and cache entries kept. */
 int cg_compiler_cache_stats(cg_compiler* c, uint64_t* hits, uint64_t* misses, uint64_t* entries);
 /* Compiles all tiers into an image blob (free with cg_free). Unseen documents parse on worker
- * threads; the blob is byte-identical to a build by a fresh compiler. */
+ * threads. A full build's blob is byte-identical to a build by a fresh compiler. After a full
+ * build, a rebuild lowers only the documents the last build did not have (the per-event
+ * PolicySet.Add / Remove of crd.go:62,85,102,114, applied to the lowered image instead of the AST)
+ * and copies every other document's lowered policies: its image decides every request as a fresh
+ * build would, but keeps the removed documents' words until the next full build (not byte-
+ * identical). A rebuild is a full one when the image-wide choices changed (hot attribute paths,
+ * an action table past 64 entries, the static entities) or the arenas hold more garbage than live
+ * words. */
 int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len);
+/* Incremental rebuilds on (default) or off (every build a full one). */
+int cg_compiler_set_incremental(cg_compiler* c, int on);
+/* The last build: *incremental 1 when it reused lowered documents, policies it lowered and reused,
+ * and a full build's reason ("first build", "hot attribute paths changed", "compaction", ...). */
+int cg_compiler_last_build(cg_compiler* c, int* incremental, uint64_t* lowered, uint64_t* reused, const char** why_full);
 /* Number of policies / tiers of a built image blob. */
 int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t* n_tiers, uint64_t* epoch);
 /* Compiled-image shape (no reference counterpart; diagnostics and tests): policies lowered to
