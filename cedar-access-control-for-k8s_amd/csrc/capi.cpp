@@ -168,15 +168,17 @@ void group_requests(cg_batch* b) {
     for (uint32_t i = 0; i < n; i++) tmp[cnt[(key[i] >> sh) & 2047u]++] = key[i];
     key.swap(tmp);
   }
-  std::vector<uint32_t> rows((size_t)n * rw), base(n), slot(n);
+  std::vector<uint32_t> rows((size_t)n * rw), base(n), slot(n), gk(h.gkeys.size());
   parallel_for(n, [&](size_t s) {
     const uint32_t o = (uint32_t)(key[s] & imask);
     std::memcpy(rows.data() + s * rw, h.rows.data() + (size_t)o * rw, (size_t)rw * 4);
     base[s] = h.req_base[o];
     slot[o] = (uint32_t)s;
+    if (!gk.empty()) gk[s] = h.gkeys[o];
   });
   h.rows.swap(rows);
   h.req_base.swap(base);
+  h.gkeys.swap(gk);
   for (auto& it : b->items)
     if (it.dev >= 0) it.dev = (int32_t)slot[(uint32_t)it.dev];
 }

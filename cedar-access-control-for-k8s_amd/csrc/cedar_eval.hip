@@ -78,6 +78,7 @@ struct KArgs {
   // first pass of a grouped batch: launch position -> request (the device sort's order, so that the
   // requests of a wave share scope-index buckets); results stay at the request's own index
   const uint32_t* ord;
+  const uint32_t* __restrict__ grows;  // ... and its rows in that order (launch position k: grows + k * row_words)
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
   uint32_t hlists;  // rows carry element-hash lists (image.h "set-membership keys")
   uint32_t l1filt;  // level-1 probes consult the key filter first (CEDARGPU_L1_FILTER=1: on, A/B)
@@ -88,6 +89,7 @@ struct KArgs {
   const uint32_t* __restrict__ sctx;   // scope bitsets (image.h): context table, rows
   const uint32_t* __restrict__ sbits;
   uint32_t sctx_mask, sbits_words;     // sbits_words 0: the image has none
+  uint32_t l2_vmask, l2_lmask;         // hot slots with level-2 value / list keys (entity-principal combos)
   uint32_t scan_big;    // more scanned buckets than this: straight to the large stage (CEDARGPU_SCAN_BIG)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
@@ -1591,6 +1593,15 @@ constexpr uint32_t SCAN_ANC = 40;
 // key-filter pass: keys per lane per round (independent loads in flight), and the filter-passing
 // keys a request lists in LDS (more: it probes every key, as with the filter off)
 constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
+// contexts a request looks up in the scope-bitset pass (more: it enumerates every key instead), and
+// the flag of a listed key the bitsets found (image.h "scope bitsets")
+constexpr uint32_t CTX_CAP = 16, LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;
+constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the rest read from the row)
+constexpr uint32_t SCAN_PB = 8;    // bit tests per lane per round (loads in flight)
+__device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t k) {  // index of the k-th set bit of m
+  for (uint32_t i = 0; i < k; i++) m &= m - 1;
+  return m ? (uint32_t)__builtin_ctz(m) : 0u;
+}
 // combos whose action / resource component keys on the entity (image.h key_combo)
 constexpr uint32_t combo_mask_of(uint32_t k, uint32_t shift, uint32_t mask) {
   uint32_t m = 0;
@@ -1598,21 +1609,31 @@ constexpr uint32_t combo_mask_of(uint32_t k, uint32_t shift, uint32_t mask) {
     if (((cb >> shift) & mask) == k) m |= 1u << cb;
   return m;
 }
-constexpr uint32_t COMBO_AENT = combo_mask_of(KC_ENT, 2, 1), COMBO_RENT = combo_mask_of(KC_ENT, 3, 3);
-template <uint32_t SEG, uint32_t MINW = 1>
+constexpr uint32_t COMBO_AENT = combo_mask_of(KC_ENT, 2, 1), COMBO_RENT = combo_mask_of(KC_ENT, 3, 3),
+                   COMBO_PENT = combo_mask_of(KC_ENT, 0, 3);
+// BITS: the variant with the scope-bitset pass (launched when a.scan_filt and the image has
+// bitsets); the other one carries none of its registers
+// STATS (CEDARGPU_SCAN_STATS=1, profiling): sums over the launch into a.stats[0..15]: [0] requests
+// [1] level-1 probes [2] level-1 entries found [3] level-2 probes [4] level-2 buckets found
+// [5] loop iterations (per wave) [6] segment iterations spent on level-2 probes [7] segment
+// iterations in all [8] prologue cycles [9] loop cycles (per wave, s_memtime) [10] keys enumerated
+template <uint32_t SEG, uint32_t MINW = 1, bool BITS = false, bool STATS = false>
 __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
+  const uint64_t t0 = STATS ? clock64() : 0;
+  uint32_t st[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // per request: its first SCAN_ANC key ancestors and its hot values, loaded in one round trip
   // before the key loop (the request block and row are cold: each key step would otherwise start
   // with a dependent HBM load)
   // rows padded off a multiple of the 64 LDS banks: the segments of a wave index them in lockstep
-  // (an image with scope bitsets stages the ancestors' key-entity indices instead of their UIDs)
-  __shared__ union {
-    uint2 anc[64 / SEG][SCAN_ANC + 1];
-    uint32_t kid[64 / SEG][SCAN_ANC + 2];  // [0]: the principal itself, [j]: key ancestor j - 1
-  } s_st;
-  auto& s_anc = s_st.anc;
-  __shared__ uint2 s_hot[64 / SEG][NHOT + 1];
-  __shared__ uint16_t s_pos[64 / SEG][SCAN_POS + 2];
+  constexpr uint32_t ANC_ST = BITS ? 32u : SCAN_ANC;  // principal key ancestors staged (UIDs)
+  __shared__ uint2 s_anc[64 / SEG][ANC_ST + 1];
+  __shared__ uint2 s_hot[64 / SEG][SCAN_HOT + 1];  // the first SCAN_HOT hot values
+  // BITS: the key-entity index of the principal ([0]) and of each staged key ancestor ([j]: j - 1),
+  // the request's contexts (combo | hs << 8, v0, v1, bitset row) and its listed keys
+  // (LIST_EXACT | context << 16 | principal index, or combo << 11 | principal index)
+  __shared__ uint32_t s_kid[BITS ? 64 / SEG : 1][SCAN_ANC + 2];
+  __shared__ uint4 s_cx[BITS ? 64 / SEG : 1][CTX_CAP];
+  __shared__ uint32_t s_pos[BITS ? 64 / SEG : 1][SCAN_POS_B + 2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
@@ -1620,8 +1641,8 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   auto sbcast = [&](uint32_t x, uint32_t k) -> uint32_t { return (uint32_t)__shfl((int)x, (int)(sbase + k)); };
   const uint32_t gid_ = blockIdx.x * (64 / SEG) + seg;
   const bool valid = gid_ < a.n_req;
-  const uint32_t gid = valid ? (a.ord ? a.ord[gid_] : gid_) : 0u;  // the request (its list and row)
-  const uint32_t* row = a.rows + (size_t)gid * a.row_words;
+  const uint32_t gid = valid ? (a.ord ? a.ord[gid_] : gid_) : 0u;  // the request (its list and results)
+  const uint32_t* row = a.grows ? a.grows + (size_t)(valid ? gid_ : 0u) * a.row_words : a.rows + (size_t)gid * a.row_words;
   const uint32_t rw = (valid && sl < RW_HDR) ? row[sl] : 0u;
   const uint32_t rw_hi = (SEG < RW_HDR && valid && SEG + sl < RW_HDR) ? row[SEG + sl] : 0u;
   auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
@@ -1641,20 +1662,31 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   uint32_t* pairs = a.scan + a.scan_n + (size_t)gid * (2 * SCAN_CAP);
   // scope-bitset pass (image.h "scope bitsets"): the principal's list carries the kidx of its owner
   // and key ancestors after its pairs (p_anc == 0: the principal has no entity, no list)
-  const bool kbits = a.scan_filt && a.sbits_words != 0;
+  const bool kbits = BITS && a.scan_filt && a.sbits_words != 0;
   const bool klist = kbits && valid && p_anc != 0;
-  const bool stl = a.scan_lds != 0 && !kbits;  // UIDs in LDS (no bitsets) for the key loop
+  const bool stl = a.scan_lds != 0;  // UIDs in LDS for the key loop
+  const uint32_t nk = (pn >> AN_KEYS_SHIFT) & AN_KEYS;
+  constexpr uint32_t LW = 3;  // list elements loaded with a list head
+  uint32_t l_lo = 0, l_hd = 0, l_w[LW] = {0, 0, 0};
   {
-    const uint32_t nk = (pn >> AN_KEYS_SHIFT) & AN_KEYS;
     if (stl) {
-      const uint32_t n_st = valid ? min(nk, SCAN_ANC) : 0u;
+      const uint32_t n_st = valid ? min(nk, ANC_ST) : 0u;
       for (uint32_t j = sl; j < n_st; j += SEG)
         s_anc[seg][j] = make_uint2(__builtin_nontemporal_load(blk + p_anc + 2 * j), __builtin_nontemporal_load(blk + p_anc + 2 * j + 1));
-    } else if (klist) {
-      const uint32_t* kl = blk + p_anc + 2 * (pn & AN_COUNT);
-      for (uint32_t j = sl; j <= min(nk, SCAN_ANC); j += SEG) s_st.kid[seg][j] = __builtin_nontemporal_load(kl + j);
     }
-    for (uint32_t h = sl; h < a.n_hot; h += SEG)
+    if (BITS && klist) {
+      const uint32_t* kl = blk + p_anc + 2 * (pn & AN_COUNT);
+      for (uint32_t j = sl; j <= min(nk, SCAN_ANC); j += SEG) s_kid[seg][j] = __builtin_nontemporal_load(kl + j);
+    }
+    // BITS: lane k < popc(l2_lmask) reads the k-th list slot's head and first LW words after it
+    // (element count or marker, elements) in the same trip
+    if (BITS && klist && a.hlists && sl < (uint32_t)__builtin_popcount(a.l2_lmask)) {
+      l_lo = row[RW_HDR + 2 * a.n_hot + nth_bit(a.l2_lmask, sl)];
+      l_hd = blk[l_lo];
+#pragma unroll
+      for (uint32_t k = 0; k < LW; k++) l_w[k] = blk[l_lo + 1 + k];  // (past a short list: its block's next words)
+    }
+    for (uint32_t h = sl; h < min(a.n_hot, SCAN_HOT); h += SEG)
       s_hot[seg][h] = valid ? *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h) : make_uint2(0u, 0u);
     wave_lds_sync();
   }
@@ -1678,19 +1710,20 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       ip = j - t2 * np_; ia = t2 % na_; ir = t2 / na_;
     }
     const uint32_t jp = ip + 1 - (pn >> 31);  // 0: the principal itself, j: ancestor j - 1
-    p = (stl && pkc == KC_ENT && jp && jp <= SCAN_ANC) ? s_anc[seg][jp - 1] : key_comp(pkc, jp, pt, pi, blk, p_anc);
+    p = (stl && pkc == KC_ENT && jp && jp <= ANC_ST) ? s_anc[seg][jp - 1] : key_comp(pkc, jp, pt, pi, blk, p_anc);
     q = key_comp(akc, ia + 1 - (an >> 31), at, ai, blk, a_anc);
     r = key_comp(rkc, ir + 1 - (rn >> 31), rt, ri, blk, r_anc);
     cbo = combo;
   };
-  // Scope-bitset pass. When every used combo's action / resource component is the request's own
-  // UID, its one key ancestor, its type or a wildcard (nA, nR <= 1: the k8s SAR shape), a combo
-  // whose principal component is an entity has one context (combo, action, resource): one lookup in
-  // the small context table gives its bitset row, and each of the principal's key ancestors costs
-  // one bit test in that row (kidx staged in LDS; the grouped requests of a wave share the row).
-  // Only keys whose bit is set, and the single keys of the other combos, are listed (as
-  // combo << 11 | principal index) and probe the scope table's 64-byte slots below: ~6 of ~62 per
-  // request on C3's group DAG instead of all of them.
+  // Scope-bitset pass (image.h "scope bitsets"). When every used combo's action / resource
+  // component is the request's own UID, its one key ancestor, its type or a wildcard (nA, nR <= 1:
+  // the k8s SAR shape), each entity-principal combo has a handful of contexts: level 1 and, per hot
+  // slot with level-2 keys, the request's value (or each element of its list). The segment's lanes
+  // look them up in the context table side by side, then test one bit per (found context,
+  // principal key ancestor) pair, all loads of a round in flight at once; only the keys whose bit
+  // is set are listed (LIST_EXACT) and probed below, once each, with no level-2 descent. The single
+  // keys of the other combos (principal type or wildcard) are listed as combo << 11 and walk both
+  // levels as before.
   const uint32_t simple = valid && (!(cm & COMBO_AENT) || nA <= 1u) && (!(cm & COMBO_RENT) || nR <= 1u) && nP < 2048u;
   const uint2 ka1 = (simple && nA == 1u) ? key_comp(KC_ENT, 1u - (an >> 31), at, ai, blk, a_anc) : make_uint2(KW_ANY, KW_ANY);
   const uint2 kr1 = (simple && nR == 1u) ? key_comp(KC_ENT, 1u - (rn >> 31), rt, ri, blk, r_anc) : make_uint2(KW_ANY, KW_ANY);
@@ -1699,71 +1732,131 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     const uint32_t rkc = cb >> 3;
     return rkc == KC_ENT ? kr1 : (rkc == KC_TYPE ? make_uint2(rt, KW_ANY) : make_uint2(KW_ANY, KW_ANY));
   };
-  auto comb_cnt = [&](uint32_t cb) -> uint32_t {
-    return ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
-  };
   // principal component ip of a combo's keys (0: the UID itself when it is a key entity)
   auto comb_p = [&](uint32_t cb, uint32_t ip) -> uint2 {
     const uint32_t pkc = cb & 3;
     if (pkc != KC_ENT) return key_comp(pkc, 0u, pt, pi, blk, p_anc);
-    return key_comp(KC_ENT, ip + 1 - (pn >> 31), pt, pi, blk, p_anc);
+    const uint32_t jp = ip + 1 - (pn >> 31);
+    return (stl && jp && jp <= ANC_ST) ? s_anc[seg][jp - 1] : key_comp(KC_ENT, jp, pt, pi, blk, p_anc);
   };
   uint32_t npos = 0;
-  if (kbits && __ballot(klist && simple) != 0) {
-    const bool on = klist && simple;
-    for (uint32_t m = cm; m; m &= m - 1) {  // wave-uniform: the image's combos
-      const uint32_t cb = __builtin_ctz(m);
-      const uint32_t cnt = on ? comb_cnt(cb) : 0u;
-      if (__ballot(cnt != 0) == 0) continue;
-      if ((cb & 3) != KC_ENT) {  // one key (principal type or wildcard): listed as is
-        if (cnt && sl == 0 && npos < SCAN_POS) s_pos[seg][npos] = (uint16_t)(cb << 11);
-        npos += cnt != 0;
-        continue;
-      }
-      // the context's bitset row: one probe chain in the context table (segment-uniform)
-      const uint2 q = comb_q(cb), r = comb_r(cb);
-      uint32_t row_ = KIDX_NONE;
-      if (cnt)
-        for (uint32_t h = ctx_hash(key_pre(cb, q.x, q.y, r.x, r.y)) & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
-          const uint4 x = *reinterpret_cast<const uint4*>(a.sctx + (size_t)h * SCTX_WORDS);
-          if (x.x == 0) break;
-          const uint2 y = *reinterpret_cast<const uint2*>(a.sctx + (size_t)h * SCTX_WORDS + 4);
-          if (x.x == (SCTX_USED | cb) && x.y == q.x && x.z == q.y && x.w == r.x && y.x == r.y) { row_ = y.y; break; }
-        }
-      const uint32_t* rowb = a.sbits + (size_t)(row_ == KIDX_NONE ? 0u : row_) * a.sbits_words;
-      const uint32_t lim = row_ == KIDX_NONE ? 0u : cnt;
-      const uint32_t self = pn >> 31;
-      for (uint32_t rb = 0; __ballot(rb < lim) != 0; rb += SEG * SCAN_PU) {
-        uint32_t fw[SCAN_PU], fk[SCAN_PU];
+  bool flt = false;
+  if (BITS && __ballot(kbits && klist && simple) != 0) {
+    bool on = kbits && klist && simple;
+    const uint32_t vm = a.l2_vmask, lm = a.l2_lmask, pe = cm & COMBO_PENT;  // wave-uniform
+    const uint32_t nvs = __builtin_popcount(vm), nls = __builtin_popcount(lm), ncb = __builtin_popcount(pe);
+    const uint32_t lc = (on && sl < nls && a.hlists) ? ((l_hd & 0x80000000u) ? 1u : l_hd) : 0u;  // list entries
+    uint32_t linc = lc;  // inclusive prefix over the segment's lanes
+    for (uint32_t o = 1; o < SEG; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)linc, o);
+      if (sl >= o) linc += y;
+    }
+    const uint32_t per = 1u + nvs + sbcast(linc, SEG - 1), nctx = ncb * per;
+    on = on && nctx <= CTX_CAP;
+    // the contexts, looked up side by side (lane j % SEG takes context j); a found one is kept
+    uint32_t nf = 0;  // contexts found (segment-uniform)
+    for (uint32_t j0 = 0; __ballot(on && j0 < nctx) != 0; j0 += SEG) {
+      const uint32_t j = j0 + sl;
+      uint32_t cb = 0, hs = SCTX_L1, v0 = 0, v1 = 0, row_ = KIDX_NONE;
+      const uint32_t ci = on ? j / per : 0u, t = on ? j - ci * per : 0u;
+      // (the list entry, by shuffles from the lane that read its slot: every lane takes part)
+      uint32_t li = 0, lb = 0, llo = 0, lhd = 0, lw = 0;
+      for (uint32_t k = 0; k < nls; k++) {
+        const uint32_t inc_k = sbcast(linc, k), c_k = sbcast(lc, k);
+        const uint32_t u = t - 1 - nvs;
+        const bool mine = t > nvs && u < inc_k && u >= inc_k - c_k;
+        uint32_t w = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < SCAN_PU; u++) {
-          const uint32_t ip = rb + u * SEG + sl;
-          const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
-          fw[u] = 0xFFFFFFFFu;  // a key whose kidx is not staged passes untested
-          fk[u] = 0;
-          if (ip < lim && jk <= SCAN_ANC) {
-            const uint32_t kid = s_st.kid[seg][jk];
-            fk[u] = kid;
-            fw[u] = kid == KIDX_NONE ? 0u : rowb[kid >> 5];
+        for (uint32_t q = 0; q < LW; q++) {
+          const uint32_t wq = sbcast(l_w[q], k);
+          if (mine && u - (inc_k - c_k) == q) w = wq;
+        }
+        const uint32_t lo_k = sbcast(l_lo, k), hd_k = sbcast(l_hd, k);
+        if (mine) { li = k; lb = inc_k - c_k; llo = lo_k; lhd = hd_k; lw = w; }
+      }
+      if (on && j < nctx) {
+        cb = nth_bit(pe, ci);
+        if (t > 0 && t <= nvs) {
+          hs = nth_bit(vm, t - 1);
+          const uint2 v = hs < SCAN_HOT ? s_hot[seg][hs] : *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * hs);
+          v0 = hot_ok(v) ? v.x : MISSING_W0;
+          v1 = hot_ok(v) ? v.y : 0u;
+        } else if (t > nvs) {
+          hs = nth_bit(lm, li) | BT_CKEY;
+          const uint32_t e = t - 1 - nvs - lb;
+          if (lhd & 0x80000000u) v0 = lhd == CL_MISSING ? MISSING_W0 : NOTSET_W0;
+          else { v0 = e < LW ? lw : blk[llo + 1 + e]; v1 = 1; }
+        }
+        const uint2 q = comb_q(cb), r = comb_r(cb);
+        for (uint32_t h = ctx_key(key_pre(cb, q.x, q.y, r.x, r.y), hs, v0, v1) & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
+          const uint4* e = reinterpret_cast<const uint4*>(a.sctx + (size_t)h * SCTX_WORDS);
+          const uint4 x = e[0], y = e[1], z = e[2];
+          if (x.x == 0) break;
+          if (x.x == (SCTX_USED | cb) && x.y == q.x && x.z == q.y && x.w == r.x && y.x == r.y && y.y == hs && y.z == v0 &&
+              y.w == v1) {
+            row_ = z.x;
+            break;
           }
         }
-#pragma unroll
-        for (uint32_t u = 0; u < SCAN_PU; u++) {
-          const uint32_t ip = rb + u * SEG + sl;
-          const bool ok = ip < lim && ((fw[u] >> (fk[u] & 31)) & 1u);
-          const uint64_t mk = sballot(ok);
-          const uint32_t at_ = npos + mbcnt64(mk);
-          if (ok && at_ < SCAN_POS) s_pos[seg][at_] = (uint16_t)((cb << 11) | ip);
-          npos += popc64(mk);
-        }
       }
+      const bool got = on && j < nctx && row_ != KIDX_NONE;
+      const uint64_t mk = sballot(got);
+      if (got) s_cx[seg][nf + mbcnt64(mk)] = make_uint4(cb | (hs << 8), v0, v1, row_);
+      nf += popc64(mk);
     }
     wave_lds_sync();
+    // (found context, key ancestor) pairs: ip 0 .. nP - 1 under each; a set bit lists the key. All
+    // SCAN_PB loads of a lane's round in flight at once.
+    const uint32_t self = pn >> 31, tot = on ? nf * nP : 0u;
+    const uint32_t* kl = blk + p_anc + 2 * (pn & AN_COUNT);
+    for (uint32_t rb = 0; __ballot(rb < tot) != 0; rb += SEG * SCAN_PB) {
+      uint32_t fw[SCAN_PB], fk[SCAN_PB];
+#pragma unroll
+      for (uint32_t u = 0; u < SCAN_PB; u++) {
+        const uint32_t t = rb + u * SEG + sl;
+        fw[u] = 0;
+        fk[u] = 0;
+        if (t < tot) {
+          const uint32_t j = t / nP, ip = t - j * nP;
+          const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
+          const uint32_t kid = jk <= SCAN_ANC ? s_kid[seg][jk] : kl[jk];
+          fk[u] = kid;
+          if (kid != KIDX_NONE) fw[u] = a.sbits[(size_t)s_cx[seg][j].w * a.sbits_words + (kid >> 5)];
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < SCAN_PB; u++) {
+        const uint32_t t = rb + u * SEG + sl;
+        const bool ok = (fw[u] >> (fk[u] & 31)) & 1u;
+        const uint64_t mk = sballot(ok);
+        const uint32_t at_ = npos + mbcnt64(mk);
+        if (ok && at_ < SCAN_POS_B) {
+          const uint32_t j = t / nP;
+          s_pos[seg][at_] = LIST_EXACT | (j << 16) | (t - j * nP);
+        }
+        npos += popc64(mk);
+      }
+    }
+    // the other combos' single keys
+    for (uint32_t m = cm & ~COMBO_PENT; m; m &= m - 1) {
+      if (on && sl == 0 && npos < SCAN_POS_B) s_pos[seg][npos] = __builtin_ctz(m) << 11;
+      npos += on ? 1u : 0u;
+    }
+    wave_lds_sync();
+    // a request off the simple shape, with more contexts or listed keys than the lists hold, or
+    // more key ancestors than are staged, enumerates every key instead
+    flt = on && npos <= SCAN_POS_B;
+    if (STATS && sl == 0 && valid) {
+      st[11] += flt;
+      st[12] += nf;
+      st[13] += on ? 1u : 0u;
+      st[14] += npos;
+      st[15] += (kbits && klist && simple) ? 1u : 0u;
+    }
   }
-  // a request off the simple shape, or with more listed keys than the list holds, enumerates every
-  // key instead
-  const bool flt = klist && simple && npos <= SCAN_POS;
   const uint32_t n_l1 = flt ? npos : n_keys;
+  const uint64_t t1 = STATS ? clock64() : 0;
+  if (STATS && valid && sl == 0) { st[0] = 1; st[10] = n_keys; }
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);
@@ -1772,13 +1865,18 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     const bool l2 = sballot(hm != 0 || csl != 0 || ck < cn) != 0;
     const bool done = !l2 && kb >= n_l1;
     if (__ballot(!done) == 0) break;
+    if (STATS) {
+      if (lane == 0) st[5]++;
+      if (sl == 0 && !done) { st[7]++; if (l2) st[6]++; }
+    }
     uint3 e = make_uint3(0, 0, 0);
     if (!done) {
       if (l2) {
+        if (STATS && (hm || csl || ck < cn)) st[3]++;
         if (hm) {
           const uint32_t h = __builtin_ctz(hm);
           hm &= hm - 1;
-          const uint2 v = stl ? s_hot[seg][h] : *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h);
+          const uint2 v = h < SCAN_HOT ? s_hot[seg][h] : *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h);
           const uint32_t v0 = hot_ok(v) ? v.x : MISSING_W0, v1 = hot_ok(v) ? v.y : 0u;
           const uint32_t h2 = bucket_hash2(h1, h, v0, v1);
           if (l2_bloom_maybe(blm, h2) && (!a.l2filt || filt_maybe(a.bfilt, a.fmask, h2)))
@@ -1817,9 +1915,15 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         const uint32_t kk = kb + sl;
         kb += SEG;
         if (kk < n_l1) {
-          if (flt) {
-            const uint32_t x = s_pos[seg][kk];
-            combo = x >> 11;
+          uint32_t x = 0;
+          if (BITS && flt) {
+            x = s_pos[seg][kk];
+            if (x & LIST_EXACT) {
+              const uint4 c = s_cx[seg][(x >> 16) & 0x7FFFu];
+              combo = c.x & 0xFFu;
+            } else {
+              combo = x >> 11;
+            }
             kp = comb_p(combo, x & 0x7FFu);
             ka = comb_q(combo);
             kr = comb_r(combo);
@@ -1829,13 +1933,22 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           w0 = BT_USED | (combo << 16);
           h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
           uint32_t cmv = 0;
-          if (flt || !a.l1filt || filt_maybe(a.bfilt, a.fmask, h1))
+          if (BITS && (x & LIST_EXACT)) {  // a key the bitsets found: probed once, no descent
+            const uint4 c = s_cx[seg][(x >> 16) & 0x7FFFu];
+            const uint32_t hs = c.x >> 8;
+            if (hs == SCTX_L1) e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, nullptr, nullptr, a.slot_split);
+            else e = probe(a.btab, a.bmask, bucket_hash2(h1, hs, c.y, c.z), w0 | BT_L2 | hs, kp, ka, kr, c.y, c.z, unused, nullptr, nullptr, a.slot_split);
+            e.z = 0;
+          } else if (flt || !a.l1filt || filt_maybe(a.bfilt, a.fmask, h1)) {
             e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, &blm, &cmv, a.slot_split);
+          }
           hm = e.z;
           csl = cmv;
+          if (STATS) { st[1]++; if (e.y || hm || csl) st[2]++; }
         }
       }
     }
+    if (STATS && l2 && e.y) st[4]++;
     // found buckets go to the request's list in segment order
     const uint64_t m = sballot(e.y != 0);
     const uint32_t pos = nb + mbcnt64(m);
@@ -1844,6 +1957,15 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     nb += popc64(m);
   }
   if (valid && sl == 0) a.scan[gid] = nb <= SCAN_CAP ? nb : SCAN_OVF;
+  if (STATS) {
+    const uint64_t t2 = clock64();
+    if (lane == 0) { st[8] = (uint32_t)(t1 - t0); st[9] = (uint32_t)(t2 - t1); }
+    for (uint32_t i = 0; i < 16; i++) {
+      uint32_t x = st[i];
+      for (uint32_t o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, (int)o);
+      if (lane == 0 && x) atomicAdd(a.stats + i, (unsigned long long)x);
+    }
+  }
 }
 
 // SEG lanes evaluate one request; a wave carries 64 / SEG requests whose dependent access chains
@@ -1886,7 +2008,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const bool valid = gid < n_req;
   const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0u;
   const uint32_t wo = a.req_idx ? gid : r;  // result slot: the worklist entry, or the request itself
-  const uint32_t* row = a.rows + (size_t)r * a.row_words;
+  const uint32_t* row = (a.grows && !a.req_idx) ? a.grows + (size_t)(valid ? gid : 0u) * a.row_words : a.rows + (size_t)r * a.row_words;
 
   // the request row streams through once: non-temporal loads, header broadcast in the segment
   const uint32_t rw = (valid && sl < RW_HDR) ? __builtin_nontemporal_load(row + sl) : 0u;
@@ -2368,6 +2490,8 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS);
   d.sctx_mask = (uint32_t)(img.sctx.size() / SCTX_WORDS) - 1;
   d.sbits_words = img.sbits_words;
+  d.l2_vmask = img.l2_vmask;
+  d.l2_lmask = img.l2_lmask;
   d.gstr_bytes = at(DS_GSTR_BYTES);
   d.n_static = img.n_static();
   d.lane_need = img.lane_need;
@@ -2389,13 +2513,17 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
 // One thread per scope-index entry: claims the first free slot of its key's linear-probe chain
 // (compare-and-swap of the slot's first word, never 0 in a used slot) and writes the rest. Keys
 // are distinct, so any insertion order yields a table every probe (probe()) resolves alike.
+// Two launches: level-1 entries (every request probes them) first, so that they head their probe
+// chains and a level-2 entry never lengthens a level-1 probe (as the host-built tables had it;
+// one mixed launch cost the C3 scan ~5 %, profiles/r03/bis).
 __global__ void __launch_bounds__(256) cedar_btab_build(const uint32_t* __restrict__ ent, uint32_t n,
-                                                        uint32_t* __restrict__ tab, uint32_t mask) {
+                                                        uint32_t* __restrict__ tab, uint32_t mask, uint32_t level2) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint4* e = reinterpret_cast<const uint4*>(ent + (size_t)i * BT_WORDS);
   const uint4 a = e[0], b = e[1], c = e[2], d = e[3];
   if (a.x == 0) return;  // the placeholder of an image without entries
+  if (((a.x & BT_L2) != 0) != (level2 != 0)) return;
   const uint32_t combo = (a.x & ~BT_USED) >> 16;
   uint32_t h = key_hash(combo, a.y, a.z, a.w, b.x, b.y, b.z);
   if (a.x & BT_L2) h = bucket_hash2(h, a.x & 0xFFu & ~BT_L2, b.w, c.x);
@@ -2417,7 +2545,8 @@ static int build_btab(const Image& img, DevImage& d) {
   hipError_t e = hipMalloc(&d.btab_mem, bytes);
   if (e == hipSuccess) e = hipMemsetAsync(d.btab_mem, 0, bytes, s);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(cedar_btab_build, dim3((n + 255) / 256), dim3(256), 0, s, d.btab, n, (uint32_t*)d.btab_mem, d.bmask);
+    for (uint32_t l2 = 0; l2 < 2; l2++)
+      hipLaunchKernelGGL(cedar_btab_build, dim3((n + 255) / 256), dim3(256), 0, s, d.btab, n, (uint32_t*)d.btab_mem, d.bmask, l2);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -2575,10 +2704,14 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.capr = b.capr;
   d.cape = b.cape;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const void* src[5] = {b.heap.data(), b.req_base.data(), b.rows.data(), b.bstr_off.data(), b.bstr_bytes.data()};
-  const size_t len[5] = {b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.bstr_off.size() * 4, b.bstr_bytes.size()};
-  size_t off[5], in_bytes = 0;
-  for (int k = 0; k < 5; k++) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
+  // the grouping keys travel only when the step groups the batch on the device
+  const bool grp = b.dev_group && b.n() >= 2 && b.gkeys.size() == b.n();
+  constexpr int NSEC = 6;
+  const void* src[NSEC] = {b.heap.data(), b.req_base.data(), b.rows.data(), b.bstr_off.data(), b.bstr_bytes.data(), b.gkeys.data()};
+  const size_t len[NSEC] = {b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.bstr_off.size() * 4, b.bstr_bytes.size(),
+                            grp ? b.gkeys.size() * 4 : 0};
+  size_t off[NSEC], in_bytes = 0;
+  for (int k = 0; k < NSEC; k++) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
   const size_t n = std::max<uint32_t>(b.n(), 1);
   // The probe kernel writes only the deciding reason list (into reasons_f; reasons_p aliases it),
   // the policy-stream kernel both lists: an indexed image's first pass needs one array.
@@ -2636,21 +2769,21 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     }
     d.scan = (uint32_t*)d.scan_blk;
   }
-  if (b.dev_group && b.n() >= 2) {  // the device grouping's order, keys, values and sort storage
+  if (grp) {  // the device grouping's order, grouped rows, bucket counters and scan storage
     const size_t tb = group_temp_bytes(b.n());
-    const size_t q = ((size_t)b.n() * 4 + 255) & ~(size_t)255;
+    const size_t q = ((size_t)b.n() * 4 + 255) & ~(size_t)255, rq = al((size_t)b.n() * b.row_words * 4);
     if (!tb) { g_err = "rocPRIM radix sort: no temporary storage size"; pool_put(pool, false, d.lane_blk, d.lane_cls); pool_put(pool, false, d.scan_blk, d.scan_cls); return -4; }
-    if ((rc = pool_get(pool, false, 4 * q + tb, &d.grp_blk, &d.grp_cls))) {
+    if ((rc = pool_get(pool, false, 3 * q + rq + tb, &d.grp_blk, &d.grp_cls))) {
       pool_put(pool, false, d.lane_blk, d.lane_cls);
       pool_put(pool, false, d.scan_blk, d.scan_cls);
       return rc;
     }
     uint8_t* g8 = (uint8_t*)d.grp_blk;
     d.ord = (uint32_t*)g8;
-    d.gkeys = (uint32_t*)(g8 + q);
-    d.gkeys2 = (uint32_t*)(g8 + 2 * q);
-    d.gvals = (uint32_t*)(g8 + 3 * q);
-    d.grp_temp = g8 + 4 * q;
+    d.gkeys2 = (uint32_t*)(g8 + q);
+    d.gvals = (uint32_t*)(g8 + 2 * q);
+    d.grows = (uint32_t*)(g8 + 3 * q);
+    d.grp_temp = g8 + 3 * q + rq;
     d.grp_temp_bytes = tb;
   }
   if ((rc = pool_get(pool, false, in_bytes, &d.in_blk, &d.in_cls))) {
@@ -2678,15 +2811,15 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // Large batches (admission objects run to ~600 B per request) are staged by several threads:
   // one core's memcpy into pinned memory runs at ~10 GB/s.
   size_t total_len = 0;
-  for (int k = 0; k < 5; k++) total_len += len[k];
+  for (int k = 0; k < NSEC; k++) total_len += len[k];
   const unsigned nt = total_len >= (8u << 20) ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
   if (nt <= 1) {
-    for (int k = 0; k < 5; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
+    for (int k = 0; k < NSEC; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
   } else {
     auto part = [&](unsigned t) {  // byte range [t, t+1) / nt of the concatenated sections
       const size_t lo = total_len * t / nt, hi = total_len * (t + 1) / nt;
       size_t pos = 0;
-      for (int k = 0; k < 5; k++) {
+      for (int k = 0; k < NSEC; k++) {
         const size_t a = std::max(lo, pos), b = std::min(hi, pos + len[k]);
         if (a < b) std::memcpy(st + off[k] + (a - pos), (const uint8_t*)src[k] + (a - pos), b - a);
         pos += len[k];
@@ -2704,6 +2837,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.rows = (uint32_t*)(in + off[2]);
   d.bstr_off = (uint32_t*)(in + off[3]);
   d.bstr_bytes = in + off[4];
+  if (grp) d.gkeys = (const uint32_t*)(in + off[5]);
   d.res = (uint32_t*)(o + o_res);
   d.reasons_f = (uint32_t*)(o + o_rf);
   d.reasons_p = (uint32_t*)(o + o_rp);
@@ -2875,6 +3009,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.sctx = img.sctx; k.sbits = img.sbits; k.sctx_mask = img.sctx_mask; k.sbits_words = img.sbits_words;
+  k.l2_vmask = img.l2_vmask; k.l2_lmask = img.l2_lmask;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
   k.lane = b.lane; k.lane_stride = img.lane_need;
@@ -2890,7 +3025,9 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.slot_split = slot_split;
   static const uint32_t scan_lds = [] { const char* e = std::getenv("CEDARGPU_SCAN_LDS"); return (e && *e == '0') ? 0u : 1u; }();
   k.scan_lds = scan_lds;
-  static const uint32_t scan_filt = [] { const char* e = std::getenv("CEDARGPU_SCAN_FILT"); return (e && *e == '0') ? 0u : 1u; }();
+  // off by default: on C3 the bitset pass's extra dependent round trips cost more than the probes
+  // it saves (scan 1.41 vs 1.11 ms per 1M, profiles/r03/ab5)
+  static const uint32_t scan_filt = [] { const char* e = std::getenv("CEDARGPU_SCAN_FILT"); return (e && *e == '1') ? 1u : 0u; }();
   k.scan_filt = scan_filt;
   // 48: C3 DAG 4.91e8 decisions/s at 32..96 alike; a list of 24 that sent every longer one to the
   // large stage measured 4.58e8 (43,485 large-stage requests instead of 25,005; profiles/r02/ab_scan_cap)
@@ -2899,6 +3036,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.stats = nullptr;
   k.n_dev = nullptr;
   k.ord = nullptr;
+  k.grows = nullptr;
   k.scan = nullptr;
   k.scan_n = 0;
   return k;
@@ -2988,7 +3126,31 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     static const uint32_t socc = [] { const char* e = std::getenv("CEDARGPU_SCAN_OCC"); return e ? (uint32_t)std::atoi(e) : 6u; }();
     static const uint32_t cocc = [] { const char* e = std::getenv("CEDARGPU_CAND_OCC"); return e ? (uint32_t)std::atoi(e) : 4u; }();
     const dim3 sg((n + 7) / 8), sb(64);
+    static const bool sstats = std::getenv("CEDARGPU_SCAN_STATS") != nullptr;
     if (k.req_idx) {  // a follow-up over the first pass's requests: their buckets are scanned
+    } else if (sstats) {
+      unsigned long long* d = nullptr;
+      std::vector<unsigned long long> h(16, 0);
+      if (hipMalloc((void**)&d, 16 * 8) == hipSuccess) {
+        KArgs ks = k;
+        ks.stats = d;
+        (void)hipMemsetAsync(d, 0, 16 * 8, s);
+        if (k.scan_filt && k.sbits_words) hipLaunchKernelGGL((cedar_scan_kernel<8, 6, true, true>), sg, sb, 0, s, ks);
+        else hipLaunchKernelGGL((cedar_scan_kernel<8, 6, false, true>), sg, sb, 0, s, ks);
+        (void)hipMemcpyAsync(h.data(), d, 16 * 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(d);
+        const double r = h[0] ? (double)h[0] : 1.0, w = (double)sg.x;
+        std::fprintf(stderr,
+                     "scan stats: requests %llu | per request: keys %.2f L1 probes %.2f found %.2f | L2 probes %.2f found %.2f | "
+                     "per wave: iterations %.2f, segment-iterations %.2f (L2 %.2f) | cycles prologue %.0f loop %.0f | bitsets: "
+                     "eligible %llu within caps %llu listed-path %llu, contexts found %.2f listed %.2f per request\n",
+                     h[0], h[10] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[5] / w, h[7] / w, h[6] / w, h[8] / w, h[9] / w,
+                     h[15], h[13], h[11], h[12] / r, h[14] / r);
+      }
+    } else if (k.scan_filt && k.sbits_words) {
+      if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6, true>), sg, sb, 0, s, k);
+      else hipLaunchKernelGGL((cedar_scan_kernel<8, 1, true>), sg, sb, 0, s, k);
     } else if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8>), sg, sb, 0, s, k);
     else if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6>), sg, sb, 0, s, k);
     else hipLaunchKernelGGL((cedar_scan_kernel<8>), sg, sb, 0, s, k);
@@ -3072,13 +3234,13 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
   k.scan = b.scan;
   k.scan_n = b.n;
-  if (b.ord) {  // grouped batch: this step's order, from the rows as uploaded (group.hip)
-    if (group_enqueue(b.rows, b.heap, b.n, b.row_words, img.n_hot, b.gkeys, b.gkeys2, b.gvals, b.ord, b.grp_temp,
-                      b.grp_temp_bytes, s)) {
-      g_err = "request grouping (rocPRIM radix sort) failed";
+  if (b.ord) {  // grouped batch: this step's order and its rows in that order (group.hip)
+    if (group_enqueue(b.gkeys, b.rows, b.n, b.row_words, b.grows, b.ord, b.gkeys2, b.gvals, b.grp_temp, b.grp_temp_bytes, s)) {
+      g_err = "request grouping failed";
       return -4;
     }
     k.ord = b.ord;
+    k.grows = b.grows;
   }
   mark(PH_GROUP, s);
   const bool two = img.indexed && split_on() && !probe_stats() && probe_seg() == 8 && probe_occ() == 3;

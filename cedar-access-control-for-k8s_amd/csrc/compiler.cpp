@@ -1276,17 +1276,34 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     }
   }
   mark("buckets");
-  // scope bitsets (image.h): a row per (combo, action, resource) context of the level-1 keys whose
-  // principal component is an entity, a bit per key entity
+  // scope bitsets (image.h "scope bitsets"): a row per context of the keys whose principal
+  // component is an entity, a bit per key entity: level-1 keys that file policies directly, and
+  // every level-2 key
   {
-    std::map<std::array<uint32_t, 5>, uint32_t> ctx;
+    std::map<std::array<uint32_t, 8>, uint32_t> ctx;
     std::vector<std::pair<uint32_t, uint32_t>> bits;  // (row, kidx)
+    auto kidx = [&](uint32_t t, uint32_t i) {
+      const uint64_t u = ((uint64_t)t << 32) | i;
+      return (uint32_t)(std::lower_bound(img.key_ents.begin(), img.key_ents.end(), u) - img.key_ents.begin());
+    };
+    img.l2_vmask = img.l2_lmask = 0;
     for (const G& g : g1) {
       const L1& k = r1[g.b].first;
       if ((k[0] & 3) != KC_ENT) continue;
-      const uint32_t row = ctx.emplace(std::array<uint32_t, 5>{k[0], k[3], k[4], k[5], k[6]}, (uint32_t)ctx.size()).first->second;
-      const uint64_t u = ((uint64_t)k[1] << 32) | k[2];
-      bits.emplace_back(row, (uint32_t)(std::lower_bound(img.key_ents.begin(), img.key_ents.end(), u) - img.key_ents.begin()));
+      img.l2_vmask |= g.hmask;
+      img.l2_lmask |= g.cmask;
+      bool direct = false;
+      for (size_t i = g.b; i < g.e && !direct; i++) direct = r1[i].second != NO_POLICY;
+      if (!direct) continue;
+      const uint32_t row = ctx.emplace(std::array<uint32_t, 8>{k[0], k[3], k[4], k[5], k[6], SCTX_L1, 0u, 0u}, (uint32_t)ctx.size()).first->second;
+      bits.emplace_back(row, kidx(k[1], k[2]));
+    }
+    for (const G& g : g2) {
+      const L1& k = r2[g.b].first.first;
+      if ((k[0] & 3) != KC_ENT) continue;
+      const auto& x = r2[g.b].first.second;
+      const uint32_t row = ctx.emplace(std::array<uint32_t, 8>{k[0], k[3], k[4], k[5], k[6], x[0], x[1], x[2]}, (uint32_t)ctx.size()).first->second;
+      bits.emplace_back(row, kidx(k[1], k[2]));
     }
     const uint64_t words = (img.key_ents.size() + 31) / 32;
     if (!ctx.empty() && words && (uint64_t)ctx.size() * words * 4 <= SBITS_MAX_BYTES) {
@@ -1298,13 +1315,14 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       img.sctx.assign((size_t)slots * SCTX_WORDS, 0);
       for (auto& c : ctx) {
         const auto& x = c.first;
-        uint32_t h = ctx_hash(key_pre(x[0], x[1], x[2], x[3], x[4])) & (slots - 1);
+        uint32_t h = ctx_key(key_pre(x[0], x[1], x[2], x[3], x[4]), x[5], x[6], x[7]) & (slots - 1);
         while (img.sctx[(size_t)h * SCTX_WORDS]) h = (h + 1) & (slots - 1);
         uint32_t* e = &img.sctx[(size_t)h * SCTX_WORDS];
-        e[0] = SCTX_USED | x[0]; e[1] = x[1]; e[2] = x[2]; e[3] = x[3]; e[4] = x[4]; e[5] = c.second;
+        e[0] = SCTX_USED | x[0];
+        for (uint32_t j = 1; j < 8; j++) e[j] = x[j];
+        e[8] = c.second;
       }
     }
-    static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
     if (times)
       std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities): %.1f MB%s\n", ctx.size(),
                    (unsigned long long)words, img.key_ents.size(), ctx.size() * words * 4 / 1e6,
@@ -1927,7 +1945,7 @@ void Image::write_blob(void* wp) const {
   w.put64(table + 16 * DS_COUNT + 8, w.n);
   w.vec(pol); w.vec(tier_end); w.vec(code);
   w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
-  w.u32(pslot_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words);
+  w.u32(pslot_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words); w.u32(l2_vmask); w.u32(l2_lmask);
   w.u32((uint32_t)key_ents.size());
   w.raw(key_ents.data(), key_ents.size() * 8);
   w.u32((uint32_t)strings.size());
@@ -1999,6 +2017,8 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->pfx = r.vec();
   img->btab_slots = r.u32();
   img->sbits_words = r.u32();
+  img->l2_vmask = r.u32();
+  img->l2_lmask = r.u32();
   if (img->pfx.size() != (size_t)img->n_hot() * PFX_LENS && !(img->pfx.empty() && !img->pslot_mask))
     throw CedarError("corrupt image (prefix lengths)");
   {
@@ -2019,7 +2039,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     for (size_t k = 0; k < nc; k++)
       if (img->sctx[k * SCTX_WORDS]) {
         used++;
-        if (img->sctx[k * SCTX_WORDS + 5] >= rows) throw CedarError("corrupt image (scope bitsets)");
+        if (img->sctx[k * SCTX_WORDS + 8] >= rows) throw CedarError("corrupt image (scope bitsets)");
       }
     if (used >= nc) throw CedarError("corrupt image (scope bitsets)");
   }

@@ -20,7 +20,7 @@ struct DevImage {
   void* btab_mem = nullptr;  // the slot table btab points to (built at load from the entry list)
   uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
   uint32_t *sctx = nullptr, *sbits = nullptr;                        // scope bitsets
-  uint32_t sctx_mask = 0, sbits_words = 0;
+  uint32_t sctx_mask = 0, sbits_words = 0, l2_vmask = 0, l2_lmask = 0;
   uint8_t* gstr_bytes = nullptr;
   // the one device allocation holding the image's device region (image.h DevSection); the arrays
   // above point into it at (blob offset - origin)
@@ -65,9 +65,12 @@ struct DevBatch {
   uint32_t* scan = nullptr;
   void* scan_blk = nullptr;
   size_t scan_cls = 0;
-  // grouped batch (Batch::dev_group): the step's first pass runs in the order ord (group.hip), sorted
-  // on the device from keys / keys2 / vals and the sort's temp storage, all in one pool block
-  uint32_t *ord = nullptr, *gkeys = nullptr, *gkeys2 = nullptr, *gvals = nullptr;
+  // grouped batch (Batch::dev_group): the step's first pass runs in the order ord with the rows
+  // copied into that order (grows), sorted on the device from the encoder's grouping keys (gkeys, an
+  // input section) through gkeys2 / gvals and the sort's temp storage; everything but gkeys in one
+  // pool block (group.hip)
+  const uint32_t* gkeys = nullptr;
+  uint32_t *ord = nullptr, *grows = nullptr, *gkeys2 = nullptr, *gvals = nullptr;
   void *grp_blk = nullptr, *grp_temp = nullptr;
   size_t grp_cls = 0, grp_temp_bytes = 0;
   uint32_t* lane = nullptr;  // per-request lane scratch (images with lane_need > LANE_WORDS)
@@ -157,10 +160,11 @@ int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream
 // when it is one kernel), candidate pass, follow-up gather, and the three follow-up worklists.
 enum StepPhase : uint32_t { PH_GROUP = 0, PH_SCAN, PH_CAND, PH_GATHER, PH_FU_BIG, PH_FU_OVF, PH_FU_GEN, STEP_PHASES };
 int dev_time_split(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_phase, float* ms_total);
-// group.hip: the device grouping of a batch (rocPRIM radix sort of 32-bit grouping keys)
+// group.hip: the device grouping of a batch (a radix sort of the encoder's 32-bit grouping keys,
+// rows copied into the new order)
+uint32_t group_bits();
 size_t group_temp_bytes(uint32_t n);
-int group_enqueue(const uint32_t* rows, const uint32_t* heap, uint32_t n, uint32_t row_words, uint32_t n_hot,
-                  uint32_t* keys, uint32_t* keys2, uint32_t* vals, uint32_t* ord, void* temp, size_t temp_bytes,
-                  void* stream);
+int group_enqueue(const uint32_t* keys, const uint32_t* rows, uint32_t n, uint32_t row_words, uint32_t* grows,
+                  uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream);
 
 }  // namespace cg

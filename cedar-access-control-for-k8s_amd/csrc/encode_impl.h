@@ -406,6 +406,25 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     }
   }
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
+  // grouping key: 8 bits of (action, resource type) | 16 of the principal's type and key ancestors |
+  // 8 of its hot values (group.hip sorts on them)
+  {
+    auto mix = [](uint32_t h, uint32_t x) {
+      h ^= x;
+      h *= 0x9E3779B1u;
+      h ^= h >> 15;
+      h *= 0x85EBCA77u;
+      return h ^ (h >> 13);
+    };
+    const uint32_t ar = mix(mix(0x51ED27Fu, row[RW_A + 1]), row[RW_R]);
+    uint32_t g = mix(0x3C6EF372u, row[RW_P]);
+    const uint32_t nk = std::min<uint32_t>((row[RW_PN] >> AN_KEYS_SHIFT) & AN_KEYS, 32u);
+    for (uint32_t j = 0; j < nk; j++) g += mix(mix(0x2545F491u, blk[row[RW_PANC] + 2 * j]), blk[row[RW_PANC] + 2 * j + 1]);
+    g = mix(g, 0x7FEB352Du);
+    uint32_t hv = 0x6C8E9CF5u;
+    for (uint32_t j = 0; j < 2 * nh; j++) hv = mix(hv, row[RW_HDR + j]);
+    E.gkey = (ar & 0xFF000000u) | ((g >> 16) << 8) | (hv >> 24);
+  }
 }
 
 }  // namespace cg

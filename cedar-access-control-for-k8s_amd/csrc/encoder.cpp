@@ -73,6 +73,7 @@ void Batch::append(EncodedRequest& e) {
   req_base.push_back((uint32_t)heap.size());
   heap.insert(heap.end(), e.blk.begin(), e.blk.end());
   rows.insert(rows.end(), e.row.begin(), e.row.end());
+  gkeys.push_back(e.gkey);
   for (auto& s : e.strs) {
     bstr_bytes.insert(bstr_bytes.end(), s.begin(), s.end());
     bstr_off.push_back((uint32_t)bstr_bytes.size());

@@ -52,6 +52,7 @@ struct Image {
   // scope bitsets (image.h "scope bitsets"): context table and one row of sbits_words per context
   std::vector<uint32_t> sctx, sbits;
   uint32_t sbits_words = 0;
+  uint32_t l2_vmask = 0, l2_lmask = 0;  // hot slots with level-2 value keys / list keys under entity-principal combos
   // index of `uid` in key_ents, KIDX_NONE when it is no key entity
   uint32_t key_index(uint64_t uid) const {
     if (!is_key_ent(uid)) return cgi::KIDX_NONE;
@@ -213,6 +214,9 @@ struct RequestIn {
 // request's string base, stored at RH_SBASE when the block is appended).
 struct EncodedRequest {
   std::vector<uint32_t> blk, row;  // heap block; columnar row (RW_BLK set on append)
+  // grouping key (group.hip): (action, resource type) | principal key ancestors | hot values,
+  // hashed fields of the row, most significant first; the device bucket-sorts on its top bits
+  uint32_t gkey = 0;
   std::vector<std::string> strs;   // request-local strings (few per request: found by linear scan)
   // interning memo over the source bytes' address: a value repeated from the same bytes (a group
   // name as entity id, parent and attribute; a type-name literal) is looked up once
@@ -235,6 +239,7 @@ struct Batch {
   std::shared_ptr<const Image> img;
   std::vector<uint32_t> heap, req_base;
   std::vector<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
+  std::vector<uint32_t> gkeys;  // one grouping key per request (EncodedRequest::gkey)
   uint32_t row_words = 0;
   // request-local strings of every request, appended as requests arrive: string j is
   // bstr_bytes[bstr_off[j] .. bstr_off[j + 1]) (bstr_off keeps a trailing end offset)

@@ -188,24 +188,35 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
   return (1ull << (b & 63u)) | (1ull << ((b >> 6) & 63u)) | (1ull << ((b >> 12) & 63u));
 }
 
-// Scope bitsets: an exact membership test for the level-1 keys whose principal component is an
-// entity (combo with pkc == KC_ENT). A key splits into its context (combo, action component,
-// resource component) and its principal key entity. Each context in use has a row of sbits_words
-// words, one bit per key entity (index into Image::key_ents, "kidx"); the bit is set when the
-// level-1 key exists. sctx: open-addressed table of SCTX_WORDS slots
-// [SCTX_USED | combo, at, ai, rt, ri, row, 0, 0] at ctx_hash(key_pre(combo, at, ai, rt, ri)).
-// A request looks its context up once per combo and tests one bit per principal key ancestor (the
+// Scope bitsets: exact membership tests for the scope-index keys whose principal component is an
+// entity (combo with pkc == KC_ENT), at both levels. A key splits into its context and its
+// principal key entity:
+//   level 1: context (combo, action component, resource component, SCTX_L1, 0, 0); the bit is set
+//            when the level-1 key files policies directly (an entry that only carries level-2 keys
+//            has no bit: it decides nothing by itself);
+//   level 2: context (combo, action, resource, hot slot h (| BT_CKEY for list keys), v0, v1); the
+//            bit is set when that level-2 key exists.
+// Each context in use has a row of sbits_words words, one bit per key entity (index into
+// Image::key_ents, "kidx"). sctx: open-addressed table of SCTX_WORDS slots
+// [SCTX_USED | combo, at, ai, rt, ri, hs, v0, v1, row, 0, 0, 0] at
+// ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1). A request looks up its contexts (per entity-
+// principal combo: level 1, each value slot of l2_vmask with its own value, each element of its
+// list slots in l2_lmask) and tests one bit per principal key ancestor in each context found (the
 // encoder lists their kidx after the ancestor pairs: [n, (type, id) x n, kidx(self), kidx x keys],
-// kidx ~0 for a UID that is no key entity); only keys whose bit is set probe the scope table. The
-// requests of a wave (grouped) share the context row, so the test reads a few shared lines.
+// kidx ~0 for a UID that is no key entity); only keys whose bit is set are probed, once each, with
+// no level-2 descent. On C3 that is ~6 probes of 64-byte slots per request instead of ~62 level-1
+// probes and their level-2 follow-ups; the grouped requests of a wave share the rows.
 // Images whose bitsets would exceed SBITS_MAX_BYTES have none (sbits_words == 0).
-constexpr uint32_t SCTX_WORDS = 8, SCTX_USED = 0x80000000u, KIDX_NONE = 0xFFFFFFFFu;
+constexpr uint32_t SCTX_WORDS = 12, SCTX_USED = 0x80000000u, SCTX_L1 = 0xFFFFu, KIDX_NONE = 0xFFFFFFFFu;
 constexpr uint64_t SBITS_MAX_BYTES = 64ull << 20;
 __host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {
   pre ^= pre >> 16;
   pre *= 0x7FEB352Du;
   pre ^= pre >> 15;
   return pre;
+}
+__host__ __device__ constexpr inline uint32_t ctx_key(uint32_t pre, uint32_t hs, uint32_t v0, uint32_t v1) {
+  return ctx_hash(pre ^ ((hs + 1) * 0x27D4EB2Fu) ^ (v0 * 0x165667B1u) ^ (v1 * 0xD3A2646Cu));
 }
 
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
@@ -422,7 +433,7 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 10;
+constexpr uint32_t IMG_VERSION = 11;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob
