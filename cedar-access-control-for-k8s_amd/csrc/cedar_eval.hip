@@ -1788,10 +1788,13 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           else { v0 = e < LW ? lw : blk[llo + 1 + e]; v1 = 1; }
         }
         const uint2 q = comb_q(cb), r = comb_r(cb);
-        for (uint32_t h = ctx_key(key_pre(cb, q.x, q.y, r.x, r.y), hs, v0, v1) & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
-          const uint4* e = reinterpret_cast<const uint4*>(a.sctx + (size_t)h * SCTX_WORDS);
+        const uint32_t hash = ctx_key(key_pre(cb, q.x, q.y, r.x, r.y), hs, v0, v1), fp = ctx_fp(hash);
+        for (uint32_t h = hash & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
+          const uint32_t f = a.sctx[h];  // the fingerprint words first: most contexts do not exist
+          if (f == 0) break;
+          if (f != fp) continue;
+          const uint4* e = reinterpret_cast<const uint4*>(a.sctx + (a.sctx_mask + 1) + (size_t)h * SCTX_WORDS);
           const uint4 x = e[0], y = e[1], z = e[2];
-          if (x.x == 0) break;
           if (x.x == (SCTX_USED | cb) && x.y == q.x && x.z == q.y && x.w == r.x && y.x == r.y && y.y == hs && y.z == v0 &&
               y.w == v1) {
             row_ = z.x;
@@ -2488,7 +2491,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.act = (uint32_t*)at(DS_ACT); d.btab = (uint32_t*)at(DS_BTAB); d.bfilt = (uint32_t*)at(DS_BFILT);
   d.bstream = (uint32_t*)at(DS_BSTREAM); d.srows = (uint32_t*)at(DS_SROWS); d.shash = (uint32_t*)at(DS_SHASH);
   d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS);
-  d.sctx_mask = (uint32_t)(img.sctx.size() / SCTX_WORDS) - 1;
+  d.sctx_mask = (uint32_t)(img.sctx.size() / (1 + SCTX_WORDS)) - 1;
   d.sbits_words = img.sbits_words;
   d.l2_vmask = img.l2_vmask;
   d.l2_lmask = img.l2_lmask;
@@ -3025,9 +3028,10 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.slot_split = slot_split;
   static const uint32_t scan_lds = [] { const char* e = std::getenv("CEDARGPU_SCAN_LDS"); return (e && *e == '0') ? 0u : 1u; }();
   k.scan_lds = scan_lds;
-  // off by default: on C3 the bitset pass's extra dependent round trips cost more than the probes
-  // it saves (scan 1.41 vs 1.11 ms per 1M, profiles/r03/ab5)
-  static const uint32_t scan_filt = [] { const char* e = std::getenv("CEDARGPU_SCAN_FILT"); return (e && *e == '1') ? 1u : 0u; }();
+  // on by default: the two-level bitset pass lists ~7.6 exact keys per C3 request instead of
+  // enumerating ~62 level-1 keys and their level-2 follow-ups (scan 1.02 -> 0.85 ms per 1M,
+  // profiles/r03/ab10); CEDARGPU_SCAN_FILT=0 enumerates (A/B)
+  static const uint32_t scan_filt = [] { const char* e = std::getenv("CEDARGPU_SCAN_FILT"); return (e && *e == '0') ? 0u : 1u; }();
   k.scan_filt = scan_filt;
   // 48: C3 DAG 4.91e8 decisions/s at 32..96 alike; a list of 24 that sent every longer one to the
   // large stage measured 4.58e8 (43,485 large-stage requests instead of 25,005; profiles/r02/ab_scan_cap)

@@ -197,9 +197,10 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 //   level 2: context (combo, action, resource, hot slot h (| BT_CKEY for list keys), v0, v1); the
 //            bit is set when that level-2 key exists.
 // Each context in use has a row of sbits_words words, one bit per key entity (index into
-// Image::key_ents, "kidx"). sctx: open-addressed table of SCTX_WORDS slots
-// [SCTX_USED | combo, at, ai, rt, ri, hs, v0, v1, row, 0, 0, 0] at
-// ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1). A request looks up its contexts (per entity-
+// Image::key_ents, "kidx"). sctx: an open-addressed table of S slots (S a power of two) at
+// ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1) & (S - 1): first S fingerprint words
+// (ctx_fp of the key's hash, 0 = empty: a few KB, so a lookup that finds nothing costs one cached
+// word), then S slots of SCTX_WORDS [SCTX_USED | combo, at, ai, rt, ri, hs, v0, v1, row, 0, 0, 0]. A request looks up its contexts (per entity-
 // principal combo: level 1, each value slot of l2_vmask with its own value, each element of its
 // list slots in l2_lmask) and tests one bit per principal key ancestor in each context found (the
 // encoder lists their kidx after the ancestor pairs: [n, (type, id) x n, kidx(self), kidx x keys],
@@ -218,6 +219,7 @@ __host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {
 __host__ __device__ constexpr inline uint32_t ctx_key(uint32_t pre, uint32_t hs, uint32_t v0, uint32_t v1) {
   return ctx_hash(pre ^ ((hs + 1) * 0x27D4EB2Fu) ^ (v0 * 0x165667B1u) ^ (v1 * 0xD3A2646Cu));
 }
+__host__ __device__ constexpr inline uint32_t ctx_fp(uint32_t hash) { return hash | 1u; }  // never 0
 
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
 __host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_t ei) {
