@@ -70,7 +70,8 @@ class Comm:
     def broadcast_image(self, ctx, image: Optional[bytes], epoch: int, root: int = 0, activate: bool = True) -> int:
         """Collective: root's compiled image reaches every rank's ctx as `epoch`. Returns its size."""
         n = ctypes.c_size_t(0)
-        buf = ctypes.create_string_buffer(image, len(image)) if image is not None else None
+        # the bytes object's own buffer (no copy of a 100 MB image; the library only reads it)
+        buf = ctypes.cast(ctypes.c_char_p(image), ctypes.c_void_p) if image is not None else None
         rc = lib.cg_broadcast_image(ctx._h, self._h, root, buf, len(image) if image is not None else 0, epoch,
                                     1 if activate else 0, ctypes.byref(n))
         if rc:

@@ -276,7 +276,7 @@ class Context:
         return lib.cg_last_error(self._h).decode()
 
     def load(self, image: bytes, epoch: int, activate: bool = True):
-        buf = ctypes.create_string_buffer(image, len(image))
+        buf = ctypes.cast(ctypes.c_char_p(image), ctypes.c_void_p)  # the bytes' own buffer (cg_image_load copies)
         rc = lib.cg_image_load(self._h, buf, len(image), epoch)
         if rc:
             raise _err(rc, self.last_error())

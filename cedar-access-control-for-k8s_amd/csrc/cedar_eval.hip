@@ -91,6 +91,7 @@ struct KArgs {
   uint32_t sctx_mask, sbits_words;     // sbits_words 0: the image has none
   uint32_t l2_vmask, l2_lmask;         // hot slots with level-2 value / list keys (entity-principal combos)
   uint32_t scan_big;    // more scanned buckets than this: straight to the large stage (CEDARGPU_SCAN_BIG)
+  uint32_t scan_heavy;  // more candidate heads than this: straight to the large stage (CEDARGPU_SCAN_HEAVY)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
   // count at scan[i] (SCAN_OVF: more than SCAN_CAP), its (first head, count | combo) pairs at
@@ -102,6 +103,9 @@ struct KArgs {
 // itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
 // the large stage, which reads the list when it holds them all
 constexpr uint32_t SCAN_CAP = 96, SCAN_OVF = 0xFFFFFFFFu, SCAN_COUNT = (1u << 27) - 1, SCAN_COMBO_SHIFT = 27;
+// scan[i] | SCAN_HEAVY: the request's buckets hold more than a.scan_heavy candidate heads, so it
+// goes straight to the large stage (the candidate pass would overflow its 64 hits and be redone)
+constexpr uint32_t SCAN_HEAVY = 0x40000000u;
 
 // Per-lane evaluation context. Every function taking it is force-inlined so that it stays in
 // registers; the only non-inlined function (structural equality) takes plain pointers.
@@ -1860,7 +1864,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const uint32_t n_l1 = flt ? npos : n_keys;
   const uint64_t t1 = STATS ? clock64() : 0;
   if (STATS && valid && sl == 0) { st[0] = 1; st[10] = n_keys; }
-  uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0;
+  uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0, heads = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);
   uint32_t csl = 0, ch = 0, cl = 0, ck = 0, cn = 0;
@@ -1958,8 +1962,10 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     if (e.y && pos < SCAN_CAP)
       *reinterpret_cast<uint2*>(pairs + 2 * pos) = make_uint2(e.x, min(e.y, SCAN_COUNT) | (combo << SCAN_COMBO_SHIFT));
     nb += popc64(m);
+    heads += min(e.y, SCAN_COUNT);
   }
-  if (valid && sl == 0) a.scan[gid] = nb <= SCAN_CAP ? nb : SCAN_OVF;
+  for (uint32_t o = SEG / 2; o > 0; o >>= 1) heads += (uint32_t)__shfl_xor((int)heads, (int)o);  // over the segment
+  if (valid && sl == 0) a.scan[gid] = nb <= SCAN_CAP ? (nb | (heads > a.scan_heavy ? SCAN_HEAVY : 0u)) : SCAN_OVF;
   if (STATS) {
     const uint64_t t2 = clock64();
     if (lane == 0) { st[8] = (uint32_t)(t1 - t0); st[9] = (uint32_t)(t2 - t1); }
@@ -2203,11 +2209,14 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     // the scan kernel found this request's buckets (cedar_scan_kernel): stage them EC at a time.
     // More buckets than the scan holds: the one-request-per-wave variant probes the index itself,
     // narrower segments hand the request to that variant (the large-stage follow-up).
-    const uint32_t nb = valid ? a.scan[r] : 0u;
+    const uint32_t nb0 = valid ? a.scan[r] : 0u;
+    const bool heavy = nb0 != SCAN_OVF && (nb0 & SCAN_HEAVY);
+    const uint32_t nb = nb0 == SCAN_OVF ? SCAN_OVF : (nb0 & ~SCAN_HEAVY);
     if (SEG == 64 && nb == SCAN_OVF) probe_loop = true;
     uint32_t nbk = nb == SCAN_OVF ? 0u : nb;
-    if (SEG < 64 && nb != SCAN_OVF && nb > a.scan_big && !a.req_idx) nbk = 0;
-    if (SEG < 64 && (nb == SCAN_OVF || (nb > a.scan_big && !a.req_idx))) nh = L::HC + 1;
+    const bool skip = SEG < 64 && nb != SCAN_OVF && (nb > a.scan_big || heavy) && !a.req_idx;
+    if (skip) nbk = 0;
+    if (SEG < 64 && (nb == SCAN_OVF || skip)) nh = L::HC + 1;
     const uint32_t* pairs = a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP);
     for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
       for (uint32_t i = sl; i < L::EC; i += SEG)
@@ -2220,6 +2229,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       ne = b0 < nbk ? min(L::EC, nbk - b0) : 0u;
       wave_lds_sync();
       flush();
+      // more hits than this pass holds: the large stage redoes the request, so stop here
+      if (SEG < 64 && nh > L::HC) nbk = 0;
     }
   }
   if (probe_loop)
@@ -3036,6 +3047,8 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   // 48: C3 DAG 4.91e8 decisions/s at 32..96 alike; a list of 24 that sent every longer one to the
   // large stage measured 4.58e8 (43,485 large-stage requests instead of 25,005; profiles/r02/ab_scan_cap)
   static const uint32_t scan_big = [] { const char* e = std::getenv("CEDARGPU_SCAN_BIG"); return e ? (uint32_t)std::atoi(e) : 48u; }();
+  static const uint32_t scan_heavy = [] { const char* e = std::getenv("CEDARGPU_SCAN_HEAVY"); return e ? (uint32_t)std::atoi(e) : 128u; }();
+  k.scan_heavy = scan_heavy;
   k.scan_big = scan_big;
   k.stats = nullptr;
   k.n_dev = nullptr;
@@ -3112,6 +3125,26 @@ static uint32_t probe_wpb() {
 // the large stage's register target: 3 waves per SIMD (168 VGPRs), which its LDS (3 four-wave
 // blocks per CU) also allows
 constexpr uint32_t BIG_MINW = 3;
+// the probe kernel's per-wave STATS counters (cedar_probe_kernel), summed
+static void print_probe_stats(const char* what, const std::vector<unsigned long long>& h, size_t nw) {
+  double sum[16] = {0};
+  std::vector<unsigned long long> tot(nw);
+  for (size_t w = 0; w < nw; w++) {
+    for (int i = 0; i < 16; i++) sum[i] += (double)h[w * 16 + i];
+    tot[w] = h[w * 16 + 12] + h[w * 16 + 13] + h[w * 16 + 14] + h[w * 16 + 15];
+  }
+  std::sort(tot.begin(), tot.end());
+  const double r = sum[0] > 0 ? sum[0] : 1.0, W = (double)nw;
+  std::fprintf(stderr,
+               "%s stats: requests %.0f | per request: L1 keys %.2f found %.2f | L2 probes %.2f found %.2f | "
+               "slots %.2f | heads %.2f scope-ok %.2f | atoms %.2f | hits %.2f | stage flushes %.2f | "
+               "candidate passes %.2f\n  per wave cycles: load %.0f probe %.0f candidates %.0f merge %.0f | total p50 %llu "
+               "p90 %llu p99 %llu max %llu\n",
+               what, sum[0], sum[1] / r, sum[2] / r, sum[3] / r, sum[4] / r, sum[5] / r, sum[6] / r, sum[7] / r, sum[8] / r,
+               sum[9] / r, sum[10] / r, sum[11] / r, sum[12] / W, sum[13] / W, sum[14] / W, sum[15] / W, tot[nw / 2],
+               tot[nw * 9 / 10], tot[nw * 99 / 100], tot[nw - 1]);
+}
+
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
   if (big && k.scan) {  // the large stage over the scan's buckets (probing only past SCAN_CAP)
     // one-wave blocks: a finished request's wave slot and LDS return at once (C3 DAG 4.996e8 vs
@@ -3159,6 +3192,23 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     else if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6>), sg, sb, 0, s, k);
     else hipLaunchKernelGGL((cedar_scan_kernel<8>), sg, sb, 0, s, k);
     if (!k.req_idx) mark(PH_SCAN, s);
+    static const bool cstats = std::getenv("CEDARGPU_CAND_STATS") != nullptr;
+    if (cstats && !k.req_idx) {  // the candidate pass's work counters (profiling)
+      const size_t nw = (n + 7) / 8;
+      unsigned long long* d = nullptr;
+      if (hipMalloc((void**)&d, nw * 16 * 8) == hipSuccess) {
+        KArgs ks = k;
+        ks.stats = d;
+        (void)hipMemsetAsync(d, 0, nw * 16 * 8, s);
+        hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, true, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, ks);
+        std::vector<unsigned long long> h(nw * 16);
+        (void)hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(d);
+        print_probe_stats("candidate pass", h, nw);
+      }
+      return;
+    }
     if (cocc == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
     else hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
     return;
@@ -3182,22 +3232,7 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     (void)hipMemcpyAsync(h.data(), dstats, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
     (void)hipFree(dstats);
-    double sum[16] = {0};
-    std::vector<unsigned long long> tot(nw);
-    for (size_t w = 0; w < nw; w++) {
-      for (int i = 0; i < 16; i++) sum[i] += (double)h[w * 16 + i];
-      tot[w] = h[w * 16 + 12] + h[w * 16 + 13] + h[w * 16 + 14] + h[w * 16 + 15];
-    }
-    std::sort(tot.begin(), tot.end());
-    const double r = sum[0] > 0 ? sum[0] : 1.0, W = (double)nw;
-    std::fprintf(stderr,
-                 "probe stats: requests %.0f | per request: L1 keys %.2f found %.2f | L2 probes %.2f found %.2f | "
-                 "slots %.2f | heads %.2f scope-ok %.2f | atoms %.2f | hits %.2f | stage flushes %.2f | "
-                 "candidate passes %.2f\n  per wave cycles: load %.0f probe %.0f candidates %.0f merge %.0f | total p50 %llu "
-                 "p90 %llu p99 %llu max %llu\n",
-                 sum[0], sum[1] / r, sum[2] / r, sum[3] / r, sum[4] / r, sum[5] / r, sum[6] / r, sum[7] / r, sum[8] / r,
-                 sum[9] / r, sum[10] / r, sum[11] / r, sum[12] / W, sum[13] / W, sum[14] / W, sum[15] / W, tot[nw / 2],
-                 tot[nw * 9 / 10], tot[nw * 99 / 100], tot[nw - 1]);
+    print_probe_stats("probe", h, nw);
     return;
   }
   if (big) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024>), grid, dim3(BLOCK), 0, s, k);
