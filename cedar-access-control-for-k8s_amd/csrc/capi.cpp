@@ -495,7 +495,8 @@ int cg_ctx_create(int device, cg_ctx** out) {
   if (!c) return CG_E_ARG;
   c->device = device;
   if (dev_stream_create(device, &c->stream)) { delete c; return CG_E_DEVICE; }
-  if (dev_pool_create(device, &c->pool)) { dev_stream_destroy(c->stream); delete c; return CG_E_DEVICE; }
+  if (dev_stream_create(device, &c->rstream)) { dev_stream_destroy(c->stream); delete c; return CG_E_DEVICE; }
+  if (dev_pool_create(device, &c->pool)) { dev_stream_destroy(c->rstream); dev_stream_destroy(c->stream); delete c; return CG_E_DEVICE; }
   *out = c;
   return CG_OK;
 }
@@ -508,6 +509,7 @@ void cg_ctx_destroy(cg_ctx* ctx) {
     ctx->images.clear();
   }
   dev_pool_destroy(ctx->pool);
+  dev_stream_destroy(ctx->rstream);
   dev_stream_destroy(ctx->stream);
   delete ctx;
 }
@@ -1063,12 +1065,12 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
       cape = clampr(cape, 4u);
       DevSubset job;
       SubsetView v;
-      int src = dev_subset_begin(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->stream, &job);
+      int src = dev_subset_begin(b->img->dev, b->dev, idx.data(), (uint32_t)idx.size(), capr, cape, mode, b->ctx->rstream, &job);
       if (!src) src = dev_subset_end(&job, &v, deadline);
       if (src == DEV_TIMEOUT) return timed_out({&job});
       if (src) {
         b->err = dev_last_error();
-        (void)dev_stream_sync(b->ctx->stream);
+        (void)dev_stream_sync(b->ctx->rstream);
         dev_subset_release(&job);
         return CG_E_DEVICE;
       }
@@ -1103,7 +1105,7 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     int brc = 0;
     for (auto& u : subs)
       if (!brc && !u.idx->empty())
-        brc = dev_subset_begin(b->img->dev, b->dev, u.idx->data(), (uint32_t)u.idx->size(), u.capr, u.cape, u.mode, b->ctx->stream, &u.job);
+        brc = dev_subset_begin(b->img->dev, b->dev, u.idx->data(), (uint32_t)u.idx->size(), u.capr, u.cape, u.mode, b->ctx->rstream, &u.job);
     for (auto& u : subs)
       if (!brc) brc = dev_subset_end(&u.job, &u.v, deadline);
     if (brc == DEV_TIMEOUT) return timed_out({&subs[0].job, &subs[1].job, &subs[2].job});
@@ -1113,7 +1115,7 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
     int arc = CG_OK;
     if (brc) {
       b->err = dev_last_error();
-      (void)dev_stream_sync(b->ctx->stream);  // nothing in flight before the blocks go back
+      (void)dev_stream_sync(b->ctx->rstream);  // nothing in flight before the blocks go back
       arc = CG_E_DEVICE;
     } else {
       try {

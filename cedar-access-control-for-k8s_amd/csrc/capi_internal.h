@@ -51,6 +51,9 @@ using cg::LoadedImage;
 struct cg_ctx {
   int device = 0;
   void* stream = nullptr;
+  // host-driven re-runs (rare) run on their own stream, so that a pipelined next batch queued on
+  // `stream` does not delay them (and they do not delay it)
+  void* rstream = nullptr;
   cg::DevPool* pool = nullptr;  // batch buffers (device + pinned staging), reused across batches
   std::mutex mu;
   std::map<uint64_t, std::shared_ptr<LoadedImage>> images;

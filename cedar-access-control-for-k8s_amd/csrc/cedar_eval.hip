@@ -2940,8 +2940,13 @@ void dev_batch_retire(DevBatch* d, std::vector<DevSubset>& held) {
   if (r) {
     r->d = *d;
     r->held.swap(held);
-    // the re-run jobs run on the batch's stream too (dev_subset_begin), so one callback covers all
-    if (hipLaunchHostFunc((hipStream_t)d->stream, retired_drained, r) == hipSuccess) {
+    // host re-runs run on the context's re-run stream: the batch's stream waits for every one still
+    // in flight, so the one callback behind it covers them all
+    bool ordered = true;
+    for (auto& j : r->held)
+      if (j.done && hipEventQuery((hipEvent_t)j.done) == hipErrorNotReady)
+        ordered = ordered && hipStreamWaitEvent((hipStream_t)d->stream, (hipEvent_t)j.done, 0) == hipSuccess;
+    if (ordered && hipLaunchHostFunc((hipStream_t)d->stream, retired_drained, r) == hipSuccess) {
       {
         std::lock_guard<std::mutex> g(pool->mu);
         pool->retired.push_back(r);

@@ -2088,13 +2088,24 @@ uint32_t request_sid(const Image& img, EncodedRequest& e, std::string_view s) {
   if (g >= 0) {
     id = (uint32_t)g;
   } else {
-    size_t j = 0;
-    while (j < e.strs.size() && e.strs[j] != s) j++;
+    // a few strings: a linear scan; past STRS_SCAN (a user in thousands of groups) a hash index,
+    // so the encode stays linear in the request's size
+    size_t j = e.strs.size();
+    if (e.strs.size() <= EncodedRequest::STRS_SCAN) {
+      for (j = 0; j < e.strs.size() && e.strs[j] != s; j++) {}
+    } else {
+      if (e.strs_ix.empty())
+        for (uint32_t k = 0; k < e.strs.size(); k++) e.strs_ix.emplace(Image::str_hash(e.strs[k]), k);
+      auto r = e.strs_ix.equal_range(Image::str_hash(s));
+      for (auto it = r.first; it != r.second; ++it)
+        if (e.strs[it->second] == s) { j = it->second; break; }
+    }
     id = img.n_gstr() + (uint32_t)j;
     if (j == e.strs.size()) {
       id = img.n_gstr() + (uint32_t)e.strs.size();
       if (id > X_MASK) throw CedarError("string table overflow");
       e.strs.emplace_back(s);
+      if (!e.strs_ix.empty()) e.strs_ix.emplace(Image::str_hash(s), (uint32_t)e.strs.size() - 1);
     }
   }
   if (e.n_memo < EncodedRequest::MEMO) {

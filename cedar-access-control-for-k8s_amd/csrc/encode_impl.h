@@ -159,12 +159,21 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   };
   // parent adjacency (ids of parents that exist in the map are followed; absent ones are leaves)
   std::vector<std::vector<uint64_t>> parents(table.size());
+  std::unordered_set<uint64_t> seen_p;  // a parent list past DEDUP_SCAN entries dedups by hashing
+  auto add_parent = [&](std::vector<uint64_t>& l, uint64_t key) {
+    if (l.size() < DEDUP_SCAN) {
+      if (std::find(l.begin(), l.end(), key) == l.end()) l.push_back(key);
+      return;
+    }
+    if (l.size() == DEDUP_SCAN || seen_p.empty()) seen_p = std::unordered_set<uint64_t>(l.begin(), l.end());
+    if (seen_p.insert(key).second) l.push_back(key);
+  };
   for (uint32_t i = 0; i < table.size(); i++) {
     const uint32_t np = src.n_parents(table[i]);
+    seen_p.clear();
     for (uint32_t k = 0; k < np; k++) {
       const auto u = uid_of(src.parent(table[i], k));
-      const uint64_t key = uid_key(u.first, u.second);
-      if (std::find(parents[i].begin(), parents[i].end(), key) == parents[i].end()) parents[i].push_back(key);
+      add_parent(parents[i], uid_key(u.first, u.second));
     }
   }
   // Static entities merged into the map (image.h "static entities"). A table entity that is also
@@ -201,8 +210,8 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       if (s < 0) continue;
       std::vector<uint64_t> sp;
       cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_PAD], sp);
-      for (const uint64_t p : sp)
-        if (std::find(parents[i].begin(), parents[i].end(), p) == parents[i].end()) parents[i].push_back(p);
+      seen_p.clear();
+      for (const uint64_t p : sp) add_parent(parents[i], p);
     }
   }
   const uint32_t n = (uint32_t)table.size();

@@ -17,6 +17,10 @@
 
 namespace cg {
 
+// Lists deduplicated while built (parents, groups) scan linearly up to this many entries and hash
+// beyond, so a principal in thousands of groups encodes in time linear in its size.
+constexpr size_t DEDUP_SCAN = 32;
+
 struct PolicyMeta {
   std::string id, filename;
   Position pos;
@@ -218,12 +222,14 @@ struct EncodedRequest {
   // hashed fields of the row, most significant first; the device bucket-sorts on its top bits
   uint32_t gkey = 0;
   std::vector<std::string> strs;   // request-local strings (few per request: found by linear scan)
+  static constexpr size_t STRS_SCAN = 16;
+  std::unordered_multimap<uint64_t, uint32_t> strs_ix;  // str_hash -> index, once strs outgrows STRS_SCAN
   // interning memo over the source bytes' address: a value repeated from the same bytes (a group
   // name as entity id, parent and attribute; a type-name literal) is looked up once
   static constexpr uint32_t MEMO = 32;
   const char* memo_p[MEMO];
   uint32_t memo_len[MEMO], memo_id[MEMO], n_memo = 0;
-  void clear() { blk.clear(); row.clear(); strs.clear(); n_memo = 0; }
+  void clear() { blk.clear(); row.clear(); strs.clear(); strs_ix.clear(); n_memo = 0; }
 };
 // Encodes (EntityMap, Request) for `img`. Thread-safe: reads the image only.
 void encode_request(const Image& img, const std::vector<EntityIn>& ents, const RequestIn& req, EncodedRequest& out);

@@ -204,14 +204,22 @@ void user_to_cedar(const std::string& name, const std::string& uid, const std::v
                    const std::vector<std::pair<std::string, std::vector<std::string>>>& extra, std::vector<EntityIn>& ents,
                    std::pair<std::string, std::string>& principal) {
   std::vector<std::pair<std::string, std::string>> parents;
+  std::unordered_set<std::string> seen;  // past DEDUP_SCAN groups (a user in thousands of them)
   for (auto& g : groups) {
     EntityIn ge;
     ge.type = kGroup;
     ge.id = g;
     ge.attrs = rec({{"name", HVal::Str(g)}});
     ents.push_back(std::move(ge));
-    if (std::find(parents.begin(), parents.end(), std::make_pair(std::string(kGroup), g)) == parents.end())
-      parents.emplace_back(kGroup, g);
+    bool fresh;
+    if (parents.size() < DEDUP_SCAN) {
+      fresh = std::find(parents.begin(), parents.end(), std::make_pair(std::string(kGroup), g)) == parents.end();
+    } else {
+      if (seen.empty())
+        for (auto& q : parents) seen.insert(q.second);
+      fresh = seen.insert(g).second;
+    }
+    if (fresh) parents.emplace_back(kGroup, g);
   }
   HVal attrs = rec({{"name", HVal::Str(name)}});
   std::string ptype = kUser;
@@ -625,6 +633,7 @@ int encode_sar_direct(const Image& img, const char* json, size_t n, EncodedReque
   std::vector<LEnt> ents;
   ents.reserve(v.groups.size() + 2);
   LEnt pe;
+  std::unordered_set<SV> seen;  // past DEDUP_SCAN groups
   for (SV g : v.groups) {
     LEnt ge;
     ge.type = kGroup;
@@ -632,7 +641,15 @@ int encode_sar_direct(const Image& img, const char* json, size_t n, EncodedReque
     ge.attrs = t.rec({{"name", t.str(g)}});
     ents.push_back(std::move(ge));
     const std::pair<SV, SV> pu{kGroup, g};
-    if (std::find(pe.parents.begin(), pe.parents.end(), pu) == pe.parents.end()) pe.parents.push_back(pu);
+    bool fresh;
+    if (pe.parents.size() < DEDUP_SCAN) {
+      fresh = std::find(pe.parents.begin(), pe.parents.end(), pu) == pe.parents.end();
+    } else {
+      if (seen.empty())
+        for (auto& q : pe.parents) seen.insert(q.second);
+      fresh = seen.insert(g).second;
+    }
+    if (fresh) pe.parents.push_back(pu);
   }
   SV ptype = kUser, pname = v.user, pns;
   bool sa = false;

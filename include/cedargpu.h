@@ -79,7 +79,11 @@ int cg_compiler_add_policy(cg_compiler* c, const char* policy_id, const char* fi
  * source). Every evaluation then sees the request's EntityMap merged with them: a static entity the
  * request lacks is present; for a UID in both, the request's attributes and the union of both parent
  * lists. The compiler builds each static entity's transitive `in`-closure row into the image.
- * Replaces any earlier set; an empty array (len 0) clears it. */
+ * Replaces any earlier set; an empty array (len 0) clears it.
+ * Limits of the device row format: an entity may have at most 65,535 transitive ancestors (request
+ * parents and static closure together), at most 32,767 of them scope-index key entities; a request
+ * past either is refused by the encoder with CG_E_PARSE / CG_E_COMPILE (never evaluated on a
+ * truncated list). */
 int cg_compiler_set_entities(cg_compiler* c, const char* json, size_t len);
 /* Drops the tiers added so far but keeps the compiler's parse cache: the incremental rebuild after
  * a store change (a CRD added / updated / removed, crd.go:45-118; a directory re-read,

@@ -139,3 +139,25 @@ def test_malformed_bodies_are_left_to_the_general_path():
     for bad in ['{"spec": {"user": "a",}}', '{"spec": [1]}', '{"kind": "x"}', '[{"spec": {}}]', '{"spec": {"user": tru}}']:
         n, nd, nm, _ = check(image, "[" + bad + "]")
         assert (n, nd, nm) == (1, 0, 0), bad
+
+
+def test_ancestor_count_limits_of_the_row_format():
+    """The request row packs an entity's ancestor count into 16 bits (image.h AN_COUNT: 65,535)
+    and its key-ancestor count into 15 (AN_KEYS: 32,767; cedargpu.h documents both): a user in
+    65,535 groups encodes, one in 65,536 is refused by the encoder (an error for that request,
+    never a truncated list)."""
+    img = _demo_image()
+
+    def sar(n_groups):
+        s = synth.make_sar("big-user", "u1", [f"g{k}" for k in range(n_groups)], "get", ns="default", resource="pods")
+        return json.dumps([s])
+
+    b = sar(65535).encode()
+    n, nd, nm, first = (ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int64())
+    assert lib.cg_encode_sar_check(img, len(img), b, len(b), ctypes.byref(n), ctypes.byref(nd), ctypes.byref(nm),
+                                   ctypes.byref(first)) == 0
+    assert n.value == 1 and nm.value == 0
+    b = sar(65536).encode()
+    rc = lib.cg_encode_sar_check(img, len(img), b, len(b), ctypes.byref(n), ctypes.byref(nd), ctypes.byref(nm),
+                                 ctypes.byref(first))
+    assert rc != 0
