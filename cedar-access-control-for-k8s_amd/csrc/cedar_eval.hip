@@ -1816,6 +1816,11 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     // SCAN_PB loads of a lane's round in flight at once.
     const uint32_t self = pn >> 31, tot = on ? nf * nP : 0u;
     const uint32_t* kl = blk + p_anc + 2 * (pn & AN_COUNT);
+    // t / nP by a multiply: exact while t * nP < 2^32 (t < CTX_CAP * nP, nP < 2048); nP == 1
+    // (whose reciprocal does not fit 32 bits) divides by itself (checked for every nP < 2048 on the
+    // host)
+    const uint32_t inv = nP > 1 ? 0xFFFFFFFFu / nP + 1u : 0u;
+    auto divp = [&](uint32_t t) { return nP > 1 ? __umulhi(t, inv) : t; };
     for (uint32_t rb = 0; __ballot(rb < tot) != 0; rb += SEG * SCAN_PB) {
       uint32_t fw[SCAN_PB], fk[SCAN_PB];
 #pragma unroll
@@ -1824,11 +1829,11 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         fw[u] = 0;
         fk[u] = 0;
         if (t < tot) {
-          const uint32_t j = t / nP, ip = t - j * nP;
+          const uint32_t j = divp(t), ip = t - j * nP;
           const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
           const uint32_t kid = jk <= SCAN_ANC ? s_kid[seg][jk] : kl[jk];
           fk[u] = kid;
-          if (kid != KIDX_NONE) fw[u] = a.sbits[(size_t)s_cx[seg][j].w * a.sbits_words + (kid >> 5)];
+          if (kid != KIDX_NONE && (kid >> 5) < a.sbits_words) fw[u] = a.sbits[(size_t)s_cx[seg][j].w * a.sbits_words + (kid >> 5)];
         }
       }
 #pragma unroll
@@ -1838,7 +1843,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         const uint64_t mk = sballot(ok);
         const uint32_t at_ = npos + mbcnt64(mk);
         if (ok && at_ < SCAN_POS_B) {
-          const uint32_t j = t / nP;
+          const uint32_t j = divp(t);
           s_pos[seg][at_] = LIST_EXACT | (j << 16) | (t - j * nP);
         }
         npos += popc64(mk);
@@ -2362,7 +2367,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       for (uint32_t i0 = 0; i0 < (m >> 1); i0 += SEG) {
         const uint32_t q = i0 + sl;  // compare-exchange pair q
         if (q < (m >> 1)) {
-          const uint32_t lo = ((q / jj) * 2 * jj) + (q % jj), hi = lo + jj;
+          const uint32_t lo = ((q & ~(jj - 1u)) << 1) | (q & (jj - 1u)), hi = lo + jj;  // (jj: a power of two)
           const uint32_t x = wl.u.hs[seg][lo], y = wl.u.hs[seg][hi];
           const bool up = (lo & k) == 0;
           if ((x > y) == up) { wl.u.hs[seg][lo] = y; wl.u.hs[seg][hi] = x; }
@@ -3155,6 +3160,22 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     // one-wave blocks: a finished request's wave slot and LDS return at once (C3 DAG 4.996e8 vs
     // 4.919e8 with 4-wave blocks, profiles/r02/ab_big_occ)
     static const uint32_t bw = [] { const char* e = std::getenv("CEDARGPU_BIG_WPB"); return e ? (uint32_t)std::atoi(e) : 1u; }();
+    static const bool bstats = std::getenv("CEDARGPU_BIG_STATS") != nullptr;
+    if (bstats) {  // the large stage's work counters (profiling)
+      unsigned long long* d = nullptr;
+      if (hipMalloc((void**)&d, (size_t)n * 16 * 8) == hipSuccess) {
+        KArgs ks = k;
+        ks.stats = d;
+        (void)hipMemsetAsync(d, 0, (size_t)n * 16 * 8, s);
+        hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, true, 1, true>), dim3(n), dim3(64), 0, s, ks);
+        std::vector<unsigned long long> h((size_t)n * 16);
+        (void)hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(d);
+        print_probe_stats("large stage", h, n);
+      }
+      return;
+    }
     if (bw == 1) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, 1, true>), dim3(n), dim3(64), 0, s, k);
     else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, WAVES, true>), dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
     return;
