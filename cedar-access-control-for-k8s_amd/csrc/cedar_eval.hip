@@ -1602,6 +1602,8 @@ constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
 constexpr uint32_t CTX_CAP = 16, LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;
 constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the rest read from the row)
 constexpr uint32_t SCAN_PB = 8;    // bit tests per lane per round (loads in flight)
+constexpr uint32_t MEMB_U = 4;     // duplicate-class members a lane copies per round (loads in flight)
+constexpr uint32_t RANK_POL = 16384;  // the large stage's rank pass: policy indices its bitmap covers
 __device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t k) {  // index of the k-th set bit of m
   for (uint32_t i = 0; i < k; i++) m &= m - 1;
   return m ? (uint32_t)__builtin_ctz(m) : 0u;
@@ -2172,19 +2174,54 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         wl.hp[seg][pos0] = q2.z;  // PW_CODE: global policy index
         wl.hm[seg][pos0] = hmv;
       }
-      // class members: the segment copies each hitting class's list together (coalesced)
-      for (uint64_t cls = sballot(hit && mlist != 0); __ballot(cls != 0);) {
-        const bool act = cls != 0;  // this segment still has a class to copy
-        const uint32_t src = act ? (uint32_t)__builtin_ctzll(cls) : lane;
-        cls &= act ? cls - 1 : 0ull;
-        const uint32_t p0 = (uint32_t)__shfl((int)pos0, (int)src), nm = (uint32_t)__shfl((int)nmem, (int)src);
-        const uint32_t mls = (uint32_t)__shfl((int)mlist, (int)src), hv = (uint32_t)__shfl((int)hmv, (int)src);
-        const uint32_t ml = act ? mls : 0u;
-        if (ml)
-          for (uint32_t j = sl; j < nm && p0 + j < L::HC; j += SEG) {
-            wl.hp[seg][p0 + j] = a.bstream[ml + 1 + j];
-            wl.hm[seg][p0 + j] = hv;
+      // class members. One-request waves (the large stage): every hitting class's list at once.
+      // Member m of the segment's classes (in lane order) finds its class lane by a binary search
+      // over the lanes' prefix counts, and the lanes load MEMB_U members each per round, all in
+      // flight together (one class at a time made its ~230 members from ~30 classes a chain of 30
+      // dependent loads: large stage 0.375 -> 0.338 ms, profiles/r03/ab14). 8-lane segments (the
+      // candidate pass: a few classes per round) copy one class at a time, coalesced, which costs
+      // them fewer registers.
+      if constexpr (SEG < 64) {
+        for (uint64_t cls = sballot(hit && mlist != 0); __ballot(cls != 0);) {
+          const bool act = cls != 0;  // this segment still has a class to copy
+          const uint32_t src = act ? (uint32_t)__builtin_ctzll(cls) : lane;
+          cls &= act ? cls - 1 : 0ull;
+          const uint32_t p0 = (uint32_t)__shfl((int)pos0, (int)src), nm = (uint32_t)__shfl((int)nmem, (int)src);
+          const uint32_t mls = (uint32_t)__shfl((int)mlist, (int)src), hv = (uint32_t)__shfl((int)hmv, (int)src);
+          const uint32_t ml = act ? mls : 0u;
+          if (ml)
+            for (uint32_t j = sl; j < nm && p0 + j < L::HC; j += SEG) {
+              wl.hp[seg][p0 + j] = a.bstream[ml + 1 + j];
+              wl.hm[seg][p0 + j] = hv;
+            }
+        }
+      } else {
+        const uint32_t cmc = (hit && mlist) ? nmem : 0u;
+        const uint32_t cinc = sscan(cmc), cs = cinc - cmc, ctot = sbcast(cinc, SEG - 1);
+        for (uint32_t m0 = 0; __ballot(m0 < ctot); m0 += MEMB_U * SEG) {
+          uint32_t dst[MEMB_U], hv[MEMB_U], v[MEMB_U];
+#pragma unroll
+          for (uint32_t u = 0; u < MEMB_U; u++) {
+            const uint32_t m = m0 + u * SEG + sl;
+            uint32_t c = 0;  // the largest class lane with cs <= m
+            for (uint32_t step = SEG / 2; step > 0; step >>= 1) {
+              const uint32_t csn = (uint32_t)__shfl((int)cs, (int)(sbase + c + step));
+              if (csn <= m) c += step;
+            }
+            const uint32_t csc = (uint32_t)__shfl((int)cs, (int)(sbase + c)), pc = (uint32_t)__shfl((int)pos0, (int)(sbase + c));
+            const uint32_t mlc = (uint32_t)__shfl((int)mlist, (int)(sbase + c));
+            hv[u] = (uint32_t)__shfl((int)hmv, (int)(sbase + c));
+            const uint32_t off = m - csc;
+            dst[u] = (m < ctot) ? pc + off : L::HC;
+            v[u] = dst[u] < L::HC ? a.bstream[mlc + 1 + off] : 0u;
           }
+#pragma unroll
+          for (uint32_t u = 0; u < MEMB_U; u++)
+            if (dst[u] < L::HC) {
+              wl.hp[seg][dst[u]] = v[u];
+              wl.hm[seg][dst[u]] = hv[u];
+            }
+        }
       }
       if (hit) {
         if (err && xpos < L::XC) {
@@ -2354,15 +2391,63 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     a.res[2 * (size_t)wo + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
 
   }
-  const uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge
-  // bitonic sort of (policy index << 8 | slot) over the wave's largest power of two >= nh
+  uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge (after a rank pass: unique ones)
+  // One-request waves with many hits over an image of <= RANK_POL policies: a rank pass instead of
+  // the sort. A bitmap over policy indices (hs[0, 512)) takes every hit, prefix popcounts per word
+  // (hs[512, 1024)) give each hit its rank among the distinct policies, and the hits scatter to
+  // their ranks: five LDS passes instead of ~36 bitonic stages over 256-1024 keys (the large
+  // stage's merge was half its time: ~230 hits per request on C3, profiles/r03/ab14).
+  bool ranked = false;
+  if constexpr (SEG == 64 && HCAP >= 1024) {
+    if (nhm > 128 && a.n_pol <= RANK_POL) {
+      ranked = true;
+      uint32_t* bm = wl.u.hs[0];
+      uint32_t* pre = wl.u.hs[0] + RANK_POL / 32;
+      const uint32_t W = (a.n_pol + 31) >> 5;
+      for (uint32_t w = lane; w < W; w += 64) bm[w] = 0u;
+      wave_lds_sync();
+      for (uint32_t i = lane; i < nhm; i += 64) {
+        const uint32_t p = wl.hp[0][i];
+        atomicOr(&bm[p >> 5], 1u << (p & 31));
+      }
+      wave_lds_sync();
+      const uint32_t per = (W + 63) / 64, w0 = min(W, lane * per), w1 = min(W, w0 + per);
+      uint32_t cnt = 0;
+      for (uint32_t w = w0; w < w1; w++) cnt += __popc(bm[w]);
+      uint32_t inc = cnt;
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += y;
+      }
+      uint32_t run = inc - cnt;
+      for (uint32_t w = w0; w < w1; w++) {
+        pre[w] = run;
+        run += __popc(bm[w]);
+      }
+      const uint32_t uniq = (uint32_t)__shfl((int)inc, 63);
+      wave_lds_sync();
+      for (uint32_t i = lane; i < nhm; i += 64) {  // (the hit's policy keeps its place in hp)
+        const uint32_t p = wl.hp[0][i];
+        const uint32_t r = pre[p >> 5] + __popc(bm[p >> 5] & ((1u << (p & 31)) - 1u));
+        wl.hp[0][i] = (r << 16) | p;
+      }
+      wave_lds_sync();
+      for (uint32_t i = lane; i < nhm; i += 64) {  // duplicates write the same rank: either is kept
+        const uint32_t x = wl.hp[0][i];
+        wl.u.hs[0][x >> 16] = ((x & 0xFFFFu) << 12) | i;
+      }
+      wave_lds_sync();
+      nhm = uniq;
+    }
+  }
+  // bitonic sort of (policy index << 12 | slot) over the wave's largest power of two >= nh
   uint32_t mloc = 2;
-  while (mloc < nhm) mloc <<= 1;
-  uint32_t m = mloc;
+  while (!ranked && mloc < nhm) mloc <<= 1;
+  uint32_t m = ranked ? 0u : mloc;
   for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
-  for (uint32_t i = sl; i < m; i += SEG) wl.u.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
+  for (uint32_t i = sl; !ranked && i < m; i += SEG) wl.u.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
   wave_lds_sync();
-  for (uint32_t k = 2; k <= m; k <<= 1) {
+  for (uint32_t k = 2; !ranked && k <= m; k <<= 1) {
     for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
       for (uint32_t i0 = 0; i0 < (m >> 1); i0 += SEG) {
         const uint32_t q = i0 + sl;  // compare-exchange pair q
