@@ -1761,6 +1761,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     on = on && nctx <= CTX_CAP;
     // the contexts, looked up side by side (lane j % SEG takes context j); a found one is kept
     uint32_t nf = 0;  // contexts found (segment-uniform)
+    bool fpdup = false;
     for (uint32_t j0 = 0; __ballot(on && j0 < nctx) != 0; j0 += SEG) {
       const uint32_t j = j0 + sl;
       uint32_t cb = 0, hs = SCTX_L1, v0 = 0, v1 = 0, row_ = KIDX_NONE;
@@ -1794,18 +1795,19 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           else { v0 = e < LW ? lw : blk[llo + 1 + e]; v1 = 1; }
         }
         const uint2 q = comb_q(cb), r = comb_r(cb);
+        // (fingerprint, row) pairs only: a fingerprint match is taken without comparing the full
+        // key. That stays exact: every key a row lists is probed in the scope table, which compares
+        // the whole key, so a row of another context can only add probes that find nothing; and
+        // the request's own context (when it exists) matches on its chain, so its bits are never
+        // missed. Two matches on one chain (32-bit fingerprints: practically never) enumerate the
+        // request's keys instead.
         const uint32_t hash = ctx_key(key_pre(cb, q.x, q.y, r.x, r.y), hs, v0, v1), fp = ctx_fp(hash);
         for (uint32_t h = hash & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
-          const uint32_t f = a.sctx[h];  // the fingerprint words first: most contexts do not exist
-          if (f == 0) break;
-          if (f != fp) continue;
-          const uint4* e = reinterpret_cast<const uint4*>(a.sctx + (a.sctx_mask + 1) + (size_t)h * SCTX_WORDS);
-          const uint4 x = e[0], y = e[1], z = e[2];
-          if (x.x == (SCTX_USED | cb) && x.y == q.x && x.z == q.y && x.w == r.x && y.x == r.y && y.y == hs && y.z == v0 &&
-              y.w == v1) {
-            row_ = z.x;
-            break;
-          }
+          const uint2 f = *reinterpret_cast<const uint2*>(a.sctx + 2 * (size_t)h);
+          if (f.x == 0) break;
+          if (f.x != fp) continue;
+          if (row_ != KIDX_NONE) { fpdup = true; break; }
+          row_ = f.y;
         }
       }
       const bool got = on && j < nctx && row_ != KIDX_NONE;
@@ -1813,6 +1815,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       if (got) s_cx[seg][nf + mbcnt64(mk)] = make_uint4(cb | (hs << 8), v0, v1, row_);
       nf += popc64(mk);
     }
+    on = on && sballot(fpdup) == 0;
     wave_lds_sync();
     // (found context, key ancestor) pairs: ip 0 .. nP - 1 under each; a set bit lists the key. All
     // SCAN_PB loads of a lane's round in flight at once.
@@ -2592,7 +2595,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.act = (uint32_t*)at(DS_ACT); d.btab = (uint32_t*)at(DS_BTAB); d.bfilt = (uint32_t*)at(DS_BFILT);
   d.bstream = (uint32_t*)at(DS_BSTREAM); d.srows = (uint32_t*)at(DS_SROWS); d.shash = (uint32_t*)at(DS_SHASH);
   d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS);
-  d.sctx_mask = (uint32_t)(img.sctx.size() / (1 + SCTX_WORDS)) - 1;
+  d.sctx_mask = (uint32_t)(img.sctx.size() / (2 + SCTX_WORDS)) - 1;
   d.sbits_words = img.sbits_words;
   d.l2_vmask = img.l2_vmask;
   d.l2_lmask = img.l2_lmask;

@@ -1024,7 +1024,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
   img.key_ents.clear();
-  img.sctx.assign(2 * (1 + SCTX_WORDS), 0); img.sbits.assign(1, 0); img.sbits_words = 0;
+  img.sctx.assign(2 * (2 + SCTX_WORDS), 0); img.sbits.assign(1, 0); img.sbits_words = 0;
   img.combo_mask = 0;
   img.pslot_mask = 0;
   img.pfx.assign((size_t)img.n_hot() * PFX_LENS, 0);
@@ -1057,7 +1057,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
     img.btab_slots = 2;
-    img.sctx.assign(2 * (1 + SCTX_WORDS), 0); img.sbits.assign(1, 0); img.sbits_words = 0;
+    img.sctx.assign(2 * (2 + SCTX_WORDS), 0); img.sbits.assign(1, 0); img.sbits_words = 0;
     return;
   }
   static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
@@ -1312,14 +1312,15 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       for (auto& b : bits) img.sbits[(size_t)b.first * words + (b.second >> 5)] |= 1u << (b.second & 31);
       uint32_t slots = 2;
       while (slots < 2 * ctx.size()) slots <<= 1;
-      img.sctx.assign((size_t)slots * (1 + SCTX_WORDS), 0);  // fingerprints, then the slots
+      img.sctx.assign((size_t)slots * (2 + SCTX_WORDS), 0);  // (fingerprint, row) pairs, then the slots
       for (auto& c : ctx) {
         const auto& x = c.first;
         const uint32_t hash = ctx_key(key_pre(x[0], x[1], x[2], x[3], x[4]), x[5], x[6], x[7]);
         uint32_t h = hash & (slots - 1);
-        while (img.sctx[h]) h = (h + 1) & (slots - 1);
-        img.sctx[h] = ctx_fp(hash);
-        uint32_t* e = &img.sctx[slots + (size_t)h * SCTX_WORDS];
+        while (img.sctx[2 * h]) h = (h + 1) & (slots - 1);
+        img.sctx[2 * h] = ctx_fp(hash);
+        img.sctx[2 * h + 1] = c.second;
+        uint32_t* e = &img.sctx[2 * (size_t)slots + (size_t)h * SCTX_WORDS];
         e[0] = SCTX_USED | x[0];
         for (uint32_t j = 1; j < 8; j++) e[j] = x[j];
         e[8] = c.second;
@@ -2031,8 +2032,8 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   }
   if (img->lane_need > LANE_MAX) throw CedarError("corrupt image (lane scratch)");
   {
-    const size_t nc = img->sctx.size() / (1 + SCTX_WORDS);
-    if (!nc || (nc & (nc - 1)) || img->sctx.size() % (1 + SCTX_WORDS) ||
+    const size_t nc = img->sctx.size() / (2 + SCTX_WORDS);
+    if (!nc || (nc & (nc - 1)) || img->sctx.size() % (2 + SCTX_WORDS) ||
         (img->sbits_words && img->sbits.size() % img->sbits_words))
       throw CedarError("corrupt image (scope bitsets)");
     // every context row in range, fingerprints exactly on the used slots, and a free slot that
@@ -2040,11 +2041,11 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     size_t used = 0;
     const size_t rows = img->sbits_words ? img->sbits.size() / img->sbits_words : 0;
     for (size_t k = 0; k < nc; k++) {
-      const uint32_t* e = &img->sctx[nc + k * SCTX_WORDS];
-      if ((img->sctx[k] != 0) != (e[0] != 0)) throw CedarError("corrupt image (scope bitsets)");
+      const uint32_t* e = &img->sctx[2 * nc + k * SCTX_WORDS];
+      if ((img->sctx[2 * k] != 0) != (e[0] != 0)) throw CedarError("corrupt image (scope bitsets)");
       if (e[0]) {
         used++;
-        if (e[8] >= rows) throw CedarError("corrupt image (scope bitsets)");
+        if (e[8] >= rows || img->sctx[2 * k + 1] != e[8]) throw CedarError("corrupt image (scope bitsets)");
       }
     }
     if (used >= nc) throw CedarError("corrupt image (scope bitsets)");

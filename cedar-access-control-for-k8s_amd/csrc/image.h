@@ -198,9 +198,10 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 //            bit is set when that level-2 key exists.
 // Each context in use has a row of sbits_words words, one bit per key entity (index into
 // Image::key_ents, "kidx"). sctx: an open-addressed table of S slots (S a power of two) at
-// ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1) & (S - 1): first S fingerprint words
-// (ctx_fp of the key's hash, 0 = empty: a few KB, so a lookup that finds nothing costs one cached
-// word), then S slots of SCTX_WORDS [SCTX_USED | combo, at, ai, rt, ri, hs, v0, v1, row, 0, 0, 0]. A request looks up its contexts (per entity-
+// ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1) & (S - 1): first S (fingerprint, row) word
+// pairs (ctx_fp of the key's hash, 0 = empty; a few tens of KB: the device's lookup reads only
+// these, see cedar_scan_kernel), then S full slots of SCTX_WORDS [SCTX_USED | combo, at, ai, rt,
+// ri, hs, v0, v1, row, 0, 0, 0] (the host's validation and diagnostics). A request looks up its contexts (per entity-
 // principal combo: level 1, each value slot of l2_vmask with its own value, each element of its
 // list slots in l2_lmask) and tests one bit per principal key ancestor in each context found (the
 // encoder lists their kidx after the ancestor pairs: [n, (type, id) x n, kidx(self), kidx x keys],
@@ -435,7 +436,7 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 11;
+constexpr uint32_t IMG_VERSION = 12;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob
