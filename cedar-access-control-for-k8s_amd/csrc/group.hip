@@ -20,17 +20,13 @@
 #include <cstdlib>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "image.h"
 
 using namespace cgi;
 
 namespace {
-
-__global__ __launch_bounds__(256) void cedar_group_iota(uint32_t* __restrict__ v, uint32_t n) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) v[i] = i;
-}
 
 // GSEG lanes per request copy its row (uint4 pieces) to its grouped position
 constexpr uint32_t GSEG = 8;
@@ -67,7 +63,9 @@ uint32_t group_bits() {
 size_t group_temp_bytes(uint32_t n) {
   size_t bytes = 0;
   uint32_t* none = nullptr;
-  if (rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, none, none, none, none, n, 32 - group_bits(), 32) != hipSuccess) return 0;
+  if (rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, none, none, rocprim::counting_iterator<uint32_t>(0u), none, n,
+                                            32 - group_bits(), 32) != hipSuccess)
+    return 0;
   return bytes;
 }
 
@@ -77,11 +75,10 @@ int group_enqueue(const uint32_t* keys, const uint32_t* rows, uint32_t n, uint32
                   uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (row_words % 4) return -1;
-  hipLaunchKernelGGL(cedar_group_iota, dim3((n + 255) / 256), dim3(256), 0, s, vals, n);
-  if (hipGetLastError() != hipSuccess) return -1;
+  (void)vals;  // (the request indices come from a counting iterator: no iota pass)
   size_t bytes = temp_bytes;
-  if (rocprim::radix_sort_pairs<SortConfig>(temp, bytes, const_cast<uint32_t*>(keys), keys2, vals, ord, n, 32 - group_bits(), 32, s) !=
-      hipSuccess)
+  if (rocprim::radix_sort_pairs<SortConfig>(temp, bytes, const_cast<uint32_t*>(keys), keys2, rocprim::counting_iterator<uint32_t>(0u), ord,
+                                            n, 32 - group_bits(), 32, s) != hipSuccess)
     return -1;
   hipLaunchKernelGGL(cedar_group_gather, dim3((n + 256 / GSEG - 1) / (256 / GSEG)), dim3(256), 0, s, ord, n,
                      reinterpret_cast<const uint4*>(rows), row_words / 4, reinterpret_cast<uint4*>(grows));
