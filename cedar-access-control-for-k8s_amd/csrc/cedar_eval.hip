@@ -462,6 +462,25 @@ __device__ __forceinline__ bool lit_at(const uint8_t* s, uint32_t pos, const uin
   return ok;
 }
 
+// s[pos, pos + n) equals the literal packed in w (4 bytes per word): LIT_U bytes a round, their
+// loads issued together (a byte loop that stops at the first mismatch makes every byte load wait
+// for the previous compare: a `like "prod-*"` prefix was 5 dependent trips to memory)
+constexpr uint32_t LIT_U = 8;
+template <class P>
+__device__ __forceinline__ bool lit_eq(const uint8_t* s, uint32_t pos, P w, uint32_t n) {
+  for (uint32_t k0 = 0; k0 < n; k0 += LIT_U) {
+    uint32_t b[LIT_U];
+#pragma unroll
+    for (uint32_t j = 0; j < LIT_U; j++) b[j] = k0 + j < n ? (uint32_t)s[pos + k0 + j] : 0u;
+    bool ok = true;
+#pragma unroll
+    for (uint32_t j = 0; j < LIT_U; j++)
+      if (k0 + j < n) ok = ok && b[j] == ((w[(k0 + j) >> 2] >> (8 * ((k0 + j) & 3))) & 0xFFu);
+    if (!ok) return false;
+  }
+  return true;
+}
+
 // `pw` points at a compiled pattern (LDS record data or global constant pool)
 template <class CT, class P>
 __device__ __forceinline__ bool like_match(const CT& c, uint32_t sid, P pw) {
@@ -475,18 +494,13 @@ __device__ __forceinline__ bool like_match(const CT& c, uint32_t sid, P pw) {
   q += 1 + ((plen + 3) >> 2);
   if (!(flags & 1)) {
     if (slen != plen) return false;
-    bool ok = true;
-    for (uint32_t k = 0; k < plen && ok; k++) ok = s[k] == ((pw[pq + (k >> 2)] >> (8 * (k & 3))) & 0xFFu);
-    return ok;
+    return lit_eq(s, 0u, pw + pq, plen);
   }
   const uint32_t sl = pw[q];
   const uint32_t sq = q + 1;
   q += 1 + ((sl + 3) >> 2);
   if (slen < plen + sl) return false;
-  bool ok = true;
-  for (uint32_t k = 0; k < plen && ok; k++) ok = s[k] == ((pw[pq + (k >> 2)] >> (8 * (k & 3))) & 0xFFu);
-  for (uint32_t k = 0; k < sl && ok; k++) ok = s[slen - sl + k] == ((pw[sq + (k >> 2)] >> (8 * (k & 3))) & 0xFFu);
-  if (!ok) return false;
+  if (!lit_eq(s, 0u, pw + pq, plen) || !lit_eq(s, slen - sl, pw + sq, sl)) return false;
   uint32_t pos = plen;
   const uint32_t end = slen - sl;
   const uint32_t nmid = flags >> 8;
