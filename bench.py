@@ -418,8 +418,20 @@ def main():
 
     dist_on = world > 1
     if dist_on:
-        dist.init_process_group(backend="gloo")
-    device = local
+        # gloo prints its connection lines on stdout; rank 0's stdout carries only the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend="gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+    # one GPU per rank; CEDARGPU_BENCH_DEVICE pins every rank to one device (a multi-rank rehearsal
+    # on a one-GPU box: the RCCL reload then reports its error, RCCL wants distinct devices)
+    device = int(os.environ.get("CEDARGPU_BENCH_DEVICE", local))
 
     image = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", policies)], epoch=1, entities=entities)
     ctx = cedargpu.Context(device)
@@ -495,7 +507,7 @@ def main():
     parity = parity_sample(policies, items, idx, b, threads, entities) if rank == 0 and items else None
     configs = (secondary_configs(ctx, args.configs_requests, threads)
                if rank == 0 and world == 1 and args.configs_requests else None)
-    reload = hot_reload(ctx, policies, rank, world, local, dist_on, entities=entities) if args.reload else None
+    reload = hot_reload(ctx, policies, rank, world, device, dist_on, entities=entities) if args.reload else None
 
     if rank == 0:
         ms_per_step = wall_s * 1e3 / args.steps
@@ -537,9 +549,9 @@ def main():
                        "device_followup_requests": followups,
                        "rerun_requests": host_reruns,
                        "request_order": (f"{args.order} as uploaded; batches of >= 65,536 requests are grouped on the "
-                                         "device inside every timed step (grouping-key kernel + rocPRIM radix sort of "
-                                         "(action, resource type), principal key ancestors, hot values; the kernels read "
-                                         "requests in that order)" if os.environ.get("CEDARGPU_GROUP_DEV", "1") != "0"
+                                         "device inside every timed step (rocPRIM radix sort of the encoder's per-request "
+                                         "key over (action, resource type), principal key ancestors, hot values, and a "
+                                         "gather of the rows into that order)" if os.environ.get("CEDARGPU_GROUP_DEV", "1") != "0"
                                          else f"{args.order}; host radix sort at submit, outside the timed step (A/B)"),
                        "parallelism": f"request-sharded x{world}, image replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
