@@ -358,6 +358,14 @@ def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96)):
     return out
 
 
+def cpu_barrier(dist, torch):
+    """A barrier over gloo on a CPU tensor. With dist.barrier() between init_process_group and the
+    contexts, cg_ctx_create found no usable GPU in both ranks of a 2-rank rehearsal (torch's
+    accelerator query alone did not break it, profiles/r03/multi); torch's bundled HIP runtime must
+    stay out of this process, libcedargpu.so links ROCm's own."""
+    dist.all_reduce(torch.zeros(1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -424,7 +432,7 @@ def main():
         os.dup2(2, 1)
         try:
             dist.init_process_group(backend="gloo")
-            dist.barrier()
+            cpu_barrier(dist, torch)
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -460,13 +468,13 @@ def main():
         b.time(args.warmup)
     device_synchronize(device)
     if dist_on:
-        dist.barrier()
+        cpu_barrier(dist, torch)
     t0 = time.perf_counter()
     kernel_ms = b.time(args.steps)  # HIP events on the evaluation stream, K launches
     device_synchronize(device)
     wall_s = time.perf_counter() - t0
     if dist_on:
-        dist.barrier()
+        cpu_barrier(dist, torch)
         t = torch.tensor([wall_s, kernel_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall_s, kernel_ms = float(t[0]), float(t[1])

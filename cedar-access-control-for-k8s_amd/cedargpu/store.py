@@ -259,7 +259,7 @@ class Context:
         self._h = _P()
         rc = lib.cg_ctx_create(device, ctypes.byref(self._h))
         if rc:
-            raise DeviceError(rc, f"no usable GPU {device}")
+            raise DeviceError(rc, f"no usable GPU {device}: {lib.cg_last_error(None).decode()}")
 
     def close(self):
         if self._h:

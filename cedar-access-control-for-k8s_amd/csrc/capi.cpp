@@ -514,7 +514,7 @@ void cg_ctx_destroy(cg_ctx* ctx) {
   delete ctx;
 }
 
-const char* cg_last_error(cg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* cg_last_error(cg_ctx* ctx) { return ctx ? ctx->err.c_str() : dev_last_error(); }
 
 int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg) {
   if (!ctx) return CG_E_ARG;

@@ -126,6 +126,8 @@ int cg_device_count(int* n);
 int cg_device_synchronize(int device);
 int cg_ctx_create(int device, cg_ctx** out);
 void cg_ctx_destroy(cg_ctx* ctx);
+/* The context's last error; with ctx == NULL, the calling thread's last device error (why a
+ * cg_ctx_create or cg_device_count failed). */
 const char* cg_last_error(cg_ctx* ctx);
 /* Gameday fault injection for the fail-safe path (the evaluator's counterpart of the reference's
  * ErrorInjector, internal/server/error_injector.go:11-50, gated there by
