@@ -1476,7 +1476,9 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
 }
 
 // Per-wave LDS of the probe kernel, one region per request segment of SEG lanes.
-template <uint32_t SEG, uint32_t HCAP>
+// SLIM (one-request waves, images of <= RANK_POL policies): no hm; a hit's kind, tier and error
+// slot ride in its hp word (SLIM_* below), so the large stage's wave takes 8,960 B of LDS.
+template <uint32_t SEG, uint32_t HCAP, bool SLIM = false>
 struct SegLds {
   static constexpr uint32_t NS = 64 / SEG;     // requests per wave
   static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : 32;  // staged buckets per request (>= 2 stages)
@@ -1499,7 +1501,7 @@ struct SegLds {
     uint32_t hs[NS][HC + PAD];         // merge: sort keys (policy index << 12 | hit slot)
   } u;
   uint32_t hp[NS][HC + PAD];       // hit: global policy index
-  uint32_t hm[NS][HC + PAD];       // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
+  uint32_t hm[NS][SLIM ? 1 : HC + PAD];  // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
   uint32_t he[NS][XC * 4 + PAD];   // error details: code | aux << 8, k, et, ei
   uint2 hot[NS][NHOT + PAD];
 };
@@ -1618,6 +1620,9 @@ constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the res
 constexpr uint32_t SCAN_PB = 8;    // bit tests per lane per round (loads in flight)
 constexpr uint32_t MEMB_U = 4;     // duplicate-class members a lane copies per round (loads in flight)
 constexpr uint32_t RANK_POL = 16384;  // the large stage's rank pass: policy indices its bitmap covers
+// SLIM hit words: policy index (< RANK_POL) | kind << 14 | tier << 16 | error slot << 24
+constexpr uint32_t SLIM_KIND = 14, SLIM_TIER = 16, SLIM_SLOT = 24, SLIM_POL = 0x3FFFu;
+static_assert(RANK_POL - 1 <= SLIM_POL, "SLIM hit words hold a policy index below RANK_POL");
 __device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t k) {  // index of the k-th set bit of m
   for (uint32_t i = 0; i < k; i++) m &= m - 1;
   return m ? (uint32_t)__builtin_ctz(m) : 0u;
@@ -2012,10 +2017,13 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
 // [14] candidate evaluation [15] merge and result writes
 // PW: waves per block. Resources are granted per block, so a block's LDS and wave slots return
 // only when its slowest wave ends; smaller blocks let fast waves' slots be reused sooner.
-template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false, uint32_t PW = WAVES, bool SPLIT = false>
+// SLIM: the large stage over an image of <= RANK_POL policies (SegLds SLIM words; merge by bitmaps).
+template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false, uint32_t PW = WAVES, bool SPLIT = false,
+          bool SLIM = false>
 __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint64_t t_start = STATS ? clock64() : 0;
-  using L = SegLds<SEG, HCAP>;
+  static_assert(!SLIM || (SEG == 64 && HCAP >= 2 * RANK_POL / 32), "SLIM: one-request waves whose hs holds the bitmap");
+  using L = SegLds<SEG, HCAP, SLIM>;
   static_assert(L::HC <= 4096 && L::XC <= 255, "hit slots are 12-bit sort payloads, error slots 8-bit");
   constexpr uint32_t NS = L::NS;
   __shared__ L wl_all[PW];
@@ -2185,11 +2193,17 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t mincl = sscan(nmem);
       const uint64_t xmask = sballot(hit && err);
       const uint32_t xpos = nx + mbcnt64(xmask);
-      const uint32_t hmv = (err ? 2u : (flags & PF_FORBID) ? 1u : 0u) | (tier << 8) | (min(xpos, 0xFFu) << 16);
+      const uint32_t kind = err ? 2u : (flags & PF_FORBID) ? 1u : 0u;
+      const uint32_t hmv = SLIM ? (kind << SLIM_KIND) | (tier << SLIM_TIER) | (min(xpos, 0xFFu) << SLIM_SLOT)
+                                : kind | (tier << 8) | (min(xpos, 0xFFu) << 16);
       const uint32_t pos0 = nh + mincl - nmem;
       if (hit && !mlist && pos0 < L::HC) {
-        wl.hp[seg][pos0] = q2.z;  // PW_CODE: global policy index
-        wl.hm[seg][pos0] = hmv;
+        if constexpr (SLIM) {
+          wl.hp[seg][pos0] = q2.z | hmv;
+        } else {
+          wl.hp[seg][pos0] = q2.z;  // PW_CODE: global policy index
+          wl.hm[seg][pos0] = hmv;
+        }
       }
       // class members. One-request waves (the large stage): every hitting class's list at once.
       // Member m of the segment's classes (in lane order) finds its class lane by a binary search
@@ -2235,8 +2249,12 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
 #pragma unroll
           for (uint32_t u = 0; u < MEMB_U; u++)
             if (dst[u] < L::HC) {
-              wl.hp[seg][dst[u]] = v[u];
-              wl.hm[seg][dst[u]] = hv[u];
+              if constexpr (SLIM) {
+                wl.hp[seg][dst[u]] = v[u] | hv[u];
+              } else {
+                wl.hp[seg][dst[u]] = v[u];
+                wl.hm[seg][dst[u]] = hv[u];
+              }
             }
         }
       }
@@ -2408,110 +2426,177 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     a.res[2 * (size_t)wo + 1] = min(nh, 0xFFFFu) | (min(nh, 0xFFFFu) << 16);  // capacity hint
 
   }
-  uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge (after a rank pass: unique ones)
-  // One-request waves with many hits over an image of <= RANK_POL policies: a rank pass instead of
-  // the sort. A bitmap over policy indices (hs[0, 512)) takes every hit, prefix popcounts per word
-  // (hs[512, 1024)) give each hit its rank among the distinct policies, and the hits scatter to
-  // their ranks: five LDS passes instead of ~36 bitonic stages over 256-1024 keys (the large
-  // stage's merge was half its time: ~230 hits per request on C3, profiles/r03/ab14).
-  bool ranked = false;
-  if constexpr (SEG == 64 && HCAP >= 1024) {
-    if (nhm > 128 && a.n_pol <= RANK_POL) {
-      ranked = true;
+  uint32_t nf = 0, np = 0, nerr = 0;  // distinct deciding forbids / permits / errors
+  if constexpr (SLIM) {
+    // Merge by bitmaps over policy indices (wl.u.hs: the bitmap, then prefix popcounts per word):
+    // the deciding tier's forbids are marked first; when none, its permits. Every such hit then
+    // stores its policy at its rank among the marked ones (a duplicate stores the same index to the
+    // same place), and the errors the same way: the reasons come out in policy order with no sort,
+    // no hm words and no sort keys in LDS.
+    if (!undecided) {
       uint32_t* bm = wl.u.hs[0];
       uint32_t* pre = wl.u.hs[0] + RANK_POL / 32;
       const uint32_t W = (a.n_pol + 31) >> 5;
-      for (uint32_t w = lane; w < W; w += 64) bm[w] = 0u;
-      wave_lds_sync();
-      for (uint32_t i = lane; i < nhm; i += 64) {
-        const uint32_t p = wl.hp[0][i];
-        atomicOr(&bm[p >> 5], 1u << (p & 31));
-      }
-      wave_lds_sync();
       const uint32_t per = (W + 63) / 64, w0 = min(W, lane * per), w1 = min(W, w0 + per);
-      uint32_t cnt = 0;
-      for (uint32_t w = w0; w < w1; w++) cnt += __popc(bm[w]);
-      uint32_t inc = cnt;
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-        if (lane >= o) inc += y;
-      }
-      uint32_t run = inc - cnt;
-      for (uint32_t w = w0; w < w1; w++) {
-        pre[w] = run;
-        run += __popc(bm[w]);
-      }
-      const uint32_t uniq = (uint32_t)__shfl((int)inc, 63);
-      wave_lds_sync();
-      for (uint32_t i = lane; i < nhm; i += 64) {  // (the hit's policy keeps its place in hp)
-        const uint32_t p = wl.hp[0][i];
-        const uint32_t r = pre[p >> 5] + __popc(bm[p >> 5] & ((1u << (p & 31)) - 1u));
-        wl.hp[0][i] = (r << 16) | p;
-      }
-      wave_lds_sync();
-      for (uint32_t i = lane; i < nhm; i += 64) {  // duplicates write the same rank: either is kept
+      auto sel = [&](uint32_t x, uint32_t kind) {
+        return ((x >> SLIM_TIER) & 0xFFu) == t && ((x >> SLIM_KIND) & 3u) == kind;
+      };
+      auto mark = [&](uint32_t kind) -> uint32_t {  // bitmap and prefix counts; the distinct count
+        for (uint32_t w = lane; w < W; w += 64) bm[w] = 0u;
+        wave_lds_sync();
+        for (uint32_t i = lane; i < nh; i += 64) {
+          const uint32_t x = wl.hp[0][i];
+          if (sel(x, kind)) atomicOr(&bm[(x & SLIM_POL) >> 5], 1u << (x & 31u));
+        }
+        wave_lds_sync();
+        uint32_t cnt = 0;
+        for (uint32_t w = w0; w < w1; w++) cnt += __popc(bm[w]);
+        uint32_t inc = cnt;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+          const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+          if (lane >= o) inc += y;
+        }
+        uint32_t run = inc - cnt;
+        for (uint32_t w = w0; w < w1; w++) {
+          pre[w] = run;
+          run += __popc(bm[w]);
+        }
+        wave_lds_sync();
+        return (uint32_t)__shfl((int)inc, 63);
+      };
+      auto rank = [&](uint32_t p) { return pre[p >> 5] + __popc(bm[p >> 5] & ((1u << (p & 31u)) - 1u)); };
+      nf = mark(1u);
+      if (!nf) np = mark(0u);
+      const uint32_t kd = nf ? 1u : 0u;
+      bool anyerr = false;
+      for (uint32_t i = lane; i < nh; i += 64) {
         const uint32_t x = wl.hp[0][i];
-        wl.u.hs[0][x >> 16] = ((x & 0xFFFFu) << 12) | i;
-      }
-      wave_lds_sync();
-      nhm = uniq;
-    }
-  }
-  // bitonic sort of (policy index << 12 | slot) over the wave's largest power of two >= nh
-  uint32_t mloc = 2;
-  while (!ranked && mloc < nhm) mloc <<= 1;
-  uint32_t m = ranked ? 0u : mloc;
-  for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
-  for (uint32_t i = sl; !ranked && i < m; i += SEG) wl.u.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
-  wave_lds_sync();
-  for (uint32_t k = 2; !ranked && k <= m; k <<= 1) {
-    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i0 = 0; i0 < (m >> 1); i0 += SEG) {
-        const uint32_t q = i0 + sl;  // compare-exchange pair q
-        if (q < (m >> 1)) {
-          const uint32_t lo = ((q & ~(jj - 1u)) << 1) | (q & (jj - 1u)), hi = lo + jj;  // (jj: a power of two)
-          const uint32_t x = wl.u.hs[seg][lo], y = wl.u.hs[seg][hi];
-          const bool up = (lo & k) == 0;
-          if ((x > y) == up) { wl.u.hs[seg][lo] = y; wl.u.hs[seg][hi] = x; }
+        anyerr = anyerr || sel(x, 2u);
+        if (sel(x, kd)) {
+          const uint32_t p = x & SLIM_POL, rk = rank(p);
+          if (rk < a.capr) __builtin_nontemporal_store(p, a.reasons_f + (size_t)wo * a.capr + rk);
         }
       }
-      wave_lds_sync();
+      if (__ballot(anyerr)) {
+        wave_lds_sync();
+        nerr = mark(2u);
+        for (uint32_t i = lane; i < nh; i += 64) {
+          const uint32_t x = wl.hp[0][i];
+          if (!sel(x, 2u)) continue;
+          const uint32_t p = x & SLIM_POL, rk = rank(p), xs = x >> SLIM_SLOT;
+          if (rk < a.cape) {
+            uint32_t* er = a.errs + ((size_t)wo * a.cape + rk) * ERR_WORDS;
+            er[0] = p; er[1] = wl.he[0][4 * xs]; er[2] = wl.he[0][4 * xs + 1]; er[3] = wl.he[0][4 * xs + 2];
+            er[4] = wl.he[0][4 * xs + 3]; er[5] = 0;
+          }
+        }
+      }
     }
-  }
-  // deciding-tier hits, duplicates (adjacent after the sort) dropped; ranks by prefix counts.
-  // Only the deciding list is written, into reasons_f (the host passes reasons_p == reasons_f):
-  // a first sweep learns whether any forbid decides.
-  auto deciding = [&](uint32_t i, uint32_t& pj, uint32_t& mj) {
-    const bool have = i < nhm;
-    const uint32_t key = have ? wl.u.hs[seg][i] : 0xFFFFFFFFu;
-    pj = key >> 12;
-    mj = have ? wl.hm[seg][key & 0xFFF] : 0u;
-    return have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.u.hs[seg][i - 1] >> 12) != pj);
-  };
-  bool deny = false;
-  for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
-    uint32_t pj, mj;
-    const bool el = deciding(c0 + sl, pj, mj);
-    deny = deny || sballot(el && (mj & 0xFF) == 1) != 0;
-  }
-  uint32_t nf = 0, np = 0, nerr = 0;
-  for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
-    uint32_t pj, mj;
-    const bool el = deciding(c0 + sl, pj, mj);
-    const uint32_t kind = mj & 0xFF;
-    const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
-    const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
-    if (el && deny && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rf);
-    if (el && !deny && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rp);
-    if (el && kind == 2 && re < a.cape) {
-      const uint32_t xs = mj >> 16;
-      uint32_t* er = a.errs + ((size_t)wo * a.cape + re) * ERR_WORDS;
-      er[0] = pj; er[1] = wl.he[seg][4 * xs]; er[2] = wl.he[seg][4 * xs + 1]; er[3] = wl.he[seg][4 * xs + 2];
-      er[4] = wl.he[seg][4 * xs + 3]; er[5] = 0;
+  } else {
+    uint32_t nhm = undecided ? 0u : nh;  // this segment's hits to merge (after a rank pass: unique ones)
+    // One-request waves with many hits over an image of <= RANK_POL policies: a rank pass instead of
+    // the sort. A bitmap over policy indices (hs[0, 512)) takes every hit, prefix popcounts per word
+    // (hs[512, 1024)) give each hit its rank among the distinct policies, and the hits scatter to
+    // their ranks: five LDS passes instead of ~36 bitonic stages over 256-1024 keys (the large
+    // stage's merge was half its time: ~230 hits per request on C3, profiles/r03/ab14).
+    bool ranked = false;
+    if constexpr (SEG == 64 && HCAP >= 1024) {
+      if (nhm > 128 && a.n_pol <= RANK_POL) {
+        ranked = true;
+        uint32_t* bm = wl.u.hs[0];
+        uint32_t* pre = wl.u.hs[0] + RANK_POL / 32;
+        const uint32_t W = (a.n_pol + 31) >> 5;
+        for (uint32_t w = lane; w < W; w += 64) bm[w] = 0u;
+        wave_lds_sync();
+        for (uint32_t i = lane; i < nhm; i += 64) {
+          const uint32_t p = wl.hp[0][i];
+          atomicOr(&bm[p >> 5], 1u << (p & 31));
+        }
+        wave_lds_sync();
+        const uint32_t per = (W + 63) / 64, w0 = min(W, lane * per), w1 = min(W, w0 + per);
+        uint32_t cnt = 0;
+        for (uint32_t w = w0; w < w1; w++) cnt += __popc(bm[w]);
+        uint32_t inc = cnt;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+          const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+          if (lane >= o) inc += y;
+        }
+        uint32_t run = inc - cnt;
+        for (uint32_t w = w0; w < w1; w++) {
+          pre[w] = run;
+          run += __popc(bm[w]);
+        }
+        const uint32_t uniq = (uint32_t)__shfl((int)inc, 63);
+        wave_lds_sync();
+        for (uint32_t i = lane; i < nhm; i += 64) {  // (the hit's policy keeps its place in hp)
+          const uint32_t p = wl.hp[0][i];
+          const uint32_t r = pre[p >> 5] + __popc(bm[p >> 5] & ((1u << (p & 31)) - 1u));
+          wl.hp[0][i] = (r << 16) | p;
+        }
+        wave_lds_sync();
+        for (uint32_t i = lane; i < nhm; i += 64) {  // duplicates write the same rank: either is kept
+          const uint32_t x = wl.hp[0][i];
+          wl.u.hs[0][x >> 16] = ((x & 0xFFFFu) << 12) | i;
+        }
+        wave_lds_sync();
+        nhm = uniq;
+      }
     }
-    nf += popc64(bf);
-    np += popc64(bp);
-    nerr += popc64(be);
+    // bitonic sort of (policy index << 12 | slot) over the wave's largest power of two >= nh
+    uint32_t mloc = 2;
+    while (!ranked && mloc < nhm) mloc <<= 1;
+    uint32_t m = ranked ? 0u : mloc;
+    for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
+    for (uint32_t i = sl; !ranked && i < m; i += SEG) wl.u.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
+    wave_lds_sync();
+    for (uint32_t k = 2; !ranked && k <= m; k <<= 1) {
+      for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+        for (uint32_t i0 = 0; i0 < (m >> 1); i0 += SEG) {
+          const uint32_t q = i0 + sl;  // compare-exchange pair q
+          if (q < (m >> 1)) {
+            const uint32_t lo = ((q & ~(jj - 1u)) << 1) | (q & (jj - 1u)), hi = lo + jj;  // (jj: a power of two)
+            const uint32_t x = wl.u.hs[seg][lo], y = wl.u.hs[seg][hi];
+            const bool up = (lo & k) == 0;
+            if ((x > y) == up) { wl.u.hs[seg][lo] = y; wl.u.hs[seg][hi] = x; }
+          }
+        }
+        wave_lds_sync();
+      }
+    }
+    // deciding-tier hits, duplicates (adjacent after the sort) dropped; ranks by prefix counts.
+    // Only the deciding list is written, into reasons_f (the host passes reasons_p == reasons_f):
+    // a first sweep learns whether any forbid decides.
+    auto deciding = [&](uint32_t i, uint32_t& pj, uint32_t& mj) {
+      const bool have = i < nhm;
+      const uint32_t key = have ? wl.u.hs[seg][i] : 0xFFFFFFFFu;
+      pj = key >> 12;
+      mj = have ? wl.hm[seg][key & 0xFFF] : 0u;
+      return have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.u.hs[seg][i - 1] >> 12) != pj);
+    };
+    bool deny = false;
+    for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
+      uint32_t pj, mj;
+      const bool el = deciding(c0 + sl, pj, mj);
+      deny = deny || sballot(el && (mj & 0xFF) == 1) != 0;
+    }
+    for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
+      uint32_t pj, mj;
+      const bool el = deciding(c0 + sl, pj, mj);
+      const uint32_t kind = mj & 0xFF;
+      const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
+      const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
+      if (el && deny && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rf);
+      if (el && !deny && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rp);
+      if (el && kind == 2 && re < a.cape) {
+        const uint32_t xs = mj >> 16;
+        uint32_t* er = a.errs + ((size_t)wo * a.cape + re) * ERR_WORDS;
+        er[0] = pj; er[1] = wl.he[seg][4 * xs]; er[2] = wl.he[seg][4 * xs + 1]; er[3] = wl.he[seg][4 * xs + 2];
+        er[4] = wl.he[seg][4 * xs + 3]; er[5] = 0;
+      }
+      nf += popc64(bf);
+      np += popc64(bp);
+      nerr += popc64(be);
+    }
   }
   if (valid && !undecided && sl == 0) {
     const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);
@@ -3237,6 +3322,13 @@ static uint32_t probe_wpb() {
 // the large stage's register target: 3 waves per SIMD (168 VGPRs), which its LDS (3 four-wave
 // blocks per CU) also allows
 constexpr uint32_t BIG_MINW = 3;
+// ... and its SLIM form (images of <= RANK_POL policies): 8,960 B of LDS lets 4 waves per SIMD in,
+// so it asks for them (128 VGPRs); CEDARGPU_BIG_SLIM=0 keeps the hm form, =3 the SLIM form at 3 (A/B)
+constexpr uint32_t BIG_SLIM_MINW = 4;
+static uint32_t big_slim(const KArgs& k) {  // 0: the hm form; else the SLIM form's waves per SIMD
+  static const uint32_t on = [] { const char* e = std::getenv("CEDARGPU_BIG_SLIM"); return e ? (uint32_t)std::atoi(e) : BIG_SLIM_MINW; }();
+  return k.n_pol <= RANK_POL ? on : 0u;
+}
 // the probe kernel's per-wave STATS counters (cedar_probe_kernel), summed
 static void print_probe_stats(const char* what, const std::vector<unsigned long long>& h, size_t nw) {
   double sum[16] = {0};
@@ -3269,7 +3361,9 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
         KArgs ks = k;
         ks.stats = d;
         (void)hipMemsetAsync(d, 0, (size_t)n * 16 * 8, s);
-        hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, true, 1, true>), dim3(n), dim3(64), 0, s, ks);
+        if (big_slim(k) == BIG_SLIM_MINW) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_SLIM_MINW, true, 1, true, true>), dim3(n), dim3(64), 0, s, ks);
+        else if (big_slim(k)) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, true, 1, true, true>), dim3(n), dim3(64), 0, s, ks);
+        else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, true, 1, true>), dim3(n), dim3(64), 0, s, ks);
         std::vector<unsigned long long> h((size_t)n * 16);
         (void)hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
@@ -3278,7 +3372,9 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
       }
       return;
     }
-    if (bw == 1) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, 1, true>), dim3(n), dim3(64), 0, s, k);
+    if (bw == 1 && big_slim(k) == BIG_SLIM_MINW) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_SLIM_MINW, false, 1, true, true>), dim3(n), dim3(64), 0, s, k);
+    else if (bw == 1 && big_slim(k)) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, 1, true, true>), dim3(n), dim3(64), 0, s, k);
+    else if (bw == 1) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, 1, true>), dim3(n), dim3(64), 0, s, k);
     else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, WAVES, true>), dim3((n + WAVES - 1) / WAVES), dim3(BLOCK), 0, s, k);
     return;
   }
