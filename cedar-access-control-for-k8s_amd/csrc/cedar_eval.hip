@@ -92,6 +92,7 @@ struct KArgs {
   uint32_t l2_vmask, l2_lmask;         // hot slots with level-2 value / list keys (entity-principal combos)
   uint32_t scan_big;    // more scanned buckets than this: straight to the large stage (CEDARGPU_SCAN_BIG)
   uint32_t scan_heavy;  // more candidate heads than this: straight to the large stage (CEDARGPU_SCAN_HEAVY)
+  uint32_t cnt_rank;    // merges of <= this many hits per request rank by counting (CEDARGPU_CNT_RANK)
   uint32_t n_static, smask, lane_stride;
   // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
   // count at scan[i] (SCAN_OVF: more than SCAN_CAP), its (first head, count | combo) pairs at
@@ -137,6 +138,7 @@ struct Ctx {
   uint32_t pb0, pb1, pb2, pb3;            // principal ancestor-or-self Bloom
   uint32_t rb0, rb1, rb2, rb3;            // resource ancestor-or-self Bloom
   const uint32_t* rowx;                   // the row's element-hash list offsets per hot slot, or null
+  __device__ uint32_t hlist(uint32_t h) const { return rowx ? rowx[h] : 0xFFFFFFFFu; }
 };
 
 // Makes a value opaque to the optimizer. Used on context fields that feed a select: otherwise
@@ -668,7 +670,7 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
     case AK_CONTAINS: {
       if (tag_of(v) != T_SET) { type_err(e, TN_SET, v); return 2u; }
       const uint32_t ref = v.w0 & X_MASK, n = v.w1;
-      const uint32_t hl = c.rowx ? c.rowx[h] : 0xFFFFFFFFu;
+      const uint32_t hl = c.hlist(h);
       uint32_t th;
       if (hl != 0xFFFFFFFFu && reg_chash(w1, w2, w3, th)) {  // element hashes first, values on a match
         bool f = false;
@@ -693,7 +695,7 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
       if (tag_of(v) != T_SET) { type_err(e, TN_SET, v); return 2u; }
       const uint32_t ref = v.w0 & X_MASK, n = v.w1;
       bool f = false, deep = false;
-      const uint32_t hl = c.rowx ? c.rowx[h] : 0xFFFFFFFFu;
+      const uint32_t hl = c.hlist(h);
       if (hl != 0xFFFFFFFFu) {  // templates of primitives (constants, primitive holes): hashes first
         bool hashable = true;
         const uint32_t* t = d + 1 + nh;
@@ -1479,7 +1481,7 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
 // SLIM (one-request waves, images of <= RANK_POL policies): no hm; a hit's kind, tier and error
 // slot ride in its hp word (SLIM_* below), so the large stage's wave takes 8,960 B of LDS.
 template <uint32_t SEG, uint32_t HCAP, bool SLIM = false>
-struct SegLds {
+struct alignas(16) SegLds {  // (16: the counting merge reads hp four words at a time)
   static constexpr uint32_t NS = 64 / SEG;     // requests per wave
   static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : 32;  // staged buckets per request (>= 2 stages)
   static constexpr uint32_t HC = HCAP;         // hits per request (more: RF_BIG / RF_GENERAL re-run)
@@ -1520,7 +1522,11 @@ struct PCtx {
   static constexpr uint32_t hstride = 1;
   uint32_t pt, pi, at, ai, rt, ri;
   uint32_t p_anc, p_nanc, r_anc, r_nanc, a_anc, a_nanc;
-  const uint32_t* rowx;  // the row's element-hash list offsets per hot slot, or null
+  // the row's element-hash list offsets per hot slot: rowb[rowo + h] (rowb launch-uniform, so the
+  // per-request part is one 32-bit word: a 64-bit pointer here was the candidate pass's spill)
+  const uint32_t* rowb;
+  uint32_t rowo;  // 0xFFFFFFFF: none
+  __device__ uint32_t hlist(uint32_t h) const { return rowo != 0xFFFFFFFFu ? rowb[rowo + h] : 0xFFFFFFFFu; }
 };
 
 // X in (qt, qi) for X with UID (st, si) and ancestor pairs at blk[off + 2k]
@@ -2029,8 +2035,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   __shared__ L wl_all[PW];
   const uint32_t lane = threadIdx.x & 63;
   L& wl = wl_all[threadIdx.x >> 6];
-  const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
-  const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
+  // (not const: the merge recomputes them, below)
+  uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
+  uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
   auto sballot = [&](bool p) -> uint64_t { return __ballot(p) & smask; };
   auto sbcast = [&](uint32_t x, uint32_t k) -> uint32_t { return (uint32_t)__shfl((int)x, (int)(sbase + k)); };
   auto smin = [&](uint32_t x) -> uint32_t {
@@ -2046,9 +2053,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   };
   const uint32_t gid = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;
-  const bool valid = gid < n_req;
+  bool valid = gid < n_req;
   const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0u;
-  const uint32_t wo = a.req_idx ? gid : r;  // result slot: the worklist entry, or the request itself
   const uint32_t* row = (a.grows && !a.req_idx) ? a.grows + (size_t)(valid ? gid : 0u) * a.row_words : a.rows + (size_t)r * a.row_words;
 
   // the request row streams through once: non-temporal loads, header broadcast in the segment
@@ -2058,7 +2064,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
   PCtx c;
   c.blk = a.heap + hdr(RW_BLK);
-  c.rowx = (valid && a.hlists) ? row + RW_HDR + 2 * a.n_hot : nullptr;
+  c.rowb = (a.grows && !a.req_idx) ? a.grows : a.rows;
+  c.rowo = (valid && a.hlists) ? (uint32_t)(row - c.rowb) + RW_HDR + 2 * a.n_hot : 0xFFFFFFFFu;
   c.cpool = a.cpool;
   c.lh = wl.he[seg];  // atoms never address lane scratch (any valid pointer)
   c.gstr_off = a.gstr_off;
@@ -2417,6 +2424,16 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   }
   const uint64_t t_loop = STATS ? clock64() : 0;
   // ---- merge: deciding tier, duplicates, policy order ----
+  // The lane's indices and result slot are recomputed here from an opaque lane id (and the request
+  // order reloaded) instead of living across the candidate loop: kept live, they were the
+  // candidate pass's register spills, whose scratch stores were ~0.2 GB of writes per 1M step.
+  uint32_t lane_m = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(lane_m));
+  seg = lane_m / SEG; sl = lane_m % SEG; sbase = seg * SEG;
+  smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
+  const uint32_t gid_m = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
+  valid = gid_m < n_req;
+  const uint32_t wo = a.req_idx ? gid_m : (valid ? (a.ord ? a.ord[gid_m] : gid_m) : 0u);  // result slot
   const uint32_t t = min_tier;
   const bool structural = sballot(general) != 0;
   const bool undecided = nh > L::HC || nx > L::XC || structural;
@@ -2437,14 +2454,14 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       uint32_t* bm = wl.u.hs[0];
       uint32_t* pre = wl.u.hs[0] + RANK_POL / 32;
       const uint32_t W = (a.n_pol + 31) >> 5;
-      const uint32_t per = (W + 63) / 64, w0 = min(W, lane * per), w1 = min(W, w0 + per);
+      const uint32_t per = (W + 63) / 64, w0 = min(W, lane_m * per), w1 = min(W, w0 + per);
       auto sel = [&](uint32_t x, uint32_t kind) {
         return ((x >> SLIM_TIER) & 0xFFu) == t && ((x >> SLIM_KIND) & 3u) == kind;
       };
       auto mark = [&](uint32_t kind) -> uint32_t {  // bitmap and prefix counts; the distinct count
-        for (uint32_t w = lane; w < W; w += 64) bm[w] = 0u;
+        for (uint32_t w = lane_m; w < W; w += 64) bm[w] = 0u;
         wave_lds_sync();
-        for (uint32_t i = lane; i < nh; i += 64) {
+        for (uint32_t i = lane_m; i < nh; i += 64) {
           const uint32_t x = wl.hp[0][i];
           if (sel(x, kind)) atomicOr(&bm[(x & SLIM_POL) >> 5], 1u << (x & 31u));
         }
@@ -2454,7 +2471,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         uint32_t inc = cnt;
         for (uint32_t o = 1; o < 64; o <<= 1) {
           const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-          if (lane >= o) inc += y;
+          if (lane_m >= o) inc += y;
         }
         uint32_t run = inc - cnt;
         for (uint32_t w = w0; w < w1; w++) {
@@ -2469,7 +2486,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       if (!nf) np = mark(0u);
       const uint32_t kd = nf ? 1u : 0u;
       bool anyerr = false;
-      for (uint32_t i = lane; i < nh; i += 64) {
+      for (uint32_t i = lane_m; i < nh; i += 64) {
         const uint32_t x = wl.hp[0][i];
         anyerr = anyerr || sel(x, 2u);
         if (sel(x, kd)) {
@@ -2480,7 +2497,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       if (__ballot(anyerr)) {
         wave_lds_sync();
         nerr = mark(2u);
-        for (uint32_t i = lane; i < nh; i += 64) {
+        for (uint32_t i = lane_m; i < nh; i += 64) {
           const uint32_t x = wl.hp[0][i];
           if (!sel(x, 2u)) continue;
           const uint32_t p = x & SLIM_POL, rk = rank(p), xs = x >> SLIM_SLOT;
@@ -2506,20 +2523,20 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         uint32_t* bm = wl.u.hs[0];
         uint32_t* pre = wl.u.hs[0] + RANK_POL / 32;
         const uint32_t W = (a.n_pol + 31) >> 5;
-        for (uint32_t w = lane; w < W; w += 64) bm[w] = 0u;
+        for (uint32_t w = lane_m; w < W; w += 64) bm[w] = 0u;
         wave_lds_sync();
-        for (uint32_t i = lane; i < nhm; i += 64) {
+        for (uint32_t i = lane_m; i < nhm; i += 64) {
           const uint32_t p = wl.hp[0][i];
           atomicOr(&bm[p >> 5], 1u << (p & 31));
         }
         wave_lds_sync();
-        const uint32_t per = (W + 63) / 64, w0 = min(W, lane * per), w1 = min(W, w0 + per);
+        const uint32_t per = (W + 63) / 64, w0 = min(W, lane_m * per), w1 = min(W, w0 + per);
         uint32_t cnt = 0;
         for (uint32_t w = w0; w < w1; w++) cnt += __popc(bm[w]);
         uint32_t inc = cnt;
         for (uint32_t o = 1; o < 64; o <<= 1) {
           const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-          if (lane >= o) inc += y;
+          if (lane_m >= o) inc += y;
         }
         uint32_t run = inc - cnt;
         for (uint32_t w = w0; w < w1; w++) {
@@ -2528,13 +2545,13 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         }
         const uint32_t uniq = (uint32_t)__shfl((int)inc, 63);
         wave_lds_sync();
-        for (uint32_t i = lane; i < nhm; i += 64) {  // (the hit's policy keeps its place in hp)
+        for (uint32_t i = lane_m; i < nhm; i += 64) {  // (the hit's policy keeps its place in hp)
           const uint32_t p = wl.hp[0][i];
           const uint32_t r = pre[p >> 5] + __popc(bm[p >> 5] & ((1u << (p & 31)) - 1u));
           wl.hp[0][i] = (r << 16) | p;
         }
         wave_lds_sync();
-        for (uint32_t i = lane; i < nhm; i += 64) {  // duplicates write the same rank: either is kept
+        for (uint32_t i = lane_m; i < nhm; i += 64) {  // duplicates write the same rank: either is kept
           const uint32_t x = wl.hp[0][i];
           wl.u.hs[0][x >> 16] = ((x & 0xFFFFu) << 12) | i;
         }
@@ -2546,10 +2563,30 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     uint32_t mloc = 2;
     while (!ranked && mloc < nhm) mloc <<= 1;
     uint32_t m = ranked ? 0u : mloc;
-    for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
-    for (uint32_t i = sl; !ranked && i < m; i += SEG) wl.u.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
+    // (a bpermute on lane_m: __shfl_xor's own lane id is the prologue's, which then stays live)
+    for (uint32_t o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane_m ^ o) << 2), (int)m));
+    // Small merges (every segment of the wave <= a.cnt_rank hits): each hit's rank is the number of
+    // the segment's keys below its own, every compare's LDS read in flight at once, instead of the
+    // bitonic network's log^2 dependent stages (keys are unique: the slot is in the low bits).
+    const bool counted = !ranked && m <= a.cnt_rank;
+    if (counted) {
+      for (uint32_t i = sl; i < nhm; i += SEG) {
+        const uint32_t ki = (wl.hp[seg][i] << 12) | i;
+        uint32_t rk = 0;
+        for (uint32_t j = 0; j < nhm; j += 4) {
+          const uint4 h4 = *reinterpret_cast<const uint4*>(&wl.hp[seg][j]);
+          rk += (((h4.x << 12) | j) < ki) ? 1u : 0u;
+          rk += (j + 1 < nhm && ((h4.y << 12) | (j + 1)) < ki) ? 1u : 0u;
+          rk += (j + 2 < nhm && ((h4.z << 12) | (j + 2)) < ki) ? 1u : 0u;
+          rk += (j + 3 < nhm && ((h4.w << 12) | (j + 3)) < ki) ? 1u : 0u;
+        }
+        wl.u.hs[seg][rk] = ki;
+      }
+      wave_lds_sync();
+    }
+    for (uint32_t i = sl; !ranked && !counted && i < m; i += SEG) wl.u.hs[seg][i] = i < nhm ? ((wl.hp[seg][i] << 12) | i) : 0xFFFFFFFFu;
     wave_lds_sync();
-    for (uint32_t k = 2; !ranked && k <= m; k <<= 1) {
+    for (uint32_t k = 2; !ranked && !counted && k <= m; k <<= 1) {
       for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
         for (uint32_t i0 = 0; i0 < (m >> 1); i0 += SEG) {
           const uint32_t q = i0 + sl;  // compare-exchange pair q
@@ -2613,9 +2650,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     for (uint32_t i = 0; i < 12; i++) {
       uint32_t x = valid ? st[i] : 0u;
       for (uint32_t o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, (int)o);
-      if (lane == 0) w[i] = x;
+      if (lane_m == 0) w[i] = x;
     }
-    if (lane == 0) {
+    if (lane_m == 0) {
       w[12] = t_load - t_start;
       w[13] = (t_loop - t_load) - t_cand;
       w[14] = t_cand;
@@ -3246,6 +3283,8 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   static const uint32_t scan_big = [] { const char* e = std::getenv("CEDARGPU_SCAN_BIG"); return e ? (uint32_t)std::atoi(e) : 48u; }();
   static const uint32_t scan_heavy = [] { const char* e = std::getenv("CEDARGPU_SCAN_HEAVY"); return e ? (uint32_t)std::atoi(e) : 128u; }();
   k.scan_heavy = scan_heavy;
+  static const uint32_t cnt_rank = [] { const char* e = std::getenv("CEDARGPU_CNT_RANK"); return e ? (uint32_t)std::atoi(e) : 32u; }();
+  k.cnt_rank = cnt_rank;
   k.scan_big = scan_big;
   k.stats = nullptr;
   k.n_dev = nullptr;

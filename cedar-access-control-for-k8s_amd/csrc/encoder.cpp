@@ -64,6 +64,8 @@ void Batch::append(EncodedRequest& e) {
   if (!row_words) row_words = img->row_words();
   if (e.row.size() != row_words || e.blk.size() < RH_WORDS) throw CedarError("request encoded for another image");
   if (heap.size() + e.blk.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
+  // (the probe kernel addresses a row's words by a 32-bit offset, PCtx::rowo)
+  if (rows.size() + row_words > 0xFFFFFFFFull) throw CedarError("batch rows exceed 16 GiB");
   size_t sbytes = 0;
   for (auto& s : e.strs) sbytes += s.size();
   if (n_bstr() + e.strs.size() >= 0xFFFFFFFFull || bstr_bytes.size() + sbytes > 0xFFFFFFFFull)

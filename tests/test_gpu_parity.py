@@ -291,6 +291,24 @@ def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, group, m
         check_items(ctx, stores, items)
 
 
+@pytest.mark.parametrize("first_tier_hits", [0, 3, 150])
+def test_large_stage_tiers_forbids_and_errors(ctx, first_tier_hits):
+    """The large stage's merge (its SLIM form on images of <= 16,384 policies: kind, tier and error
+    slot in the hit word, bitmaps over policy indices) over two tiers: the deciding tier is the
+    first with a hit; its forbids, else its permits, are the reasons, and its errors (attributes the
+    request lacks) are listed; duplicate-class members and hits of the other tier are dropped."""
+    t0 = "\n".join(f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 5} }};'
+                   for i in range(first_tier_hits))
+    t1 = "\n".join((f'forbid (principal in k8s::Group::"g{i % 3}", action == k8s::Action::"get", resource) '
+                    f'when {{ principal.nick == "n{i % 4}" }};') if i % 9 == 0 else
+                   f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
+                   for i in range(400))
+    stores = [cedargpu.MemoryStore("tier0.cedar", t0), cedargpu.MemoryStore("tier1.cedar", t1)]
+    g = Gen(97)
+    items = [g.item() for _ in range(300)]
+    check_items(ctx, stores, items)
+
+
 def test_followup_sized_by_previous_batch(ctx):
     """Most requests collect > 64 reasons: the first batch on an image follows up at most 64 of
     them on the device and re-runs the rest from the host; the next batch on that image sizes its
