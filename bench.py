@@ -391,6 +391,8 @@ def main():
                     help="caller threads of the serving-queue check (0: skip)")
     ap.add_argument("--serve-requests", type=int, default=262_144)
     ap.add_argument("--serve-max-batch", type=int, default=8192)
+    ap.add_argument("--no-submit-to-results", dest="submit_to_results", action="store_false",
+                    help="skip the 1M-request submit -> results measurement after the timed region")
     ap.add_argument("--configs-requests", type=int, default=32_768,
                     help="requests per secondary config (C2, C4) after the timed region (0: skip)")
     args = ap.parse_args()
@@ -461,6 +463,7 @@ def main():
     b.wait()  # correctness pass: results downloaded, follow-ups folded, host re-runs (if any) done
     t_first = time.perf_counter()
     followups, host_reruns = b.followups(), b.reruns()
+    io = b.io()
     n_reasons = [b.reasons(i)[0].__len__() for i in range(len(b))]
     alg_bytes = algorithmic_bytes(sars, n_reasons, has_like=True)
 
@@ -486,6 +489,30 @@ def main():
         phases = {k: v / split_steps for k, v in phases.items()}
     except AttributeError:  # an A/B build (CEDARGPU_AB_LIB) that predates cg_batch_time_split
         phases, split_total = {"total": kernel_ms / args.steps * split_steps}, kernel_ms / args.steps * split_steps
+
+    # the same 1M-request batch from the webhook's side: encoded again (SAR bodies -> request
+    # blocks on the host threads), then submit -> results visible on the host, timed on the warm
+    # buffer pool: string finalize, pinned staging, the one H2D copy, the complete step, the D2H
+    # copy and the result binding. Outside the timed region (PCIe-inclusive; not `value`).
+    s2r = None
+    if rank == 0 and args.submit_to_results:
+        payload2 = synth.sars_json(sars)
+        b2 = ctx.batch()
+        t0e = time.perf_counter()
+        b2.add_sar_json(payload2)
+        t1e = time.perf_counter()
+        del payload2
+        b2.submit()
+        b2.wait()
+        t2e = time.perf_counter()
+        io2 = b2.io()
+        s2r = {"requests": len(b2), "encode_s": t1e - t0e, "encode_per_s": len(b2) / (t1e - t0e),
+               "submit_to_results_ms": (t2e - t1e) * 1e3, "decisions_per_s": len(b2) / (t2e - t1e),
+               "h2d_bytes": io2["h2d_bytes"], "d2h_bytes": io2["d2h_bytes"],
+               "what": "cg_batch_add_sar_json over the 1M SAR bodies (host threads), then cg_batch_submit -> "
+                       "cg_batch_wait: H2D of the request heap / rows / strings, the complete device step, "
+                       "D2H of the results"}
+        b2.close()
 
     # submit -> results-visible latency on small batches (includes H2D, launch, D2H)
     lat = []
@@ -521,8 +548,16 @@ def main():
         ms_per_step = wall_s * 1e3 / args.steps
         decisions = args.batch * world * args.steps
         avg_kernel_ms = kernel_ms / args.steps
-        achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
-        traffic = None
+        step_achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        # the dominant kernel: the step phase with the most device time (HIP events on the step's
+        # stream at every phase boundary); SURVEY §8(d) prices the whole decision's bytes, so
+        # `achieved` is those bytes over that kernel's time (the whole step's figure beside it)
+        dom = max((k for k in phases if k != "total"), key=phases.get) if len(phases) > 1 else "total"
+        dom_ms = phases.get(dom, avg_kernel_ms)
+        achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+        dom_kernel = {"scan": "cedar_scan_kernel<8, 6, true>", "candidates": "cedar_probe_kernel<8, 64, 4, SPLIT>",
+                      "fu_big": "cedar_probe_kernel<64, 1024, 4, SPLIT, SLIM>", "group": "rocPRIM onesweep + cedar_group_gather"}.get(dom, dom)
+        traffic, pmc_kernels = None, None
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
         if os.path.exists(pmc):
             try:
@@ -530,8 +565,21 @@ def main():
                 if (pj.get("policies") == args.policies and pj.get("batch") == args.batch
                         and pj.get("hierarchy", "flat") == args.hierarchy):
                     traffic = pj.get("hbm_bytes_per_launch")
+                    pmc_kernels = pj.get("kernels")
             except Exception:
                 traffic = None
+        # VALU busy fraction of the dominant kernel (SURVEY §8(d) honesty note): a wave64 VALU
+        # instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md), 1,024 SIMDs at 2.4 GHz
+        valu = None
+        prefix = {"scan": "cedar_scan_kernel<8u, 6u, true", "candidates": "cedar_probe_kernel<8u, 64u"}.get(dom)
+        if pmc_kernels and prefix:
+            for name, c in pmc_kernels.items():
+                if name.startswith(prefix) and "SQ_INSTS_VALU" in c:
+                    valu = {"kernel": name, "valu_insts": c["SQ_INSTS_VALU"],
+                            "valu_busy_frac": c["SQ_INSTS_VALU"] * 2 / (1024 * 2.4e9 * dom_ms * 1e-3),
+                            "valu_share_of_issued": c["SQ_INSTS_VALU"] / max(1.0, c["SQ_INSTS_VALU"] + c.get("SQ_INSTS_SALU", 0)
+                                                                            + c.get("SQ_INSTS_VMEM_RD", 0) + c.get("SQ_INSTS_LDS", 0))}
+                    break
         out = {
             "metric": "authz decisions/sec (node) at 10k policies",
             "value": decisions / wall_s,
@@ -564,13 +612,24 @@ def main():
                        "parallelism": f"request-sharded x{world}, image replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "dominant_kernel": dom_kernel, "dominant_phase": dom, "dominant_kernel_ms": dom_ms,
+                         "step_achieved": step_achieved, "step_frac": step_achieved / HBM_PEAK_GBS,
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes_per_decision": alg_bytes / args.batch,
                          "phases_ms": phases, "phases_total_ms": split_total / split_steps,
-                         "dominant_phase": max(phases, key=phases.get),
-                         "launch": "one complete step on one stream: the device grouping (key kernel + rocPRIM sort), cedar_scan_kernel, the SPLIT candidate pass, "
-                                   "cedar_fu_gather and the follow-up launches (rocprofv3 split in profiles/r02/)",
+                         "valu": valu,
+                         "launch": "one complete step on one stream: the device grouping (rocPRIM onesweep sort of the encoder's "
+                                   "keys + cedar_group_gather), cedar_scan_kernel, the SPLIT candidate pass, cedar_fu_gather and "
+                                   "the follow-up launches (rocprofv3 split in profiles/r04/)",
+                         "achieved_is": "SURVEY §8(d) algorithmic bytes of every decision in the step / the dominant kernel's "
+                                        "time (HIP events at its phase boundaries); step_achieved: over the whole step",
                          "traffic_source": "PMC FETCH_SIZE x2 + WRITE_SIZE summed over one step's dispatches "
                                            "(tools/pmc_kernels.sh, profiles/pmc_latest.json)" if traffic else None},
+            "transfer": {"h2d_bytes_per_request": io["h2d_bytes"] / args.batch, "d2h_bytes_per_request": io["d2h_bytes"] / args.batch,
+                         "ancestor_list_words": io["list_words"], "ancestor_list_words_shared": io["list_words_shared"],
+                         "what": "the one H2D upload (request heap with interned ancestor lists, rows, strings, grouping "
+                                 "keys) and the one D2H result copy of the 1M-request batch"},
+            "submit_to_results_1m": s2r,
             "cpu_baseline": baseline,
             "parity_sample": parity,
             "reload": reload,

@@ -9,7 +9,7 @@ The product path has no CPU fallback: importing this package fails loudly when l
 is missing, and evaluation raises `DeviceError` when no GPU is present.
 """
 from ._lib import CedarGPUError, CompileError, DeadlineError, DeviceError, lib, lib_path  # noqa: F401
-from .store import (ALLOW_ALL_ADMISSION, FAULT_DEVICE_ERROR, FAULT_NONE, FAULT_STALL, AdmissionHandler,  # noqa: F401
+from .store import (ALLOW_ALL_ADMISSION, FAULT_BAD_KIDX, FAULT_DEVICE_ERROR, FAULT_NONE, FAULT_STALL, AdmissionHandler,  # noqa: F401
                     Authorizer, AVPStore, Batch, Compiler, Context, CRDStore, DirectoryStore, MemoryStore, PolicyStore,
                     Queue, StaticStore, TieredPolicyStores, admission_to_cedar_json, atomic_policies, build_image,
-                    device_count, image_stats)
+                    device_count, image_stats, index_stats)

@@ -80,6 +80,7 @@ _SIGS = {
     "cg_image_stats": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u32)] * 4),
     "cg_image_policy_atomic": (ctypes.c_int, [P, sz, u32, ctypes.POINTER(ctypes.c_int)]),
     "cg_image_indexed": (ctypes.c_int, [P, sz, ctypes.POINTER(ctypes.c_int)]),
+    "cg_image_index_stats": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u32)] * 6),
     "cg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "cg_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "cg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(P)]),
@@ -111,12 +112,15 @@ _SIGS = {
     "cg_batch_reruns": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
     "cg_batch_followups": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
     "cg_batch_bytes": (ctypes.c_int, [P, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+    "cg_batch_io": (ctypes.c_int, [P] + [ctypes.POINTER(ctypes.c_uint64)] * 4),
     "cg_batch_add_sar_json": (ctypes.c_int, [P, cstr, sz]),
     "cg_sar_to_cedar_json": (ctypes.c_int, [cstr, sz, P, sz, ctypes.POINTER(sz)]),
     "cg_batch_authz": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
     "cg_is_authorized_json": (ctypes.c_int, [P, cstr, sz, ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz)]),
     "cg_encode_sar_check": (ctypes.c_int, [P, sz, cstr, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
                                            ctypes.POINTER(u32), ctypes.POINTER(i64)]),
+    "cg_encode_items_check": (ctypes.c_int, [P, sz, cstr, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                             ctypes.POINTER(i64)]),
     "cg_batch_add_admission_json": (ctypes.c_int, [P, cstr, sz]),
     "cg_batch_admit": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), P, sz,
                                       ctypes.POINTER(sz)]),

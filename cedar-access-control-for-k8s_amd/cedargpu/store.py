@@ -18,7 +18,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
 from ._lib import CG_E_RANGE, CompileError, DeadlineError, DeviceError, _err, lib
 
-FAULT_NONE, FAULT_DEVICE_ERROR, FAULT_STALL = 0, 1, 2
+FAULT_NONE, FAULT_DEVICE_ERROR, FAULT_STALL, FAULT_BAD_KIDX = 0, 1, 2, 3
 DOC_SKIP_INVALID = 1
 
 
@@ -240,6 +240,16 @@ def image_stats(image: bytes) -> dict:
             "hot": u[3].value, "actions": u[4].value, "stream_words": u[5].value, "indexed": bool(ix.value)}
 
 
+def index_stats(image: bytes) -> dict:
+    """Scope-index shape of a compiled image (cg_image_index_stats): list-keyed hot slots, key
+    combos, index entries, scope-bitset contexts."""
+    u = [ctypes.c_uint32() for _ in range(6)]
+    if lib.cg_image_index_stats(image, len(image), *(ctypes.byref(x) for x in u)):
+        raise ValueError("not a compiled policy image")
+    return dict(zip(("cslot_mask", "pslot_mask", "combo_mask", "entries", "contexts", "sbits_words"),
+                    (x.value for x in u)))
+
+
 def atomic_policies(image: bytes) -> List[bool]:
     """Per policy (image order): lowered to predicate atoms (True) or bytecode."""
     n = image_stats(image)["policies"]
@@ -303,7 +313,8 @@ class Context:
 
     def inject_fault(self, kind: int, arg: int = 0):
         """Gameday fault injection (cg_ctx_inject_fault): FAULT_DEVICE_ERROR fails the next `arg`
-        submits, FAULT_STALL delays every batch by `arg` microseconds on the device."""
+        submits, FAULT_STALL delays every batch by `arg` microseconds on the device, FAULT_BAD_KIDX
+        makes the next `arg` batches carry key-entity indices of another image (they fail)."""
         rc = lib.cg_ctx_inject_fault(self._h, kind, arg)
         if rc:
             raise _err(rc, "inject_fault failed")
@@ -460,6 +471,15 @@ class Batch:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         lib.cg_batch_bytes(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return a.value, b.value, c.value
+
+    def io(self) -> dict:
+        """PCIe bytes of the submitted batch (one H2D upload, one D2H result copy) and its ancestor-
+        list words, total and served by an interned copy (cg_batch_io)."""
+        v = [ctypes.c_uint64() for _ in range(4)]
+        rc = lib.cg_batch_io(self._h, *(ctypes.byref(x) for x in v))
+        if rc:
+            raise _err(rc, "batch io failed")
+        return dict(zip(("h2d_bytes", "d2h_bytes", "list_words", "list_words_shared"), (x.value for x in v)))
 
 
 class Queue:

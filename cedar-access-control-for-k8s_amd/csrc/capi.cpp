@@ -11,6 +11,7 @@
 
 #include "admission.h"
 #include "capi_internal.h"
+#include "encode_impl.h"
 #include "sar.h"
 
 namespace {
@@ -154,7 +155,7 @@ void group_requests(cg_batch* b) {
     const uint64_t ar = mix(mix(0x51ED27Fu, row[cgi::RW_A + 1]), row[cgi::RW_R]);
     // groups: the principal's ancestor (type, id) pairs
     uint64_t g = mix(0x9E3779B97F4A7C15ull, row[cgi::RW_P]);
-    const size_t anc = (size_t)row[cgi::RW_BLK] + row[cgi::RW_PANC];
+    const size_t anc = (uint32_t)(row[cgi::RW_BLK] + row[cgi::RW_PANC]);  // (signed offset: mod 2^32)
     for (uint32_t j = 0; j < 2 * (row[cgi::RW_PN] & cgi::AN_COUNT) && anc + j < h.heap.size(); j++) g = mix(g, h.heap[anc + j]);
     uint64_t hv = 0x2545F4914F6CDD1Dull;
     for (uint32_t j = cgi::RW_HDR; j < rw; j++) hv = mix(hv, row[j]);
@@ -183,33 +184,100 @@ void group_requests(cg_batch* b) {
     if (it.dev >= 0) it.dev = (int32_t)slot[(uint32_t)it.dev];
 }
 
-// One SubjectAccessReview through the webhook's host steps, into `e` (or a fast-path decision).
-struct SarSlot {
-  int fast = -1;
-  std::string reason, err;
-  int rc = CG_OK;
-  EncodedRequest e;
-};
-
-void sar_to_slot(const Image& img, const char* p, size_t n, SarSlot& s) {
-  try {
-    const int d = encode_sar_direct(img, p, n, s.e, s.fast, s.reason);
-    if (d == 2) return;
-    s.fast = -1;
-    if (d == 1) return;
-    JVal v = json_parse(p, n);
-    Attributes a = attributes_from_sar(v);
-    s.fast = authorize_fast_path(a, s.reason);
-    if (s.fast >= 0) return;
-    std::vector<EntityIn> ents;
-    RequestIn req;
-    record_to_cedar(a, ents, req);
-    encode_request(img, ents, req, s.e);
-  } catch (const CedarError& e) {
-    s.err = e.what(); s.rc = CG_E_PARSE;
-  } catch (const std::exception& e) {
-    s.err = e.what(); s.rc = CG_E_ARG;
+// CG_FAULT_BAD_KIDX: every principal's key-entity indices (image.h "scope bitsets") pushed past
+// the image's key entities, as a batch encoded for another image would carry them (lists are
+// shared between requests: the change is idempotent).
+void corrupt_key_indices(Batch& h) {
+  if (!h.img->sbits_words) return;
+  const uint32_t rw = h.row_words;
+  for (uint32_t i = 0; i < h.n(); i++) {
+    const uint32_t* row = h.rows.data() + (size_t)i * rw;
+    if (!row[cgi::RW_PANC]) continue;
+    const uint32_t pn = row[cgi::RW_PN], n = pn & cgi::AN_COUNT, keys = (pn >> cgi::AN_KEYS_SHIFT) & cgi::AN_KEYS;
+    uint32_t* kl = h.heap.data() + (uint32_t)(row[cgi::RW_BLK] + row[cgi::RW_PANC]) + 2 * (size_t)n;
+    for (uint32_t j = 0; j <= keys; j++)
+      if (kl[j] != cgi::KIDX_NONE) kl[j] |= 0x40000000u;
   }
+}
+
+// Bulk encoding (cg_batch_add_sar_json / cg_batch_add_admission_json over a JSON array of at least
+// 64 KiB). The elements split into contiguous chunks; worker threads take chunks in turn and encode
+// each element straight into the chunk's own Batch part (ancestor lists interned per part), and the
+// parts are concatenated in order with their offsets shifted, side by side (Batch::concat). No
+// per-element buffers and no serial append. All or nothing: the first failing element's error is
+// returned and the batch is left as it was.
+struct BulkOut {
+  bool host = false;  // decided on the host (fast path / skip / review error): no device request
+  int fast = -1;
+  std::string reason;
+};
+template <class F>  // f(element k, EncodedRequest& e, BulkOut& o): encodes e, or sets o.host
+int bulk_add(cg_batch* b, size_t n, F&& f) {
+  const unsigned t = host_workers(n);
+  const size_t per = std::max<size_t>(256, (n + 8 * (size_t)t - 1) / (8 * (size_t)t));
+  const size_t nc = (n + per - 1) / per;
+  struct Chunk {
+    Batch part;
+    std::vector<int32_t> fast;  // per element: -1 a device request, else its host result
+    std::vector<std::pair<uint32_t, std::string>> reasons;  // (element in chunk, reason / error text)
+    int rc = CG_OK;
+    std::string err;
+  };
+  std::vector<Chunk> ch(nc);
+  for (auto& c : ch) c.part.img = b->host.img;
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    EncodedRequest e;
+    BulkOut o;
+    for (size_t c; (c = next++) < nc;) {
+      Chunk& C = ch[c];
+      const size_t lo = c * per, hi = std::min(n, lo + per);
+      C.fast.reserve(hi - lo);
+      for (size_t k = lo; k < hi; k++) {
+        o.host = false;
+        o.fast = -1;
+        o.reason.clear();
+        try {
+          f(k, e, o);
+          if (!o.host) C.part.append(e);
+        } catch (const CedarError& x) {
+          C.rc = CG_E_PARSE; C.err = x.what();
+        } catch (const std::bad_alloc&) {
+          C.rc = CG_E_ARG; C.err = "out of host memory";
+        } catch (const std::exception& x) {
+          C.rc = CG_E_ARG; C.err = x.what();
+        }
+        if (C.rc) break;
+        if (o.host && !o.reason.empty()) C.reasons.emplace_back((uint32_t)(k - lo), std::move(o.reason));
+        C.fast.push_back(o.host ? o.fast : -1);
+      }
+    }
+  };
+  {
+    std::vector<std::thread> ws;
+    for (unsigned k = 1; k < t; k++) ws.emplace_back(work);
+    work();
+    for (auto& w : ws) w.join();
+  }
+  for (auto& c : ch)  // chunks are contiguous and stop at their first failure: the first one in order
+    if (c.rc) { b->err = c.err; return c.rc; }
+  GUARD(b->err, {
+    size_t n_items = b->items.size();
+    for (auto& c : ch) n_items += c.fast.size();
+    b->items.reserve(n_items);
+    int32_t dev = (int32_t)b->host.n();
+    std::vector<Batch> parts;
+    parts.reserve(nc);
+    for (auto& c : ch) {
+      const uint32_t i0 = (uint32_t)b->items.size();
+      for (const int32_t f : c.fast) b->items.push_back(f < 0 ? cg_batch::Item{dev++, -1} : cg_batch::Item{-1, f});
+      for (auto& r : c.reasons) b->fast_reason[i0 + r.first] = std::move(r.second);
+      parts.push_back(std::move(c.part));
+    }
+    ch.clear();
+    b->host.concat(parts, t);
+    return CG_OK;
+  })
 }
 
 // cg_encode_sar_check: every SAR of the array through the direct path and the general path.
@@ -241,8 +309,18 @@ int encode_sar_check(const void* image, size_t len, const char* sars, size_t n, 
       RequestIn req;
       record_to_cedar(at, ents, req);
       EncodedRequest general;
-      encode_request(*img, ents, req, general);
-      same = d == 1 && direct.blk == general.blk && direct.row == general.row && direct.strs == general.strs;
+      // the general path walks every hierarchy itself, so the direct path's cached ancestor
+      // records (encode_impl.h ClosureCache) are checked against the walk word for word
+      enc::t_no_closure_cache = true;
+      try {
+        encode_request(*img, ents, req, general);
+      } catch (...) {
+        enc::t_no_closure_cache = false;
+        throw;
+      }
+      enc::t_no_closure_cache = false;
+      same = d == 1 && direct.blk == general.blk && direct.row == general.row && direct.strs == general.strs &&
+             direct.anc == general.anc && direct.anc_at == general.anc_at;
     }
     if (!same) {
       nm++;
@@ -456,6 +534,23 @@ int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* 
   }
 }
 
+int cg_image_index_stats(const void* image, size_t len, uint32_t* cslot_mask, uint32_t* pslot_mask, uint32_t* combo_mask,
+                         uint32_t* entries, uint32_t* contexts, uint32_t* sbits_words) {
+  if (!image) return CG_E_ARG;
+  try {
+    auto img = Image::deserialize((const uint8_t*)image, len);
+    if (cslot_mask) *cslot_mask = img->cslot_mask;
+    if (pslot_mask) *pslot_mask = img->pslot_mask;
+    if (combo_mask) *combo_mask = img->combo_mask;
+    if (entries) *entries = (uint32_t)(img->btab.size() / cgi::BT_WORDS);
+    if (contexts) *contexts = img->sbits_words ? (uint32_t)(img->sbits.size() / img->sbits_words) : 0u;
+    if (sbits_words) *sbits_words = img->sbits_words;
+    return CG_OK;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 int cg_image_policy_atomic(const void* image, size_t len, uint32_t i, int* atomic) {
   if (!image || !atomic) return CG_E_ARG;
@@ -519,9 +614,10 @@ const char* cg_last_error(cg_ctx* ctx) { return ctx ? ctx->err.c_str() : dev_las
 int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg) {
   if (!ctx) return CG_E_ARG;
   switch (kind) {
-    case CG_FAULT_NONE: ctx->fault_errors = 0; ctx->fault_stall_us = 0; return CG_OK;
+    case CG_FAULT_NONE: ctx->fault_errors = 0; ctx->fault_stall_us = 0; ctx->fault_kidx = 0; return CG_OK;
     case CG_FAULT_DEVICE_ERROR: ctx->fault_errors = arg; return CG_OK;
     case CG_FAULT_STALL: ctx->fault_stall_us = std::min<uint64_t>(arg, 2000000u); return CG_OK;
+    case CG_FAULT_BAD_KIDX: ctx->fault_kidx = arg; return CG_OK;
     default: return CG_E_ARG;
   }
 }
@@ -660,25 +756,24 @@ int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len) {
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
   std::vector<std::pair<size_t, size_t>> elems;
   if (len >= 65536 && split_array(json, len, elems) && host_workers(elems.size()) > 1) {
-    // bulk: parse, convert and encode elements on worker threads; append in order. All or nothing.
-    std::vector<SarSlot> slots(elems.size());
+    // bulk: parse, convert and encode elements on worker threads into per-chunk parts (bulk_add)
     const Image& img = *b->host.img;
-    parallel_for(elems.size(), [&](size_t k) { sar_to_slot(img, json + elems[k].first, elems[k].second, slots[k]); });
-    for (auto& sl : slots)
-      if (sl.rc) { b->err = sl.err; return sl.rc; }
-    GUARD(b->err, {
-      for (auto& sl : slots) {
-        if (sl.fast >= 0) {
-          b->fast_reason[(uint32_t)b->items.size()] = std::move(sl.reason);
-          b->items.push_back({-1, sl.fast});
-          continue;
-        }
-        b->items.push_back({(int32_t)b->host.n(), -1});
-        b->host.append(sl.e);
-        sl.e = EncodedRequest();
-      }
-      return CG_OK;
-    })
+    return bulk_add(b, elems.size(), [&](size_t k, EncodedRequest& e, BulkOut& o) {
+      const char* p = json + elems[k].first;
+      const size_t m = elems[k].second;
+      const int d = encode_sar_direct(img, p, m, e, o.fast, o.reason);
+      if (d == 2) { o.host = true; return; }
+      if (d == 1) return;
+      JVal v = json_parse(p, m);
+      Attributes a = attributes_from_sar(v);
+      o.reason.clear();
+      o.fast = authorize_fast_path(a, o.reason);
+      if (o.fast >= 0) { o.host = true; return; }
+      std::vector<EntityIn> ents;
+      RequestIn req;
+      record_to_cedar(a, ents, req);
+      encode_request(img, ents, req, e);
+    });
   }
   GUARD(b->err, {
     JVal v = json_parse(json, len);
@@ -766,50 +861,65 @@ int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t 
   GUARD(err, { return encode_sar_check(image, len, sars, n, n_items, n_direct, n_mismatch, first_mismatch); })
 }
 
+int cg_encode_items_check(const void* image, size_t len, const char* items, size_t n, uint32_t* n_items,
+                          uint32_t* n_mismatch, int64_t* first_mismatch) {
+  if (!image || !items) return CG_E_ARG;
+  std::string err;
+  GUARD(err, {
+    auto img = Image::deserialize((const uint8_t*)image, len);
+    JVal v = json_parse(items, n);
+    if (v.t != JVal::Arr) throw CedarError("expected a JSON array");
+    uint32_t nm = 0;
+    int64_t first = -1;
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    for (size_t k = 0; k < v.arr.size(); k++) {
+      decode_json_item(v.arr[k], ents, req);
+      EncodedRequest a;
+      EncodedRequest w;
+      encode_request(*img, ents, req, a);  // ancestor records from the closure cache where it applies
+      enc::t_no_closure_cache = true;
+      try {
+        encode_request(*img, ents, req, w);  // the general walk
+      } catch (...) {
+        enc::t_no_closure_cache = false;
+        throw;
+      }
+      enc::t_no_closure_cache = false;
+      if (a.blk != w.blk || a.row != w.row || a.anc != w.anc || a.anc_at != w.anc_at || a.strs != w.strs || a.gkey != w.gkey) {
+        nm++;
+        if (first < 0) first = (int64_t)k;
+      }
+    }
+    if (n_items) *n_items = (uint32_t)v.arr.size();
+    if (n_mismatch) *n_mismatch = nm;
+    if (first_mismatch) *first_mismatch = first;
+    return CG_OK;
+  })
+}
+
 int cg_batch_add_admission_json(cg_batch* b, const char* json, size_t len) {
   if (!b || !json) return CG_E_ARG;
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
   std::vector<std::pair<size_t, size_t>> elems;
   if (len >= 65536 && split_array(json, len, elems) && host_workers(elems.size()) > 1) {
-    // bulk: parse, flatten and encode reviews on worker threads; append in order. All or nothing.
-    struct Slot {
-      int outcome = ADM_EVAL, rc = CG_OK;
-      std::string err;
-      EncodedRequest e;
-    };
-    std::vector<Slot> slots(elems.size());
+    // bulk: parse, flatten and encode reviews on worker threads into per-chunk parts (bulk_add)
     const Image& img = *b->host.img;
-    parallel_for(elems.size(), [&](size_t k) {
-      Slot& sl = slots[k];
-      try {
-        JVal v = json_parse(json + elems[k].first, elems[k].second);
-        const AdmissionRequest a = admission_request_from_json(v);
-        std::vector<EntityIn> ents;
-        RequestIn req;
-        sl.outcome = admission_to_cedar(a, ents, req, sl.err);
-        if (sl.outcome == ADM_EVAL) encode_request(img, ents, req, sl.e);
-      } catch (const CedarError& e) {
-        sl.err = e.what(); sl.rc = CG_E_PARSE;
-      } catch (const std::exception& e) {
-        sl.err = e.what(); sl.rc = CG_E_ARG;
+    return bulk_add(b, elems.size(), [&](size_t k, EncodedRequest& e, BulkOut& o) {
+      JVal v = json_parse(json + elems[k].first, elems[k].second);
+      const AdmissionRequest a = admission_request_from_json(v);
+      std::vector<EntityIn> ents;
+      RequestIn req;
+      std::string err;
+      const int outcome = admission_to_cedar(a, ents, req, err);
+      if (outcome != ADM_EVAL) {
+        o.host = true;
+        o.fast = outcome;
+        if (outcome == ADM_ERROR) o.reason = std::move(err);
+        return;
       }
+      encode_request(img, ents, req, e);
     });
-    for (auto& sl : slots)
-      if (sl.rc) { b->err = sl.err; return sl.rc; }
-    GUARD(b->err, {
-      for (auto& sl : slots) {
-        const uint32_t i = (uint32_t)b->items.size();
-        if (sl.outcome != ADM_EVAL) {
-          b->items.push_back({-1, sl.outcome});
-          if (sl.outcome == ADM_ERROR) b->fast_reason[i] = std::move(sl.err);
-          continue;
-        }
-        b->items.push_back({(int32_t)b->host.n(), -1});
-        b->host.append(sl.e);
-        sl.e = EncodedRequest();
-      }
-      return CG_OK;
-    })
   }
   GUARD(b->err, {
     JVal v = json_parse(json, len);
@@ -939,6 +1049,11 @@ int cg_batch_submit(cg_batch* b) {
       b->err = "injected device error (cg_ctx_inject_fault CG_FAULT_DEVICE_ERROR)";
       return CG_E_DEVICE;
     }
+  for (uint64_t f = b->ctx->fault_kidx.load(); f;)
+    if (b->ctx->fault_kidx.compare_exchange_weak(f, f - 1)) {
+      corrupt_key_indices(b->host);
+      break;
+    }
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   tr.mark("upload");
   if (const uint64_t us = b->ctx->fault_stall_us.load())
@@ -953,14 +1068,31 @@ int cg_batch_submit(cg_batch* b) {
 
 int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   if (!b) return CG_E_ARG;
+  const int64_t deadline = timeout_ns < 0 ? -1 : dev_now_ns() + timeout_ns;
+  return cg::batch_wait(b, deadline, deadline);
+}
+
+}  // extern "C"
+
+int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
   if (!b->submitted) { b->err = "batch not submitted"; return CG_E_STATE; }
   if (b->done) return CG_OK;
   if (b->failed) return b->failed;
-  const int64_t deadline = timeout_ns < 0 ? -1 : dev_now_ns() + timeout_ns;
   LatTrace tr("wait");
-  if (const int drc = dev_download_finish(b->dev, b->host, deadline)) {
-    b->err = dev_last_error();
-    return drc == DEV_TIMEOUT ? CG_E_TIMEOUT : CG_E_DEVICE;  // a timeout leaves the batch in flight
+  if (!b->downloaded) {
+    if (const int drc = dev_download_finish(b->dev, b->host, download_deadline)) {
+      b->err = dev_last_error();
+      return drc == DEV_TIMEOUT ? CG_E_TIMEOUT : CG_E_DEVICE;  // a timeout leaves the batch in flight
+    }
+    b->downloaded = true;
+    if (b->host.fu_cnt && b->host.fu_cnt[FU_KINDS]) {
+      // the scan found key-entity indices that are not the image's: the batch was encoded for
+      // another image (or corrupted), so none of its answers can be trusted; callers fail safe
+      b->err = std::to_string(b->host.fu_cnt[FU_KINDS]) +
+               " request(s) carry key-entity indices outside the image's: batch not encoded for this image";
+      b->failed = CG_E_DEVICE;
+      return CG_E_DEVICE;
+    }
   }
   tr.mark("sync_copy");
   // Overflowed result lists: re-run just those requests. Capacity overflows of the probe kernel
@@ -1161,6 +1293,8 @@ int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   return CG_OK;
 }
 
+extern "C" {
+
 int cg_batch_reruns(cg_batch* b, uint32_t* n) {
   if (!b || !n) return CG_E_ARG;
   if (!b->done) return CG_E_STATE;
@@ -1234,6 +1368,15 @@ int cg_batch_bytes(cg_batch* b, uint64_t* batch_bytes, uint64_t* image_bytes, ui
   if (batch_bytes) *batch_bytes = b->dev.bytes;
   if (image_bytes) *image_bytes = b->img->dev.bytes;
   if (heap_bytes) *heap_bytes = (uint64_t)b->host.heap.size() * 4;
+  return CG_OK;
+}
+
+int cg_batch_io(cg_batch* b, uint64_t* h2d_bytes, uint64_t* d2h_bytes, uint64_t* list_words, uint64_t* list_words_shared) {
+  if (!b) return CG_E_ARG;
+  if (h2d_bytes) *h2d_bytes = b->submitted ? b->dev.bytes - b->dev.out_bytes : 0;
+  if (d2h_bytes) *d2h_bytes = b->submitted ? b->dev.out_bytes : 0;
+  if (list_words) *list_words = b->host.anc_words;
+  if (list_words_shared) *list_words_shared = b->host.anc_shared_words;
   return CG_OK;
 }
 

@@ -48,6 +48,14 @@ struct CapHint {
 
 using cg::LoadedImage;
 
+struct cg_batch;
+namespace cg {
+// cg_batch_wait with separate deadlines (steady-clock ns, < 0 none) for the results' download and
+// for the host re-runs after it: the serving queue polls the download in short slices (so that
+// closing the queue over a hung device stays bounded) without giving a re-run only a slice's time.
+int batch_wait(cg_batch* b, int64_t download_deadline, int64_t rerun_deadline);
+}  // namespace cg
+
 struct cg_ctx {
   int device = 0;
   void* stream = nullptr;
@@ -62,7 +70,7 @@ struct cg_ctx {
   uint64_t next_serial = 1;  // under mu
   cg::CapHint hint;          // under mu
   // cg_ctx_inject_fault: submits left to fail, and the device stall before each batch (us)
-  std::atomic<uint64_t> fault_errors{0}, fault_stall_us{0};
+  std::atomic<uint64_t> fault_errors{0}, fault_stall_us{0}, fault_kidx{0};
 };
 
 struct cg_batch {
@@ -71,6 +79,7 @@ struct cg_batch {
   cg::Batch host;
   cg::DevBatch dev;
   bool submitted = false, done = false;
+  bool downloaded = false;  // the first pass's results (and follow-ups) are in the pinned block
   int failed = 0;        // a host re-run missed its deadline: every later wait returns this
   uint32_t n_rerun = 0;  // requests re-run by cg_batch_wait
   uint32_t n_fu[cg::FU_KINDS] = {0, 0, 0};  // requests finished by each on-device follow-up worklist

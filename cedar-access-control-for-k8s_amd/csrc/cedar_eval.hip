@@ -89,6 +89,8 @@ struct KArgs {
   const uint32_t* __restrict__ sctx;   // scope bitsets (image.h): context table, rows
   const uint32_t* __restrict__ sbits;
   uint32_t sctx_mask, sbits_words;     // sbits_words 0: the image has none
+  uint32_t n_kent;                     // key entities: a request's key-entity indices are below it
+  uint32_t* bad_kidx;                  // count of requests whose indices are not (null: not counted)
   uint32_t l2_vmask, l2_lmask;         // hot slots with level-2 value / list keys (entity-principal combos)
   uint32_t scan_big;    // more scanned buckets than this: straight to the large stage (CEDARGPU_SCAN_BIG)
   uint32_t scan_heavy;  // more candidate heads than this: straight to the large stage (CEDARGPU_SCAN_HEAVY)
@@ -369,28 +371,30 @@ __device__ __forceinline__ const uint32_t* ent_row(const Ctx& c, uint32_t idx) {
   return (idx & ENT_STATIC) ? c.srows + (size_t)(idx & ~ENT_STATIC) * ENT_WORDS : c.blk + RH_WORDS + idx * ENT_WORDS;
 }
 
-// exact membership in a heap ancestor list: pairs at blk[off + 2k], independent loads, 4 per step
+// exact membership in an ancestor list: pairs at blk[off + 2k] (off signed: a request's lists sit
+// ahead of its block, image.h "ancestor lists"), independent loads, 4 per step
 __device__ __forceinline__ bool anc_scan(const uint32_t* blk, uint32_t off, uint32_t n, uint32_t qt, uint32_t qi) {
+  const uint32_t* l = blk + (int32_t)off;
   bool f = false;
   uint32_t k = 0;
   for (; k + 4 <= n && !f; k += 4) {
-    const uint32_t* q = blk + off + 2 * k;
+    const uint32_t* q = l + 2 * k;
     const uint32_t t0 = q[0], i0 = q[1], t1 = q[2], i1 = q[3], t2 = q[4], i2 = q[5], t3 = q[6], i3 = q[7];
     f = (t0 == qt && i0 == qi) | (t1 == qt && i1 == qi) | (t2 == qt && i2 == qi) | (t3 == qt && i3 == qi);
   }
-  for (; k < n && !f; k++) f = blk[off + 2 * k] == qt && blk[off + 2 * k + 1] == qi;
+  for (; k < n && !f; k++) f = l[2 * k] == qt && l[2 * k + 1] == qi;
   return f;
 }
 
 // ancestor list of an entity: pairs at base[off + 2k] (a static entity's closure row lives in the
-// constant pool)
+// constant pool; a table entity's list in the heap, at a signed block-relative ref)
 __device__ __forceinline__ void anc_of(const Ctx& c, uint32_t idx, const uint32_t*& base, uint32_t& off, uint32_t& n) {
   base = c.blk; off = 0; n = 0;
   if (idx == NO_ENT) return;
-  if (idx & ENT_STATIC) base = c.cpool;
   const uint32_t ref = ent_row(c, idx)[ER_ANC] & OFF_MASK;
-  n = base[ref];
-  off = ref + 1;
+  const uint32_t* l = (idx & ENT_STATIC) ? c.cpool + ref : c.blk + sext26(ref);
+  n = l[0];
+  base = l + 1;
 }
 
 __device__ __forceinline__ bool anc_has(const Ctx& c, uint32_t idx, uint32_t qt, uint32_t qi) {
@@ -1546,7 +1550,8 @@ __device__ __forceinline__ uint2 key_comp(uint32_t kc, uint32_t j, uint32_t st, 
                                           uint32_t off) {
   if (kc == KC_WILD) return make_uint2(KW_ANY, KW_ANY);
   if (kc == KC_TYPE) return make_uint2(st, KW_ANY);
-  return j ? make_uint2(__builtin_nontemporal_load(blk + off + 2 * (j - 1)), __builtin_nontemporal_load(blk + off + 2 * (j - 1) + 1))
+  const uint32_t* l = blk + (int32_t)off;  // (signed: image.h "ancestor lists")
+  return j ? make_uint2(__builtin_nontemporal_load(l + 2 * (j - 1)), __builtin_nontemporal_load(l + 2 * (j - 1) + 1))
            : make_uint2(st, si);
 }
 
@@ -1696,6 +1701,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const bool kbits = BITS && a.scan_filt && a.sbits_words != 0;
   const bool klist = kbits && valid && p_anc != 0;
   const bool stl = a.scan_lds != 0;  // UIDs in LDS for the key loop
+  const uint32_t* pl = blk + (int32_t)p_anc;  // the principal's list (signed: image.h "ancestor lists")
   const uint32_t nk = (pn >> AN_KEYS_SHIFT) & AN_KEYS;
   constexpr uint32_t LW = 3;  // list elements loaded with a list head
   uint32_t l_lo = 0, l_hd = 0, l_w[LW] = {0, 0, 0};
@@ -1703,10 +1709,10 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     if (stl) {
       const uint32_t n_st = valid ? min(nk, ANC_ST) : 0u;
       for (uint32_t j = sl; j < n_st; j += SEG)
-        s_anc[seg][j] = make_uint2(__builtin_nontemporal_load(blk + p_anc + 2 * j), __builtin_nontemporal_load(blk + p_anc + 2 * j + 1));
+        s_anc[seg][j] = make_uint2(__builtin_nontemporal_load(pl + 2 * j), __builtin_nontemporal_load(pl + 2 * j + 1));
     }
     if (BITS && klist) {
-      const uint32_t* kl = blk + p_anc + 2 * (pn & AN_COUNT);
+      const uint32_t* kl = pl + 2 * (pn & AN_COUNT);
       for (uint32_t j = sl; j <= min(nk, SCAN_ANC); j += SEG) s_kid[seg][j] = __builtin_nontemporal_load(kl + j);
     }
     // BITS: lane k < popc(l2_lmask) reads the k-th list slot's head and first LW words after it
@@ -1845,12 +1851,15 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     // (found context, key ancestor) pairs: ip 0 .. nP - 1 under each; a set bit lists the key. All
     // SCAN_PB loads of a lane's round in flight at once.
     const uint32_t self = pn >> 31, tot = on ? nf * nP : 0u;
-    const uint32_t* kl = blk + p_anc + 2 * (pn & AN_COUNT);
+    const uint32_t* kl = pl + 2 * (pn & AN_COUNT);
     // t / nP by a multiply: exact while t * nP < 2^32 (t < CTX_CAP * nP, nP < 2048); nP == 1
     // (whose reciprocal does not fit 32 bits) divides by itself (checked for every nP < 2048 on the
     // host)
     const uint32_t inv = nP > 1 ? 0xFFFFFFFFu / nP + 1u : 0u;
     auto divp = [&](uint32_t t) { return nP > 1 ? __umulhi(t, inv) : t; };
+    // a key-entity index past the image's key entities (a batch encoded for another image): the
+    // request enumerates every key instead (exact), and is counted so that the batch fails
+    bool badk = false;
     for (uint32_t rb = 0; __ballot(rb < tot) != 0; rb += SEG * SCAN_PB) {
       uint32_t fw[SCAN_PB], fk[SCAN_PB];
 #pragma unroll
@@ -1863,7 +1872,8 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
           const uint32_t kid = jk <= SCAN_ANC ? s_kid[seg][jk] : kl[jk];
           fk[u] = kid;
-          if (kid != KIDX_NONE && (kid >> 5) < a.sbits_words) fw[u] = a.sbits[(size_t)s_cx[seg][j].w * a.sbits_words + (kid >> 5)];
+          if (kid < a.n_kent) fw[u] = a.sbits[(size_t)s_cx[seg][j].w * a.sbits_words + (kid >> 5)];
+          else badk = badk || kid != KIDX_NONE;
         }
       }
 #pragma unroll
@@ -1878,6 +1888,10 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         }
         npos += popc64(mk);
       }
+    }
+    if (sballot(badk) != 0) {
+      if (on && sl == 0 && a.bad_kidx) atomicAdd(a.bad_kidx, 1u);
+      on = false;
     }
     // the other combos' single keys
     for (uint32_t m = cm & ~COMBO_PENT; m; m &= m - 1) {
@@ -2733,6 +2747,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS);
   d.sctx_mask = (uint32_t)(img.sctx.size() / (2 + SCTX_WORDS)) - 1;
   d.sbits_words = img.sbits_words;
+  d.n_kent = (uint32_t)img.key_ents.size();
   d.l2_vmask = img.l2_vmask;
   d.l2_lmask = img.l2_lmask;
   d.gstr_bytes = at(DS_GSTR_BYTES);
@@ -2976,7 +2991,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024))};
   size_t o_fu = o_er + al(n * d.cape * ERR_WORDS * 4);
   const size_t o_cnt = o_fu;
-  o_fu += al(FU_KINDS * 4);
+  o_fu += al((FU_KINDS + 1) * 4);
   size_t o_k[FU_KINDS][5];
   for (uint32_t k = 0; k < FU_KINDS; k++) {
     auto& f = d.fu[k];
@@ -3257,6 +3272,8 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.sctx = img.sctx; k.sbits = img.sbits; k.sctx_mask = img.sctx_mask; k.sbits_words = img.sbits_words;
+  k.n_kent = img.n_kent;
+  k.bad_kidx = b.fu_cnt ? b.fu_cnt + FU_KINDS : nullptr;
   k.l2_vmask = img.l2_vmask; k.l2_lmask = img.l2_lmask;
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
@@ -3545,6 +3562,8 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
     k.grows = b.grows;
   }
   mark(PH_GROUP, s);
+  // the worklist counters and the scan's bad-index count start at zero before the first pass
+  if (b.fu_cnt) HIPCHK(hipMemsetAsync(b.fu_cnt, 0, (FU_KINDS + 1) * 4, s), "memset worklists");
   const bool two = img.indexed && split_on() && !probe_stats() && probe_seg() == 8 && probe_occ() == 3;
   launch_eval(img, k, b.n, s);
   HIPCHK(hipGetLastError(), "launch");
@@ -3554,7 +3573,6 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
     for (uint32_t p = PH_GATHER; p < STEP_PHASES; p++) mark(p, s);
     return 0;
   }
-  HIPCHK(hipMemsetAsync(b.fu_cnt, 0, FU_KINDS * 4, s), "memset worklists");
   FuLists wl;
   for (uint32_t q = 0; q < FU_KINDS; q++) { wl.ids[q] = b.fu[q].ids; wl.cap[q] = b.fu[q].cap; }
   hipLaunchKernelGGL(cedar_fu_gather, dim3((b.n + GATHER_ITEMS * 256 - 1) / (GATHER_ITEMS * 256)), dim3(256), 0, s, b.res,
@@ -3638,8 +3656,9 @@ int64_t dev_now_ns() {
   return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Waits for `ev` until deadline_ns (< 0: none): spins with yields for the first ~50 us (results
-// of a latency-bound batch arrive within that), then sleeps 10 us between queries.
+// Waits for `ev` until deadline_ns (< 0: none): spins with yields for the first ~500 us (results
+// of a latency-bound batch arrive within that: the serving queue's submitter polls every batch in
+// 10 ms slices), then sleeps 10 us between queries.
 static int wait_event(hipEvent_t ev, int64_t deadline_ns, const char* what) {
   if (deadline_ns < 0) {
     HIPCHK(hipEventSynchronize(ev), what);
@@ -3655,7 +3674,7 @@ static int wait_event(hipEvent_t ev, int64_t deadline_ns, const char* what) {
       g_err = std::string(what) + ": deadline exceeded";
       return DEV_TIMEOUT;
     }
-    if (now - t0 < 50000) std::this_thread::yield();
+    if (now - t0 < 500000) std::this_thread::yield();
     else std::this_thread::sleep_for(std::chrono::microseconds(10));
   }
 }
@@ -3769,47 +3788,63 @@ int dev_stall(int device, void* stream, uint64_t us) {
 int dev_time_split(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_phase, float* ms_total) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
-  std::vector<hipEvent_t> ev((size_t)iters * (STEP_PHASES + 1));
-  for (auto& e : ev) HIPCHK(hipEventCreate(&e), "event");
-  int rc = 0;
-  for (uint32_t i = 0; i < iters && !rc; i++) {
-    t_marks = &ev[(size_t)i * (STEP_PHASES + 1)];
-    (void)hipEventRecord(t_marks[0], s);
-    rc = enqueue_step(img, b, s);
-    t_marks = nullptr;
+  // every event created is destroyed on every path (and the step's marks never outlive them)
+  struct Events {
+    std::vector<hipEvent_t> v;
+    ~Events() {
+      t_marks = nullptr;
+      for (auto e : v) (void)hipEventDestroy(e);
+    }
+  } ev;
+  ev.v.reserve((size_t)iters * (STEP_PHASES + 1));
+  for (size_t i = 0; i < (size_t)iters * (STEP_PHASES + 1); i++) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e), "event");
+    ev.v.push_back(e);
   }
-  if (!rc) HIPCHK(hipEventSynchronize(ev.back()), "event sync");
+  for (uint32_t i = 0; i < iters; i++) {
+    t_marks = &ev.v[(size_t)i * (STEP_PHASES + 1)];
+    HIPCHK(hipEventRecord(t_marks[0], s), "event record");
+    const int rc = enqueue_step(img, b, s);
+    t_marks = nullptr;
+    if (rc) return rc;
+  }
+  HIPCHK(hipEventSynchronize(ev.v.back()), "event sync");
   for (uint32_t p = 0; p < STEP_PHASES; p++) ms_phase[p] = 0.f;
   *ms_total = 0.f;
-  for (uint32_t i = 0; i < iters && !rc; i++) {
-    const hipEvent_t* m = &ev[(size_t)i * (STEP_PHASES + 1)];
+  // enqueue_step marks every phase of every step (an empty phase is two adjacent marks): a phase
+  // without its events is an error, not a zero
+  for (uint32_t i = 0; i < iters; i++) {
+    const hipEvent_t* m = &ev.v[(size_t)i * (STEP_PHASES + 1)];
     for (uint32_t p = 0; p < STEP_PHASES; p++) {
       float t = 0.f;
-      if (hipEventElapsedTime(&t, m[p], m[p + 1]) == hipSuccess) ms_phase[p] += t;
+      HIPCHK(hipEventElapsedTime(&t, m[p], m[p + 1]), "phase elapsed time");
+      ms_phase[p] += t;
     }
     float t = 0.f;
-    if (hipEventElapsedTime(&t, m[0], m[STEP_PHASES]) == hipSuccess) *ms_total += t;
+    HIPCHK(hipEventElapsedTime(&t, m[0], m[STEP_PHASES]), "step elapsed time");
+    *ms_total += t;
   }
-  for (auto& e : ev) (void)hipEventDestroy(e);
-  return rc;
+  return 0;
 }
 
 int dev_time_eval(const DevImage& img, DevBatch& b, uint32_t iters, void* stream, float* ms_total) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0), "event");
-  HIPCHK(hipEventCreate(&e1), "event");
-  HIPCHK(hipEventRecord(e0, s), "event record");
+  struct Ev {
+    hipEvent_t e = nullptr;
+    ~Ev() { if (e) (void)hipEventDestroy(e); }
+  } e0, e1;
+  HIPCHK(hipEventCreate(&e0.e), "event");
+  HIPCHK(hipEventCreate(&e1.e), "event");
+  HIPCHK(hipEventRecord(e0.e, s), "event record");
   for (uint32_t i = 0; i < iters; i++) {
     const int rc = enqueue_step(img, b, s);
     if (rc) return rc;
   }
-  HIPCHK(hipEventRecord(e1, s), "event record");
-  HIPCHK(hipEventSynchronize(e1), "event sync");
-  HIPCHK(hipEventElapsedTime(ms_total, e0, e1), "elapsed");
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  HIPCHK(hipEventRecord(e1.e, s), "event record");
+  HIPCHK(hipEventSynchronize(e1.e), "event sync");
+  HIPCHK(hipEventElapsedTime(ms_total, e0.e, e1.e), "elapsed");
   return 0;
 }
 

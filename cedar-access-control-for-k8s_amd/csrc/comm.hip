@@ -51,6 +51,15 @@ static bool comm_wait(cg_comm* c, int64_t timeout_ms, std::string& why) {
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
+// An RCCL call that fails at enqueue may leave the communicator in an error state: abort it as a
+// failed wait does, so that a later call reports CG_E_STATE at once instead of blocking in a
+// collective until the timeout.
+static void comm_abort(cg_comm* c) {
+  if (c->aborted) return;
+  if (c->nccl) (void)ncclCommAbort(c->nccl);
+  c->nccl = nullptr;
+  c->aborted = true;
+}
 static int64_t comm_timeout_ms() {
   static const int64_t t = [] { const char* e = std::getenv("CEDARGPU_COMM_TIMEOUT_MS"); return e ? (int64_t)std::atoll(e) : 60000; }();
   return t;
@@ -126,6 +135,7 @@ int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, siz
             (r = ncclBroadcast(dn, dn, 8, ncclUint8, root, c->nccl, c->stream)) == ncclSuccess &&
             comm_wait(c, comm_timeout_ms(), why) && hipMemcpy(&n, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
   if (!ok) {
+    if (r != ncclSuccess) comm_abort(c);
     (void)hipFree(dn);
     return fail(std::string("length broadcast: ") + (why.empty() ? ncclGetErrorString(r) : why.c_str()));
   }
@@ -144,6 +154,7 @@ int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, siz
        (r = ncclAllReduce(dn, dn, 1, ncclUint64, ncclMin, c->nccl, c->stream)) == ncclSuccess &&
        comm_wait(c, comm_timeout_ms(), why) && hipMemcpy(&ready, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
   (void)hipFree(dn);
+  if (r != ncclSuccess) comm_abort(c);
   if (!ok || !ready) {
     if (buf) (void)hipFree(buf);
     return fail(!ok ? std::string("readiness all-reduce: ") + (why.empty() ? ncclGetErrorString(r) : why.c_str())
@@ -152,7 +163,7 @@ int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, siz
   // a failure from here on (RCCL error, dead peer, timeout) aborts this rank's communicator
   r = ncclBroadcast(buf, buf, (size_t)n, ncclUint8, root, c->nccl, c->stream);
   if (r != ncclSuccess || !comm_wait(c, comm_timeout_ms(), why)) {
-    if (r != ncclSuccess && !c->aborted) { (void)ncclCommAbort(c->nccl); c->nccl = nullptr; c->aborted = true; }
+    if (r != ncclSuccess) comm_abort(c);
     (void)hipFree(buf);
     return fail(std::string("image broadcast: ") + (why.empty() ? ncclGetErrorString(r) : why.c_str()));
   }

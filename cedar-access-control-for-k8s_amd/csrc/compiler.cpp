@@ -1696,6 +1696,10 @@ static std::shared_ptr<Image> compile_incremental(LowerState& S, const std::vect
   img->act = A.act;
   img->hot = A.hot;
   img->amask_ok = A.amask_ok;
+  // every slot a contains / containsAny atom of the arenas reads (Compiler::atom sets it while
+  // lowering; removed documents' slots linger, which only costs their rows a list): the scope index
+  // then never files prefix keys on them, as a fresh build would not
+  img->cslot_mask = A.cslot_mask;
   std::vector<Compiler::AttrKey> akeys;
   size_t total = 0;
   for (auto& tp : parsed) total += tp.size();
@@ -1849,6 +1853,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     Image& A = S.arena;
     A.strings = img->strings; A.sid = img->sid; A.code = img->code; A.cpool = img->cpool;
     A.ext_msgs = img->ext_msgs; A.act = img->act; A.hot = img->hot; A.amask_ok = img->amask_ok;
+    A.cslot_mask = img->cslot_mask;
     S.C.hot = C.hot; S.C.hot_depth = C.hot_depth; S.C.act_index = C.act_index;
     S.gen++;
     std::vector<uint32_t> kept(docs.size(), 0);
@@ -2118,6 +2123,8 @@ uint32_t request_sid(const Image& img, EncodedRequest& e, std::string_view s) {
 }
 
 void Image::build_lookup() {
+  static std::atomic<uint64_t> next_id{0};
+  cache_id = ++next_id;  // the encoder's per-thread closure caches key on it (encode_impl.h)
   size_t cap = 16;
   while (cap < 2 * strings.size() + 16) cap <<= 1;
   lookup.assign(cap, 0);

@@ -21,6 +21,7 @@ struct DevImage {
   uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
   uint32_t *sctx = nullptr, *sbits = nullptr;                        // scope bitsets
   uint32_t sctx_mask = 0, sbits_words = 0, l2_vmask = 0, l2_lmask = 0;
+  uint32_t n_kent = 0;  // key entities (Image::key_ents): valid key-entity indices are below it
   uint8_t* gstr_bytes = nullptr;
   // the one device allocation holding the image's device region (image.h DevSection); the arrays
   // above point into it at (blob offset - origin)
@@ -55,7 +56,9 @@ struct DevBatch {
   //   FU_GEN  structural comparisons (RF_GENERAL) or any overflow of a non-indexed image: the
   //           policy-stream kernel
   // fu_cnt[k] = requests the gather found for worklist k (device-side; entries past fu[k].cap are
-  // left to the host re-run). fu[k].cap == 0: worklist k off.
+  // left to the host re-run). fu[k].cap == 0: worklist k off. fu_cnt[FU_KINDS]: requests whose
+  // key-entity indices fall outside the image's (BAD_KIDX: encoded for another image; the scan
+  // enumerates their keys instead and the batch fails with CG_E_DEVICE).
   uint32_t* fu_cnt = nullptr;
   struct FollowUp {
     uint32_t *ids = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;

@@ -121,7 +121,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   for (uint8_t x : b.bstr_bytes) h = h * 31 + x;
   g_sink += h;
   const size_t n = std::max<uint32_t>(d.n, 1);
-  const size_t words = n * 2 + 2 * n * d.capr + n * d.cape * ERR_WORDS + FU_KINDS;
+  const size_t words = n * 2 + 2 * n * d.capr + n * d.cape * ERR_WORDS + FU_KINDS + 1;
   d.out_bytes = words * 4;
   d.out_blk = std::calloc(words, 4);
   if (!d.out_blk) { g_err = "out of memory"; return -5; }

@@ -10,6 +10,7 @@
 //     (emit the context / entity attributes record into `out` exactly as emit_heap_value does)
 #pragma once
 #include <algorithm>
+#include <cstdlib>
 #include <string_view>
 #include <unordered_map>
 #include <unordered_set>
@@ -126,6 +127,57 @@ struct UidIndex {
   }
 };
 
+// An ancestor-list record (EncodedRequest::anc) of `owner` over the ancestor set `anc` (any order,
+// no repeats): [n, (type, id) x n] in order_ancestors order, then on a scope-bitset image the key-
+// entity index of the owner and of each leading key ancestor. Returns the key-ancestor count.
+inline uint32_t make_record(const Image& img, uint64_t owner, std::vector<uint64_t>& anc, std::vector<uint32_t>& out) {
+  const uint32_t keys = order_ancestors(img, anc);
+  out.push_back((uint32_t)anc.size());
+  for (const uint64_t a : anc) { out.push_back((uint32_t)(a >> 32)); out.push_back((uint32_t)a); }
+  if (img.sbits_words) {
+    out.push_back(img.key_index(owner));
+    for (uint32_t j = 0; j < keys; j++) out.push_back(img.key_index(anc[j]));
+  }
+  return keys;
+}
+
+// Per-thread cache of ancestor-list records for the common request shape (a SubjectAccessReview's
+// user with its groups, over a static group hierarchy): a table entity without request-given
+// parents has its static closure row as ancestry (or none), and an entity whose request-given
+// parents have none of their own has the union of its parents' closures. Both are pure functions of
+// the image and, for the latter, of (entity, merged parent list), so a thread computes each once
+// per image instead of walking the hierarchy for every request.
+struct ClosureCache {
+  uint64_t img_id = 0;
+  std::vector<std::vector<uint32_t>> srec;  // static row -> record (empty: not built yet)
+  std::vector<uint32_t> skeys;
+  struct Ent {
+    uint64_t uid = 0;
+    std::vector<uint64_t> parents;
+    std::vector<uint32_t> rec;
+    uint32_t keys = 0;
+  };
+  std::unordered_map<uint64_t, Ent> ents;  // by hash of (uid, parents)
+  static constexpr size_t MAX_ENTS = 1u << 16;
+  void bind(const Image& img) {
+    if (img_id == img.cache_id && img_id) return;
+    img_id = img.cache_id;
+    srec.assign(img.n_static(), {});
+    skeys.assign(img.n_static(), 0);
+    ents.clear();
+  }
+};
+inline ClosureCache& closure_cache() {
+  thread_local ClosureCache c;
+  return c;
+}
+// set on a thread to encode with the general walk only (cg_encode_sar_check compares the two)
+inline thread_local bool t_no_closure_cache = false;
+inline bool closure_cache_on() {
+  static const bool on = !(std::getenv("CEDARGPU_CLOSURE_CACHE") && *std::getenv("CEDARGPU_CLOSURE_CACHE") == '0');
+  return on;
+}
+
 inline void emit_empty_record(std::vector<uint32_t>& out, uint32_t& w0, uint32_t& w1) {
   const uint32_t off = (uint32_t)out.size();
   out.push_back(0);
@@ -241,12 +293,89 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   std::vector<uint64_t> anc, nodes, cl;
   std::vector<uint32_t> n_key(n, 0);
   std::unordered_set<uint64_t> seen_big;
-  // image with scope bitsets: after an ancestor list's pairs, the key-entity index of its owner and
-  // of each of its `keys` leading (key-entity) ancestors (image.h "scope bitsets")
-  auto push_kidx = [&](uint64_t owner, uint32_t keys) {
-    if (!img.sbits_words) return;
-    blk.push_back(img.key_index(owner));
-    for (uint32_t j = 0; j < keys; j++) blk.push_back(img.key_index(anc[j]));
+  // one ancestor-list record (EncodedRequest::anc): the pairs of `anc` and, on an image with scope
+  // bitsets, the key-entity index of its owner and of each of its `keys` leading (key-entity)
+  // ancestors (image.h "scope bitsets"); returns the record's index
+  std::vector<uint32_t>& al = E.anc;
+  auto put_list = [&](uint64_t owner, uint32_t keys) {
+    E.anc_at.push_back((uint32_t)al.size());
+    al.push_back((uint32_t)anc.size());
+    for (const uint64_t a : anc) { al.push_back((uint32_t)(a >> 32)); al.push_back((uint32_t)a); }
+    if (img.sbits_words) {
+      al.push_back(img.key_index(owner));
+      for (uint32_t j = 0; j < keys; j++) al.push_back(img.key_index(anc[j]));
+    }
+    return (uint32_t)E.anc_at.size() - 1;
+  };
+  auto put_words = [&](const std::vector<uint32_t>& w) {
+    E.anc_at.push_back((uint32_t)al.size());
+    al.insert(al.end(), w.begin(), w.end());
+    return (uint32_t)E.anc_at.size() - 1;
+  };
+  // The closure cache (ClosureCache) applies when no table entity with request-given parents is the
+  // target of a static edge: then no static path leads back into the request's own edges.
+  bool shortcut = closure_cache_on() && !t_no_closure_cache;
+  for (uint32_t i = 0; i < n && shortcut; i++)
+    if (table[i] & FROM_STATIC) shortcut = false;
+    else if (has_static && src.n_parents(table[i]) && img.is_static_target(index.keys[i])) shortcut = false;
+  ClosureCache* cc = nullptr;
+  if (shortcut) {
+    cc = &closure_cache();
+    cc->bind(img);
+  }
+  auto req_parents = [&](uint32_t i) { return !(table[i] & FROM_STATIC) && src.n_parents(table[i]) > 0; };
+  // the record of table entity i from the cache; false: the general walk below
+  auto cached = [&](uint32_t i) -> bool {
+    const uint64_t uid = index.keys[i];
+    if (!req_parents(i)) {
+      const int32_t s = has_static ? img.static_row(uid) : -1;
+      if (s < 0) {  // no parents anywhere
+        anc.clear();
+        n_key[i] = 0;
+        blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_list(uid, 0);
+        return true;
+      }
+      std::vector<uint32_t>& r = cc->srec[(size_t)s];
+      if (r.empty()) {
+        anc.clear();
+        cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_ANC] & OFF_MASK, anc);
+        std::sort(anc.begin(), anc.end());
+        anc.erase(std::unique(anc.begin(), anc.end()), anc.end());
+        cc->skeys[(size_t)s] = make_record(img, uid, anc, r);
+      }
+      n_key[i] = cc->skeys[(size_t)s];
+      blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(r);
+      return true;
+    }
+    const std::vector<uint64_t>& ps = parents[i];
+    uint64_t h = uid * 0x9E3779B97F4A7C15ull;
+    for (const uint64_t p : ps) {
+      const int32_t at = index.find(p);
+      if (at >= 0 && req_parents((uint32_t)at)) return false;  // a request edge above a request edge
+      h = (h ^ p) * 0xBF58476D1CE4E5B9ull;
+      h ^= h >> 31;
+    }
+    auto it = cc->ents.find(h);
+    if (it == cc->ents.end() || it->second.uid != uid || it->second.parents != ps) {
+      anc.clear();
+      for (const uint64_t p : ps) {
+        anc.push_back(p);
+        const int32_t s = has_static ? img.static_row(p) : -1;
+        if (s >= 0) cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_ANC] & OFF_MASK, anc);
+      }
+      std::sort(anc.begin(), anc.end());
+      anc.erase(std::unique(anc.begin(), anc.end()), anc.end());
+      if (cc->ents.size() >= ClosureCache::MAX_ENTS) cc->ents.clear();
+      ClosureCache::Ent& e = cc->ents[h];
+      e.uid = uid;
+      e.parents = ps;
+      e.rec.clear();
+      e.keys = make_record(img, uid, anc, e.rec);
+      it = cc->ents.find(h);
+    }
+    n_key[i] = it->second.keys;
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(it->second.rec);
+    return true;
   };
   for (uint32_t i = 0; i < n; i++) {
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_TYPE] = (uint32_t)(index.keys[i] >> 32);
@@ -260,6 +389,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     }
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ATTR0] = w0;
     blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ATTR1] = w1;
+    if (shortcut && cached(i)) continue;
     // transitive ancestors (through the merged map; cycles tolerated)
     anc.clear();
     seen_big.clear();
@@ -292,11 +422,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       }
     }
     n_key[i] = order_ancestors(img, anc);
-    const uint32_t off = (uint32_t)blk.size();
-    blk.push_back((uint32_t)anc.size());
-    for (const uint64_t a : anc) { blk.push_back((uint32_t)(a >> 32)); blk.push_back((uint32_t)a); }
-    push_kidx(index.keys[i], n_key[i]);
-    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = mk_ref(SP_HEAP, off);
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_list(index.keys[i], n_key[i]);  // a record index until appended
   }
   // ---- columnar row: UIDs, ancestor lists, hot paths resolved as attribute access would ----
   E.row.assign(img.row_words(), 0);
@@ -304,23 +430,21 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   row[RW_P] = pu.first; row[RW_P + 1] = pu.second;
   row[RW_A] = au.first; row[RW_A + 1] = au.second;
   row[RW_R] = ru.first; row[RW_R + 1] = ru.second;
-  // ancestor lists of P / A / R (a static entity outside the table: its closure row, copied into
-  // the block so the probe kernel reads every list block-relative), with the key counts
+  // ancestor lists of P / A / R (a static entity outside the table: its closure row as a record of
+  // its own, so the probe kernel reads every list the same way), with the key counts; the row names
+  // record k as k + 1 until appended
   auto anc_into = [&](uint32_t idx, const std::pair<uint32_t, uint32_t>& self, uint32_t w_off, uint32_t w_n) {
     uint32_t cnt = 0, keys = 0;
     if (idx != NO_ENT && (idx & ENT_STATIC)) {
       anc.clear();
       cpool_uids(img, img.srows[(size_t)(idx & ~ENT_STATIC) * ENT_WORDS + ER_ANC] & OFF_MASK, anc);
       keys = order_ancestors(img, anc);
-      row[w_off] = (uint32_t)blk.size() + 1;
-      blk.push_back((uint32_t)anc.size());
-      for (const uint64_t a : anc) { blk.push_back((uint32_t)(a >> 32)); blk.push_back((uint32_t)a); }
-      push_kidx(uid_key(self.first, self.second), keys);
+      row[w_off] = put_list(uid_key(self.first, self.second), keys) + 1;
       cnt = (uint32_t)anc.size();
     } else if (idx != NO_ENT) {
-      const uint32_t ref = blk[RH_WORDS + idx * ENT_WORDS + ER_ANC] & OFF_MASK;
-      row[w_off] = ref + 1;
-      cnt = blk[ref];
+      const uint32_t rec = blk[RH_WORDS + idx * ENT_WORDS + ER_ANC];
+      row[w_off] = rec + 1;
+      cnt = E.anc_rec(rec)[0];
       keys = n_key[idx];
     }
     if (cnt > AN_COUNT || keys > AN_KEYS) throw CedarError("entity has too many ancestors for the device row format");
@@ -334,12 +458,13 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   if (img.amask_ok) {
     uint64_t am = 0;
     const uint32_t n_act = (uint32_t)img.act.size() / 2;
-    const uint32_t aoff = row[RW_AANC], an = row[RW_AN] & AN_COUNT;
+    const uint32_t an = row[RW_AN] & AN_COUNT;
+    const uint32_t* al_ = an ? E.anc_pairs(row[RW_AANC]) : nullptr;
     for (uint32_t k = 0; k < n_act; k++) {
       const uint32_t qt = img.act[2 * k], qi = img.act[2 * k + 1];
       const bool self = au.first == qt && au.second == qi;
       bool hit = self;
-      for (uint32_t j = 0; j < an && !hit; j++) hit = blk[aoff + 2 * j] == qt && blk[aoff + 2 * j + 1] == qi;
+      for (uint32_t j = 0; j < an && !hit; j++) hit = al_[2 * j] == qt && al_[2 * j + 1] == qi;
       if (hit) am |= 1ull << k;
       if (self) row[RW_ASELF] = k;
     }
@@ -428,7 +553,8 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     const uint32_t ar = mix(mix(0x51ED27Fu, row[RW_A + 1]), row[RW_R]);
     uint32_t g = mix(0x3C6EF372u, row[RW_P]);
     const uint32_t nk = std::min<uint32_t>((row[RW_PN] >> AN_KEYS_SHIFT) & AN_KEYS, 32u);
-    for (uint32_t j = 0; j < nk; j++) g += mix(mix(0x2545F491u, blk[row[RW_PANC] + 2 * j]), blk[row[RW_PANC] + 2 * j + 1]);
+    const uint32_t* pl = nk ? E.anc_pairs(row[RW_PANC]) : nullptr;
+    for (uint32_t j = 0; j < nk; j++) g += mix(mix(0x2545F491u, pl[2 * j]), pl[2 * j + 1]);
     g = mix(g, 0x7FEB352Du);
     uint32_t hv = 0x6C8E9CF5u;
     for (uint32_t j = 0; j < 2 * nh; j++) hv = mix(hv, row[RW_HDR + j]);

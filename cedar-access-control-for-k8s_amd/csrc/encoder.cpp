@@ -9,6 +9,8 @@
 // encodes a request (encode_request) and the batch appends it with copies (Batch::append). Each entity row carries a pointer to its
 // transitive ancestor list (the closure of `parents` through the map), so `in` is a linear scan.
 #include <algorithm>
+#include <atomic>
+#include <thread>
 
 #include "encode_impl.h"
 
@@ -63,16 +65,38 @@ void encode_request(const Image& img, const std::vector<EntityIn>& ents, const R
 void Batch::append(EncodedRequest& e) {
   if (!row_words) row_words = img->row_words();
   if (e.row.size() != row_words || e.blk.size() < RH_WORDS) throw CedarError("request encoded for another image");
-  if (heap.size() + e.blk.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
+  if (heap.size() + e.blk.size() + e.anc.size() > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
   // (the probe kernel addresses a row's words by a 32-bit offset, PCtx::rowo)
   if (rows.size() + row_words > 0xFFFFFFFFull) throw CedarError("batch rows exceed 16 GiB");
   size_t sbytes = 0;
   for (auto& s : e.strs) sbytes += s.size();
   if (n_bstr() + e.strs.size() >= 0xFFFFFFFFull || bstr_bytes.size() + sbytes > 0xFFFFFFFFull)
     throw CedarError("batch string table overflow");
+  // ancestor-list records: interned ahead of the block, which points back at them
+  const uint32_t n_rec = (uint32_t)e.anc_at.size();
+  uint32_t at_small[16];
+  std::vector<uint32_t> at_big;
+  uint32_t* at = n_rec <= 16 ? at_small : (at_big.resize(n_rec), at_big.data());
+  const uint64_t room = (uint64_t)e.anc.size() + 16;  // the block starts at most this far past a new record
+  for (uint32_t k = 0; k < n_rec; k++) {
+    const uint32_t s = e.anc_at[k], t = k + 1 < n_rec ? e.anc_at[k + 1] : (uint32_t)e.anc.size();
+    at[k] = intern_list(e.anc.data() + s, t - s, room);
+  }
+  const uint32_t B = (uint32_t)heap.size();
+  const uint32_t nent = e.blk[RH_NENT];
+  for (uint32_t i = 0; i < nent; i++) {
+    uint32_t& w = e.blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC];
+    if (w >= n_rec) throw CedarError("request encoded without its ancestor lists");
+    w = mk_ref(SP_HEAP, (at[w] - B) & OFF_MASK);
+  }
+  for (const uint32_t f : {RW_PANC, RW_RANC, RW_AANC}) {
+    uint32_t& w = e.row[f];
+    if (w > n_rec) throw CedarError("request encoded without its ancestor lists");
+    if (w) w = at[w - 1] - B + 1;  // (mod 2^32: negative)
+  }
   e.blk[RH_SBASE] = n_bstr();
-  e.row[RW_BLK] = (uint32_t)heap.size();
-  req_base.push_back((uint32_t)heap.size());
+  e.row[RW_BLK] = B;
+  req_base.push_back(B);
   heap.insert(heap.end(), e.blk.begin(), e.blk.end());
   rows.insert(rows.end(), e.row.begin(), e.row.end());
   gkeys.push_back(e.gkey);
@@ -80,6 +104,82 @@ void Batch::append(EncodedRequest& e) {
     bstr_bytes.insert(bstr_bytes.end(), s.begin(), s.end());
     bstr_off.push_back((uint32_t)bstr_bytes.size());
   }
+}
+
+// One ancestor-list record into the heap, or the copy an earlier block appended (equal words,
+// close enough that a block starting `room` words past the heap end still reaches it).
+uint32_t Batch::intern_list(const uint32_t* w, uint32_t n, uint64_t room) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+  for (uint32_t k = 0; k < n; k++) {
+    h = (h ^ w[k]) * 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+  }
+  anc_words += n;
+  auto it = anc_memo.find(h);
+  if (it != anc_memo.end()) {
+    const uint32_t o = it->second;
+    if (heap.size() + room - o <= ANC_REACH && std::equal(w, w + n, heap.begin() + o)) {
+      anc_shared_words += n;
+      return o;
+    }
+  }
+  if (heap.size() + n > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
+  const uint32_t o = (uint32_t)heap.size();
+  heap.insert(heap.end(), w, w + n);
+  anc_memo[h] = o;
+  return o;
+}
+
+void Batch::concat(std::vector<Batch>& parts, unsigned threads) {
+  if (!row_words) row_words = img->row_words();
+  const size_t np = parts.size();
+  std::vector<size_t> ho(np), ro(np), so(np), bo(np);
+  size_t H = heap.size(), R = req_base.size(), S = n_bstr(), SB = bstr_bytes.size();
+  for (size_t k = 0; k < np; k++) {
+    const Batch& p = parts[k];
+    if (p.n() && p.row_words != row_words) throw CedarError("request encoded for another image");
+    ho[k] = H; ro[k] = R; so[k] = S; bo[k] = SB;
+    H += p.heap.size(); R += p.n(); S += p.n_bstr(); SB += p.bstr_bytes.size();
+    anc_words += p.anc_words;
+    anc_shared_words += p.anc_shared_words;
+  }
+  if (H > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
+  if (R * row_words > 0xFFFFFFFFull) throw CedarError("batch rows exceed 16 GiB");
+  if (S >= 0xFFFFFFFFull || SB > 0xFFFFFFFFull) throw CedarError("batch string table overflow");
+  heap.resize(H);
+  req_base.resize(R);
+  rows.resize(R * row_words);
+  gkeys.resize(R);
+  bstr_off.resize(S + 1);
+  bstr_bytes.resize(SB);
+  auto copy = [&](size_t k) {
+    Batch& p = parts[k];
+    const uint32_t hs = (uint32_t)ho[k], ss = (uint32_t)so[k], bs = (uint32_t)bo[k];
+    if (!p.heap.empty()) std::memcpy(heap.data() + ho[k], p.heap.data(), p.heap.size() * 4);
+    for (uint32_t i = 0; i < p.n(); i++) {
+      const uint32_t base = p.req_base[i] + hs;
+      req_base[ro[k] + i] = base;
+      heap[base + RH_SBASE] += ss;  // request-local strings: the part's numbering, shifted
+      uint32_t* row = rows.data() + (ro[k] + i) * row_words;
+      std::memcpy(row, p.rows.data() + (size_t)i * row_words, (size_t)row_words * 4);
+      row[RW_BLK] += hs;
+      gkeys[ro[k] + i] = p.gkeys[i];
+    }
+    for (uint32_t j = 0; j < p.n_bstr(); j++) bstr_off[ss + 1 + j] = p.bstr_off[1 + j] + bs;
+    if (!p.bstr_bytes.empty()) std::memcpy(bstr_bytes.data() + bo[k], p.bstr_bytes.data(), p.bstr_bytes.size());
+    p = Batch();  // its memory goes back as soon as it is copied
+  };
+  threads = std::max(1u, std::min<unsigned>(threads, (unsigned)np));
+  if (threads <= 1) {
+    for (size_t k = 0; k < np; k++) copy(k);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> ws;
+  for (unsigned t = 1; t < threads; t++)
+    ws.emplace_back([&] { for (size_t k; (k = next++) < np;) copy(k); });
+  for (size_t k; (k = next++) < np;) copy(k);
+  for (auto& w : ws) w.join();
 }
 
 void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {

@@ -103,6 +103,7 @@ struct Image {
   // 0 = empty; size is a power of two. Built by build_lookup once the table is final.
   std::vector<uint64_t> lookup;
   void build_lookup();
+  uint64_t cache_id = 0;  // unique per build_lookup (per final image): keys the encoder's caches
   int32_t find(std::string_view s) const {
     if (lookup.empty()) {
       auto it = sid.find(std::string(s));
@@ -218,6 +219,11 @@ struct RequestIn {
 // request's string base, stored at RH_SBASE when the block is appended).
 struct EncodedRequest {
   std::vector<uint32_t> blk, row;  // heap block; columnar row (RW_BLK set on append)
+  // Ancestor lists ([n, (type, id) x n] + the key-entity indices of a scope-bitset image), kept out
+  // of the block: record k starts at anc[anc_at[k]]. The block's ER_ANC words and the row's
+  // RW_*ANC words name records (k, and k + 1 with 0 = none) until Batch::append interns each
+  // record in the batch heap (one copy per distinct list) and points them at it.
+  std::vector<uint32_t> anc, anc_at;
   // grouping key (group.hip): (action, resource type) | principal key ancestors | hot values,
   // hashed fields of the row, most significant first; the device bucket-sorts on its top bits
   uint32_t gkey = 0;
@@ -229,7 +235,10 @@ struct EncodedRequest {
   static constexpr uint32_t MEMO = 32;
   const char* memo_p[MEMO];
   uint32_t memo_len[MEMO], memo_id[MEMO], n_memo = 0;
-  void clear() { blk.clear(); row.clear(); strs.clear(); strs_ix.clear(); n_memo = 0; }
+  void clear() { blk.clear(); row.clear(); anc.clear(); anc_at.clear(); strs.clear(); strs_ix.clear(); n_memo = 0; }
+  // words of record k / the first pair of the list a row word (k + 1) names
+  const uint32_t* anc_rec(uint32_t k) const { return anc.data() + anc_at[k]; }
+  const uint32_t* anc_pairs(uint32_t row_word) const { return anc_rec(row_word - 1) + 1; }
 };
 // Encodes (EntityMap, Request) for `img`. Thread-safe: reads the image only.
 void encode_request(const Image& img, const std::vector<EntityIn>& ents, const RequestIn& req, EncodedRequest& out);
@@ -252,6 +261,12 @@ struct Batch {
   std::vector<uint32_t> bstr_off{0};
   std::vector<uint8_t> bstr_bytes;
   uint32_t n_bstr() const { return (uint32_t)bstr_off.size() - 1; }
+  // Interned ancestor lists (EncodedRequest::anc): content hash -> heap offset of the copy that
+  // later blocks reference (image.h "ancestor lists"). Requests of one principal share one list,
+  // so a batch carries each distinct list once and grouped neighbours read the same lines.
+  std::unordered_map<uint64_t, uint32_t> anc_memo;
+  uint64_t anc_words = 0, anc_shared_words = 0;  // list words appended / list words served by a copy
+  uint32_t intern_list(const uint32_t* w, uint32_t n, uint64_t room);
   // results
   uint32_t capr = 8, cape = 4;
   // on-device follow-up sizing (device.h FuKind), from the previous batch on the same image:
@@ -274,7 +289,9 @@ struct Batch {
     const uint32_t *ids = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
     uint32_t cap = 0, capr = 0, cape = 0;
   } fu[3];
-  const uint32_t* fu_cnt = nullptr;  // requests each worklist's gather found (may exceed cap)
+  // requests each worklist's gather found (may exceed cap); [FU_KINDS]: requests whose key-entity
+  // indices were not the image's (device.h DevBatch::fu_cnt)
+  const uint32_t* fu_cnt = nullptr;
   struct BigRef { const uint32_t *r = nullptr, *e = nullptr; uint32_t nr = 0, ne_words = 0; };
   std::vector<BigRef> big;
   void set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words);
@@ -284,6 +301,10 @@ struct Batch {
   std::string str(uint32_t i, uint32_t id) const;
   void add(const std::vector<EntityIn>& ents, const RequestIn& req);  // encode_request + append
   void append(EncodedRequest& e);                                     // moves e's strings
+  // Appends whole batches encoded on other threads (same image), in order: each part's heap, rows,
+  // grouping keys and strings are copied at their offsets and its block-relative words stay valid
+  // (request bases, RW_BLK and RH_SBASE are shifted). `threads` copy the parts side by side.
+  void concat(std::vector<Batch>& parts, unsigned threads);
   void finalize_strings();
   // decision: 1 allow, 0 deny; fills the Go-JSON rendering of the cedar.Diagnostic
   bool decision(uint32_t i) const;

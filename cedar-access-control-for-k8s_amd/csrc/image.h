@@ -66,6 +66,14 @@ enum ReqHdr : uint32_t {
 };
 enum EntRow : uint32_t { ER_TYPE = 0, ER_ID = 1, ER_ATTR0 = 2, ER_ATTR1 = 3, ER_ANC = 4, ER_PAD = 5, ENT_WORDS = 6 };
 constexpr uint32_t NO_ENT = 0xFFFFFFFFu;
+// Ancestor lists of request entities live outside their blocks: the batch heap holds each distinct
+// list once ([n, (type, id) x n], then the key-entity indices on a scope-bitset image), ahead of the
+// first block that uses it, and every block whose entity has that ancestry points back at it. So a
+// table entity's ER_ANC is an SP_HEAP ref whose 26-bit offset is signed (two's complement,
+// block-relative, at most ANC_REACH words back), and the row's RW_PANC / RW_RANC / RW_AANC are
+// signed 32-bit block-relative offsets of the first pair.
+constexpr uint32_t ANC_REACH = (1u << 25) - 1;
+__host__ __device__ constexpr inline int32_t sext26(uint32_t off) { return (int32_t)(off << 6) >> 6; }
 
 // ---- static entities (the image's entity hierarchy) -------------------------------------------
 // Entities compiled into the image (cg_compiler_set_entities): a group / namespace hierarchy the
@@ -276,7 +284,7 @@ enum RowW : uint32_t {
   RW_P = 0,      // principal (type sid, id sid)
   RW_A = 2,      // action
   RW_R = 4,      // resource
-  RW_PANC = 6,   // block-relative offset of the principal's ancestor (type, id) pairs
+  RW_PANC = 6,   // block-relative offset (signed) of the principal's ancestor (type, id) pairs
   RW_RANC = 7,
   RW_AANC = 8,
   RW_PN = 9,     // ancestor counts (AN_COUNT); an indexed image's lists hold the ancestors that are

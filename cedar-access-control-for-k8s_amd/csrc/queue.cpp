@@ -125,11 +125,10 @@ struct cg_queue {
   static constexpr uint32_t DEPTH = 2;  // batches per submitter: one running, the next queued
 
   // cg_queue_destroy waits this long for the device to drain what was dealt, then fails the rest
-  // (CEDARGPU_QUEUE_STOP_GRACE_MS, default 2000): a hung GPU cannot block shutdown forever
-  static int64_t stop_grace_ns() {
-    static const int64_t g = [] { const char* e = std::getenv("CEDARGPU_QUEUE_STOP_GRACE_MS"); return (int64_t)(e ? std::atoll(e) : 2000) * 1000000; }();
-    return g;
-  }
+  // (CEDARGPU_QUEUE_STOP_GRACE_MS when the destroy begins, default 2000): a hung GPU cannot block
+  // shutdown forever
+  std::atomic<int64_t> grace_ns{2000000000};
+  int64_t stop_grace_ns() const { return grace_ns.load(); }
   bool stopping_too_long() const;
   void fail_backlog(std::deque<std::shared_ptr<Ticket>>& backlog);
 
@@ -169,9 +168,14 @@ void cg_queue::work(QWorker& w) {
   auto finish = [&](std::shared_ptr<QBatch>& qb) {
     if (!qb->rc) {
       // no deadline while the queue runs; once it is closing, at most its grace (a hung device
-      // then fails the batch's callers and cg_queue_destroy returns)
+      // then fails the batch's callers and cg_queue_destroy returns). The download is polled in
+      // 10 ms slices even while running, so a close that begins during a wait on a hung device is
+      // seen; host re-runs after it get the rest of the grace (none while running).
       int rc;
-      while ((rc = cg_batch_wait(qb->b, stop_ns.load() ? 10000000 : -1)) == CG_E_TIMEOUT && !stopping_too_long()) {
+      for (;;) {
+        const int64_t t = stop_ns.load();
+        rc = cg::batch_wait(qb->b, now_ns() + 10000000, t ? t + stop_grace_ns() : -1);
+        if (rc != CG_E_TIMEOUT || qb->b->downloaded || stopping_too_long()) break;
       }
       if (rc) {
         qb->rc = rc;
@@ -441,6 +445,7 @@ int cg_queue_create(cg_ctx* ctx, uint32_t max_batch, uint32_t max_delay_us, cg_q
 
 void cg_queue_destroy(cg_queue* q) {
   if (!q) return;
+  if (const char* e = std::getenv("CEDARGPU_QUEUE_STOP_GRACE_MS")) q->grace_ns.store((int64_t)std::max(0LL, std::atoll(e)) * 1000000);
   q->stop_ns.store(now_ns());
   q->stop.store(true);
   q->pending.fetch_add(1);  // wakes the flusher, which deals what it holds and returns

@@ -115,6 +115,12 @@ int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t*
 int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* n_hot, uint32_t* n_actions,
                    uint32_t* stream_words);
 
+/* Scope-index shape (diagnostics and tests): hot slots whose rows carry element-hash lists (sets a
+ * contains / containsAny atom reads) and prefix-hash lists (`like "lit*"` keys), level-1 key combos
+ * in use, index entries, and scope-bitset contexts x words per context row. */
+int cg_image_index_stats(const void* image, size_t len, uint32_t* cslot_mask, uint32_t* pslot_mask,
+                         uint32_t* combo_mask, uint32_t* entries, uint32_t* contexts, uint32_t* sbits_words);
+
 /* 1 when policy i (image order) lowered to predicate atoms, 0 when it runs as bytecode. */
 int cg_image_policy_atomic(const void* image, size_t len, uint32_t i, int* atomic);
 /* 1 when the image is evaluated by the probe kernel over the scope index (all policies atomic). */
@@ -134,10 +140,14 @@ const char* cg_last_error(cg_ctx* ctx);
  * --confirm-non-prod-inject-errors; not for production). CG_FAULT_DEVICE_ERROR: the next `arg`
  * batch submits on ctx fail with CG_E_DEVICE without touching the device. CG_FAULT_STALL: every
  * batch submit first runs a device kernel that waits `arg` microseconds (at most 2 s), as a slow or
- * stuck GPU would. CG_FAULT_NONE clears both. */
+ * stuck GPU would. CG_FAULT_BAD_KIDX: the next `arg` batches carry principal key-entity indices the
+ * image does not have, as a batch encoded for another image would; the device detects them (the
+ * requests fall back to exact key enumeration) and cg_batch_wait fails the batch with CG_E_DEVICE.
+ * CG_FAULT_NONE clears all. */
 #define CG_FAULT_NONE 0
 #define CG_FAULT_DEVICE_ERROR 1
 #define CG_FAULT_STALL 2
+#define CG_FAULT_BAD_KIDX 3
 int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg);
 /* Copies and uploads an image; the caller keeps ownership of `image`. Not active until activated. */
 int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch);
@@ -220,6 +230,10 @@ int cg_batch_reruns(cg_batch* b, uint32_t* n);
 int cg_batch_followups(cg_batch* b, uint32_t* counts);
 /* Device bytes of the batch (heap + results) and of its image. */
 int cg_batch_bytes(cg_batch* b, uint64_t* batch_bytes, uint64_t* image_bytes, uint64_t* heap_bytes);
+/* What the batch moves over PCIe once submitted: the one H2D upload (request heap, rows, strings,
+ * grouping keys) and the one D2H result copy; and the ancestor-list words its requests carried and
+ * how many of those an earlier request's interned copy served (image.h "ancestor lists"). */
+int cg_batch_io(cg_batch* b, uint64_t* h2d_bytes, uint64_t* d2h_bytes, uint64_t* list_words, uint64_t* list_words_shared);
 
 /* ---- authorization webhook path (SubjectAccessReview in, authorizer.Decision + reason out) ----
  * Appends SubjectAccessReview JSON objects (one or an array) as the reference's /v1/authorize
@@ -237,6 +251,11 @@ int cg_sar_to_cedar_json(const char* sar_json, size_t len, char* out, size_t cap
  * direct path took, *n_mismatch those whose encodings (or fast-path results) differ. */
 int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t n, uint32_t* n_items,
                         uint32_t* n_direct, uint32_t* n_mismatch, int64_t* first_mismatch);
+/* Host-only consistency check of the request encoder: every Cedar-JSON item of the array `items`
+ * (cg_batch_add_json's format) is encoded twice for `image`, with the per-thread ancestor-record
+ * cache and with the general hierarchy walk; *n_mismatch counts items whose encodings differ. */
+int cg_encode_items_check(const void* image, size_t len, const char* items, size_t n, uint32_t* n_items,
+                          uint32_t* n_mismatch, int64_t* first_mismatch);
 /* authorizer.Decision for item i (0 Deny, 1 Allow, 2 NoOpinion) and the reason string the
  * reference returns (diagnosticToReason JSON, a fast-path literal, or ""). */
 int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t cap, size_t* need);

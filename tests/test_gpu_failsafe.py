@@ -179,3 +179,73 @@ def test_authorizer_deadline_under_stall(ctx):
     finally:
         actx.inject_fault(cedargpu.FAULT_NONE)
         actx.close()
+
+
+def test_queue_close_bounded_on_a_stalled_device(ctx):
+    """cg_queue_destroy over a device that does not finish: a submitter already waiting
+    on its in-flight batch polls the download in slices, so the close returns after the grace
+    (CEDARGPU_QUEUE_STOP_GRACE_MS) and the batch's caller gets an error instead of hanging."""
+    import threading
+    cedargpu.TieredPolicyStores([cedargpu.MemoryStore("demo.cedar", DEMO_AUTHZ)], ctx=ctx)
+    sars = _sars()
+    q = cedargpu.Queue(ctx, max_batch=256, max_delay_us=0)
+    got = []
+    old = os.environ.get("CEDARGPU_QUEUE_STOP_GRACE_MS")
+    try:
+        assert q.authorize(sars[-1], timeout=5.0)  # warm
+        ctx.inject_fault(cedargpu.FAULT_STALL, 1_500_000)
+        th = threading.Thread(target=lambda: got.append(q.authorize_failsafe(sars[-1])))
+        th.start()
+        time.sleep(0.2)  # the submitter is now waiting on the stalled batch
+        os.environ["CEDARGPU_QUEUE_STOP_GRACE_MS"] = "200"
+        t0 = time.perf_counter()
+        q.close()
+        dt = time.perf_counter() - t0
+        th.join(timeout=5.0)
+        assert not th.is_alive()
+        assert dt < 0.8, dt                                   # the grace, not the 1.5 s stall
+        assert got == [(cedargpu.Authorizer.NO_OPINION, "")]  # the caller failed safe
+    finally:
+        if old is None:
+            os.environ.pop("CEDARGPU_QUEUE_STOP_GRACE_MS", None)
+        else:
+            os.environ["CEDARGPU_QUEUE_STOP_GRACE_MS"] = old
+        ctx.inject_fault(cedargpu.FAULT_NONE)
+        q.close()
+        time.sleep(1.6)  # the stalled batch drains before the context goes
+
+
+def test_bad_key_entity_indices_fail_the_batch(ctx):
+    """a key-entity index outside the image's (a batch encoded for another
+    image) used to read as "bit not set" in the scan's bitset pass, dropping the key without a
+    signal. The scan now counts such requests (and enumerates their keys exactly), and the batch
+    fails with CG_E_DEVICE, so the webhook answers fail safe instead of trusting the batch."""
+    pop = synth.Population(seed=17, n_users=400, n_groups=60, dag_depth=5)
+    text = synth.abac_policies(400, seed=17, pop=pop)
+    ents = pop.static_entities()
+    tiers = cedargpu.TieredPolicyStores([cedargpu.MemoryStore("c3.cedar", text)], ctx=ctx, entities=ents)
+    assert tiers.ready()
+    assert cedargpu.index_stats(tiers.image)["contexts"] > 0, "the workload must use the scope bitsets"
+    sars = synth.random_sars(300, seed=18, pop=pop)
+    payload = json.dumps(sars)
+    b = ctx.batch()
+    b.add_sar_json(payload)
+    b.submit()
+    b.wait()
+    normal = [b.authz(i) for i in range(len(b))]
+    b.close()
+    ctx.inject_fault(cedargpu.FAULT_BAD_KIDX, 1)
+    b = ctx.batch()
+    try:
+        b.add_sar_json(payload)
+        b.submit()
+        with pytest.raises(cedargpu.DeviceError):
+            b.wait()
+    finally:
+        b.close()
+    b = ctx.batch()  # the fault was consumed: the next batch decides as before
+    b.add_sar_json(payload)
+    b.submit()
+    b.wait()
+    assert [b.authz(i) for i in range(len(b))] == normal
+    b.close()

@@ -179,3 +179,29 @@ def test_incremental_with_repeated_policy_ids():
     assert comp.last_build()["incremental"] is True
     assert _meta(img) == _meta(_fresh(stores2, 2)) and _meta(img)[0] == 4
     comp.close()
+
+
+def test_incremental_keeps_contains_slots_out_of_prefix_keys():
+    """A slot a contains atom reads carries element hashes, so the scope index never files `like
+    "lit*"` prefix keys on it (image.h "prefix level-2 keys"). An incremental build that adds
+    prefix-pattern policies on such a slot must make the same choice as a fresh build: its index
+    shape (list-keyed slots, prefix-keyed slots, entries) equals the fresh image's."""
+    base = "\n".join(f'permit (principal, action == k8s::Action::"get", resource) when {{ context.tags.contains("t{k}") }};'
+                     for k in range(40))
+    base += "\n" + "\n".join(f'permit (principal, action == k8s::Action::"list", resource) when {{ context.path like "/p{k}*" }};'
+                             for k in range(40))
+    extra = "\n".join(f'forbid (principal, action == k8s::Action::"get", resource) when {{ context.tags like "x{k}*" }};'
+                      for k in range(5))
+    docs = [("a", "uid-a", base)]
+    comp = cedargpu.Compiler()
+    comp.build([cedargpu.CRDStore(docs)], epoch=1)
+    docs2 = docs + [("b", "uid-b", extra)]
+    img = comp.build([cedargpu.CRDStore(docs2)], epoch=2)
+    assert comp.last_build()["incremental"] is True
+    fresh = _fresh([cedargpu.CRDStore(docs2)], 2)
+    got, want = cedargpu.index_stats(img), cedargpu.index_stats(fresh)
+    assert want["cslot_mask"] != 0 and want["pslot_mask"] != 0          # both kinds of list slots in use
+    assert want["cslot_mask"] & want["pslot_mask"] == 0                 # never one slot for both
+    assert got == want
+    assert _meta(img) == _meta(fresh)
+    comp.close()

@@ -161,3 +161,27 @@ def test_ancestor_count_limits_of_the_row_format():
     rc = lib.cg_encode_sar_check(img, len(img), b, len(b), ctypes.byref(n), ctypes.byref(nd), ctypes.byref(nm),
                                  ctypes.byref(first))
     assert rc != 0
+
+
+def test_closure_cache_matches_the_hierarchy_walk():
+    """The encoder's per-thread ancestor-record cache (encode_impl.h ClosureCache: static closure
+    rows, unions of parents' closures) against the general hierarchy walk, word for word, on random
+    EntityMaps over random static hierarchies: request edges on static groups, static-only
+    principals, cycles, re-parented static targets (which must take the walk). Host only."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from randgen import Gen
+    for seed in range(6):
+        g = Gen(900 + seed, static=True)
+        ents = g.static_entities()
+        image = cedargpu.build_image([cedargpu.MemoryStore("p.cedar", synth.abac_policies(200, seed=seed))], entities=ents)
+        items = []
+        for _ in range(300):
+            e, r = g.item()
+            items.append({"entities": e, "request": r})
+        b = json.dumps(items).encode()
+        n, nm, first = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int64()
+        assert lib.cg_encode_items_check(image, len(image), b, len(b), ctypes.byref(n), ctypes.byref(nm),
+                                         ctypes.byref(first)) == 0
+        assert n.value == len(items)
+        assert nm.value == 0, items[first.value]
