@@ -463,7 +463,10 @@ def main():
     b.wait()  # correctness pass: results downloaded, follow-ups folded, host re-runs (if any) done
     t_first = time.perf_counter()
     followups, host_reruns = b.followups(), b.reruns()
-    io = b.io()
+    try:
+        io = b.io()
+    except AttributeError:  # an A/B build (CEDARGPU_AB_LIB) that predates cg_batch_io
+        io = {"h2d_bytes": 0, "d2h_bytes": 0, "list_words": 0, "list_words_shared": 0}
     n_reasons = [b.reasons(i)[0].__len__() for i in range(len(b))]
     alg_bytes = algorithmic_bytes(sars, n_reasons, has_like=True)
 
@@ -505,7 +508,10 @@ def main():
         b2.submit()
         b2.wait()
         t2e = time.perf_counter()
-        io2 = b2.io()
+        try:
+            io2 = b2.io()
+        except AttributeError:
+            io2 = {"h2d_bytes": 0, "d2h_bytes": 0}
         s2r = {"requests": len(b2), "encode_s": t1e - t0e, "encode_per_s": len(b2) / (t1e - t0e),
                "submit_to_results_ms": (t2e - t1e) * 1e3, "decisions_per_s": len(b2) / (t2e - t1e),
                "h2d_bytes": io2["h2d_bytes"], "d2h_bytes": io2["d2h_bytes"],

@@ -1041,6 +1041,15 @@ int cg_batch_submit(cg_batch* b) {
     const uint32_t fit = (uint32_t)std::min<uint64_t>(64u, budget / (8ull * std::max<uint32_t>(1u, n))) & ~7u;
     if (std::min(want_capr, fit) > b->host.capr) b->host.capr = std::min(want_capr, fit);
   }
+  // A small batch runs as one launch whose waves hold up to 1,024 hits each (device.h
+  // DevBatch::small) and has no on-device follow-up: its reason lists get room for most of those
+  // (within 2 MB per batch), so that a many-hit request seldom needs a host re-run.
+  // (Within 512 KB of reasons and 256 KB of errors per batch: the D2H copy carries them all; a
+  // longer list takes one of the batch's overflow slots.)
+  if (b->img->host->indexed && n <= dev_small_n()) {
+    b->host.capr = std::max(b->host.capr, std::min<uint32_t>(1024u, std::max<uint32_t>(32u, (uint32_t)((512u << 10) / (4ull * n)))) & ~7u);
+    b->host.cape = std::max(b->host.cape, std::min<uint32_t>(32u, std::max<uint32_t>(4u, (uint32_t)((256u << 10) / (24ull * n)))));
+  }
   if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   GUARD(b->err, { group_requests(b); })
   tr.mark("group");

@@ -101,6 +101,12 @@ struct KArgs {
   // scan + scan_n + i * 2 * SCAN_CAP
   uint32_t* scan;
   uint32_t scan_n;
+  // one-launch small batches (DevBatch::small): a request whose deciding list outgrows capr takes
+  // an overflow slot (ovf_cnt: slots taken) and writes its whole result there, laid out like a
+  // follow-up worklist entry (ids, res, reasons, errors) that cg_batch_wait folds in
+  uint32_t* ovf_cnt;
+  uint32_t *ovf_ids, *ovf_res, *ovf_rf, *ovf_er;
+  uint32_t ovf_cap, ovf_capr, ovf_cape;
 };
 // SCAN_CAP: bucket pairs a request's list holds (more: SCAN_OVF, the large stage probes the index
 // itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
@@ -2458,6 +2464,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
 
   }
   uint32_t nf = 0, np = 0, nerr = 0;  // distinct deciding forbids / permits / errors
+  uint32_t oslot = 0xFFFFFFFFu;       // the overflow slot this request's result went to (SLIM)
   if constexpr (SLIM) {
     // Merge by bitmaps over policy indices (wl.u.hs: the bitmap, then prefix popcounts per word):
     // the deciding tier's forbids are marked first; when none, its permits. Every such hit then
@@ -2499,24 +2506,35 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       nf = mark(1u);
       if (!nf) np = mark(0u);
       const uint32_t kd = nf ? 1u : 0u;
+      // a deciding list longer than the request's slot: an overflow slot when the launch has them
+      if (a.ovf_cnt && valid && (nf ? nf : np) > a.capr) {
+        uint32_t o = 0;
+        if (lane_m == 0) o = atomicAdd(a.ovf_cnt, 1u);
+        o = (uint32_t)__shfl((int)o, 0);
+        oslot = o < a.ovf_cap ? o : 0xFFFFFFFFu;
+      }
+      uint32_t* rdst = oslot != 0xFFFFFFFFu ? a.ovf_rf + (size_t)oslot * a.ovf_capr : a.reasons_f + (size_t)wo * a.capr;
+      const uint32_t rcap = oslot != 0xFFFFFFFFu ? a.ovf_capr : a.capr;
       bool anyerr = false;
       for (uint32_t i = lane_m; i < nh; i += 64) {
         const uint32_t x = wl.hp[0][i];
         anyerr = anyerr || sel(x, 2u);
         if (sel(x, kd)) {
           const uint32_t p = x & SLIM_POL, rk = rank(p);
-          if (rk < a.capr) __builtin_nontemporal_store(p, a.reasons_f + (size_t)wo * a.capr + rk);
+          if (rk < rcap) __builtin_nontemporal_store(p, rdst + rk);
         }
       }
       if (__ballot(anyerr)) {
         wave_lds_sync();
         nerr = mark(2u);
+        const uint32_t ecap = oslot != 0xFFFFFFFFu ? a.ovf_cape : a.cape;
+        uint32_t* edst = oslot != 0xFFFFFFFFu ? a.ovf_er + (size_t)oslot * a.ovf_cape * ERR_WORDS : a.errs + (size_t)wo * a.cape * ERR_WORDS;
         for (uint32_t i = lane_m; i < nh; i += 64) {
           const uint32_t x = wl.hp[0][i];
           if (!sel(x, 2u)) continue;
           const uint32_t p = x & SLIM_POL, rk = rank(p), xs = x >> SLIM_SLOT;
-          if (rk < a.cape) {
-            uint32_t* er = a.errs + ((size_t)wo * a.cape + rk) * ERR_WORDS;
+          if (rk < ecap) {
+            uint32_t* er = edst + (size_t)rk * ERR_WORDS;
             er[0] = p; er[1] = wl.he[0][4 * xs]; er[2] = wl.he[0][4 * xs + 1]; er[3] = wl.he[0][4 * xs + 2];
             er[4] = wl.he[0][4 * xs + 3]; er[5] = 0;
           }
@@ -2653,6 +2671,12 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     const uint32_t dec = nf ? DEC_DENY : (np ? DEC_ALLOW : DEC_DENY);
     const uint32_t nr = nf ? nf : np;
     uint32_t fl = RF_VALID | (nf ? RF_FORBID : 0u);
+    if (oslot != 0xFFFFFFFFu) {  // the whole result in the overflow slot; the request's own says so
+      const uint32_t fo = fl | ((nr > a.ovf_capr || nerr > a.ovf_cape) ? RF_OVERFLOW : 0u);
+      a.ovf_ids[oslot] = wo;
+      a.ovf_res[2 * (size_t)oslot] = dec | (t << 8) | (fo << 16);
+      a.ovf_res[2 * (size_t)oslot + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
+    }
     if (nr > a.capr || nerr > a.cape) fl |= RF_OVERFLOW;
     a.res[2 * (size_t)wo] = dec | (t << 8) | (fl << 16);
     a.res[2 * (size_t)wo + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
@@ -2948,6 +2972,11 @@ void dev_pool_destroy(DevPool* p) {
 
 static bool split_on();
 
+uint32_t dev_small_n() {  // (read per batch: tests cover both paths at small sizes)
+  const char* e = std::getenv("CEDARGPU_SMALL_N");
+  return e ? (uint32_t)std::atoi(e) : 2048u;
+}
+
 // One pinned staging block and one device block for the inputs (256-B aligned sections), one for
 // the results; a batch costs two copies and a memset, and no allocation once the pool is warm.
 int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, DevPool* pool) {
@@ -2961,6 +2990,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.row_words = b.row_words;
   d.capr = b.capr;
   d.cape = b.cape;
+  d.small = b.img->indexed && split_on() && b.n() && b.n() <= dev_small_n();
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   // the grouping keys travel only when the step groups the batch on the device
   const bool grp = b.dev_group && b.n() >= 2 && b.gkeys.size() == b.n();
@@ -2974,8 +3004,9 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // The probe kernel writes only the deciding reason list (into reasons_f; reasons_p aliases it),
   // the policy-stream kernel both lists: an indexed image's first pass needs one array.
   const bool one_list = b.img->indexed != 0;
-  const size_t o_res = 0, o_rf = al(n * 2 * 4), o_rp = one_list ? o_rf : o_rf + al(n * d.capr * 4),
-               o_er = o_rp + al(n * d.capr * 4);
+  // the worklist counters sit right behind res: the upload's one memset zeroes both
+  const size_t o_res = 0, o_cnt = al(n * 2 * 4), o_rf = o_cnt + al((FU_KINDS + 1) * 4),
+               o_rp = one_list ? o_rf : o_rf + al(n * d.capr * 4), o_er = o_rp + al(n * d.capr * 4);
   // On-device follow-up worklists. Entries: n / 32 (4..64) by default, or what the previous batch
   // on this image needed (the caller's hint), within a byte budget per worklist. Reasons per entry:
   // FU_BIG 256 unless the hint says otherwise (64..1024, the large stage's hit capacity), FU_OVF 64
@@ -2990,8 +3021,6 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024)),
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024))};
   size_t o_fu = o_er + al(n * d.cape * ERR_WORDS * 4);
-  const size_t o_cnt = o_fu;
-  o_fu += al((FU_KINDS + 1) * 4);
   size_t o_k[FU_KINDS][5];
   for (uint32_t k = 0; k < FU_KINDS; k++) {
     auto& f = d.fu[k];
@@ -3001,7 +3030,15 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     const size_t lists = probe_kind ? 1 : 2;
     const size_t entry = 4 * (1 + 2 + lists * (size_t)f.capr + (size_t)f.cape * ERR_WORDS);
     const uint32_t want = std::min<uint32_t>(b.n(), std::max(fu_default, b.fu_want[k]));
-    f.cap = (fu_on && b.n() && (!probe_kind || b.img->indexed)) ? (uint32_t)std::min<size_t>(want, budget_k[k] / entry) : 0u;
+    f.cap = (fu_on && b.n() && !d.small && (!probe_kind || b.img->indexed)) ? (uint32_t)std::min<size_t>(want, budget_k[k] / entry) : 0u;
+    if (d.small && k == FU_BIG && fu_on && b.img->n_pol() <= RANK_POL) {
+      // the small path's overflow slots (KArgs::ovf_*, its SLIM merge): whole results of up to
+      // 1,024 reasons and 32 errors for n / 16 requests (at least 8); every slot travels back in the
+      // one D2H copy, so they stay few
+      f.capr = 1024;
+      f.cape = 32;
+      f.cap = std::min<uint32_t>(b.n(), std::max<uint32_t>(8u, b.n() / 16u));
+    }
     o_k[k][0] = o_fu;                                        // ids
     o_k[k][1] = o_k[k][0] + al((size_t)f.cap * 4);           // res
     o_k[k][2] = o_k[k][1] + al((size_t)f.cap * 2 * 4);       // reasons_f
@@ -3020,7 +3057,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     if ((rc = pool_get(pool, false, lane_bytes, &d.lane_blk, &d.lane_cls))) return rc;
     d.lane = (uint32_t*)d.lane_blk;
   }
-  if (b.img->indexed && split_on() && b.n()) {  // the index scan's bucket lists
+  if (b.img->indexed && split_on() && b.n() && !d.small) {  // the index scan's bucket lists
     if ((rc = pool_get(pool, false, (size_t)b.n() * (1 + 2 * SCAN_CAP) * 4, &d.scan_blk, &d.scan_cls))) {
       pool_put(pool, false, d.lane_blk, d.lane_cls);
       return rc;
@@ -3114,7 +3151,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.pending = true;
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
   HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
-  HIPCHK(hipMemsetAsync(d.res, 0, n * 2 * 4, s), "memset res");
+  HIPCHK(hipMemsetAsync(d.res, 0, o_rf, s), "memset res");  // (and the worklist counters)
   return 0;
 }
 
@@ -3309,6 +3346,9 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.grows = nullptr;
   k.scan = nullptr;
   k.scan_n = 0;
+  k.ovf_cnt = nullptr;
+  k.ovf_ids = k.ovf_res = k.ovf_rf = k.ovf_er = nullptr;
+  k.ovf_cap = k.ovf_capr = k.ovf_cape = 0;
   return k;
 }
 
@@ -3551,6 +3591,25 @@ static void launch_eval(const DevImage& img, const KArgs& k, uint32_t n, hipStre
 // dev_time_eval times it.
 static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
   KArgs k = make_args(img, b, nullptr, b.n, b.res, b.reasons_f, b.reasons_p, b.errs, b.capr, b.cape);
+  if (b.small) {
+    // one launch: a wave per request probes the index itself (no scan lists), evaluates its
+    // candidates and merges up to 1,024 hits; the reason capacity was sized for it at submit, and
+    // a longer deciding list goes to an overflow slot (the FU_BIG worklist's entries, SLIM form)
+    mark(PH_GROUP, s);
+    const auto& f = b.fu[FU_BIG];
+    if (b.fu_cnt && f.cap && big_slim(k)) {
+      if (b.stepped) HIPCHK(hipMemsetAsync(b.fu_cnt, 0, (FU_KINDS + 1) * 4, s), "memset worklists");
+      k.ovf_cnt = b.fu_cnt + FU_BIG;
+      k.ovf_ids = f.ids; k.ovf_res = f.res; k.ovf_rf = f.rf; k.ovf_er = f.er;
+      k.ovf_cap = f.cap; k.ovf_capr = f.capr; k.ovf_cape = f.cape;
+    }
+    b.stepped = true;
+    if (big_slim(k)) hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_SLIM_MINW, false, 1, false, true>), dim3(b.n), dim3(64), 0, s, k);
+    else hipLaunchKernelGGL((cedar_probe_kernel<64, 1024, BIG_MINW, false, 1, false>), dim3(b.n), dim3(64), 0, s, k);
+    HIPCHK(hipGetLastError(), "launch");
+    for (uint32_t p = PH_SCAN; p < STEP_PHASES; p++) mark(p, s);
+    return 0;
+  }
   k.scan = b.scan;
   k.scan_n = b.n;
   if (b.ord) {  // grouped batch: this step's order and its rows in that order (group.hip)

@@ -80,6 +80,11 @@ struct DevBatch {
   void* lane_blk = nullptr;
   size_t lane_cls = 0;
   uint32_t n = 0, capr = 0, cape = 0, row_words = 0;
+  // a small batch of an indexed image (n <= dev_small_n()): the whole step is one launch of the
+  // one-request-per-wave probe kernel (no scan lists, no gather, no follow-up launches; what its
+  // lists cannot hold goes to the host re-run)
+  bool small = false;
+  bool stepped = false;  // the step ran once since the upload (later steps reset their counters)
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)
   size_t in_cls = 0, out_cls = 0, stage_cls = 0, out_bytes = 0;
@@ -88,6 +93,9 @@ struct DevBatch {
   bool pending = false;    // work enqueued on the batch's buffers not yet waited for
 };
 
+// Batches of at most this many requests on an indexed image run as one launch (DevBatch::small);
+// CEDARGPU_SMALL_N overrides (0: never).
+uint32_t dev_small_n();
 // All functions return 0 on success, or a negative CG_E_* code with dev_last_error() set.
 const char* dev_last_error();
 int dev_count(int* n);

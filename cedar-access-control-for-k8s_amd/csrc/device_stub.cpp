@@ -45,6 +45,7 @@ struct DevPool {
 
 const char* dev_last_error() { return g_err.c_str(); }
 int dev_count(int* n) { *n = 8; return 0; }  // contexts 0..7 (multi-context queue tests)
+uint32_t dev_small_n() { return 0; }  // the stand-in has one evaluation path
 int dev_select(int) { return 0; }
 int dev_synchronize(int) { return 0; }
 

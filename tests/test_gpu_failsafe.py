@@ -226,7 +226,7 @@ def test_bad_key_entity_indices_fail_the_batch(ctx):
     tiers = cedargpu.TieredPolicyStores([cedargpu.MemoryStore("c3.cedar", text)], ctx=ctx, entities=ents)
     assert tiers.ready()
     assert cedargpu.index_stats(tiers.image)["contexts"] > 0, "the workload must use the scope bitsets"
-    sars = synth.random_sars(300, seed=18, pop=pop)
+    sars = synth.random_sars(2600, seed=18, pop=pop)  # past dev_small_n(): the scan's bitset pass runs
     payload = json.dumps(sars)
     b = ctx.batch()
     b.add_sar_json(payload)

@@ -106,6 +106,8 @@ def test_random_atomic_policies_vs_oracle(ctx, seed, monkeypatch):
     """Policies lowered to predicate atoms (incl. label-selector record templates)."""
     if seed % 2:  # odd seeds: the batch grouped by principal before upload (results mapped back)
         monkeypatch.setenv("CEDARGPU_GROUP", "1")
+    if seed % 4 >= 2:  # the split first pass (scan + candidate pass + follow-ups) at this size too
+        monkeypatch.setenv("CEDARGPU_SMALL_N", "0")
     g = Gen(5000 + seed)
     stores = [cedargpu.MemoryStore(f"a{t}.cedar", g.atomic_policies(g.r.randint(1, 40))) for t in range(g.r.randint(1, 2))]
     items = [g.item() for _ in range(400)]
@@ -278,6 +280,8 @@ def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, group, m
         monkeypatch.setenv("CEDARGPU_FOLLOWUP", followup)
     if group:  # the batch grouped by principal before upload
         monkeypatch.setenv("CEDARGPU_GROUP", group)
+    if not followup:  # the split first pass and its on-device follow-ups (else the one-launch small path)
+        monkeypatch.setenv("CEDARGPU_SMALL_N", "0")
     pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
                      for i in range(n))
     pols += '\nforbid (principal, action == k8s::Action::"create", resource) when { principal has nick };'
@@ -291,8 +295,9 @@ def test_index_kernel_hit_overflow_reruns(ctx, n, first_capr, followup, group, m
         check_items(ctx, stores, items)
 
 
+@pytest.mark.parametrize("small_n", [None, "0"])
 @pytest.mark.parametrize("first_tier_hits", [0, 3, 150])
-def test_large_stage_tiers_forbids_and_errors(ctx, first_tier_hits):
+def test_large_stage_tiers_forbids_and_errors(ctx, first_tier_hits, small_n, monkeypatch):
     """The large stage's merge (its SLIM form on images of <= 16,384 policies: kind, tier and error
     slot in the hit word, bitmaps over policy indices) over two tiers: the deciding tier is the
     first with a hit; its forbids, else its permits, are the reasons, and its errors (attributes the
@@ -303,16 +308,19 @@ def test_large_stage_tiers_forbids_and_errors(ctx, first_tier_hits):
                     f'when {{ principal.nick == "n{i % 4}" }};') if i % 9 == 0 else
                    f'permit (principal in k8s::Group::"g{i % 3}", action, resource) when {{ principal.age > {i % 7} }};'
                    for i in range(400))
+    if small_n:  # the split first pass and its large-stage follow-up (else the one-launch small path)
+        monkeypatch.setenv("CEDARGPU_SMALL_N", small_n)
     stores = [cedargpu.MemoryStore("tier0.cedar", t0), cedargpu.MemoryStore("tier1.cedar", t1)]
     g = Gen(97)
     items = [g.item() for _ in range(300)]
     check_items(ctx, stores, items)
 
 
-def test_followup_sized_by_previous_batch(ctx):
+def test_followup_sized_by_previous_batch(ctx, monkeypatch):
     """Most requests collect > 64 reasons: the first batch on an image follows up at most 64 of
     them on the device and re-runs the rest from the host; the next batch on that image sizes its
     follow-up by the share the first one saw, so it re-runs none. Both agree with the oracle."""
+    monkeypatch.setenv("CEDARGPU_SMALL_N", "0")  # the split first pass: the on-device follow-up is its part
     pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 2}", action, resource);' for i in range(200))
     stores = [cedargpu.MemoryStore("hits.cedar", pols)]
     img = cedargpu.build_image(stores, epoch=951)
@@ -362,10 +370,11 @@ def _oracle_diags(stores, items):
             for e, r in items]
 
 
-def test_capacity_hint_short_then_long_lists(ctx):
+def test_capacity_hint_short_then_long_lists(ctx, monkeypatch):
     """one image, a batch of ~70-reason requests (FU_BIG capacity hint 96), then one of
     ~200 (longer than the hint: the follow-up overflows and the host re-runs), then another of ~200
     (the hint grew: no re-run). Every batch matches the oracle."""
+    monkeypatch.setenv("CEDARGPU_SMALL_N", "0")  # the split first pass and its on-device follow-ups
     pols = "\n".join(f"permit (principal, action, resource) when {{ principal.level >= {i} }};" for i in range(260))
     stores = [cedargpu.MemoryStore("levels.cedar", pols)]
     ctx.load(cedargpu.build_image(stores, epoch=961), 961)
@@ -467,9 +476,11 @@ def check_items_ref(ctx, stores, items, want_indexed=None, entities=None):
 
 
 @pytest.mark.parametrize("seed", range(16))
-def test_probe_kernel_random_atomic(ctx, seed):
+def test_probe_kernel_random_atomic(ctx, seed, monkeypatch):
     """All-atomic random corpora (nested paths, &&/||/!/if trees, in-sets, is-in, var == E,
     label-selector templates, multi-tier) through the probe kernel vs the oracle."""
+    if seed % 2:  # the split first pass at this size too (even seeds: the one-launch small path)
+        monkeypatch.setenv("CEDARGPU_SMALL_N", "0")
     g = Gen(9000 + seed)
     texts = [(f"p{t}.cedar", g.atomic_policies(g.r.randint(1, 60))) for t in range(g.r.randint(1, 3))]
     stores = _atomic_only(texts)
@@ -628,9 +639,11 @@ def test_static_entities_random_general(ctx, seed):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_static_entities_random_atomic(ctx, seed):
+def test_static_entities_random_atomic(ctx, seed, monkeypatch):
     """The same through the probe kernel: key enumeration over the merged ancestors, key entities
     first."""
+    if seed % 2:  # the split first pass at this size too (even seeds: the one-launch small path)
+        monkeypatch.setenv("CEDARGPU_SMALL_N", "0")
     g = Gen(12000 + seed, static=True)
     statics = g.static_entities()
     texts = [(f"p{t}.cedar", g.atomic_policies(g.r.randint(1, 50))) for t in range(g.r.randint(1, 2))]
@@ -721,12 +734,14 @@ def test_lowered_shapes_vs_oracle(ctx, name):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_probe_kernel_duplicate_classes(ctx, seed):
+def test_probe_kernel_duplicate_classes(ctx, seed, monkeypatch):
     """Duplicate policies (identical text under other IDs, the same condition with other action
     lists, across tiers and effects, erroring ones included) are filed once as a class and hit for
     every member: reasons, errors and their order vs the oracle, through the first pass and the
     large stage (classes of up to ~100 members)."""
     import random
+    if seed % 2:  # the split first pass at this size too (even seeds: the one-launch small path)
+        monkeypatch.setenv("CEDARGPU_SMALL_N", "0")
     g = Gen(12000 + seed)
     r = random.Random(seed)
     texts = [(f"p{t}.cedar", g.atomic_policies(g.r.randint(4, 30))) for t in range(g.r.randint(1, 3))]
