@@ -543,7 +543,7 @@ int cg_image_index_stats(const void* image, size_t len, uint32_t* cslot_mask, ui
     if (pslot_mask) *pslot_mask = img->pslot_mask;
     if (combo_mask) *combo_mask = img->combo_mask;
     if (entries) *entries = (uint32_t)(img->btab.size() / cgi::BT_WORDS);
-    if (contexts) *contexts = img->sbits_words ? (uint32_t)(img->sbits.size() / img->sbits_words) : 0u;
+    if (contexts) *contexts = img->sbits_words ? (uint32_t)(img->sbits.size() / 2 / img->sbits_words) : 0u;
     if (sbits_words) *sbits_words = img->sbits_words;
     return CG_OK;
   } catch (const std::exception&) {

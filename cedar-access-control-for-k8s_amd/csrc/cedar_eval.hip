@@ -86,8 +86,9 @@ struct KArgs {
   uint32_t slot_split;  // probes load a slot's first 16 B, the rest only on a key match (CEDARGPU_SLOT_SPLIT)
   uint32_t scan_lds;    // the scan stages key ancestors and hot values in LDS up front (CEDARGPU_SCAN_LDS)
   uint32_t scan_filt;   // the scan tests principal keys against the scope bitsets first (CEDARGPU_SCAN_FILT)
-  const uint32_t* __restrict__ sctx;   // scope bitsets (image.h): context table, rows
-  const uint32_t* __restrict__ sbits;
+  const uint32_t* __restrict__ sctx;   // scope bitsets (image.h): context table, (bits, rank) rows,
+  const uint32_t* __restrict__ sbits;  //   and every set bit's bucket at its rank
+  const uint32_t* __restrict__ svals;
   uint32_t sctx_mask, sbits_words;     // sbits_words 0: the image has none
   uint32_t n_kent;                     // key entities: a request's key-entity indices are below it
   uint32_t* bad_kidx;                  // count of requests whose indices are not (null: not counted)
@@ -1667,12 +1668,15 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // before the key loop (the request block and row are cold: each key step would otherwise start
   // with a dependent HBM load)
   // rows padded off a multiple of the 64 LDS banks: the segments of a wave index them in lockstep
-  constexpr uint32_t ANC_ST = BITS ? 32u : SCAN_ANC;  // principal key ancestors staged (UIDs)
-  __shared__ uint2 s_anc[64 / SEG][ANC_ST + 1];
+  // (BITS: no UIDs staged: a key the bitsets find is read from svals, no key hash or probe; a
+  // request off the bitset path reads its key ancestors from its list)
+  constexpr uint32_t ANC_ST = BITS ? 1u : SCAN_ANC;  // principal key ancestors staged (UIDs)
+  __shared__ uint2 s_anc[BITS ? 1 : 64 / SEG][ANC_ST + 1];
   __shared__ uint2 s_hot[64 / SEG][SCAN_HOT + 1];  // the first SCAN_HOT hot values
   // BITS: the key-entity index of the principal ([0]) and of each staged key ancestor ([j]: j - 1),
   // the request's contexts (combo | hs << 8, v0, v1, bitset row) and its listed keys
-  // (LIST_EXACT | context << 16 | principal index, or combo << 11 | principal index)
+  // (LIST_EXACT | combo << 26 | the bit's rank in svals, or combo << 11 for a type / wildcard
+  // principal combo's single key)
   __shared__ uint32_t s_kid[BITS ? 64 / SEG : 1][SCAN_ANC + 2];
   __shared__ uint4 s_cx[BITS ? 64 / SEG : 1][CTX_CAP];
   __shared__ uint32_t s_pos[BITS ? 64 / SEG : 1][SCAN_POS_B + 2];
@@ -1706,7 +1710,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   // and key ancestors after its pairs (p_anc == 0: the principal has no entity, no list)
   const bool kbits = BITS && a.scan_filt && a.sbits_words != 0;
   const bool klist = kbits && valid && p_anc != 0;
-  const bool stl = a.scan_lds != 0;  // UIDs in LDS for the key loop
+  const bool stl = !BITS && a.scan_lds != 0;  // UIDs in LDS for the key loop
   const uint32_t* pl = blk + (int32_t)p_anc;  // the principal's list (signed: image.h "ancestor lists")
   const uint32_t nk = (pn >> AN_KEYS_SHIFT) & AN_KEYS;
   constexpr uint32_t LW = 3;  // list elements loaded with a list head
@@ -1798,7 +1802,6 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     on = on && nctx <= CTX_CAP;
     // the contexts, looked up side by side (lane j % SEG takes context j); a found one is kept
     uint32_t nf = 0;  // contexts found (segment-uniform)
-    bool fpdup = false;
     for (uint32_t j0 = 0; __ballot(on && j0 < nctx) != 0; j0 += SEG) {
       const uint32_t j = j0 + sl;
       uint32_t cb = 0, hs = SCTX_L1, v0 = 0, v1 = 0, row_ = KIDX_NONE;
@@ -1838,13 +1841,17 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         // the request's own context (when it exists) matches on its chain, so its bits are never
         // missed. Two matches on one chain (32-bit fingerprints: practically never) enumerate the
         // request's keys instead.
-        const uint32_t hash = ctx_key(key_pre(cb, q.x, q.y, r.x, r.y), hs, v0, v1), fp = ctx_fp(hash);
+        // the whole 32-byte slot in one trip, compared word for word (exact: a found context's
+        // set bits are the request's keys themselves)
+        const uint32_t hash = ctx_key(key_pre(cb, q.x, q.y, r.x, r.y), hs, v0, v1), w0c = ctx_w0(cb, hs);
         for (uint32_t h = hash & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
-          const uint2 f = *reinterpret_cast<const uint2*>(a.sctx + 2 * (size_t)h);
-          if (f.x == 0) break;
-          if (f.x != fp) continue;
-          if (row_ != KIDX_NONE) { fpdup = true; break; }
-          row_ = f.y;
+          const uint4* slp = reinterpret_cast<const uint4*>(a.sctx + (size_t)h * SCTX_WORDS);
+          const uint4 x = slp[0], y = slp[1];
+          if (x.x == 0) break;
+          if (x.x == w0c && x.y == q.x && x.z == q.y && x.w == r.x && y.x == r.y && y.y == v0 && y.z == v1) {
+            row_ = y.w;
+            break;
+          }
         }
       }
       const bool got = on && j < nctx && row_ != KIDX_NONE;
@@ -1852,7 +1859,6 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       if (got) s_cx[seg][nf + mbcnt64(mk)] = make_uint4(cb | (hs << 8), v0, v1, row_);
       nf += popc64(mk);
     }
-    on = on && sballot(fpdup) == 0;
     wave_lds_sync();
     // (found context, key ancestor) pairs: ip 0 .. nP - 1 under each; a set bit lists the key. All
     // SCAN_PB loads of a lane's round in flight at once.
@@ -1867,31 +1873,33 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     // request enumerates every key instead (exact), and is counted so that the batch fails
     bool badk = false;
     for (uint32_t rb = 0; __ballot(rb < tot) != 0; rb += SEG * SCAN_PB) {
-      uint32_t fw[SCAN_PB], fk[SCAN_PB];
+      uint2 fw[SCAN_PB];
+      uint32_t fk[SCAN_PB], fc[SCAN_PB];
 #pragma unroll
       for (uint32_t u = 0; u < SCAN_PB; u++) {
         const uint32_t t = rb + u * SEG + sl;
-        fw[u] = 0;
+        fw[u] = make_uint2(0u, 0u);
         fk[u] = 0;
+        fc[u] = 0;
         if (t < tot) {
           const uint32_t j = divp(t), ip = t - j * nP;
           const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
           const uint32_t kid = jk <= SCAN_ANC ? s_kid[seg][jk] : kl[jk];
+          const uint4 c = s_cx[seg][j];
           fk[u] = kid;
-          if (kid < a.n_kent) fw[u] = a.sbits[(size_t)s_cx[seg][j].w * a.sbits_words + (kid >> 5)];
+          fc[u] = c.x & 0xFFu;
+          // the bit's word and the rank of the word's first bit, in one 8-byte load
+          if (kid < a.n_kent) fw[u] = *reinterpret_cast<const uint2*>(a.sbits + 2 * ((size_t)c.w * a.sbits_words + (kid >> 5)));
           else badk = badk || kid != KIDX_NONE;
         }
       }
 #pragma unroll
       for (uint32_t u = 0; u < SCAN_PB; u++) {
-        const uint32_t t = rb + u * SEG + sl;
-        const bool ok = (fw[u] >> (fk[u] & 31)) & 1u;
+        const uint32_t b = fk[u] & 31u;
+        const bool ok = (fw[u].x >> b) & 1u;
         const uint64_t mk = sballot(ok);
         const uint32_t at_ = npos + mbcnt64(mk);
-        if (ok && at_ < SCAN_POS_B) {
-          const uint32_t j = divp(t);
-          s_pos[seg][at_] = LIST_EXACT | (j << 16) | (t - j * nP);
-        }
+        if (ok && at_ < SCAN_POS_B) s_pos[seg][at_] = LIST_EXACT | (fc[u] << 26) | (fw[u].y + __popc(fw[u].x & ((1u << b) - 1u)));
         npos += popc64(mk);
       }
     }
@@ -1980,29 +1988,24 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           uint32_t x = 0;
           if (BITS && flt) {
             x = s_pos[seg][kk];
-            if (x & LIST_EXACT) {
-              const uint4 c = s_cx[seg][(x >> 16) & 0x7FFFu];
-              combo = c.x & 0xFFu;
-            } else {
-              combo = x >> 11;
-            }
-            kp = comb_p(combo, x & 0x7FFu);
-            ka = comb_q(combo);
-            kr = comb_r(combo);
+            combo = (x & LIST_EXACT) ? (x >> 26) & 31u : x >> 11;
           } else {
             key_at(kk, combo, kp, ka, kr);
           }
-          w0 = BT_USED | (combo << 16);
-          h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
           uint32_t cmv = 0;
-          if (BITS && (x & LIST_EXACT)) {  // a key the bitsets found: probed once, no descent
-            const uint4 c = s_cx[seg][(x >> 16) & 0x7FFFu];
-            const uint32_t hs = c.x >> 8;
-            if (hs == SCTX_L1) e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, nullptr, nullptr, a.slot_split);
-            else e = probe(a.btab, a.bmask, bucket_hash2(h1, hs, c.y, c.z), w0 | BT_L2 | hs, kp, ka, kr, c.y, c.z, unused, nullptr, nullptr, a.slot_split);
-            e.z = 0;
-          } else if (flt || !a.l1filt || filt_maybe(a.bfilt, a.fmask, h1)) {
-            e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, &blm, &cmv, a.slot_split);
+          if (BITS && (x & LIST_EXACT)) {  // a key the bitsets found: its bucket at the bit's rank
+            const uint2 v = *reinterpret_cast<const uint2*>(a.svals + 2 * (size_t)(x & 0x3FFFFFFu));
+            e = make_uint3(v.x, v.y, 0u);
+          } else {
+            if (BITS && flt) {
+              kp = comb_p(combo, 0u);
+              ka = comb_q(combo);
+              kr = comb_r(combo);
+            }
+            w0 = BT_USED | (combo << 16);
+            h1 = key_hash(combo, kp.x, kp.y, ka.x, ka.y, kr.x, kr.y);
+            if (flt || !a.l1filt || filt_maybe(a.bfilt, a.fmask, h1))
+              e = probe(a.btab, a.bmask, h1, w0, kp, ka, kr, 0, 0, unused, &blm, &cmv, a.slot_split);
           }
           hm = e.z;
           csl = cmv;
@@ -2768,8 +2771,8 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.cpool = (uint32_t*)at(DS_CPOOL); d.gstr_off = (uint32_t*)at(DS_GSTR_OFF); d.hot = (uint32_t*)at(DS_HOT);
   d.act = (uint32_t*)at(DS_ACT); d.btab = (uint32_t*)at(DS_BTAB); d.bfilt = (uint32_t*)at(DS_BFILT);
   d.bstream = (uint32_t*)at(DS_BSTREAM); d.srows = (uint32_t*)at(DS_SROWS); d.shash = (uint32_t*)at(DS_SHASH);
-  d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS);
-  d.sctx_mask = (uint32_t)(img.sctx.size() / (2 + SCTX_WORDS)) - 1;
+  d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS); d.svals = (uint32_t*)at(DS_SVALS);
+  d.sctx_mask = (uint32_t)(img.sctx.size() / SCTX_WORDS) - 1;
   d.sbits_words = img.sbits_words;
   d.n_kent = (uint32_t)img.key_ents.size();
   d.l2_vmask = img.l2_vmask;
@@ -3308,7 +3311,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.act = img.act; k.n_act = img.n_act; k.amask_ok = img.amask_ok;
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
-  k.sctx = img.sctx; k.sbits = img.sbits; k.sctx_mask = img.sctx_mask; k.sbits_words = img.sbits_words;
+  k.sctx = img.sctx; k.sbits = img.sbits; k.svals = img.svals; k.sctx_mask = img.sctx_mask; k.sbits_words = img.sbits_words;
   k.n_kent = img.n_kent;
   k.bad_kidx = b.fu_cnt ? b.fu_cnt + FU_KINDS : nullptr;
   k.l2_vmask = img.l2_vmask; k.l2_lmask = img.l2_lmask;

@@ -1024,7 +1024,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
   img.key_ents.clear();
-  img.sctx.assign(2 * (2 + SCTX_WORDS), 0); img.sbits.assign(1, 0); img.sbits_words = 0;
+  img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0;
   img.combo_mask = 0;
   img.pslot_mask = 0;
   img.pfx.assign((size_t)img.n_hot() * PFX_LENS, 0);
@@ -1057,7 +1057,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
     img.btab_slots = 2;
-    img.sctx.assign(2 * (2 + SCTX_WORDS), 0); img.sbits.assign(1, 0); img.sbits_words = 0;
+    img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0;
     return;
   }
   static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
@@ -1278,16 +1278,19 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   mark("buckets");
   // scope bitsets (image.h "scope bitsets"): a row per context of the keys whose principal
   // component is an entity, a bit per key entity: level-1 keys that file policies directly, and
-  // every level-2 key
+  // every level-2 key. The bits' buckets (svals) are known once the heads are laid out, below.
+  std::map<std::array<uint32_t, 8>, uint32_t> ctx;
+  struct SBit { uint32_t row, kidx, grp; };  // grp: g1 index, or g2 index | SB_L2
+  constexpr uint32_t SB_L2 = 0x80000000u;
+  std::vector<SBit> sbit;
   {
-    std::map<std::array<uint32_t, 8>, uint32_t> ctx;
-    std::vector<std::pair<uint32_t, uint32_t>> bits;  // (row, kidx)
     auto kidx = [&](uint32_t t, uint32_t i) {
       const uint64_t u = ((uint64_t)t << 32) | i;
       return (uint32_t)(std::lower_bound(img.key_ents.begin(), img.key_ents.end(), u) - img.key_ents.begin());
     };
     img.l2_vmask = img.l2_lmask = 0;
-    for (const G& g : g1) {
+    for (size_t gi = 0; gi < g1.size(); gi++) {
+      const G& g = g1[gi];
       const L1& k = r1[g.b].first;
       if ((k[0] & 3) != KC_ENT) continue;
       img.l2_vmask |= g.hmask;
@@ -1296,40 +1299,16 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       for (size_t i = g.b; i < g.e && !direct; i++) direct = r1[i].second != NO_POLICY;
       if (!direct) continue;
       const uint32_t row = ctx.emplace(std::array<uint32_t, 8>{k[0], k[3], k[4], k[5], k[6], SCTX_L1, 0u, 0u}, (uint32_t)ctx.size()).first->second;
-      bits.emplace_back(row, kidx(k[1], k[2]));
+      sbit.push_back({row, kidx(k[1], k[2]), (uint32_t)gi});
     }
-    for (const G& g : g2) {
+    for (size_t gi = 0; gi < g2.size(); gi++) {
+      const G& g = g2[gi];
       const L1& k = r2[g.b].first.first;
       if ((k[0] & 3) != KC_ENT) continue;
       const auto& x = r2[g.b].first.second;
       const uint32_t row = ctx.emplace(std::array<uint32_t, 8>{k[0], k[3], k[4], k[5], k[6], x[0], x[1], x[2]}, (uint32_t)ctx.size()).first->second;
-      bits.emplace_back(row, kidx(k[1], k[2]));
+      sbit.push_back({row, kidx(k[1], k[2]), (uint32_t)gi | SB_L2});
     }
-    const uint64_t words = (img.key_ents.size() + 31) / 32;
-    if (!ctx.empty() && words && (uint64_t)ctx.size() * words * 4 <= SBITS_MAX_BYTES) {
-      img.sbits_words = (uint32_t)words;
-      img.sbits.assign((size_t)ctx.size() * words, 0);
-      for (auto& b : bits) img.sbits[(size_t)b.first * words + (b.second >> 5)] |= 1u << (b.second & 31);
-      uint32_t slots = 2;
-      while (slots < 2 * ctx.size()) slots <<= 1;
-      img.sctx.assign((size_t)slots * (2 + SCTX_WORDS), 0);  // (fingerprint, row) pairs, then the slots
-      for (auto& c : ctx) {
-        const auto& x = c.first;
-        const uint32_t hash = ctx_key(key_pre(x[0], x[1], x[2], x[3], x[4]), x[5], x[6], x[7]);
-        uint32_t h = hash & (slots - 1);
-        while (img.sctx[2 * h]) h = (h + 1) & (slots - 1);
-        img.sctx[2 * h] = ctx_fp(hash);
-        img.sctx[2 * h + 1] = c.second;
-        uint32_t* e = &img.sctx[2 * (size_t)slots + (size_t)h * SCTX_WORDS];
-        e[0] = SCTX_USED | x[0];
-        for (uint32_t j = 1; j < 8; j++) e[j] = x[j];
-        e[8] = c.second;
-      }
-    }
-    if (times)
-      std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities): %.1f MB%s\n", ctx.size(),
-                   (unsigned long long)words, img.key_ents.size(), ctx.size() * words * 4 / 1e6,
-                   img.sbits_words ? "" : " (over the cap: none)");
   }
   // record heads (bucket order) then the ext area (one full record per policy)
   uint32_t n_heads = 0;
@@ -1389,18 +1368,25 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     img.bfilt[2 * blk + 1] |= (uint32_t)(need >> 32);
   };
   mark("tables");
-  for (const G& g : g1) {
+  std::vector<uint32_t> g1_first(g1.size()), g1_cnt(g1.size()), g2_first(g2.size()), g2_cnt(g2.size());
+  for (size_t gi = 0; gi < g1.size(); gi++) {
+    const G& g = g1[gi];
     const L1& k = r1[g.b].first;
     const uint32_t first = put_heads(r1.begin() + (long)g.b, r1.begin() + (long)g.e);
+    g1_first[gi] = first;
+    g1_cnt[gi] = head - first;
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], g.cmask, 0, first,
                                   head - first, g.hmask, g.bloom[0], g.bloom[1], g.bloom[2], g.bloom[3]};
     insert(l1_hash(k), e);
     filt_add(l1_hash(k));
   }
-  for (const G& g : g2) {
+  for (size_t gi = 0; gi < g2.size(); gi++) {
+    const G& g = g2[gi];
     const L1& k = r2[g.b].first.first;
     const auto& x = r2[g.b].first.second;
     const uint32_t first = put_heads(r2.begin() + (long)g.b, r2.begin() + (long)g.e);
+    g2_first[gi] = first;
+    g2_cnt[gi] = head - first;
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16) | BT_L2 | x[0], k[1], k[2], k[3], k[4], k[5], k[6], x[1], x[2],
                                   first, head - first, 0, 0, 0, 0, 0};
     insert(bucket_hash2(l1_hash(k), x[0], x[1], x[2]), e);
@@ -1408,6 +1394,48 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   }
   if (img.btab.empty()) img.btab.assign(BT_WORDS, 0);  // never empty buffers
   mark("heads+slots");
+  // the bitset rows as (bits, rank) word pairs, every set bit's bucket at its rank, and the context
+  // table (image.h "scope bitsets")
+  const uint64_t words = (img.key_ents.size() + 31) / 32;
+  // (a listed key carries its bit's rank in 26 bits: cedar_scan_kernel)
+  if (!ctx.empty() && words && (uint64_t)ctx.size() * words * 8 <= SBITS_MAX_BYTES && sbit.size() < (1u << 26)) {
+    img.sbits_words = (uint32_t)words;
+    std::vector<uint32_t> bitw((size_t)ctx.size() * words, 0);
+    for (auto& b : sbit) bitw[(size_t)b.row * words + (b.kidx >> 5)] |= 1u << (b.kidx & 31);
+    img.sbits.assign(2 * bitw.size(), 0);
+    uint32_t rank = 0;
+    for (size_t w = 0; w < bitw.size(); w++) {
+      img.sbits[2 * w] = bitw[w];
+      img.sbits[2 * w + 1] = rank;
+      rank += (uint32_t)__builtin_popcount(bitw[w]);
+    }
+    img.svals.assign(2 * (size_t)std::max<uint32_t>(rank, 1u), 0);
+    for (auto& b : sbit) {
+      const size_t w = (size_t)b.row * words + (b.kidx >> 5);
+      const uint32_t r = img.sbits[2 * w + 1] + (uint32_t)__builtin_popcount(bitw[w] & ((1u << (b.kidx & 31)) - 1u));
+      const bool l2 = (b.grp & SB_L2) != 0;
+      const uint32_t gi = b.grp & ~SB_L2;
+      img.svals[2 * (size_t)r] = l2 ? g2_first[gi] : g1_first[gi];
+      img.svals[2 * (size_t)r + 1] = l2 ? g2_cnt[gi] : g1_cnt[gi];
+    }
+    uint32_t slots = 2;
+    while (slots < 2 * ctx.size()) slots <<= 1;
+    img.sctx.assign((size_t)slots * SCTX_WORDS, 0);
+    for (auto& c : ctx) {
+      const auto& x = c.first;
+      uint32_t h = ctx_key(key_pre(x[0], x[1], x[2], x[3], x[4]), x[5], x[6], x[7]) & (slots - 1);
+      while (img.sctx[(size_t)h * SCTX_WORDS]) h = (h + 1) & (slots - 1);
+      uint32_t* e = &img.sctx[(size_t)h * SCTX_WORDS];
+      e[0] = ctx_w0(x[0], x[5]);
+      e[1] = x[1]; e[2] = x[2]; e[3] = x[3]; e[4] = x[4]; e[5] = x[6]; e[6] = x[7];
+      e[7] = c.second;
+    }
+  }
+  if (times)
+    std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities, %zu set bits): %.1f MB%s\n", ctx.size(),
+                 (unsigned long long)words, img.key_ents.size(), sbit.size(), ctx.size() * words * 8 / 1e6,
+                 img.sbits_words ? "" : " (over the cap: none)");
+  mark("bitsets");
 }
 
 // Parses every document of the tiers, through the cache when one is given (unseen documents on
@@ -1937,7 +1965,7 @@ void Image::write_blob(void* wp) const {
   auto words = [](const std::vector<uint32_t>& v) { return std::make_pair((const void*)v.data(), v.size() * 4); };
   const std::pair<const void*, size_t> sec[DS_COUNT] = {
       words(pstream), words(tier_cend), words(chunks), words(cpool), words(gstr_off), words(hot), words(act),
-      words(btab), words(bfilt), words(bstream), words(srows), words(shash), words(sctx), words(sbits),
+      words(btab), words(bfilt), words(bstream), words(srows), words(shash), words(sctx), words(sbits), words(svals),
       std::make_pair((const void*)gstr_bytes.data(), gstr_bytes.size())};
   w.align(DS_ALIGN);
   const size_t begin = w.n;
@@ -2010,7 +2038,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   sec_words(DS_CPOOL, img->cpool); sec_words(DS_GSTR_OFF, img->gstr_off); sec_words(DS_HOT, img->hot);
   sec_words(DS_ACT, img->act); sec_words(DS_BTAB, img->btab); sec_words(DS_BFILT, img->bfilt);
   sec_words(DS_BSTREAM, img->bstream); sec_words(DS_SROWS, img->srows); sec_words(DS_SHASH, img->shash);
-  sec_words(DS_SCTX, img->sctx); sec_words(DS_SBITS, img->sbits);
+  sec_words(DS_SCTX, img->sctx); sec_words(DS_SBITS, img->sbits); sec_words(DS_SVALS, img->svals);
   {
     const uint64_t off = img->dev_off[DS_GSTR_BYTES], len = img->dev_len[DS_GSTR_BYTES];
     if (off % DS_ALIGN || off < img->dev_begin || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
@@ -2037,23 +2065,27 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   }
   if (img->lane_need > LANE_MAX) throw CedarError("corrupt image (lane scratch)");
   {
-    const size_t nc = img->sctx.size() / (2 + SCTX_WORDS);
-    if (!nc || (nc & (nc - 1)) || img->sctx.size() % (2 + SCTX_WORDS) ||
-        (img->sbits_words && img->sbits.size() % img->sbits_words))
+    const size_t nc = img->sctx.size() / SCTX_WORDS;
+    if (!nc || (nc & (nc - 1)) || img->sctx.size() % SCTX_WORDS || img->sbits.size() % 2 ||
+        (img->sbits_words && (img->sbits.size() / 2) % img->sbits_words) || img->svals.size() < 2 || img->svals.size() % 2)
       throw CedarError("corrupt image (scope bitsets)");
-    // every context row in range, fingerprints exactly on the used slots, and a free slot that
-    // ends every probe chain
+    // every context row in range, a free slot that ends every probe chain, and ranks that number
+    // every set bit within svals
     size_t used = 0;
-    const size_t rows = img->sbits_words ? img->sbits.size() / img->sbits_words : 0;
+    const size_t rows = img->sbits_words ? img->sbits.size() / 2 / img->sbits_words : 0;
     for (size_t k = 0; k < nc; k++) {
-      const uint32_t* e = &img->sctx[2 * nc + k * SCTX_WORDS];
-      if ((img->sctx[2 * k] != 0) != (e[0] != 0)) throw CedarError("corrupt image (scope bitsets)");
-      if (e[0]) {
-        used++;
-        if (e[8] >= rows || img->sctx[2 * k + 1] != e[8]) throw CedarError("corrupt image (scope bitsets)");
-      }
+      const uint32_t* e = &img->sctx[k * SCTX_WORDS];
+      if (!e[0]) continue;
+      used++;
+      if (!(e[0] & SCTX_USED) || e[7] >= rows) throw CedarError("corrupt image (scope bitsets)");
     }
     if (used >= nc) throw CedarError("corrupt image (scope bitsets)");
+    uint32_t rank = 0;
+    for (size_t w = 0; w < img->sbits.size() / 2; w++) {
+      if (img->sbits[2 * w + 1] != rank) throw CedarError("corrupt image (scope bitsets)");
+      rank += (uint32_t)__builtin_popcount(img->sbits[2 * w]);
+    }
+    if ((size_t)rank * 2 > img->svals.size()) throw CedarError("corrupt image (scope bitsets)");
   }
   {
     const size_t ns = img->shash.size() / SH_WORDS;

@@ -54,7 +54,7 @@ struct Image {
   // encoder lists a request's ancestors that are among them first (image.h RW_PN)
   std::vector<uint64_t> key_ents;
   // scope bitsets (image.h "scope bitsets"): context table and one row of sbits_words per context
-  std::vector<uint32_t> sctx, sbits;
+  std::vector<uint32_t> sctx, sbits, svals;  // sbits: (bits, rank) per word; svals: (first, count) per set bit
   uint32_t sbits_words = 0;
   uint32_t l2_vmask = 0, l2_lmask = 0;  // hot slots with level-2 value keys / list keys under entity-principal combos
   // index of `uid` in key_ents, KIDX_NONE when it is no key entity

@@ -205,19 +205,21 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 //   level 2: context (combo, action, resource, hot slot h (| BT_CKEY for list keys), v0, v1); the
 //            bit is set when that level-2 key exists.
 // Each context in use has a row of sbits_words words, one bit per key entity (index into
-// Image::key_ents, "kidx"). sctx: an open-addressed table of S slots (S a power of two) at
-// ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1) & (S - 1): first S (fingerprint, row) word
-// pairs (ctx_fp of the key's hash, 0 = empty; a few tens of KB: the device's lookup reads only
-// these, see cedar_scan_kernel), then S full slots of SCTX_WORDS [SCTX_USED | combo, at, ai, rt,
-// ri, hs, v0, v1, row, 0, 0, 0] (the host's validation and diagnostics). A request looks up its contexts (per entity-
-// principal combo: level 1, each value slot of l2_vmask with its own value, each element of its
-// list slots in l2_lmask) and tests one bit per principal key ancestor in each context found (the
-// encoder lists their kidx after the ancestor pairs: [n, (type, id) x n, kidx(self), kidx x keys],
-// kidx ~0 for a UID that is no key entity); only keys whose bit is set are probed, once each, with
-// no level-2 descent. On C3 that is ~6 probes of 64-byte slots per request instead of ~62 level-1
-// probes and their level-2 follow-ups; the grouped requests of a wave share the rows.
-// Images whose bitsets would exceed SBITS_MAX_BYTES have none (sbits_words == 0).
-constexpr uint32_t SCTX_WORDS = 12, SCTX_USED = 0x80000000u, SCTX_L1 = 0xFFFFu, KIDX_NONE = 0xFFFFFFFFu;
+// Image::key_ents, "kidx"), stored as (bits, rank) word pairs: rank = the set bits of every earlier
+// word of every row, so a set bit's global rank is rank + popcount of the word's lower bits. svals
+// holds each set bit's bucket at its rank: (first head, head count) of the key's own scope-index
+// entry, what a probe of that key in btab would return. sctx: an open-addressed table of S slots (S
+// a power of two) at ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1) & (S - 1), SCTX_WORDS
+// each: [SCTX_USED | combo << 16 | hs, at, ai, rt, ri, v0, v1, row] (0 = empty; 32 bytes, one
+// round trip, compared whole). A request looks up its contexts (per entity-principal combo: level
+// 1, each value slot of l2_vmask with its own value, each element of its list slots in l2_lmask)
+// and tests one bit per principal key ancestor in each context found (the encoder lists their kidx
+// after the ancestor pairs: [n, (type, id) x n, kidx(self), kidx x keys], kidx ~0 for a UID that is
+// no key entity); every set bit is a found bucket, read from svals at its rank: no key hash and no
+// btab probe. On C3 that is ~8 bucket reads from a ~0.1 MB table per request instead of ~62
+// level-1 probes of 64-byte slots and their level-2 follow-ups; the grouped requests of a wave
+// share the rows. Images whose bitsets would exceed SBITS_MAX_BYTES have none (sbits_words == 0).
+constexpr uint32_t SCTX_WORDS = 8, SCTX_USED = 0x80000000u, SCTX_L1 = 0xFFFFu, KIDX_NONE = 0xFFFFFFFFu;
 constexpr uint64_t SBITS_MAX_BYTES = 64ull << 20;
 __host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {
   pre ^= pre >> 16;
@@ -228,7 +230,7 @@ __host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {
 __host__ __device__ constexpr inline uint32_t ctx_key(uint32_t pre, uint32_t hs, uint32_t v0, uint32_t v1) {
   return ctx_hash(pre ^ ((hs + 1) * 0x27D4EB2Fu) ^ (v0 * 0x165667B1u) ^ (v1 * 0xD3A2646Cu));
 }
-__host__ __device__ constexpr inline uint32_t ctx_fp(uint32_t hash) { return hash | 1u; }  // never 0
+__host__ __device__ constexpr inline uint32_t ctx_w0(uint32_t combo, uint32_t hs) { return SCTX_USED | (combo << 16) | (hs & 0xFFFFu); }
 
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
 __host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_t ei) {
@@ -444,14 +446,14 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 12;
+constexpr uint32_t IMG_VERSION = 13;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob
 // itself when a collective delivered it to device memory), with each array at its blob offset.
 enum DevSection : uint32_t {
   DS_PSTREAM, DS_TIER_CEND, DS_CHUNKS, DS_CPOOL, DS_GSTR_OFF, DS_HOT, DS_ACT, DS_BTAB, DS_BFILT, DS_BSTREAM,
-  DS_SROWS, DS_SHASH, DS_SCTX, DS_SBITS, DS_GSTR_BYTES, DS_COUNT
+  DS_SROWS, DS_SHASH, DS_SCTX, DS_SBITS, DS_SVALS, DS_GSTR_BYTES, DS_COUNT
 };
 constexpr uint32_t DS_ALIGN = 256;
 
