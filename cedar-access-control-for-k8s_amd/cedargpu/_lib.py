@@ -121,6 +121,7 @@ _SIGS = {
                                            ctypes.POINTER(u32), ctypes.POINTER(i64)]),
     "cg_encode_items_check": (ctypes.c_int, [P, sz, cstr, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
                                              ctypes.POINTER(i64)]),
+    "cg_json_split_check": (ctypes.c_int, [cstr, sz, u32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_int)]),
     "cg_batch_add_admission_json": (ctypes.c_int, [P, cstr, sz]),
     "cg_batch_admit": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), P, sz,
                                       ctypes.POINTER(sz)]),

@@ -1,5 +1,6 @@
 // C-ABI implementation (include/cedargpu.h). No exception crosses this boundary.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cctype>
 #include <cstdio>
@@ -55,38 +56,191 @@ struct cg_compiler {
 namespace {
 
 // Element texts of a top-level JSON array (bracket / string balance only; each element is parsed
-// on its own afterwards). False when the text is not an array.
-bool split_array(const char* p, size_t n, std::vector<std::pair<size_t, size_t>>& out) {
+// on its own afterwards). False when the text is not an array. One pass: string bodies are skipped
+// with memchr (most of a SubjectAccessReview's bytes), everything else through a byte-class table.
+bool split_array_serial(const char* p, size_t n, std::vector<std::pair<size_t, size_t>>& out) {
+  enum : uint8_t { C_OTHER = 0, C_WS, C_QUOTE, C_OPEN, C_CLOSE, C_COMMA };
+  static const auto cls = [] {
+    std::array<uint8_t, 256> t{};
+    t[' '] = t['\t'] = t['\n'] = t['\r'] = t['\f'] = t['\v'] = C_WS;
+    t['"'] = C_QUOTE;
+    t['['] = t['{'] = C_OPEN;
+    t[']'] = t['}'] = C_CLOSE;
+    t[','] = C_COMMA;
+    return t;
+  }();
+  const unsigned char* u = reinterpret_cast<const unsigned char*>(p);
   size_t i = 0;
-  while (i < n && std::isspace((unsigned char)p[i])) i++;
+  while (i < n && cls[u[i]] == C_WS) i++;
   if (i == n || p[i] != '[') return false;
   i++;
+  out.reserve(out.size() + n / 256);
   int depth = 0;
   size_t start = std::string::npos;
-  for (; i < n; i++) {
-    const char ch = p[i];
-    if (ch == '"') {
-      if (start == std::string::npos) start = i;
-      for (i++; i < n && p[i] != '"'; i++)
-        if (p[i] == '\\') i++;
-      continue;
-    }
-    if (std::isspace((unsigned char)ch)) continue;
-    if (start == std::string::npos && ch != ',' && !(depth == 0 && ch == ']')) start = i;
-    if (ch == '[' || ch == '{') depth++;
-    else if (ch == ']' || ch == '}') {
-      if (depth == 0) {  // end of the top-level array
-        if (start != std::string::npos) out.emplace_back(start, i - start);
-        return true;
+  while (i < n) {
+    switch (cls[u[i]]) {
+      case C_WS:
+        i++;
+        continue;
+      case C_QUOTE: {
+        if (start == std::string::npos) start = i;
+        size_t j = i + 1;
+        for (;;) {  // the closing quote: one not preceded by an odd run of backslashes
+          const void* q = std::memchr(p + j, '"', n - j);
+          if (!q) return false;
+          j = (size_t)((const char*)q - p);
+          size_t bs = 0;
+          while (j - bs > i + 1 && p[j - 1 - bs] == '\\') bs++;
+          if (!(bs & 1)) break;
+          j++;
+        }
+        i = j + 1;
+        continue;
       }
-      depth--;
-    } else if (ch == ',' && depth == 0) {
-      if (start == std::string::npos) return false;
-      out.emplace_back(start, i - start);
-      start = std::string::npos;
+      case C_OPEN:
+        if (start == std::string::npos) start = i;
+        depth++;
+        break;
+      case C_CLOSE:
+        if (depth == 0) {  // end of the top-level array
+          if (start != std::string::npos) out.emplace_back(start, i - start);
+          return true;
+        }
+        depth--;
+        break;
+      case C_COMMA:
+        if (depth == 0) {
+          if (start == std::string::npos) return false;
+          out.emplace_back(start, i - start);
+          start = std::string::npos;
+        }
+        break;
+      default:
+        if (start == std::string::npos) start = i;
+        break;
     }
+    i++;
   }
   return false;
+}
+
+// The same over a large text on several threads. A quote is unescaped when an even run of
+// backslashes precedes it, which each thread sees in the bytes themselves, so its region's quote
+// parity and its bracket-depth change (for both string states at its start) need no neighbour;
+// prefix sums over the regions then give each region's starting state, and a second pass lists the
+// elements that start in each region. Falls back to the serial scan on anything unusual.
+bool split_array_regions(const char* p, size_t n, std::vector<std::pair<size_t, size_t>>& out, unsigned T);
+bool split_array(const char* p, size_t n, std::vector<std::pair<size_t, size_t>>& out) {
+  unsigned T = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (const char* e = std::getenv("CEDARGPU_HOST_THREADS")) T = (unsigned)std::max(1, std::atoi(e));
+  if (n < (8u << 20) || T < 2) return split_array_serial(p, n, out);
+  return split_array_regions(p, n, out, T);
+}
+bool split_array_regions(const char* p, size_t n, std::vector<std::pair<size_t, size_t>>& out, unsigned T) {
+  T = (unsigned)std::max<size_t>(1, std::min<size_t>(T, n / 2 + 1));
+  size_t lo = 0;
+  while (lo < n && std::isspace((unsigned char)p[lo])) lo++;
+  if (lo == n || p[lo] != '[') return false;
+  lo++;
+  auto unescaped = [&](size_t j) {  // p[j] == '"' and not escaped
+    size_t bs = 0;
+    while (j - bs > 0 && p[j - 1 - bs] == '\\') bs++;
+    return !(bs & 1);
+  };
+  struct Reg {
+    size_t b, e;
+    uint64_t quotes = 0;           // unescaped quotes in the region
+    int64_t depth[2] = {0, 0};     // depth change starting outside / inside a string
+    bool in = false;               // the string state at its start (from the prefix)
+    int64_t d0 = 0;                // the depth at its start
+    std::vector<std::pair<size_t, size_t>> el;
+    size_t open = std::string::npos;  // an element still open at the region's end (its start)
+    bool bad = false, done = false;
+  };
+  std::vector<Reg> rg(T);
+  for (unsigned t = 0; t < T; t++) { rg[t].b = lo + (n - lo) * t / T; rg[t].e = lo + (n - lo) * (t + 1) / T; }
+  auto par = [&](auto&& fn) {
+    std::vector<std::thread> ws;
+    for (unsigned t = 1; t < T; t++) ws.emplace_back(fn, t);
+    fn(0u);
+    for (auto& w : ws) w.join();
+  };
+  // pass 1, one sweep: the two string states at a region's start stay complementary at every byte
+  // (the same quotes toggle both), so a bracket counts towards the state it is outside of
+  par([&](unsigned t) {
+    Reg& r = rg[t];
+    const unsigned char* u = reinterpret_cast<const unsigned char*>(p);
+    bool in = false;  // (starting outside)
+    int64_t d[2] = {0, 0};
+    uint64_t q = 0;
+    for (size_t i = r.b; i < r.e; i++) {
+      const unsigned char c = u[i];
+      if (c == '"') {
+        if (unescaped(i)) { in = !in; q++; }
+        continue;
+      }
+      const int delta = (c == '[' || c == '{') ? 1 : (c == ']' || c == '}') ? -1 : 0;
+      if (delta) d[in ? 1 : 0] += delta;
+    }
+    r.depth[0] = d[0];
+    r.depth[1] = d[1];
+    r.quotes = q;
+  });
+  bool in = false;
+  int64_t d = 0;
+  for (auto& r : rg) {
+    r.in = in;
+    r.d0 = d;
+    d += r.depth[in ? 1 : 0];
+    if (r.quotes & 1) in = !in;
+  }
+  // second pass: the separators at the array's own level (depth 0, outside strings): its commas,
+  // and its closing bracket (in the first region that reaches it)
+  par([&](unsigned t) {
+    Reg& r = rg[t];
+    bool in2 = r.in;
+    int64_t dd = r.d0;
+    for (size_t i = r.b; i < r.e; i++) {
+      if (in2) {  // to the closing quote, at memchr speed
+        const void* qp = std::memchr(p + i, '"', r.e - i);
+        if (!qp) break;
+        i = (size_t)((const char*)qp - p);
+        if (unescaped(i)) in2 = false;
+        continue;
+      }
+      const char c = p[i];
+      if (c == '"') { if (unescaped(i)) in2 = true; continue; }
+      if (c == '[' || c == '{') { dd++; continue; }
+      if (c == ']' || c == '}') {
+        if (dd == 0) { r.el.emplace_back(i, 1); r.done = true; return; }  // the array's end
+        dd--;
+        continue;
+      }
+      if (c == ',' && dd == 0) r.el.emplace_back(i, 0);
+    }
+    if (dd < 0) r.bad = true;
+  });
+  // elements between consecutive separators, as the serial scan cuts them: from the first
+  // non-space byte after a separator up to the next separator; an empty one before a comma is an
+  // error, an empty one before the closing bracket ends the array
+  size_t prev = lo - 1;  // the '['
+  bool ended = false;
+  for (unsigned t = 0; t < T && !ended; t++) {
+    const Reg& r = rg[t];
+    if (r.bad) { out.clear(); return split_array_serial(p, n, out); }
+    for (const auto& sp : r.el) {
+      size_t st = prev + 1;
+      while (st < sp.first && std::isspace((unsigned char)p[st])) st++;
+      if (st == sp.first) {
+        if (!sp.second) return false;  // `[,` or `,,`
+      } else {
+        out.emplace_back(st, sp.first - st);
+      }
+      prev = sp.first;
+      if (sp.second) { ended = true; break; }
+    }
+  }
+  return ended;
 }
 
 // Worker threads for host-side bulk work: at most 16 (a GPU's share of host cores), and one per
@@ -169,7 +323,8 @@ void group_requests(cg_batch* b) {
     for (uint32_t i = 0; i < n; i++) tmp[cnt[(key[i] >> sh) & 2047u]++] = key[i];
     key.swap(tmp);
   }
-  std::vector<uint32_t> rows((size_t)n * rw), base(n), slot(n), gk(h.gkeys.size());
+  PodVec<uint32_t> rows((size_t)n * rw), base(n), gk(h.gkeys.size());
+  std::vector<uint32_t> slot(n);
   parallel_for(n, [&](size_t s) {
     const uint32_t o = (uint32_t)(key[s] & imask);
     std::memcpy(rows.data() + s * rw, h.rows.data() + (size_t)o * rw, (size_t)rw * 4);
@@ -213,6 +368,7 @@ struct BulkOut {
 };
 template <class F>  // f(element k, EncodedRequest& e, BulkOut& o): encodes e, or sets o.host
 int bulk_add(cg_batch* b, size_t n, F&& f) {
+  LatTrace tr("bulk");
   const unsigned t = host_workers(n);
   const size_t per = std::max<size_t>(256, (n + 8 * (size_t)t - 1) / (8 * (size_t)t));
   const size_t nc = (n + per - 1) / per;
@@ -259,6 +415,7 @@ int bulk_add(cg_batch* b, size_t n, F&& f) {
     work();
     for (auto& w : ws) w.join();
   }
+  tr.mark("encode");
   for (auto& c : ch)  // chunks are contiguous and stop at their first failure: the first one in order
     if (c.rc) { b->err = c.err; return c.rc; }
   GUARD(b->err, {
@@ -275,7 +432,9 @@ int bulk_add(cg_batch* b, size_t n, F&& f) {
       parts.push_back(std::move(c.part));
     }
     ch.clear();
+    tr.mark("items");
     b->host.concat(parts, t);
+    tr.mark("concat");
     return CG_OK;
   })
 }
@@ -755,7 +914,9 @@ int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len) {
   if (!b || !json) return CG_E_ARG;
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
   std::vector<std::pair<size_t, size_t>> elems;
+  LatTrace tr("split");
   if (len >= 65536 && split_array(json, len, elems) && host_workers(elems.size()) > 1) {
+    tr.mark("split");
     // bulk: parse, convert and encode elements on worker threads into per-chunk parts (bulk_add)
     const Image& img = *b->host.img;
     return bulk_add(b, elems.size(), [&](size_t k, EncodedRequest& e, BulkOut& o) {
@@ -859,6 +1020,21 @@ int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t 
   if (!image || !sars) return CG_E_ARG;
   std::string err;
   GUARD(err, { return encode_sar_check(image, len, sars, n, n_items, n_direct, n_mismatch, first_mismatch); })
+}
+
+int cg_json_split_check(const char* json, size_t n, uint32_t threads, int64_t* n_elems, int* same) {
+  if (!json || !n_elems || !same) return CG_E_ARG;
+  std::vector<std::pair<size_t, size_t>> a, b;
+  const bool ra = split_array_serial(json, n, a);
+  bool rb;
+  {
+    // the parallel split on `threads` regions whatever the size (CEDARGPU_HOST_THREADS and the
+    // 8 MiB floor are bypassed for the check)
+    rb = split_array_regions(json, n, b, std::max(2u, threads));
+  }
+  *n_elems = ra ? (int64_t)a.size() : -1;
+  *same = (ra == rb) && (!ra || a == b);
+  return CG_OK;
 }
 
 int cg_encode_items_check(const void* image, size_t len, const char* items, size_t n, uint32_t* n_items,

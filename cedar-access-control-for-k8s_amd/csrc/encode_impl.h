@@ -10,6 +10,9 @@
 //     (emit the context / entity attributes record into `out` exactly as emit_heap_value does)
 #pragma once
 #include <algorithm>
+#include <mutex>
+#include <memory>
+#include <atomic>
 #include <cstdlib>
 #include <string_view>
 #include <unordered_map>
@@ -20,6 +23,7 @@
 namespace cg {
 
 uint32_t request_sid(const Image& img, EncodedRequest& e, std::string_view s);
+uint64_t list_hash(const uint32_t* w, uint32_t n);  // an ancestor-list record's content hash (encoder.cpp)
 
 namespace enc {
 using namespace cgi;
@@ -141,36 +145,50 @@ inline uint32_t make_record(const Image& img, uint64_t owner, std::vector<uint64
   return keys;
 }
 
-// Per-thread cache of ancestor-list records for the common request shape (a SubjectAccessReview's
+}  // namespace enc
+
+// Per-image cache of ancestor-list records for the common request shape (a SubjectAccessReview's
 // user with its groups, over a static group hierarchy): a table entity without request-given
 // parents has its static closure row as ancestry (or none), and an entity whose request-given
 // parents have none of their own has the union of its parents' closures. Both are pure functions of
-// the image and, for the latter, of (entity, merged parent list), so a thread computes each once
-// per image instead of walking the hierarchy for every request.
-struct ClosureCache {
-  uint64_t img_id = 0;
-  std::vector<std::vector<uint32_t>> srec;  // static row -> record (empty: not built yet)
-  std::vector<uint32_t> skeys;
+// the image and, for the latter, of (entity, merged parent list), so every encoding thread shares
+// one computation of each: static rows are published once (compare-and-swap), the rest live in a
+// sharded map under per-shard locks. The image holds the cache (Image::enc_cache).
+struct EncCache {
+  struct Rec {
+    std::vector<uint32_t> words;
+    uint32_t keys = 0;
+    uint64_t hash = 0;  // list_hash(words): Batch::append interns the record without rehashing it
+  };
+  std::unique_ptr<std::atomic<const Rec*>[]> srec;  // static row -> record (null: not built yet)
+  size_t n_static = 0;
   struct Ent {
     uint64_t uid = 0;
     std::vector<uint64_t> parents;
-    std::vector<uint32_t> rec;
-    uint32_t keys = 0;
+    Rec rec;
   };
-  std::unordered_map<uint64_t, Ent> ents;  // by hash of (uid, parents)
-  static constexpr size_t MAX_ENTS = 1u << 16;
-  void bind(const Image& img) {
-    if (img_id == img.cache_id && img_id) return;
-    img_id = img.cache_id;
-    srec.assign(img.n_static(), {});
-    skeys.assign(img.n_static(), 0);
-    ents.clear();
+  static constexpr uint32_t SHARDS = 64;
+  static constexpr size_t MAX_PER_SHARD = 4096;
+  struct alignas(64) Shard {
+    std::mutex mu;
+    std::unordered_map<uint64_t, Ent> map;  // by hash of (uid, parents)
+  } shards[SHARDS];
+  explicit EncCache(size_t ns) : srec(new std::atomic<const Rec*>[ns ? ns : 1]), n_static(ns) {
+    for (size_t i = 0; i < ns; i++) srec[i].store(nullptr, std::memory_order_relaxed);
+  }
+  ~EncCache() {
+    for (size_t i = 0; i < n_static; i++) delete srec[i].load();
   }
 };
-inline ClosureCache& closure_cache() {
-  thread_local ClosureCache c;
-  return c;
+inline EncCache& enc_cache(const Image& img) {
+  std::shared_ptr<EncCache> p = std::atomic_load(&img.enc_cache);
+  if (!p) {
+    auto n = std::make_shared<EncCache>(img.n_static());
+    if (std::atomic_compare_exchange_strong(&img.enc_cache, &p, n)) p = n;  // (else p: the winner's)
+  }
+  return *p;  // (the image keeps it alive)
 }
+namespace enc {
 // set on a thread to encode with the general walk only (cg_encode_sar_check compares the two)
 inline thread_local bool t_no_closure_cache = false;
 inline bool closure_cache_on() {
@@ -307,22 +325,20 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     }
     return (uint32_t)E.anc_at.size() - 1;
   };
-  auto put_words = [&](const std::vector<uint32_t>& w) {
+  auto put_words = [&](const EncCache::Rec& r) {
+    E.anc_hash.resize(E.anc_at.size(), 0);
+    E.anc_hash.push_back(r.hash);
     E.anc_at.push_back((uint32_t)al.size());
-    al.insert(al.end(), w.begin(), w.end());
+    al.insert(al.end(), r.words.begin(), r.words.end());
     return (uint32_t)E.anc_at.size() - 1;
   };
-  // The closure cache (ClosureCache) applies when no table entity with request-given parents is the
+  // The closure cache (EncCache) applies when no table entity with request-given parents is the
   // target of a static edge: then no static path leads back into the request's own edges.
   bool shortcut = closure_cache_on() && !t_no_closure_cache;
   for (uint32_t i = 0; i < n && shortcut; i++)
     if (table[i] & FROM_STATIC) shortcut = false;
     else if (has_static && src.n_parents(table[i]) && img.is_static_target(index.keys[i])) shortcut = false;
-  ClosureCache* cc = nullptr;
-  if (shortcut) {
-    cc = &closure_cache();
-    cc->bind(img);
-  }
+  EncCache* cc = shortcut ? &enc_cache(img) : nullptr;
   auto req_parents = [&](uint32_t i) { return !(table[i] & FROM_STATIC) && src.n_parents(table[i]) > 0; };
   // the record of table entity i from the cache; false: the general walk below
   auto cached = [&](uint32_t i) -> bool {
@@ -335,16 +351,21 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
         blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_list(uid, 0);
         return true;
       }
-      std::vector<uint32_t>& r = cc->srec[(size_t)s];
-      if (r.empty()) {
+      const EncCache::Rec* r = cc->srec[(size_t)s].load(std::memory_order_acquire);
+      if (!r) {
+        auto* nr = new EncCache::Rec();
         anc.clear();
         cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_ANC] & OFF_MASK, anc);
         std::sort(anc.begin(), anc.end());
         anc.erase(std::unique(anc.begin(), anc.end()), anc.end());
-        cc->skeys[(size_t)s] = make_record(img, uid, anc, r);
+        nr->keys = make_record(img, uid, anc, nr->words);
+        nr->hash = list_hash(nr->words.data(), (uint32_t)nr->words.size());
+        const EncCache::Rec* expect = nullptr;
+        if (cc->srec[(size_t)s].compare_exchange_strong(expect, nr, std::memory_order_acq_rel)) r = nr;
+        else { delete nr; r = expect; }  // another thread published the same record first
       }
-      n_key[i] = cc->skeys[(size_t)s];
-      blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(r);
+      n_key[i] = r->keys;
+      blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(*r);
       return true;
     }
     const std::vector<uint64_t>& ps = parents[i];
@@ -355,26 +376,34 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       h = (h ^ p) * 0xBF58476D1CE4E5B9ull;
       h ^= h >> 31;
     }
-    auto it = cc->ents.find(h);
-    if (it == cc->ents.end() || it->second.uid != uid || it->second.parents != ps) {
-      anc.clear();
-      for (const uint64_t p : ps) {
-        anc.push_back(p);
-        const int32_t s = has_static ? img.static_row(p) : -1;
-        if (s >= 0) cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_ANC] & OFF_MASK, anc);
+    EncCache::Shard& sh = cc->shards[(h >> 58) & (EncCache::SHARDS - 1)];
+    {
+      std::lock_guard<std::mutex> g(sh.mu);
+      auto it = sh.map.find(h);
+      if (it != sh.map.end() && it->second.uid == uid && it->second.parents == ps) {
+        n_key[i] = it->second.rec.keys;
+        blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(it->second.rec);
+        return true;
       }
-      std::sort(anc.begin(), anc.end());
-      anc.erase(std::unique(anc.begin(), anc.end()), anc.end());
-      if (cc->ents.size() >= ClosureCache::MAX_ENTS) cc->ents.clear();
-      ClosureCache::Ent& e = cc->ents[h];
-      e.uid = uid;
-      e.parents = ps;
-      e.rec.clear();
-      e.keys = make_record(img, uid, anc, e.rec);
-      it = cc->ents.find(h);
     }
-    n_key[i] = it->second.keys;
-    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(it->second.rec);
+    anc.clear();
+    for (const uint64_t p : ps) {
+      anc.push_back(p);
+      const int32_t s = has_static ? img.static_row(p) : -1;
+      if (s >= 0) cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_ANC] & OFF_MASK, anc);
+    }
+    std::sort(anc.begin(), anc.end());
+    anc.erase(std::unique(anc.begin(), anc.end()), anc.end());
+    EncCache::Ent e;
+    e.uid = uid;
+    e.parents = ps;
+    e.rec.keys = make_record(img, uid, anc, e.rec.words);
+    e.rec.hash = list_hash(e.rec.words.data(), (uint32_t)e.rec.words.size());
+    n_key[i] = e.rec.keys;
+    blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(e.rec);
+    std::lock_guard<std::mutex> g(sh.mu);
+    if (sh.map.size() >= EncCache::MAX_PER_SHARD) sh.map.clear();
+    sh.map[h] = std::move(e);
     return true;
   };
   for (uint32_t i = 0; i < n; i++) {

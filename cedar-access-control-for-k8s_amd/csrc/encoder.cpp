@@ -80,7 +80,7 @@ void Batch::append(EncodedRequest& e) {
   const uint64_t room = (uint64_t)e.anc.size() + 16;  // the block starts at most this far past a new record
   for (uint32_t k = 0; k < n_rec; k++) {
     const uint32_t s = e.anc_at[k], t = k + 1 < n_rec ? e.anc_at[k + 1] : (uint32_t)e.anc.size();
-    at[k] = intern_list(e.anc.data() + s, t - s, room);
+    at[k] = intern_list(e.anc.data() + s, t - s, room, k < e.anc_hash.size() ? e.anc_hash[k] : 0);
   }
   const uint32_t B = (uint32_t)heap.size();
   const uint32_t nent = e.blk[RH_NENT];
@@ -108,12 +108,17 @@ void Batch::append(EncodedRequest& e) {
 
 // One ancestor-list record into the heap, or the copy an earlier block appended (equal words,
 // close enough that a block starting `room` words past the heap end still reaches it).
-uint32_t Batch::intern_list(const uint32_t* w, uint32_t n, uint64_t room) {
+uint64_t list_hash(const uint32_t* w, uint32_t n) {
   uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
   for (uint32_t k = 0; k < n; k++) {
     h = (h ^ w[k]) * 0xBF58476D1CE4E5B9ull;
     h ^= h >> 29;
   }
+  return h | 1;  // (never 0: 0 means "not computed")
+}
+
+uint32_t Batch::intern_list(const uint32_t* w, uint32_t n, uint64_t room, uint64_t hash) {
+  const uint64_t h = hash ? hash : list_hash(w, n);
   anc_words += n;
   auto it = anc_memo.find(h);
   if (it != anc_memo.end()) {

@@ -21,12 +21,27 @@ namespace cg {
 // beyond, so a principal in thousands of groups encodes in time linear in its size.
 constexpr size_t DEDUP_SCAN = 32;
 
+// An allocator whose resize() leaves new elements uninitialised: a batch's large arrays are
+// written in full right after they grow (Batch::concat), so zero-filling them first would be a
+// serial pass over hundreds of MB.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U> struct rebind { using other = NoInitAlloc<U>; };
+  NoInitAlloc() = default;
+  template <class U> NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <class U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+  template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+template <class T> using PodVec = std::vector<T, NoInitAlloc<T>>;
+
 struct PolicyMeta {
   std::string id, filename;
   Position pos;
   uint32_t tier = 0;
   bool forbid = false;
 };
+
+struct EncCache;  // encode_impl.h
 
 // A compiled, immutable policy image (one per policy epoch). Device sections are the vectors
 // uploaded verbatim; the rest is host-side metadata for rendering diagnostics.
@@ -104,6 +119,8 @@ struct Image {
   std::vector<uint64_t> lookup;
   void build_lookup();
   uint64_t cache_id = 0;  // unique per build_lookup (per final image): keys the encoder's caches
+  // the encoder's ancestor-record cache (encode_impl.h EncCache), made on first use
+  mutable std::shared_ptr<EncCache> enc_cache;
   int32_t find(std::string_view s) const {
     if (lookup.empty()) {
       auto it = sid.find(std::string(s));
@@ -224,6 +241,7 @@ struct EncodedRequest {
   // RW_*ANC words name records (k, and k + 1 with 0 = none) until Batch::append interns each
   // record in the batch heap (one copy per distinct list) and points them at it.
   std::vector<uint32_t> anc, anc_at;
+  std::vector<uint64_t> anc_hash;  // per record: its content hash when known (a cached record), else 0
   // grouping key (group.hip): (action, resource type) | principal key ancestors | hot values,
   // hashed fields of the row, most significant first; the device bucket-sorts on its top bits
   uint32_t gkey = 0;
@@ -235,7 +253,7 @@ struct EncodedRequest {
   static constexpr uint32_t MEMO = 32;
   const char* memo_p[MEMO];
   uint32_t memo_len[MEMO], memo_id[MEMO], n_memo = 0;
-  void clear() { blk.clear(); row.clear(); anc.clear(); anc_at.clear(); strs.clear(); strs_ix.clear(); n_memo = 0; }
+  void clear() { blk.clear(); row.clear(); anc.clear(); anc_at.clear(); anc_hash.clear(); strs.clear(); strs_ix.clear(); n_memo = 0; }
   // words of record k / the first pair of the list a row word (k + 1) names
   const uint32_t* anc_rec(uint32_t k) const { return anc.data() + anc_at[k]; }
   const uint32_t* anc_pairs(uint32_t row_word) const { return anc_rec(row_word - 1) + 1; }
@@ -252,21 +270,21 @@ int encode_sar_direct(const Image& img, const char* json, size_t n, EncodedReque
 // Host side of a device batch: encoded request heap + string table; results after evaluation.
 struct Batch {
   std::shared_ptr<const Image> img;
-  std::vector<uint32_t> heap, req_base;
-  std::vector<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
-  std::vector<uint32_t> gkeys;  // one grouping key per request (EncodedRequest::gkey)
+  PodVec<uint32_t> heap, req_base;
+  PodVec<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
+  PodVec<uint32_t> gkeys;  // one grouping key per request (EncodedRequest::gkey)
   uint32_t row_words = 0;
   // request-local strings of every request, appended as requests arrive: string j is
   // bstr_bytes[bstr_off[j] .. bstr_off[j + 1]) (bstr_off keeps a trailing end offset)
-  std::vector<uint32_t> bstr_off{0};
-  std::vector<uint8_t> bstr_bytes;
+  PodVec<uint32_t> bstr_off{0};
+  PodVec<uint8_t> bstr_bytes;
   uint32_t n_bstr() const { return (uint32_t)bstr_off.size() - 1; }
   // Interned ancestor lists (EncodedRequest::anc): content hash -> heap offset of the copy that
   // later blocks reference (image.h "ancestor lists"). Requests of one principal share one list,
   // so a batch carries each distinct list once and grouped neighbours read the same lines.
   std::unordered_map<uint64_t, uint32_t> anc_memo;
   uint64_t anc_words = 0, anc_shared_words = 0;  // list words appended / list words served by a copy
-  uint32_t intern_list(const uint32_t* w, uint32_t n, uint64_t room);
+  uint32_t intern_list(const uint32_t* w, uint32_t n, uint64_t room, uint64_t hash = 0);
   // results
   uint32_t capr = 8, cape = 4;
   // on-device follow-up sizing (device.h FuKind), from the previous batch on the same image:

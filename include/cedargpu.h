@@ -256,6 +256,10 @@ int cg_encode_sar_check(const void* image, size_t len, const char* sars, size_t 
  * cache and with the general hierarchy walk; *n_mismatch counts items whose encodings differ. */
 int cg_encode_items_check(const void* image, size_t len, const char* items, size_t n, uint32_t* n_items,
                           uint32_t* n_mismatch, int64_t* first_mismatch);
+/* Host-only consistency check of the bulk paths' JSON array splitter: `json` split into its top-level
+ * elements by the serial scan and by the parallel one over `threads` regions; *n_elems = the element
+ * count (-1: not an array), *same = 1 when both agree exactly. */
+int cg_json_split_check(const char* json, size_t n, uint32_t threads, int64_t* n_elems, int* same);
 /* authorizer.Decision for item i (0 Deny, 1 Allow, 2 NoOpinion) and the reason string the
  * reference returns (diagnosticToReason JSON, a fast-path literal, or ""). */
 int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t cap, size_t* need);

@@ -185,3 +185,37 @@ def test_closure_cache_matches_the_hierarchy_walk():
                                          ctypes.byref(first)) == 0
         assert n.value == len(items)
         assert nm.value == 0, items[first.value]
+
+
+def _split(text: str, threads: int):
+    b = text.encode("utf-8")
+    n, same = ctypes.c_int64(), ctypes.c_int()
+    assert lib.cg_json_split_check(b, len(b), threads, ctypes.byref(n), ctypes.byref(same)) == 0
+    return n.value, same.value
+
+
+def test_parallel_array_split_matches_serial():
+    """The bulk paths split a large JSON array on several threads (capi.cpp split_array_regions:
+    quote parity per region, prefix sums, separators at the array's level). Against the serial
+    scan, element for element: strings holding brackets, commas, escaped quotes and backslash runs
+    that straddle region boundaries, nested values, scalars, whitespace, malformed arrays."""
+    r = random.Random(5)
+    pieces = ['"a,b"', '"[{"', '"}]"', '"x\\\\"', '"q\\"[,"', '"\\\\\\"}"', '{"k": [1, {"z": "]"}], "v": "\\\\"}',
+              '[1, 2, [3]]', '17', 'true', 'null', '{"s": "a\\\\\\\\"}', '{ }', '[ ]', '"\\u005b"']
+    for _ in range(300):
+        els = [r.choice(pieces) for _ in range(r.randint(0, 40))]
+        sep = r.choice([",", ", ", " ,\n", ","])
+        text = r.choice(["", " ", "\n"]) + "[" + r.choice(["", " "]) + sep.join(els) + r.choice(["", " "]) + "]"
+        for threads in (2, 3, 7, 16, 61):
+            n, same = _split(text, threads)
+            assert same == 1, (text, threads)
+            assert n == len(els)
+    for bad in ["[1,,2]", "[,1]", "[1", '["a]', "{}", "[1]]", '[1, "\\"]']:
+        for threads in (2, 5):
+            n, same = _split(bad, threads)
+            assert same == 1, (bad, threads)
+    sars = synth.random_sars(3000, seed=9, pop=synth.Population(seed=9, n_users=500, n_groups=40))
+    text = json.dumps(sars)
+    for threads in (2, 8, 16, 64):
+        n, same = _split(text, threads)
+        assert same == 1 and n == len(sars)
