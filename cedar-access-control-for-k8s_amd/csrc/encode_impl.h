@@ -196,6 +196,27 @@ inline bool closure_cache_on() {
   return on;
 }
 
+// The encoder's working lists, kept per thread so that a request costs no allocations once a
+// thread has encoded a few (each call clears them; capacities stay).
+struct Scratch {
+  std::vector<uint32_t> table, n_key, hs;
+  UidIndex index;
+  std::vector<std::vector<uint64_t>> parents;
+  std::unordered_set<uint64_t> seen_p, seen_big;
+  std::vector<uint64_t> anc, nodes, cl, sp, extended;
+  void reset() {
+    table.clear(); n_key.clear(); hs.clear();
+    index.keys.clear(); index.map.clear();
+    for (auto& p : parents) p.clear();
+    seen_p.clear(); seen_big.clear();
+    anc.clear(); nodes.clear(); cl.clear(); sp.clear(); extended.clear();
+  }
+};
+inline Scratch& scratch() {
+  thread_local Scratch s;
+  return s;
+}
+
 inline void emit_empty_record(std::vector<uint32_t>& out, uint32_t& w0, uint32_t& w1) {
   const uint32_t off = (uint32_t)out.size();
   out.push_back(0);
@@ -212,8 +233,10 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   auto sid = [&](std::string_view s) { return request_sid(img, E, s); };
   std::vector<uint32_t>& blk = E.blk;
   // entity table (EntityMap semantics: a repeated UID replaces the earlier entity)
-  std::vector<uint32_t> table;  // source entity of each table slot
-  UidIndex index;
+  Scratch& S = scratch();
+  S.reset();
+  std::vector<uint32_t>& table = S.table;  // source entity of each table slot
+  UidIndex& index = S.index;
   const uint32_t n_in = src.n_ents();
   for (uint32_t e = 0; e < n_in; e++) {
     const uint32_t t = sid(src.type(e)), id = sid(src.id(e));
@@ -228,8 +251,9 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     return std::make_pair(t, sid(u.second));
   };
   // parent adjacency (ids of parents that exist in the map are followed; absent ones are leaves)
-  std::vector<std::vector<uint64_t>> parents(table.size());
-  std::unordered_set<uint64_t> seen_p;  // a parent list past DEDUP_SCAN entries dedups by hashing
+  std::vector<std::vector<uint64_t>>& parents = S.parents;
+  if (parents.size() < table.size()) parents.resize(table.size());
+  std::unordered_set<uint64_t>& seen_p = S.seen_p;  // a parent list past DEDUP_SCAN entries dedups by hashing
   auto add_parent = [&](std::vector<uint64_t>& l, uint64_t key) {
     if (l.size() < DEDUP_SCAN) {
       if (std::find(l.begin(), l.end(), key) == l.end()) l.push_back(key);
@@ -255,7 +279,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   constexpr uint32_t FROM_STATIC = 0x80000000u;  // table slot holding static row (slot & ~FROM_STATIC)
   if (has_static) {
     const uint32_t n0 = (uint32_t)table.size();
-    std::vector<uint64_t> extended;  // table entities with parents that some static edge names
+    std::vector<uint64_t>& extended = S.extended;  // table entities with parents that some static edge names
     for (uint32_t i = 0; i < n0; i++)
       if (!parents[i].empty() && img.is_static_target(index.keys[i])) extended.push_back(index.keys[i]);
     if (!extended.empty()) {
@@ -272,13 +296,14 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
         if (!hit) continue;
         index.add(k);
         table.push_back(FROM_STATIC | s);
-        parents.emplace_back();
+        if (parents.size() < table.size()) parents.resize(table.size());  // (a cleared list from the scratch)
       }
     }
     for (uint32_t i = 0; i < table.size(); i++) {
       const int32_t s = (table[i] & FROM_STATIC) ? (int32_t)(table[i] & ~FROM_STATIC) : img.static_row(index.keys[i]);
       if (s < 0) continue;
-      std::vector<uint64_t> sp;
+      std::vector<uint64_t>& sp = S.sp;
+      sp.clear();
       cpool_uids(img, img.srows[(size_t)s * ENT_WORDS + ER_PAD], sp);
       seen_p.clear();
       for (const uint64_t p : sp) add_parent(parents[i], p);
@@ -308,9 +333,12 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     src.emit_ctx(blk, img, E, w0, w1);
     blk[RH_CTX] = w0; blk[RH_CTX + 1] = w1;
   }
-  std::vector<uint64_t> anc, nodes, cl;
-  std::vector<uint32_t> n_key(n, 0);
-  std::unordered_set<uint64_t> seen_big;
+  std::vector<uint64_t>& anc = S.anc;
+  std::vector<uint64_t>& nodes = S.nodes;
+  std::vector<uint64_t>& cl = S.cl;
+  std::vector<uint32_t>& n_key = S.n_key;
+  n_key.assign(n, 0);
+  std::unordered_set<uint64_t>& seen_big = S.seen_big;
   // one ancestor-list record (EncodedRequest::anc): the pairs of `anc` and, on an image with scope
   // bitsets, the key-entity index of its owner and of each of its `keys` leading (key-entity)
   // ancestors (image.h "scope bitsets"); returns the record's index
@@ -541,7 +569,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   // prefix keys (image.h "prefix level-2 keys"): a string's prefix hashes at the slot's lengths
   if (img.list_mask()) {
     for (uint32_t h = 0; h < nh; h++) row[RW_HDR + 2 * nh + h] = 0xFFFFFFFFu;  // no list
-    std::vector<uint32_t> hs;
+    std::vector<uint32_t>& hs = S.hs;
     for (uint32_t m = img.list_mask(); m; m &= m - 1) {
       const uint32_t h = (uint32_t)__builtin_ctz(m);
       const uint32_t w0 = row[RW_HDR + 2 * h], w1 = row[RW_HDR + 2 * h + 1], tag = w0 >> TAG_SHIFT;
