@@ -90,6 +90,10 @@ _SIGS = {
     "cg_image_load": (ctypes.c_int, [P, P, sz, u64]),
     "cg_image_load_device": (ctypes.c_int, [P, P, sz, u64, P]),
     "cg_image_load_peer": (ctypes.c_int, [P, P, u64]),
+    "cg_image_delta": (ctypes.c_int, [P, sz, P, sz, ctypes.POINTER(P), ctypes.POINTER(sz)]),
+    "cg_image_patch": (ctypes.c_int, [P, sz, P, sz, ctypes.POINTER(P), ctypes.POINTER(sz)]),
+    "cg_delta_info": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u64)] * 4),
+    "cg_image_load_delta": (ctypes.c_int, [P, u64, P, sz, u64]),
     "cg_image_activate": (ctypes.c_int, [P, u64]),
     "cg_image_active": (ctypes.c_int, [P, ctypes.POINTER(u64)]),
     "cg_image_unload": (ctypes.c_int, [P, u64]),
@@ -98,6 +102,7 @@ _SIGS = {
     "cg_comm_destroy": (None, [P]),
     "cg_comm_last_error": (cstr, [P]),
     "cg_broadcast_image": (ctypes.c_int, [P, P, ctypes.c_int, P, sz, u64, ctypes.c_int, ctypes.POINTER(sz)]),
+    "cg_broadcast_delta": (ctypes.c_int, [P, P, ctypes.c_int, u64, P, sz, u64, ctypes.c_int, ctypes.POINTER(sz)]),
     "cg_batch_create": (ctypes.c_int, [P, ctypes.POINTER(P)]),
     "cg_batch_destroy": (None, [P]),
     "cg_batch_add_json": (ctypes.c_int, [P, cstr, sz]),
@@ -136,6 +141,8 @@ _SIGS = {
                                                    ctypes.POINTER(sz)]),
     "cg_queue_dropped": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
     "cg_queue_stats": (ctypes.c_int, [P] + [ctypes.POINTER(u64)] * 5),
+    "cg_queue_metrics_get": (ctypes.c_int, [P, P, sz]),
+    "cg_metrics_latency_bounds": (ctypes.POINTER(u64), [ctypes.POINTER(u32)]),
     "cg_queue_loadgen": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), u32, u32, u64,
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u64),
                                         ctypes.POINTER(u64), ctypes.POINTER(u64)]),

@@ -77,3 +77,15 @@ class Comm:
         if rc:
             raise _err(rc, "image broadcast: " + lib.cg_comm_last_error(self._h).decode())
         return n.value
+
+    def broadcast_delta(self, ctx, base_epoch: int, delta: Optional[bytes], epoch: int, root: int = 0,
+                        activate: bool = True) -> int:
+        """Collective: root's delta image against `base_epoch` is applied on every rank's GPU as
+        `epoch` (activated only when every rank applied it). Returns the delta's size."""
+        n = ctypes.c_size_t(0)
+        buf = ctypes.cast(ctypes.c_char_p(delta), ctypes.c_void_p) if delta is not None else None
+        rc = lib.cg_broadcast_delta(ctx._h, self._h, root, base_epoch, buf, len(delta) if delta is not None else 0,
+                                    epoch, 1 if activate else 0, ctypes.byref(n))
+        if rc:
+            raise _err(rc, "delta broadcast: " + lib.cg_comm_last_error(self._h).decode())
+        return n.value

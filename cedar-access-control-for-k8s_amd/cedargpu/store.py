@@ -45,6 +45,26 @@ def device_synchronize(device: int = 0):
         raise DeviceError(rc, f"hipDeviceSynchronize failed on {device}")
 
 
+
+LAT_BOUNDS, BATCH_BUCKETS = 21, 14  # include/cedargpu.h CG_LAT_BOUNDS, CG_BATCH_BUCKETS
+
+
+class QueueMetrics(ctypes.Structure):
+    """include/cedargpu.h cg_queue_metrics."""
+    _fields_ = [
+        ("requests", ctypes.c_uint64 * 4),
+        ("latency", (ctypes.c_uint64 * (LAT_BOUNDS + 1)) * 4),
+        ("latency_sum_ns", ctypes.c_uint64 * 4),
+        ("fast", ctypes.c_uint64),
+        ("batches", ctypes.c_uint64),
+        ("batch_size", ctypes.c_uint64 * (BATCH_BUCKETS + 1)),
+        ("batch_latency", ctypes.c_uint64 * (LAT_BOUNDS + 1)),
+        ("batch_latency_sum_ns", ctypes.c_uint64),
+        ("abandoned", ctypes.c_uint64),
+        ("active_epoch", ctypes.c_uint64),
+        ("activations", ctypes.c_uint64),
+    ]
+
 class PolicyStore:
     """A policy source. `documents()` yields (kind, args) fed to the compiler."""
 
@@ -240,6 +260,41 @@ def image_stats(image: bytes) -> dict:
             "hot": u[3].value, "actions": u[4].value, "stream_words": u[5].value, "indexed": bool(ix.value)}
 
 
+def _buf(b: bytes):
+    return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p)  # the bytes' own buffer (read only)
+
+
+def image_delta(base: bytes, new: bytes) -> bytes:
+    """cg_image_delta: the delta image that turns blob `base` into blob `new` (include/cedargpu.h)."""
+    out, n = _P(), ctypes.c_size_t(0)
+    rc = lib.cg_image_delta(_buf(base), len(base), _buf(new), len(new), ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise _err(rc, "image delta failed")
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        lib.cg_free(out)
+
+
+def image_patch(base: bytes, delta: bytes) -> bytes:
+    """cg_image_patch: base + delta on the host (raises on a malformed delta or another base)."""
+    out, n = _P(), ctypes.c_size_t(0)
+    rc = lib.cg_image_patch(_buf(base), len(base), _buf(delta), len(delta), ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise _err(rc, "delta does not apply to this base")
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        lib.cg_free(out)
+
+
+def delta_info(delta: bytes) -> dict:
+    v = [ctypes.c_uint64() for _ in range(4)]
+    if lib.cg_delta_info(_buf(delta), len(delta), *(ctypes.byref(x) for x in v)):
+        raise ValueError("not a delta image")
+    return dict(zip(("base_len", "new_len", "ops", "literal_bytes"), (x.value for x in v)))
+
+
 def index_stats(image: bytes) -> dict:
     """Scope-index shape of a compiled image (cg_image_index_stats): list-keyed hot slots, key
     combos, index entries, scope-bitset contexts."""
@@ -298,6 +353,15 @@ class Context:
     def load_peer(self, src: "Context", epoch: int, activate: bool = True):
         """cg_image_load_peer: `src`'s image for `epoch`, host tables shared, device copy GPU to GPU."""
         rc = lib.cg_image_load_peer(self._h, src._h, epoch)
+        if rc:
+            raise _err(rc, self.last_error())
+        if activate:
+            self.activate(epoch)
+
+    def load_delta(self, base_epoch: int, delta: bytes, epoch: int, activate: bool = True):
+        """cg_image_load_delta: the image `delta` makes of this context's `base_epoch` image, built
+        on the GPU from the base's device copy, loaded as `epoch`."""
+        rc = lib.cg_image_load_delta(self._h, base_epoch, _buf(delta), len(delta), epoch)
         if rc:
             raise _err(rc, self.last_error())
         if activate:
@@ -564,6 +628,27 @@ class Queue:
         if lib.cg_queue_dropped(self._h, ctypes.byref(d)) == 0:
             out["dropped"] = d.value
         return out
+
+    def metrics(self) -> dict:
+        """cg_queue_metrics_get: request_total / request_duration by outcome (Deny, Allow, NoOpinion,
+        error), batch-size and batch-latency histograms, the active epoch (metrics.go:27-65)."""
+        m = QueueMetrics()
+        rc = lib.cg_queue_metrics_get(self._h, ctypes.byref(m), ctypes.sizeof(m))
+        if rc:
+            raise _err(rc, "queue metrics failed")
+        n = ctypes.c_uint32()
+        bp = lib.cg_metrics_latency_bounds(ctypes.byref(n))
+        outcomes = ("deny", "allow", "no_opinion", "error")
+        return {
+            "latency_bounds_ns": [bp[i] for i in range(n.value)],
+            "requests": {o: m.requests[i] for i, o in enumerate(outcomes)},
+            "latency": {o: list(m.latency[i]) for i, o in enumerate(outcomes)},
+            "latency_sum_ns": {o: m.latency_sum_ns[i] for i, o in enumerate(outcomes)},
+            "fast": m.fast, "batches": m.batches,
+            "batch_size": list(m.batch_size), "batch_latency": list(m.batch_latency),
+            "batch_latency_sum_ns": m.batch_latency_sum_ns,
+            "abandoned": m.abandoned, "active_epoch": m.active_epoch, "activations": m.activations,
+        }
 
     def loadgen(self, sars_json: Sequence[str], threads: int, total: int) -> dict:
         """Bench support: `threads` native threads issue `total` blocking authorize calls."""

@@ -12,6 +12,7 @@
 
 #include "admission.h"
 #include "capi_internal.h"
+#include "delta.h"
 #include "encode_impl.h"
 #include "sar.h"
 
@@ -686,7 +687,7 @@ int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* 
     if (n_atomic) *n_atomic = img->n_atomic;
     if (n_hot) *n_hot = (uint32_t)img->hot.size() / cgi::HOT_WORDS;
     if (n_actions) *n_actions = (uint32_t)img->act.size() / 2;
-    if (stream_words) *stream_words = (uint32_t)img->pstream.size();
+    if (stream_words) *stream_words = (uint32_t)(img->dev_len[cgi::DS_PSTREAM] / 4);
     return CG_OK;
   } catch (const std::exception&) {
     return CG_E_ARG;
@@ -701,8 +702,8 @@ int cg_image_index_stats(const void* image, size_t len, uint32_t* cslot_mask, ui
     if (cslot_mask) *cslot_mask = img->cslot_mask;
     if (pslot_mask) *pslot_mask = img->pslot_mask;
     if (combo_mask) *combo_mask = img->combo_mask;
-    if (entries) *entries = (uint32_t)(img->btab.size() / cgi::BT_WORDS);
-    if (contexts) *contexts = img->sbits_words ? (uint32_t)(img->sbits.size() / 2 / img->sbits_words) : 0u;
+    if (entries) *entries = (uint32_t)(img->dev_len[cgi::DS_BTAB] / 4 / cgi::BT_WORDS);
+    if (contexts) *contexts = img->sbits_words ? (uint32_t)(img->dev_len[cgi::DS_SBITS] / 8 / img->sbits_words) : 0u;
     if (sbits_words) *sbits_words = img->sbits_words;
     return CG_OK;
   } catch (const std::exception&) {
@@ -830,6 +831,106 @@ int cg_image_load_device(cg_ctx* ctx, void* dev_blob, size_t len, uint64_t epoch
   return CG_OK;
 }
 
+int cg_image_delta(const void* base, size_t base_len, const void* next, size_t next_len, uint8_t** delta, size_t* delta_len) {
+  if (!base || !next || !delta || !delta_len) return CG_E_ARG;
+  try {
+    std::vector<uint8_t> d = image_delta((const uint8_t*)base, base_len, (const uint8_t*)next, next_len);
+    uint8_t* p = (uint8_t*)std::malloc(d.size());
+    if (!p) return CG_E_ARG;
+    std::memcpy(p, d.data(), d.size());
+    *delta = p;
+    *delta_len = d.size();
+    return CG_OK;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+}
+
+int cg_image_patch(const void* base, size_t base_len, const void* delta, size_t delta_len, uint8_t** out, size_t* out_len) {
+  if (!base || !delta || !out || !out_len) return CG_E_ARG;
+  try {
+    std::vector<uint8_t> b = image_patch((const uint8_t*)base, base_len, (const uint8_t*)delta, delta_len);
+    uint8_t* p = (uint8_t*)std::malloc(std::max<size_t>(b.size(), 1));
+    if (!p) return CG_E_ARG;
+    if (!b.empty()) std::memcpy(p, b.data(), b.size());
+    *out = p;
+    *out_len = b.size();
+    return CG_OK;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+}
+
+int cg_delta_info(const void* delta, size_t len, uint64_t* base_len, uint64_t* new_len, uint64_t* ops, uint64_t* literal_bytes) {
+  if (!delta) return CG_E_ARG;
+  try {
+    const DeltaPlan p = delta_plan((const uint8_t*)delta, len);
+    if (base_len) *base_len = p.base_len;
+    if (new_len) *new_len = p.new_len;
+    if (ops) *ops = p.n_ops;
+    if (literal_bytes) *literal_bytes = p.lit_len;
+    return CG_OK;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+}
+
+int cg_image_load_delta(cg_ctx* ctx, uint64_t base_epoch, const void* delta, size_t len, uint64_t epoch) {
+  if (!ctx || !delta) return CG_E_ARG;
+  std::shared_ptr<LoadedImage> base;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    auto it = ctx->images.find(base_epoch);
+    if (it == ctx->images.end()) { ctx->err = "no image loaded for the delta's base epoch"; return CG_E_STATE; }
+    base = it->second;
+  }
+  DeltaPlan plan;
+  try {
+    plan = delta_plan((const uint8_t*)delta, len);
+  } catch (const std::exception& e) {
+    ctx->err = e.what();
+    return CG_E_ARG;
+  }
+  if (!base->dev.blob_len || plan.base_len != base->dev.blob_len) {
+    ctx->err = "delta image is for another base (length)";
+    return CG_E_ARG;
+  }
+  // the new blob, built on the GPU from the base's device blob; the host tables from a copy of it
+  void* nb = nullptr;
+  if (dev_blob_patch(ctx->device, base->dev, plan.pieces.data(), plan.pieces.size() / 3, plan.lit, plan.lit_len,
+                     plan.fix, plan.n_fix, (size_t)plan.new_len, &nb)) {
+    ctx->err = dev_last_error();
+    return CG_E_DEVICE;
+  }
+  std::shared_ptr<Image> img;
+  try {
+    std::vector<uint8_t> host(plan.new_len);
+    if (dev_to_host(ctx->device, nb, host.size(), host.data())) {
+      dev_free(ctx->device, nb);
+      ctx->err = dev_last_error();
+      return CG_E_DEVICE;
+    }
+    if (blob_sum(host.data(), host.size()) != plan.new_sum) throw CedarError("delta image does not reproduce the new image (checksum)");
+    img = Image::deserialize(host.data(), host.size());
+  } catch (const std::exception& e) {
+    dev_free(ctx->device, nb);
+    ctx->err = e.what();
+    return CG_E_ARG;
+  }
+  img->epoch = epoch;
+  auto li = std::make_shared<LoadedImage>();
+  li->host = img;
+  if (dev_image_adopt(ctx->device, *img, nb, &li->dev)) {
+    dev_free(ctx->device, nb);
+    ctx->err = dev_last_error();
+    return CG_E_DEVICE;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  li->serial = ctx->next_serial++;
+  ctx->images[epoch] = li;
+  return CG_OK;
+}
+
 int cg_image_load_peer(cg_ctx* dst, cg_ctx* src, uint64_t epoch) {
   if (!dst || !src) return CG_E_ARG;
   std::shared_ptr<LoadedImage> from;
@@ -853,6 +954,7 @@ int cg_image_activate(cg_ctx* ctx, uint64_t epoch) {
   std::lock_guard<std::mutex> g(ctx->mu);
   auto it = ctx->images.find(epoch);
   if (it == ctx->images.end()) { ctx->err = "no image loaded for epoch"; return CG_E_STATE; }
+  if (ctx->active != it->second) ctx->activations++;
   ctx->active = it->second;
   return CG_OK;
 }
@@ -915,9 +1017,10 @@ int cg_batch_add_sar_json(cg_batch* b, const char* json, size_t len) {
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
   std::vector<std::pair<size_t, size_t>> elems;
   LatTrace tr("split");
-  if (len >= 65536 && split_array(json, len, elems) && host_workers(elems.size()) > 1) {
+  if (len >= 65536 && split_array(json, len, elems)) {
     tr.mark("split");
-    // bulk: parse, convert and encode elements on worker threads into per-chunk parts (bulk_add)
+    // bulk: parse, convert and encode elements on worker threads into per-chunk parts (bulk_add;
+    // one worker too: the direct path per element, no JSON tree of the whole array)
     const Image& img = *b->host.img;
     return bulk_add(b, elems.size(), [&](size_t k, EncodedRequest& e, BulkOut& o) {
       const char* p = json + elems[k].first;
@@ -1220,11 +1323,11 @@ int cg_batch_submit(cg_batch* b) {
   // A small batch runs as one launch whose waves hold up to 1,024 hits each (device.h
   // DevBatch::small) and has no on-device follow-up: its reason lists get room for most of those
   // (within 2 MB per batch), so that a many-hit request seldom needs a host re-run.
-  // (Within 512 KB of reasons and 256 KB of errors per batch: the D2H copy carries them all; a
-  // longer list takes one of the batch's overflow slots.)
+  // (Within 512 KB of reasons and 64 KB of errors per batch: the D2H copy carries them all; a
+  // longer list takes one of the batch's overflow slots, which travel back only when taken.)
   if (b->img->host->indexed && n <= dev_small_n()) {
     b->host.capr = std::max(b->host.capr, std::min<uint32_t>(1024u, std::max<uint32_t>(32u, (uint32_t)((512u << 10) / (4ull * n)))) & ~7u);
-    b->host.cape = std::max(b->host.cape, std::min<uint32_t>(32u, std::max<uint32_t>(4u, (uint32_t)((256u << 10) / (24ull * n)))));
+    b->host.cape = std::max(b->host.cape, std::min<uint32_t>(32u, std::max<uint32_t>(2u, (uint32_t)((64u << 10) / (24ull * n)))));
   }
   if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   GUARD(b->err, { group_requests(b); })

@@ -71,6 +71,7 @@ struct cg_ctx {
   cg::CapHint hint;          // under mu
   // cg_ctx_inject_fault: submits left to fail, and the device stall before each batch (us)
   std::atomic<uint64_t> fault_errors{0}, fault_stall_us{0}, fault_kidx{0};
+  std::atomic<uint64_t> activations{0};  // cg_image_activate switches (cg_queue_metrics)
 };
 
 struct cg_batch {

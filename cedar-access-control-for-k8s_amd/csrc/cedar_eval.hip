@@ -1488,6 +1488,10 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
   return x;
 }
 
+// bucket words in LDS: first head index | key combo << EF_COMBO (the image keeps heads below 2^27)
+constexpr uint32_t EF_COMBO = 27, EF_FIRST = (1u << EF_COMBO) - 1u;
+// segments with a FLAT state region (only the 8-lane candidate pass uses it)
+constexpr uint32_t FLAT_NS(uint32_t seg) { return seg == 8 ? 8u : 1u; }
 // Per-wave LDS of the probe kernel, one region per request segment of SEG lanes.
 // SLIM (one-request waves, images of <= RANK_POL policies): no hm; a hit's kind, tier and error
 // slot ride in its hp word (SLIM_* below), so the large stage's wave takes 8,960 B of LDS.
@@ -1507,9 +1511,8 @@ struct alignas(16) SegLds {  // (16: the counting merge reads hp four words at a
   // the staged buckets live until the key loop ends, the merge's sort keys only after it: one region
   union {
     struct {
-      uint32_t efirst[NS][EC + PAD];   // found bucket: first head index
+      uint32_t efirst[NS][EC + PAD];   // found bucket: first head index | key combo << EF_COMBO
       uint32_t epre[NS][EC + PAD];     // candidate counts, then their exclusive prefix
-      uint32_t ecombo[NS][EC + PAD];   // key combo of the bucket's level-1 key
     } b;
     uint32_t hs[NS][HC + PAD];         // merge: sort keys (policy index << 12 | hit slot)
   } u;
@@ -1517,6 +1520,11 @@ struct alignas(16) SegLds {  // (16: the counting merge reads hp four words at a
   uint32_t hm[NS][SLIM ? 1 : HC + PAD];  // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
   uint32_t he[NS][XC * 4 + PAD];   // error details: code | aux << 8, k, et, ei
   uint2 hot[NS][NHOT + PAD];
+  // the candidate pass's wave-wide task pool (FLAT: SPLIT, 8-lane segments): every segment's request
+  // context, for lanes that evaluate another segment's candidates, and its running state
+  uint4 cx[FLAT_NS(SEG)][4];       // (blk, pt, pi, at), (ai, rt, ri, p_anc), (r_anc, a_anc, nanc p|r, a_nanc | self << 16), (rowo, am lo, am hi, 0)
+  uint32_t sst[FLAT_NS(SEG)][4];   // hits recorded, error details, lowest tier with a hit, flags (1: structural)
+  uint32_t sne[FLAT_NS(SEG)];      // buckets staged
 };
 
 // Slim per-request context of the probe kernel (everything wave-uniform but the pointers' data).
@@ -2111,10 +2119,30 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
                            : make_uint2(0u, 0u);
   // action masks over the image action table (`==` and `in`), resolved by the encoder
   uint64_t am = 0, as = 0;
+  uint32_t aself = 0xFFFFu;
   if (a.amask_ok) {
     am = ((uint64_t)hdr(RW_AM1) << 32) | hdr(RW_AM0);
     const uint32_t self = hdr(RW_ASELF);
     as = (valid && self < 64u) ? (1ull << self) : 0ull;
+    aself = (valid && self < 64u) ? self : 0xFFFFu;
+  }
+  // FLAT (the SPLIT candidate pass with 8-lane segments): the wave's lanes take candidates from a
+  // pool over all of its requests, so each segment's request context and running state live in LDS
+  constexpr bool FLAT = SPLIT && SEG == 8;
+  if constexpr (FLAT) {
+    // (every value here was read with the whole wave active: hdr() is a cross-lane read)
+    const uint32_t blk_off = (uint32_t)(c.blk - a.heap);
+    if (sl == 0) {
+      wl.cx[seg][0] = make_uint4(blk_off, c.pt, c.pi, c.at);
+      wl.cx[seg][1] = make_uint4(c.ai, c.rt, c.ri, c.p_anc);
+      wl.cx[seg][2] = make_uint4(c.r_anc, c.a_anc, c.p_nanc | (c.r_nanc << 16), c.a_nanc | (aself << 16));
+      wl.cx[seg][3] = make_uint4(c.rowo, (uint32_t)am, (uint32_t)(am >> 32), 0u);
+      wl.sst[seg][0] = 0u;
+      wl.sst[seg][1] = 0u;
+      wl.sst[seg][2] = a.n_tiers - 1;
+      wl.sst[seg][3] = 0u;
+      wl.sne[seg] = 0u;
+    }
   }
   wave_lds_sync();
 
@@ -2162,8 +2190,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         if (wl.u.b.epre[seg][mid] <= idx) lo = mid;
         else hi = mid;
       }
-      const uint32_t hidx = ok ? wl.u.b.efirst[seg][lo] + (idx - wl.u.b.epre[seg][lo]) : 0u;
-      const uint32_t bcombo = ok ? wl.u.b.ecombo[seg][lo] : 0u;
+      const uint32_t ef = ok ? wl.u.b.efirst[seg][lo] : 0u;
+      const uint32_t hidx = ok ? (ef & EF_FIRST) + (idx - wl.u.b.epre[seg][lo]) : 0u;
+      const uint32_t bcombo = ef >> EF_COMBO;
       const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
       const uint4* d4 = reinterpret_cast<const uint4*>(head);
       const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
@@ -2305,6 +2334,160 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     wave_lds_sync();
     if (STATS) t_cand += clock64() - t_c0;
   };
+  // The FLAT candidate pass: the wave's staged candidates (every segment's buckets, prefix-summed)
+  // form one pool, 64 a round, so a wave takes as many rounds as its whole pool needs instead of
+  // as many as its longest request does (C3: ~1 round where 8-lane segments took ~2). A lane builds
+  // its candidate's request context from LDS; hits, error details, the lowest hit tier and the
+  // structural flag go to that request's region through LDS atomics (the merge orders hits by policy,
+  // so their slots' order does not matter).
+  auto flush_flat = [&]() {
+    const uint64_t t_c0 = STATS ? clock64() : 0;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; __ballot(b0 < ne); b0 += SEG) {
+      const uint32_t b = b0 + sl;
+      const uint32_t cnt = b < ne ? wl.u.b.epre[seg][b] : 0u;
+      const uint32_t inc = sscan(cnt);
+      wave_lds_sync();
+      if (b < ne) wl.u.b.epre[seg][b] = carry + inc - cnt;
+      carry += sbcast(inc, SEG - 1);
+      wave_lds_sync();
+    }
+    // a request whose hits already overflowed takes no more candidates (the large stage redoes it)
+    const uint32_t mine = wl.sst[seg][0] > L::HC ? 0u : carry;
+    uint32_t cum[NS + 1];
+    cum[0] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NS; k++) cum[k + 1] = cum[k] + (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)(k * SEG));
+    const uint32_t W = cum[NS];
+    for (uint32_t base = 0; base < W; base += 64) {
+      const uint32_t g = base + lane;
+      bool ok = g < W;
+      uint32_t s = 0, cb = 0;
+#pragma unroll
+      for (uint32_t k = 1; k < NS; k++)
+        if (g >= cum[k]) { s = k; cb = cum[k]; }
+      const uint32_t idx = g - cb;
+      uint32_t lo = 0, hi = ok ? wl.sne[s] : 1u;  // bucket of candidate idx: last b with epre[b] <= idx
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (wl.u.b.epre[s][mid] <= idx) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t ef = ok ? wl.u.b.efirst[s][lo] : 0u;
+      const uint32_t hidx = ok ? (ef & EF_FIRST) + (idx - wl.u.b.epre[s][lo]) : 0u;
+      const uint32_t bcombo = ef >> EF_COMBO;
+      const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
+      const uint4* d4 = reinterpret_cast<const uint4*>(head);
+      const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+      // the candidate's request (segment s)
+      const uint4 x0 = wl.cx[s][0], x1 = wl.cx[s][1], x2 = wl.cx[s][2], x3 = wl.cx[s][3];
+      PCtx tc;
+      tc.blk = a.heap + x0.x;
+      tc.cpool = a.cpool;
+      tc.lh = wl.he[s];
+      tc.gstr_off = a.gstr_off;
+      tc.gstr_bytes = a.gstr_bytes;
+      tc.bstr_off = a.bstr_off;
+      tc.bstr_bytes = a.bstr_bytes;
+      tc.n_gstr = a.n_gstr;
+      tc.hotl = wl.hot[s];
+      tc.pt = x0.y; tc.pi = x0.z; tc.at = x0.w;
+      tc.ai = x1.x; tc.rt = x1.y; tc.ri = x1.z; tc.p_anc = x1.w;
+      tc.r_anc = x2.x; tc.a_anc = x2.y; tc.p_nanc = x2.z & 0xFFFFu; tc.r_nanc = x2.z >> 16; tc.a_nanc = x2.w & 0xFFFFu;
+      tc.rowb = c.rowb;
+      tc.rowo = x3.x;
+      const uint64_t tam = ((uint64_t)x3.z << 32) | x3.y;
+      const uint32_t tself = x2.w >> 16;
+      const uint64_t tas = tself < 64u ? (1ull << tself) : 0ull;
+      const uint32_t flags = q0.x, kinds = q0.y;
+      const uint32_t tier = (flags >> 8) & 0xFF;
+      ok = ok && tier <= wl.sst[s][2];
+      const uint32_t pk = kinds & 0xFF, ak = (kinds >> 8) & 0xFF, rk = (kinds >> 16) & 0xFF;
+      // scope re-check (as flush)
+      if (ak != SK_ANY) {
+        if (a.amask_ok) {
+          const uint64_t pm = ((uint64_t)q3.w << 32) | q3.z;
+          ok = ok && (((ak == SK_EQ ? tas : tam) & pm) != 0);
+        } else if (ak == SK_EQ) {
+          ok = ok && tc.at == q1.y && tc.ai == q1.z;
+        } else if (ak == SK_IN) {
+          ok = ok && anc_in(tc.blk, tc.a_anc, tc.a_nanc, tc.at, tc.ai, q1.y, q1.z);
+        } else if (((bcombo >> 2) & 1) != KC_ENT) {
+          bool any = false;
+          for (uint32_t x = 0; ok && x < q1.y && !any; x++)
+            any = anc_in(tc.blk, tc.a_anc, tc.a_nanc, tc.at, tc.ai, a.cpool[q1.z + 2 * x], a.cpool[q1.z + 2 * x + 1]);
+          ok = ok && any;
+        }
+      }
+      if (pk == SK_IS || pk == SK_ISIN) ok = ok && tc.pt == q0.z;
+      if (pk == SK_EQ) ok = ok && tc.pt == q0.w && tc.pi == q1.x;
+      else if ((pk == SK_IN || pk == SK_ISIN) && (bcombo & 3) != KC_ENT)
+        ok = ok && anc_in(tc.blk, tc.p_anc, tc.p_nanc, tc.pt, tc.pi, q0.w, q1.x);
+      if (rk == SK_IS || rk == SK_ISIN) ok = ok && tc.rt == q1.w;
+      if (rk == SK_EQ) ok = ok && tc.rt == q2.x && tc.ri == q2.y;
+      else if ((rk == SK_IN || rk == SK_ISIN) && (bcombo >> 3) != KC_ENT)
+        ok = ok && anc_in(tc.blk, tc.r_anc, tc.r_nanc, tc.rt, tc.ri, q2.x, q2.y);
+      const uint32_t na = q3.x / ATOM_WORDS;
+      const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
+      uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
+      if (STATS) { st[6] += g < W; st[7] += ok; st[11] += lane < NS; }
+      bool err = false, structural_hit = false;
+      Err e{0, 0, 0, 0, 0};
+      while (__ballot(pc < na)) {
+        if (pc < na) {
+          const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
+          const uint32_t rr = eval_atom<false>(tc, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
+          if (STATS) st[8]++;
+          if (rr == 3u) { structural_hit = true; pc = AT_UNSAT; }
+          else if (rr == 2u) { err = true; pc = AT_UNSAT; }
+          else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
+        }
+      }
+      const bool hit = ok && (err || pc == AT_SAT);
+      const uint32_t mlist = q2.w;
+      const uint32_t nmem = hit ? (mlist ? a.bstream[mlist] : 1u) : 0u;
+      if (STATS) st[9] += nmem;
+      const uint32_t pos0 = hit ? atomicAdd(&wl.sst[s][0], nmem) : 0u;
+      const uint32_t xpos = (hit && err) ? atomicAdd(&wl.sst[s][1], 1u) : 0u;
+      const uint32_t kind = err ? 2u : (flags & PF_FORBID) ? 1u : 0u;
+      const uint32_t hmv = kind | (tier << 8) | (min(xpos, 0xFFu) << 16);
+      if (hit && !mlist && pos0 < L::HC) {
+        wl.hp[s][pos0] = q2.z;
+        wl.hm[s][pos0] = hmv;
+      }
+      if (hit && mlist) {  // a duplicate class: every member, MEMB_U loads in flight
+        for (uint32_t j = 0; j < nmem && pos0 + j < L::HC; j += MEMB_U) {
+          uint32_t v[MEMB_U];
+#pragma unroll
+          for (uint32_t u = 0; u < MEMB_U; u++) v[u] = (j + u < nmem && pos0 + j + u < L::HC) ? a.bstream[mlist + 1 + j + u] : 0u;
+#pragma unroll
+          for (uint32_t u = 0; u < MEMB_U; u++)
+            if (j + u < nmem && pos0 + j + u < L::HC) {
+              wl.hp[s][pos0 + j + u] = v[u];
+              wl.hm[s][pos0 + j + u] = hmv;
+            }
+        }
+      }
+      if (hit && err && xpos < L::XC) {
+        wl.he[s][4 * xpos] = e.code | (e.aux << 8);
+        wl.he[s][4 * xpos + 1] = e.k;
+        wl.he[s][4 * xpos + 2] = e.et;
+        wl.he[s][4 * xpos + 3] = e.ei;
+      }
+      if (hit) atomicMin(&wl.sst[s][2], tier);
+      if (structural_hit) atomicOr(&wl.sst[s][3], 1u);
+      wave_lds_sync();
+    }
+    ne = 0;
+    if (STATS && sl == 0) st[10]++;
+    wave_lds_sync();
+    // this request's running state, back in its segment's registers
+    nh = wl.sst[seg][0];
+    nx = wl.sst[seg][1];
+    min_tier = wl.sst[seg][2];
+    general = wl.sst[seg][3] != 0u;
+    if (STATS) t_cand += clock64() - t_c0;
+  };
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0;
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);  // level-2 bloom of this lane's level-1 entry
@@ -2324,18 +2507,25 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     const bool skip = SEG < 64 && nb != SCAN_OVF && (nb > a.scan_big || heavy) && !a.req_idx;
     if (skip) nbk = 0;
     if (SEG < 64 && (nb == SCAN_OVF || skip)) nh = L::HC + 1;
+    if constexpr (FLAT) {
+      if (sl == 0) wl.sst[seg][0] = nh;
+      wave_lds_sync();
+    }
     const uint32_t* pairs = a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP);
     for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
       for (uint32_t i = sl; i < L::EC; i += SEG)
         if (b0 + i < nbk) {
           const uint2 q = *reinterpret_cast<const uint2*>(pairs + 2 * (b0 + i));
-          wl.u.b.efirst[seg][i] = q.x;
+          wl.u.b.efirst[seg][i] = q.x | ((q.y >> SCAN_COMBO_SHIFT) << EF_COMBO);
           wl.u.b.epre[seg][i] = q.y & SCAN_COUNT;
-          wl.u.b.ecombo[seg][i] = q.y >> SCAN_COMBO_SHIFT;
         }
       ne = b0 < nbk ? min(L::EC, nbk - b0) : 0u;
+      if constexpr (FLAT) {
+        if (sl == 0) wl.sne[seg] = ne;
+      }
       wave_lds_sync();
-      flush();
+      if constexpr (FLAT) flush_flat();
+      else flush();
       // more hits than this pass holds: the large stage redoes the request, so stop here
       if (SEG < 64 && nh > L::HC) nbk = 0;
     }
@@ -2435,9 +2625,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint64_t m = sballot(e.y != 0);
       if (e.y) {
         const uint32_t pos = ne + mbcnt64(m);
-        wl.u.b.efirst[seg][pos] = e.x;
+        wl.u.b.efirst[seg][pos] = e.x | (combo << EF_COMBO);
         wl.u.b.epre[seg][pos] = e.y;
-        wl.u.b.ecombo[seg][pos] = combo;
       }
       ne += popc64(m);
       wave_lds_sync();
@@ -2772,7 +2961,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.act = (uint32_t*)at(DS_ACT); d.btab = (uint32_t*)at(DS_BTAB); d.bfilt = (uint32_t*)at(DS_BFILT);
   d.bstream = (uint32_t*)at(DS_BSTREAM); d.srows = (uint32_t*)at(DS_SROWS); d.shash = (uint32_t*)at(DS_SHASH);
   d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS); d.svals = (uint32_t*)at(DS_SVALS);
-  d.sctx_mask = (uint32_t)(img.sctx.size() / SCTX_WORDS) - 1;
+  d.sctx_mask = (uint32_t)(img.dev_len[DS_SCTX] / 4 / SCTX_WORDS) - 1;
   d.sbits_words = img.sbits_words;
   d.n_kent = (uint32_t)img.key_ents.size();
   d.l2_vmask = img.l2_vmask;
@@ -2783,7 +2972,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.cslot_mask = img.list_mask();
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
   d.bmask = img.btab_slots - 1;
-  d.fmask = (uint32_t)(img.bfilt.size() / 2) - 1;
+  d.fmask = (uint32_t)(img.dev_len[DS_BFILT] / 8) - 1;
   d.indexed = img.indexed;
   d.combo_mask = img.combo_mask;
   d.n_act = (uint32_t)img.act.size() / 2;
@@ -2824,7 +3013,7 @@ __global__ void __launch_bounds__(256) cedar_btab_build(const uint32_t* __restri
 // Builds the image's slot table from its entry list (d.btab points at the list in the region).
 static int build_btab(const Image& img, DevImage& d) {
   const size_t bytes = (size_t)img.btab_slots * BT_WORDS * 4;
-  const uint32_t n = (uint32_t)(img.btab.size() / BT_WORDS);
+  const uint32_t n = (uint32_t)(img.dev_len[DS_BTAB] / 4 / BT_WORDS);
   hipStream_t s;
   HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   hipError_t e = hipMalloc(&d.btab_mem, bytes);
@@ -2846,18 +3035,21 @@ static int build_btab(const Image& img, DevImage& d) {
   return 0;
 }
 
+// (the whole blob: the host part rides along, ~15 % of a large image, so that a delta image can
+// be applied on the device against it)
 int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage* out) {
   HIPCHK(hipSetDevice(device), "hipSetDevice");
-  const size_t n = img.dev_end - img.dev_begin;
+  const size_t n = img.blob_len;
   void* base = nullptr;
   HIPCHK(hipMalloc(&base, std::max<size_t>(n, DS_ALIGN)), "hipMalloc image");
-  if (hipMemcpy(base, blob + img.dev_begin, n, hipMemcpyHostToDevice) != hipSuccess) {
+  if (hipMemcpy(base, blob, n, hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(base);
     g_err = "H2D image";
     return -5;
   }
   DevImage d;
-  image_fields(img, device, base, img.dev_begin, d);
+  image_fields(img, device, base, 0, d);
+  d.blob_len = n;
   if (const int rc = build_btab(img, d)) { (void)hipFree(base); return rc; }
   *out = d;
   return 0;
@@ -2865,10 +3057,13 @@ int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage
 
 int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* out) {
   HIPCHK(hipSetDevice(device), "hipSetDevice");
-  const size_t n = img.dev_end - img.dev_begin;
+  // the source's whole blob when it has it, else its region
+  const bool whole = src.blob_len != 0 && src.origin == 0;
+  const uint64_t origin = whole ? 0 : img.dev_begin;
+  const size_t n = whole ? src.blob_len : img.dev_end - img.dev_begin;
   void* base = nullptr;
   HIPCHK(hipMalloc(&base, std::max<size_t>(n, DS_ALIGN)), "hipMalloc image");
-  const uint8_t* from = (const uint8_t*)src.base + (img.dev_begin - src.origin);
+  const uint8_t* from = (const uint8_t*)src.base + (origin - src.origin);
   const hipError_t e = device == src.device ? hipMemcpy(base, from, n, hipMemcpyDeviceToDevice)
                                             : hipMemcpyPeer(base, device, from, src.device, n);
   if (e != hipSuccess) {
@@ -2876,7 +3071,8 @@ int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* 
     return fail(e, "peer copy of the image");
   }
   DevImage d;
-  image_fields(img, device, base, img.dev_begin, d);
+  image_fields(img, device, base, origin, d);
+  d.blob_len = whole ? n : 0;
   if (const int rc = build_btab(img, d)) { (void)hipFree(base); return rc; }
   *out = d;
   return 0;
@@ -2886,9 +3082,81 @@ int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out)
   HIPCHK(hipSetDevice(device), "hipSetDevice");
   DevImage d;
   image_fields(img, device, dev_blob, 0, d);
+  d.blob_len = img.blob_len;
   if (const int rc = build_btab(img, d)) return rc;  // the caller still owns dev_blob on failure
   *out = d;
   return 0;
+}
+
+// Delta images: one workgroup per piece (<= DL_PIECE bytes) copies it from the base blob or the
+// literal bytes into the new blob, 16 bytes a lane when the piece's ends and both addresses allow
+// (every piece of an unshifted section does), else 4, else 1. Pure copy: HBM-bound, ~2x the new
+// blob's bytes at most; a one-CRD C5 delta moves ~110 MB through HBM in well under a millisecond.
+__global__ void __launch_bounds__(256) cedar_blob_patch(const uint64_t* __restrict__ pc, const uint8_t* __restrict__ base,
+                                                        const uint8_t* __restrict__ lit, uint8_t* __restrict__ out) {
+  const uint64_t dst = pc[3 * (size_t)blockIdx.x], len = pc[3 * (size_t)blockIdx.x + 1], src = pc[3 * (size_t)blockIdx.x + 2];
+  const uint8_t* s = (src & DL_LIT) ? lit + (src & ~DL_LIT) : base + src;
+  uint8_t* d = out + dst;
+  const uint64_t al = (uint64_t)(uintptr_t)s | (uint64_t)(uintptr_t)d | len;
+  if ((al & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    for (uint64_t i = threadIdx.x; i < len / 16; i += 256) d4[i] = s4[i];
+  } else if ((al & 3) == 0) {
+    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(s);
+    uint32_t* d1 = reinterpret_cast<uint32_t*>(d);
+    for (uint64_t i = threadIdx.x; i < len / 4; i += 256) d1[i] = s1[i];
+  } else {
+    for (uint64_t i = threadIdx.x; i < len; i += 256) d[i] = s[i];
+  }
+}
+
+// the word fixups, after the pieces (a later launch on the same stream)
+__global__ void __launch_bounds__(256) cedar_blob_fix(const uint32_t* __restrict__ fx, uint32_t n, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[fx[2 * i]] = fx[2 * i + 1];
+}
+
+int dev_blob_patch(int device, const DevImage& base, const uint64_t* pieces, size_t n_pieces, const uint8_t* lit,
+                   size_t lit_len, const uint32_t* fix, size_t n_fix, size_t new_len, void** out) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  if (!base.blob_len || base.origin != 0) { g_err = "the base image has no device blob"; return -2; }
+  if (n_pieces > 0x7FFFFFFFu || n_fix > 0x7FFFFFFFu) { g_err = "delta too large"; return -2; }
+  void* nb = nullptr;
+  void* stage = nullptr;
+  const size_t pbytes = n_pieces * 24, fbytes = n_fix * 8, sbytes = pbytes + fbytes + lit_len;
+  HIPCHK(hipMalloc(&nb, std::max<size_t>(new_len, DS_ALIGN)), "hipMalloc image");
+  hipError_t e = hipMalloc(&stage, std::max<size_t>(sbytes, 16));
+  hipStream_t s = nullptr;
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMemcpyAsync(stage, pieces, pbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && fbytes) e = hipMemcpyAsync((uint8_t*)stage + pbytes, fix, fbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && lit_len) e = hipMemcpyAsync((uint8_t*)stage + pbytes + fbytes, lit, lit_len, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && n_pieces) {
+    hipLaunchKernelGGL(cedar_blob_patch, dim3((uint32_t)n_pieces), dim3(256), 0, s, (const uint64_t*)stage,
+                       (const uint8_t*)base.base, (const uint8_t*)stage + pbytes + fbytes, (uint8_t*)nb);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && n_fix) {
+    hipLaunchKernelGGL(cedar_blob_fix, dim3((uint32_t)((n_fix + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t*)((const uint8_t*)stage + pbytes), (uint32_t)n_fix, (uint32_t*)nb);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (s) (void)hipStreamDestroy(s);
+  if (stage) (void)hipFree(stage);
+  if (e != hipSuccess) {
+    (void)hipFree(nb);
+    return fail(e, "delta image patch");
+  }
+  *out = nb;
+  return 0;
+}
+
+void dev_free(int device, void* p) {
+  if (!p) return;
+  (void)hipSetDevice(device);
+  (void)hipFree(p);
 }
 
 int dev_to_host(int device, const void* src, size_t n, void* dst) {
@@ -3036,11 +3304,11 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     f.cap = (fu_on && b.n() && !d.small && (!probe_kind || b.img->indexed)) ? (uint32_t)std::min<size_t>(want, budget_k[k] / entry) : 0u;
     if (d.small && k == FU_BIG && fu_on && b.img->n_pol() <= RANK_POL) {
       // the small path's overflow slots (KArgs::ovf_*, its SLIM merge): whole results of up to
-      // 1,024 reasons and 32 errors for n / 16 requests (at least 8); every slot travels back in the
-      // one D2H copy, so they stay few
+      // 1,024 reasons and 32 errors for n / 8 requests (at least 8); only the slots a batch takes
+      // travel back (dev_download_finish)
       f.capr = 1024;
       f.cape = 32;
-      f.cap = std::min<uint32_t>(b.n(), std::max<uint32_t>(8u, b.n() / 16u));
+      f.cap = std::min<uint32_t>(b.n(), std::max<uint32_t>(8u, b.n() / 8u));
     }
     o_k[k][0] = o_fu;                                        // ids
     o_k[k][1] = o_k[k][0] + al((size_t)f.cap * 4);           // res
@@ -3050,6 +3318,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     o_fu = o_k[k][4] + al((size_t)f.cap * f.cape * ERR_WORDS * 4);
   }
   d.out_bytes = o_fu;
+  d.dl_bytes = (d.small && d.fu[FU_BIG].cap) ? o_k[FU_BIG][0] : o_fu;
   int rc;
   if (b.img->lane_need > LANE_WORDS) {  // per-request lane scratch of the GLANE stream kernel
     const size_t lane_bytes = (size_t)n * b.img->lane_need * 4;
@@ -3111,7 +3380,13 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   size_t total_len = 0;
   for (int k = 0; k < NSEC; k++) total_len += len[k];
   const unsigned nt = total_len >= (8u << 20) ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
-  if (nt <= 1) {
+  uint8_t* in = (uint8_t*)d.in_blk;
+  // one core and a batch of >= 512 KB: staged below in pieces, each piece's H2D queued as soon as
+  // it is staged (the copy engine moves piece k while the host stages piece k + 1)
+  const bool pipelined = nt <= 1 && in_bytes >= (512u << 10);
+  if (pipelined) {
+    // (staged with the upload, below)
+  } else if (nt <= 1) {
     for (int k = 0; k < NSEC; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
   } else {
     auto part = [&](unsigned t) {  // byte range [t, t+1) / nt of the concatenated sections
@@ -3128,7 +3403,6 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     part(0);
     for (auto& th : ts) th.join();
   }
-  uint8_t* in = (uint8_t*)d.in_blk;
   uint8_t* o = (uint8_t*)d.out_blk;
   d.heap = (uint32_t*)(in + off[0]);
   d.req_base = (uint32_t*)(in + off[1]);
@@ -3153,7 +3427,26 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.stream = stream;
   d.pending = true;
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
-  HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  if (pipelined) {
+    const size_t piece = std::max<size_t>(256u << 10, (in_bytes / 4 + 4095) & ~(size_t)4095);
+    size_t sent = 0;
+    for (int k = 0; k < NSEC; k++) {
+      // a section longer than a piece goes in piece-sized parts
+      for (size_t a = 0; a < len[k];) {
+        const size_t b = std::min(len[k], a + piece);
+        std::memcpy(st + off[k] + a, (const uint8_t*)src[k] + a, b - a);
+        a = b;
+        const size_t end = a < len[k] ? off[k] + a : (k + 1 < NSEC ? off[k + 1] : in_bytes);
+        if (end - sent >= piece || (a >= len[k] && k + 1 == NSEC)) {
+          HIPCHK(hipMemcpyAsync(in + sent, st + sent, end - sent, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+          sent = end;
+        }
+      }
+    }
+    if (sent < in_bytes) HIPCHK(hipMemcpyAsync(in + sent, st + sent, in_bytes - sent, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  } else {
+    HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  }
   HIPCHK(hipMemsetAsync(d.res, 0, o_rf, s), "memset res");  // (and the worklist counters)
   return 0;
 }
@@ -3796,12 +4089,33 @@ static void bind_results(const DevBatch& b, Batch& host) {
   }
 }
 
+// A small batch's overflow slots after its results arrived: the ones it took (the counter), each
+// array's used prefix (the kernel has finished: plain copies, off the batch's stream, which may
+// already run the next batch).
+static int fetch_overflow(DevBatch& b) {
+  if (!b.dl_bytes || b.dl_bytes >= b.out_bytes || !b.fu_cnt) return 0;
+  const uint8_t* base = (const uint8_t*)b.out_blk;
+  uint8_t* st = (uint8_t*)b.stage;
+  const uint32_t taken = *(const uint32_t*)(st + ((const uint8_t*)(b.fu_cnt + FU_BIG) - base));
+  const auto& f = b.fu[FU_BIG];
+  const size_t used = std::min<uint32_t>(taken, f.cap);
+  if (!used) return 0;
+  const std::pair<const uint32_t*, size_t> arr[4] = {
+      {f.ids, used * 4}, {f.res, used * 8}, {f.rf, used * f.capr * 4}, {f.er, used * f.cape * ERR_WORDS * 4}};
+  for (const auto& a : arr) {
+    const size_t o = (const uint8_t*)a.first - base;
+    HIPCHK(hipMemcpy(st + o, base + o, a.second, hipMemcpyDeviceToHost), "D2H overflow slots");
+  }
+  return 0;
+}
+
 int dev_download(DevBatch& b, Batch& host, void* stream) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
-  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
+  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
   HIPCHK(hipStreamSynchronize(s), "sync download");
   b.pending = false;
+  if (const int rc = fetch_overflow(b)) return rc;
   bind_results(b, host);
   return 0;
 }
@@ -3814,10 +4128,12 @@ int dev_download_async(DevBatch& b, void* stream) {
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     b.done = (void*)e;
   }
-  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
+  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
   HIPCHK(hipEventRecord((hipEvent_t)b.done, s), "event record");
   return 0;
 }
+
+
 
 int dev_download_finish(DevBatch& b, Batch& host, int64_t deadline_ns) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
@@ -3826,6 +4142,7 @@ int dev_download_finish(DevBatch& b, Batch& host, int64_t deadline_ns) {
     if (rc) return rc;  // DEV_TIMEOUT: still in flight (pending), wait again or destroy
   }
   b.pending = false;
+  if (const int rc = fetch_overflow(b)) return rc;
   bind_results(b, host);
   return 0;
 }

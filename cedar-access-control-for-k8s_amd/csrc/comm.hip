@@ -178,4 +178,81 @@ int cg_broadcast_image(cg_ctx* ctx, cg_comm* c, int root, const void* image, siz
   return CG_OK;
 }
 
+// Collective: a delta image (cg_image_delta against `base_epoch`, which every rank holds) from
+// `root` to every rank, applied on each GPU (cg_image_load_delta) and loaded as `epoch`. Only the
+// delta's bytes cross xGMI (a one-CRD edit of the 100k-policy C5 image: ~0.1 % of the full blob).
+// A last all-reduce makes the ranks agree: `epoch` is activated (activate != 0) only when every
+// rank applied the delta, and every rank then returns the same result.
+int cg_broadcast_delta(cg_ctx* ctx, cg_comm* c, int root, uint64_t base_epoch, const void* delta, size_t len,
+                       uint64_t epoch, int activate, size_t* out_len) {
+  if (!ctx || !c || root < 0 || root >= c->nranks) return CG_E_ARG;
+  if (c->aborted || !c->nccl) { c->err = "communicator aborted by an earlier failure; recreate it"; return CG_E_STATE; }
+  auto fail = [&](const std::string& m) { c->err = m; return CG_E_DEVICE; };
+  std::string why;
+  if (hipSetDevice(c->device) != hipSuccess) return fail("hipSetDevice failed");
+  uint64_t* dn = nullptr;
+  if (hipMalloc((void**)&dn, 8) != hipSuccess) return fail("hipMalloc failed");
+  // one 8-byte collective on the comm stream; false (communicator aborted on enqueue errors) on failure
+  auto coll8 = [&](uint64_t& v, bool bcast) {
+    ncclResult_t r = ncclSuccess;
+    const bool ok = hipMemcpy(dn, &v, 8, hipMemcpyHostToDevice) == hipSuccess &&
+                    (r = bcast ? ncclBroadcast(dn, dn, 8, ncclUint8, root, c->nccl, c->stream)
+                               : ncclAllReduce(dn, dn, 1, ncclUint64, ncclMin, c->nccl, c->stream)) == ncclSuccess &&
+                    comm_wait(c, comm_timeout_ms(), why) && hipMemcpy(&v, dn, 8, hipMemcpyDeviceToHost) == hipSuccess;
+    if (r != ncclSuccess) {
+      comm_abort(c);
+      why = ncclGetErrorString(r);
+    }
+    return ok;
+  };
+  uint64_t n = (c->rank == root && delta) ? (uint64_t)len : 0;
+  if (!coll8(n, true)) { (void)hipFree(dn); return fail("length broadcast: " + why); }
+  if (n == 0) {
+    (void)hipFree(dn);
+    c->err = "the root has no delta to broadcast";
+    return CG_E_ARG;
+  }
+  void* buf = nullptr;
+  uint64_t ready = hipMalloc(&buf, (size_t)n) == hipSuccess ? 1u : 0u;
+  if (ready && c->rank == root && hipMemcpy(buf, delta, (size_t)n, hipMemcpyHostToDevice) != hipSuccess) ready = 0;
+  if (!coll8(ready, false) || !ready) {
+    if (buf) (void)hipFree(buf);
+    (void)hipFree(dn);
+    return fail(!why.empty() ? "readiness all-reduce: " + why : std::string("a rank could not allocate the delta buffer"));
+  }
+  ncclResult_t r = ncclBroadcast(buf, buf, (size_t)n, ncclUint8, root, c->nccl, c->stream);
+  if (r != ncclSuccess || !comm_wait(c, comm_timeout_ms(), why)) {
+    if (r != ncclSuccess) comm_abort(c);
+    (void)hipFree(buf);
+    (void)hipFree(dn);
+    return fail("delta broadcast: " + (why.empty() ? std::string(ncclGetErrorString(r)) : why));
+  }
+  std::vector<uint8_t> host;
+  const void* hd = delta;
+  int rc = CG_OK;
+  if (c->rank != root) {
+    host.resize((size_t)n);
+    if (hipMemcpy(host.data(), buf, (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) rc = CG_E_DEVICE;
+    hd = host.data();
+  }
+  (void)hipFree(buf);
+  std::string local;
+  if (rc == CG_OK) {
+    rc = cg_image_load_delta(ctx, base_epoch, hd, (size_t)n, epoch);
+    if (rc) local = cg_last_error(ctx);
+  } else {
+    local = "D2H of the delta failed";
+  }
+  uint64_t all = rc == CG_OK ? 1u : 0u;
+  if (!coll8(all, false)) { (void)hipFree(dn); return fail("result all-reduce: " + why); }
+  (void)hipFree(dn);
+  if (!all) {
+    c->err = rc ? local : std::string("another rank could not apply the delta (epoch loaded here, not activated)");
+    return rc ? rc : CG_E_STATE;
+  }
+  if (activate && (rc = cg_image_activate(ctx, epoch))) { c->err = cg_last_error(ctx); return rc; }
+  if (out_len) *out_len = (size_t)n;
+  return CG_OK;
+}
+
 }  // extern "C"

@@ -1320,6 +1320,8 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   for (uint32_t p = 0; p < n; p++)
     if (mcnt[p] > 1) { mlist[p] = (uint32_t)ext_end; ext_end += 1 + mcnt[p]; }
   if (ext_end >= (1ull << 32)) throw CedarError("scope index exceeds 16 GiB");
+  // (the candidate pass packs a bucket's first head with its key combination: 27 bits, cedar_eval.hip EF_COMBO)
+  if (n_heads >= (1u << 27)) throw CedarError("scope index exceeds 2^27 policy heads");
   img.bstream.assign(std::max<uint64_t>(ext_end, HEAD_WORDS), 0);
   for (uint32_t p = 0; p < n; p++) {
     std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
@@ -2025,6 +2027,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   for (uint32_t k = 0; k < DS_COUNT; k++) { img->dev_off[k] = r.u64(); img->dev_len[k] = r.u64(); }
   img->dev_begin = r.u64();
   img->dev_end = r.u64();
+  img->blob_len = n;
   if (img->dev_begin % DS_ALIGN || img->dev_end % DS_ALIGN || img->dev_begin > img->dev_end || img->dev_end > n ||
       img->dev_begin < (size_t)(r.p - p))
     throw CedarError("corrupt image (device region)");
@@ -2034,11 +2037,18 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     v.resize(len / 4);
     if (len) std::memcpy(v.data(), p + off, len);  // an empty section (no static entities) has no storage
   };
-  sec_words(DS_PSTREAM, img->pstream); sec_words(DS_TIER_CEND, img->tier_cend); sec_words(DS_CHUNKS, img->chunks);
+  // The host keeps the sections it reads (encoder tables, string table, static entities); the
+  // device-only ones (policy stream, scope index, bitsets: ~85 % of a large image) are validated
+  // in place and only their sizes kept (Image::dev_len), so a load copies them once, to the device
+  auto sec_view = [&](uint32_t k) -> std::pair<const uint32_t*, size_t> {
+    const uint64_t off = img->dev_off[k], len = img->dev_len[k];
+    if (off % DS_ALIGN || off < img->dev_begin || len % 4 || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
+    return {reinterpret_cast<const uint32_t*>(p + off), (size_t)(len / 4)};
+  };
+  for (uint32_t k : {DS_PSTREAM, DS_BTAB, DS_BFILT, DS_BSTREAM, DS_SCTX, DS_SBITS, DS_SVALS}) (void)sec_view(k);
+  sec_words(DS_TIER_CEND, img->tier_cend); sec_words(DS_CHUNKS, img->chunks);
   sec_words(DS_CPOOL, img->cpool); sec_words(DS_GSTR_OFF, img->gstr_off); sec_words(DS_HOT, img->hot);
-  sec_words(DS_ACT, img->act); sec_words(DS_BTAB, img->btab); sec_words(DS_BFILT, img->bfilt);
-  sec_words(DS_BSTREAM, img->bstream); sec_words(DS_SROWS, img->srows); sec_words(DS_SHASH, img->shash);
-  sec_words(DS_SCTX, img->sctx); sec_words(DS_SBITS, img->sbits); sec_words(DS_SVALS, img->svals);
+  sec_words(DS_ACT, img->act); sec_words(DS_SROWS, img->srows); sec_words(DS_SHASH, img->shash);
   {
     const uint64_t off = img->dev_off[DS_GSTR_BYTES], len = img->dev_len[DS_GSTR_BYTES];
     if (off % DS_ALIGN || off < img->dev_begin || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
@@ -2059,33 +2069,37 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     throw CedarError("corrupt image (prefix lengths)");
   {
     // entries < slots: every insertion finds a free slot and every probe chain ends at one
-    const size_t ne = img->btab.size() / BT_WORDS, nb = img->btab_slots, nf = img->bfilt.size();
-    if (!ne || img->btab.size() % BT_WORDS || nb < 2 || (nb & (nb - 1)) || ne >= nb || nf < 2 || (nf & (nf - 1)))
+    const size_t bw = sec_view(DS_BTAB).second, nf = sec_view(DS_BFILT).second;
+    const size_t ne = bw / BT_WORDS, nb = img->btab_slots;
+    if (!ne || bw % BT_WORDS || nb < 2 || (nb & (nb - 1)) || ne >= nb || nf < 2 || (nf & (nf - 1)))
       throw CedarError("corrupt image (scope index)");
   }
   if (img->lane_need > LANE_MAX) throw CedarError("corrupt image (lane scratch)");
   {
-    const size_t nc = img->sctx.size() / SCTX_WORDS;
-    if (!nc || (nc & (nc - 1)) || img->sctx.size() % SCTX_WORDS || img->sbits.size() % 2 ||
-        (img->sbits_words && (img->sbits.size() / 2) % img->sbits_words) || img->svals.size() < 2 || img->svals.size() % 2)
+    const auto [sctx, sctx_n] = sec_view(DS_SCTX);
+    const auto [sbits, sbits_n] = sec_view(DS_SBITS);
+    const size_t svals_n = sec_view(DS_SVALS).second;
+    const size_t nc = sctx_n / SCTX_WORDS;
+    if (!nc || (nc & (nc - 1)) || sctx_n % SCTX_WORDS || sbits_n % 2 ||
+        (img->sbits_words && (sbits_n / 2) % img->sbits_words) || svals_n < 2 || svals_n % 2)
       throw CedarError("corrupt image (scope bitsets)");
     // every context row in range, a free slot that ends every probe chain, and ranks that number
     // every set bit within svals
     size_t used = 0;
-    const size_t rows = img->sbits_words ? img->sbits.size() / 2 / img->sbits_words : 0;
+    const size_t rows = img->sbits_words ? sbits_n / 2 / img->sbits_words : 0;
     for (size_t k = 0; k < nc; k++) {
-      const uint32_t* e = &img->sctx[k * SCTX_WORDS];
+      const uint32_t* e = sctx + k * SCTX_WORDS;
       if (!e[0]) continue;
       used++;
       if (!(e[0] & SCTX_USED) || e[7] >= rows) throw CedarError("corrupt image (scope bitsets)");
     }
     if (used >= nc) throw CedarError("corrupt image (scope bitsets)");
     uint32_t rank = 0;
-    for (size_t w = 0; w < img->sbits.size() / 2; w++) {
-      if (img->sbits[2 * w + 1] != rank) throw CedarError("corrupt image (scope bitsets)");
-      rank += (uint32_t)__builtin_popcount(img->sbits[2 * w]);
+    for (size_t w = 0; w < sbits_n / 2; w++) {
+      if (sbits[2 * w + 1] != rank) throw CedarError("corrupt image (scope bitsets)");
+      rank += (uint32_t)__builtin_popcount(sbits[2 * w]);
     }
-    if ((size_t)rank * 2 > img->svals.size()) throw CedarError("corrupt image (scope bitsets)");
+    if ((size_t)rank * 2 > svals_n) throw CedarError("corrupt image (scope bitsets)");
   }
   {
     const size_t ns = img->shash.size() / SH_WORDS;
@@ -2098,9 +2112,14 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   if (!img->key_ents.empty()) std::memcpy(img->key_ents.data(), r.p, img->key_ents.size() * 8);
   r.p += img->key_ents.size() * 8;
   if (img->sbits_words && img->sbits_words != (img->key_ents.size() + 31) / 32) throw CedarError("corrupt image (scope bitsets)");
+  // (no `sid` map: a loaded image finds strings through `lookup`, build_lookup below)
   uint32_t ns = r.u32();
-  for (uint32_t i = 0; i < ns; i++) { img->strings.push_back(r.str()); img->sid.emplace(img->strings.back(), i); }
+  r.need((size_t)ns * 4);
+  img->strings.reserve(ns);
+  for (uint32_t i = 0; i < ns; i++) img->strings.push_back(r.str());
   uint32_t nm = r.u32();
+  r.need((size_t)nm * 40);  // (two length words, three u64, two u32 each at least)
+  img->meta.reserve(nm);
   for (uint32_t i = 0; i < nm; i++) {
     PolicyMeta m;
     m.id = r.str(); m.filename = r.str();

@@ -27,6 +27,9 @@ struct DevImage {
   // above point into it at (blob offset - origin)
   void* base = nullptr;
   uint64_t origin = 0, region = 0;  // blob offset of base[0]; region bytes (dev_end - dev_begin)
+  // the whole blob is on the device (origin 0, blob_len bytes at base): a delta image can patch it
+  // on the device (dev_blob_patch)
+  uint64_t blob_len = 0;
   uint32_t n_static = 0, smask = 0;
   uint32_t lane_need = 0;  // lane-scratch words per request (> LANE_WORDS: the GLANE stream kernel)
   uint32_t cslot_mask = 0;  // rows carry element-hash / prefix-hash lists (Image::list_mask, image.h)
@@ -85,6 +88,9 @@ struct DevBatch {
   // lists cannot hold goes to the host re-run)
   bool small = false;
   bool stepped = false;  // the step ran once since the upload (later steps reset their counters)
+  // small batches download the results up to the overflow slots (dl_bytes of out_bytes); the slots
+  // a batch took follow once its counter is read (dev_download_finish)
+  size_t dl_bytes = 0;
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)
   size_t in_cls = 0, out_cls = 0, stage_cls = 0, out_bytes = 0;
@@ -101,15 +107,26 @@ const char* dev_last_error();
 int dev_count(int* n);
 int dev_select(int device);
 int dev_synchronize(int device);
-// Device copy of an image read from `blob` (Image::deserialize): its device region in one
-// allocation and one H2D copy.
+// Device copy of an image read from `blob` (Image::deserialize): the whole blob (the device region
+// and, for delta images, the host part) in one allocation and one H2D copy.
 int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage* out);
 // Device copy on `device` of an image already on another (or the same) device: one peer copy of
-// the region (xGMI between GPUs).
+// the blob (xGMI between GPUs).
 int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* out);
 // Adopts `dev_blob`, the whole serialized blob already in device memory on `device` (hipMalloc'd,
 // e.g. the buffer a broadcast wrote): the arrays point into it, and dev_image_free frees it.
 int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out);
+// Delta images (delta.cpp): builds on `device` a new blob of new_len bytes from the base image's
+// device blob (base.blob_len > 0) and literal bytes. pieces: (dst, len, src) triples covering
+// [0, new_len), each at most DL_PIECE bytes; src is a base-blob offset, or DL_LIT | an offset into
+// lit; then the word fixups (word index, value) pairs. One H2D copy of pieces, fixups and
+// literals, two kernel launches; *out receives the new device
+// buffer (hipMalloc'd: dev_image_adopt takes it, else dev_free).
+constexpr uint64_t DL_LIT = 1ull << 63;
+constexpr uint64_t DL_PIECE = 64 * 1024;
+int dev_blob_patch(int device, const DevImage& base, const uint64_t* pieces, size_t n_pieces, const uint8_t* lit,
+                   size_t lit_len, const uint32_t* fix, size_t n_fix, size_t new_len, void** out);
+void dev_free(int device, void* p);
 // Copies n bytes of device memory on `device` to host memory (pinned staging, one copy).
 int dev_to_host(int device, const void* src, size_t n, void* dst);
 void dev_image_free(DevImage* d);

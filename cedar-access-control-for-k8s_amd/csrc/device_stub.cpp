@@ -61,29 +61,46 @@ static void stub_image(int device, const Image& img, DevImage& d) {
 int dev_image_upload(int device, const Image& img, const uint8_t* blob, DevImage* out) {
   DevImage d;
   stub_image(device, img, d);
-  d.base = std::malloc(std::max<size_t>(d.region, 1));
+  d.base = std::malloc(std::max<size_t>(img.blob_len, 1));
   if (!d.base) { g_err = "out of memory"; return -5; }
-  std::memcpy(d.base, blob + img.dev_begin, d.region);  // the H2D copy of the device region
-  d.origin = img.dev_begin;
+  std::memcpy(d.base, blob, img.blob_len);  // the H2D copy of the whole blob
+  d.origin = 0;
+  d.blob_len = img.blob_len;
   *out = d;
   return 0;
 }
 int dev_image_copy(int device, const Image& img, const DevImage& src, DevImage* out) {
   DevImage d;
   stub_image(device, img, d);
-  d.base = std::malloc(std::max<size_t>(d.region, 1));
+  d.base = std::malloc(std::max<size_t>(src.blob_len, 1));
   if (!d.base) { g_err = "out of memory"; return -5; }
-  std::memcpy(d.base, (const uint8_t*)src.base + (img.dev_begin - src.origin), d.region);
-  d.origin = img.dev_begin;
+  std::memcpy(d.base, src.base, src.blob_len);
+  d.origin = 0;
+  d.blob_len = src.blob_len;
   *out = d;
   return 0;
 }
+int dev_blob_patch(int, const DevImage& base, const uint64_t* pieces, size_t n_pieces, const uint8_t* lit, size_t,
+                   const uint32_t* fix, size_t n_fix, size_t new_len, void** out) {
+  if (!base.blob_len || base.origin != 0) { g_err = "the base image has no device blob"; return -2; }
+  uint8_t* nb = (uint8_t*)std::malloc(std::max<size_t>(new_len, 1));
+  if (!nb) { g_err = "out of memory"; return -5; }
+  for (size_t k = 0; k < n_pieces; k++) {
+    const uint64_t dst = pieces[3 * k], len = pieces[3 * k + 1], src = pieces[3 * k + 2];
+    std::memcpy(nb + dst, (src & DL_LIT) ? lit + (src & ~DL_LIT) : (const uint8_t*)base.base + src, len);
+  }
+  for (size_t k = 0; k < n_fix; k++) std::memcpy(nb + 4 * (size_t)fix[2 * k], &fix[2 * k + 1], 4);
+  *out = nb;
+  return 0;
+}
+void dev_free(int, void* p) { std::free(p); }
 // the stub's "device memory" is host malloc memory (cg_image_load_device callers of the stub pass it)
 int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out) {
   DevImage d;
   stub_image(device, img, d);
   d.base = dev_blob;
   d.origin = 0;
+  d.blob_len = img.blob_len;
   *out = d;
   return 0;
 }
@@ -261,4 +278,5 @@ int cg_comm_create(int, int, int, const uint8_t*, size_t, cg_comm** out) {
 void cg_comm_destroy(cg_comm*) {}
 const char* cg_comm_last_error(cg_comm*) { return "no collectives in the sanitizer build"; }
 int cg_broadcast_image(cg_ctx*, cg_comm*, int, const void*, size_t, uint64_t, int, size_t*) { return CG_E_DEVICE; }
+int cg_broadcast_delta(cg_ctx*, cg_comm*, int, uint64_t, const void*, size_t, uint64_t, int, size_t*) { return CG_E_DEVICE; }
 }

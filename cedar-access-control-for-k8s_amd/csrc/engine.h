@@ -44,7 +44,9 @@ struct PolicyMeta {
 struct EncCache;  // encode_impl.h
 
 // A compiled, immutable policy image (one per policy epoch). Device sections are the vectors
-// uploaded verbatim; the rest is host-side metadata for rendering diagnostics.
+// uploaded verbatim; the rest is host-side metadata for rendering diagnostics. An image read from a
+// blob (deserialize) leaves the device-only sections empty (pstream, btab, bfilt, bstream, sctx,
+// sbits, svals: dev_len holds their sizes): the host never reads them after the upload.
 struct Image {
   uint64_t epoch = 0;
   std::vector<uint32_t> pol, tier_end, code, cpool, gstr_off, hot;  // hot: HOT_WORDS per hot path
@@ -161,6 +163,7 @@ struct Image {
   // byte sizes, and the region's bounds (blob offsets)
   uint64_t dev_off[cgi::DS_COUNT] = {}, dev_len[cgi::DS_COUNT] = {};
   uint64_t dev_begin = 0, dev_end = 0;
+  uint64_t blob_len = 0;  // the blob's size (deserialize)
   static std::shared_ptr<Image> deserialize(const uint8_t* p, size_t n);
 };
 

@@ -45,6 +45,7 @@ struct Ticket;
 
 struct QBatch {
   cg_batch* b = nullptr;
+  Clock::time_point t_submit{};  // batch latency: submit -> results published
   int rc = CG_OK;
   std::string err;
   std::vector<std::shared_ptr<Ticket>> tickets;  // released (cleared) when the batch is published
@@ -92,6 +93,32 @@ int64_t now_ns() {
   return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
 }
 
+// cg_queue_metrics' latency buckets (ns, "le"): 10 us .. 10 s, holding the reference's
+// request_duration_seconds buckets (metrics.go:43: 0.25, 0.5, 0.7, 1, 1.5, 3, 5, 10 s)
+constexpr uint64_t k_lat_bounds[CG_LAT_BOUNDS] = {
+    10000,     25000,     50000,      100000,     250000,     500000,     1000000,
+    2500000,   5000000,   10000000,   25000000,   50000000,   100000000,  250000000,
+    500000000, 700000000, 1000000000, 1500000000, 3000000000, 5000000000, 10000000000};
+uint32_t lat_bucket(uint64_t ns) {
+  return (uint32_t)(std::lower_bound(k_lat_bounds, k_lat_bounds + CG_LAT_BOUNDS, ns) - k_lat_bounds);
+}
+uint32_t size_bucket(uint64_t n) {
+  uint32_t k = 0;
+  while (k < CG_BATCH_BUCKETS && (1ull << k) < n) k++;
+  return k;
+}
+
+// the serving metrics (relaxed counters; a few atomics per call)
+struct QMetrics {
+  std::atomic<uint64_t> req[4]{}, lat[4][CG_LAT_BOUNDS + 1]{}, lat_sum[4]{};
+  std::atomic<uint64_t> bsize[CG_BATCH_BUCKETS + 1]{}, blat[CG_LAT_BOUNDS + 1]{}, blat_sum{0};
+  void request(uint32_t outcome, uint64_t ns) {
+    req[outcome].fetch_add(1, std::memory_order_relaxed);
+    lat[outcome][lat_bucket(ns)].fetch_add(1, std::memory_order_relaxed);
+    lat_sum[outcome].fetch_add(ns, std::memory_order_relaxed);
+  }
+};
+
 }  // namespace
 
 // one GPU's submitter: runs the batches dealt to its context, in order
@@ -121,6 +148,7 @@ struct cg_queue {
   std::condition_variable slot_cv;
   std::atomic<uint64_t> n_batches{0}, n_requests{0}, n_fast{0}, max_seen{0}, device_ns{0}, n_abandoned{0};
   std::atomic<int64_t> stop_ns{0};  // when cg_queue_destroy began (steady clock)
+  QMetrics m;
 
   static constexpr uint32_t DEPTH = 2;  // batches per submitter: one running, the next queued
 
@@ -187,6 +215,9 @@ void cg_queue::work(QWorker& w) {
     busy_since = now;
     w.n_batches++;
     w.n_requests += qb->b->items.size();
+    const uint64_t bl = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - qb->t_submit).count();
+    m.blat[lat_bucket(bl)].fetch_add(1, std::memory_order_relaxed);
+    m.blat_sum.fetch_add(bl, std::memory_order_relaxed);
     publish(*qb);
     {
       std::lock_guard<std::mutex> g(slot_mu);
@@ -209,7 +240,8 @@ void cg_queue::work(QWorker& w) {
       }
     }
     if (qb) {
-      if (!inflight) busy_since = Clock::now();
+      qb->t_submit = Clock::now();
+      if (!inflight) busy_since = qb->t_submit;
       if (!qb->rc) {
         const int rc = cg_batch_submit(qb->b);
         if (rc) {
@@ -318,6 +350,7 @@ void cg_queue::run() {
     }
     n_batches++;
     const uint64_t n = qb->b->items.size();
+    m.bsize[size_bucket(n)].fetch_add(1, std::memory_order_relaxed);
     for (uint64_t m = max_seen.load(); n > m && !max_seen.compare_exchange_weak(m, n);) {
     }
     rr++;
@@ -468,9 +501,10 @@ int cg_queue_gpu_stats(cg_queue* q, uint32_t k, uint64_t* batches, uint64_t* req
 
 const char* cg_queue_last_error(void) { return t_err.c_str(); }
 
-int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout_ns, int* decision,
-                           char* reason, size_t cap, size_t* need) {
-  if (!q || !sar_json || !decision) return CG_E_ARG;
+namespace {
+
+int authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout_ns, int* decision, char* reason,
+                  size_t cap, size_t* need) {
   const int64_t deadline = timeout_ns < 0 ? -1 : now_ns() + timeout_ns;
   TicketP tp = std::make_shared<Ticket>();
   Ticket& t = *tp;
@@ -508,9 +542,8 @@ int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_
   return submit_ticket(q, tp, deadline, decision, reason, cap, need, true);
 }
 
-int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int64_t timeout_ns, int* allow,
-                                char* diag, size_t cap, size_t* need) {
-  if (!q || !item_json || !allow) return CG_E_ARG;
+int is_authorized_json(cg_queue* q, const char* item_json, size_t len, int64_t timeout_ns, int* allow, char* diag,
+                       size_t cap, size_t* need) {
   const int64_t deadline = timeout_ns < 0 ? -1 : now_ns() + timeout_ns;
   std::vector<EntityIn> ents;
   RequestIn req;
@@ -526,6 +559,35 @@ int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, 
   return submit_ticket(q, tp, deadline, allow, diag, cap, need, false);
 }
 
+// outcome index of a call (cg_queue_metrics.requests): the decision when it is valid
+uint32_t outcome(int rc, int d, bool admission) {
+  if (rc != CG_OK && rc != CG_E_RANGE) return 3u;
+  if (admission) return d ? 1u : 0u;
+  return (d >= 0 && d < 3) ? (uint32_t)d : 3u;
+}
+
+}  // namespace
+
+int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout_ns, int* decision,
+                           char* reason, size_t cap, size_t* need) {
+  if (!q || !sar_json || !decision) return CG_E_ARG;
+  const auto t0 = Clock::now();
+  const int rc = authorize_sar(q, sar_json, len, timeout_ns, decision, reason, cap, need);
+  q->m.request(outcome(rc, *decision, false),
+               (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
+  return rc;
+}
+
+int cg_queue_is_authorized_json(cg_queue* q, const char* item_json, size_t len, int64_t timeout_ns, int* allow,
+                                char* diag, size_t cap, size_t* need) {
+  if (!q || !item_json || !allow) return CG_E_ARG;
+  const auto t0 = Clock::now();
+  const int rc = is_authorized_json(q, item_json, len, timeout_ns, allow, diag, cap, need);
+  q->m.request(outcome(rc, *allow, true),
+               (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
+  return rc;
+}
+
 int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t* fast, uint64_t* max_batch,
                    uint64_t* device_ns) {
   if (!q) return CG_E_ARG;
@@ -534,6 +596,35 @@ int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t*
   if (fast) *fast = q->n_fast.load();
   if (max_batch) *max_batch = q->max_seen.load();
   if (device_ns) *device_ns = q->device_ns.load();
+  return CG_OK;
+}
+
+const uint64_t* cg_metrics_latency_bounds(uint32_t* n) {
+  if (n) *n = CG_LAT_BOUNDS;
+  return k_lat_bounds;
+}
+
+int cg_queue_metrics_get(cg_queue* q, cg_queue_metrics* out, size_t size) {
+  if (!q || !out || size != sizeof(cg_queue_metrics)) return CG_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  auto rd = [](const std::atomic<uint64_t>& x) { return x.load(std::memory_order_relaxed); };
+  for (uint32_t o = 0; o < 4; o++) {
+    out->requests[o] = rd(q->m.req[o]);
+    for (uint32_t b = 0; b <= CG_LAT_BOUNDS; b++) out->latency[o][b] = rd(q->m.lat[o][b]);
+    out->latency_sum_ns[o] = rd(q->m.lat_sum[o]);
+  }
+  out->fast = rd(q->n_fast);
+  out->batches = rd(q->n_batches);
+  for (uint32_t b = 0; b <= CG_BATCH_BUCKETS; b++) out->batch_size[b] = rd(q->m.bsize[b]);
+  for (uint32_t b = 0; b <= CG_LAT_BOUNDS; b++) out->batch_latency[b] = rd(q->m.blat[b]);
+  out->batch_latency_sum_ns = rd(q->m.blat_sum);
+  out->abandoned = rd(q->n_abandoned);
+  cg_ctx* c = q->ctxs[0];
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    out->active_epoch = c->active ? c->active->host->epoch : 0;
+  }
+  out->activations = rd(c->activations);
   return CG_OK;
 }
 

@@ -162,6 +162,24 @@ int cg_image_load_device(cg_ctx* ctx, void* dev_blob, size_t len, uint64_t epoch
  * is copied GPU to GPU (xGMI peer copy; a device copy when both contexts use the same GPU). The
  * in-process multi-GPU reload: compile once, cg_image_load on one context, this on the others. */
 int cg_image_load_peer(cg_ctx* dst, cg_ctx* src, uint64_t epoch);
+/* ---- delta images (src/delta.h) ----
+ * A policy edit changes a few policies of a large image: the reference applies each CRD informer
+ * event to its PolicySet in place (store/crd.go:45-118, mutations at :62,85,102,114). Here the root
+ * compiles the new epoch (incrementally) and ships only the bytes that differ from the image every
+ * GPU already holds. cg_image_delta: the delta that turns blob `base` into blob `next` (malloc'd,
+ * cg_free). cg_image_patch: the new blob from base + delta on the host (checked against the delta's
+ * checksum of the new blob; CG_E_ARG on any mismatch). cg_delta_info: a delta's sizes. */
+int cg_image_delta(const void* base, size_t base_len, const void* next, size_t next_len, uint8_t** delta,
+                   size_t* delta_len);
+int cg_image_patch(const void* base, size_t base_len, const void* delta, size_t delta_len, uint8_t** out,
+                   size_t* out_len);
+int cg_delta_info(const void* delta, size_t len, uint64_t* base_len, uint64_t* new_len, uint64_t* ops,
+                  uint64_t* literal_bytes);
+/* Loads as `epoch` the image a delta makes of the image ctx holds for `base_epoch`: the new blob is
+ * built on the GPU from the base's device copy (one copy kernel over the delta's operations), its
+ * checksum checked, the host tables read from it. CG_E_STATE: no such base; CG_E_ARG: the delta is
+ * malformed or for another base. Not active until activated. */
+int cg_image_load_delta(cg_ctx* ctx, uint64_t base_epoch, const void* delta, size_t len, uint64_t epoch);
 /* Atomically makes `epoch` the image new batches bind to; in-flight batches keep theirs. */
 int cg_image_activate(cg_ctx* ctx, uint64_t epoch);
 int cg_image_active(cg_ctx* ctx, uint64_t* epoch);
@@ -185,6 +203,12 @@ const char* cg_comm_last_error(cg_comm* comm);
  * return CG_E_STATE until it is recreated. */
 int cg_broadcast_image(cg_ctx* ctx, cg_comm* comm, int root, const void* image, size_t len, uint64_t epoch,
                        int activate, size_t* out_len);
+/* Collective: root's delta image against `base_epoch` (every rank holds it) is broadcast and applied
+ * on every GPU (cg_image_load_delta) as `epoch`. The ranks agree on the outcome (a last all-reduce):
+ * `epoch` is activated (activate != 0) only when every rank applied the delta. Failure handling as
+ * cg_broadcast_image. *out_len (may be NULL) receives the delta's size. */
+int cg_broadcast_delta(cg_ctx* ctx, cg_comm* comm, int root, uint64_t base_epoch, const void* delta, size_t len,
+                       uint64_t epoch, int activate, size_t* out_len);
 
 /* ---- batches of (EntityMap, Request) ---- */
 /* Creates a batch bound to the currently active image. */
@@ -324,6 +348,38 @@ int cg_queue_stats(cg_queue* q, uint64_t* batches, uint64_t* requests, uint64_t*
 /* Requests the queue dropped unevaluated because their callers' deadlines passed while they still
  * waited for a batch (the callers already returned CG_E_TIMEOUT and failed safe). */
 int cg_queue_dropped(cg_queue* q, uint64_t* abandoned);
+
+/* ---- metrics (the reference's cedar_authorizer_* collectors, metrics/metrics.go:27-65) ----
+ * A snapshot of the queue's serving metrics for a Prometheus exporter on the host side:
+ * - request_total{decision} and request_duration_seconds{decision}: every cg_queue_authorize_sar /
+ *   cg_queue_is_authorized_json call, by outcome (Deny, Allow, NoOpinion, error; an admission call's
+ *   allow counts as Allow, its deny as Deny), with its latency from entry to return. The reference
+ *   records only non-Deny decisions and errors (server.go:81-90): its exporter skips index 0.
+ * - the batch-size and batch-latency (submit -> results published) histograms and the active
+ *   image epoch that SURVEY §5 asks for beside them.
+ * Latency buckets are "le" buckets over cg_metrics_latency_bounds (ns; 10 µs .. 10 s, a superset of
+ * the reference's 0.25-10 s buckets, metrics.go:43), counted per bucket (not cumulative); the last
+ * bucket is +Inf. Batch-size bucket k counts batches of size <= 2^k; the last one, the rest. */
+#define CG_LAT_BOUNDS 21
+#define CG_BATCH_BUCKETS 14
+typedef struct cg_queue_metrics {
+  uint64_t requests[4];                   /* by outcome: 0 Deny, 1 Allow, 2 NoOpinion, 3 error */
+  uint64_t latency[4][CG_LAT_BOUNDS + 1]; /* per outcome, per latency bucket */
+  uint64_t latency_sum_ns[4];
+  uint64_t fast;                          /* answered on the host (fast path), included above */
+  uint64_t batches;
+  uint64_t batch_size[CG_BATCH_BUCKETS + 1];
+  uint64_t batch_latency[CG_LAT_BOUNDS + 1];
+  uint64_t batch_latency_sum_ns;
+  uint64_t abandoned;                     /* cg_queue_dropped */
+  uint64_t active_epoch;                  /* ctxs[0]'s active image (cg_image_active; 0: none) */
+  uint64_t activations;                   /* cg_image_activate calls that switched ctxs[0]'s image */
+} cg_queue_metrics;
+/* The CG_LAT_BOUNDS bucket upper bounds in nanoseconds. */
+const uint64_t* cg_metrics_latency_bounds(uint32_t* n);
+/* Fills *out (size: sizeof(cg_queue_metrics), checked). Counters are read one by one (relaxed):
+ * a snapshot taken while calls run may be a few calls apart between fields. */
+int cg_queue_metrics_get(cg_queue* q, cg_queue_metrics* out, size_t size);
 /* Bench support: `threads` threads issue `total` blocking cg_queue_authorize_sar calls cycling
  * over sars[0..n); wall seconds, per-call latency p50/p99/max (ns) and decision counts
  * counts[0..3) = (Deny, Allow, NoOpinion). */

@@ -28,6 +28,31 @@ def test_exports_every_declared_symbol():
     assert declared == set(cedargpu._lib.EXPORTED)
 
 
+def test_metrics_layout_and_buckets():
+    """cg_queue_metrics (the reference's request_total / request_duration_seconds, metrics.go:27-47):
+    the binding's struct matches the header's, and the latency buckets hold the reference's."""
+    import ctypes
+    hdr = open(os.path.join(ROOT, "include", "cedargpu.h")).read()
+    nb = int(re.search(r"#define CG_LAT_BOUNDS (\d+)", hdr).group(1))
+    nz = int(re.search(r"#define CG_BATCH_BUCKETS (\d+)", hdr).group(1))
+    assert (nb, nz) == (cedargpu.store.LAT_BOUNDS, cedargpu.store.BATCH_BUCKETS)
+    body = re.search(r"typedef struct cg_queue_metrics \{(.*?)\} cg_queue_metrics;", hdr, re.S).group(1)
+    words = 0
+    for m in re.finditer(r"uint64_t (\w+)((?:\[[^\]]+\])*);", body):
+        n = 1
+        for dim in re.findall(r"\[([^\]]+)\]", m.group(2)):
+            n *= eval(dim.replace("CG_LAT_BOUNDS", str(nb)).replace("CG_BATCH_BUCKETS", str(nz)))
+        words += n
+    assert ctypes.sizeof(cedargpu.store.QueueMetrics) == 8 * words
+    n = ctypes.c_uint32()
+    bp = cedargpu.lib.cg_metrics_latency_bounds(ctypes.byref(n))
+    bounds = [bp[i] for i in range(n.value)]
+    assert n.value == nb and bounds == sorted(bounds)
+    for sec in (0.25, 0.5, 0.7, 1, 1.5, 3, 5, 10):
+        assert round(sec * 1e9) in bounds
+    assert cedargpu.lib.cg_queue_metrics_get(None, None, 0) != 0
+
+
 def test_version():
     assert b"gfx950" in cedargpu.lib.cg_version()
 
@@ -116,3 +141,65 @@ def test_c3_workload_is_fully_atomic():
     img = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", synth.abac_policies(2000, seed=31, pop=pop))])
     st = cedargpu.image_stats(img)
     assert st["atomic"] == st["policies"] == 2000, st
+
+
+# ------------------------------------------------------------------ delta images (§8 f2)
+def _tenant_docs(n_pol=4000, n_ns=40, seed=51):
+    tpop = synth.Population(seed=7, n_namespaces=n_ns)
+    return synth.multitenant_policies(n_pol, seed=seed, pop=tpop)
+
+
+def test_delta_one_document_edit_is_small_and_exact():
+    """A one-CRD edit (crd.go:62 update event) through the incremental compiler: the delta is a
+    small fraction of the image and base + delta reproduces the new blob byte for byte."""
+    docs = _tenant_docs()
+    comp = cedargpu.Compiler()
+    try:
+        a = comp.build([cedargpu.CRDStore(docs)], epoch=1)
+        docs[7] = (docs[7][0], docs[7][1], docs[7][2].replace("permit", "forbid", 1))
+        b = comp.build([cedargpu.CRDStore(docs)], epoch=2)
+        docs.append(("new-tenant", "new.cedar", 'permit(principal, action == k8s::Action::"get", resource);'))
+        c = comp.build([cedargpu.CRDStore(docs)], epoch=3)
+    finally:
+        comp.close()
+    # an edited document: < 1 % of the image; an added one (every later head index moves: word
+    # fixups for the scope-index entries, the bitset values re-sent) < 10 %
+    for base, new, frac in ((a, b, 0.01), (b, c, 0.10), (a, c, 0.10)):
+        d = cedargpu.image_delta(base, new)
+        info = cedargpu.delta_info(d)
+        assert info["base_len"] == len(base) and info["new_len"] == len(new)
+        assert len(d) < frac * len(new), (len(d), len(new))
+        assert cedargpu.image_patch(base, d) == new
+    # identical images: copies only (the header's epoch aside)
+    d = cedargpu.image_delta(a, a)
+    assert cedargpu.delta_info(d)["literal_bytes"] == 0 and cedargpu.image_patch(a, d) == a
+
+
+def test_delta_arbitrary_bytes_and_rejections():
+    import random
+    rnd = random.Random(5)
+    base = bytes(rnd.getrandbits(8) for _ in range(50_000))
+    # an insertion, a deletion and an overwrite: the shifts are found again
+    new = base[:1000] + b"inserted" * 40 + base[1000:20_000] + base[21_000:40_000] + b"\x00" * 300 + base[40_300:]
+    d = cedargpu.image_delta(base, new)
+    assert cedargpu.image_patch(base, d) == new
+    assert cedargpu.delta_info(d)["literal_bytes"] < 2000
+    for b2, n2 in ((b"", b"abc"), (b"abc", b""), (b"", b""), (base, base[::-1])):
+        assert cedargpu.image_patch(b2, cedargpu.image_delta(b2, n2)) == n2
+    # another base (length), a flipped literal byte (checksum), truncation, a bad magic
+    with pytest.raises(cedargpu.CedarGPUError):
+        cedargpu.image_patch(base[:-1], d)
+    lit_at = len(d) - 1
+    bad = bytearray(d)
+    bad[lit_at] ^= 1
+    with pytest.raises(cedargpu.CedarGPUError):
+        cedargpu.image_patch(base, bytes(bad))
+    with pytest.raises(cedargpu.CedarGPUError):
+        cedargpu.image_patch(base, d[:-5])
+    with pytest.raises(ValueError):
+        cedargpu.delta_info(b"XXXX" + d[4:])
+    # an operation pointing outside the base
+    bad = bytearray(d)
+    bad[56 + 16:56 + 24] = (len(base) + 10).to_bytes(8, "little")  # the first operation's src
+    with pytest.raises(cedargpu.CedarGPUError):
+        cedargpu.image_patch(base, bytes(bad))

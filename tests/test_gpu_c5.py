@@ -168,3 +168,52 @@ def test_incremental_image_decides_like_a_fresh_build(ctx):
     for (ok, _, diag, _), g in zip(want, [got[0][i] for i in idx]):
         wd = 1 if ok else (0 if diag.startswith('{"reasons"') else 2)
         assert g == (wd, diag if wd != 2 else "")
+
+
+def test_delta_reload_decides_like_a_full_load(ctx):
+    """§8 f2 delta images: CRD events (update, delete, add) compiled incrementally, shipped as a
+    delta against the loaded epoch and rebuilt on the GPU (cg_image_load_delta) decide exactly as
+    the full image loaded the ordinary way, and as the C++ oracle over the new store snapshot; a
+    delta-loaded image serves as the base of the next delta; bad deltas are refused."""
+    pop = synth.Population(seed=7, n_namespaces=200)
+    docs = synth.multitenant_policies(20_000, seed=52, pop=pop)
+    comp = cedargpu.Compiler()
+    img1 = comp.build([cedargpu.CRDStore(docs)], epoch=21)
+    ctx.load(img1, 21, activate=False)
+    docs2 = list(docs)
+    docs2[40] = (docs2[40][0], docs2[40][1], docs2[40][2].replace("permit", "forbid"))  # update
+    del docs2[77]                                                                      # delete
+    docs2.append(("tenant-new", "uid-new", docs[5][2]))                                # add
+    img2 = comp.build([cedargpu.CRDStore(docs2)], epoch=22)
+    docs3 = list(docs2)
+    docs3[120] = (docs3[120][0], docs3[120][1], docs3[120][2].replace("permit", "forbid"))
+    img3 = comp.build([cedargpu.CRDStore(docs3)], epoch=23)
+    comp.close()
+    d12, d23 = cedargpu.image_delta(img1, img2), cedargpu.image_delta(img2, img3)
+    assert len(d23) < len(img3) // 100  # an update alone: a small delta
+    ctx.load_delta(21, d12, 22, activate=False)
+    ctx.load_delta(22, d23, 23, activate=False)  # the delta-loaded epoch as the next base
+    ctx.load(img3, 24, activate=False)             # the same image, loaded in full
+    sars = (synth.random_sars(1500, seed=5002, pop=pop) + _targeted(docs3, (40, 120, len(docs3) - 1), 60, 10))
+    items = _items(sars)
+    got = {}
+    for ep in (23, 24):
+        ctx.activate(ep)
+        b = _batch(ctx, items)
+        b.submit()
+        b.wait()
+        got[ep] = _results(b)
+        b.close()
+    assert got[23] == got[24]
+    want = _want(docs3, items)
+    assert got[23] == want
+    # refusals: no such base, another base, a corrupted literal / operation
+    with pytest.raises(cedargpu.CedarGPUError):
+        ctx.load_delta(999, d12, 30)
+    with pytest.raises(cedargpu.CedarGPUError):
+        ctx.load_delta(23, d12, 31)
+    bad = bytearray(d23)
+    bad[-1] ^= 0xFF
+    with pytest.raises(cedargpu.CedarGPUError):
+        ctx.load_delta(22, bytes(bad), 32)
+    ctx.activate(23)

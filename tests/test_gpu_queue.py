@@ -125,9 +125,21 @@ def test_queue_loadgen_counts_match_batch(ctx):
     q = cedargpu.Queue(ctx, max_batch=512)
     r = q.loadgen([json.dumps(s) for s in sars], threads=32, total=2 * len(sars))
     st = q.stats()
+    m = q.metrics()
     q.close()
     assert [r["deny"], r["allow"], r["no_opinion"]] == [2 * w for w in want]
     assert st["batches"] >= 8 and st["max_batch"] <= 512
+    # metrics (cg_queue_metrics_get): request_total by decision = the loadgen's counts, every call in
+    # exactly one latency bucket, batches in the size histogram, the active epoch
+    assert [m["requests"][k] for k in ("deny", "allow", "no_opinion")] == [2 * w for w in want]
+    assert m["requests"]["error"] == 0
+    for k in ("deny", "allow", "no_opinion"):
+        assert sum(m["latency"][k]) == m["requests"][k]
+        assert m["latency_sum_ns"][k] > 0 or m["requests"][k] == 0
+    assert sum(m["batch_size"]) == m["batches"] == st["batches"]
+    assert sum(m["batch_size"][10:]) == 0  # max_batch 512 = 2^9
+    assert sum(m["batch_latency"]) == m["batches"] and m["batch_latency_sum_ns"] > 0
+    assert m["active_epoch"] == 103 and m["activations"] >= 1
 
 
 def test_queue_errors(ctx):

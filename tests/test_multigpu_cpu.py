@@ -85,10 +85,20 @@ def _queue_worker(rank, world, port, out):
         pop = synth.Population(seed=3, n_users=200, n_groups=20)
         text = synth.abac_policies(300, seed=3, pop=pop)
 
-        def reload(epoch, extra=""):
-            blob = [cg.build_image([cg.MemoryStore("c3.cedar", text + extra)], epoch=epoch) if rank == 0 else None]
-            dist.broadcast_object_list(blob, src=0)
-            ctxs[0].load(blob[0], epoch)       # new requests encode against it from here on
+        comp = cg.Compiler() if rank == 0 else None
+        prev = {}
+
+        def reload(epoch, extra="", delta=False):
+            # the second reload travels as a delta image against the first (cg_image_load_delta)
+            blob = comp.build([cg.MemoryStore("c3.cedar", text + extra)], epoch=epoch) if rank == 0 else None
+            msg = [cg.image_delta(prev["blob"], blob) if (rank == 0 and delta) else blob]
+            if rank == 0:
+                prev["blob"] = blob
+            dist.broadcast_object_list(msg, src=0)
+            if delta:
+                ctxs[0].load_delta(epoch - 1, msg[0], epoch)
+            else:
+                ctxs[0].load(msg[0], epoch)    # new requests encode against it from here on
             ctxs[1].load_peer(ctxs[0], epoch)  # the second GPU follows (its batches fall back meanwhile)
 
         ctxs = [cg.Context(2 * rank), cg.Context(2 * rank + 1)]
@@ -108,11 +118,13 @@ def _queue_worker(rank, world, port, out):
         th = [threading.Thread(target=caller, args=(k,)) for k in range(8)]
         for t in th:
             t.start()
-        reload(2, '\nforbid (principal, action == k8s::Action::"reload-check", resource);')
+        reload(2, '\nforbid (principal, action == k8s::Action::"reload-check", resource);', delta=True)
         for t in th:
             t.join()
         stats = q.gpu_stats()
         q.close()
+        if comp:
+            comp.close()
         active = []
         for c in ctxs:
             e = cg._lib.u64()
