@@ -466,7 +466,7 @@ def main():
     sizing.submit()
     sizing.wait()
     sizing.close()
-    payload = synth.sars_json(sars)  # the SAR bodies as the webhook receives them (not timed)
+    payload = synth.sars_json(sars).encode()  # the SAR bodies as the webhook receives them: bytes (not timed)
     t_build = time.perf_counter()
     b = ctx.batch()
     b.add_sar_json(payload)  # cg_batch_add_sar_json: SAR conversion + columnar encode, host threads
@@ -512,7 +512,7 @@ def main():
     # copy and the result binding. Outside the timed region (PCIe-inclusive; not `value`).
     s2r = None
     if rank == 0 and args.submit_to_results:
-        payload2 = synth.sars_json(sars)
+        payload2 = synth.sars_json(sars).encode()
         b2 = ctx.batch()
         t0e = time.perf_counter()
         b2.add_sar_json(payload2)

@@ -29,8 +29,9 @@ def _timeout_ns(timeout: Optional[float]) -> int:
 _P = ctypes.c_void_p
 
 
-def _b(s: str) -> bytes:
-    return s.encode("utf-8")
+def _b(s) -> bytes:
+    """UTF-8 bytes of a str; bytes (a request body as received) pass through without a copy."""
+    return s if isinstance(s, (bytes, bytearray)) else s.encode("utf-8")
 
 
 def device_count() -> int:
@@ -412,14 +413,15 @@ class Batch:
     def add(self, entities: list, request: dict):
         self.add_json(json.dumps({"entities": entities, "request": request}))
 
-    def add_sar_json(self, payload: str):
-        """SubjectAccessReview JSON (object or array) -> entities via the C++ model (sar.cpp)."""
+    def add_sar_json(self, payload):
+        """SubjectAccessReview JSON (object or array; str, or bytes as received) -> entities via the
+        C++ model (sar.cpp)."""
         b = _b(payload)
         rc = lib.cg_batch_add_sar_json(self._h, b, len(b))
         if rc:
             raise _err(rc, "SubjectAccessReview encode failed")
 
-    def add_admission_json(self, payload: str):
+    def add_admission_json(self, payload):
         """AdmissionReview JSON (object or array) -> entities via the C++ model (admission.cpp)."""
         b = _b(payload)
         rc = lib.cg_batch_add_admission_json(self._h, b, len(b))

@@ -113,6 +113,7 @@ struct QMetrics {
   std::atomic<uint64_t> req[4]{}, lat[4][CG_LAT_BOUNDS + 1]{}, lat_sum[4]{};
   std::atomic<uint64_t> bsize[CG_BATCH_BUCKETS + 1]{}, blat[CG_LAT_BOUNDS + 1]{}, blat_sum{0};
   void request(uint32_t outcome, uint64_t ns) {
+    if (outcome > 3) return;
     req[outcome].fetch_add(1, std::memory_order_relaxed);
     lat[outcome][lat_bucket(ns)].fetch_add(1, std::memory_order_relaxed);
     lat_sum[outcome].fetch_add(ns, std::memory_order_relaxed);
@@ -559,9 +560,12 @@ int is_authorized_json(cg_queue* q, const char* item_json, size_t len, int64_t t
   return submit_ticket(q, tp, deadline, allow, diag, cap, need, false);
 }
 
-// outcome index of a call (cg_queue_metrics.requests): the decision when it is valid
+// outcome index of a call (cg_queue_metrics.requests): the decision when it is valid; 4: not
+// recorded (CG_E_RANGE: the caller repeats the call with room for the reason, which is the one
+// counted)
 uint32_t outcome(int rc, int d, bool admission) {
-  if (rc != CG_OK && rc != CG_E_RANGE) return 3u;
+  if (rc == CG_E_RANGE) return 4u;
+  if (rc != CG_OK) return 3u;
   if (admission) return d ? 1u : 0u;
   return (d >= 0 && d < 3) ? (uint32_t)d : 3u;
 }

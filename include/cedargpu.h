@@ -353,7 +353,8 @@ int cg_queue_dropped(cg_queue* q, uint64_t* abandoned);
  * A snapshot of the queue's serving metrics for a Prometheus exporter on the host side:
  * - request_total{decision} and request_duration_seconds{decision}: every cg_queue_authorize_sar /
  *   cg_queue_is_authorized_json call, by outcome (Deny, Allow, NoOpinion, error; an admission call's
- *   allow counts as Allow, its deny as Deny), with its latency from entry to return. The reference
+ *   allow counts as Allow, its deny as Deny), with its latency from entry to return; a call that
+ *   returns CG_E_RANGE is not counted (its repeat with room for the reason is). The reference
  *   records only non-Deny decisions and errors (server.go:81-90): its exporter skips index 0.
  * - the batch-size and batch-latency (submit -> results published) histograms and the active
  *   image epoch that SURVEY §5 asks for beside them.

@@ -69,6 +69,47 @@ def test_c4_admission_forbids(ctx):
     assert _check(ctx, text, synth.admission_reviews(1500, seed=12)) > 0
 
 
+def test_c4_bench_size_vs_cpp_oracle(ctx):
+    """C4 at its bench configuration (BENCH configs.c4_admission_1k): 1,000 admission forbids plus
+    the allow-all tier over 4,096 ConfigMap / Secret reviews of the bench's generator, where about
+    half of the requests collect more hits than the first pass holds and finish in the large stage.
+    Every review's (allowed, code, message) against the C++ oracle (oracle/cedar_ref.cpp) through
+    handler.go:43-80's mapping (km.admission_handle)."""
+    from cedar_ref import RefPolicySet, items_json
+    text = synth.admission_policies(1000, seed=3)
+    reviews = synth.admission_reviews(4096, seed=4000)
+    h = cedargpu.AdmissionHandler(_stores(text), ctx=ctx)
+    got = h.handle_batch(reviews)
+    want, items, idx = {}, [], []
+    for i, r in enumerate(reviews):
+        req = km.admission_request_from_review(r)
+        if req.namespace in ("kube-system", "cedar-k8s-authz-system"):
+            want[i] = (True, 200, "")
+            continue
+        try:
+            em, creq = km.admission_to_cedar(req)
+        except (km.WalkError, KeyError):
+            want[i] = (False, 500, None)
+            continue
+        items.append((co.entities_to_json(em), co.request_to_json(creq)))
+        idx.append(i)
+    ref = RefPolicySet.from_stores(_stores(text))
+    ref.load_items(items_json(items))
+    for i, (ok, _, _, reasons) in zip(idx, ref.evaluate(16)):
+        want[i] = (ok, 200, reasons if not ok and reasons not in ("", "[]", "null") else "")
+    ref.close()
+    n_deny = n_long = 0
+    for i, g in enumerate(got):
+        w = want[i]
+        if w[1] == 500:
+            assert g[:2] == (False, 500), (i, g)
+            continue
+        assert tuple(g) == w, (i, reviews[i], g, w)
+        n_deny += not g[0]
+        n_long += not g[0] and g[2].count('"policy"') > 64  # more reasons than the first pass holds
+    assert n_deny > 1000 and n_long > 0, (n_deny, n_long)
+
+
 def test_admission_variants(ctx):
     text = "\n".join(v for k, v in sorted(CORPUS["demo"].items()) if k.startswith("admission"))
     out, errs = _variants()

@@ -19,7 +19,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
                                entities=pop.static_entities())
     ctx = cedargpu.Context(0)
     ctx.load(img, 1)
-    payload = synth.sars_json(synth.random_sars(N, seed=1000, pop=pop))
+    payload = synth.sars_json(synth.random_sars(N, seed=1000, pop=pop)).encode()
     out = []
     for rep in range(3):
         b = ctx.batch()
