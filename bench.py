@@ -554,6 +554,28 @@ def main():
                 nxt.add_sar_json(chunks[(k + 1) % len(chunks)])
         lat.sort()
 
+    # small batches (the serving path's sizes): the complete step's device time (HIP events, one
+    # launch below CEDARGPU_SMALL_N = 2,048 requests) and submit -> results wall time per size
+    small = None
+    if rank == 0 and args.latency_batches:
+        small = {}
+        for n in (64, 256, 2048):
+            chunks = [synth.sars_json(sars[k * n:(k + 1) * n]).encode() for k in range(8)]
+            sl, dev = [], None
+            for it in range(80):
+                sb = ctx.batch()
+                sb.add_sar_json(chunks[it % 8])
+                t1 = time.perf_counter()
+                sb.submit()
+                sb.wait()
+                sl.append((time.perf_counter() - t1) * 1e3)
+                if it == 79:
+                    dev = sb.time(50) / 50
+                sb.close()
+            sl = sorted(sl[16:])
+            small[str(n)] = {"device_step_ms": dev, "device_us_per_batch": dev * 1e3, "s2r_p50_ms": sl[len(sl) // 2],
+                             "s2r_p90_ms": sl[int(len(sl) * 0.9)]}
+
     serving = None
     if rank == 0 and args.serve_threads and args.serve_requests:
         serving = serve(ctx, sars, args.serve_threads, args.serve_requests, args.serve_max_batch)
@@ -574,8 +596,8 @@ def main():
         dom = max((k for k in phases if k != "total"), key=phases.get) if len(phases) > 1 else "total"
         dom_ms = phases.get(dom, avg_kernel_ms)
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-        dom_kernel = {"scan": "cedar_scan_kernel<8, 6, true>", "candidates": "cedar_probe_kernel<8, 64, 4, SPLIT>",
-                      "fu_big": "cedar_probe_kernel<64, 1024, 4, SPLIT, SLIM>", "group": "rocPRIM onesweep + cedar_group_gather"}.get(dom, dom)
+        dom_kernel = {"scan": "cedar_scan_kernel<8, 6, true>", "candidates": "cedar_probe_kernel<8, 64, 4, SPLIT> (pooled)",
+                      "fu_big": "cedar_probe_kernel<64, 1024, 4, SPLIT, SLIM>", "group": "rocPRIM onesweep"}.get(dom, dom)
         traffic, pmc_kernels = None, None
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
         if os.path.exists(pmc):
@@ -625,8 +647,8 @@ def main():
                        "rerun_requests": host_reruns,
                        "request_order": (f"{args.order} as uploaded; batches of >= 65,536 requests are grouped on the "
                                          "device inside every timed step (rocPRIM radix sort of the encoder's per-request "
-                                         "key over (action, resource type), principal key ancestors, hot values, and a "
-                                         "gather of the rows into that order)" if os.environ.get("CEDARGPU_GROUP_DEV", "1") != "0"
+                                         "key over (action, resource type), principal key ancestors, hot values; the "
+                                         "first-pass kernels read the rows through that order)" if os.environ.get("CEDARGPU_GROUP_DEV", "1") != "0"
                                          else f"{args.order}; host radix sort at submit, outside the timed step (A/B)"),
                        "parallelism": f"request-sharded x{world}, image replicated"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -638,8 +660,8 @@ def main():
                          "phases_ms": phases, "phases_total_ms": split_total / split_steps,
                          "valu": valu,
                          "launch": "one complete step on one stream: the device grouping (rocPRIM onesweep sort of the encoder's "
-                                   "keys + cedar_group_gather), cedar_scan_kernel, the SPLIT candidate pass, cedar_fu_gather and "
-                                   "the follow-up launches (rocprofv3 split in profiles/r04/)",
+                                   "keys), cedar_scan_kernel, the SPLIT candidate pass, cedar_fu_gather and the follow-up "
+                                   "launches (rocprofv3 kernel stats in profiles/r04/)",
                          "achieved_is": "SURVEY §8(d) algorithmic bytes of every decision in the step / the dominant kernel's "
                                         "time (HIP events at its phase boundaries); step_achieved: over the whole step",
                          "traffic_source": "PMC FETCH_SIZE x2 + WRITE_SIZE summed over one step's dispatches "
@@ -654,6 +676,7 @@ def main():
             "reload": reload,
             "serving": serving,
             "configs": configs,
+            "small_batches": small,
             "latency": {"batch": args.latency_batch, "p50_ms": lat[len(lat) // 2] if lat else None,
                         "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
                         "p999_ms": lat[min(len(lat) - 1, int(len(lat) * 0.999))] if lat else None,

@@ -3338,7 +3338,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   }
   if (grp) {  // the device grouping's order, grouped rows, bucket counters and scan storage
     const size_t tb = group_temp_bytes(b.n());
-    const size_t q = ((size_t)b.n() * 4 + 255) & ~(size_t)255, rq = al((size_t)b.n() * b.row_words * 4);
+    const size_t q = ((size_t)b.n() * 4 + 255) & ~(size_t)255, rq = group_gather() ? al((size_t)b.n() * b.row_words * 4) : 0;
     if (!tb) { g_err = "rocPRIM radix sort: no temporary storage size"; pool_put(pool, false, d.lane_blk, d.lane_cls); pool_put(pool, false, d.scan_blk, d.scan_cls); return -4; }
     if ((rc = pool_get(pool, false, 3 * q + rq + tb, &d.grp_blk, &d.grp_cls))) {
       pool_put(pool, false, d.lane_blk, d.lane_cls);
@@ -3349,7 +3349,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     d.ord = (uint32_t*)g8;
     d.gkeys2 = (uint32_t*)(g8 + q);
     d.gvals = (uint32_t*)(g8 + 2 * q);
-    d.grows = (uint32_t*)(g8 + 3 * q);
+    d.grows = group_gather() ? (uint32_t*)(g8 + 3 * q) : nullptr;
     d.grp_temp = g8 + 3 * q + rq;
     d.grp_temp_bytes = tb;
   }
@@ -3892,7 +3892,7 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
       return -4;
     }
     k.ord = b.ord;
-    k.grows = b.grows;
+    k.grows = group_gather() ? b.grows : nullptr;
   }
   mark(PH_GROUP, s);
   // the worklist counters and the scan's bad-index count start at zero before the first pass

@@ -191,6 +191,7 @@ int dev_time_split(const DevImage& img, DevBatch& b, uint32_t iters, void* strea
 // group.hip: the device grouping of a batch (a radix sort of the encoder's 32-bit grouping keys,
 // rows copied into the new order)
 uint32_t group_bits();
+bool group_gather();  // the grouped rows are copied into order (else read through the order)
 size_t group_temp_bytes(uint32_t n);
 int group_enqueue(const uint32_t* keys, const uint32_t* rows, uint32_t n, uint32_t row_words, uint32_t* grows,
                   uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream);

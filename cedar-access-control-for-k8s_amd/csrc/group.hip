@@ -8,11 +8,12 @@
 //
 // Here the order is computed on the device in every step from the 32-bit grouping key the encoder
 // writes per request (Batch::gkeys: a hash of fields it encodes anyway, on the encoding threads):
-//   1. rocPRIM's radix sort (onesweep, stable) orders (key, request) pairs: ord[k] = the request
-//      evaluated k-th;
-//   2. a gather copies each request's row to its position (grows), so the first-pass kernels read
-//      rows contiguously in group order while results and scan lists stay at each request's own
-//      index.
+// rocPRIM's radix sort (onesweep, stable) orders (key, request) pairs: ord[k] = the request
+// evaluated k-th. The first-pass kernels read each request's row through the order (whole 64-byte
+// lines at random); results and scan lists stay at each request's own index. (Round 3 copied the
+// rows into order first, so that those kernels read them contiguously: the copy cost 0.077 ms per
+// 1M and 0.26 GB of traffic, and saved the kernels 0.016 ms: 690 vs 718 M decisions/s on C3,
+// gpurun_out/r04gab; CEDARGPU_GROUP_GATHER=1 brings it back.)
 // A bucket sort with one atomic per request into 2^20-2^22 counters was 3-5x slower: popular
 // principals' identical keys serialize their atomics (0.52-1.34 ms per 1M, profiles/r03/ab6).
 #include <hip/hip_runtime.h>
@@ -58,6 +59,12 @@ uint32_t group_bits() {
   return b;
 }
 
+// CEDARGPU_GROUP_GATHER=1: the rows copied into group order (grows) for the first-pass kernels
+bool group_gather() {
+  static const bool g = [] { const char* e = std::getenv("CEDARGPU_GROUP_GATHER"); return e && *e == '1'; }();
+  return g;
+}
+
 // Temporary storage rocPRIM's radix sort needs for n pairs (onesweep at every size: the default
 // takes its merge-sort path up to 2^20 pairs, ~0.16 ms per 1M on gfx950, profiles/r03/ab1).
 size_t group_temp_bytes(uint32_t n) {
@@ -80,6 +87,7 @@ int group_enqueue(const uint32_t* keys, const uint32_t* rows, uint32_t n, uint32
   if (rocprim::radix_sort_pairs<SortConfig>(temp, bytes, const_cast<uint32_t*>(keys), keys2, rocprim::counting_iterator<uint32_t>(0u), ord,
                                             n, 32 - group_bits(), 32, s) != hipSuccess)
     return -1;
+  if (!group_gather()) return hipGetLastError() == hipSuccess ? 0 : -1;
   hipLaunchKernelGGL(cedar_group_gather, dim3((n + 256 / GSEG - 1) / (256 / GSEG)), dim3(256), 0, s, ord, n,
                      reinterpret_cast<const uint4*>(rows), row_words / 4, reinterpret_cast<uint4*>(grows));
   return hipGetLastError() == hipSuccess ? 0 : -1;
