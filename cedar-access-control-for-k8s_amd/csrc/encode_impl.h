@@ -180,13 +180,22 @@ struct EncCache {
     for (size_t i = 0; i < n_static; i++) delete srec[i].load();
   }
 };
+// (per thread, the last image's cache without touching the shared_ptr: libstdc++'s atomic
+// shared_ptr operations take a mutex from a small address-hashed pool, one and the same for every
+// thread encoding against one image, and copying the pointer bounces its reference count between
+// the cores; the thread keeps its own reference until it encodes against another image)
 inline EncCache& enc_cache(const Image& img) {
+  thread_local uint64_t t_id = 0;
+  thread_local std::shared_ptr<EncCache> t_keep;
+  if (t_keep && img.cache_id && t_id == img.cache_id) return *t_keep;
   std::shared_ptr<EncCache> p = std::atomic_load(&img.enc_cache);
   if (!p) {
     auto n = std::make_shared<EncCache>(img.n_static());
     if (std::atomic_compare_exchange_strong(&img.enc_cache, &p, n)) p = n;  // (else p: the winner's)
   }
-  return *p;  // (the image keeps it alive)
+  t_keep = p;
+  t_id = img.cache_id;
+  return *p;
 }
 namespace enc {
 // set on a thread to encode with the general walk only (cg_encode_sar_check compares the two)

@@ -8,6 +8,7 @@
 // strings compare by ID), then request-locally, so encoding needs no batch-wide state: any thread
 // encodes a request (encode_request) and the batch appends it with copies (Batch::append). Each entity row carries a pointer to its
 // transitive ancestor list (the closure of `parents` through the map), so `in` is a linear scan.
+#include <sys/mman.h>
 #include <algorithm>
 #include <atomic>
 #include <thread>
@@ -15,6 +16,32 @@
 #include "encode_impl.h"
 
 namespace cg {
+
+bool hugepages_on() {
+  static const bool on = [] { const char* e = std::getenv("CEDARGPU_HUGEPAGES"); return e && *e == '1'; }();
+  return on;
+}
+
+// 2 MiB-aligned (the tag huge_unmap checks: the heap never returns such a block), advised huge
+void* huge_map(size_t bytes) {
+  constexpr size_t H = 2u << 20;
+  const size_t len = (bytes + H - 1) & ~(H - 1);
+  void* raw = mmap(nullptr, len + H, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (raw == MAP_FAILED) return nullptr;
+  const uintptr_t r = (uintptr_t)raw, a = (r + H - 1) & ~(uintptr_t)(H - 1);
+  if (a > r) munmap(raw, a - r);
+  if (r + len + H > a + len) munmap((void*)(a + len), r + len + H - (a + len));
+  (void)madvise((void*)a, len, MADV_HUGEPAGE);
+  return (void*)a;
+}
+
+bool huge_unmap(void* p, size_t bytes) {
+  constexpr size_t H = 2u << 20;
+  if (!p || ((uintptr_t)p & (H - 1))) return false;
+  munmap(p, (bytes + H - 1) & ~(H - 1));
+  return true;
+}
+
 using namespace cgi;
 
 void emit_heap_value(const HVal& v, std::vector<uint32_t>& out, const Image& img, EncodedRequest& e, uint32_t& w0,

@@ -21,9 +21,16 @@ namespace cg {
 // beyond, so a principal in thousands of groups encodes in time linear in its size.
 constexpr size_t DEDUP_SCAN = 32;
 
+// huge-page-backed anonymous mappings (encoder.cpp): huge_map returns null on failure (the caller
+// falls back to the heap); huge_unmap returns false for a block huge_map did not make
+bool hugepages_on();
+void* huge_map(size_t bytes);
+bool huge_unmap(void* p, size_t bytes);
+
 // An allocator whose resize() leaves new elements uninitialised: a batch's large arrays are
 // written in full right after they grow (Batch::concat), so zero-filling them first would be a
 // serial pass over hundreds of MB.
+
 template <class T>
 struct NoInitAlloc : std::allocator<T> {
   template <class U> struct rebind { using other = NoInitAlloc<U>; };
@@ -31,6 +38,23 @@ struct NoInitAlloc : std::allocator<T> {
   template <class U> NoInitAlloc(const NoInitAlloc<U>&) {}
   template <class U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
   template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+  // CEDARGPU_HUGEPAGES=1: blocks of >= 2 MiB (a bulk encode's batch parts and the concatenated
+  // batch: ~1 GB per 1M SARs) from huge-page-backed mappings, whose first touches fault 2 MiB at a
+  // time (A/B: with the kernel's synchronous compaction on advised regions it can lose).
+  T* allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes >= huge_min() && huge_on()) {
+      if (void* p = huge_map(bytes)) return static_cast<T*>(p);
+    }
+    return std::allocator<T>::allocate(n);
+  }
+  void deallocate(T* p, size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes >= huge_min() && huge_on() && huge_unmap(p, bytes)) return;
+    std::allocator<T>::deallocate(p, n);
+  }
+  static constexpr size_t huge_min() { return 2u << 20; }
+  static bool huge_on() { return hugepages_on(); }
 };
 template <class T> using PodVec = std::vector<T, NoInitAlloc<T>>;
 
