@@ -904,14 +904,30 @@ int cg_image_load_delta(cg_ctx* ctx, uint64_t base_epoch, const void* delta, siz
   }
   std::shared_ptr<Image> img;
   try {
-    std::vector<uint8_t> host(plan.new_len);
-    if (dev_to_host(ctx->device, nb, host.size(), host.data())) {
-      dev_free(ctx->device, nb);
-      ctx->err = dev_last_error();
-      return CG_E_DEVICE;
-    }
-    if (blob_sum(host.data(), host.size()) != plan.new_sum) throw CedarError("delta image does not reproduce the new image (checksum)");
-    img = Image::deserialize(host.data(), host.size());
+    // the new blob's checksum on the device; then the host reads back only what deserialize reads:
+    // the header and section table, the sections the host keeps, and the host part (not the policy
+    // stream or the scope index: ~70 % of a large image)
+    uint64_t sum = 0;
+    if (dev_blob_sum(ctx->device, nb, (size_t)plan.new_len, &sum)) throw std::runtime_error(dev_last_error());
+    if (sum != plan.new_sum) throw CedarError("delta image does not reproduce the new image (checksum)");
+    std::unique_ptr<uint8_t[]> host(new uint8_t[std::max<uint64_t>(plan.new_len, 1)]);
+    const size_t n = (size_t)plan.new_len, table = 16 + 16 * ((size_t)cgi::DS_COUNT + 1);
+    auto d2h = [&](size_t lo, size_t hi) {
+      if (hi > lo && dev_to_host(ctx->device, (const uint8_t*)nb + lo, hi - lo, host.get() + lo)) throw std::runtime_error(dev_last_error());
+    };
+    if (n < table) throw CedarError("truncated image");
+    d2h(0, table);
+    uint64_t off[cgi::DS_COUNT + 1];
+    for (uint32_t k = 0; k < cgi::DS_COUNT; k++) std::memcpy(&off[k], host.get() + 16 + 16 * k, 8);
+    std::memcpy(&off[cgi::DS_COUNT], host.get() + 16 + 16 * cgi::DS_COUNT + 8, 8);  // the device region's end
+    bool ok = true;
+    for (uint32_t k = 0; k < cgi::DS_COUNT; k++) ok = ok && off[k] <= off[k + 1] && off[k + 1] <= n;
+    if (!ok || off[0] < table) throw CedarError("corrupt image (device region)");
+    static_assert(cgi::DS_PSTREAM == 0 && cgi::DS_BTAB + 1 == cgi::DS_BFILT && cgi::DS_BFILT + 1 == cgi::DS_BSTREAM, "section order");
+    d2h(table, (size_t)off[cgi::DS_PSTREAM]);
+    d2h((size_t)off[cgi::DS_PSTREAM + 1], (size_t)off[cgi::DS_BTAB]);
+    d2h((size_t)off[cgi::DS_BSTREAM + 1], n);
+    img = Image::deserialize(host.get(), n);
   } catch (const std::exception& e) {
     dev_free(ctx->device, nb);
     ctx->err = e.what();

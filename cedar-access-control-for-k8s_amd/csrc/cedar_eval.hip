@@ -113,6 +113,7 @@ struct KArgs {
 // itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
 // the large stage, which reads the list when it holds them all
 constexpr uint32_t SCAN_CAP = 96, SCAN_OVF = 0xFFFFFFFFu, SCAN_COUNT = (1u << 27) - 1, SCAN_COMBO_SHIFT = 27;
+static_assert(SCAN_CAP >= 64, "the SPLIT probe kernel reads one pair per lane (up to 64) before it knows the count");
 // scan[i] | SCAN_HEAVY: the request's buckets hold more than a.scan_heavy candidate heads, so it
 // goes straight to the large stage (the candidate pass would overflow its 64 hits and be redone)
 constexpr uint32_t SCAN_HEAVY = 0x40000000u;
@@ -2093,6 +2094,16 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   // segments narrower than the header hold its upper words in a second register
   const uint32_t rw_hi = (SEG < RW_HDR && valid && SEG + sl < RW_HDR) ? __builtin_nontemporal_load(row + SEG + sl) : 0u;
   auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
+  // SPLIT: the scan list's count and each lane's first bucket pair, issued with the row loads (they
+  // depend only on r), so the staging below does not wait for a second trip after the row's
+  uint32_t scan_nb0 = 0;
+  uint2 scan_q0 = make_uint2(0u, 0u);
+  if constexpr (SPLIT) {
+    if (valid) {
+      scan_nb0 = a.scan[r];
+      scan_q0 = *reinterpret_cast<const uint2*>(a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP) + 2 * sl);
+    }
+  }
   PCtx c;
   c.blk = a.heap + hdr(RW_BLK);
   c.rowb = (a.grows && !a.req_idx) ? a.grows : a.rows;
@@ -2499,7 +2510,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     // the scan kernel found this request's buckets (cedar_scan_kernel): stage them EC at a time.
     // More buckets than the scan holds: the one-request-per-wave variant probes the index itself,
     // narrower segments hand the request to that variant (the large-stage follow-up).
-    const uint32_t nb0 = valid ? a.scan[r] : 0u;
+    const uint32_t nb0 = scan_nb0;
     const bool heavy = nb0 != SCAN_OVF && (nb0 & SCAN_HEAVY);
     const uint32_t nb = nb0 == SCAN_OVF ? SCAN_OVF : (nb0 & ~SCAN_HEAVY);
     if (SEG == 64 && nb == SCAN_OVF) probe_loop = true;
@@ -2515,7 +2526,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
       for (uint32_t i = sl; i < L::EC; i += SEG)
         if (b0 + i < nbk) {
-          const uint2 q = *reinterpret_cast<const uint2*>(pairs + 2 * (b0 + i));
+          const uint2 q = (b0 == 0 && i == sl) ? scan_q0 : *reinterpret_cast<const uint2*>(pairs + 2 * (b0 + i));
           wl.u.b.efirst[seg][i] = q.x | ((q.y >> SCAN_COMBO_SHIFT) << EF_COMBO);
           wl.u.b.epre[seg][i] = q.y & SCAN_COUNT;
         }
@@ -3157,6 +3168,52 @@ void dev_free(int device, void* p) {
   if (!p) return;
   (void)hipSetDevice(device);
   (void)hipFree(p);
+}
+
+// delta.h blob_word_mix, on the device (the same formula: the two must agree bit for bit)
+__device__ __forceinline__ uint64_t dev_word_mix(uint64_t w, uint64_t i) {
+  uint64_t z = w ^ (i * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// blob_sum (delta.h) on the device: 16-byte loads (two words) over a grid-stride loop, a wave
+// reduction, one 64-bit atomic add per wave; the zero-padded last word by thread 0
+__global__ void __launch_bounds__(256) cedar_blob_sum(const uint8_t* __restrict__ p, uint64_t n, unsigned long long* __restrict__ out) {
+  const uint64_t nq = n / 16;
+  uint64_t acc = 0;
+  for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (uint64_t)gridDim.x * 256) {
+    const uint4 v = reinterpret_cast<const uint4*>(p)[q];
+    acc += dev_word_mix(((uint64_t)v.y << 32) | v.x, 2 * q) + dev_word_mix(((uint64_t)v.w << 32) | v.z, 2 * q + 1);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (uint64_t o = nq * 16; o < n; o += 8) {
+      uint64_t w = 0;
+      for (uint64_t b = 0; b < 8 && o + b < n; b++) w |= (uint64_t)p[o + b] << (8 * b);
+      acc += dev_word_mix(w, o / 8);
+    }
+  for (uint32_t o = 32; o > 0; o >>= 1) acc += (uint64_t)__shfl_xor((long long)acc, (int)o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
+int dev_blob_sum(int device, const void* p, size_t n, uint64_t* out) {
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  unsigned long long* d = nullptr;
+  HIPCHK(hipMalloc((void**)&d, 8), "hipMalloc");
+  hipError_t e = hipMemset(d, 0, 8);
+  if (e == hipSuccess) {
+    const uint64_t nq = n / 16;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (nq + 255) / 256));
+    hipLaunchKernelGGL(cedar_blob_sum, dim3(blocks), dim3(256), 0, 0, (const uint8_t*)p, (uint64_t)n, d);
+    e = hipGetLastError();
+  }
+  unsigned long long v = 0;
+  if (e == hipSuccess) e = hipMemcpy(&v, d, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(e, "blob checksum");
+  *out = (uint64_t)v + (uint64_t)n;
+  return 0;
 }
 
 int dev_to_host(int device, const void* src, size_t n, void* dst) {

@@ -249,15 +249,21 @@ void diff_region(const uint8_t* N, const uint8_t* B, const Region& r, RBuf& o) {
 }  // namespace
 
 uint64_t blob_sum(const uint8_t* p, size_t n) {
-  constexpr size_t C = 4u << 20;
+  constexpr size_t C = 4u << 20;  // bytes per task (a multiple of 8)
   const size_t nc = (n + C - 1) / C;
-  std::vector<uint64_t> hc(nc);
-  parallel_for(nc, 1, [&](size_t k) { hc[k] = hash_bytes(p + k * C, std::min(C, n - k * C), 0x51ED270B27B4A3C1ull + k); });
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
-  for (uint64_t x : hc) {
-    h = (h ^ x) * 0x94D049BB133111EBull;
-    h ^= h >> 29;
-  }
+  std::vector<uint64_t> part(nc, 0);
+  parallel_for(nc, 1, [&](size_t k) {
+    const size_t lo = k * C, hi = std::min(n, lo + C);
+    uint64_t acc = 0;
+    for (size_t o = lo; o < hi; o += 8) {
+      uint64_t w = 0;
+      std::memcpy(&w, p + o, std::min<size_t>(8, hi - o));
+      acc += blob_word_mix(w, o / 8);
+    }
+    part[k] = acc;
+  });
+  uint64_t h = n;
+  for (uint64_t x : part) h += x;
   return h;
 }
 

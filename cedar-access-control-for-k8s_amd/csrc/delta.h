@@ -21,10 +21,18 @@
 namespace cg {
 
 constexpr uint32_t DL_MAGIC = 0x4C444743u;  // "CGDL"
-constexpr uint32_t DL_VERSION = 2;
+constexpr uint32_t DL_VERSION = 3;
 constexpr size_t DL_HEAD = 56;
 
-// 64-bit checksum of a blob (4 MiB chunks hashed on up to 16 threads, then combined in order)
+// 64-bit checksum of a blob: the sum (mod 2^64) over its 8-byte little-endian words (the last one
+// zero-padded) of mix(word ^ index * K), plus the length. Order-keyed by the index and
+// associative, so up to 16 host threads or a GPU kernel (dev_blob_sum) compute it in any split.
+inline uint64_t blob_word_mix(uint64_t w, uint64_t i) {
+  uint64_t z = w ^ (i * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
 uint64_t blob_sum(const uint8_t* p, size_t n);
 
 // The delta that turns `base` into `next`. Both are image blobs: the diff pairs their regions

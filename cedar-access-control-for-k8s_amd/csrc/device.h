@@ -127,6 +127,8 @@ constexpr uint64_t DL_PIECE = 64 * 1024;
 int dev_blob_patch(int device, const DevImage& base, const uint64_t* pieces, size_t n_pieces, const uint8_t* lit,
                    size_t lit_len, const uint32_t* fix, size_t n_fix, size_t new_len, void** out);
 void dev_free(int device, void* p);
+// blob_sum (delta.h) of n bytes of device memory, computed on the device
+int dev_blob_sum(int device, const void* p, size_t n, uint64_t* out);
 // Copies n bytes of device memory on `device` to host memory (pinned staging, one copy).
 int dev_to_host(int device, const void* src, size_t n, void* dst);
 void dev_image_free(DevImage* d);

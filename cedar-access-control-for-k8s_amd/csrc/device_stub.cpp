@@ -17,6 +17,7 @@
 #include <thread>
 
 #include "../../include/cedargpu.h"
+#include "delta.h"
 #include "device.h"
 #include "engine.h"
 
@@ -94,6 +95,10 @@ int dev_blob_patch(int, const DevImage& base, const uint64_t* pieces, size_t n_p
   return 0;
 }
 void dev_free(int, void* p) { std::free(p); }
+int dev_blob_sum(int, const void* p, size_t n, uint64_t* out) {
+  *out = blob_sum((const uint8_t*)p, n);
+  return 0;
+}
 // the stub's "device memory" is host malloc memory (cg_image_load_device callers of the stub pass it)
 int dev_image_adopt(int device, const Image& img, void* dev_blob, DevImage* out) {
   DevImage d;
