@@ -56,6 +56,7 @@ uint64_t hash_bytes(const uint8_t* p, size_t n, uint64_t seed) {
 // ---- regions: the image blob's header, device sections and host part (image.h DevSection) ----
 struct Region {
   size_t nb, ne, bb, be;  // [nb, ne) of the new blob against [bb, be) of the base
+  int64_t shift0 = 0;     // base offset (from bb) the comparison of nb starts at
 };
 
 // section offsets of an image blob, or false when it is not one
@@ -162,7 +163,7 @@ void diff_region(const uint8_t* N, const uint8_t* B, const Region& r, RBuf& o) {
   bool indexed = false;
   uint64_t pw = 1;  // RP^(WIN-1)
   for (size_t i = 1; i < WIN; i++) pw *= RP;
-  int64_t shift = 0;  // base position = new position + shift
+  int64_t shift = r.shift0;  // base position = new position + shift
   size_t pos = 0, lit_start = SIZE_MAX;
   uint32_t miss = 0;
   auto flush_lit = [&](size_t end) {
@@ -270,11 +271,26 @@ uint64_t blob_sum(const uint8_t* p, size_t n) {
 std::vector<uint8_t> image_delta(const uint8_t* base, size_t base_len, const uint8_t* next, size_t next_len) {
   std::vector<Region> rs;
   std::vector<size_t> cn, cb;
+  std::vector<Region> whole;
   if (layout(next, next_len, cn) && layout(base, base_len, cb) && cn.size() == cb.size()) {
     for (size_t k = 0; k + 1 < cn.size(); k++)
-      if (cn[k + 1] > cn[k]) rs.push_back({cn[k], cn[k + 1], cb[k], cb[k + 1]});
+      if (cn[k + 1] > cn[k]) whole.push_back({cn[k], cn[k + 1], cb[k], cb[k + 1]});
   } else if (next_len) {
-    rs.push_back({0, next_len, 0, base_len});
+    whole.push_back({0, next_len, 0, base_len});
+  }
+  // regions over PIECE bytes are diffed in pieces on separate threads (C5's 49 MB head stream was
+  // one thread's 20 ms): piece j of the new region against the base region's same span, widened
+  // by MARGIN on both sides so that a shift across the cut still finds its match
+  constexpr size_t PIECE = 4u << 20, MARGIN = 256u << 10;
+  for (const Region& w : whole) {
+    const size_t nl = w.ne - w.nb, bl = w.be - w.bb;
+    if (nl <= PIECE) { rs.push_back(w); continue; }
+    for (size_t o = 0; o < nl; o += PIECE) {
+      const size_t lo = o > MARGIN ? o - MARGIN : 0, hi = std::min(bl, o + PIECE + MARGIN);
+      Region r{w.nb + o, w.nb + std::min(nl, o + PIECE), w.bb + std::min(lo, bl), w.bb + std::max(std::min(lo, bl), hi)};
+      r.shift0 = (int64_t)o - (int64_t)std::min(lo, bl);
+      rs.push_back(r);
+    }
   }
   std::vector<RBuf> out(rs.size());
   uint64_t sum = 0;
