@@ -25,6 +25,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <algorithm>
@@ -1520,10 +1522,13 @@ struct alignas(16) SegLds {  // (16: the counting merge reads hp four words at a
   uint32_t hp[NS][HC + PAD];       // hit: global policy index
   uint32_t hm[NS][SLIM ? 1 : HC + PAD];  // hit: kind (0 permit, 1 forbid, 2 error) | tier << 8 | error slot << 16
   uint32_t he[NS][XC * 4 + PAD];   // error details: code | aux << 8, k, et, ei
-  uint2 hot[NS][NHOT + PAD];
+  // (hot rows one uint2 longer: the pooled candidate pass reads slot h of several requests' rows in
+  // lockstep, which unpadded rows (64 words apart) put on the same banks)
+  uint2 hot[NS][NHOT + (NS > 1 ? 1 : 0)];
   // the candidate pass's wave-wide task pool (FLAT: SPLIT, 8-lane segments): every segment's request
-  // context, for lanes that evaluate another segment's candidates, and its running state
-  uint4 cx[FLAT_NS(SEG)][4];       // (blk, pt, pi, at), (ai, rt, ri, p_anc), (r_anc, a_anc, nanc p|r, a_nanc | self << 16), (rowo, am lo, am hi, 0)
+  // context, for lanes that evaluate another segment's candidates, and its running state (rows of
+  // 5 uint4, the last unused: 80 bytes apart, 8 requests' rows on disjoint banks)
+  uint4 cx[FLAT_NS(SEG)][FLAT_NS(SEG) > 1 ? 5 : 4];  // (blk, pt, pi, at), (ai, rt, ri, p_anc), (r_anc, a_anc, nanc p|r, a_nanc | self << 16), (rowo, am lo, am hi, 0)
   uint32_t sst[FLAT_NS(SEG)][4];   // hits recorded, error details, lowest tier with a hit, flags (1: structural)
   uint32_t sne[FLAT_NS(SEG)];      // buckets staged
 };
@@ -3307,6 +3312,59 @@ uint32_t dev_small_n() {  // (read per batch: tests cover both paths at small si
 
 // One pinned staging block and one device block for the inputs (256-B aligned sections), one for
 // the results; a batch costs two copies and a memset, and no allocation once the pool is warm.
+// A few persistent helper threads for the staging copy of mid-sized batches (256 KB .. 8 MB: a
+// 2,048-request batch stages 1.8 MB, ~95 us on one core): a copy is cut in STAGE_PARTS pieces, the
+// helpers take all but the caller's own, the caller waits for them (a spawn per batch would cost
+// what the copy saves). One copy at a time; a second caller copies alone.
+namespace {
+struct StagePool {
+  static constexpr unsigned HELPERS = 3;
+  std::mutex mu, busy;
+  std::condition_variable cv;
+  std::function<void(unsigned)> job;  // job(k) for part k = 1..HELPERS
+  uint64_t gen = 0;
+  std::atomic<unsigned> left{0};
+  std::vector<std::thread> ts;
+  StagePool() {
+    for (unsigned t = 0; t < HELPERS; t++)
+      ts.emplace_back([this, t] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::function<void(unsigned)> j;
+          {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return gen != seen; });
+            seen = gen;
+            j = job;
+          }
+          j(t + 1);
+          left.fetch_sub(1, std::memory_order_release);
+        }
+      });
+    for (auto& t : ts) t.detach();  // process-lifetime helpers (never joined at exit)
+  }
+  // fn(k) for k = 0..HELPERS; false when another copy holds the pool (the caller runs them all)
+  bool run(const std::function<void(unsigned)>& fn) {
+    std::unique_lock<std::mutex> own(busy, std::try_to_lock);
+    if (!own.owns_lock()) return false;
+    left.store(HELPERS, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      job = fn;
+      gen++;
+    }
+    cv.notify_all();
+    fn(0);
+    while (left.load(std::memory_order_acquire)) std::this_thread::yield();
+    return true;
+  }
+};
+StagePool& stage_pool() {
+  static StagePool* p = new StagePool();  // (leaked: detached helpers outlive static destruction)
+  return *p;
+}
+}  // namespace
+
 int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, DevPool* pool) {
   HIPCHK(hipSetDevice(device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
@@ -3438,7 +3496,21 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   for (int k = 0; k < NSEC; k++) total_len += len[k];
   const unsigned nt = total_len >= (8u << 20) ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
   uint8_t* in = (uint8_t*)d.in_blk;
-  if (nt <= 1) {
+  // byte range [t, t+1) / parts of the concatenated sections
+  auto part_copy = [&](unsigned t, unsigned parts) {
+    const size_t lo = total_len * t / parts, hi = total_len * (t + 1) / parts;
+    size_t pos = 0;
+    for (int k = 0; k < NSEC; k++) {
+      const size_t a = std::max(lo, pos), e = std::min(hi, pos + len[k]);
+      if (a < e) std::memcpy(st + off[k] + (a - pos), (const uint8_t*)src[k] + (a - pos), e - a);
+      pos += len[k];
+    }
+  };
+  static const bool pooled = !(std::getenv("CEDARGPU_STAGE_POOL") && *std::getenv("CEDARGPU_STAGE_POOL") == '0');
+  if (nt <= 1 && pooled && total_len >= (256u << 10) &&
+      stage_pool().run([&](unsigned t) { part_copy(t, StagePool::HELPERS + 1); })) {
+    // (staged by the pool)
+  } else if (nt <= 1) {
     for (int k = 0; k < NSEC; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
   } else {
     auto part = [&](unsigned t) {  // byte range [t, t+1) / nt of the concatenated sections
