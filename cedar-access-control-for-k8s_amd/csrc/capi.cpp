@@ -1420,7 +1420,7 @@ int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
       h.ppm[q] = (uint32_t)std::min<uint64_t>(1000000u, (uint64_t)b->host.fu_cnt[q] * 1000000u / std::max<uint32_t>(1u, n));
       const uint32_t cnt = std::min(b->host.fu_cnt[q], fu.cap);
       for (uint32_t k = 0; k < cnt; k++) {
-        const uint32_t i = fu.ids[k];
+        const uint32_t i = fu.ids[k] & ~0x80000000u;  // (FU_DONE: an entry the first pass finished)
         if (i >= n) { b->err = "follow-up worklist out of range"; return CG_E_DEVICE; }
         const uint32_t fl = fu.res[2 * k] >> 16;
         if (!(fl & cgi::RF_VALID) || (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) continue;

@@ -114,6 +114,9 @@ struct KArgs {
 // SCAN_CAP: bucket pairs a request's list holds (more: SCAN_OVF, the large stage probes the index
 // itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
 // the large stage, which reads the list when it holds them all
+// a follow-up worklist entry the first pass already finished (its id | FU_DONE): the follow-up
+// launch skips it, the host folds its result as any other
+constexpr uint32_t FU_DONE = 0x80000000u;
 constexpr uint32_t SCAN_CAP = 96, SCAN_OVF = 0xFFFFFFFFu, SCAN_COUNT = (1u << 27) - 1, SCAN_COMBO_SHIFT = 27;
 static_assert(SCAN_CAP >= 64, "the SPLIT probe kernel reads one pair per lane (up to 64) before it knows the count");
 // scan[i] | SCAN_HEAVY: the request's buckets hold more than a.scan_heavy candidate heads, so it
@@ -2091,7 +2094,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint32_t gid = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;
   bool valid = gid < n_req;
-  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0u;
+  const uint32_t r0 = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0u;
+  if (a.req_idx && (r0 & FU_DONE)) valid = false;  // finished by the first pass (its overflow slot)
+  const uint32_t r = valid ? r0 : 0u;
   const uint32_t* row = (a.grows && !a.req_idx) ? a.grows + (size_t)(valid ? gid : 0u) * a.row_words : a.rows + (size_t)r * a.row_words;
 
   // the request row streams through once: non-temporal loads, header broadcast in the segment
@@ -2660,7 +2665,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   seg = lane_m / SEG; sl = lane_m % SEG; sbase = seg * SEG;
   smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
   const uint32_t gid_m = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
-  valid = gid_m < n_req;
+  valid = gid_m < n_req && !(a.req_idx && (a.req_idx[gid_m] & FU_DONE));
   const uint32_t wo = a.req_idx ? gid_m : (valid ? (a.ord ? a.ord[gid_m] : gid_m) : 0u);  // result slot
   const uint32_t t = min_tier;
   const bool structural = sballot(general) != 0;
@@ -2851,22 +2856,40 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       return have && ((mj >> 8) & 0xFF) == t && (i == 0 || (wl.u.hs[seg][i - 1] >> 12) != pj);
     };
     bool deny = false;
+    uint32_t tf = 0, tp = 0, te = 0;  // the deciding lists' lengths
     for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
       uint32_t pj, mj;
       const bool el = deciding(c0 + sl, pj, mj);
-      deny = deny || sballot(el && (mj & 0xFF) == 1) != 0;
+      tf += popc64(sballot(el && (mj & 0xFF) == 1));
+      tp += popc64(sballot(el && (mj & 0xFF) == 0));
+      te += popc64(sballot(el && (mj & 0xFF) == 2));
     }
+    deny = tf != 0;
+    // A list longer than the request's capacity (at most 64 reasons and 8 errors here): its whole
+    // result goes to an overflow slot of the long-list follow-up's worklist (KArgs::ovf_*, taken in
+    // the first pass of a large batch), flagged done, so that follow-up has nothing left to run
+    // (only a result the slot holds whole: duplicate classes record a hit per member, so a request
+    // decided with 8 error details may list 50 errors; such a one keeps RF_OVERFLOW and the re-runs)
+    if (a.ovf_cnt && valid && ((deny ? tf : tp) > a.capr || te > a.cape) && (deny ? tf : tp) <= a.ovf_capr && te <= a.ovf_cape) {
+      uint32_t o = 0;
+      if (sl == 0) o = atomicAdd(a.ovf_cnt, 1u);
+      o = sbcast(o, 0);
+      oslot = o < a.ovf_cap ? o : 0xFFFFFFFFu;
+    }
+    const uint32_t rcap = oslot != 0xFFFFFFFFu ? a.ovf_capr : a.capr, ecap = oslot != 0xFFFFFFFFu ? a.ovf_cape : a.cape;
+    uint32_t* rdst = oslot != 0xFFFFFFFFu ? a.ovf_rf + (size_t)oslot * a.ovf_capr : a.reasons_f + (size_t)wo * a.capr;
+    uint32_t* edst = oslot != 0xFFFFFFFFu ? a.ovf_er + (size_t)oslot * a.ovf_cape * ERR_WORDS : a.errs + (size_t)wo * a.cape * ERR_WORDS;
     for (uint32_t c0 = 0; __ballot(c0 < nhm); c0 += SEG) {
       uint32_t pj, mj;
       const bool el = deciding(c0 + sl, pj, mj);
       const uint32_t kind = mj & 0xFF;
       const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
       const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
-      if (el && deny && kind == 1 && rf < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rf);
-      if (el && !deny && kind == 0 && rp < a.capr) __builtin_nontemporal_store(pj, a.reasons_f + (size_t)wo * a.capr + rp);
-      if (el && kind == 2 && re < a.cape) {
+      if (el && deny && kind == 1 && rf < rcap) __builtin_nontemporal_store(pj, rdst + rf);
+      if (el && !deny && kind == 0 && rp < rcap) __builtin_nontemporal_store(pj, rdst + rp);
+      if (el && kind == 2 && re < ecap) {
         const uint32_t xs = mj >> 16;
-        uint32_t* er = a.errs + ((size_t)wo * a.cape + re) * ERR_WORDS;
+        uint32_t* er = edst + (size_t)re * ERR_WORDS;
         er[0] = pj; er[1] = wl.he[seg][4 * xs]; er[2] = wl.he[seg][4 * xs + 1]; er[3] = wl.he[seg][4 * xs + 2];
         er[4] = wl.he[seg][4 * xs + 3]; er[5] = 0;
       }
@@ -2881,11 +2904,13 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     uint32_t fl = RF_VALID | (nf ? RF_FORBID : 0u);
     if (oslot != 0xFFFFFFFFu) {  // the whole result in the overflow slot; the request's own says so
       const uint32_t fo = fl | ((nr > a.ovf_capr || nerr > a.ovf_cape) ? RF_OVERFLOW : 0u);
-      a.ovf_ids[oslot] = wo;
+      a.ovf_ids[oslot] = wo | (SLIM ? 0u : FU_DONE);
       a.ovf_res[2 * (size_t)oslot] = dec | (t << 8) | (fo << 16);
       a.ovf_res[2 * (size_t)oslot + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
     }
-    if (nr > a.capr || nerr > a.cape) fl |= RF_OVERFLOW;
+    // (a large batch's slot holds the final result: the request's own then carries no RF_OVERFLOW,
+    // which would list it for the follow-up again)
+    if ((nr > a.capr || nerr > a.cape) && (SLIM || oslot == 0xFFFFFFFFu)) fl |= RF_OVERFLOW;
     a.res[2 * (size_t)wo] = dec | (t << 8) | (fl << 16);
     a.res[2 * (size_t)wo + 1] = min(nr, 0xFFFFu) | (min(nerr, 0xFFFFu) << 16);
   }
@@ -3270,7 +3295,10 @@ static int pool_get(DevPool* p, bool host, size_t n, void** out, size_t* cls) {
       return 0;
     }
   }
-  if (host) HIPCHK(hipHostMalloc(out, *cls, hipHostMallocDefault), "hipHostMalloc");
+  // CEDARGPU_PINNED_NONCOHERENT=1: pinned blocks the GPU may cache (they are only ever DMA
+  // copy sources and targets, never read by kernels) (A/B: the host's own reads of the results)
+  static const unsigned pflags = [] { const char* e = std::getenv("CEDARGPU_PINNED_NONCOHERENT"); return (e && *e == '1') ? hipHostMallocNonCoherent : hipHostMallocDefault; }();
+  if (host) HIPCHK(hipHostMalloc(out, *cls, pflags), "hipHostMalloc");
   else HIPCHK(hipMalloc(out, *cls), "hipMalloc");
   std::lock_guard<std::mutex> g(p->mu);
   p->owned.emplace_back(*out, host);
@@ -4015,6 +4043,16 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
   }
   k.scan = b.scan;
   k.scan_n = b.n;
+  // the candidate pass finishes long reason lists itself, into the long-list follow-up's worklist
+  // (entries flagged FU_DONE: that launch skips them, the host folds them); CEDARGPU_LONG_SLOTS=0
+  // leaves them to the follow-up launch
+  static const bool long_slots = !(std::getenv("CEDARGPU_LONG_SLOTS") && *std::getenv("CEDARGPU_LONG_SLOTS") == '0');
+  if (long_slots && b.fu_cnt && b.fu[FU_OVF].cap && img.indexed) {
+    const auto& f = b.fu[FU_OVF];
+    k.ovf_cnt = b.fu_cnt + FU_OVF;
+    k.ovf_ids = f.ids; k.ovf_res = f.res; k.ovf_rf = f.rf; k.ovf_er = f.er;
+    k.ovf_cap = f.cap; k.ovf_capr = f.capr; k.ovf_cape = f.cape;
+  }
   if (b.ord) {  // grouped batch: this step's order and its rows in that order (group.hip)
     if (group_enqueue(b.gkeys, b.rows, b.n, b.row_words, b.grows, b.ord, b.gkeys2, b.gvals, b.grp_temp, b.grp_temp_bytes, s)) {
       g_err = "request grouping failed";
@@ -4209,10 +4247,13 @@ static int fetch_overflow(DevBatch& b) {
   if (!used) return 0;
   const std::pair<const uint32_t*, size_t> arr[4] = {
       {f.ids, used * 4}, {f.res, used * 8}, {f.rf, used * f.capr * 4}, {f.er, used * f.cape * ERR_WORDS * 4}};
+  // (four copies on the null stream, one wait: the batch's own stream may already run the next
+  // batch, and the null stream does not order against these non-blocking streams)
   for (const auto& a : arr) {
     const size_t o = (const uint8_t*)a.first - base;
-    HIPCHK(hipMemcpy(st + o, base + o, a.second, hipMemcpyDeviceToHost), "D2H overflow slots");
+    HIPCHK(hipMemcpyAsync(st + o, base + o, a.second, hipMemcpyDeviceToHost, nullptr), "D2H overflow slots");
   }
+  HIPCHK(hipStreamSynchronize(nullptr), "D2H overflow slots");
   return 0;
 }
 

@@ -114,12 +114,17 @@ def test_random_atomic_policies_vs_oracle(ctx, seed, monkeypatch):
     check_items(ctx, stores, items)
 
 
+@pytest.mark.parametrize("small_n", [None, "0"])
 @pytest.mark.parametrize("first_capr", [None, "8", "1"])
-def test_random_overflowing_result_lists(ctx, first_capr, monkeypatch):
+def test_random_overflowing_result_lists(ctx, first_capr, small_n, monkeypatch):
     """300 policies: many requests exceed the inline reason/error capacity -> re-run path (with
-    the batch's adaptive first-pass capacity, and pinned to 8 and 1 reasons per effect)."""
+    the batch's adaptive first-pass capacity, and pinned to 8 and 1 reasons per effect). On the
+    split path (small_n "0") the candidate pass writes such lists into the long-list follow-up's
+    slots (FU_DONE entries) until they run out, the rest take the follow-up / host re-run."""
     if first_capr:
         monkeypatch.setenv("CEDARGPU_FIRST_CAPR", first_capr)
+    if small_n:
+        monkeypatch.setenv("CEDARGPU_SMALL_N", small_n)
     g = Gen(77)
     stores = [cedargpu.MemoryStore("big.cedar", g.policies(300))]
     items = [g.item() for _ in range(200)]
