@@ -35,6 +35,10 @@ struct LatTrace {
     line += std::to_string(std::chrono::duration<double, std::micro>(n - t).count());
     t = n;
   }
+  void val(const char* k, double v) {
+    if (!on()) return;
+    line += " "; line += k; line += "="; line += std::to_string(v);
+  }
   ~LatTrace() { if (on() && !line.empty()) std::fprintf(stderr, "LAT %s%s\n", what, line.c_str()); }
 };
 }  // namespace
@@ -1414,6 +1418,7 @@ int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
     if ((fl & cgi::RF_VALID) && !(fl & (cgi::RF_GENERAL | cgi::RF_BIG)))
       h.first_maxr = std::max(h.first_maxr, b->host.res[2 * (size_t)i + 1] & 0xFFFF);
   }
+  tr.mark("maxr");
   if (b->host.fu_cnt) {
     for (uint32_t q = 0; q < FU_KINDS; q++) {
       const auto& fu = b->host.fu[q];
@@ -1436,8 +1441,10 @@ int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
                           fu.er + (size_t)k * fu.cape * cgi::ERR_WORDS, ne * cgi::ERR_WORDS);
         })
       }
+      if (cnt) tr.val(q == FU_BIG ? "nbig" : "nfu", cnt);
     }
   }
+  tr.mark("fu");
   {
     std::lock_guard<std::mutex> g(b->ctx->mu);
     // a batch without FU_BIG / FU_GEN entries keeps the image's last known list lengths
@@ -1445,6 +1452,7 @@ int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
     if (!h.gen_maxr && b->ctx->hint.serial == h.serial) h.gen_maxr = b->ctx->hint.gen_maxr;
     b->ctx->hint = h;
   }
+  tr.mark("fold");
   std::vector<uint32_t> idx_probe, idx_big, idx_gen;
   uint32_t capr_p = 0, cape_p = 0, capr_b = 0, cape_b = 0, capr_g = 0, cape_g = 0;
   for (uint32_t i = 0; i < n; i++) {

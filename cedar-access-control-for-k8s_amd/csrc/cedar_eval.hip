@@ -3462,6 +3462,13 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   }
   d.out_bytes = o_fu;
   d.dl_bytes = (d.small && d.fu[FU_BIG].cap) ? o_k[FU_BIG][0] : o_fu;
+  // Small batches: results written by the kernel into the pinned block (DevBatch::zc). The
+  // counters move into the input block, whose copy carries their zeros.
+  static const bool zc_on = !(std::getenv("CEDARGPU_ZERO_COPY") && *std::getenv("CEDARGPU_ZERO_COPY") == '0');
+  d.zc = d.small && zc_on;
+  const size_t o_incnt = in_bytes;
+  if (d.zc) in_bytes += al((FU_KINDS + 1) * 4);
+  const size_t o_zc = al(in_bytes);
   int rc;
   if (b.img->lane_need > LANE_WORDS) {  // per-request lane scratch of the GLANE stream kernel
     const size_t lane_bytes = (size_t)n * b.img->lane_need * 4;
@@ -3502,14 +3509,14 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     pool_put(pool, false, d.grp_blk, d.grp_cls);
     return rc;
   }
-  if ((rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) {
+  if (!d.zc && (rc = pool_get(pool, false, d.out_bytes, &d.out_blk, &d.out_cls))) {
     pool_put(pool, false, d.in_blk, d.in_cls);
     pool_put(pool, false, d.lane_blk, d.lane_cls);
     pool_put(pool, false, d.scan_blk, d.scan_cls);
     pool_put(pool, false, d.grp_blk, d.grp_cls);
     return rc;
   }
-  if ((rc = pool_get(pool, true, std::max(in_bytes, d.out_bytes), &d.stage, &d.stage_cls))) {
+  if ((rc = pool_get(pool, true, d.zc ? o_zc + d.out_bytes : std::max(in_bytes, d.out_bytes), &d.stage, &d.stage_cls))) {
     pool_put(pool, false, d.in_blk, d.in_cls);
     pool_put(pool, false, d.out_blk, d.out_cls);
     pool_put(pool, false, d.lane_blk, d.lane_cls);
@@ -3556,6 +3563,23 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     for (auto& th : ts) th.join();
   }
   uint8_t* o = (uint8_t*)d.out_blk;
+  if (d.zc) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, d.stage, 0) != hipSuccess || !dp) {
+      g_err = "hipHostGetDevicePointer: pinned block not mapped for the device";
+      pool_put(pool, false, d.in_blk, d.in_cls);
+      pool_put(pool, true, d.stage, d.stage_cls);
+      pool_put(pool, false, d.lane_blk, d.lane_cls);
+      pool_put(pool, false, d.scan_blk, d.scan_cls);
+      pool_put(pool, false, d.grp_blk, d.grp_cls);
+      return -4;
+    }
+    o = (uint8_t*)dp + o_zc;
+    d.zc_out = st + o_zc;
+    d.zc_cnt = (uint32_t*)(st + o_zc + o_cnt);
+    std::memset(st + o_incnt, 0, (FU_KINDS + 1) * 4);  // the counters (they travel with the inputs)
+    std::memset(d.zc_out + o_res, 0, n * 2 * 4);        // res: RF_VALID clear until written
+  }
   d.heap = (uint32_t*)(in + off[0]);
   d.req_base = (uint32_t*)(in + off[1]);
   d.rows = (uint32_t*)(in + off[2]);
@@ -3566,7 +3590,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.reasons_f = (uint32_t*)(o + o_rf);
   d.reasons_p = (uint32_t*)(o + o_rp);
   d.errs = (uint32_t*)(o + o_er);
-  d.fu_cnt = (uint32_t*)(o + o_cnt);
+  d.fu_cnt = (uint32_t*)(d.zc ? in + o_incnt : o + o_cnt);
   for (uint32_t k = 0; k < FU_KINDS; k++) {
     auto& f = d.fu[k];
     f.ids = (uint32_t*)(o + o_k[k][0]);
@@ -3582,7 +3606,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // (one copy: staging in pieces with an H2D per piece, to overlap the two, made 1-2k-request
   // batches 0.06-0.07 ms slower on the box, gpurun_out/r04flat3)
   HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
-  HIPCHK(hipMemsetAsync(d.res, 0, o_rf, s), "memset res");  // (and the worklist counters)
+  if (!d.zc) HIPCHK(hipMemsetAsync(d.res, 0, o_rf, s), "memset res");  // (and the worklist counters)
   return 0;
 }
 
@@ -4211,14 +4235,15 @@ void dev_subset_release(DevSubset* job) {
 static void bind_results(const DevBatch& b, Batch& host) {
   host.capr = b.capr;
   host.cape = b.cape;
-  uint8_t* st = (uint8_t*)b.stage;
-  const uint8_t* base = (const uint8_t*)b.out_blk;
+  // (zero-copy: the results sit at zc_out, whose device view is the one the kernel wrote through)
+  uint8_t* st = b.zc ? b.zc_out : (uint8_t*)b.stage;
+  const uint8_t* base = b.zc ? (const uint8_t*)b.res : (const uint8_t*)b.out_blk;
   auto at = [&](const uint32_t* dev) { return (uint32_t*)(st + ((const uint8_t*)dev - base)); };
   host.res = b.n ? at(b.res) : nullptr;
   host.reasons_f = b.n ? at(b.reasons_f) : nullptr;
   host.reasons_p = b.n ? at(b.reasons_p) : nullptr;
   host.errs = b.n ? at(b.errs) : nullptr;
-  host.fu_cnt = (b.n && b.fu_cnt) ? at(b.fu_cnt) : nullptr;
+  host.fu_cnt = (b.n && b.fu_cnt) ? (b.zc ? b.zc_cnt : at(b.fu_cnt)) : nullptr;
   for (uint32_t k = 0; k < FU_KINDS; k++) {
     host.fu[k] = Batch::FollowUp();
     const auto& f = b.fu[k];
@@ -4238,7 +4263,7 @@ static void bind_results(const DevBatch& b, Batch& host) {
 // array's used prefix (the kernel has finished: plain copies, off the batch's stream, which may
 // already run the next batch).
 static int fetch_overflow(DevBatch& b) {
-  if (!b.dl_bytes || b.dl_bytes >= b.out_bytes || !b.fu_cnt) return 0;
+  if (b.zc || !b.dl_bytes || b.dl_bytes >= b.out_bytes || !b.fu_cnt) return 0;
   const uint8_t* base = (const uint8_t*)b.out_blk;
   uint8_t* st = (uint8_t*)b.stage;
   const uint32_t taken = *(const uint32_t*)(st + ((const uint8_t*)(b.fu_cnt + FU_BIG) - base));
@@ -4260,7 +4285,8 @@ static int fetch_overflow(DevBatch& b) {
 int dev_download(DevBatch& b, Batch& host, void* stream) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
-  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
+  if (b.zc && b.fu_cnt) HIPCHK(hipMemcpyAsync(b.zc_cnt, b.fu_cnt, (FU_KINDS + 1) * 4, hipMemcpyDeviceToHost, s), "D2H counters");
+  else if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
   HIPCHK(hipStreamSynchronize(s), "sync download");
   b.pending = false;
   if (const int rc = fetch_overflow(b)) return rc;
@@ -4276,7 +4302,8 @@ int dev_download_async(DevBatch& b, void* stream) {
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     b.done = (void*)e;
   }
-  if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
+  if (b.zc && b.fu_cnt) HIPCHK(hipMemcpyAsync(b.zc_cnt, b.fu_cnt, (FU_KINDS + 1) * 4, hipMemcpyDeviceToHost, s), "D2H counters");
+  else if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
   HIPCHK(hipEventRecord((hipEvent_t)b.done, s), "event record");
   return 0;
 }

@@ -35,24 +35,6 @@ void parallel_for(size_t n, size_t grain, F&& fn) {
   for (auto& t : ts) t.join();
 }
 
-uint64_t hash_bytes(const uint8_t* p, size_t n, uint64_t seed) {
-  uint64_t h = seed ^ (n * 0xC2B2AE3D27D4EB4Full);
-  for (; n >= 8; n -= 8, p += 8) {
-    uint64_t w;
-    std::memcpy(&w, p, 8);
-    h = (h ^ (w * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
-    h ^= h >> 31;
-  }
-  if (n) {
-    uint64_t w = 0;
-    std::memcpy(&w, p, n);
-    h = (h ^ (w * 0xBF58476D1CE4E5B9ull)) * 0x94D049BB133111EBull;
-    h ^= h >> 31;
-  }
-  h *= 0xFF51AFD7ED558CCDull;
-  return h ^ (h >> 33);
-}
-
 // ---- regions: the image blob's header, device sections and host part (image.h DevSection) ----
 struct Region {
   size_t nb, ne, bb, be;  // [nb, ne) of the new blob against [bb, be) of the base

@@ -91,6 +91,13 @@ struct DevBatch {
   // small batches download the results up to the overflow slots (dl_bytes of out_bytes); the slots
   // a batch took follow once its counter is read (dev_download_finish)
   size_t dl_bytes = 0;
+  // zero-copy results (small batches, CEDARGPU_ZERO_COPY=0 turns it off): the kernel writes res,
+  // the reason / error lists and the overflow slots straight into the pinned block at zc_out
+  // (behind the staged inputs); only the counters, which take device atomics and live in the input
+  // block, come back by copy (to zc_cnt). No results copy and no second round trip for the slots.
+  bool zc = false;
+  uint8_t* zc_out = nullptr;
+  uint32_t* zc_cnt = nullptr;
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)
   size_t in_cls = 0, out_cls = 0, stage_cls = 0, out_bytes = 0;
