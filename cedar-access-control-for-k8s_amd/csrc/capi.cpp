@@ -328,7 +328,7 @@ void group_requests(cg_batch* b) {
     for (uint32_t i = 0; i < n; i++) tmp[cnt[(key[i] >> sh) & 2047u]++] = key[i];
     key.swap(tmp);
   }
-  PodVec<uint32_t> rows((size_t)n * rw), base(n), gk(h.gkeys.size());
+  PinVec<uint32_t> rows((size_t)n * rw), base(n), gk(h.gkeys.size());
   std::vector<uint32_t> slot(n);
   parallel_for(n, [&](size_t s) {
     const uint32_t o = (uint32_t)(key[s] & imask);

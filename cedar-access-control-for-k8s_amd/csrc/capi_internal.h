@@ -91,6 +91,19 @@ struct cg_batch {
   std::map<uint32_t, std::string> fast_reason;  // authz fast paths: the reason; admission: error text
   std::vector<cg::DevSubset> held;  // re-run result blocks the host lists point into (Batch::big)
   ~cg_batch() {
+    if (dev.direct && dev.pending) {
+      // inputs were copied straight from these arrays (pinned blocks) and the copy may still run:
+      // they go with the retired batch and return to the pinned pool once its stream drains
+      struct Arrays { cg::PinVec<uint32_t> heap, req_base, rows, gkeys, bstr_off; cg::PinVec<uint8_t> bstr_bytes; };
+      try {
+        auto a = std::make_shared<Arrays>();
+        a->heap.swap(host.heap); a->req_base.swap(host.req_base); a->rows.swap(host.rows);
+        a->gkeys.swap(host.gkeys); a->bstr_off.swap(host.bstr_off); a->bstr_bytes.swap(host.bstr_bytes);
+        dev.keep = std::move(a);
+      } catch (...) {
+        cg::dev_batch_free(&dev);  // (drains the stream first)
+      }
+    }
     dev_batch_retire(&dev, held);  // never waits: blocks still in use return once the stream drains
   }
   int32_t dev_of(uint32_t i) const { return i < items.size() ? items[i].dev : -1; }

@@ -3311,10 +3311,82 @@ static void pool_put(DevPool* p, bool host, void* blk, size_t cls) {
   (host ? p->host_free : p->dev_free).emplace(cls, blk);
 }
 
+// ---- pinned blocks for batch arrays (engine.h pinned_take) ----
+// Process-wide, power-of-two classes PIN_MIN..PIN_MAX, recycled and never freed; on once a device
+// context exists (the first dev_pool_create), so processes that only encode never touch the
+// runtime. CEDARGPU_PINNED_ARRAYS=0 turns them off; CEDARGPU_PINNED_ARRAYS_MB caps the total
+// (default 256 MB; past it arrays come from the heap and are staged as before).
+namespace {
+struct PinnedArrays {
+  std::mutex mu;
+  std::multimap<size_t, void*> idle;        // class -> block
+  std::unordered_map<const void*, size_t> cls;  // block -> class
+  size_t held = 0, cap = 0;
+};
+PinnedArrays& pinned_arrays() {
+  static PinnedArrays* p = new PinnedArrays();  // (leaked: arrays may outlive static destruction)
+  return *p;
+}
+std::atomic<bool> g_pin_on{false};
+}  // namespace
+
+void* pinned_take(size_t bytes) {
+  if (!g_pin_on.load(std::memory_order_relaxed)) return nullptr;
+  const size_t c = size_class(bytes);
+  auto& pa = pinned_arrays();
+  {
+    std::lock_guard<std::mutex> g(pa.mu);
+    auto it = pa.idle.find(c);
+    if (it != pa.idle.end()) {
+      void* b = it->second;
+      pa.idle.erase(it);
+      return b;
+    }
+    if (pa.held + c > pa.cap) return nullptr;
+    pa.held += c;
+  }
+  void* b = nullptr;
+  if (hipHostMalloc(&b, c, hipHostMallocDefault) != hipSuccess || !b) {
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> g(pa.mu);
+    pa.held -= c;
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(pa.mu);
+  pa.cls.emplace(b, c);
+  return b;
+}
+
+bool pinned_give(void* p, size_t) {
+  if (!p) return false;
+  auto& pa = pinned_arrays();
+  std::lock_guard<std::mutex> g(pa.mu);
+  auto it = pa.cls.find(p);
+  if (it == pa.cls.end()) return false;
+  pa.idle.emplace(it->second, p);
+  return true;
+}
+
+bool pinned_block(const void* p, size_t bytes) {
+  if (!p) return false;
+  auto& pa = pinned_arrays();
+  std::lock_guard<std::mutex> g(pa.mu);
+  auto it = pa.cls.find(p);
+  return it != pa.cls.end() && bytes <= it->second;
+}
+
 int dev_pool_create(int device, DevPool** out) {
   *out = new (std::nothrow) DevPool();
   if (!*out) { g_err = "out of host memory"; return -1; }
   (*out)->device = device;
+  static const bool pin = [] {
+    const char* e = std::getenv("CEDARGPU_PINNED_ARRAYS");
+    if (e && *e == '0') return false;
+    const char* m = std::getenv("CEDARGPU_PINNED_ARRAYS_MB");
+    pinned_arrays().cap = (size_t)(m ? std::max(0, std::atoi(m)) : 256) << 20;
+    return true;
+  }();
+  if (pin) g_pin_on.store(true, std::memory_order_relaxed);
   return 0;
 }
 
@@ -3412,8 +3484,25 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   const void* src[NSEC] = {b.heap.data(), b.req_base.data(), b.rows.data(), b.bstr_off.data(), b.bstr_bytes.data(), b.gkeys.data()};
   const size_t len[NSEC] = {b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.bstr_off.size() * 4, b.bstr_bytes.size(),
                             grp ? b.gkeys.size() * 4 : 0};
+  // Sections the encoder wrote into pinned blocks (engine.h pinned_take: a small batch's heap and
+  // rows) are copied from there directly ("direct"); the rest is staged into one pinned block and
+  // copied in one piece. Device layout: staged sections | (zero-copy) counters | direct sections.
+  static const bool zc_on = !(std::getenv("CEDARGPU_ZERO_COPY") && *std::getenv("CEDARGPU_ZERO_COPY") == '0');
+  d.zc = d.small && zc_on;
+  // (each copy costs ~10 us of queue gap on the device: the heap goes direct from PIN_MIN, the
+  // other sections from 1 MB, CEDARGPU_DIRECT_MIN_KB; a 2,048-request C3 batch: its 1.8 MB heap
+  // direct, 0.6 MB staged; submit -> results 173 -> 157 us, all four direct 159 us)
+  static const size_t direct_min = [] { const char* e = std::getenv("CEDARGPU_DIRECT_MIN_KB"); return (size_t)(e ? std::max(64, std::atoi(e)) : 1024) << 10; }();
+  bool direct[NSEC];
+  for (int k = 0; k < NSEC; k++) direct[k] = len[k] >= (k == 0 ? PIN_MIN : direct_min) && pinned_block(src[k], len[k]);
   size_t off[NSEC], in_bytes = 0;
-  for (int k = 0; k < NSEC; k++) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
+  for (int k = 0; k < NSEC; k++)
+    if (!direct[k]) { off[k] = in_bytes; in_bytes += al(std::max<size_t>(len[k], 4)); }
+  const size_t o_incnt = in_bytes;  // (zero-copy: the counters ride with the staged inputs)
+  if (d.zc) in_bytes += al((FU_KINDS + 1) * 4);
+  const size_t stage_in = in_bytes;
+  for (int k = 0; k < NSEC; k++)
+    if (direct[k]) { off[k] = in_bytes; in_bytes += al(len[k]); }
   const size_t n = std::max<uint32_t>(b.n(), 1);
   // The probe kernel writes only the deciding reason list (into reasons_f; reasons_p aliases it),
   // the policy-stream kernel both lists: an indexed image's first pass needs one array.
@@ -3462,13 +3551,9 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   }
   d.out_bytes = o_fu;
   d.dl_bytes = (d.small && d.fu[FU_BIG].cap) ? o_k[FU_BIG][0] : o_fu;
-  // Small batches: results written by the kernel into the pinned block (DevBatch::zc). The
-  // counters move into the input block, whose copy carries their zeros.
-  static const bool zc_on = !(std::getenv("CEDARGPU_ZERO_COPY") && *std::getenv("CEDARGPU_ZERO_COPY") == '0');
-  d.zc = d.small && zc_on;
-  const size_t o_incnt = in_bytes;
-  if (d.zc) in_bytes += al((FU_KINDS + 1) * 4);
-  const size_t o_zc = al(in_bytes);
+  // Small batches: results written by the kernel into the pinned block (DevBatch::zc), behind the
+  // staged inputs.
+  const size_t o_zc = al(stage_in);
   int rc;
   if (b.img->lane_need > LANE_WORDS) {  // per-request lane scratch of the GLANE stream kernel
     const size_t lane_bytes = (size_t)n * b.img->lane_need * 4;
@@ -3516,7 +3601,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     pool_put(pool, false, d.grp_blk, d.grp_cls);
     return rc;
   }
-  if ((rc = pool_get(pool, true, d.zc ? o_zc + d.out_bytes : std::max(in_bytes, d.out_bytes), &d.stage, &d.stage_cls))) {
+  if ((rc = pool_get(pool, true, d.zc ? o_zc + d.out_bytes : std::max(stage_in, d.out_bytes), &d.stage, &d.stage_cls))) {
     pool_put(pool, false, d.in_blk, d.in_cls);
     pool_put(pool, false, d.out_blk, d.out_cls);
     pool_put(pool, false, d.lane_blk, d.lane_cls);
@@ -3528,7 +3613,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // Large batches (admission objects run to ~600 B per request) are staged by several threads:
   // one core's memcpy into pinned memory runs at ~10 GB/s.
   size_t total_len = 0;
-  for (int k = 0; k < NSEC; k++) total_len += len[k];
+  for (int k = 0; k < NSEC; k++) total_len += direct[k] ? 0 : len[k];
   const unsigned nt = total_len >= (8u << 20) ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
   uint8_t* in = (uint8_t*)d.in_blk;
   // byte range [t, t+1) / parts of the concatenated sections
@@ -3536,6 +3621,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     const size_t lo = total_len * t / parts, hi = total_len * (t + 1) / parts;
     size_t pos = 0;
     for (int k = 0; k < NSEC; k++) {
+      if (direct[k]) continue;
       const size_t a = std::max(lo, pos), e = std::min(hi, pos + len[k]);
       if (a < e) std::memcpy(st + off[k] + (a - pos), (const uint8_t*)src[k] + (a - pos), e - a);
       pos += len[k];
@@ -3546,12 +3632,13 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
       stage_pool().run([&](unsigned t) { part_copy(t, StagePool::HELPERS + 1); })) {
     // (staged by the pool)
   } else if (nt <= 1) {
-    for (int k = 0; k < NSEC; k++) if (len[k]) std::memcpy(st + off[k], src[k], len[k]);
+    for (int k = 0; k < NSEC; k++) if (len[k] && !direct[k]) std::memcpy(st + off[k], src[k], len[k]);
   } else {
     auto part = [&](unsigned t) {  // byte range [t, t+1) / nt of the concatenated sections
       const size_t lo = total_len * t / nt, hi = total_len * (t + 1) / nt;
       size_t pos = 0;
       for (int k = 0; k < NSEC; k++) {
+        if (direct[k]) continue;
         const size_t a = std::max(lo, pos), b = std::min(hi, pos + len[k]);
         if (a < b) std::memcpy(st + off[k] + (a - pos), (const uint8_t*)src[k] + (a - pos), b - a);
         pos += len[k];
@@ -3605,7 +3692,13 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
   // (one copy: staging in pieces with an H2D per piece, to overlap the two, made 1-2k-request
   // batches 0.06-0.07 ms slower on the box, gpurun_out/r04flat3)
-  HIPCHK(hipMemcpyAsync(in, st, in_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  HIPCHK(hipMemcpyAsync(in, st, stage_in, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  // (the direct sources belong to the host batch, which keeps them until this stream has drained:
+  // cg_batch's destructor hands them to the retired batch, DevBatch::keep)
+  for (int k = 0; k < NSEC; k++)
+    if (direct[k]) HIPCHK(hipMemcpyAsync(in + off[k], src[k], len[k], hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D (pinned array)");
+  d.direct = false;
+  for (int k = 0; k < NSEC; k++) d.direct = d.direct || direct[k];
   if (!d.zc) HIPCHK(hipMemsetAsync(d.res, 0, o_rf, s), "memset res");  // (and the worklist counters)
   return 0;
 }

@@ -3,6 +3,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 namespace cg {
@@ -98,6 +99,10 @@ struct DevBatch {
   bool zc = false;
   uint8_t* zc_out = nullptr;
   uint32_t* zc_cnt = nullptr;
+  // some inputs were copied straight from the host batch's pinned arrays (engine.h pinned_take):
+  // until the stream drains, those arrays are kept alive by `keep` (set when the batch is retired)
+  bool direct = false;
+  std::shared_ptr<void> keep;
   size_t heap_words = 0, bytes = 0;
   void *in_blk = nullptr, *out_blk = nullptr, *stage = nullptr;  // pool blocks (device, device, pinned)
   size_t in_cls = 0, out_cls = 0, stage_cls = 0, out_bytes = 0;

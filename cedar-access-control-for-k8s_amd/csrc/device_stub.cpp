@@ -118,6 +118,11 @@ void dev_image_free(DevImage* d) {
   *d = DevImage();
 }
 
+// (no pinned memory here: every batch array lives on the heap and is staged)
+void* pinned_take(size_t) { return nullptr; }
+bool pinned_give(void*, size_t) { return false; }
+bool pinned_block(const void*, size_t) { return false; }
+
 int dev_pool_create(int device, DevPool** out) {
   *out = new DevPool();
   (*out)->device = device;

@@ -147,18 +147,37 @@ uint64_t list_hash(const uint32_t* w, uint32_t n) {
 uint32_t Batch::intern_list(const uint32_t* w, uint32_t n, uint64_t room, uint64_t hash) {
   const uint64_t h = hash ? hash : list_hash(w, n);
   anc_words += n;
-  auto it = anc_memo.find(h);
-  if (it != anc_memo.end()) {
-    const uint32_t o = it->second;
+  const uint64_t key = h | 1u;
+  if (2 * (memo_used + 1) > memo.size() / 2) {  // (load <= 1/2; pairs of words)
+    PodVec<uint64_t> old;
+    old.swap(memo);
+    memo.assign(std::max<size_t>(512, old.size() * 2), 0);
+    const size_t mask = memo.size() / 2 - 1;
+    for (size_t j = 0; j < old.size(); j += 2)
+      if (old[j]) {
+        size_t s = (size_t)(old[j] >> 1) & mask;
+        while (memo[2 * s]) s = (s + 1) & mask;
+        memo[2 * s] = old[j];
+        memo[2 * s + 1] = old[j + 1];
+      }
+  }
+  const size_t mask = memo.size() / 2 - 1;
+  size_t s = (size_t)(key >> 1) & mask;
+  while (memo[2 * s] && memo[2 * s] != key) s = (s + 1) & mask;
+  if (memo[2 * s]) {
+    const uint32_t o = (uint32_t)memo[2 * s + 1];
     if (heap.size() + room - o <= ANC_REACH && std::equal(w, w + n, heap.begin() + o)) {
       anc_shared_words += n;
       return o;
     }
+  } else {
+    memo_used++;
   }
   if (heap.size() + n > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
   const uint32_t o = (uint32_t)heap.size();
   heap.insert(heap.end(), w, w + n);
-  anc_memo[h] = o;
+  memo[2 * s] = key;
+  memo[2 * s + 1] = o;
   return o;
 }
 

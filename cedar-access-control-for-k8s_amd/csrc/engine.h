@@ -27,6 +27,17 @@ bool hugepages_on();
 void* huge_map(size_t bytes);
 bool huge_unmap(void* p, size_t bytes);
 
+// Pinned (page-locked, device-mapped) blocks for the host arrays a batch uploads (cedar_eval.hip;
+// the host-only build has none): a small batch's heap and rows are encoded straight into memory
+// the copy engine reads, so its upload needs no staging copy. pinned_take returns null when pinned
+// blocks are off (no device context yet, CEDARGPU_PINNED_ARRAYS=0, or the cap is reached);
+// pinned_give returns false for a block it did not hand out; pinned_block tells whether [p, p+n)
+// lies in one of its blocks.
+void* pinned_take(size_t bytes);
+bool pinned_give(void* p, size_t bytes);
+bool pinned_block(const void* p, size_t bytes);
+constexpr size_t PIN_MIN = 64u << 10, PIN_MAX = 16u << 20;  // array sizes that take pinned blocks
+
 // An allocator whose resize() leaves new elements uninitialised: a batch's large arrays are
 // written in full right after they grow (Batch::concat), so zero-filling them first would be a
 // serial pass over hundreds of MB.
@@ -57,6 +68,27 @@ struct NoInitAlloc : std::allocator<T> {
   static bool huge_on() { return hugepages_on(); }
 };
 template <class T> using PodVec = std::vector<T, NoInitAlloc<T>>;
+
+// A batch's uploaded arrays: NoInitAlloc, with arrays of PIN_MIN..PIN_MAX bytes in pinned blocks
+// when there are any (pinned_take), which the upload copies from without staging.
+template <class T>
+struct PinAlloc : NoInitAlloc<T> {
+  template <class U> struct rebind { using other = PinAlloc<U>; };
+  PinAlloc() = default;
+  template <class U> PinAlloc(const PinAlloc<U>&) {}
+  T* allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes >= PIN_MIN && bytes <= PIN_MAX)
+      if (void* p = pinned_take(bytes)) return static_cast<T*>(p);
+    return NoInitAlloc<T>::allocate(n);
+  }
+  void deallocate(T* p, size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes >= PIN_MIN && bytes <= PIN_MAX && pinned_give(p, bytes)) return;
+    NoInitAlloc<T>::deallocate(p, n);
+  }
+};
+template <class T> using PinVec = std::vector<T, PinAlloc<T>>;
 
 struct PolicyMeta {
   std::string id, filename;
@@ -297,19 +329,23 @@ int encode_sar_direct(const Image& img, const char* json, size_t n, EncodedReque
 // Host side of a device batch: encoded request heap + string table; results after evaluation.
 struct Batch {
   std::shared_ptr<const Image> img;
-  PodVec<uint32_t> heap, req_base;
-  PodVec<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
-  PodVec<uint32_t> gkeys;  // one grouping key per request (EncodedRequest::gkey)
+  PinVec<uint32_t> heap, req_base;
+  PinVec<uint32_t> rows;  // columnar request rows (image.h RowW), row_words each
+  PinVec<uint32_t> gkeys;  // one grouping key per request (EncodedRequest::gkey)
   uint32_t row_words = 0;
   // request-local strings of every request, appended as requests arrive: string j is
   // bstr_bytes[bstr_off[j] .. bstr_off[j + 1]) (bstr_off keeps a trailing end offset)
-  PodVec<uint32_t> bstr_off{0};
-  PodVec<uint8_t> bstr_bytes;
+  PinVec<uint32_t> bstr_off{0};
+  PinVec<uint8_t> bstr_bytes;
   uint32_t n_bstr() const { return (uint32_t)bstr_off.size() - 1; }
   // Interned ancestor lists (EncodedRequest::anc): content hash -> heap offset of the copy that
   // later blocks reference (image.h "ancestor lists"). Requests of one principal share one list,
   // so a batch carries each distinct list once and grouped neighbours read the same lines.
-  std::unordered_map<uint64_t, uint32_t> anc_memo;
+  // (open addressing over one array, so a part's memo is one block, not a node per list: freeing
+  // thousands of nodes after every bulk encode left the allocator's bins to sort on the next
+  // large allocation, 50-90 us on the serving path)
+  PodVec<uint64_t> memo;  // (hash | 1) << 0 in the even word, heap offset in the odd one; 0: empty
+  size_t memo_used = 0;
   uint64_t anc_words = 0, anc_shared_words = 0;  // list words appended / list words served by a copy
   uint32_t intern_list(const uint32_t* w, uint32_t n, uint64_t room, uint64_t hash = 0);
   // results
@@ -338,7 +374,9 @@ struct Batch {
   // indices were not the image's (device.h DevBatch::fu_cnt)
   const uint32_t* fu_cnt = nullptr;
   struct BigRef { const uint32_t *r = nullptr, *e = nullptr; uint32_t nr = 0, ne_words = 0; };
-  std::vector<BigRef> big;
+  std::vector<BigRef> bigs;      // lists held outside the first pass's slots
+  std::vector<uint32_t> big_ix;  // per request: 1 + its index in bigs, or 0 (empty: none)
+  const BigRef* big_of(uint32_t i) const { return (!big_ix.empty() && big_ix[i]) ? &bigs[big_ix[i] - 1] : nullptr; }
   void set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words);
 
   uint32_t n() const { return (uint32_t)req_base.size(); }

@@ -17,8 +17,8 @@ bool Batch::decision(uint32_t i) const { return (res[2 * (size_t)i] & 0xFF) == D
 void Batch::reason_ids(uint32_t i, std::vector<uint32_t>& out) const {
   out.clear();
   uint32_t n = res[2 * (size_t)i + 1] & 0xFFFF;
-  if (!big.empty() && big[i].r) {
-    out.assign(big[i].r, big[i].r + big[i].nr);
+  if (const BigRef* b = big_of(i)) {
+    out.assign(b->r, b->r + b->nr);
     return;
   }
   uint32_t flags = res[2 * (size_t)i] >> 16;
@@ -27,15 +27,20 @@ void Batch::reason_ids(uint32_t i, std::vector<uint32_t>& out) const {
 }
 
 void Batch::set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words) {
-  if (big.empty()) big.resize(n());
-  big[i] = BigRef{reasons, errs, nr, nerr_words};
+  if (big_ix.empty()) big_ix.assign(n(), 0u);
+  if (big_ix[i]) {
+    bigs[big_ix[i] - 1] = BigRef{reasons, errs, nr, nerr_words};
+  } else {
+    bigs.push_back(BigRef{reasons, errs, nr, nerr_words});
+    big_ix[i] = (uint32_t)bigs.size();
+  }
 }
 
 void Batch::error_recs(uint32_t i, std::vector<uint32_t>& out) const {
   out.clear();
   uint32_t n = res[2 * (size_t)i + 1] >> 16;
-  if (!big.empty() && big[i].r) {
-    out.assign(big[i].e, big[i].e + big[i].ne_words);
+  if (const BigRef* b = big_of(i)) {
+    out.assign(b->e, b->e + b->ne_words);
     return;
   }
   for (uint32_t k = 0; k < n && k < cape; k++)
