@@ -249,3 +249,36 @@ def test_bad_key_entity_indices_fail_the_batch(ctx):
     b.wait()
     assert [b.authz(i) for i in range(len(b))] == normal
     b.close()
+
+
+def test_closed_in_flight_batch_keeps_its_pinned_arrays(ctx):
+    """A small batch whose heap went to the device straight from a pinned block (engine.h PinVec,
+    dev_batch_upload's direct copy), closed while in flight: its arrays go with the retired batch
+    until the stream drains (cg_batch's destructor, DevBatch::keep), and the batches after it, which
+    take the same pinned blocks again, decide as before."""
+    pop = synth.Population(seed=7, dag_depth=6)
+    img = cedargpu.build_image([cedargpu.MemoryStore("c3.cedar", synth.abac_policies(2000, seed=31, pop=pop))], epoch=1,
+                               entities=pop.static_entities())
+    ctx.load(img, 1)
+    payload = synth.sars_json(synth.random_sars(2048, seed=5, pop=pop)).encode()
+    b = ctx.batch()
+    b.add_sar_json(payload)
+    assert b.bytes()[2] >= 64 << 10  # a heap the upload copies straight from its pinned block
+    b.submit()
+    b.wait()
+    want = [b.authz(i) for i in range(len(b))]
+    b.close()
+    ctx.inject_fault(cedargpu.FAULT_STALL, 200_000)
+    for _ in range(3):
+        b = ctx.batch()
+        b.add_sar_json(payload)
+        b.submit()
+        b.close()  # in flight: retired, never waited
+    ctx.inject_fault(cedargpu.FAULT_NONE)
+    for _ in range(3):
+        b = ctx.batch()
+        b.add_sar_json(payload)
+        b.submit()
+        b.wait(timeout=5.0)
+        assert [b.authz(i) for i in range(len(b))] == want
+        b.close()
