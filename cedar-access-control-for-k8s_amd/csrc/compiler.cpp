@@ -993,6 +993,37 @@ struct Compiler {
 
 }  // namespace
 
+// std::sort of v over up to `threads` threads: sorted pieces, then merged pairwise (each round's
+// merges side by side). Same result as one std::sort for a strict total order.
+template <class T>
+static void parallel_sort(std::vector<T>& v, unsigned threads) {
+  const size_t n = v.size();
+  unsigned parts = 1;
+  while (parts * 2 <= threads && n / (parts * 2) >= (1u << 15)) parts *= 2;
+  if (parts == 1) { std::sort(v.begin(), v.end()); return; }
+  std::vector<size_t> cut(parts + 1);
+  for (unsigned k = 0; k <= parts; k++) cut[k] = n * k / parts;
+  {
+    std::vector<std::thread> ts;
+    for (unsigned k = 1; k < parts; k++) ts.emplace_back([&, k] { std::sort(v.begin() + (long)cut[k], v.begin() + (long)cut[k + 1]); });
+    std::sort(v.begin(), v.begin() + (long)cut[1]);
+    for (auto& t : ts) t.join();
+  }
+  std::vector<T> buf(n);
+  std::vector<T>* src = &v;
+  std::vector<T>* dst = &buf;
+  for (unsigned w = 1; w < parts; w *= 2) {
+    std::vector<std::thread> ts;
+    for (unsigned k = 0; k < parts; k += 2 * w) {
+      const size_t a = cut[k], m = cut[std::min(parts, k + w)], e = cut[std::min(parts, k + 2 * w)];
+      ts.emplace_back([=] { std::merge(src->begin() + (long)a, src->begin() + (long)m, src->begin() + (long)m, src->begin() + (long)e, dst->begin() + (long)a); });
+    }
+    for (auto& t : ts) t.join();
+    std::swap(src, dst);
+  }
+  if (src != &v) v.swap(*src);
+}
+
 // fn(i) for i in [0, n) on up to 16 threads (chunks of 4,096)
 static void parallel_range(size_t n, const std::function<void(size_t)>& fn) {
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -1204,9 +1235,11 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       i2[i] = {((uint64_t)h2s[i] << 32) | x_hash(r2[i].first.second), r2[i].second, (uint32_t)i};
     });
     mark("sort keys");
-    std::thread t1([&] { std::sort(i1.begin(), i1.end()); });
-    std::thread t2([&] { std::sort(kents.begin(), kents.end()); });
-    std::sort(i2.begin(), i2.end());
+    // (the longest of the three, i2, on half the threads)
+    const unsigned hw = std::max(2u, std::min(16u, std::thread::hardware_concurrency()));
+    std::thread t1([&] { parallel_sort(i1, hw / 4); });
+    std::thread t2([&] { parallel_sort(kents, hw / 4); });
+    parallel_sort(i2, hw / 2);
     t1.join();
     t2.join();
     mark("sort core");
@@ -1333,28 +1366,13 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   // (the candidate pass packs a bucket's first head with its key combination: 27 bits, cedar_eval.hip EF_COMBO)
   if (n_heads >= (1u << 27)) throw CedarError("scope index exceeds 2^27 policy heads");
   img.bstream.assign(std::max<uint64_t>(ext_end, HEAD_WORDS), 0);
-  for (uint32_t p = 0; p < n; p++) {
+  parallel_range(n, [&](size_t p) {
     std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
     if (mlist[p]) {
       img.bstream[mlist[p]] = mcnt[p];
       std::copy(mflat.begin() + moff[p], mflat.begin() + moff[p + 1], img.bstream.begin() + mlist[p] + 1);  // ascending
     }
-  }
-  uint32_t head = 0;
-  auto put_heads = [&](auto begin, auto end) {
-    const uint32_t first = head;
-    for (auto it = begin; it != end; ++it) {
-      const uint32_t p = it->second;
-      if (p == NO_POLICY) continue;
-      uint32_t* hd = &img.bstream[(size_t)head * HEAD_WORDS];
-      const uint32_t* src = &img.pstream[rec_off[p]];
-      std::copy(src, src + std::min<uint32_t>(rec_len[p], HEAD_WORDS), hd);
-      hd[PW_EXT] = ext[p];
-      hd[PW_CODE_N] = mlist[p];  // heads: the duplicate class's member list (0: the policy alone)
-      head++;
-    }
-    return first;
-  };
+  });
   mark("ext area");
   const size_t n_entries = g1.size() + g2.size();
   // slots: the power of two >= 8x the entries while the table stays within 64 MB, and >= 2x in any
@@ -1367,9 +1385,6 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   while (size * 4 < slack * n_entries && (size_t)size * 2 * BT_WORDS * 4 <= (64u << 20)) size <<= 1;
   // the entries only: the device inserts them into `size` slots at load (cedar_btab_build)
   img.btab_slots = size;
-  img.btab.clear();
-  img.btab.reserve(std::max<size_t>(n_entries, 1) * BT_WORDS);
-  auto insert = [&](uint32_t, const uint32_t* e) { img.btab.insert(img.btab.end(), e, e + BT_WORDS); };
   size_t blocks = 16;
   while (blocks * 4 < n_entries) blocks <<= 1;  // >= 16 bits per entry
   img.bfilt.assign(2 * blocks, 0);
@@ -1380,29 +1395,59 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     img.bfilt[2 * blk + 1] |= (uint32_t)(need >> 32);
   };
   mark("tables");
+  // Each group's heads sit at its first (prefix sums of its records that file a policy), in group
+  // order (level-1 groups, then level-2); the groups' heads and bucket entries are then written
+  // side by side, the filter after them.
   std::vector<uint32_t> g1_first(g1.size()), g1_cnt(g1.size()), g2_first(g2.size()), g2_cnt(g2.size());
-  for (size_t gi = 0; gi < g1.size(); gi++) {
+  parallel_range(g1.size(), [&](size_t gi) {
+    uint32_t c = 0;
+    for (size_t i = g1[gi].b; i < g1[gi].e; i++) c += r1[i].second != NO_POLICY;
+    g1_cnt[gi] = c;
+  });
+  parallel_range(g2.size(), [&](size_t gi) {
+    uint32_t c = 0;
+    for (size_t i = g2[gi].b; i < g2[gi].e; i++) c += r2[i].second != NO_POLICY;
+    g2_cnt[gi] = c;
+  });
+  {
+    uint32_t head = 0;
+    for (size_t gi = 0; gi < g1.size(); gi++) { g1_first[gi] = head; head += g1_cnt[gi]; }
+    for (size_t gi = 0; gi < g2.size(); gi++) { g2_first[gi] = head; head += g2_cnt[gi]; }
+  }
+  auto put_heads = [&](auto begin, auto end, uint32_t head) {
+    for (auto it = begin; it != end; ++it) {
+      const uint32_t p = it->second;
+      if (p == NO_POLICY) continue;
+      uint32_t* hd = &img.bstream[(size_t)head * HEAD_WORDS];
+      const uint32_t* src = &img.pstream[rec_off[p]];
+      std::copy(src, src + std::min<uint32_t>(rec_len[p], HEAD_WORDS), hd);
+      hd[PW_EXT] = ext[p];
+      hd[PW_CODE_N] = mlist[p];  // heads: the duplicate class's member list (0: the policy alone)
+      head++;
+    }
+  };
+  img.btab.assign(n_entries * BT_WORDS, 0);
+  parallel_range(g1.size(), [&](size_t gi) {
     const G& g = g1[gi];
     const L1& k = r1[g.b].first;
-    const uint32_t first = put_heads(r1.begin() + (long)g.b, r1.begin() + (long)g.e);
-    g1_first[gi] = first;
-    g1_cnt[gi] = head - first;
-    const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], g.cmask, 0, first,
-                                  head - first, g.hmask, g.bloom[0], g.bloom[1], g.bloom[2], g.bloom[3]};
-    insert(l1_hash(k), e);
-    filt_add(l1_hash(k));
-  }
-  for (size_t gi = 0; gi < g2.size(); gi++) {
+    put_heads(r1.begin() + (long)g.b, r1.begin() + (long)g.e, g1_first[gi]);
+    const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16), k[1], k[2], k[3], k[4], k[5], k[6], g.cmask, 0, g1_first[gi],
+                                  g1_cnt[gi], g.hmask, g.bloom[0], g.bloom[1], g.bloom[2], g.bloom[3]};
+    std::copy(e, e + BT_WORDS, img.btab.begin() + (long)(gi * BT_WORDS));
+  });
+  parallel_range(g2.size(), [&](size_t gi) {
     const G& g = g2[gi];
     const L1& k = r2[g.b].first.first;
     const auto& x = r2[g.b].first.second;
-    const uint32_t first = put_heads(r2.begin() + (long)g.b, r2.begin() + (long)g.e);
-    g2_first[gi] = first;
-    g2_cnt[gi] = head - first;
+    put_heads(r2.begin() + (long)g.b, r2.begin() + (long)g.e, g2_first[gi]);
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16) | BT_L2 | x[0], k[1], k[2], k[3], k[4], k[5], k[6], x[1], x[2],
-                                  first, head - first, 0, 0, 0, 0, 0};
-    insert(bucket_hash2(l1_hash(k), x[0], x[1], x[2]), e);
-    filt_add(bucket_hash2(l1_hash(k), x[0], x[1], x[2]));
+                                  g2_first[gi], g2_cnt[gi], 0, 0, 0, 0, 0};
+    std::copy(e, e + BT_WORDS, img.btab.begin() + (long)((g1.size() + gi) * BT_WORDS));
+  });
+  for (size_t gi = 0; gi < g1.size(); gi++) filt_add(l1_hash(r1[g1[gi].b].first));
+  for (size_t gi = 0; gi < g2.size(); gi++) {
+    const auto& x = r2[g2[gi].b].first.second;
+    filt_add(bucket_hash2(l1_hash(r2[g2[gi].b].first.first), x[0], x[1], x[2]));
   }
   if (img.btab.empty()) img.btab.assign(BT_WORDS, 0);  // never empty buffers
   mark("heads+slots");

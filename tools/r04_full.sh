@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -1 gpurun_out/$TAG/pytest.log
 CEDARGPU_TRACE_LAT=1 timeout -k 10 600 python -u bench.py > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || { echo "bench failed"; tail -20 gpurun_out/$TAG/bench.err; exit 1; }
 python3 tools/bench_brief.py gpurun_out/$TAG/bench.json
-grep "LAT bulk\|LAT split" gpurun_out/$TAG/bench.err | head -6
+grep -m 6 "LAT bulk\|LAT split" gpurun_out/$TAG/bench.err || true
