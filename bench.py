@@ -681,8 +681,9 @@ def main():
                         "p99_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
                         "p999_ms": lat[min(len(lat) - 1, int(len(lat) * 0.999))] if lat else None,
                         "max_ms": lat[-1] if lat else None, "batches": len(lat),
-                        "what": "cg_batch_submit -> cg_batch_wait (string finalize, H2D, kernel, D2H, overflow "
-                                "re-runs) per batch of pre-encoded SubjectAccessReviews"},
+                        "what": "cg_batch_submit -> cg_batch_wait (string finalize, H2D, kernel writing its "
+                                "results into pinned host memory, the counters' D2H, overflow folds and re-runs) "
+                                "per batch of pre-encoded SubjectAccessReviews"},
             "host": {"encode_s": t_enc - t_build, "first_pass_s": t_first - t_enc},
         }
         if baseline:

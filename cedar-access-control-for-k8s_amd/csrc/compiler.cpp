@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <charconv>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -1853,19 +1854,35 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
       size_t n = 0;
       for (size_t k = 0; k < tiers[t].size(); k++) n += docs[di + k]->size();
       parsed[t].reserve(n);
-      std::unordered_map<std::string, size_t> ids;
+      // (keys view the IDs in parsed[t], which never reallocates: reserved above)
+      std::unordered_map<std::string_view, size_t> ids;
       ids.reserve(n);
       for (auto& doc : tiers[t]) {
         const std::vector<Policy>& ps = *docs[di];
         if (!doc.explicit_id.empty() && ps.size() != 1)
           throw CedarError("document for policy " + doc.explicit_id + " must hold exactly one policy");
         for (size_t i = 0; i < ps.size(); i++) {
-          PRef r{&ps[i], doc.explicit_id.empty() ? doc.id_prefix + std::to_string(i) + doc.id_suffix : doc.explicit_id,
-                 doc.zero_position ? &k_empty_name : &ps[i].filename, doc.zero_position ? Position{} : ps[i].pos,
-                 (uint32_t)di, (uint32_t)i};
+          std::string id;
+          if (doc.explicit_id.empty()) {
+            char nb[24];
+            const auto tc = std::to_chars(nb, nb + sizeof nb, i);
+            id.reserve(doc.id_prefix.size() + (size_t)(tc.ptr - nb) + doc.id_suffix.size());
+            id.append(doc.id_prefix).append(nb, tc.ptr).append(doc.id_suffix);
+          } else {
+            id = doc.explicit_id;
+          }
+          PRef r{&ps[i], std::move(id), doc.zero_position ? &k_empty_name : &ps[i].filename,
+                 doc.zero_position ? Position{} : ps[i].pos, (uint32_t)di, (uint32_t)i};
           auto it = ids.find(r.id);
-          if (it != ids.end()) parsed[t][it->second] = std::move(r);
-          else { ids.emplace(r.id, parsed[t].size()); parsed[t].push_back(std::move(r)); }
+          if (it != ids.end()) {  // a repeated ID replaces the earlier policy in its place
+            const size_t at = it->second;
+            ids.erase(it);
+            parsed[t][at] = std::move(r);
+            ids.emplace(parsed[t][at].id, at);
+          } else {
+            parsed[t].push_back(std::move(r));
+            ids.emplace(parsed[t].back().id, parsed[t].size() - 1);
+          }
         }
         di++;
       }
