@@ -76,6 +76,8 @@ _SIGS = {
     "cg_compiler_add_document_ex": (ctypes.c_int, [P, cstr, cstr, sz, cstr, cstr, ctypes.c_int]),
     "cg_compiler_doc_errors": (ctypes.c_int, [P, P, sz, ctypes.POINTER(sz)]),
     "cg_compiler_build": (ctypes.c_int, [P, u64, ctypes.POINTER(P), ctypes.POINTER(sz)]),
+    "cg_compiler_build_sized": (ctypes.c_int, [P, u64, ctypes.POINTER(sz)]),
+    "cg_compiler_write_image": (ctypes.c_int, [P, P, sz]),
     "cg_image_info": (ctypes.c_int, [P, sz, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u64)]),
     "cg_image_stats": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u32)] * 4),
     "cg_image_policy_atomic": (ctypes.c_int, [P, sz, u32, ctypes.POINTER(ctypes.c_int)]),

@@ -18,6 +18,11 @@ from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
 from ._lib import CG_E_RANGE, CompileError, DeadlineError, DeviceError, _err, lib
 
+# an uninitialised bytes object of n bytes (filled by the library before it is returned)
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+
 FAULT_NONE, FAULT_DEVICE_ERROR, FAULT_STALL, FAULT_BAD_KIDX = 0, 1, 2, 3
 DOC_SKIP_INVALID = 1
 
@@ -213,15 +218,18 @@ class Compiler:
                     rc = lib.cg_compiler_add_policy(c, _b(pid), _b(fname), tb, len(tb), 1 if zero else 0)
                 if rc:
                     raise _err(rc, lib.cg_compiler_last_error(c).decode())
-        out = _P()
+        # the blob is serialized straight into a new bytes object (cg_compiler_build_sized, then
+        # cg_compiler_write_image into its storage before anything else can see it): no second
+        # copy of a 100 MB image
         n = ctypes.c_size_t(0)
-        rc = lib.cg_compiler_build(c, epoch, ctypes.byref(out), ctypes.byref(n))
+        rc = lib.cg_compiler_build_sized(c, epoch, ctypes.byref(n))
         if rc:
             raise _err(rc, lib.cg_compiler_last_error(c).decode())
-        try:
-            return ctypes.string_at(out, n.value)
-        finally:
-            lib.cg_free(out)
+        blob = _new_bytes(None, n.value)
+        rc = lib.cg_compiler_write_image(c, ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p), n.value)
+        if rc:
+            raise _err(rc, lib.cg_compiler_last_error(c).decode())
+        return blob
 
     def doc_errors(self) -> List[dict]:
         """[{"filename", "error"}] of the documents the last build left out (skip_invalid stores)."""

@@ -56,6 +56,7 @@ struct cg_compiler {
   std::string statics_json;
   BuildInfo last;
   std::string err;
+  std::shared_ptr<Image> built;  // cg_compiler_build_sized's image until cg_compiler_write_image
 };
 
 namespace {
@@ -668,6 +669,39 @@ int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* l
     c->err = e.what();
     return CG_E_ARG;
   }
+}
+
+int cg_compiler_build_sized(cg_compiler* c, uint64_t epoch, size_t* len) {
+  if (!c || !len) return CG_E_ARG;
+  try {
+    c->skipped.clear();
+    c->built.reset();
+    c->built = compile_image(c->tiers, epoch, &c->cache, &c->statics, &c->skipped, c->incremental ? c->lower.get() : nullptr,
+                             c->statics_gen, &c->last);
+    *len = c->built->blob_size();
+    return CG_OK;
+  } catch (const CedarError& e) {
+    c->err = e.what();
+    std::string m = e.what();
+    return (m.find("device") != std::string::npos || m.find("not supported") != std::string::npos) ? CG_E_COMPILE : CG_E_PARSE;
+  } catch (const std::exception& e) {
+    c->err = e.what();
+    return CG_E_ARG;
+  }
+}
+
+int cg_compiler_write_image(cg_compiler* c, void* out, size_t cap) {
+  if (!c || !out) return CG_E_ARG;
+  if (!c->built) { c->err = "no image built (cg_compiler_build_sized)"; return CG_E_STATE; }
+  if (cap < c->built->blob_size()) { c->err = "buffer smaller than the image blob"; return CG_E_RANGE; }
+  try {
+    c->built->serialize_into((uint8_t*)out);
+  } catch (const std::exception& e) {
+    c->err = e.what();
+    return CG_E_ARG;
+  }
+  c->built.reset();
+  return CG_OK;
 }
 
 int cg_image_info(const void* image, size_t len, uint32_t* n_policies, uint32_t* n_tiers, uint64_t* epoch) {

@@ -29,6 +29,7 @@
 #include <functional>
 #include <map>
 #include <thread>
+#include <tuple>
 
 #include "engine.h"
 
@@ -2010,7 +2011,15 @@ static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "the blob's word arrays
 struct W {
   uint8_t* b = nullptr;
   size_t n = 0;
-  void raw(const void* p, size_t k) { if (b && k) std::memcpy(b + n, p, k); n += k; }
+  // (serialize_into: copies of >= 1 MB are collected here and run on several threads afterwards)
+  std::vector<std::tuple<uint8_t*, const void*, size_t>>* defer = nullptr;
+  void raw(const void* p, size_t k) {
+    if (b && k) {
+      if (defer && k >= (1u << 20)) defer->emplace_back(b + n, p, k);
+      else std::memcpy(b + n, p, k);
+    }
+    n += k;
+  }
   void u32(uint32_t v) { raw(&v, 4); }
   void u64(uint64_t v) { raw(&v, 8); }
   void put64(size_t at, uint64_t v) { if (b) std::memcpy(b + at, &v, 8); }
@@ -2090,6 +2099,32 @@ uint8_t* Image::serialize_malloc(size_t* len) const {
   write_blob(&w);
   *len = c.n;
   return p;
+}
+
+size_t Image::blob_size() const {
+  W c;
+  write_blob(&c);
+  return c.n;
+}
+
+void Image::serialize_into(uint8_t* out) const {
+  std::vector<std::tuple<uint8_t*, const void*, size_t>> big;
+  W w{out, 0, &big};
+  write_blob(&w);
+  // the deferred copies in 4 MB pieces over up to 8 threads
+  std::vector<std::tuple<uint8_t*, const uint8_t*, size_t>> pieces;
+  for (auto& [d, src, k] : big)
+    for (size_t o = 0; o < k; o += (4u << 20))
+      pieces.emplace_back(d + o, (const uint8_t*)src + o, std::min<size_t>(4u << 20, k - o));
+  const unsigned nt = (unsigned)std::min<size_t>(pieces.size(), std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t i; (i = next++) < pieces.size();) std::memcpy(std::get<0>(pieces[i]), std::get<1>(pieces[i]), std::get<2>(pieces[i]));
+  };
+  std::vector<std::thread> ts;
+  for (unsigned t = 1; t < nt; t++) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
 }
 
 std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {

@@ -214,6 +214,8 @@ struct Image {
   }
   std::vector<uint8_t> serialize() const;
   uint8_t* serialize_malloc(size_t* len) const;  // the blob in one malloc'd buffer (cg_free)
+  size_t blob_size() const;
+  void serialize_into(uint8_t* out) const;  // blob_size() bytes; large sections on several threads
   void write_blob(void* writer) const;
   // device region of the blob this image was read from (image.h DevSection): section offsets and
   // byte sizes, and the region's bounds (blob offsets)

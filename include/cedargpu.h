@@ -102,6 +102,12 @@ int cg_compiler_cache_stats(cg_compiler* c, uint64_t* hits, uint64_t* misses, ui
  * an action table past 64 entries, the static entities) or the arenas hold more garbage than live
  * words. */
 int cg_compiler_build(cg_compiler* c, uint64_t epoch, uint8_t** image, size_t* len);
+/* The same build in two steps, for callers that own the blob's memory: cg_compiler_build_sized
+ * compiles and holds the image, returning its blob size; cg_compiler_write_image serializes it into
+ * the caller's buffer of at least that size (large sections copied on several threads) and drops
+ * it. No intermediate copy of the blob (C5's 113 MB image). */
+int cg_compiler_build_sized(cg_compiler* c, uint64_t epoch, size_t* len);
+int cg_compiler_write_image(cg_compiler* c, void* out, size_t cap);
 /* Incremental rebuilds on (default) or off (every build a full one). */
 int cg_compiler_set_incremental(cg_compiler* c, int on);
 /* The last build: *incremental 1 when it reused lowered documents, policies it lowered and reused,
