@@ -203,3 +203,32 @@ def test_delta_arbitrary_bytes_and_rejections():
     bad[56 + 16:56 + 24] = (len(base) + 10).to_bytes(8, "little")  # the first operation's src
     with pytest.raises(cedargpu.CedarGPUError):
         cedargpu.image_patch(base, bytes(bad))
+
+
+def test_two_step_build_writes_the_same_blob():
+    """cg_compiler_build_sized + cg_compiler_write_image (Compiler.build's path: the blob serialized
+    straight into the caller's buffer, sections of >= 1 MB copied on several threads) gives the
+    bytes cg_compiler_build returns; a write without a held image, or into a short buffer, fails."""
+    import ctypes
+    lib = cedargpu._lib.lib
+    pop = synth.Population(seed=3, n_users=200, n_groups=40)
+    text = synth.abac_policies(3000, seed=9, pop=pop)
+    c = cedargpu.Compiler()
+    two = c.build([cedargpu.MemoryStore("p.cedar", text)], epoch=5, entities=pop.static_entities())
+    c.close()
+    assert len(two) > (1 << 20)  # past the deferred-copy size
+    c = cedargpu.Compiler()
+    c.build([cedargpu.MemoryStore("p.cedar", text)], epoch=5, entities=pop.static_entities())  # same documents held
+    out, n = ctypes.c_void_p(), ctypes.c_size_t(0)
+    assert lib.cg_compiler_build(c._h, 5, ctypes.byref(out), ctypes.byref(n)) == 0
+    one = ctypes.string_at(out, n.value)
+    lib.cg_free(out)
+    assert one == two
+    buf = ctypes.create_string_buffer(16)
+    assert lib.cg_compiler_write_image(c._h, buf, 16) != 0  # nothing held
+    assert lib.cg_compiler_build_sized(c._h, 5, ctypes.byref(n)) == 0
+    assert lib.cg_compiler_write_image(c._h, buf, 16) != 0  # too short
+    big = ctypes.create_string_buffer(n.value)
+    assert lib.cg_compiler_write_image(c._h, big, n.value) == 0
+    assert big.raw == two
+    c.close()
