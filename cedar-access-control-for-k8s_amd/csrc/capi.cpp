@@ -57,6 +57,7 @@ struct cg_compiler {
   BuildInfo last;
   std::string err;
   std::shared_ptr<Image> built;  // cg_compiler_build_sized's image until cg_compiler_write_image
+  size_t built_len = 0;
 };
 
 namespace {
@@ -678,7 +679,7 @@ int cg_compiler_build_sized(cg_compiler* c, uint64_t epoch, size_t* len) {
     c->built.reset();
     c->built = compile_image(c->tiers, epoch, &c->cache, &c->statics, &c->skipped, c->incremental ? c->lower.get() : nullptr,
                              c->statics_gen, &c->last);
-    *len = c->built->blob_size();
+    *len = c->built_len = c->built->blob_size();
     return CG_OK;
   } catch (const CedarError& e) {
     c->err = e.what();
@@ -693,7 +694,7 @@ int cg_compiler_build_sized(cg_compiler* c, uint64_t epoch, size_t* len) {
 int cg_compiler_write_image(cg_compiler* c, void* out, size_t cap) {
   if (!c || !out) return CG_E_ARG;
   if (!c->built) { c->err = "no image built (cg_compiler_build_sized)"; return CG_E_STATE; }
-  if (cap < c->built->blob_size()) { c->err = "buffer smaller than the image blob"; return CG_E_RANGE; }
+  if (cap < c->built_len) { c->err = "buffer smaller than the image blob"; return CG_E_RANGE; }
   try {
     c->built->serialize_into((uint8_t*)out);
   } catch (const std::exception& e) {

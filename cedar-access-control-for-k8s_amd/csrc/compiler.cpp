@@ -1314,16 +1314,17 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   // scope bitsets (image.h "scope bitsets"): a row per context of the keys whose principal
   // component is an entity, a bit per key entity: level-1 keys that file policies directly, and
   // every level-2 key. The bits' buckets (svals) are known once the heads are laid out, below.
-  // (hashed while filled, walked in key order below: 290k lookups into a std::map were 87 ms of
-  // a 100k-policy build)
-  struct CtxHash {
-    size_t operator()(const std::array<uint32_t, 8>& a) const {
-      uint64_t h = 0x9E3779B97F4A7C15ull;
-      for (uint32_t w : a) h = (h ^ w) * 0xBF58476D1CE4E5B9ull, h ^= h >> 29;
-      return (size_t)h;
-    }
+  // Contexts get their rows in first-seen order (level-1 groups, then level-2), walked in key
+  // order below. Keys, hashes and key-entity indices are computed side by side; the rows are then
+  // assigned in order through one open-addressing table (290k lookups into a std::map were 87 ms
+  // of a 100k-policy build).
+  using CtxKey = std::array<uint32_t, 8>;
+  auto ctx_hash = [](const CtxKey& a) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (uint32_t w : a) h = (h ^ w) * 0xBF58476D1CE4E5B9ull, h ^= h >> 29;
+    return h;
   };
-  std::unordered_map<std::array<uint32_t, 8>, uint32_t, CtxHash> ctx;
+  std::vector<std::pair<CtxKey, uint32_t>> ctx;  // (key, row) in row order
   struct SBit { uint32_t row, kidx, grp; };  // grp: g1 index, or g2 index | SB_L2
   constexpr uint32_t SB_L2 = 0x80000000u;
   std::vector<SBit> sbit;
@@ -1333,6 +1334,10 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       return (uint32_t)(std::lower_bound(img.key_ents.begin(), img.key_ents.end(), u) - img.key_ents.begin());
     };
     img.l2_vmask = img.l2_lmask = 0;
+    // candidates: the level-1 groups that file policies directly, then every level-2 group, of
+    // entity-principal combos
+    struct Cand { CtxKey key; uint64_t h; uint32_t kidx, grp; };
+    std::vector<uint32_t> c1;
     for (size_t gi = 0; gi < g1.size(); gi++) {
       const G& g = g1[gi];
       const L1& k = r1[g.b].first;
@@ -1341,17 +1346,42 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       img.l2_lmask |= g.cmask;
       bool direct = false;
       for (size_t i = g.b; i < g.e && !direct; i++) direct = r1[i].second != NO_POLICY;
-      if (!direct) continue;
-      const uint32_t row = ctx.emplace(std::array<uint32_t, 8>{k[0], k[3], k[4], k[5], k[6], SCTX_L1, 0u, 0u}, (uint32_t)ctx.size()).first->second;
-      sbit.push_back({row, kidx(k[1], k[2]), (uint32_t)gi});
+      if (direct) c1.push_back((uint32_t)gi);
     }
-    for (size_t gi = 0; gi < g2.size(); gi++) {
-      const G& g = g2[gi];
-      const L1& k = r2[g.b].first.first;
-      if ((k[0] & 3) != KC_ENT) continue;
-      const auto& x = r2[g.b].first.second;
-      const uint32_t row = ctx.emplace(std::array<uint32_t, 8>{k[0], k[3], k[4], k[5], k[6], x[0], x[1], x[2]}, (uint32_t)ctx.size()).first->second;
-      sbit.push_back({row, kidx(k[1], k[2]), (uint32_t)gi | SB_L2});
+    std::vector<uint32_t> c2;
+    c2.reserve(g2.size());
+    for (size_t gi = 0; gi < g2.size(); gi++)
+      if ((r2[g2[gi].b].first.first[0] & 3) == KC_ENT) c2.push_back((uint32_t)gi);
+    std::vector<Cand> cand(c1.size() + c2.size());
+    parallel_range(cand.size(), [&](size_t c) {
+      Cand& o = cand[c];
+      if (c < c1.size()) {
+        const L1& k = r1[g1[c1[c]].b].first;
+        o.key = CtxKey{k[0], k[3], k[4], k[5], k[6], SCTX_L1, 0u, 0u};
+        o.kidx = kidx(k[1], k[2]);
+        o.grp = c1[c];
+      } else {
+        const uint32_t gi = c2[c - c1.size()];
+        const L1& k = r2[g2[gi].b].first.first;
+        const auto& x = r2[g2[gi].b].first.second;
+        o.key = CtxKey{k[0], k[3], k[4], k[5], k[6], x[0], x[1], x[2]};
+        o.kidx = kidx(k[1], k[2]);
+        o.grp = gi | SB_L2;
+      }
+      o.h = ctx_hash(o.key);
+    });
+    size_t slots = 16;
+    while (slots < 2 * cand.size()) slots <<= 1;
+    std::vector<uint32_t> table(slots, 0);  // row + 1
+    sbit.reserve(cand.size());
+    for (const Cand& o : cand) {
+      size_t h = (size_t)o.h & (slots - 1);
+      while (table[h] && ctx[table[h] - 1].first != o.key) h = (h + 1) & (slots - 1);
+      if (!table[h]) {
+        ctx.emplace_back(o.key, (uint32_t)ctx.size());
+        table[h] = (uint32_t)ctx.size();
+      }
+      sbit.push_back({table[h] - 1, o.kidx, o.grp});
     }
   }
   mark("scope ctx");
@@ -1480,7 +1510,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     uint32_t slots = 2;
     while (slots < 2 * ctx.size()) slots <<= 1;
     img.sctx.assign((size_t)slots * SCTX_WORDS, 0);
-    std::vector<std::pair<std::array<uint32_t, 8>, uint32_t>> ctx_sorted(ctx.begin(), ctx.end());
+    std::vector<std::pair<CtxKey, uint32_t>> ctx_sorted(ctx.begin(), ctx.end());
     std::sort(ctx_sorted.begin(), ctx_sorted.end());
     for (auto& c : ctx_sorted) {
       const auto& x = c.first;
