@@ -1283,33 +1283,44 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   // groups: [begin, end) ranges of one key; level-1 hmask from the level-2 keys under it
   struct G { size_t b, e; uint32_t hmask = 0, cmask = 0; uint32_t bloom[4] = {0, 0, 0, 0}; };
   std::vector<G> g1, g2;
-  for (size_t i = 0; i < r1.size();) {
-    size_t j = i;
-    while (j < r1.size() && r1[j].first == r1[i].first) j++;
-    g1.push_back({i, j});
-    i = j;
-  }
-  for (size_t i = 0; i < r2.size();) {
-    size_t j = i;
-    while (j < r2.size() && r2[j].first == r2[i].first) j++;
-    g2.push_back({i, j});
-    i = j;
-  }
-  for (size_t a = 0, k = 0; a < g2.size(); a++) {  // both in the same level-1 order
+  // group starts flagged side by side, collected in order
+  auto group = [&](const auto& r, std::vector<G>& out) {
+    const size_t n = r.size();
+    std::vector<uint8_t> st(n);
+    parallel_range(n, [&](size_t i) { st[i] = i == 0 || !(r[i].first == r[i - 1].first); });
+    for (size_t i = 0; i < n; i++)
+      if (st[i]) {
+        if (!out.empty()) out.back().e = i;
+        out.push_back({i, n});
+      }
+  };
+  group(r1, g1);
+  group(r2, g2);
+  // each level-2 group's level-1 group by binary search over (hash, key) (both lists in that
+  // order), its bits OR-ed in atomically: groups side by side, the same masks as in order
+  std::vector<uint32_t> h1g(g1.size());
+  parallel_range(g1.size(), [&](size_t k) { h1g[k] = l1_hash(r1[g1[k].b].first); });
+  parallel_range(g2.size(), [&](size_t a) {
     const L1& key = r2[g2[a].b].first.first;
     const uint32_t hk = l1_hash(key);
-    while (k < g1.size() && l1_less(r1[g1[k].b].first, l1_hash(r1[g1[k].b].first), key, hk)) k++;
+    size_t lo = 0, hi = g1.size();
+    while (lo < hi) {
+      const size_t mid = (lo + hi) / 2;
+      if (l1_less(r1[g1[mid].b].first, h1g[mid], key, hk)) lo = mid + 1;
+      else hi = mid;
+    }
+    const size_t k = lo;
     if (k < g1.size() && r1[g1[k].b].first == key) {
       const auto& x = r2[g2[a].b].first.second;
-      if (x[0] & BT_CKEY) g1[k].cmask |= 1u << (x[0] & ~BT_CKEY);
-      else g1[k].hmask |= 1u << x[0];
+      if (x[0] & BT_CKEY) __atomic_fetch_or(&g1[k].cmask, 1u << (x[0] & ~BT_CKEY), __ATOMIC_RELAXED);
+      else __atomic_fetch_or(&g1[k].hmask, 1u << x[0], __ATOMIC_RELAXED);
       const uint32_t bits = l2_bloom_bits(bucket_hash2(key_hash(key[0], key[1], key[2], key[3], key[4], key[5], key[6]), x[0], x[1], x[2]));
       for (uint32_t j = 0; j < 3; j++) {
-        const uint32_t b = (bits >> (7 * j)) & 127u;
-        g1[k].bloom[b >> 5] |= 1u << (b & 31);
+        const uint32_t bb = (bits >> (7 * j)) & 127u;
+        __atomic_fetch_or(&g1[k].bloom[bb >> 5], 1u << (bb & 31), __ATOMIC_RELAXED);
       }
     }
-  }
+  });
   mark("buckets");
   // scope bitsets (image.h "scope bitsets"): a row per context of the keys whose principal
   // component is an entity, a bit per key entity: level-1 keys that file policies directly, and
