@@ -1833,26 +1833,36 @@ static std::shared_ptr<Image> compile_incremental(LowerState& S, const std::vect
   std::vector<Compiler::AttrKey> akeys;
   size_t total = 0;
   for (auto& tp : parsed) total += tp.size();
-  img->pol.reserve(total * POL_WORDS);
-  img->meta.reserve(total);
-  akeys.reserve(total);
-  for (size_t t = 0; t < parsed.size(); t++) {
-    for (auto& r : parsed[t]) {
-      LowerState::Doc& D = *dref[r.doc];
-      D.used = S.gen;
-      const LowerState::Pol& P = D.pols[r.idx];
-      const size_t at = img->pol.size();
-      img->pol.insert(img->pol.end(), P.w.begin(), P.w.end());
-      img->pol[at + PW_FLAGS] |= (uint32_t)t << 8;
-      if (P.w[PW_FLAGS] & PF_ATOMIC) img->n_atomic++;
-      else img->lane_need = std::max(img->lane_need, P.w[PW_LANE]);
-      akeys.push_back(P.key);
-      PolicyMeta m;
-      m.id = r.id; m.filename = *r.filename; m.pos = r.pos; m.tier = (uint32_t)t;
-      m.forbid = r.p->forbid;
-      img->meta.push_back(std::move(m));
+  // every policy's words, key and metadata at its index, written side by side
+  std::vector<std::pair<uint32_t, uint32_t>> at(total);  // (tier, index in tier)
+  {
+    size_t q = 0;
+    for (size_t t = 0; t < parsed.size(); t++) {
+      for (size_t i = 0; i < parsed[t].size(); i++) at[q++] = {(uint32_t)t, (uint32_t)i};
+      img->tier_end.push_back((uint32_t)q);
     }
-    img->tier_end.push_back(img->n_pol());
+  }
+  for (auto& tp : parsed)
+    for (auto& r : tp) dref[r.doc]->used = S.gen;
+  img->pol.resize(total * POL_WORDS);
+  img->meta.resize(total);
+  akeys.resize(total);
+  std::vector<uint8_t> atomic(total);
+  parallel_range(total, [&](size_t q) {
+    const uint32_t t = at[q].first;
+    const PRef& r = parsed[t][at[q].second];
+    const LowerState::Pol& P = dref[r.doc]->pols[r.idx];
+    std::copy(P.w.begin(), P.w.end(), img->pol.begin() + (long)(q * POL_WORDS));
+    img->pol[q * POL_WORDS + PW_FLAGS] |= t << 8;
+    atomic[q] = (P.w[PW_FLAGS] & PF_ATOMIC) != 0;
+    akeys[q] = P.key;
+    PolicyMeta& m = img->meta[q];
+    m.id = r.id; m.filename = *r.filename; m.pos = r.pos; m.tier = t;
+    m.forbid = r.p->forbid;
+  });
+  for (size_t q = 0; q < total; q++) {
+    if (atomic[q]) img->n_atomic++;
+    else img->lane_need = std::max(img->lane_need, img->pol[q * POL_WORDS + PW_LANE]);
   }
   // documents this build did not use leave the cache; their words stay in the arenas as garbage
   size_t live = S.base_words;
