@@ -1001,7 +1001,7 @@ template <class T>
 static void parallel_sort(std::vector<T>& v, unsigned threads) {
   const size_t n = v.size();
   unsigned parts = 1;
-  while (parts * 2 <= threads && n / (parts * 2) >= (1u << 15)) parts *= 2;
+  while (parts * 2 <= threads && n / (parts * 2) >= (1u << 14)) parts *= 2;
   if (parts == 1) { std::sort(v.begin(), v.end()); return; }
   std::vector<size_t> cut(parts + 1);
   for (unsigned k = 0; k <= parts; k++) cut[k] = n * k / parts;
@@ -1138,7 +1138,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     });
     for (uint32_t q = 0; q < n; q++) rep[q] = q;
     if (!off) {
-      std::sort(hq.begin(), hq.end());
+      parallel_sort(hq, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
       auto same = [&](uint32_t x, uint32_t y) {
         const uint32_t L = klen(x);
         if (klen(y) != L) return false;
