@@ -12,4 +12,4 @@ from ._lib import CedarGPUError, CompileError, DeadlineError, DeviceError, lib, 
 from .store import (ALLOW_ALL_ADMISSION, FAULT_BAD_KIDX, FAULT_DEVICE_ERROR, FAULT_NONE, FAULT_STALL, AdmissionHandler,  # noqa: F401
                     Authorizer, AVPStore, Batch, Compiler, Context, CRDStore, DirectoryStore, MemoryStore, PolicyStore,
                     Queue, StaticStore, TieredPolicyStores, admission_to_cedar_json, atomic_policies, build_image,
-                    delta_info, device_count, image_delta, image_patch, image_stats, index_stats)
+                    delta_info, device_count, image_delta, image_patch, image_stats, index_stats, pinned_stats)

@@ -89,6 +89,7 @@ _SIGS = {
     "cg_ctx_destroy": (None, [P]),
     "cg_last_error": (cstr, [P]),
     "cg_ctx_inject_fault": (ctypes.c_int, [P, ctypes.c_int, u64]),
+    "cg_pinned_stats": (ctypes.c_int, [ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     "cg_image_load": (ctypes.c_int, [P, P, sz, u64]),
     "cg_image_load_device": (ctypes.c_int, [P, P, sz, u64, P]),
     "cg_image_load_peer": (ctypes.c_int, [P, P, u64]),

@@ -393,6 +393,14 @@ class Context:
             raise _err(rc, "inject_fault failed")
 
 
+def pinned_stats() -> dict:
+    """cg_pinned_stats: the encoder's process-wide pinned pool (bytes held, idle blocks) and the
+    number of batches closed in flight that kept their arrays until their stream drained."""
+    held, idle, kept = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    lib.cg_pinned_stats(ctypes.byref(held), ctypes.byref(idle), ctypes.byref(kept))
+    return {"held_bytes": held.value, "idle_blocks": idle.value, "kept_batches": kept.value}
+
+
 class Batch:
     def __init__(self, ctx: Context):
         self.ctx = ctx

@@ -821,6 +821,12 @@ int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg) {
   }
 }
 
+int cg_pinned_stats(uint64_t* held_bytes, uint64_t* idle_blocks, uint64_t* kept_batches) {
+  cg::pinned_stats(held_bytes, idle_blocks);
+  if (kept_batches) *kept_batches = cg::g_pinned_kept.load(std::memory_order_relaxed);
+  return CG_OK;
+}
+
 int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch) {
   if (!ctx || !image) return CG_E_ARG;
   std::shared_ptr<Image> img;

@@ -100,6 +100,7 @@ struct cg_batch {
         a->heap.swap(host.heap); a->req_base.swap(host.req_base); a->rows.swap(host.rows);
         a->gkeys.swap(host.gkeys); a->bstr_off.swap(host.bstr_off); a->bstr_bytes.swap(host.bstr_bytes);
         dev.keep = std::move(a);
+        cg::g_pinned_kept.fetch_add(1, std::memory_order_relaxed);
       } catch (...) {
         cg::dev_batch_free(&dev);  // (drains the stream first)
       }

@@ -3282,6 +3282,11 @@ static size_t size_class(size_t n) {
   return c;
 }
 
+static bool pinned_noncoherent() {
+  static const bool on = [] { const char* e = std::getenv("CEDARGPU_PINNED_NONCOHERENT"); return e && *e == '1'; }();
+  return on;
+}
+
 static int pool_get(DevPool* p, bool host, size_t n, void** out, size_t* cls) {
   *cls = size_class(n);
   pool_reap(p);
@@ -3295,9 +3300,10 @@ static int pool_get(DevPool* p, bool host, size_t n, void** out, size_t* cls) {
       return 0;
     }
   }
-  // CEDARGPU_PINNED_NONCOHERENT=1: pinned blocks the GPU may cache (they are only ever DMA
-  // copy sources and targets, never read by kernels) (A/B: the host's own reads of the results)
-  static const unsigned pflags = [] { const char* e = std::getenv("CEDARGPU_PINNED_NONCOHERENT"); return (e && *e == '1') ? hipHostMallocNonCoherent : hipHostMallocDefault; }();
+  // CEDARGPU_PINNED_NONCOHERENT=1: pinned blocks the GPU may cache (A/B: the host's own reads of
+  // the results). Kernels write zero-copy results into these blocks (DevBatch::zc), so that option
+  // turns zero-copy off (dev_batch_upload): non-coherent blocks are then only DMA sources and targets.
+  const unsigned pflags = pinned_noncoherent() ? hipHostMallocNonCoherent : hipHostMallocDefault;
   if (host) HIPCHK(hipHostMalloc(out, *cls, pflags), "hipHostMalloc");
   else HIPCHK(hipMalloc(out, *cls), "hipMalloc");
   std::lock_guard<std::mutex> g(p->mu);
@@ -3365,6 +3371,13 @@ bool pinned_give(void* p, size_t) {
   if (it == pa.cls.end()) return false;
   pa.idle.emplace(it->second, p);
   return true;
+}
+
+void pinned_stats(uint64_t* held_bytes, uint64_t* idle_blocks) {
+  auto& pa = pinned_arrays();
+  std::lock_guard<std::mutex> g(pa.mu);
+  if (held_bytes) *held_bytes = pa.held;
+  if (idle_blocks) *idle_blocks = pa.idle.size();
 }
 
 bool pinned_block(const void* p, size_t bytes) {
@@ -3488,7 +3501,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // rows) are copied from there directly ("direct"); the rest is staged into one pinned block and
   // copied in one piece. Device layout: staged sections | (zero-copy) counters | direct sections.
   static const bool zc_on = !(std::getenv("CEDARGPU_ZERO_COPY") && *std::getenv("CEDARGPU_ZERO_COPY") == '0');
-  d.zc = d.small && zc_on;
+  d.zc = d.small && zc_on && !pinned_noncoherent();
   // (each copy costs ~10 us of queue gap on the device: the heap goes direct from PIN_MIN, the
   // other sections from 1 MB, CEDARGPU_DIRECT_MIN_KB; a 2,048-request C3 batch: its 1.8 MB heap
   // direct, 0.6 MB staged; submit -> results 173 -> 157 us, all four direct 159 us)
@@ -3689,6 +3702,10 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.bytes = in_bytes + d.out_bytes;
   d.stream = stream;
   d.pending = true;
+  // (set before the copy into *out: ~cg_batch reads out->direct to keep the direct sources alive
+  // past a close while in flight, DevBatch::keep)
+  d.direct = false;
+  for (int k = 0; k < NSEC; k++) d.direct = d.direct || direct[k];
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
   // (one copy: staging in pieces with an H2D per piece, to overlap the two, made 1-2k-request
   // batches 0.06-0.07 ms slower on the box, gpurun_out/r04flat3)
@@ -3697,8 +3714,6 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // cg_batch's destructor hands them to the retired batch, DevBatch::keep)
   for (int k = 0; k < NSEC; k++)
     if (direct[k]) HIPCHK(hipMemcpyAsync(in + off[k], src[k], len[k], hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D (pinned array)");
-  d.direct = false;
-  for (int k = 0; k < NSEC; k++) d.direct = d.direct || direct[k];
   if (!d.zc) HIPCHK(hipMemsetAsync(d.res, 0, o_rf, s), "memset res");  // (and the worklist counters)
   return 0;
 }
@@ -4276,12 +4291,14 @@ int64_t dev_now_ns() {
 // Waits for `ev` until deadline_ns (< 0: none): spins with yields for the first ~500 us (results
 // of a latency-bound batch arrive within that: the serving queue's submitter polls every batch in
 // 10 ms slices), then sleeps 10 us between queries.
-static int wait_event(hipEvent_t ev, int64_t deadline_ns, const char* what) {
+// t0 (0: now) is when the caller's first wait on this event began: a caller that waits in slices
+// spins once per event, not once per slice.
+static int wait_event(hipEvent_t ev, int64_t deadline_ns, const char* what, int64_t t0 = 0) {
   if (deadline_ns < 0) {
     HIPCHK(hipEventSynchronize(ev), what);
     return 0;
   }
-  const int64_t t0 = dev_now_ns();
+  if (!t0) t0 = dev_now_ns();
   for (;;) {
     const hipError_t q = hipEventQuery(ev);
     if (q == hipSuccess) return 0;
@@ -4398,6 +4415,7 @@ int dev_download_async(DevBatch& b, void* stream) {
   if (b.zc && b.fu_cnt) HIPCHK(hipMemcpyAsync(b.zc_cnt, b.fu_cnt, (FU_KINDS + 1) * 4, hipMemcpyDeviceToHost, s), "D2H counters");
   else if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
   HIPCHK(hipEventRecord((hipEvent_t)b.done, s), "event record");
+  b.wait_t0 = 0;
   return 0;
 }
 
@@ -4406,7 +4424,8 @@ int dev_download_async(DevBatch& b, void* stream) {
 int dev_download_finish(DevBatch& b, Batch& host, int64_t deadline_ns) {
   HIPCHK(hipSetDevice(b.device), "hipSetDevice");
   if (b.done) {
-    const int rc = wait_event((hipEvent_t)b.done, deadline_ns, "batch");
+    if (!b.wait_t0) b.wait_t0 = dev_now_ns();
+    const int rc = wait_event((hipEvent_t)b.done, deadline_ns, "batch", b.wait_t0);
     if (rc) return rc;  // DEV_TIMEOUT: still in flight (pending), wait again or destroy
   }
   b.pending = false;

@@ -109,6 +109,7 @@ struct DevBatch {
   void* stream = nullptr;  // the stream the batch's work runs on
   void* done = nullptr;    // event after the result download (dev_download_async)
   bool pending = false;    // work enqueued on the batch's buffers not yet waited for
+  int64_t wait_t0 = 0;     // when the first wait on `done` began (dev_now_ns; 0: not yet)
 };
 
 // Batches of at most this many requests on an indexed image run as one launch (DevBatch::small);

@@ -122,6 +122,10 @@ void dev_image_free(DevImage* d) {
 void* pinned_take(size_t) { return nullptr; }
 bool pinned_give(void*, size_t) { return false; }
 bool pinned_block(const void*, size_t) { return false; }
+void pinned_stats(uint64_t* held_bytes, uint64_t* idle_blocks) {
+  if (held_bytes) *held_bytes = 0;
+  if (idle_blocks) *idle_blocks = 0;
+}
 
 int dev_pool_create(int device, DevPool** out) {
   *out = new DevPool();

@@ -16,6 +16,10 @@
 #include "encode_impl.h"
 
 namespace cg {
+std::atomic<uint64_t> g_pinned_kept{0};
+}  // namespace cg
+
+namespace cg {
 
 bool hugepages_on() {
   static const bool on = [] { const char* e = std::getenv("CEDARGPU_HUGEPAGES"); return e && *e == '1'; }();

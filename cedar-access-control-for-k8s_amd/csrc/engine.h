@@ -36,6 +36,8 @@ bool huge_unmap(void* p, size_t bytes);
 void* pinned_take(size_t bytes);
 bool pinned_give(void* p, size_t bytes);
 bool pinned_block(const void* p, size_t bytes);
+void pinned_stats(uint64_t* held_bytes, uint64_t* idle_blocks);
+extern std::atomic<uint64_t> g_pinned_kept;  // batches closed in flight that kept their arrays
 constexpr size_t PIN_MIN = 64u << 10, PIN_MAX = 16u << 20;  // array sizes that take pinned blocks
 
 // An allocator whose resize() leaves new elements uninitialised: a batch's large arrays are

@@ -155,6 +155,11 @@ const char* cg_last_error(cg_ctx* ctx);
 #define CG_FAULT_STALL 2
 #define CG_FAULT_BAD_KIDX 3
 int cg_ctx_inject_fault(cg_ctx* ctx, int kind, uint64_t arg);
+/* Diagnostics of the process-wide pinned pool the encoder writes small batches' arrays into:
+ * bytes of pinned blocks held, blocks idle (free for the next batch), and batches that were closed
+ * while their upload from those blocks could still run and so handed their arrays to the retired
+ * batch until its stream drains. Any pointer may be NULL. (No reference counterpart: a test hook.) */
+int cg_pinned_stats(uint64_t* held_bytes, uint64_t* idle_blocks, uint64_t* kept_batches);
 /* Copies and uploads an image; the caller keeps ownership of `image`. Not active until activated. */
 int cg_image_load(cg_ctx* ctx, const void* image, size_t len, uint64_t epoch);
 /* Loads an image whose serialized blob is already in device memory on ctx's device, e.g. the

@@ -269,11 +269,15 @@ def test_closed_in_flight_batch_keeps_its_pinned_arrays(ctx):
     want = [b.authz(i) for i in range(len(b))]
     b.close()
     ctx.inject_fault(cedargpu.FAULT_STALL, 200_000)
+    kept0 = cedargpu.pinned_stats()["kept_batches"]
     for _ in range(3):
         b = ctx.batch()
         b.add_sar_json(payload)
         b.submit()
         b.close()  # in flight: retired, never waited
+    # the mechanism itself: each closed in-flight batch handed its pinned arrays to the retired batch
+    # (a batch whose DevBatch::direct never reached cg_batch would return them to the pool at once)
+    assert cedargpu.pinned_stats()["kept_batches"] - kept0 == 3
     ctx.inject_fault(cedargpu.FAULT_NONE)
     for _ in range(3):
         b = ctx.batch()
