@@ -1128,8 +1128,27 @@ struct Evaluator {
     return reach(a, &t, 1);
   }
 
-  static bool as_bool(const Val& v) {
-    if (v.t != VT::Bool) type_error("bool", v);
+  // Errors are values, as in cedar-go (an evaluation returns (Value, error)): a failing step sets
+  // `failed` and the message, and every caller returns at once (CHK). No exception crosses the
+  // evaluator, so a policy that errors costs what a false one does.
+  bool failed = false;
+  std::string emsg;
+  Val fail(std::string m) {
+    failed = true;
+    emsg = std::move(m);
+    return Val();
+  }
+  Val terr(const char* expected, const Val& got) {
+    return fail(std::string("type error: expected ") + expected + ", got " + type_name(got));
+  }
+#define CHK(x)             \
+  do {                     \
+    (x);                   \
+    if (failed) return {}; \
+  } while (0)
+  // v must be a bool: false on a type error (failed set)
+  bool as_bool(const Val& v) {
+    if (v.t != VT::Bool) { terr("bool", v); return false; }
     return v.i != 0;
   }
   static Val B(bool b) { Val v; v.t = VT::Bool; v.i = b; return v; }
@@ -1139,115 +1158,185 @@ struct Evaluator {
     switch (e.k) {
       case EK::Lit: return e.lit;
       case EK::Var: return e.var == 0 ? it.principal : e.var == 1 ? it.action : e.var == 2 ? it.resource : it.context;
-      case EK::And:
-        if (!as_bool(ev(*e.kids[0]))) return B(false);
-        return B(as_bool(ev(*e.kids[1])));
-      case EK::Or:
-        if (as_bool(ev(*e.kids[0]))) return B(true);
-        return B(as_bool(ev(*e.kids[1])));
-      case EK::Not: return B(!as_bool(ev(*e.kids[0])));
+      case EK::And: {
+        Val x;
+        CHK(x = ev(*e.kids[0]));
+        bool bx;
+        CHK(bx = as_bool(x));
+        if (!bx) return B(false);
+        Val y;
+        CHK(y = ev(*e.kids[1]));
+        bool by;
+        CHK(by = as_bool(y));
+        return B(by);
+      }
+      case EK::Or: {
+        Val x;
+        CHK(x = ev(*e.kids[0]));
+        bool bx;
+        CHK(bx = as_bool(x));
+        if (bx) return B(true);
+        Val y;
+        CHK(y = ev(*e.kids[1]));
+        bool by;
+        CHK(by = as_bool(y));
+        return B(by);
+      }
+      case EK::Not: {
+        Val x;
+        CHK(x = ev(*e.kids[0]));
+        bool bx;
+        CHK(bx = as_bool(x));
+        return B(!bx);
+      }
       case EK::Neg: {
-        Val v = ev(*e.kids[0]);
-        if (v.t != VT::Long) type_error("long", v);
-        if (v.i == INT64_MIN) throw EvalError{"integer overflow"};
+        Val v;
+        CHK(v = ev(*e.kids[0]));
+        if (v.t != VT::Long) return terr("long", v);
+        if (v.i == INT64_MIN) return fail("integer overflow");
         return L(-v.i);
       }
-      case EK::If: return as_bool(ev(*e.kids[0])) ? ev(*e.kids[1]) : ev(*e.kids[2]);
+      case EK::If: {
+        Val c;
+        CHK(c = ev(*e.kids[0]));
+        bool bc;
+        CHK(bc = as_bool(c));
+        return bc ? ev(*e.kids[1]) : ev(*e.kids[2]);
+      }
       case EK::Bin: {
-        Val a = ev(*e.kids[0]);
-        Val b = ev(*e.kids[1]);
+        Val a, b;
+        CHK(a = ev(*e.kids[0]));
+        CHK(b = ev(*e.kids[1]));
         return binop(e.op, a, b);
       }
       case EK::Has: {
-        Val v = ev(*e.kids[0]);
+        Val v;
+        CHK(v = ev(*e.kids[0]));
         if (v.t == VT::Ent) {
           const Entity* en = find(v);
           return B(en && rec_get(en->attrs.agg, e.name));
         }
         if (v.t == VT::Rec) return B(rec_get(v.agg, e.name) != nullptr);
-        type_error("entity or record", v);
+        return terr("entity or record", v);
       }
       case EK::Attr: {
-        Val v = ev(*e.kids[0]);
+        Val v;
+        CHK(v = ev(*e.kids[0]));
         if (v.t == VT::Ent) {
           const Entity* en = find(v);
-          if (!en) throw EvalError{"entity `" + uid_str(v) + "` does not exist"};
+          if (!en) return fail("entity `" + uid_str(v) + "` does not exist");
           const Val* x = rec_get(en->attrs.agg, e.name);
-          if (!x) throw EvalError{"`" + uid_str(v) + "` does not have the attribute `" + e.name + "`"};
+          if (!x) return fail("`" + uid_str(v) + "` does not have the attribute `" + e.name + "`");
           return *x;
         }
         if (v.t == VT::Rec) {
           const Val* x = rec_get(v.agg, e.name);
-          if (!x) throw EvalError{"record does not have the attribute `" + e.name + "`"};
+          if (!x) return fail("record does not have the attribute `" + e.name + "`");
           return *x;
         }
-        type_error("entity or record", v);
+        return terr("entity or record", v);
       }
       case EK::Like: {
-        Val v = ev(*e.kids[0]);
-        if (v.t != VT::Str) type_error("string", v);
+        Val v;
+        CHK(v = ev(*e.kids[0]));
+        if (v.t != VT::Str) return terr("string", v);
         return B(like_match(*v.s, e.pat, 0, 0));
       }
       case EK::Is: {
-        Val v = ev(*e.kids[0]);
-        if (v.t != VT::Ent) type_error("entity", v);
+        Val v;
+        CHK(v = ev(*e.kids[0]));
+        if (v.t != VT::Ent) return terr("entity", v);
         if (*v.et != e.name) return B(false);
         if (!e.has_in) return B(true);
-        return B(in_op(v, ev(*e.kids[1])));
+        Val w;
+        CHK(w = ev(*e.kids[1]));
+        bool r;
+        CHK(r = in_op(v, w));
+        return B(r);
       }
       case EK::Set: {
         Agg* a = A.agg();
-        for (auto& k : e.kids) set_add(a, ev(*k));
+        for (auto& k : e.kids) {
+          Val x;
+          CHK(x = ev(*k));
+          set_add(a, x);
+        }
         Val v; v.t = VT::Set; v.agg = a;
         return v;
       }
       case EK::Rec: {
         Agg* a = A.agg();
-        for (size_t k = 0; k < e.kids.size(); k++) a->fields.emplace_back(&e.keys[k], ev(*e.kids[k]));
+        for (size_t k = 0; k < e.kids.size(); k++) {
+          Val x;
+          CHK(x = ev(*e.kids[k]));
+          a->fields.emplace_back(&e.keys[k], x);
+        }
         rec_sort(a);
         Val v; v.t = VT::Rec; v.agg = a;
         return v;
       }
       case EK::Call: {
         std::vector<Val> args;
-        for (auto& k : e.kids) args.push_back(ev(*k));
-        if (args.size() != 1 || args[0].t != VT::Str) throw EvalError{e.name + " takes one string argument"};
+        for (auto& k : e.kids) {
+          Val x;
+          CHK(x = ev(*k));
+          args.push_back(x);
+        }
+        if (args.size() != 1 || args[0].t != VT::Str) return fail(e.name + " takes one string argument");
         Val v;
-        if (e.name == "decimal") { v.t = VT::Dec; v.i = parse_decimal(*args[0].s); return v; }
-        if (e.name == "ip") { v.t = VT::IP; v.ip = A.ip(parse_ip(*args[0].s)); return v; }
-        throw EvalError{"unknown extension function " + e.name};
+        // (the literal parsers report a malformed text by exception, shared with the JSON reader;
+        // converted to a value here, on the extension-call path only)
+        try {
+          if (e.name == "decimal") { v.t = VT::Dec; v.i = parse_decimal(*args[0].s); return v; }
+          if (e.name == "ip") { v.t = VT::IP; v.ip = A.ip(parse_ip(*args[0].s)); return v; }
+        } catch (EvalError& x) {
+          return fail(x.msg);
+        }
+        return fail("unknown extension function " + e.name);
       }
       case EK::Method: {
-        Val recv = ev(*e.kids[0]);
+        Val recv;
+        CHK(recv = ev(*e.kids[0]));
         std::vector<Val> args;
-        for (size_t k = 1; k < e.kids.size(); k++) args.push_back(ev(*e.kids[k]));
+        for (size_t k = 1; k < e.kids.size(); k++) {
+          Val x;
+          CHK(x = ev(*e.kids[k]));
+          args.push_back(x);
+        }
         return method(recv, e.name, args);
       }
     }
-    throw EvalError{"bad expression"};
+    return fail("bad expression");
   }
 
+  // a in b; false with `failed` set on a type error
   bool in_op(const Val& a, const Val& b) {
-    if (a.t != VT::Ent) type_error("entity", a);
+    if (a.t != VT::Ent) { terr("entity", a); return false; }
     if (b.t == VT::Ent) return entity_in(a, *b.et, *b.s);
     if (b.t == VT::Set) {
-      for (auto& x : b.agg->el) if (x.t != VT::Ent) type_error("entity", x);
+      for (auto& x : b.agg->el)
+        if (x.t != VT::Ent) { terr("entity", x); return false; }
       std::vector<KV> ts;
       for (auto& x : b.agg->el) ts.push_back(KV{*x.et, *x.s});
       return reach(a, ts.data(), ts.size());
     }
-    type_error("set or entity", b);
+    terr("set or entity", b);
+    return false;
   }
 
   Val binop(Bin op, const Val& a, const Val& b) {
     switch (op) {
       case Bin::Eq: return B(veq(a, b));
       case Bin::Ne: return B(!veq(a, b));
-      case Bin::In: return B(in_op(a, b));
+      case Bin::In: {
+        bool r;
+        CHK(r = in_op(a, b));
+        return B(r);
+      }
       default: break;
     }
-    if (a.t != VT::Long) type_error("long", a);
-    if (b.t != VT::Long) type_error("long", b);
+    if (a.t != VT::Long) return terr("long", a);
+    if (b.t != VT::Long) return terr("long", b);
     const int64_t x = a.i, y = b.i;
     int64_t z = 0;
     switch (op) {
@@ -1255,22 +1344,22 @@ struct Evaluator {
       case Bin::Le: return B(x <= y);
       case Bin::Gt: return B(x > y);
       case Bin::Ge: return B(x >= y);
-      case Bin::Add: if (__builtin_add_overflow(x, y, &z)) throw EvalError{"integer overflow"}; return L(z);
-      case Bin::Sub: if (__builtin_sub_overflow(x, y, &z)) throw EvalError{"integer overflow"}; return L(z);
-      default: if (__builtin_mul_overflow(x, y, &z)) throw EvalError{"integer overflow"}; return L(z);
+      case Bin::Add: if (__builtin_add_overflow(x, y, &z)) return fail("integer overflow"); return L(z);
+      case Bin::Sub: if (__builtin_sub_overflow(x, y, &z)) return fail("integer overflow"); return L(z);
+      default: if (__builtin_mul_overflow(x, y, &z)) return fail("integer overflow"); return L(z);
     }
   }
 
   Val method(const Val& recv, const std::string& name, const std::vector<Val>& args) {
     if (name == "contains" || name == "containsAll" || name == "containsAny") {
-      if (recv.t != VT::Set) type_error("set", recv);
-      if (args.size() != 1) throw EvalError{name + " takes one argument"};
+      if (recv.t != VT::Set) return terr("set", recv);
+      if (args.size() != 1) return fail(name + " takes one argument");
       if (name == "contains") {
         for (auto& x : recv.agg->el) if (veq(x, args[0])) return B(true);
         return B(false);
       }
       const Val& o = args[0];
-      if (o.t != VT::Set) type_error("set", o);
+      if (o.t != VT::Set) return terr("set", o);
       if (name == "containsAll") {
         for (auto& y : o.agg->el) {
           bool f = false;
@@ -1284,16 +1373,14 @@ struct Evaluator {
       return B(false);
     }
     if (name == "isEmpty") {
-      if (recv.t != VT::Set) type_error("set", recv);
+      if (recv.t != VT::Set) return terr("set", recv);
       return B(recv.agg->el.empty());
     }
     if (name == "lessThan" || name == "lessThanOrEqual" || name == "greaterThan" || name == "greaterThanOrEqual") {
-      if (recv.t != VT::Dec) type_error("decimal", recv);
-      if (args.empty() || args[0].t != VT::Dec) {
-        Val none;  // a missing argument reports the Python oracle's "unknown" type name
-        if (args.empty()) throw EvalError{"type error: expected decimal, got unknown"};
-        type_error("decimal", args[0]);
-      }
+      if (recv.t != VT::Dec) return terr("decimal", recv);
+      // a missing argument reports the Python oracle's "unknown" type name
+      if (args.empty()) return fail("type error: expected decimal, got unknown");
+      if (args[0].t != VT::Dec) return terr("decimal", args[0]);
       const int64_t x = recv.i, y = args[0].i;
       if (name == "lessThan") return B(x < y);
       if (name == "lessThanOrEqual") return B(x <= y);
@@ -1301,7 +1388,7 @@ struct Evaluator {
       return B(x >= y);
     }
     if (name == "isIpv4" || name == "isIpv6" || name == "isLoopback" || name == "isMulticast" || name == "isInRange") {
-      if (recv.t != VT::IP) type_error("IP", recv);
+      if (recv.t != VT::IP) return terr("IP", recv);
       const IPv& ip = *recv.ip;
       if (name == "isIpv4") return B(!ip.v6);
       if (name == "isIpv6") return B(ip.v6);
@@ -1311,16 +1398,14 @@ struct Evaluator {
         return B(ip.a[15] == 1);
       }
       if (name == "isMulticast") return B(ip.v6 ? ip.a[0] == 0xFF : (ip.a[0] >> 4) == 0xE);
-      if (args.empty()) throw EvalError{"type error: expected IP, got unknown"};
-      if (args[0].t != VT::IP) type_error("IP", args[0]);
+      if (args.empty()) return fail("type error: expected IP, got unknown");
+      if (args[0].t != VT::IP) return terr("IP", args[0]);
       const IPv& o = *args[0].ip;
       if (o.v6 != ip.v6) return B(false);
       if (ip.prefix < o.prefix) return B(false);
       uint8_t na[16], nb[16];
       ip_network(ip, na);
-      IPv on = o;
       ip_network(o, nb);
-      (void)on;
       // ip.network within o.network: o's prefix bits of ip's network equal o's network
       const int n = ip.v6 ? 16 : 4;
       for (int k = 0; k < n; k++) {
@@ -1330,8 +1415,9 @@ struct Evaluator {
       }
       return B(true);
     }
-    throw EvalError{"unknown method " + name};
+    return fail("unknown method " + name);
   }
+#undef CHK
 
   bool scope_match(const Scope& sc, const Val& v) {
     switch (sc.k) {
@@ -1349,13 +1435,17 @@ struct Evaluator {
     return false;
   }
 
-  // satisfied? throws EvalError (the policy is then skipped and reported)
+  // satisfied? On an error: false with `failed` set and the message in emsg (the policy is then
+  // skipped and reported); the caller clears `failed` before the next policy.
   bool eval_policy(const Policy& p) {
     if (!scope_match(p.p, it.principal)) return false;
     if (!scope_match(p.a, it.action)) return false;
     if (!scope_match(p.r, it.resource)) return false;
     for (auto& c : p.conds) {
-      bool v = as_bool(ev(*c.second));
+      const Val x = ev(*c.second);
+      if (failed) return false;
+      const bool v = as_bool(x);
+      if (failed) return false;
       if (c.first && !v) return false;
       if (!c.first && v) return false;
     }
@@ -1389,11 +1479,10 @@ void is_authorized(const Tier& t, Evaluator& ev, Result& r) {
   r.errors.clear();
   for (uint32_t k = 0; k < t.pols.size(); k++) {
     const Policy& p = t.pols[k];
-    bool sat;
-    try {
-      sat = ev.eval_policy(p);
-    } catch (EvalError& e) {
-      r.errors.emplace_back(k, "while evaluating policy `" + p.id + "`: " + e.msg);
+    ev.failed = false;
+    const bool sat = ev.eval_policy(p);
+    if (ev.failed) {
+      r.errors.emplace_back(k, "while evaluating policy `" + p.id + "`: " + ev.emsg);
       continue;
     }
     if (!sat) continue;
@@ -1405,7 +1494,7 @@ void is_authorized(const Tier& t, Evaluator& ev, Result& r) {
 }
 
 void tiered(const std::vector<Tier>& tiers, const Item& it, Arena& A, Result& r, const Item* statics) {
-  Evaluator ev{it, A, statics};
+  Evaluator ev{it, A, statics, false, {}};
   r = Result();
   for (uint32_t t = 0; t < tiers.size(); t++) {
     A.clear();
