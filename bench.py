@@ -338,12 +338,13 @@ def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=180.0, ent
     return out
 
 
-def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96)):
+def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96, 192, 256, 384, 512)):
     """End-to-end webhook path through the serving queue: `threads` native caller threads each
     issue blocking cg_queue_authorize_sar calls (SAR JSON in, Decision + reason out), which the
     queue batches onto the GPU. Host JSON parsing, SAR conversion and encoding are inside. Then the
-    same at fewer callers (`sweep`): the highest rate whose p99 stays under 1 ms is
-    `best_under_1ms` (the north star's latency bound)."""
+    same at fewer and at more callers (`sweep`, up to 4x the box's 128 default): the highest rate
+    whose p99 stays under 1 ms is `best_under_1ms` (the north star's latency bound), and
+    `knee_threads` the first caller count whose p99 crosses 1 ms."""
     import cedargpu
     enc = [json.dumps(s, separators=(",", ":")) for s in sars]
     q = cedargpu.Queue(ctx, max_batch=max_batch, max_delay_us=0)
@@ -361,9 +362,12 @@ def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96)):
                 "max_batch": st["max_batch"], "device_busy_frac": st["device_ns"] / 1e9 / r["seconds"]}
 
     out = point(threads, total)
-    curve = [point(nt, max(16384, total // 4)) for nt in sweep if nt < threads]
-    ok = [p for p in curve + [out] if p["p99_us"] < 1000.0]
-    out["curve"] = [{k: p[k] for k in ("threads", "decisions_per_s", "p50_us", "p99_us", "max_us", "mean_batch")} for p in curve]
+    curve = [point(nt, max(16384, total // 4)) for nt in sweep if nt != threads]
+    allp = sorted(curve + [out], key=lambda p: p["threads"])
+    ok = [p for p in allp if p["p99_us"] < 1000.0]
+    out["curve"] = [{k: p[k] for k in ("threads", "decisions_per_s", "p50_us", "p99_us", "max_us", "mean_batch")} for p in allp]
+    out["knee_threads"] = next((p["threads"] for p in allp if p["p99_us"] >= 1000.0), None)
+    out["max_threads_tested"] = allp[-1]["threads"]
     out["best_under_1ms"] = max(ok, key=lambda p: p["decisions_per_s"])["decisions_per_s"] if ok else None
     out["best_under_1ms_threads"] = max(ok, key=lambda p: p["decisions_per_s"])["threads"] if ok else None
     out["what"] = ("cg_queue_authorize_sar per request from native threads (JSON parse, SAR conversion, columnar encode, "
@@ -512,25 +516,39 @@ def main():
     # copy and the result binding. Outside the timed region (PCIe-inclusive; not `value`).
     s2r = None
     if rank == 0 and args.submit_to_results:
+        # Twice: the first pass takes this batch size's pool blocks (the timed batch `b` still holds
+        # its own), so the second, timed one runs on a warm pool with no allocation inside.
         payload2 = synth.sars_json(sars).encode()
-        b2 = ctx.batch()
-        t0e = time.perf_counter()
-        b2.add_sar_json(payload2)
-        t1e = time.perf_counter()
+        for rep in range(2):
+            b2 = ctx.batch()
+            t0e = time.perf_counter()
+            b2.add_sar_json(payload2)
+            t1e = time.perf_counter()
+            try:
+                b2.set_profile(True)
+            except AttributeError:  # an A/B build without cg_batch_set_profile
+                pass
+            b2.submit()
+            b2.wait()
+            t2e = time.perf_counter()
+            if rep == 0:
+                b2.close()
         del payload2
-        b2.submit()
-        b2.wait()
-        t2e = time.perf_counter()
         try:
             io2 = b2.io()
         except AttributeError:
             io2 = {"h2d_bytes": 0, "d2h_bytes": 0}
+        try:
+            split = b2.profile()
+        except Exception:
+            split = None
         s2r = {"requests": len(b2), "encode_s": t1e - t0e, "encode_per_s": len(b2) / (t1e - t0e),
                "submit_to_results_ms": (t2e - t1e) * 1e3, "decisions_per_s": len(b2) / (t2e - t1e),
-               "h2d_bytes": io2["h2d_bytes"], "d2h_bytes": io2["d2h_bytes"],
+               "h2d_bytes": io2["h2d_bytes"], "d2h_bytes": io2["d2h_bytes"], "split_ms": split,
                "what": "cg_batch_add_sar_json over the 1M SAR bodies (host threads), then cg_batch_submit -> "
-                       "cg_batch_wait: H2D of the request heap / rows / strings, the complete device step, "
-                       "D2H of the results"}
+                       "cg_batch_wait on a warm buffer pool (the second of two such batches): H2D of the request "
+                       "heap / rows / strings, the complete device step, D2H of the results; split_ms from "
+                       "cg_batch_profile (host phases, and HIP events around the copies and the step)"}
         b2.close()
 
     # submit -> results-visible latency on small batches (includes H2D, launch, D2H)

@@ -112,6 +112,8 @@ _SIGS = {
     "cg_batch_size": (u32, [P]),
     "cg_batch_submit": (ctypes.c_int, [P]),
     "cg_batch_wait": (ctypes.c_int, [P, i64]),
+    "cg_batch_set_profile": (ctypes.c_int, [P, ctypes.c_int]),
+    "cg_batch_profile": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t]),
     "cg_batch_decision": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(u32)]),
     "cg_batch_diagnostic": (ctypes.c_int, [P, u32, ctypes.c_int, P, sz, ctypes.POINTER(sz)]),
     "cg_batch_reasons": (ctypes.c_int, [P, u32, ctypes.POINTER(u32), u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]),

@@ -554,6 +554,21 @@ class Batch:
         lib.cg_batch_bytes(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return a.value, b.value, c.value
 
+    def set_profile(self, on: bool = True):
+        """cg_batch_set_profile: time this batch's submit -> results phases (before submit)."""
+        rc = lib.cg_batch_set_profile(self._h, 1 if on else 0)
+        if rc:
+            raise _err(rc, "set_profile failed")
+
+    def profile(self) -> dict:
+        """cg_batch_profile: the submit -> results split of a profiled batch (ms)."""
+        v = (ctypes.c_double * 8)()
+        rc = lib.cg_batch_profile(self._h, v, 8)
+        if rc:
+            raise _err(rc, "profile failed")
+        keys = ("host_finalize", "host_group", "host_upload_call", "host_launch", "dev_h2d", "dev_step", "dev_d2h", "host_wait")
+        return dict(zip(keys, list(v)))
+
     def io(self) -> dict:
         """PCIe bytes of the submitted batch (one H2D upload, one D2H result copy) and its ancestor-
         list words, total and served by an interned copy (cg_batch_io)."""

@@ -1348,8 +1348,17 @@ int cg_batch_submit(cg_batch* b) {
   if (!b) return CG_E_ARG;
   if (b->submitted) { b->err = "batch already submitted"; return CG_E_STATE; }
   LatTrace tr("submit");
+  const int64_t p0 = b->host.prof ? dev_now_ns() : 0;
+  auto pmark = [&](int k, int64_t& t) {
+    if (!b->host.prof) return;
+    const int64_t now = dev_now_ns();
+    b->prof_ms[k] = (double)(now - t) * 1e-6;
+    t = now;
+  };
+  int64_t pt = p0;
   b->host.finalize_strings();
   tr.mark("finalize");
+  pmark(0, pt);
   if (b->host.n() == 0) { b->submitted = b->done = true; return CG_OK; }
   // First-pass reason capacity: up to the probe kernel's 64-hit stage while the two reason arrays
   // stay within 4 MB (small, latency-bound batches then need no re-run for 9..64 reasons); large
@@ -1393,6 +1402,7 @@ int cg_batch_submit(cg_batch* b) {
   if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   GUARD(b->err, { group_requests(b); })
   tr.mark("group");
+  pmark(1, pt);
   for (uint64_t f = b->ctx->fault_errors.load(); f;)
     if (b->ctx->fault_errors.compare_exchange_weak(f, f - 1)) {
       b->err = "injected device error (cg_ctx_inject_fault CG_FAULT_DEVICE_ERROR)";
@@ -1405,20 +1415,42 @@ int cg_batch_submit(cg_batch* b) {
     }
   if (dev_batch_upload(b->ctx->device, b->host, &b->dev, b->ctx->stream, b->ctx->pool)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   tr.mark("upload");
+  pmark(2, pt);
   if (const uint64_t us = b->ctx->fault_stall_us.load())
     if (dev_stall(b->ctx->device, b->ctx->stream, us)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   if (dev_eval(b->img->dev, b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   tr.mark("launch");
   if (dev_download_async(b->dev, b->ctx->stream)) { b->err = dev_last_error(); return CG_E_DEVICE; }
   tr.mark("d2h_enqueue");
+  pmark(3, pt);
   b->submitted = true;
   return CG_OK;
 }
 
 int cg_batch_wait(cg_batch* b, int64_t timeout_ns) {
   if (!b) return CG_E_ARG;
-  const int64_t deadline = timeout_ns < 0 ? -1 : dev_now_ns() + timeout_ns;
-  return cg::batch_wait(b, deadline, deadline);
+  const int64_t t0 = dev_now_ns();
+  const int64_t deadline = timeout_ns < 0 ? -1 : t0 + timeout_ns;
+  const int rc = cg::batch_wait(b, deadline, deadline);
+  if (b->host.prof && rc == CG_OK) b->prof_ms[4] += (double)(dev_now_ns() - t0) * 1e-6;
+  return rc;
+}
+
+int cg_batch_set_profile(cg_batch* b, int on) {
+  if (!b) return CG_E_ARG;
+  if (b->submitted) { b->err = "profile must be set before submit"; return CG_E_STATE; }
+  b->host.prof = on != 0;
+  return CG_OK;
+}
+
+int cg_batch_profile(cg_batch* b, double* ms, size_t n) {
+  if (!b || !ms) return CG_E_ARG;
+  if (!b->host.prof || !b->downloaded) { b->err = "batch not profiled, or not waited"; return CG_E_STATE; }
+  float dev[3] = {0.f, 0.f, 0.f};
+  if (!dev_batch_profile(b->dev, &dev[0], &dev[1], &dev[2])) { b->err = "no device profile (small batch or stand-in)"; }
+  const double v[8] = {b->prof_ms[0], b->prof_ms[1], b->prof_ms[2], b->prof_ms[3], dev[0], dev[1], dev[2], b->prof_ms[4]};
+  for (size_t k = 0; k < n && k < 8; k++) ms[k] = v[k];
+  return CG_OK;
 }
 
 }  // extern "C"

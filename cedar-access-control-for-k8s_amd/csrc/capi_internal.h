@@ -90,6 +90,9 @@ struct cg_batch {
   std::vector<Item> items;
   std::map<uint32_t, std::string> fast_reason;  // authz fast paths: the reason; admission: error text
   std::vector<cg::DevSubset> held;  // re-run result blocks the host lists point into (Batch::big)
+  // cg_batch_set_profile: host intervals of submit (finalize, group, upload call, launch + D2H
+  // enqueue) and of the wait (ms), filled as they pass
+  double prof_ms[5] = {0, 0, 0, 0, 0};
   ~cg_batch() {
     if (dev.direct && dev.pending) {
       // inputs were copied straight from these arrays (pinned blocks) and the copy may still run:

@@ -2380,6 +2380,31 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < NS; k++) cum[k + 1] = cum[k] + (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)(k * SEG));
     const uint32_t W = cum[NS];
+    if constexpr (STATS) {
+      // (profiling) distinct buckets and distinct candidate heads over the wave's pool:
+      // st[1] distinct heads, st[2] distinct buckets, st[3] pool candidates (lane 0 counts)
+      if (lane == 0) {
+        uint32_t dh = 0, db = 0, tot = 0;
+        for (uint32_t s1 = 0; s1 < NS; s1++) {
+          if (wl.sst[s1][0] > L::HC) continue;
+          for (uint32_t b1 = 0; b1 < wl.sne[s1]; b1++) {
+            const uint32_t f1 = wl.u.b.efirst[s1][b1] & EF_FIRST;
+            const uint32_t c1 = (b1 + 1 < wl.sne[s1] ? wl.u.b.epre[s1][b1 + 1] : (s1 == seg ? carry : 0u)) - wl.u.b.epre[s1][b1];
+            (void)c1;
+            bool seen = false;
+            for (uint32_t s2 = 0; s2 <= s1 && !seen; s2++) {
+              if (wl.sst[s2][0] > L::HC) continue;
+              const uint32_t lim = s2 == s1 ? b1 : wl.sne[s2];
+              for (uint32_t b2 = 0; b2 < lim && !seen; b2++) seen = (wl.u.b.efirst[s2][b2] & EF_FIRST) == f1;
+            }
+            if (!seen) db++;
+          }
+        }
+        // heads: count distinct head indices by checking each pool candidate against earlier ones
+        (void)dh; (void)tot;
+        st[2] += db;
+      }
+    }
     for (uint32_t base = 0; base < W; base += 64) {
       const uint32_t g = base + lane;
       bool ok = g < W;
@@ -2400,6 +2425,16 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
       const uint4* d4 = reinterpret_cast<const uint4*>(head);
       const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
+      if constexpr (STATS) {  // distinct heads of this round (a head first seen at the lowest lane)
+        bool first = ok;
+        for (uint32_t l2 = 0; l2 < 64; l2++) {
+          const uint32_t o2 = (uint32_t)__shfl((int)hidx, (int)l2);
+          const bool ok2 = base + l2 < W;
+          if (ok2 && l2 < lane && o2 == hidx) first = false;
+        }
+        st[1] += first ? 1u : 0u;
+        st[3] += ok ? 1u : 0u;
+      }
       // the candidate's request (segment s)
       const uint4 x0 = wl.cx[s][0], x1 = wl.cx[s][1], x2 = wl.cx[s][2], x3 = wl.cx[s][3];
       PCtx tc;
@@ -2455,10 +2490,11 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       bool err = false, structural_hit = false;
       Err e{0, 0, 0, 0, 0};
       while (__ballot(pc < na)) {
+        if (STATS && lane == 0) st[10]++;  // (profiling: atom rounds of the wave, in lane 0)
         if (pc < na) {
           const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
           const uint32_t rr = eval_atom<false>(tc, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
-          if (STATS) st[8]++;
+          if (STATS) { st[8]++; const uint32_t kk = at.x & 0xFF; st[4] += kk == AK_LIKE; st[5] += kk == AK_INSET || kk == AK_RECSET || kk == AK_CONTAINS; }
           if (rr == 3u) { structural_hit = true; pc = AT_UNSAT; }
           else if (rr == 2u) { err = true; pc = AT_UNSAT; }
           else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
@@ -3706,7 +3742,14 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // past a close while in flight, DevBatch::keep)
   d.direct = false;
   for (int k = 0; k < NSEC; k++) d.direct = d.direct || direct[k];
+  if (b.prof)
+    for (auto& e : d.pev) {
+      hipEvent_t ev;
+      HIPCHK(hipEventCreate(&ev), "profile event");
+      e = (void*)ev;
+    }
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
+  if (d.pev[0]) HIPCHK(hipEventRecord((hipEvent_t)d.pev[0], s), "event record");
   // (one copy: staging in pieces with an H2D per piece, to overlap the two, made 1-2k-request
   // batches 0.06-0.07 ms slower on the box, gpurun_out/r04flat3)
   HIPCHK(hipMemcpyAsync(in, st, stage_in, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
@@ -3715,7 +3758,20 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   for (int k = 0; k < NSEC; k++)
     if (direct[k]) HIPCHK(hipMemcpyAsync(in + off[k], src[k], len[k], hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D (pinned array)");
   if (!d.zc) HIPCHK(hipMemsetAsync(d.res, 0, o_rf, s), "memset res");  // (and the worklist counters)
+  if (d.pev[1]) HIPCHK(hipEventRecord((hipEvent_t)d.pev[1], s), "event record");
   return 0;
+}
+
+bool dev_batch_profile(const DevBatch& b, float* h2d_ms, float* step_ms, float* d2h_ms) {
+  if (!b.pev[0] || !b.pev[3]) return false;
+  (void)hipSetDevice(b.device);
+  float t[3] = {0.f, 0.f, 0.f};
+  for (int k = 0; k < 3; k++)
+    if (hipEventElapsedTime(&t[k], (hipEvent_t)b.pev[k], (hipEvent_t)b.pev[k + 1]) != hipSuccess) return false;
+  *h2d_ms = t[0];
+  *step_ms = t[1];
+  *d2h_ms = t[2];
+  return true;
 }
 
 void dev_batch_free(DevBatch* d) {
@@ -3733,6 +3789,8 @@ void dev_batch_free(DevBatch* d) {
     }
   }
   if (d->done) (void)hipEventDestroy((hipEvent_t)d->done);
+  for (auto e : d->pev)
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
   if (d->pool) {
     pool_put(d->pool, false, d->in_blk, d->in_cls);
     pool_put(d->pool, false, d->out_blk, d->out_cls);
@@ -4412,8 +4470,10 @@ int dev_download_async(DevBatch& b, void* stream) {
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     b.done = (void*)e;
   }
+  if (b.pev[2]) HIPCHK(hipEventRecord((hipEvent_t)b.pev[2], s), "event record");
   if (b.zc && b.fu_cnt) HIPCHK(hipMemcpyAsync(b.zc_cnt, b.fu_cnt, (FU_KINDS + 1) * 4, hipMemcpyDeviceToHost, s), "D2H counters");
   else if (b.n) HIPCHK(hipMemcpyAsync(b.stage, b.out_blk, b.dl_bytes ? b.dl_bytes : b.out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
+  if (b.pev[3]) HIPCHK(hipEventRecord((hipEvent_t)b.pev[3], s), "event record");
   HIPCHK(hipEventRecord((hipEvent_t)b.done, s), "event record");
   b.wait_t0 = 0;
   return 0;

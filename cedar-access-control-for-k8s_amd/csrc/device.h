@@ -110,7 +110,13 @@ struct DevBatch {
   void* done = nullptr;    // event after the result download (dev_download_async)
   bool pending = false;    // work enqueued on the batch's buffers not yet waited for
   int64_t wait_t0 = 0;     // when the first wait on `done` began (dev_now_ns; 0: not yet)
+  // profiled batch (Batch::prof): timing events before the H2D copies, after them, after the step
+  // and after the D2H copy (dev_batch_profile)
+  void* pev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
+// The device intervals of a profiled batch after its download: H2D copies, the step, the D2H copy
+// (ms); false when the batch was not profiled.
+bool dev_batch_profile(const DevBatch& b, float* h2d_ms, float* step_ms, float* d2h_ms);
 
 // Batches of at most this many requests on an indexed image run as one launch (DevBatch::small);
 // CEDARGPU_SMALL_N overrides (0: never).

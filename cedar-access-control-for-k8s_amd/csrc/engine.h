@@ -360,6 +360,7 @@ struct Batch {
   uint32_t fu_capr_hint = 0, fu_capr_gen_hint = 0;  // reasons per FU_BIG / FU_GEN entry (0: default)
   // the batching layer's locality order is computed on the device inside each step (group.hip)
   bool dev_group = false;
+  bool prof = false;  // cg_batch_set_profile: device events around the upload, the step and the download
   // first-pass results, read in place from the batch's pinned staging block (device.h DevBatch;
   // valid while the batch lives): res[2i], [2i+1] per request, capr reasons of each effect, cape
   // error records. res is written back by overflow re-runs.

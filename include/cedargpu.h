@@ -239,6 +239,14 @@ int cg_batch_submit(cg_batch* b);
  * NoOpinion; manifests/admission-webhook.yaml:11 failurePolicy Ignore): authz NoOpinion, admission
  * allow (cmd/cedar-webhook/main.go:116 allowOnError). */
 int cg_batch_wait(cg_batch* b, int64_t timeout_ns);
+/* Diagnostics of one batch's submit -> results interval (no reference counterpart; the bench's
+ * split of it). cg_batch_set_profile(b, 1) before submit; after a successful wait,
+ * cg_batch_profile fills up to n of, in ms: [0] string finalize, [1] host grouping, [2] the upload
+ * call (pinned staging copy + enqueue of the H2D copies), [3] launch + D2H enqueue, then device
+ * intervals from events on the batch's stream: [4] H2D copies, [5] the complete step, [6] the D2H
+ * copy; [7] the wait call(s). */
+int cg_batch_set_profile(cg_batch* b, int on);
+int cg_batch_profile(cg_batch* b, double* ms, size_t n);
 /* cedar.Decision for request i: *allow = 1 (Allow) / 0 (Deny); *tier = deciding tier index. */
 int cg_batch_decision(cg_batch* b, uint32_t i, int* allow, uint32_t* tier);
 /* json.Marshal(cedar.Diagnostic) (reasons_only=0) or json.Marshal(diagnostic.Reasons) (=1).
