@@ -110,6 +110,9 @@ struct KArgs {
   uint32_t* ovf_cnt;
   uint32_t *ovf_ids, *ovf_res, *ovf_rf, *ovf_er;
   uint32_t ovf_cap, ovf_capr, ovf_cape;
+  // inline like atoms (image.h AK_LIKEI): like slots, their words' row offset, and the hot-row index
+  // the probe kernel stages them at (0xFFFFFFFF: not staged; the atom reads the string's bytes)
+  uint32_t lslot, like_off, like_base;
 };
 // SCAN_CAP: bucket pairs a request's list holds (more: SCAN_OVF, the large stage probes the index
 // itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
@@ -154,6 +157,8 @@ struct Ctx {
   uint32_t rb0, rb1, rb2, rb3;            // resource ancestor-or-self Bloom
   const uint32_t* rowx;                   // the row's element-hash list offsets per hot slot, or null
   __device__ uint32_t hlist(uint32_t h) const { return rowx ? rowx[h] : 0xFFFFFFFFu; }
+  static constexpr uint32_t lkb = 0xFFFFFFFFu;  // like words not staged (AK_LIKEI reads the bytes)
+  static constexpr uint32_t lslot = 0u;
 };
 
 // Makes a value opaque to the optimizer. Used on context fields that feed a select: otherwise
@@ -582,6 +587,39 @@ __device__ __forceinline__ void hot_err(const CT& c, uint32_t h, uint2 v, Err& e
   e.ei = d[3];
 }
 
+// AK_LIKEI: string sid (the value of hot slot h) like the inline pattern (p0, p1: prefix then suffix
+// bytes; f: prefix length | suffix length << 4 | star << 8). The string's length and first / last 8
+// bytes come from the staged like words (c.lkb), else from the string itself.
+template <class CT>
+__device__ __forceinline__ bool likei(const CT& c, uint32_t h, uint32_t sid, uint32_t p0, uint32_t p1, uint32_t f) {
+  uint32_t len;
+  uint64_t pre = 0, suf = 0;
+  if (c.lkb != 0xFFFFFFFFu) {
+    const uint32_t k = c.lkb + 3u * (uint32_t)__popc(c.lslot & ((1u << h) - 1u));
+    const uint2 x = hot_get(c, k), y = hot_get(c, k + 1), z = hot_get(c, k + 2);
+    len = x.x;
+    pre = ((uint64_t)y.x << 32) | x.y;
+    suf = ((uint64_t)z.x << 32) | y.y;
+  } else {
+    const uint8_t* s;
+    str_span(c, sid, s, len);
+    const uint32_t n = min(len, 8u);
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++)
+      if (j < n) {
+        pre |= (uint64_t)s[j] << (8 * j);
+        suf |= (uint64_t)s[len - 1 - j] << (8 * (7 - j));
+      }
+  }
+  const uint32_t pl = f & 15u, sl = (f >> 4) & 15u;
+  const uint64_t pat = ((uint64_t)p1 << 32) | p0;
+  auto msk = [](uint32_t n) { return n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull); };
+  if (!(f & 256u)) return len == pl && ((pre ^ pat) & msk(pl)) == 0;
+  if (len < pl + sl || ((pre ^ pat) & msk(pl)) != 0) return false;
+  if (!sl) return true;
+  return (suf >> (64 - 8 * sl)) == ((pat >> (8 * pl)) & msk(sl));  // (sl >= 1: pl <= 7)
+}
+
 // ---- atoms ---------------------------------------------------------------------------------
 // rec = this policy's LDS record (atom data lives there). Returns 0 false, 1 true, 2 error.
 // AK_RECSET helpers: compare a request value with one template operand (const or hot hole).
@@ -702,6 +740,11 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
     case AK_LIKE:
       if (tag_of(v) != T_STR) { type_err(e, TN_STRING, v); return 2u; }
       return like_match(c, v.w1, rec + w1) ? 1u : 0u;
+    case AK_LIKEI:
+      if (tag_of(v) != T_STR) { type_err(e, TN_STRING, v); return 2u; }
+      return likei(c, h, v.w1, w1, w2, w3) ? 1u : 0u;
+    case AK_INSTR:
+      return (tag_of(v) == T_STR && (v.w1 == w1 || v.w1 == w2 || v.w1 == w3)) ? 1u : 0u;
     case AK_RECSET: {
       const uint32_t* d = rec + w1;
       const uint32_t nh = d[0];
@@ -1555,6 +1598,7 @@ struct PCtx {
   const uint32_t* rowb;
   uint32_t rowo;  // 0xFFFFFFFF: none
   __device__ uint32_t hlist(uint32_t h) const { return rowo != 0xFFFFFFFFu ? rowb[rowo + h] : 0xFFFFFFFFu; }
+  uint32_t lkb, lslot;  // like words staged at hot index lkb (0xFFFFFFFF: not), like slots (KArgs)
 };
 
 // X in (qt, qi) for X with UID (st, si) and ancestor pairs at blk[off + 2k]
@@ -2138,6 +2182,13 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     wl.hot[seg][h] = valid ? make_uint2(__builtin_nontemporal_load(row + RW_HDR + 2 * h),
                                         __builtin_nontemporal_load(row + RW_HDR + 2 * h + 1))
                            : make_uint2(0u, 0u);
+  c.lkb = a.like_base;
+  c.lslot = a.lslot;
+  if (a.like_base != 0xFFFFFFFFu)  // the like words, as hot entries behind the hot values
+    for (uint32_t j = sl; j < 3u * (uint32_t)__popc(a.lslot); j += SEG)
+      wl.hot[seg][a.like_base + j] = valid ? make_uint2(__builtin_nontemporal_load(row + a.like_off + 2 * j),
+                                                        __builtin_nontemporal_load(row + a.like_off + 2 * j + 1))
+                                           : make_uint2(0u, 0u);
   // action masks over the image action table (`==` and `in`), resolved by the encoder
   uint64_t am = 0, as = 0;
   uint32_t aself = 0xFFFFu;
@@ -2248,7 +2299,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         ok = ok && anc_in(c.blk, c.r_anc, c.r_nanc, c.rt, c.ri, q2.x, q2.y);
       // conditions: this lane's atom graph (first HEAD_ATOMS atoms in the head, the rest and all
       // atom data in the policy's full record at PW_EXT)
-      const uint32_t na = q3.x / ATOM_WORDS;
+      const uint32_t na = (q3.x & 0xFFFFu) / ATOM_WORDS;
       const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
       uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
       if (STATS) { st[6] += idx < total; st[7] += ok; st[11] += sl == 0; }
@@ -2268,7 +2319,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       // for every member, all sharing the head's error detail
       const bool hit = ok && (err || pc == AT_SAT);
       const uint32_t mlist = q2.w;
-      const uint32_t nmem = hit ? (mlist ? a.bstream[mlist] : 1u) : 0u;
+      const uint32_t nmem = hit ? (mlist ? ((q3.x >> 16) != 0xFFFFu ? (q3.x >> 16) : a.bstream[mlist]) : 1u) : 0u;  // (head word 12: the class size)
       if (STATS) st[9] += nmem;
       const uint32_t mincl = sscan(nmem);
       const uint64_t xmask = sballot(hit && err);
@@ -2452,6 +2503,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       tc.r_anc = x2.x; tc.a_anc = x2.y; tc.p_nanc = x2.z & 0xFFFFu; tc.r_nanc = x2.z >> 16; tc.a_nanc = x2.w & 0xFFFFu;
       tc.rowb = c.rowb;
       tc.rowo = x3.x;
+      tc.lkb = a.like_base;
+      tc.lslot = a.lslot;
       const uint64_t tam = ((uint64_t)x3.z << 32) | x3.y;
       const uint32_t tself = x2.w >> 16;
       const uint64_t tas = tself < 64u ? (1ull << tself) : 0ull;
@@ -2483,7 +2536,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       if (rk == SK_EQ) ok = ok && tc.rt == q2.x && tc.ri == q2.y;
       else if ((rk == SK_IN || rk == SK_ISIN) && (bcombo >> 3) != KC_ENT)
         ok = ok && anc_in(tc.blk, tc.r_anc, tc.r_nanc, tc.rt, tc.ri, q2.x, q2.y);
-      const uint32_t na = q3.x / ATOM_WORDS;
+      const uint32_t na = (q3.x & 0xFFFFu) / ATOM_WORDS;
       const uint32_t* rec = a.bstream + q3.y;  // PW_EXT (word 13)
       uint32_t pc = ok ? (na ? 0u : AT_SAT) : AT_UNSAT;
       if (STATS) { st[6] += g < W; st[7] += ok; st[11] += lane < NS; }
@@ -2502,7 +2555,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       }
       const bool hit = ok && (err || pc == AT_SAT);
       const uint32_t mlist = q2.w;
-      const uint32_t nmem = hit ? (mlist ? a.bstream[mlist] : 1u) : 0u;
+      const uint32_t nmem = hit ? (mlist ? ((q3.x >> 16) != 0xFFFFu ? (q3.x >> 16) : a.bstream[mlist]) : 1u) : 0u;  // (head word 12: the class size)
       if (STATS) st[9] += nmem;
       const uint32_t pos0 = hit ? atomicAdd(&wl.sst[s][0], nmem) : 0u;
       const uint32_t xpos = (hit && err) ? atomicAdd(&wl.sst[s][1], 1u) : 0u;
@@ -3047,6 +3100,8 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.n_static = img.n_static();
   d.lane_need = img.lane_need;
   d.cslot_mask = img.list_mask();
+  d.lslot_mask = img.lslot_mask;
+  d.like_off = img.like_off();
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
   d.bmask = img.btab_slots - 1;
   d.fmask = (uint32_t)(img.dev_len[DS_BFILT] / 8) - 1;
@@ -3937,6 +3992,12 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
   k.lane = b.lane; k.lane_stride = img.lane_need;
   k.hlists = img.cslot_mask ? 1u : 0u;
+  // like words staged behind the hot values while both fit the probe kernel's hot rows (32 entries;
+  // CEDARGPU_LIKE_STAGE=0: never, A/B): else AK_LIKEI reads the string's bytes
+  static const bool like_stage = !(std::getenv("CEDARGPU_LIKE_STAGE") && *std::getenv("CEDARGPU_LIKE_STAGE") == '0');
+  k.lslot = img.lslot_mask;
+  k.like_off = img.like_off;
+  k.like_base = (like_stage && img.lslot_mask && img.n_hot + 3u * (uint32_t)__builtin_popcount(img.lslot_mask) <= NHOT) ? img.n_hot : 0xFFFFFFFFu;
   // off by default: the scope table is sized for ~1.06-slot chains, where a miss costs one slot load
   // and the filter only adds a round trip in front of every hit (profiles/r02/ab_slack)
   static const uint32_t l1filt = [] { const char* e = std::getenv("CEDARGPU_L1_FILTER"); return (e && *e == '1') ? 1u : 0u; }();

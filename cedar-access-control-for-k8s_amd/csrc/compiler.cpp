@@ -452,11 +452,35 @@ struct Compiler {
       case EK::Attr:
         if ((h = hot_of(*e)) < 0) return false;
         return put(AK_BOOL, (uint32_t)h);
-      case EK::Like:
+      case EK::Like: {
         if ((h = hot_of(*e->kids[0])) < 0 || e->kids[0]->k != EK::Attr) return false;
+        // one star at most and literals within 8 bytes: inline (AK_LIKEI), nothing to read but the
+        // row's like words (CEDARGPU_NO_LIKEI: the record form everywhere, A/B)
+        static const bool no_likei = std::getenv("CEDARGPU_NO_LIKEI") != nullptr;
+        std::string pre, suf;
+        bool star = false, inl = !no_likei;
+        for (auto& pc : e->pat) {
+          if (pc.star) {
+            if (star && !suf.empty()) inl = false;  // a middle literal
+            star = true;
+          } else {
+            (star ? suf : pre) += pc.lit;
+          }
+        }
+        if (inl && pre.size() + suf.size() <= LIKEI_MAX) {
+          uint64_t b = 0;
+          const std::string lit = pre + suf;
+          for (size_t j = 0; j < lit.size(); j++) b |= (uint64_t)(uint8_t)lit[j] << (8 * j);
+          w[1] = (uint32_t)b;
+          w[2] = (uint32_t)(b >> 32);
+          w[3] = (uint32_t)pre.size() | ((uint32_t)suf.size() << 4) | (star ? 1u << 8 : 0u);
+          I.lslot_mask |= 1u << h;
+          return put(AK_LIKEI, (uint32_t)h);
+        }
         w[1] = pattern_into(e->pat, adata);
         *patch = true;
         return put(AK_LIKE, (uint32_t)h);
+      }
       case EK::Lit:
         if (e->lit.k != VK::Bool) return false;
         *neg = !e->lit.b;
@@ -473,6 +497,12 @@ struct Compiler {
         if (recv.k == EK::Set && fold(recv, s)) {
           if (arg.k != EK::Attr || (h = hot_of(arg)) < 0) return false;
           for (auto& x : s.elems) if (!is_prim(x)) return false;
+          bool strs = !s.elems.empty() && s.elems.size() <= 3;
+          for (auto& x : s.elems) strs = strs && x.k == VK::Str;
+          if (strs) {  // 1 to 3 strings: inline (AK_INSTR), repeats fill the unused words
+            for (uint32_t j = 0; j < 3; j++) w[1 + j] = intern(s.elems[std::min<size_t>(j, s.elems.size() - 1)].s);
+            return put(AK_INSTR, (uint32_t)h);
+          }
           uint32_t off = (uint32_t)adata.size();
           for (auto& x : s.elems) { uint32_t r[3]; reg_form(x, r); adata.insert(adata.end(), r, r + 3); }
           w[1] = off;
@@ -791,12 +821,18 @@ struct Compiler {
       }
       // hot(h) like "lit*..." on the spine: a prefix key on the pattern's opening literal (a
       // pattern without a star is its whole literal, which is also a prefix of every match)
-      if (kind == AK_LIKE && f == AT_UNSAT && t != AT_UNSAT) {
-        const uint32_t* pw = &at[a[1] - POL_WORDS];  // [flags, prefix len, prefix bytes ...]
-        const uint32_t len = std::min(pw[1], PFX_MAX);
-        if (len > 0) {
-          uint8_t bytes[PFX_MAX];
+      if ((kind == AK_LIKE || kind == AK_LIKEI) && f == AT_UNSAT && t != AT_UNSAT) {
+        uint32_t len = 0;
+        uint8_t bytes[PFX_MAX];
+        if (kind == AK_LIKE) {
+          const uint32_t* pw = &at[a[1] - POL_WORDS];  // [flags, prefix len, prefix bytes ...]
+          len = std::min(pw[1], PFX_MAX);
           for (uint32_t j = 0; j < len; j++) bytes[j] = (uint8_t)(pw[2 + (j >> 2)] >> (8 * (j & 3)));
+        } else {  // inline: the prefix is the first (w3 & 15) bytes of w1, w2
+          len = a[3] & 15u;
+          for (uint32_t j = 0; j < len; j++) bytes[j] = (uint8_t)(a[1 + (j >> 2)] >> (8 * (j & 3)));
+        }
+        if (len > 0) {
           k.ok = true;
           k.contains = true;
           k.plen = len;
@@ -1466,6 +1502,9 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       std::copy(src, src + std::min<uint32_t>(rec_len[p], HEAD_WORDS), hd);
       hd[PW_EXT] = ext[p];
       hd[PW_CODE_N] = mlist[p];  // heads: the duplicate class's member list (0: the policy alone)
+      // heads: the class size in PW_SLOTS' upper half (0xFFFF: read it from the list), so a hit
+      // needs no load before its members'
+      hd[PW_SLOTS] = (hd[PW_SLOTS] & 0xFFFFu) | (std::min<uint32_t>(mcnt[p], 0xFFFFu) << 16);
       head++;
     }
   };
@@ -1830,6 +1869,7 @@ static std::shared_ptr<Image> compile_incremental(LowerState& S, const std::vect
   // lowering; removed documents' slots linger, which only costs their rows a list): the scope index
   // then never files prefix keys on them, as a fresh build would not
   img->cslot_mask = A.cslot_mask;
+  img->lslot_mask = A.lslot_mask;  // (the same: removed documents' like slots linger)
   std::vector<Compiler::AttrKey> akeys;
   size_t total = 0;
   for (auto& tp : parsed) total += tp.size();
@@ -2010,6 +2050,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     A.strings = img->strings; A.sid = img->sid; A.code = img->code; A.cpool = img->cpool;
     A.ext_msgs = img->ext_msgs; A.act = img->act; A.hot = img->hot; A.amask_ok = img->amask_ok;
     A.cslot_mask = img->cslot_mask;
+    A.lslot_mask = img->lslot_mask;
     S.C.hot = C.hot; S.C.hot_depth = C.hot_depth; S.C.act_index = C.act_index;
     S.gen++;
     std::vector<uint32_t> kept(docs.size(), 0);
@@ -2117,7 +2158,7 @@ void Image::write_blob(void* wp) const {
   w.put64(table + 16 * DS_COUNT + 8, w.n);
   w.vec(pol); w.vec(tier_end); w.vec(code);
   w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
-  w.u32(pslot_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words); w.u32(l2_vmask); w.u32(l2_lmask);
+  w.u32(pslot_mask); w.u32(lslot_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words); w.u32(l2_vmask); w.u32(l2_lmask);
   w.u32((uint32_t)key_ents.size());
   w.raw(key_ents.data(), key_ents.size() * 8);
   w.u32((uint32_t)strings.size());
@@ -2220,6 +2261,8 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->lane_need = r.u32();
   img->cslot_mask = r.u32();
   img->pslot_mask = r.u32();
+  img->lslot_mask = r.u32();
+  if (img->n_hot() < 32 && (img->lslot_mask >> img->n_hot())) throw CedarError("corrupt image (like slots)");
   img->pfx = r.vec();
   img->btab_slots = r.u32();
   img->sbits_words = r.u32();

@@ -605,6 +605,24 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       blk.insert(blk.end(), hs.begin(), hs.end());
     }
   }
+  // like words (image.h AK_LIKEI): per like slot the string's length, first and last 8 bytes
+  if (img.lslot_mask) {
+    uint32_t* lw = row + img.like_off();
+    for (uint32_t m = img.lslot_mask; m; m &= m - 1, lw += LIKE_WORDS) {
+      const uint32_t h = (uint32_t)__builtin_ctz(m);
+      const uint32_t w0 = row[RW_HDR + 2 * h], w1 = row[RW_HDR + 2 * h + 1];
+      for (uint32_t j = 0; j < LIKE_WORDS; j++) lw[j] = 0;
+      if ((w0 >> TAG_SHIFT) != T_STR) continue;  // (the atom's type check decides first)
+      const std::string_view sv = w1 < img.n_gstr() ? std::string_view(img.strings[w1]) : std::string_view(E.strs[w1 - img.n_gstr()]);
+      const size_t n = sv.size(), k = std::min<size_t>(n, 8);
+      uint64_t pre = 0, suf = 0;
+      for (size_t j = 0; j < k; j++) pre |= (uint64_t)(uint8_t)sv[j] << (8 * j);
+      for (size_t j = 0; j < k; j++) suf |= (uint64_t)(uint8_t)sv[n - 1 - j] << (8 * (7 - j));
+      lw[0] = n > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)n;
+      lw[1] = (uint32_t)pre; lw[2] = (uint32_t)(pre >> 32);
+      lw[3] = (uint32_t)suf; lw[4] = (uint32_t)(suf >> 32);
+    }
+  }
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
   // grouping key: 8 bits of (action, resource type) | 16 of the principal's type and key ancestors |
   // 8 of its hot values (group.hip sorts on them)

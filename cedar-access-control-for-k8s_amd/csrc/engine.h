@@ -173,7 +173,12 @@ struct Image {
   uint32_t pslot_mask = 0;
   std::vector<uint32_t> pfx;
   uint32_t list_mask() const { return cslot_mask | pslot_mask; }
-  uint32_t row_words() const { return (cgi::RW_HDR + 2 * n_hot() + (list_mask() ? n_hot() : 0u) + 3) & ~3u; }
+  // hot slots an inline `like` atom reads (image.h AK_LIKEI): rows then carry LIKE_WORDS per slot
+  // after the list offsets
+  uint32_t lslot_mask = 0;
+  uint32_t n_like() const { return (uint32_t)__builtin_popcount(lslot_mask); }
+  uint32_t like_off() const { return cgi::RW_HDR + 2 * n_hot() + (list_mask() ? n_hot() : 0u); }
+  uint32_t row_words() const { return (like_off() + cgi::LIKE_WORDS * n_like() + 3) & ~3u; }
   // string -> id over a string_view: open addressing, entries (hash high 32 bits << 32 | id + 1),
   // 0 = empty; size is a power of two. Built by build_lookup once the table is final.
   std::vector<uint64_t> lookup;

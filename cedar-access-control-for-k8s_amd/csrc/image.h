@@ -260,7 +260,18 @@ enum AtomKind : uint32_t {
   AK_TRUE,        // constant true (`true`; `false` is AK_TRUE with t and f swapped)
   AK_INANY,       // var h in [entity literals]: (type, id) pairs @record+w1, n = w2
   AK_EQV,         // var h == entity literal (w1 type, w2 id)
+  // Inline forms (no record data: the atom's words are all it reads, plus the request's row):
+  AK_LIKEI,       // hot h (must be string) like a pattern of at most one star whose literals fit 8 bytes:
+                  // w1, w2 = prefix bytes then suffix bytes (little-endian), w3 = prefix length | suffix
+                  // length << 4 | star << 8. Reads the string's length and its first and last 8 bytes
+                  // from the row's like words (LIKE_WORDS per slot of the image's lslot_mask), staged
+                  // with the hot values; from the string itself where they are not staged
+  AK_INSTR,       // [string constants].contains(hot h): 1 to 3 string ids in w1..w3 (repeats fill)
 };
+// like words of a like slot in the request row (after the list offsets): string length, its first 8
+// bytes (zero-padded), its last 8 bytes (the last byte highest; zero-padded below a short string),
+// and a pad word; staged as 3 uint2 hot entries behind the hot values
+constexpr uint32_t LIKE_WORDS = 6, LIKEI_MAX = 8;
 constexpr uint32_t AT_UNSAT = 0xFE, AT_SAT = 0xFF, MAX_ATOMS = 0xFD;
 // AK_RECSET data, all offsets relative to the policy record:
 //   [n_holes, hole hot index ...]                     holes in source (evaluation) order
@@ -446,7 +457,7 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 13;
+constexpr uint32_t IMG_VERSION = 14;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob

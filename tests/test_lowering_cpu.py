@@ -1,6 +1,8 @@
 """The shapes of tests/lowering_cases.py compile to device images (no CG_E_COMPILE for valid Cedar
 within the documented limits) and the two oracles agree on them; GPU parity is in
 tests/test_gpu_parity.py (test_lowered_shapes_vs_oracle)."""
+import os
+
 import pytest
 
 import cedar_oracle as co
@@ -52,3 +54,16 @@ def test_contains_shapes_index_and_oracles_agree():
     st = cedargpu.image_stats(img)
     assert st["indexed"] and st["policies"] == st["atomic"] == 12, st
     _compare([[("c.cedar", cc.POLICIES)]], cc.items(300))
+
+
+def test_inline_like_and_string_set_atoms_index():
+    """The inline atoms (image.h AK_LIKEI / AK_INSTR) keep a policy atomic and indexed, and an inline
+    `like` with a literal prefix still files a prefix key (tests/test_gpu_inline_atoms.py runs them)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_inline_atoms import _policies
+    img = cedargpu.build_image([cedargpu.MemoryStore("inline.cedar", _policies())], epoch=1)
+    st = cedargpu.image_stats(img)
+    assert st["atomic"] == st["policies"] and st["indexed"], st
+    ix = cedargpu.index_stats(img)
+    assert ix["pslot_mask"], ix  # `like "ab*"` etc.: prefix keys on resource.name
