@@ -43,6 +43,12 @@ using namespace cgi;
 namespace {
 
 constexpr int BLOCK = 256;
+// Diagnostic builds only (never the shipped library): CG_DBG removes one part of the pooled
+// candidate pass to time the rest (results are wrong): 1 no atom evaluation, 2 no hit recording
+// past the count, 3 no merge, 4 every lane loads the same head (tools/gpu_session.sh dbg step).
+#ifndef CG_DBG
+#define CG_DBG 0
+#endif
 
 struct RV {
   uint32_t w0, w1, w2;
@@ -2147,7 +2153,12 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint32_t rw = (valid && sl < RW_HDR) ? __builtin_nontemporal_load(row + sl) : 0u;
   // segments narrower than the header hold its upper words in a second register
   const uint32_t rw_hi = (SEG < RW_HDR && valid && SEG + sl < RW_HDR) ? __builtin_nontemporal_load(row + SEG + sl) : 0u;
-  auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
+  // (one-request waves: the header is wave-uniform, read into scalar registers, which keeps the
+  // request context out of the large stage's VGPRs)
+  auto hdr = [&](uint32_t k) -> uint32_t {
+    if constexpr (SEG == 64) return (uint32_t)__builtin_amdgcn_readlane((int)rw, (int)k);
+    return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG);
+  };
   // SPLIT: the scan list's count and each lane's first bucket pair, issued with the row loads (they
   // depend only on r), so the staging below does not wait for a second trip after the row's
   uint32_t scan_nb0 = 0;
@@ -2431,32 +2442,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < NS; k++) cum[k + 1] = cum[k] + (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)(k * SEG));
     const uint32_t W = cum[NS];
-    if constexpr (STATS) {
-      // (profiling) distinct buckets and distinct candidate heads over the wave's pool:
-      // st[1] distinct heads, st[2] distinct buckets, st[3] pool candidates (lane 0 counts)
-      if (lane == 0) {
-        uint32_t dh = 0, db = 0, tot = 0;
-        for (uint32_t s1 = 0; s1 < NS; s1++) {
-          if (wl.sst[s1][0] > L::HC) continue;
-          for (uint32_t b1 = 0; b1 < wl.sne[s1]; b1++) {
-            const uint32_t f1 = wl.u.b.efirst[s1][b1] & EF_FIRST;
-            const uint32_t c1 = (b1 + 1 < wl.sne[s1] ? wl.u.b.epre[s1][b1 + 1] : (s1 == seg ? carry : 0u)) - wl.u.b.epre[s1][b1];
-            (void)c1;
-            bool seen = false;
-            for (uint32_t s2 = 0; s2 <= s1 && !seen; s2++) {
-              if (wl.sst[s2][0] > L::HC) continue;
-              const uint32_t lim = s2 == s1 ? b1 : wl.sne[s2];
-              for (uint32_t b2 = 0; b2 < lim && !seen; b2++) seen = (wl.u.b.efirst[s2][b2] & EF_FIRST) == f1;
-            }
-            if (!seen) db++;
-          }
-        }
-        // heads: count distinct head indices by checking each pool candidate against earlier ones
-        (void)dh; (void)tot;
-        st[2] += db;
-      }
-    }
     for (uint32_t base = 0; base < W; base += 64) {
+      const uint64_t t_r0 = STATS ? clock64() : 0;
       const uint32_t g = base + lane;
       bool ok = g < W;
       uint32_t s = 0, cb = 0;
@@ -2473,18 +2460,21 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t ef = ok ? wl.u.b.efirst[s][lo] : 0u;
       const uint32_t hidx = ok ? (ef & EF_FIRST) + (idx - wl.u.b.epre[s][lo]) : 0u;
       const uint32_t bcombo = ef >> EF_COMBO;
-      const uint32_t* head = a.bstream + (size_t)hidx * HEAD_WORDS;
+      const uint32_t* head = a.bstream + (size_t)(CG_DBG == 4 ? 0u : hidx) * HEAD_WORDS;
       const uint4* d4 = reinterpret_cast<const uint4*>(head);
       const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
-      if constexpr (STATS) {  // distinct heads of this round (a head first seen at the lowest lane)
-        bool first = ok;
-        for (uint32_t l2 = 0; l2 < 64; l2++) {
-          const uint32_t o2 = (uint32_t)__shfl((int)hidx, (int)l2);
-          const bool ok2 = base + l2 < W;
-          if (ok2 && l2 < lane && o2 == hidx) first = false;
-        }
-        st[1] += first ? 1u : 0u;
-        st[3] += ok ? 1u : 0u;
+      // (profiling: cycles of the round's parts, lane 0: st[1] candidate lookup, st[2] head load,
+      // st[3] atoms, st[5] hit recording)
+      uint64_t tr0 = 0;
+      if constexpr (STATS) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        tr0 = clock64();
+        if (lane == 0) st[1] += (uint32_t)(tr0 - t_r0);
+        const uint32_t keep = q0.x ^ q1.x ^ q2.x ^ q3.x;
+        asm volatile("" :: "v"(keep));
+        const uint64_t tr1 = clock64();
+        if (lane == 0) st[2] += (uint32_t)(tr1 - tr0);
+        tr0 = tr1;
       }
       // the candidate's request (segment s)
       const uint4 x0 = wl.cx[s][0], x1 = wl.cx[s][1], x2 = wl.cx[s][2], x3 = wl.cx[s][3];
@@ -2542,12 +2532,13 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       if (STATS) { st[6] += g < W; st[7] += ok; st[11] += lane < NS; }
       bool err = false, structural_hit = false;
       Err e{0, 0, 0, 0, 0};
+      if (CG_DBG == 1) pc = ok ? AT_SAT : AT_UNSAT;
       while (__ballot(pc < na)) {
         if (STATS && lane == 0) st[10]++;  // (profiling: atom rounds of the wave, in lane 0)
         if (pc < na) {
           const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
           const uint32_t rr = eval_atom<false>(tc, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
-          if (STATS) { st[8]++; const uint32_t kk = at.x & 0xFF; st[4] += kk == AK_LIKE; st[5] += kk == AK_INSET || kk == AK_RECSET || kk == AK_CONTAINS; }
+          if (STATS) { st[8]++; st[4] += (at.x & 0xFF) == AK_LIKE || (at.x & 0xFF) == AK_LIKEI; }
           if (rr == 3u) { structural_hit = true; pc = AT_UNSAT; }
           else if (rr == 2u) { err = true; pc = AT_UNSAT; }
           else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
@@ -2557,7 +2548,12 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t mlist = q2.w;
       const uint32_t nmem = hit ? (mlist ? ((q3.x >> 16) != 0xFFFFu ? (q3.x >> 16) : a.bstream[mlist]) : 1u) : 0u;  // (head word 12: the class size)
       if (STATS) st[9] += nmem;
-      const uint32_t pos0 = hit ? atomicAdd(&wl.sst[s][0], nmem) : 0u;
+      if constexpr (STATS) {
+        const uint64_t tr1 = clock64();
+        if (lane == 0) st[3] += (uint32_t)(tr1 - tr0);
+        tr0 = tr1;
+      }
+      const uint32_t pos0 = hit ? atomicAdd(&wl.sst[s][0], CG_DBG == 2 ? 1u : nmem) : 0u;
       const uint32_t xpos = (hit && err) ? atomicAdd(&wl.sst[s][1], 1u) : 0u;
       const uint32_t kind = err ? 2u : (flags & PF_FORBID) ? 1u : 0u;
       const uint32_t hmv = kind | (tier << 8) | (min(xpos, 0xFFu) << 16);
@@ -2565,7 +2561,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         wl.hp[s][pos0] = q2.z;
         wl.hm[s][pos0] = hmv;
       }
-      if (hit && mlist) {  // a duplicate class: every member, MEMB_U loads in flight
+      if (CG_DBG != 2 && hit && mlist) {  // a duplicate class: every member, MEMB_U loads in flight
         for (uint32_t j = 0; j < nmem && pos0 + j < L::HC; j += MEMB_U) {
           uint32_t v[MEMB_U];
 #pragma unroll
@@ -2587,6 +2583,10 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       if (hit) atomicMin(&wl.sst[s][2], tier);
       if (structural_hit) atomicOr(&wl.sst[s][3], 1u);
       wave_lds_sync();
+      if constexpr (STATS) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (lane == 0) st[5] += (uint32_t)(clock64() - tr0);
+      }
     }
     ne = 0;
     if (STATS && sl == 0) st[10]++;
@@ -2758,7 +2758,14 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint32_t wo = a.req_idx ? gid_m : (valid ? (a.ord ? a.ord[gid_m] : gid_m) : 0u);  // result slot
   const uint32_t t = min_tier;
   const bool structural = sballot(general) != 0;
-  const bool undecided = nh > L::HC || nx > L::XC || structural;
+  const bool undecided = (CG_DBG == 3 && FLAT) ? false : (nh > L::HC || nx > L::XC || structural);
+  if constexpr (CG_DBG == 3 && FLAT) {  // (diagnostic: the merge skipped)
+    if (valid && sl == 0) {
+      a.res[2 * (size_t)wo] = DEC_DENY | (t << 8) | (RF_VALID << 16);
+      a.res[2 * (size_t)wo + 1] = 0;
+    }
+    return;
+  }
   if (valid && undecided && sl == 0) {
     const uint32_t why = (structural || L::HC >= 1024) ? RF_GENERAL : RF_BIG;
     a.res[2 * (size_t)wo] = DEC_DENY | (t << 8) | ((RF_VALID | RF_OVERFLOW | why) << 16);

@@ -31,7 +31,7 @@ for step in "$@"; do
       for leg in "${LEGS[@]}" "${LEGS[@]}"; do
         env $leg timeout -k 10 300 python -u bench.py --no-cpu-baseline --latency-batches 0 --serve-threads 0 --no-reload --configs-requests 0 --no-submit-to-results ${BENCH_ARGS} > $O/quick_$k.json 2> $O/quick_$k.err || { echo "bench failed ($leg)"; tail -20 $O/quick_$k.err; exit 1; }
         python3 -c "
-import json; d=json.load(open('$O/quick_$k.json')); p=d['config'].get('phases_ms',{})
+import json; d=json.load(open('$O/quick_$k.json')); p=d['roofline'].get('phases_ms',{})
 print('[$leg]', round(d['value']/1e6,1), 'M/s ms', round(d['ms_per_step'],4), 'phases', {a: round(b,4) for a,b in p.items()}, 'parity', d['parity_sample'])"
         k=$((k+1))
       done ;;
