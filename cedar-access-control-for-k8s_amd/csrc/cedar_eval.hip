@@ -771,14 +771,17 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
           for (uint32_t q = 0; q < nk && hashable; q++) {
             const uint32_t* fl = t + 1 + RS_FIELD_WORDS * q;
             uint32_t fh = 0;
+            // (a field that is no primitive hashes by its tag alone, as the encoder hashes a record
+            // element's nested sets and records (encode_impl.h mem_chash): equal records still hash
+            // alike, and a hash match is compared exactly)
             if (fl[1] == RF_CONST) {
               hashable = reg_chash(fl[2], fl[3], fl[4], fh);
             } else if (fl[1] == RF_HOLE) {
               const uint2 hv3 = hot_get(c, fl[2]);
               const RV hx = load_val(c, hv3.x, hv3.y);
-              hashable = reg_chash(hx.w0, hx.w1, hx.w2, fh);
-            } else {
-              hashable = false;
+              if (!reg_chash(hx.w0, hx.w1, hx.w2, fh)) fh = chash_prim(tag_of(hx), 0u, 0u);
+            } else {  // RF_SETLIT: a set
+              fh = chash_prim(T_SET, 0u, 0u);
             }
             th = chash_mix(chash_mix(th, fl[0]), fh);
           }
@@ -1550,10 +1553,13 @@ constexpr uint32_t FLAT_NS(uint32_t seg) { return seg == 8 ? 8u : 1u; }
 // Per-wave LDS of the probe kernel, one region per request segment of SEG lanes.
 // SLIM (one-request waves, images of <= RANK_POL policies): no hm; a hit's kind, tier and error
 // slot ride in its hp word (SLIM_* below), so the large stage's wave takes 8,960 B of LDS.
-template <uint32_t SEG, uint32_t HCAP, bool SLIM = false>
+// HOTC: hot entries per request row (the compact candidate pass: images of <= 16 hot values and
+// staged like words).
+template <uint32_t SEG, uint32_t HCAP, bool SLIM = false, uint32_t HOTC = NHOT>
 struct alignas(16) SegLds {  // (16: the counting merge reads hp four words at a time)
   static constexpr uint32_t NS = 64 / SEG;     // requests per wave
-  static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : 32;  // staged buckets per request (>= 2 stages)
+  // staged buckets per request (>= 2 stages; the compact candidate pass stages 16 at a time)
+  static constexpr uint32_t EC = SEG >= 32 ? 2 * SEG : (HOTC < NHOT ? 16 : 32);
   static constexpr uint32_t HC = HCAP;         // hits per request (more: RF_BIG / RF_GENERAL re-run)
   // error details per request (more: the on-device follow-up, which holds 32; more still: the
   // stream kernel). 32 keeps the large stage's 4-wave block under 53 KB: 3 blocks per CU
@@ -1576,13 +1582,17 @@ struct alignas(16) SegLds {  // (16: the counting merge reads hp four words at a
   uint32_t he[NS][XC * 4 + PAD];   // error details: code | aux << 8, k, et, ei
   // (hot rows one uint2 longer: the pooled candidate pass reads slot h of several requests' rows in
   // lockstep, which unpadded rows (64 words apart) put on the same banks)
-  uint2 hot[NS][NHOT + (NS > 1 ? 1 : 0)];
+  uint2 hot[NS][HOTC + (NS > 1 ? 1 : 0)];
   // the candidate pass's wave-wide task pool (FLAT: SPLIT, 8-lane segments): every segment's request
   // context, for lanes that evaluate another segment's candidates, and its running state (rows of
   // 5 uint4, the last unused: 80 bytes apart, 8 requests' rows on disjoint banks)
   uint4 cx[FLAT_NS(SEG)][FLAT_NS(SEG) > 1 ? 5 : 4];  // (blk, pt, pi, at), (ai, rt, ri, p_anc), (r_anc, a_anc, nanc p|r, a_nanc | self << 16), (rowo, am lo, am hi, 0)
   uint32_t sst[FLAT_NS(SEG)][4];   // hits recorded, error details, lowest tier with a hit, flags (1: structural)
   uint32_t sne[FLAT_NS(SEG)];      // buckets staged
+  // the compact pooled candidate pass: each lane's candidate's head atoms (the head's second 64
+  // bytes, loaded with its descriptor), [atom][lane], so the atom loop reads LDS, not memory
+  static constexpr bool ATOMS = NS == 8 && HOTC < NHOT;
+  uint4 at4[ATOMS ? HEAD_ATOMS : 1][ATOMS ? 64 : 1];
 };
 
 // Slim per-request context of the probe kernel (everything wave-uniform but the pointers' data).
@@ -2115,11 +2125,11 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
 // only when its slowest wave ends; smaller blocks let fast waves' slots be reused sooner.
 // SLIM: the large stage over an image of <= RANK_POL policies (SegLds SLIM words; merge by bitmaps).
 template <uint32_t SEG, uint32_t HCAP, uint32_t MINW = 1, bool STATS = false, uint32_t PW = WAVES, bool SPLIT = false,
-          bool SLIM = false>
+          bool SLIM = false, uint32_t HOTC = NHOT>
 __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint64_t t_start = STATS ? clock64() : 0;
   static_assert(!SLIM || (SEG == 64 && HCAP >= 2 * RANK_POL / 32), "SLIM: one-request waves whose hs holds the bitmap");
-  using L = SegLds<SEG, HCAP, SLIM>;
+  using L = SegLds<SEG, HCAP, SLIM, HOTC>;
   static_assert(L::HC <= 4096 && L::XC <= 255, "hit slots are 12-bit sort payloads, error slots 8-bit");
   constexpr uint32_t NS = L::NS;
   __shared__ L wl_all[PW];
@@ -2195,7 +2205,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
                            : make_uint2(0u, 0u);
   c.lkb = a.like_base;
   c.lslot = a.lslot;
-  if (a.like_base != 0xFFFFFFFFu)  // the like words, as hot entries behind the hot values
+  if (a.like_base != 0xFFFFFFFFu)  // the like words, as hot entries behind the hot values (the launch
+                                   // picks a HOTC that holds them)
     for (uint32_t j = sl; j < 3u * (uint32_t)__popc(a.lslot); j += SEG)
       wl.hot[seg][a.like_base + j] = valid ? make_uint2(__builtin_nontemporal_load(row + a.like_off + 2 * j),
                                                         __builtin_nontemporal_load(row + a.like_off + 2 * j + 1))
@@ -2443,7 +2454,6 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     for (uint32_t k = 0; k < NS; k++) cum[k + 1] = cum[k] + (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)(k * SEG));
     const uint32_t W = cum[NS];
     for (uint32_t base = 0; base < W; base += 64) {
-      const uint64_t t_r0 = STATS ? clock64() : 0;
       const uint32_t g = base + lane;
       bool ok = g < W;
       uint32_t s = 0, cb = 0;
@@ -2463,18 +2473,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t* head = a.bstream + (size_t)(CG_DBG == 4 ? 0u : hidx) * HEAD_WORDS;
       const uint4* d4 = reinterpret_cast<const uint4*>(head);
       const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
-      // (profiling: cycles of the round's parts, lane 0: st[1] candidate lookup, st[2] head load,
-      // st[3] atoms, st[5] hit recording)
-      uint64_t tr0 = 0;
-      if constexpr (STATS) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        tr0 = clock64();
-        if (lane == 0) st[1] += (uint32_t)(tr0 - t_r0);
-        const uint32_t keep = q0.x ^ q1.x ^ q2.x ^ q3.x;
-        asm volatile("" :: "v"(keep));
-        const uint64_t tr1 = clock64();
-        if (lane == 0) st[2] += (uint32_t)(tr1 - tr0);
-        tr0 = tr1;
+      if constexpr (L::ATOMS) {  // the head's atoms, in flight with its descriptor, parked in LDS
+        const uint4 a0 = d4[4], a1 = d4[5], a2 = d4[6], a3 = d4[7];
+        wl.at4[0][lane] = a0; wl.at4[1][lane] = a1; wl.at4[2][lane] = a2; wl.at4[3][lane] = a3;
       }
       // the candidate's request (segment s)
       const uint4 x0 = wl.cx[s][0], x1 = wl.cx[s][1], x2 = wl.cx[s][2], x3 = wl.cx[s][3];
@@ -2535,24 +2536,31 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       if (CG_DBG == 1) pc = ok ? AT_SAT : AT_UNSAT;
       while (__ballot(pc < na)) {
         if (STATS && lane == 0) st[10]++;  // (profiling: atom rounds of the wave, in lane 0)
+        // (profiling, lane 0: cycles and count of the atom rounds in which some lane evaluates a
+        // set atom (RECSET / CONTAINS): st[1], st[2]; of the other rounds: st[3], st[5])
+        const uint64_t ta0 = STATS ? clock64() : 0;
+        bool set_atom = false;
         if (pc < na) {
-          const uint4 at = *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
+          const uint4 at = (L::ATOMS && pc < HEAD_ATOMS) ? wl.at4[L::ATOMS ? pc : 0][lane]
+                                                          : *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
+          if (STATS) set_atom = (at.x & 0xFF) == AK_RECSET || (at.x & 0xFF) == AK_CONTAINS;
           const uint32_t rr = eval_atom<false>(tc, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
           if (STATS) { st[8]++; st[4] += (at.x & 0xFF) == AK_LIKE || (at.x & 0xFF) == AK_LIKEI; }
           if (rr == 3u) { structural_hit = true; pc = AT_UNSAT; }
           else if (rr == 2u) { err = true; pc = AT_UNSAT; }
           else pc = rr ? ((at.x >> 16) & 0xFF) : (at.x >> 24);
         }
+        if constexpr (STATS) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          const uint32_t dt = (uint32_t)(clock64() - ta0);
+          const bool any_set = __ballot(set_atom) != 0;
+          if (lane == 0) { if (any_set) { st[1] += dt; st[2]++; } else { st[3] += dt; st[5]++; } }
+        }
       }
       const bool hit = ok && (err || pc == AT_SAT);
       const uint32_t mlist = q2.w;
       const uint32_t nmem = hit ? (mlist ? ((q3.x >> 16) != 0xFFFFu ? (q3.x >> 16) : a.bstream[mlist]) : 1u) : 0u;  // (head word 12: the class size)
       if (STATS) st[9] += nmem;
-      if constexpr (STATS) {
-        const uint64_t tr1 = clock64();
-        if (lane == 0) st[3] += (uint32_t)(tr1 - tr0);
-        tr0 = tr1;
-      }
       const uint32_t pos0 = hit ? atomicAdd(&wl.sst[s][0], CG_DBG == 2 ? 1u : nmem) : 0u;
       const uint32_t xpos = (hit && err) ? atomicAdd(&wl.sst[s][1], 1u) : 0u;
       const uint32_t kind = err ? 2u : (flags & PF_FORBID) ? 1u : 0u;
@@ -2583,10 +2591,6 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       if (hit) atomicMin(&wl.sst[s][2], tier);
       if (structural_hit) atomicOr(&wl.sst[s][3], 1u);
       wave_lds_sync();
-      if constexpr (STATS) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        if (lane == 0) st[5] += (uint32_t)(clock64() - tr0);
-      }
     }
     ne = 0;
     if (STATS && sl == 0) st[10]++;
@@ -4218,7 +4222,16 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
       }
       return;
     }
-    if (cocc == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
+    // The compact candidate pass (CEDARGPU_CAND_COMPACT=0: off): images whose hot values and like
+    // words fit 16 entries take 32-hit rows and 16-entry hot rows, and spend the 4 KB of LDS that
+    // saves on each lane's head atoms (SegLds::at4): 10.1 KB per wave as before, 4 waves per SIMD
+    // (CEDARGPU_CAND_OCC=5: 96 VGPRs, which spills 128 B per lane: 0.99 vs 0.67 ms, gpurun_out/r05g)
+    static const bool compact_on = !(std::getenv("CEDARGPU_CAND_COMPACT") && *std::getenv("CEDARGPU_CAND_COMPACT") == '0');
+    const uint32_t hot_need = k.n_hot + (k.like_base != 0xFFFFFFFFu ? 3u * (uint32_t)__builtin_popcount(k.lslot) : 0u);
+    static const uint32_t cocc_c = [] { const char* e = std::getenv("CEDARGPU_CAND_OCC"); return e ? (uint32_t)std::atoi(e) : 4u; }();
+    if (compact_on && hot_need <= 16 && cocc_c == 4)
+      hipLaunchKernelGGL((cedar_probe_kernel<8, 32, 4, false, 1, true, false, 16>), dim3((n + 7) / 8), dim3(64), 0, s, k);
+    else if (cocc == 4) hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
     else hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 3, false, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, k);
     return;
   }
