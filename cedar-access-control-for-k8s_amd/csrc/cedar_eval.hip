@@ -119,7 +119,21 @@ struct KArgs {
   // inline like atoms (image.h AK_LIKEI): like slots, their words' row offset, and the hot-row index
   // the probe kernel stages them at (0xFFFFFFFF: not staged; the atom reads the string's bytes)
   uint32_t lslot, like_off, like_base;
+  // first pass of a grouped batch: runs of xcd_chunk consecutive waves (of the grouped order) on
+  // one XCD (blocks are dealt round-robin over the 8 XCDs), so neighbours share that XCD's L2;
+  // 0: block order (xcd_block)
+  uint32_t xcd_chunk;
 };
+// Block b of nb one-wave blocks -> the wave it runs: block b lands on XCD b % 8 as its (b / 8)-th
+// block; chunks of C consecutive waves go to one XCD, chunks dealt round-robin (a bijection on the
+// first multiple of 8C blocks, the rest in place). Speed only: any mapping is correct.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t C) {
+  if (!C) return b;
+  const uint32_t full = nb - nb % (8u * C);
+  if (b >= full) return b;
+  const uint32_t x = b & 7u, j = b >> 3;
+  return ((j / C) * 8u + x) * C + (j % C);
+}
 // SCAN_CAP: bucket pairs a request's list holds (more: SCAN_OVF, the large stage probes the index
 // itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
 // the large stage, which reads the list when it holds them all
@@ -1762,7 +1776,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
   auto sballot = [&](bool p) -> uint64_t { return __ballot(p) & smask; };
   auto sbcast = [&](uint32_t x, uint32_t k) -> uint32_t { return (uint32_t)__shfl((int)x, (int)(sbase + k)); };
-  const uint32_t gid_ = blockIdx.x * (64 / SEG) + seg;
+  const uint32_t gid_ = xcd_block(blockIdx.x, gridDim.x, a.ord ? a.xcd_chunk : 0u) * (64 / SEG) + seg;
   const bool valid = gid_ < a.n_req;
   const uint32_t gid = valid ? (a.ord ? a.ord[gid_] : gid_) : 0u;  // the request (its list and results)
   const uint32_t* row = a.grows ? a.grows + (size_t)(valid ? gid_ : 0u) * a.row_words : a.rows + (size_t)gid * a.row_words;
@@ -2151,7 +2165,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     }
     return x;
   };
-  const uint32_t gid = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
+  const uint32_t blk_w = (PW == 1 && a.ord && !a.req_idx) ? xcd_block(blockIdx.x, gridDim.x, a.xcd_chunk) : blockIdx.x;
+  const uint32_t gid = (blk_w * PW + (threadIdx.x >> 6)) * NS + seg;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;
   bool valid = gid < n_req;
   const uint32_t r0 = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0u;
@@ -2172,11 +2187,15 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   // SPLIT: the scan list's count and each lane's first bucket pair, issued with the row loads (they
   // depend only on r), so the staging below does not wait for a second trip after the row's
   uint32_t scan_nb0 = 0;
-  uint2 scan_q0 = make_uint2(0u, 0u);
+  uint2 scan_q0 = make_uint2(0u, 0u), scan_q1 = make_uint2(0u, 0u);
   if constexpr (SPLIT) {
     if (valid) {
       scan_nb0 = a.scan[r];
       scan_q0 = *reinterpret_cast<const uint2*>(a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP) + 2 * sl);
+      // 8-lane segments: each lane's second pair too (a request of 9..16 buckets then stages with no
+      // second trip; SCAN_CAP >= 64 keeps it inside the request's list)
+      if constexpr (SEG == 8)
+        scan_q1 = *reinterpret_cast<const uint2*>(a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP) + 2 * (sl + SEG));
     }
   }
   PCtx c;
@@ -2230,7 +2249,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       wl.cx[seg][0] = make_uint4(blk_off, c.pt, c.pi, c.at);
       wl.cx[seg][1] = make_uint4(c.ai, c.rt, c.ri, c.p_anc);
       wl.cx[seg][2] = make_uint4(c.r_anc, c.a_anc, c.p_nanc | (c.r_nanc << 16), c.a_nanc | (aself << 16));
-      wl.cx[seg][3] = make_uint4(c.rowo, (uint32_t)am, (uint32_t)(am >> 32), 0u);
+      wl.cx[seg][3] = make_uint4(c.rowo, (uint32_t)am, (uint32_t)(am >> 32), r);  // (r: the merge's result slot)
       wl.sst[seg][0] = 0u;
       wl.sst[seg][1] = 0u;
       wl.sst[seg][2] = a.n_tiers - 1;
@@ -2629,7 +2648,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
       for (uint32_t i = sl; i < L::EC; i += SEG)
         if (b0 + i < nbk) {
-          const uint2 q = (b0 == 0 && i == sl) ? scan_q0 : *reinterpret_cast<const uint2*>(pairs + 2 * (b0 + i));
+          const uint2 q = (b0 == 0 && i == sl) ? scan_q0
+                          : (SEG == 8 && b0 == 0 && i == sl + SEG) ? scan_q1
+                                                                   : *reinterpret_cast<const uint2*>(pairs + 2 * (b0 + i));
           wl.u.b.efirst[seg][i] = q.x | ((q.y >> SCAN_COMBO_SHIFT) << EF_COMBO);
           wl.u.b.epre[seg][i] = q.y & SCAN_COUNT;
         }
@@ -2757,9 +2778,11 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   asm volatile("" : "+v"(lane_m));
   seg = lane_m / SEG; sl = lane_m % SEG; sbase = seg * SEG;
   smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
-  const uint32_t gid_m = (blockIdx.x * PW + (threadIdx.x >> 6)) * NS + seg;
+  const uint32_t gid_m = (((PW == 1 && a.ord && !a.req_idx) ? xcd_block(blockIdx.x, gridDim.x, a.xcd_chunk) : blockIdx.x) * PW + (threadIdx.x >> 6)) * NS + seg;
   valid = gid_m < n_req && !(a.req_idx && (a.req_idx[gid_m] & FU_DONE));
-  const uint32_t wo = a.req_idx ? gid_m : (valid ? (a.ord ? a.ord[gid_m] : gid_m) : 0u);  // result slot
+  // result slot (FLAT: the request index parked in its context row, an LDS read instead of a
+  // dependent reload of the order)
+  const uint32_t wo = a.req_idx ? gid_m : (valid ? (FLAT ? wl.cx[seg][3].w : (a.ord ? a.ord[gid_m] : gid_m)) : 0u);
   const uint32_t t = min_tier;
   const bool structural = sballot(general) != 0;
   const bool undecided = (CG_DBG == 3 && FLAT) ? false : (nh > L::HC || nx > L::XC || structural);
@@ -4006,6 +4029,8 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   // like words staged behind the hot values while both fit the probe kernel's hot rows (32 entries;
   // CEDARGPU_LIKE_STAGE=0: never, A/B): else AK_LIKEI reads the string's bytes
   static const bool like_stage = !(std::getenv("CEDARGPU_LIKE_STAGE") && *std::getenv("CEDARGPU_LIKE_STAGE") == '0');
+  static const uint32_t xcd_chunk = [] { const char* e = std::getenv("CEDARGPU_XCD_CHUNK"); return e ? (uint32_t)std::atoi(e) : 0u; }();
+  k.xcd_chunk = xcd_chunk;
   k.lslot = img.lslot_mask;
   k.like_off = img.like_off;
   k.like_base = (like_stage && img.lslot_mask && img.n_hot + 3u * (uint32_t)__builtin_popcount(img.lslot_mask) <= NHOT) ? img.n_hot : 0xFFFFFFFFu;

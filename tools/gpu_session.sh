@@ -43,6 +43,21 @@ print('[$leg]', round(d['value']/1e6,1), 'M/s ms', round(d['ms_per_step'],4), 'p
       find $O/rocprof -name "*kernel_stats.csv" -exec head -12 {} \; ;;
     pmc)
       bash tools/pmc_kernels.sh $TAG/pmc || exit 1 ;;
+    pmcb)
+      # memory-pipeline busy / stall counters per kernel (each pass its own run, within the per-block
+      # limits: TA 2, TD 2, TCP 4, TCC 4, GRBM 2)
+      P=$GRAFT_REPO_ROOT/$O/pmcb
+      mkdir -p $P
+      ARGS="--steps 3 --warmup 1 --no-cpu-baseline --latency-batches 0 --parity-sample 0 --no-reload --serve-threads 0 --configs-requests 0 --no-submit-to-results ${BENCH_ARGS}"
+      for pass in "ta:TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE" \
+                  "tcp:TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum" \
+                  "tcc:TCC_HIT_sum TCC_MISS_sum TCC_TAG_STALL_sum TCC_BUSY_sum" ; do
+        name=${pass%%:*}; ctrs=${pass#*:}
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $P/$name -o run -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS) > $P/$name.log 2>&1 || { echo "pass $name failed"; tail -20 $P/$name.log; exit 1; }
+      done
+      for K in cedar_scan_kernel "cedar_probe_kernel<8u, 32u" "cedar_probe_kernel<8u, 64u" "cedar_probe_kernel<64u, 1024u"; do
+        echo "== $K"; PMC_KERNEL="$K" python3 tools/pmc_summary.py $P
+      done > $P/summary.txt; cat $P/summary.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
