@@ -97,6 +97,7 @@ struct KArgs {
   const uint32_t* __restrict__ sctx;   // scope bitsets (image.h): context table, (bits, rank) rows,
   const uint32_t* __restrict__ sbits;  //   and every set bit's bucket at its rank
   const uint32_t* __restrict__ svals;
+  const uint32_t* __restrict__ sbloom;  // context filter (image.h ctx_bloom_*; null: none)
   uint32_t sctx_mask, sbits_words;     // sbits_words 0: the image has none
   uint32_t n_kent;                     // key entities: a request's key-entity indices are below it
   uint32_t* bad_kidx;                  // count of requests whose indices are not (null: not counted)
@@ -1935,7 +1936,14 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         // the whole 32-byte slot in one trip, compared word for word (exact: a found context's
         // set bits are the request's keys themselves)
         const uint32_t hash = ctx_key(key_pre(cb, q.x, q.y, r.x, r.y), hs, v0, v1), w0c = ctx_w0(cb, hs);
-        for (uint32_t h = hash & a.sctx_mask;; h = (h + 1) & a.sctx_mask) {
+        bool maybe = true;  // the context filter first: most contexts a request names do not exist
+        if (a.sbloom) {
+          const uint32_t bw = ctx_bloom_words(a.sctx_mask + 1u);
+          const uint2 fw = *reinterpret_cast<const uint2*>(a.sbloom + 2 * (size_t)ctx_bloom_at(hash, bw));
+          const uint64_t need = ctx_bloom_bits(hash);
+          maybe = ((((uint64_t)fw.y << 32) | fw.x) & need) == need;
+        }
+        for (uint32_t h = hash & a.sctx_mask; maybe; h = (h + 1) & a.sctx_mask) {
           const uint4* slp = reinterpret_cast<const uint4*>(a.sctx + (size_t)h * SCTX_WORDS);
           const uint4 x = slp[0], y = slp[1];
           if (x.x == 0) break;
@@ -3125,6 +3133,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.act = (uint32_t*)at(DS_ACT); d.btab = (uint32_t*)at(DS_BTAB); d.bfilt = (uint32_t*)at(DS_BFILT);
   d.bstream = (uint32_t*)at(DS_BSTREAM); d.srows = (uint32_t*)at(DS_SROWS); d.shash = (uint32_t*)at(DS_SHASH);
   d.sctx = (uint32_t*)at(DS_SCTX); d.sbits = (uint32_t*)at(DS_SBITS); d.svals = (uint32_t*)at(DS_SVALS);
+  d.sbloom = (uint32_t*)at(DS_SBLOOM);
   d.sctx_mask = (uint32_t)(img.dev_len[DS_SCTX] / 4 / SCTX_WORDS) - 1;
   d.sbits_words = img.sbits_words;
   d.n_kent = (uint32_t)img.key_ents.size();
@@ -4019,6 +4028,9 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.n_req = n; k.capr = capr; k.cape = cape;
   k.btab = img.btab; k.bfilt = img.bfilt; k.bstream = img.bstream; k.bmask = img.bmask; k.fmask = img.fmask;
   k.sctx = img.sctx; k.sbits = img.sbits; k.svals = img.svals; k.sctx_mask = img.sctx_mask; k.sbits_words = img.sbits_words;
+  // the context filter (CEDARGPU_CTX_BLOOM=0: probe every context, A/B)
+  static const bool ctx_bloom = !(std::getenv("CEDARGPU_CTX_BLOOM") && *std::getenv("CEDARGPU_CTX_BLOOM") == '0');
+  k.sbloom = ctx_bloom ? img.sbloom : nullptr;
   k.n_kent = img.n_kent;
   k.bad_kidx = b.fu_cnt ? b.fu_cnt + FU_KINDS : nullptr;
   k.l2_vmask = img.l2_vmask; k.l2_lmask = img.l2_lmask;

@@ -1093,7 +1093,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
   img.key_ents.clear();
-  img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0;
+  img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0; img.sbloom.assign(2 * ctx_bloom_words(2), 0);
   img.combo_mask = 0;
   img.pslot_mask = 0;
   img.pfx.assign((size_t)img.n_hot() * PFX_LENS, 0);
@@ -1126,7 +1126,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
     img.btab_slots = 2;
-    img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0;
+    img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0; img.sbloom.assign(2 * ctx_bloom_words(2), 0);
     return;
   }
   static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
@@ -1570,6 +1570,17 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       e[0] = ctx_w0(x[0], x[5]);
       e[1] = x[1]; e[2] = x[2]; e[3] = x[3]; e[4] = x[4]; e[5] = x[6]; e[6] = x[7];
       e[7] = c.second;
+    }
+    // the context filter: every context's key (the kernel's lookup hash)
+    const uint32_t bw = ctx_bloom_words(slots);
+    img.sbloom.assign(2 * (size_t)bw, 0);
+    for (auto& c : ctx) {
+      const auto& x = c.first;
+      const uint32_t hash = ctx_key(key_pre(x[0], x[1], x[2], x[3], x[4]), x[5], x[6], x[7]);
+      const uint32_t w = ctx_bloom_at(hash, bw);
+      const uint64_t b = ctx_bloom_bits(hash);
+      img.sbloom[2 * (size_t)w] |= (uint32_t)b;
+      img.sbloom[2 * (size_t)w + 1] |= (uint32_t)(b >> 32);
     }
   }
   if (times)
@@ -2143,7 +2154,7 @@ void Image::write_blob(void* wp) const {
   const std::pair<const void*, size_t> sec[DS_COUNT] = {
       words(pstream), words(tier_cend), words(chunks), words(cpool), words(gstr_off), words(hot), words(act),
       words(btab), words(bfilt), words(bstream), words(srows), words(shash), words(sctx), words(sbits), words(svals),
-      std::make_pair((const void*)gstr_bytes.data(), gstr_bytes.size())};
+      words(sbloom), std::make_pair((const void*)gstr_bytes.data(), gstr_bytes.size())};
   w.align(DS_ALIGN);
   const size_t begin = w.n;
   for (uint32_t k = 0; k < DS_COUNT; k++) {
@@ -2246,7 +2257,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     if (off % DS_ALIGN || off < img->dev_begin || len % 4 || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");
     return {reinterpret_cast<const uint32_t*>(p + off), (size_t)(len / 4)};
   };
-  for (uint32_t k : {DS_PSTREAM, DS_BTAB, DS_BFILT, DS_BSTREAM, DS_SCTX, DS_SBITS, DS_SVALS}) (void)sec_view(k);
+  for (uint32_t k : {DS_PSTREAM, DS_BTAB, DS_BFILT, DS_BSTREAM, DS_SCTX, DS_SBITS, DS_SVALS, DS_SBLOOM}) (void)sec_view(k);
   sec_words(DS_TIER_CEND, img->tier_cend); sec_words(DS_CHUNKS, img->chunks);
   sec_words(DS_CPOOL, img->cpool); sec_words(DS_GSTR_OFF, img->gstr_off); sec_words(DS_HOT, img->hot);
   sec_words(DS_ACT, img->act); sec_words(DS_SROWS, img->srows); sec_words(DS_SHASH, img->shash);
@@ -2284,7 +2295,8 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     const size_t svals_n = sec_view(DS_SVALS).second;
     const size_t nc = sctx_n / SCTX_WORDS;
     if (!nc || (nc & (nc - 1)) || sctx_n % SCTX_WORDS || sbits_n % 2 ||
-        (img->sbits_words && (sbits_n / 2) % img->sbits_words) || svals_n < 2 || svals_n % 2)
+        (img->sbits_words && (sbits_n / 2) % img->sbits_words) || svals_n < 2 || svals_n % 2 ||
+        sec_view(DS_SBLOOM).second != 2 * (size_t)ctx_bloom_words((uint32_t)nc))
       throw CedarError("corrupt image (scope bitsets)");
     // every context row in range, a free slot that ends every probe chain, and ranks that number
     // every set bit within svals

@@ -21,6 +21,7 @@ struct DevImage {
   void* btab_mem = nullptr;  // the slot table btab points to (built at load from the entry list)
   uint32_t *srows = nullptr, *shash = nullptr;                      // static entities
   uint32_t *sctx = nullptr, *sbits = nullptr, *svals = nullptr;     // scope bitsets
+  uint32_t* sbloom = nullptr;                                        // their context filter
   uint32_t sctx_mask = 0, sbits_words = 0, l2_vmask = 0, l2_lmask = 0;
   uint32_t n_kent = 0;  // key entities (Image::key_ents): valid key-entity indices are below it
   uint8_t* gstr_bytes = nullptr;

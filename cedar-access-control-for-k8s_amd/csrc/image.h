@@ -231,6 +231,17 @@ __host__ __device__ constexpr inline uint32_t ctx_key(uint32_t pre, uint32_t hs,
   return ctx_hash(pre ^ ((hs + 1) * 0x27D4EB2Fu) ^ (v0 * 0x165667B1u) ^ (v1 * 0xD3A2646Cu));
 }
 __host__ __device__ constexpr inline uint32_t ctx_w0(uint32_t combo, uint32_t hs) { return SCTX_USED | (combo << 16) | (hs & 0xFFFFu); }
+// Context filter (sbloom): a blocked Bloom filter over the contexts' keys, one 64-bit word per key
+// holding 3 bits, max(16, slots / 8) words for a table of `slots` context slots (~16 bits per key).
+// A request tests it before it probes the table: ~3 of 4 contexts a C3 request looks up do not
+// exist, and the filter's few KB stay cached where each absent probe cost a line of the table.
+__host__ __device__ constexpr inline uint32_t ctx_bloom_words(uint32_t slots) { return slots / 8 > 16 ? slots / 8 : 16; }
+__host__ __device__ constexpr inline uint32_t ctx_bloom_at(uint32_t hash, uint32_t words) { return ((hash * 0x9E3779B1u) >> 7) & (words - 1); }
+__host__ __device__ constexpr inline uint64_t ctx_bloom_bits(uint32_t hash) {
+  uint32_t g = hash * 0x85EBCA77u;
+  g ^= g >> 13;
+  return (1ull << (g & 63u)) | (1ull << ((g >> 6) & 63u)) | (1ull << ((g >> 12) & 63u));
+}
 
 // 128-bit Bloom filter over entity UIDs (string-id pairs), identical on host and device.
 __host__ __device__ constexpr inline uint32_t uid_bloom_bit(uint32_t et, uint32_t ei) {
@@ -464,7 +475,7 @@ constexpr uint32_t IMG_VERSION = 14;
 // itself when a collective delivered it to device memory), with each array at its blob offset.
 enum DevSection : uint32_t {
   DS_PSTREAM, DS_TIER_CEND, DS_CHUNKS, DS_CPOOL, DS_GSTR_OFF, DS_HOT, DS_ACT, DS_BTAB, DS_BFILT, DS_BSTREAM,
-  DS_SROWS, DS_SHASH, DS_SCTX, DS_SBITS, DS_SVALS, DS_GSTR_BYTES, DS_COUNT
+  DS_SROWS, DS_SHASH, DS_SCTX, DS_SBITS, DS_SVALS, DS_SBLOOM, DS_GSTR_BYTES, DS_COUNT
 };
 constexpr uint32_t DS_ALIGN = 256;
 
