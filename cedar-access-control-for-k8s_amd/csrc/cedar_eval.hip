@@ -1719,7 +1719,7 @@ __device__ __forceinline__ bool l2_bloom_maybe(uint4 b, uint32_t h2) {
 // LDS and no candidate evaluation: far fewer registers than the probe kernel, so more requests are
 // in flight per CU; the probe kernel's SPLIT variant then evaluates the buckets' heads.
 // principal key ancestors the scan stages in LDS per request (more: read from the request block)
-constexpr uint32_t SCAN_ANC = 64;
+constexpr uint32_t SCAN_ANC = 40;
 // key-filter pass: keys per lane per round (independent loads in flight), and the filter-passing
 // keys a request lists in LDS (more: it probes every key, as with the filter off)
 constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
@@ -1829,22 +1829,6 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       s_hot[seg][h] = valid ? *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h) : make_uint2(0u, 0u);
     wave_lds_sync();
   }
-  // BITS: the staged key-entity indices checked once: every one the image's (a batch encoded for
-  // another image: `kbad`, the request then enumerates its keys and is counted) and the key
-  // ancestors' ascending, all of them staged (`kin`: the contexts' inline lists can be searched in
-  // them, image.h SCTX_INLINE)
-  bool kbad = false, kin = false;
-  if (BITS && klist) {
-    const uint32_t nst = min(nk, SCAN_ANC);
-    bool bad = false, uns = false;
-    for (uint32_t j = sl; j <= nst; j += SEG) {
-      const uint32_t kid = s_kid[seg][j];
-      bad = bad || (kid >= a.n_kent && !(j == 0 && kid == KIDX_NONE));
-      uns = uns || (j >= 2 && kid <= s_kid[seg][j - 1]);
-    }
-    kbad = sballot(bad) != 0;
-    kin = nk <= SCAN_ANC && sballot(uns) == 0 && !kbad;
-  }
   // level-1 key k of the request: its combo and (principal, action, resource) components
   auto key_at = [&](uint32_t k, uint32_t& cbo, uint2& p, uint2& q, uint2& r) {
     uint32_t j = k, combo = 0;
@@ -1908,14 +1892,11 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     }
     const uint32_t per = 1u + nvs + sbcast(linc, SEG - 1), nctx = ncb * per;
     on = on && nctx <= CTX_CAP;
-    // the contexts, looked up side by side (lane j % SEG takes context j); a found one is kept:
-    // bitset contexts at s_cx[0, nf) (combo | hs << 8, v0, v1, row), contexts with an inline list
-    // (when the request can search it, kin) at s_cx[CTX_CAP - 1 - k] (combo | hs << 8, slot, n,
-    // rank of the row's first set bit)
-    uint32_t nf = 0, nfi = 0;  // contexts found (segment-uniform)
+    // the contexts, looked up side by side (lane j % SEG takes context j); a found one is kept
+    uint32_t nf = 0;  // contexts found (segment-uniform)
     for (uint32_t j0 = 0; __ballot(on && j0 < nctx) != 0; j0 += SEG) {
       const uint32_t j = j0 + sl;
-      uint32_t cb = 0, hs = SCTX_L1, v0 = 0, v1 = 0, row_ = KIDX_NONE, slot_ = 0, n_inl = 0, base_ = 0;
+      uint32_t cb = 0, hs = SCTX_L1, v0 = 0, v1 = 0, row_ = KIDX_NONE;
       const uint32_t ci = on ? j / per : 0u, t = on ? j - ci * per : 0u;
       // (the list entry, by shuffles from the lane that read its slot: every lane takes part)
       uint32_t li = 0, lb = 0, llo = 0, lhd = 0, lw = 0;
@@ -1964,61 +1945,20 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         }
         for (uint32_t h = hash & a.sctx_mask; maybe; h = (h + 1) & a.sctx_mask) {
           const uint4* slp = reinterpret_cast<const uint4*>(a.sctx + (size_t)h * SCTX_WORDS);
-          const uint4 x = slp[0], y = slp[1], z = slp[2];  // (the key, its row, the inline list's size and rank)
+          const uint4 x = slp[0], y = slp[1];
           if (x.x == 0) break;
           if (x.x == w0c && x.y == q.x && x.z == q.y && x.w == r.x && y.x == r.y && y.y == v0 && y.z == v1) {
             row_ = y.w;
-            slot_ = h;
-            n_inl = z.x;
-            base_ = z.y;
             break;
           }
         }
       }
       const bool got = on && j < nctx && row_ != KIDX_NONE;
-      const bool inl = got && kin && n_inl != 0;
-      const uint64_t mk = sballot(got && !inl), mi = sballot(inl);
-      if (got && !inl) s_cx[seg][nf + mbcnt64(mk)] = make_uint4(cb | (hs << 8), v0, v1, row_);
-      if (inl) s_cx[seg][CTX_CAP - 1 - (nfi + mbcnt64(mi))] = make_uint4(cb | (hs << 8), slot_, n_inl, base_);
+      const uint64_t mk = sballot(got);
+      if (got) s_cx[seg][nf + mbcnt64(mk)] = make_uint4(cb | (hs << 8), v0, v1, row_);
       nf += popc64(mk);
-      nfi += popc64(mi);
     }
     wave_lds_sync();
-    // inline lists (image.h SCTX_INLINE): each of the context's set bits searched among the
-    // request's key ancestors (ascending in s_kid[1..nk], the principal itself at s_kid[0]); SCAN_IU
-    // entries per lane a round, their LDS searches interleaved. A found one lists its key at its rank.
-    {
-      constexpr uint32_t SCAN_IU = 4;
-      const uint32_t self_kid = (pn >> 31) ? s_kid[seg][0] : KIDX_NONE;
-      for (uint32_t k = 0; __ballot(on && k < nfi) != 0; k++) {
-        const bool act = on && k < nfi;
-        const uint4 c = act ? s_cx[seg][CTX_CAP - 1 - k] : make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t* lw = a.sctx + (size_t)c.y * SCTX_WORDS + SCTX_LIST;
-        for (uint32_t e0 = 0; __ballot(e0 < c.z) != 0; e0 += SEG * SCAN_IU) {
-          uint32_t kid[SCAN_IU], pos[SCAN_IU];
-#pragma unroll
-          for (uint32_t u = 0; u < SCAN_IU; u++) {
-            const uint32_t e = e0 + u * SEG + sl;
-            kid[u] = e < c.z ? (lw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu : 0xFFFFFFFFu;
-            pos[u] = 0;  // entries of s_kid[1..nk] below kid[u]
-          }
-#pragma unroll
-          for (uint32_t step = 64; step; step >>= 1)
-#pragma unroll
-            for (uint32_t u = 0; u < SCAN_IU; u++)
-              if (pos[u] + step <= nk && s_kid[seg][pos[u] + step] < kid[u]) pos[u] += step;
-#pragma unroll
-          for (uint32_t u = 0; u < SCAN_IU; u++) {
-            const uint32_t e = e0 + u * SEG + sl;
-            const bool ok = e < c.z && ((pos[u] + 1 <= nk && s_kid[seg][pos[u] + 1] == kid[u]) || kid[u] == self_kid);
-            const uint64_t mk = sballot(ok);
-            const uint32_t at_ = npos + mbcnt64(mk);
-            if (ok && at_ < SCAN_POS_B) s_pos[seg][at_] = LIST_EXACT | ((c.x & 0xFFu) << 26) | (c.w + e);
-            npos += popc64(mk);
-          }
-        }
-      }
-    }
     // (found context, key ancestor) pairs: ip 0 .. nP - 1 under each; a set bit lists the key. All
     // SCAN_PB loads of a lane's round in flight at once.
     const uint32_t self = pn >> 31, tot = on ? nf * nP : 0u;
@@ -2030,7 +1970,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     auto divp = [&](uint32_t t) { return nP > 1 ? __umulhi(t, inv) : t; };
     // a key-entity index past the image's key entities (a batch encoded for another image): the
     // request enumerates every key instead (exact), and is counted so that the batch fails
-    bool badk = kbad;
+    bool badk = false;
     for (uint32_t rb = 0; __ballot(rb < tot) != 0; rb += SEG * SCAN_PB) {
       uint2 fw[SCAN_PB];
       uint32_t fk[SCAN_PB], fc[SCAN_PB];

@@ -1560,10 +1560,6 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     uint32_t slots = 2;
     while (slots < 2 * ctx.size()) slots <<= 1;
     img.sctx.assign((size_t)slots * SCTX_WORDS, 0);
-    // each row's set bits in kidx order, for the short ones' inline lists (image.h SCTX_INLINE)
-    std::vector<uint32_t> row_n(ctx.size(), 0);
-    for (size_t r = 0; r < ctx.size(); r++)
-      for (size_t w = 0; w < words; w++) row_n[r] += (uint32_t)__builtin_popcount(bitw[r * words + w]);
     std::vector<std::pair<CtxKey, uint32_t>> ctx_sorted(ctx.begin(), ctx.end());
     std::sort(ctx_sorted.begin(), ctx_sorted.end());
     for (auto& c : ctx_sorted) {
@@ -1574,21 +1570,6 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       e[0] = ctx_w0(x[0], x[5]);
       e[1] = x[1]; e[2] = x[2]; e[3] = x[3]; e[4] = x[4]; e[5] = x[6]; e[6] = x[7];
       e[7] = c.second;
-      // the row's set bits inline when they are few (16-bit kidx): the probe brings them along
-      static const bool inl_off = std::getenv("CEDARGPU_NO_CTX_INLINE") != nullptr;  // (A/B)
-      const uint32_t n = row_n[c.second];
-      if (!inl_off && n && n <= SCTX_INLINE && img.key_ents.size() < 65536) {
-        const size_t w0 = (size_t)c.second * words;
-        e[SCTX_N] = n;
-        e[SCTX_BASE] = img.sbits[2 * w0 + 1];
-        uint32_t k = 0;
-        for (size_t w = 0; w < words; w++)
-          for (uint32_t m = img.sbits[2 * (w0 + w)]; m; m &= m - 1) {
-            const uint32_t kid = (uint32_t)(w * 32 + __builtin_ctz(m));
-            e[SCTX_LIST + k / 2] |= kid << (16 * (k & 1));
-            k++;
-          }
-      }
     }
     // the context filter: every context's key (the kernel's lookup hash)
     const uint32_t bw = ctx_bloom_words(slots);
@@ -2325,17 +2306,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
       const uint32_t* e = sctx + k * SCTX_WORDS;
       if (!e[0]) continue;
       used++;
-      if (!(e[0] & SCTX_USED) || e[7] >= rows || e[SCTX_N] > SCTX_INLINE) throw CedarError("corrupt image (scope bitsets)");
-      if (e[SCTX_N]) {  // an inline list: the row's set bits, ascending, at its rank
-        const uint32_t* bw = sbits + 2 * (size_t)e[7] * img->sbits_words;
-        if (e[SCTX_BASE] != bw[1]) throw CedarError("corrupt image (scope bitsets)");
-        uint32_t k = 0;
-        for (uint32_t w = 0; w < img->sbits_words && k <= e[SCTX_N]; w++)
-          for (uint32_t m = bw[2 * w]; m && k <= e[SCTX_N]; m &= m - 1, k++)
-            if (k < e[SCTX_N] && ((e[SCTX_LIST + k / 2] >> (16 * (k & 1))) & 0xFFFFu) != w * 32 + (uint32_t)__builtin_ctz(m))
-              throw CedarError("corrupt image (scope bitsets)");
-        if (k != e[SCTX_N]) throw CedarError("corrupt image (scope bitsets)");
-      }
+      if (!(e[0] & SCTX_USED) || e[7] >= rows) throw CedarError("corrupt image (scope bitsets)");
     }
     if (used >= nc) throw CedarError("corrupt image (scope bitsets)");
     uint32_t rank = 0;

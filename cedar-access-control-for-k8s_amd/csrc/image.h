@@ -210,8 +210,8 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 // holds each set bit's bucket at its rank: (first head, head count) of the key's own scope-index
 // entry, what a probe of that key in btab would return. sctx: an open-addressed table of S slots (S
 // a power of two) at ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1) & (S - 1), SCTX_WORDS
-// each: [SCTX_USED | combo << 16 | hs, at, ai, rt, ri, v0, v1, row, inline list...] (0 = empty; the
-// key's 32 bytes compared whole, the slot one 128-byte line). A request looks up its contexts (per entity-principal combo: level
+// each: [SCTX_USED | combo << 16 | hs, at, ai, rt, ri, v0, v1, row] (0 = empty; 32 bytes, one
+// round trip, compared whole). A request looks up its contexts (per entity-principal combo: level
 // 1, each value slot of l2_vmask with its own value, each element of its list slots in l2_lmask)
 // and tests one bit per principal key ancestor in each context found (the encoder lists their kidx
 // after the ancestor pairs: [n, (type, id) x n, kidx(self), kidx x keys], kidx ~0 for a UID that is
@@ -219,14 +219,7 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 // btab probe. On C3 that is ~8 bucket reads from a ~0.1 MB table per request instead of ~62
 // level-1 probes of 64-byte slots and their level-2 follow-ups; the grouped requests of a wave
 // share the rows. Images whose bitsets would exceed SBITS_MAX_BYTES have none (sbits_words == 0).
-// Inline posting lists: a slot is 32 words (one 128-byte line); words 8.. hold the context's set
-// bits as a list when it is short: [8] n (0: use the bitset row), [9] the rank of the row's first set
-// bit, [10..31] up to SCTX_INLINE kidx as 16-bit halves, ascending (images of < 65,536 key
-// entities). The probe that finds the context brings the list along, so a request intersects it
-// with its own sorted key ancestors in LDS instead of testing one bit row word per ancestor (~6
-// lines of a C3 row per context).
-constexpr uint32_t SCTX_WORDS = 32, SCTX_USED = 0x80000000u, SCTX_L1 = 0xFFFFu, KIDX_NONE = 0xFFFFFFFFu;
-constexpr uint32_t SCTX_N = 8, SCTX_BASE = 9, SCTX_LIST = 10, SCTX_INLINE = 2 * (SCTX_WORDS - SCTX_LIST);
+constexpr uint32_t SCTX_WORDS = 8, SCTX_USED = 0x80000000u, SCTX_L1 = 0xFFFFu, KIDX_NONE = 0xFFFFFFFFu;
 constexpr uint64_t SBITS_MAX_BYTES = 64ull << 20;
 __host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {
   pre ^= pre >> 16;
