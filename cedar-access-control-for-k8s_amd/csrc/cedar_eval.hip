@@ -124,6 +124,7 @@ struct KArgs {
   // one XCD (blocks are dealt round-robin over the 8 XCDs), so neighbours share that XCD's L2;
   // 0: block order (xcd_block)
   uint32_t xcd_chunk;
+  uint32_t park;  // compact candidate pass: head atoms parked in LDS with the descriptor (2 or 4)
 };
 // Block b of nb one-wave blocks -> the wave it runs: block b lands on XCD b % 8 as its (b / 8)-th
 // block; chunks of C consecutive waves go to one XCD, chunks dealt round-robin (a bijection on the
@@ -2500,9 +2501,13 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t* head = a.bstream + (size_t)(CG_DBG == 4 ? 0u : hidx) * HEAD_WORDS;
       const uint4* d4 = reinterpret_cast<const uint4*>(head);
       const uint4 q0 = d4[0], q1 = d4[1], q2 = d4[2], q3 = d4[3];
-      if constexpr (L::ATOMS) {  // the head's atoms, in flight with its descriptor, parked in LDS
-        const uint4 a0 = d4[4], a1 = d4[5], a2 = d4[6], a3 = d4[7];
-        wl.at4[0][lane] = a0; wl.at4[1][lane] = a1; wl.at4[2][lane] = a2; wl.at4[3][lane] = a3;
+      if constexpr (L::ATOMS) {  // the head's first atoms, in flight with its descriptor, parked in LDS
+        const uint4 a0 = d4[4], a1 = d4[5];
+        wl.at4[0][lane] = a0; wl.at4[1][lane] = a1;
+        if (a.park > 2) {
+          const uint4 a2 = d4[6], a3 = d4[7];
+          wl.at4[2][lane] = a2; wl.at4[3][lane] = a3;
+        }
       }
       // the candidate's request (segment s)
       const uint4 x0 = wl.cx[s][0], x1 = wl.cx[s][1], x2 = wl.cx[s][2], x3 = wl.cx[s][3];
@@ -2568,7 +2573,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
         const uint64_t ta0 = STATS ? clock64() : 0;
         bool set_atom = false;
         if (pc < na) {
-          const uint4 at = (L::ATOMS && pc < HEAD_ATOMS) ? wl.at4[L::ATOMS ? pc : 0][lane]
+          const uint4 at = (L::ATOMS && pc < a.park) ? wl.at4[L::ATOMS ? pc : 0][lane]
                                                           : *reinterpret_cast<const uint4*>((pc < HEAD_ATOMS ? head : rec) + POL_WORDS + ATOM_WORDS * pc);
           if (STATS) set_atom = (at.x & 0xFF) == AK_RECSET || (at.x & 0xFF) == AK_CONTAINS;
           const uint32_t rr = eval_atom<false>(tc, rec, at.x & 0xFF, (at.x >> 8) & 0xFF, at.y, at.z, at.w, e);
@@ -4043,6 +4048,8 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   static const bool like_stage = !(std::getenv("CEDARGPU_LIKE_STAGE") && *std::getenv("CEDARGPU_LIKE_STAGE") == '0');
   static const uint32_t xcd_chunk = [] { const char* e = std::getenv("CEDARGPU_XCD_CHUNK"); return e ? (uint32_t)std::atoi(e) : 0u; }();
   k.xcd_chunk = xcd_chunk;
+  static const uint32_t park = [] { const char* e = std::getenv("CEDARGPU_PARK_ATOMS"); return e && std::atoi(e) == 2 ? 2u : 4u; }();
+  k.park = park;
   k.lslot = img.lslot_mask;
   k.like_off = img.like_off;
   k.like_base = (like_stage && img.lslot_mask && img.n_hot + 3u * (uint32_t)__builtin_popcount(img.lslot_mask) <= NHOT) ? img.n_hot : 0xFFFFFFFFu;
