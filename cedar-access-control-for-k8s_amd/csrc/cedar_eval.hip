@@ -4244,6 +4244,8 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
       }
     } else if (k.scan_filt && k.sbits_words) {
       if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6, true>), sg, sb, 0, s, k);
+      else if (socc == 7) hipLaunchKernelGGL((cedar_scan_kernel<8, 7, true>), sg, sb, 0, s, k);
+      else if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8, true>), sg, sb, 0, s, k);
       else hipLaunchKernelGGL((cedar_scan_kernel<8, 1, true>), sg, sb, 0, s, k);
     } else if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8>), sg, sb, 0, s, k);
     else if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6>), sg, sb, 0, s, k);
