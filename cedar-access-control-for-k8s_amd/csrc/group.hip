@@ -21,7 +21,6 @@
 #include <cstdlib>
 
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "image.h"
 
@@ -42,11 +41,59 @@ __global__ __launch_bounds__(256) void cedar_group_gather(const uint32_t* __rest
   for (uint32_t j = sl; j < row_vec; j += GSEG) dst[j] = src[j];
 }
 
+// vals[i] = i, four per lane (vals 16-byte aligned; the tail of the last uint4 past n is scratch)
+__global__ __launch_bounds__(256) void cedar_group_iota(uint4* __restrict__ vals, uint32_t n) {
+  const uint32_t i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i < n) vals[i / 4] = make_uint4(i, i + 1, i + 2, i + 3);
+}
+
 }  // namespace
 
 namespace cg {
 
+// rocPRIM's onesweep configuration for (u32 key, u32 request) pairs. Its gfx950 default sorts
+// 1024 x 16 = 16384 pairs per block: 64 blocks per 1M requests, a quarter of the CUs, each pass
+// latency-bound (~27 us per 8-bit pass, profiles/r04/final2). CEDARGPU_SORT_CFG picks a smaller
+// block (A/B): 1 = 256x16, 2 = 512x8, 3 = 256x8, 4 = 512x16, 5 = 256x12, 6 = 512x8 with a
+// 512x8 histogram, 7 = 1024x4 with a 512x8 histogram (the default: 256 blocks, group 0.086-0.092
+// ms per 1M vs 0.121-0.129 at 0, gpurun_out/r05n, r05o); 0 = rocPRIM's default. (12-bit digits,
+// two places for 24 bits: the histogram kernel needs 192 KB of LDS.)
+template <unsigned B, unsigned I, unsigned HB = 1024, unsigned HI = 16, unsigned BITS = 8>
+using OneSweep = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<HB, HI>, rocprim::kernel_config<B, I>, BITS,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
 using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+
+static int sort_cfg() {
+  static const int c = [] {
+    const char* e = std::getenv("CEDARGPU_SORT_CFG");
+    const int v = e ? std::atoi(e) : 7;
+    return v < 0 || v > 7 ? 7 : v;
+  }();
+  return c;
+}
+
+template <class Cfg>
+hipError_t sort_with(void* temp, size_t& bytes, uint32_t* keys, uint32_t* keys2, const uint32_t* vals, uint32_t* ord,
+                     uint32_t n, uint32_t lo, hipStream_t s) {
+  return rocprim::radix_sort_pairs<Cfg>(temp, bytes, keys, keys2, vals, ord, n, lo, 32, s);
+}
+
+static hipError_t group_sort(void* temp, size_t& bytes, uint32_t* keys, uint32_t* keys2, const uint32_t* vals, uint32_t* ord,
+                             uint32_t n, uint32_t lo, hipStream_t s) {
+  switch (sort_cfg()) {
+    case 1: return sort_with<OneSweep<256, 16>>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+    case 2: return sort_with<OneSweep<512, 8>>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+    case 3: return sort_with<OneSweep<256, 8>>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+    case 4: return sort_with<OneSweep<512, 16>>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+    case 5: return sort_with<OneSweep<256, 12>>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+    case 6: return sort_with<OneSweep<512, 8, 512, 8>>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+    case 7: return sort_with<OneSweep<1024, 4, 512, 8>>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+    default: return sort_with<SortConfig>(temp, bytes, keys, keys2, vals, ord, n, lo, s);
+  }
+}
 
 // key bits sorted, from the top: CEDARGPU_GROUP_BITS (24 by default: three onesweep passes, the
 // (action, resource type) and principal fields; 0.19 vs 0.22 ms per 1M at 32, profiles/r03/ab11)
@@ -70,8 +117,7 @@ bool group_gather() {
 size_t group_temp_bytes(uint32_t n) {
   size_t bytes = 0;
   uint32_t* none = nullptr;
-  if (rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, none, none, rocprim::counting_iterator<uint32_t>(0u), none, n,
-                                            32 - group_bits(), 32) != hipSuccess)
+  if (group_sort(nullptr, bytes, none, none, none, none, n, 32 - group_bits(), nullptr) != hipSuccess)
     return 0;
   return bytes;
 }
@@ -82,10 +128,12 @@ int group_enqueue(const uint32_t* keys, const uint32_t* rows, uint32_t n, uint32
                   uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (row_words % 4) return -1;
-  (void)vals;  // (the request indices come from a counting iterator: no iota pass)
+  // The request indices are written out (one pass over n words) rather than read from a counting
+  // iterator: rocPRIM copies a counting iterator and the keys into its buffers (two passes) before
+  // an odd number of digit places.
+  hipLaunchKernelGGL(cedar_group_iota, dim3((n + 1023) / 1024), dim3(256), 0, s, reinterpret_cast<uint4*>(vals), n);
   size_t bytes = temp_bytes;
-  if (rocprim::radix_sort_pairs<SortConfig>(temp, bytes, const_cast<uint32_t*>(keys), keys2, rocprim::counting_iterator<uint32_t>(0u), ord,
-                                            n, 32 - group_bits(), 32, s) != hipSuccess)
+  if (group_sort(temp, bytes, const_cast<uint32_t*>(keys), keys2, vals, ord, n, 32 - group_bits(), s) != hipSuccess)
     return -1;
   if (!group_gather()) return hipGetLastError() == hipSuccess ? 0 : -1;
   hipLaunchKernelGGL(cedar_group_gather, dim3((n + 256 / GSEG - 1) / (256 / GSEG)), dim3(256), 0, s, ord, n,
