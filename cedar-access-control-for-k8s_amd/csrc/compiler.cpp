@@ -455,8 +455,12 @@ struct Compiler {
       case EK::Like: {
         if ((h = hot_of(*e->kids[0])) < 0 || e->kids[0]->k != EK::Attr) return false;
         // one star at most and literals within 8 bytes: inline (AK_LIKEI), nothing to read but the
-        // row's like words (CEDARGPU_NO_LIKEI: the record form everywhere, A/B)
+        // value's first and last 8 bytes (CEDARGPU_NO_LIKEI: the record form everywhere, A/B).
+        // CEDARGPU_LIKE_WORDS=1 also ships those bytes in the row (6 words per like slot, image.h
+        // LIKE_WORDS): neutral on the step in the round-5 A/B, and 48 B more per C3
+        // request to upload, so off by default.
         static const bool no_likei = std::getenv("CEDARGPU_NO_LIKEI") != nullptr;
+        static const bool like_words = [] { const char* v = std::getenv("CEDARGPU_LIKE_WORDS"); return v && *v == '1'; }();
         std::string pre, suf;
         bool star = false, inl = !no_likei;
         for (auto& pc : e->pat) {
@@ -474,7 +478,7 @@ struct Compiler {
           w[1] = (uint32_t)b;
           w[2] = (uint32_t)(b >> 32);
           w[3] = (uint32_t)pre.size() | ((uint32_t)suf.size() << 4) | (star ? 1u << 8 : 0u);
-          I.lslot_mask |= 1u << h;
+          if (like_words) I.lslot_mask |= 1u << h;
           return put(AK_LIKEI, (uint32_t)h);
         }
         w[1] = pattern_into(e->pat, adata);

@@ -213,8 +213,9 @@ struct Scratch {
   std::vector<std::vector<uint64_t>> parents;
   std::unordered_set<uint64_t> seen_p, seen_big;
   std::vector<uint64_t> anc, nodes, cl, sp, extended;
+  std::vector<uint32_t> attrs;  // a table entity's attributes emitted for the static comparison
   void reset() {
-    table.clear(); n_key.clear(); hs.clear();
+    table.clear(); n_key.clear(); hs.clear(); attrs.clear();
     index.keys.clear(); index.map.clear();
     for (auto& p : parents) p.clear();
     seen_p.clear(); seen_big.clear();
@@ -224,6 +225,31 @@ struct Scratch {
 inline Scratch& scratch() {
   thread_local Scratch s;
   return s;
+}
+
+// CEDARGPU_STATIC_ELIDE=0 keeps every request entity in the table (A/B, tests)
+inline bool static_elide_on() {
+  static const bool on = [] { const char* e = std::getenv("CEDARGPU_STATIC_ELIDE"); return !(e && *e == '0'); }();
+  return on;
+}
+
+// a request entity's attributes (record w0, w1 emitted into `m`) equal a static entity's (record
+// sw0, sw1 in the constant pool) field for field, every field an inline primitive (bool, string,
+// small long, entity UID): equal words are then equal values
+inline bool static_attrs_equal(const Image& img, uint32_t sw0, uint32_t sw1, const std::vector<uint32_t>& m, uint32_t w0,
+                               uint32_t w1) {
+  if ((sw0 >> TAG_SHIFT) != T_REC || (w0 >> TAG_SHIFT) != T_REC || sw1 != w1) return false;
+  if (((sw0 & X_MASK) >> SPACE_SHIFT) != SP_CPOOL || ((w0 & X_MASK) >> SPACE_SHIFT) != SP_HEAP) return false;
+  const uint32_t so = sw0 & OFF_MASK, ro = w0 & OFF_MASK;
+  if ((size_t)so + 1 + 3 * (size_t)sw1 > img.cpool.size() || (size_t)ro + 1 + 3 * (size_t)w1 > m.size()) return false;
+  for (uint32_t j = 0; j < w1; j++) {
+    const uint32_t* a = &img.cpool[so + 1 + 3 * j];
+    const uint32_t* b = &m[ro + 1 + 3 * j];
+    const uint32_t tag = a[1] >> TAG_SHIFT;
+    if (tag != T_BOOL && tag != T_STR && tag != T_LONG && tag != T_ENT) return false;
+    if (a[0] != b[0] || a[1] != b[1] || a[2] != b[2]) return false;
+  }
+  return true;
 }
 
 inline void emit_empty_record(std::vector<uint32_t>& out, uint32_t& w0, uint32_t& w1) {
@@ -318,9 +344,45 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       for (const uint64_t p : sp) add_parent(parents[i], p);
     }
   }
+  const auto pu = uid_of(src.principal()), au = uid_of(src.action()), ru = uid_of(src.resource());
+  // A table entity that merges to exactly its static entity (no parents of its own, attributes equal
+  // to the static ones field for field) leaves the table: lookups of its UID then find the static
+  // row, whose attributes and closure row are what the merge would give. (The SAR path's group
+  // entities, {name} with no parents, over a static group hierarchy: ~140 B per request.) P / A / R
+  // stay, and only records of inline primitives are compared.
+  if (has_static && static_elide_on()) {
+    const uint64_t pk = uid_key(pu.first, pu.second), ak = uid_key(au.first, au.second), rk = uid_key(ru.first, ru.second);
+    uint32_t kept = 0;
+    bool dropped = false;
+    for (uint32_t i = 0; i < (uint32_t)table.size(); i++) {
+      const uint64_t k = index.keys[i];
+      bool elide = false;
+      if (!(table[i] & FROM_STATIC) && k != pk && k != ak && k != rk && src.n_parents(table[i]) == 0) {
+        const int32_t s = img.static_row(k);
+        if (s >= 0) {
+          const uint32_t* sr = &img.srows[(size_t)s * ENT_WORDS];
+          S.attrs.clear();
+          uint32_t w0, w1;
+          src.emit_attrs(table[i], S.attrs, img, E, w0, w1);
+          elide = static_attrs_equal(img, sr[ER_ATTR0], sr[ER_ATTR1], S.attrs, w0, w1);
+        }
+      }
+      if (elide) { dropped = true; continue; }
+      table[kept] = table[i];
+      index.keys[kept] = k;
+      std::swap(parents[kept], parents[i]);
+      kept++;
+    }
+    if (dropped) {
+      table.resize(kept);
+      index.keys.resize(kept);
+      index.map.clear();
+      if (kept > 32)
+        for (uint32_t i = 0; i < kept; i++) index.map.emplace(index.keys[i], i);
+    }
+  }
   const uint32_t n = (uint32_t)table.size();
   blk.resize(RH_WORDS + (size_t)n * ENT_WORDS, 0);
-  const auto pu = uid_of(src.principal()), au = uid_of(src.action()), ru = uid_of(src.resource());
   for (auto* u : {&pu, &au, &ru})
     if (u->first > X_MASK) throw CedarError("string table overflow");
   blk[RH_NENT] = n;
@@ -406,7 +468,11 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       return true;
     }
     const std::vector<uint64_t>& ps = parents[i];
-    uint64_t h = uid * 0x9E3779B97F4A7C15ull;
+    // The record names its owner only as a key entity (make_record: key_index), so an owner that is
+    // none caches under its parents alone: users with one group set share a record (and a user's
+    // UID string, request-local, never splits the cache).
+    const uint64_t cu = img.is_key_ent(uid) ? uid : ~0ull;
+    uint64_t h = cu * 0x9E3779B97F4A7C15ull;
     for (const uint64_t p : ps) {
       const int32_t at = index.find(p);
       if (at >= 0 && req_parents((uint32_t)at)) return false;  // a request edge above a request edge
@@ -417,7 +483,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     {
       std::lock_guard<std::mutex> g(sh.mu);
       auto it = sh.map.find(h);
-      if (it != sh.map.end() && it->second.uid == uid && it->second.parents == ps) {
+      if (it != sh.map.end() && it->second.uid == cu && it->second.parents == ps) {
         n_key[i] = it->second.rec.keys;
         blk[RH_WORDS + (size_t)i * ENT_WORDS + ER_ANC] = put_words(it->second.rec);
         return true;
@@ -432,7 +498,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     std::sort(anc.begin(), anc.end());
     anc.erase(std::unique(anc.begin(), anc.end()), anc.end());
     EncCache::Ent e;
-    e.uid = uid;
+    e.uid = cu;
     e.parents = ps;
     e.rec.keys = make_record(img, uid, anc, e.rec.words);
     e.rec.hash = list_hash(e.rec.words.data(), (uint32_t)e.rec.words.size());
@@ -641,7 +707,11 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     for (uint32_t j = 0; j < nk; j++) g += mix(mix(0x2545F491u, pl[2 * j]), pl[2 * j + 1]);
     g = mix(g, 0x7FEB352Du);
     uint32_t hv = 0x6C8E9CF5u;
-    for (uint32_t j = 0; j < 2 * nh; j++) hv = mix(hv, row[RW_HDR + j]);
+    // (a request-local string, in no image key, mixes as one value: its id is a table position)
+    for (uint32_t j = 0; j < nh; j++) {
+      const uint32_t w0 = row[RW_HDR + 2 * j], w1 = row[RW_HDR + 2 * j + 1];
+      hv = mix(mix(hv, w0), (w0 >> TAG_SHIFT) == T_STR && w1 >= img.n_gstr() ? img.n_gstr() : w1);
+    }
     E.gkey = (ar & 0xFF000000u) | ((g >> 16) << 8) | (hv >> 24);
   }
 }

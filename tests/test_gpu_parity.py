@@ -631,6 +631,53 @@ def test_static_dag_handmade(ctx):
     check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
 
 
+def test_static_entities_request_copies(ctx):
+    """Request entities that repeat a static entity: an exact copy (attributes equal, no parents
+    of its own: the encoder leaves it out of the request's table, encode_impl.h), and copies that
+    differ (another attribute value, an extra or a missing attribute, a parent of its own, a
+    non-primitive attribute), which override or extend the static one. Policies read the groups'
+    attributes through an entity-valued principal attribute and test membership."""
+    G = lambda g: {"type": "k8s::Group", "id": g}
+    ents = [{"uid": G("g1"), "attrs": {"name": "g1", "level": 1}, "parents": [G("top")]},
+            {"uid": G("g2"), "attrs": {"name": "g2"}, "parents": [G("top")]},
+            {"uid": G("top"), "attrs": {"name": "top"}, "parents": []},
+            {"uid": G("side"), "attrs": {}, "parents": []}]
+    pols = [
+        'permit (principal, action == k8s::Action::"get", resource) when { principal.team.name == "g1" };',
+        'permit (principal, action == k8s::Action::"list", resource) when { principal.team has level && principal.team.level == 1 };',
+        'forbid (principal, action == k8s::Action::"list", resource) when { principal.team.name == "renamed" };',
+        'permit (principal in k8s::Group::"top", action == k8s::Action::"watch", resource);',
+        'permit (principal in k8s::Group::"side", action == k8s::Action::"delete", resource);',
+        'permit (principal, action == k8s::Action::"patch", resource) when { principal.team has tags && principal.team.tags.contains("a") };',
+    ]
+    stores = [cedargpu.MemoryStore("c.cedar", "\n".join(pols))]
+    copies = [
+        None,
+        {"uid": G("g1"), "attrs": {"name": "g1", "level": 1}, "parents": []},  # exact copy
+        {"uid": G("g2"), "attrs": {"name": "g2"}, "parents": []},  # exact copy
+        {"uid": G("g1"), "attrs": {"name": "renamed", "level": 1}, "parents": []},
+        {"uid": G("g1"), "attrs": {"name": "g1"}, "parents": []},  # a missing attribute
+        {"uid": G("g2"), "attrs": {"name": "g2", "level": 1}, "parents": []},  # an extra one
+        {"uid": G("g2"), "attrs": {"name": "g2"}, "parents": [G("side")]},  # a parent of its own
+        {"uid": G("g1"), "attrs": {"name": "g1", "level": 1, "tags": ["a", "b"]}, "parents": []},
+        {"uid": G("top"), "attrs": {"name": "top"}, "parents": []},
+        {"uid": G("side"), "attrs": {}, "parents": []},
+    ]
+    items = []
+    for k, cp in enumerate(copies):
+        for team in ("g1", "g2"):
+            for member in (None, team):
+                for verb in ("get", "list", "watch", "delete", "patch"):
+                    user = {"uid": {"type": "k8s::User", "id": f"u{k}"}, "attrs": {"name": f"u{k}", "team": {"__entity": G(team)}},
+                            "parents": [G(member)] if member else []}
+                    ej = [user] + ([cp] if cp else [])
+                    req = {"principal": user["uid"], "action": {"type": "k8s::Action", "id": verb},
+                           "resource": {"type": "k8s::Resource", "id": "r"}, "context": {}}
+                    items.append((ej, req))
+    check_items(ctx, stores, items, entities=ents)
+    check_items_ref(ctx, stores, items, entities=ents)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_static_entities_random_general(ctx, seed):
     """Random general policies (policy-stream kernel, bytecode) with an image-level static

@@ -29,10 +29,10 @@ for step in "$@"; do
       [ ${#LEGS[@]} -eq 0 ] && LEGS=("")
       k=0
       for leg in "${LEGS[@]}" "${LEGS[@]}"; do
-        env $leg timeout -k 10 300 python -u bench.py --no-cpu-baseline --latency-batches 0 --serve-threads 0 --no-reload --configs-requests 0 --no-submit-to-results ${BENCH_ARGS} > $O/quick_$k.json 2> $O/quick_$k.err || { echo "bench failed ($leg)"; tail -20 $O/quick_$k.err; exit 1; }
+        env $leg timeout -k 10 300 python -u bench.py --no-cpu-baseline --latency-batches 0 --serve-threads 0 --no-reload --configs-requests 0 ${QUICK_S2R:---no-submit-to-results} ${BENCH_ARGS} > $O/quick_$k.json 2> $O/quick_$k.err || { echo "bench failed ($leg)"; tail -20 $O/quick_$k.err; exit 1; }
         python3 -c "
 import json; d=json.load(open('$O/quick_$k.json')); p=d['roofline'].get('phases_ms',{})
-print('[$leg]', round(d['value']/1e6,1), 'M/s ms', round(d['ms_per_step'],4), 'phases', {a: round(b,4) for a,b in p.items()}, 'parity', d['parity_sample'])"
+s=d.get('submit_to_results_1m') or {}; print('[$leg]', round(d['value']/1e6,1), 'M/s ms', round(d['ms_per_step'],4), 'phases', {a: round(b,4) for a,b in p.items()}, 'parity', d['parity_sample']['mismatches'], 's2r', s and (round(s['submit_to_results_ms'],1), 'ms', round(s['h2d_bytes']/s['requests']), 'B/req h2d', 'enc', round(s['encode_s'],3), 's', s.get('split_ms')))"
         k=$((k+1))
       done ;;
     bench)
