@@ -410,7 +410,7 @@ def main():
     ap.add_argument("--serve-max-batch", type=int, default=8192)
     ap.add_argument("--no-submit-to-results", dest="submit_to_results", action="store_false",
                     help="skip the 1M-request submit -> results measurement after the timed region")
-    ap.add_argument("--configs-requests", type=int, default=32_768,
+    ap.add_argument("--configs-requests", type=int, default=262_144,
                     help="requests per secondary config (C2, C4) after the timed region (0: skip)")
     args = ap.parse_args()
 

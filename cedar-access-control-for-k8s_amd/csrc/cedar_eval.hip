@@ -125,6 +125,7 @@ struct KArgs {
   // 0: block order (xcd_block)
   uint32_t xcd_chunk;
   uint32_t park;  // compact candidate pass: head atoms parked in LDS with the descriptor (2 or 4)
+  uint32_t cls;   // candidate pass: a duplicate class's hit takes one slot, reported as RS_CLASS
 };
 // Block b of nb one-wave blocks -> the wave it runs: block b lands on XCD b % 8 as its (b / 8)-th
 // block; chunks of C consecutive waves go to one XCD, chunks dealt round-robin (a bijection on the
@@ -1730,6 +1731,7 @@ constexpr uint32_t CTX_CAP = 16, LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;
 constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the rest read from the row)
 constexpr uint32_t SCAN_PB = 8;    // bit tests per lane per round (loads in flight)
 constexpr uint32_t MEMB_U = 4;     // duplicate-class members a lane copies per round (loads in flight)
+constexpr uint32_t HM_CLASS = 1u << 24;  // hit-slot word (wl.hm): the slot holds a whole duplicate class
 constexpr uint32_t RANK_POL = 16384;  // the large stage's rank pass: policy indices its bitmap covers
 // SLIM hit words: policy index (< RANK_POL) | kind << 14 | tier << 16 | error slot << 24
 constexpr uint32_t SLIM_KIND = 14, SLIM_TIER = 16, SLIM_SLOT = 24, SLIM_POL = 0x3FFFu;
@@ -2591,17 +2593,20 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       }
       const bool hit = ok && (err || pc == AT_SAT);
       const uint32_t mlist = q2.w;
-      const uint32_t nmem = hit ? (mlist ? ((q3.x >> 16) != 0xFFFFu ? (q3.x >> 16) : a.bstream[mlist]) : 1u) : 0u;  // (head word 12: the class size)
+      // a duplicate class that holds (no error) takes one slot under its representative, which the
+      // merge reports as an RS_CLASS reason; one that errs records every member with the error
+      const bool whole = a.cls && mlist && !err;
+      const uint32_t nmem = hit ? ((mlist && !whole) ? ((q3.x >> 16) != 0xFFFFu ? (q3.x >> 16) : a.bstream[mlist]) : 1u) : 0u;  // (head word 12: the class size)
       if (STATS) st[9] += nmem;
       const uint32_t pos0 = hit ? atomicAdd(&wl.sst[s][0], CG_DBG == 2 ? 1u : nmem) : 0u;
       const uint32_t xpos = (hit && err) ? atomicAdd(&wl.sst[s][1], 1u) : 0u;
       const uint32_t kind = err ? 2u : (flags & PF_FORBID) ? 1u : 0u;
-      const uint32_t hmv = kind | (tier << 8) | (min(xpos, 0xFFu) << 16);
-      if (hit && !mlist && pos0 < L::HC) {
+      const uint32_t hmv = kind | (tier << 8) | (min(xpos, 0xFFu) << 16) | (whole ? HM_CLASS : 0u);
+      if (hit && (!mlist || whole) && pos0 < L::HC) {
         wl.hp[s][pos0] = q2.z;
         wl.hm[s][pos0] = hmv;
       }
-      if (CG_DBG != 2 && hit && mlist) {  // a duplicate class: every member, MEMB_U loads in flight
+      if (CG_DBG != 2 && hit && mlist && !whole) {  // a duplicate class: every member, MEMB_U loads in flight
         for (uint32_t j = 0; j < nmem && pos0 + j < L::HC; j += MEMB_U) {
           uint32_t v[MEMB_U];
 #pragma unroll
@@ -3021,8 +3026,9 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       const uint32_t kind = mj & 0xFF;
       const uint64_t bf = sballot(el && kind == 1), bp = sballot(el && kind == 0), be = sballot(el && kind == 2);
       const uint32_t rf = nf + mbcnt64(bf), rp = np + mbcnt64(bp), re = nerr + mbcnt64(be);
-      if (el && deny && kind == 1 && rf < rcap) __builtin_nontemporal_store(pj, rdst + rf);
-      if (el && !deny && kind == 0 && rp < rcap) __builtin_nontemporal_store(pj, rdst + rp);
+      const uint32_t pw = pj | ((mj & HM_CLASS) ? RS_CLASS : 0u);
+      if (el && deny && kind == 1 && rf < rcap) __builtin_nontemporal_store(pw, rdst + rf);
+      if (el && !deny && kind == 0 && rp < rcap) __builtin_nontemporal_store(pw, rdst + rp);
       if (el && kind == 2 && re < ecap) {
         const uint32_t xs = mj >> 16;
         uint32_t* er = edst + (size_t)re * ERR_WORDS;
@@ -3150,6 +3156,7 @@ static void image_fields(const Image& img, int device, void* base, uint64_t orig
   d.cslot_mask = img.list_mask();
   d.lslot_mask = img.lslot_mask;
   d.like_off = img.like_off();
+  d.cls_compact = img.cls_off.empty() ? 0u : 1u;
   d.smask = (uint32_t)(img.shash.size() / SH_WORDS) - 1;
   d.bmask = img.btab_slots - 1;
   d.fmask = (uint32_t)(img.dev_len[DS_BFILT] / 8) - 1;
@@ -4050,6 +4057,9 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.xcd_chunk = xcd_chunk;
   static const uint32_t park = [] { const char* e = std::getenv("CEDARGPU_PARK_ATOMS"); return e && std::atoi(e) == 2 ? 2u : 4u; }();
   k.park = park;
+  // CEDARGPU_CLASS_SLOTS=0: every member of a duplicate class takes a hit slot (A/B)
+  static const bool cls_slots = !(std::getenv("CEDARGPU_CLASS_SLOTS") && *std::getenv("CEDARGPU_CLASS_SLOTS") == '0');
+  k.cls = cls_slots && img.cls_compact ? 1u : 0u;
   k.lslot = img.lslot_mask;
   k.like_off = img.like_off;
   k.like_base = (like_stage && img.lslot_mask && img.n_hot + 3u * (uint32_t)__builtin_popcount(img.lslot_mask) <= NHOT) ? img.n_hot : 0xFFFFFFFFu;

@@ -1205,6 +1205,12 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     std::vector<uint32_t> fill(moff.begin(), moff.end() - 1);
     for (uint32_t q = 0; q < n; q++) mflat[fill[rep[q]]++] = q;  // ascending per class
   }
+  img.cls_off.clear();
+  img.cls_mem.clear();
+  if (std::any_of(mcnt.begin(), mcnt.end(), [](uint32_t c) { return c > 1; })) {
+    img.cls_off = moff;
+    img.cls_mem = mflat;
+  }
   mark("classes");
   constexpr uint32_t NO_POLICY = 0xFFFFFFFFu;  // a level-1 entry that only carries level-2 keys
   std::vector<std::pair<L1, uint32_t>> r1;
@@ -2186,6 +2192,7 @@ void Image::write_blob(void* wp) const {
   }
   w.u32((uint32_t)ext_msgs.size());
   for (auto& s : ext_msgs) w.str(s);
+  w.vec(cls_off); w.vec(cls_mem);
 }
 
 std::vector<uint8_t> Image::serialize() const {
@@ -2349,6 +2356,16 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   uint32_t ne = r.u32();
   for (uint32_t i = 0; i < ne; i++) img->ext_msgs.push_back(r.str());
   if (img->pol.size() != (size_t)img->meta.size() * POL_WORDS) throw CedarError("corrupt image");
+  img->cls_off = r.vec(); img->cls_mem = r.vec();
+  {  // every policy in at most one class, the offsets ascending
+    const size_t np = img->meta.size();
+    bool ok = img->cls_off.empty() ? img->cls_mem.empty()
+                                   : img->cls_off.size() == np + 1 && img->cls_off[0] == 0 && img->cls_off[np] == img->cls_mem.size() &&
+                                         img->cls_mem.size() <= np;
+    for (size_t q = 0; ok && q < np && !img->cls_off.empty(); q++) ok = img->cls_off[q] <= img->cls_off[q + 1];
+    for (size_t k = 0; ok && k < img->cls_mem.size(); k++) ok = img->cls_mem[k] < np;
+    if (!ok) throw CedarError("corrupt image (duplicate classes)");
+  }
   img->build_lookup();
   return img;
 }

@@ -36,6 +36,7 @@ struct DevImage {
   uint32_t lane_need = 0;  // lane-scratch words per request (> LANE_WORDS: the GLANE stream kernel)
   uint32_t cslot_mask = 0;  // rows carry element-hash / prefix-hash lists (Image::list_mask, image.h)
   uint32_t lslot_mask = 0, like_off = 0;  // like slots (Image::lslot_mask) and their row offset
+  uint32_t cls_compact = 0;  // the host lists duplicate classes (Image::cls_off): one hit slot per class
   uint32_t n_pol = 0, n_tiers = 0, n_gstr = 0, n_hot = 0, n_act = 0, amask_ok = 0, has_bytecode = 1, indexed = 0, bmask = 0, fmask = 0, combo_mask = 0;
   size_t bytes = 0;
 };

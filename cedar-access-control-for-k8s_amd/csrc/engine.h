@@ -122,6 +122,11 @@ struct Image {
   // open-addressed table of btab_slots slots (image.h "scope index") is built on the device from
   // them at load (cedar_btab_build), so blobs and reload broadcasts carry no empty slots.
   std::vector<uint32_t> btab, bfilt, bstream;  // bfilt: key filter, 2 words per block
+  // duplicate classes (host side, image.h "duplicate classes"): the members of the class whose
+  // representative (lowest member) is policy p are cls_mem[cls_off[p] .. cls_off[p + 1]), ascending;
+  // both empty when no two policies share a record. The first pass may report a class by its
+  // representative (a reason word with RS_CLASS set), which Batch::reason_ids expands.
+  std::vector<uint32_t> cls_off, cls_mem;
   uint32_t btab_slots = 1;
   uint32_t indexed = 0;
   uint32_t combo_mask = 0;  // level-1 key combos in use (bit key_combo(..))

@@ -446,6 +446,10 @@ enum Decision : uint32_t { DEC_DENY = 0, DEC_ALLOW = 1 };
 // comparison, or hits beyond even the large re-run stage); the host re-runs it on the stream
 // kernel. RF_BIG: more hits than the probe kernel stages per request; re-run on its large variant.
 enum ResFlags : uint32_t { RF_FORBID = 1, RF_OVERFLOW = 2, RF_VALID = 4, RF_GENERAL = 8, RF_BIG = 16 };
+// A reason word with RS_CLASS set names a whole duplicate class by its representative (the first
+// pass records a class hit in one slot; the host lists the members, Image::cls_off / cls_mem), so a
+// request whose hits are one 150-member class fits the first pass. n_reasons counts words.
+constexpr uint32_t RS_CLASS = 0x80000000u;
 // error record: policy, code | aux << 8, k (string id), et (string id), ei (string id), pad
 constexpr uint32_t ERR_WORDS = 6;
 enum ErrCode : uint32_t {
@@ -468,7 +472,7 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 14;
+constexpr uint32_t IMG_VERSION = 15;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob

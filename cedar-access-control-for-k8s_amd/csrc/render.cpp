@@ -7,6 +7,8 @@
 //    "errors":[{"policy":ID,"position":{...},"message":M}]}
 // Reasons/errors are listed in policy insertion order (canonical order; cedar-go's own order
 // comes from Go map iteration and is not defined).
+#include <algorithm>
+
 #include "engine.h"
 
 namespace cg {
@@ -19,11 +21,26 @@ void Batch::reason_ids(uint32_t i, std::vector<uint32_t>& out) const {
   uint32_t n = res[2 * (size_t)i + 1] & 0xFFFF;
   if (const BigRef* b = big_of(i)) {
     out.assign(b->r, b->r + b->nr);
-    return;
+  } else {
+    uint32_t flags = res[2 * (size_t)i] >> 16;
+    const uint32_t* src = (flags & RF_FORBID) ? reasons_f : reasons_p;
+    for (uint32_t k = 0; k < n && k < capr; k++) out.push_back(src[(size_t)i * capr + k]);
   }
-  uint32_t flags = res[2 * (size_t)i] >> 16;
-  const uint32_t* src = (flags & RF_FORBID) ? reasons_f : reasons_p;
-  for (uint32_t k = 0; k < n && k < capr; k++) out.push_back(src[(size_t)i * capr + k]);
+  // duplicate classes reported by their representative: every member, then policy order again
+  // (the classes and the single policies are disjoint, so the list stays duplicate-free)
+  bool cls = false;
+  for (const uint32_t r : out) cls |= (r & RS_CLASS) != 0;
+  if (!cls) return;
+  const size_t n0 = out.size();
+  for (size_t k = 0; k < n0; k++) {
+    const uint32_t r = out[k];
+    if (!(r & RS_CLASS)) continue;
+    const uint32_t p = r & ~RS_CLASS;
+    if (img->cls_off.empty() || p + 1 >= img->cls_off.size()) throw CedarError("reason names an unknown duplicate class");
+    out[k] = img->cls_mem[img->cls_off[p]];
+    out.insert(out.end(), img->cls_mem.begin() + img->cls_off[p] + 1, img->cls_mem.begin() + img->cls_off[p + 1]);
+  }
+  std::sort(out.begin(), out.end());
 }
 
 void Batch::set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words) {

@@ -326,7 +326,9 @@ def test_followup_sized_by_previous_batch(ctx, monkeypatch):
     them on the device and re-runs the rest from the host; the next batch on that image sizes its
     follow-up by the share the first one saw, so it re-runs none. Both agree with the oracle."""
     monkeypatch.setenv("CEDARGPU_SMALL_N", "0")  # the split first pass: the on-device follow-up is its part
-    pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 2}", action, resource);' for i in range(200))
+    # (distinct records: a duplicate class would take one hit slot, image.h RS_CLASS)
+    pols = "\n".join(f'permit (principal in k8s::Group::"g{i % 2}", action, resource) unless {{ resource == k8s::Resource::"none{i}" }};'
+                     for i in range(200))
     stores = [cedargpu.MemoryStore("hits.cedar", pols)]
     img = cedargpu.build_image(stores, epoch=951)
     ctx.load(img, 951)
