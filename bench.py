@@ -614,7 +614,7 @@ def main():
         dom = max((k for k in phases if k != "total"), key=phases.get) if len(phases) > 1 else "total"
         dom_ms = phases.get(dom, avg_kernel_ms)
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-        dom_kernel = {"scan": "cedar_scan_kernel<8, 6, true>", "candidates": "cedar_probe_kernel<8, 64, 4, SPLIT> (pooled)",
+        dom_kernel = {"scan": "cedar_scan_kernel<8, 6, true>", "candidates": "cedar_probe_kernel<8, 32, 4, SPLIT, HOTC 16> (pooled, compact)",
                       "fu_big": "cedar_probe_kernel<64, 1024, 4, SPLIT, SLIM>", "group": "rocPRIM onesweep"}.get(dom, dom)
         traffic, pmc_kernels = None, None
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -630,7 +630,7 @@ def main():
         # VALU busy fraction of the dominant kernel (SURVEY §8(d) honesty note): a wave64 VALU
         # instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md), 1,024 SIMDs at 2.4 GHz
         valu = None
-        prefix = {"scan": "cedar_scan_kernel<8u, 6u, true", "candidates": "cedar_probe_kernel<8u, 64u"}.get(dom)
+        prefix = {"scan": "cedar_scan_kernel<8u, 6u, true", "candidates": "cedar_probe_kernel<8u, 32u"}.get(dom)
         if pmc_kernels and prefix:
             for name, c in pmc_kernels.items():
                 if name.startswith(prefix) and "SQ_INSTS_VALU" in c:

@@ -16,6 +16,10 @@
 // gpurun_out/r04gab; CEDARGPU_GROUP_GATHER=1 brings it back.)
 // A bucket sort with one atomic per request into 2^20-2^22 counters was 3-5x slower: popular
 // principals' identical keys serialize their atomics (0.52-1.34 ms per 1M, profiles/r03/ab6).
+// Ordering only within tiles of 4-16k requests (one block-local LDS radix sort per tile, one
+// launch: 0.027-0.058 ms) made the scan 0.11 ms slower: equal keys must meet across the whole
+// batch (round 5, profiles/r05/ab/r05v). 24 key bits stay best: 16 bits sort in 0.061 ms but the
+// scan loses 0.036 ms, 32 bits cost 0.022 ms more sort for a 0.014 ms slower scan (r05w).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>

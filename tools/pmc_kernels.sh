@@ -18,7 +18,7 @@ run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAV
 run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE && \
 run fetch FETCH_SIZE && \
 run write WRITE_SIZE && \
-for K in cedar_scan_kernel "cedar_probe_kernel<8u, 64u" "cedar_probe_kernel<64u, 1024u"; do
+for K in cedar_scan_kernel "cedar_probe_kernel<8u, 32u" "cedar_probe_kernel<64u, 1024u"; do
   echo "== $K"; PMC_KERNEL="$K" python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $OUT
 done > $OUT/summary.txt && cat $OUT/summary.txt && \
 python3 $GRAFT_REPO_ROOT/tools/pmc_step.py $OUT 10000 1048576 dag > $OUT/step.json && python3 -c "import json; d=json.load(open('$OUT/step.json')); print('step HBM bytes', d.get('hbm_bytes_per_launch'), 'steps', d.get('steps_fetch'))"
