@@ -691,7 +691,9 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   }
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
   // grouping key: 8 bits of (action, resource type) | 16 of the principal's type and key ancestors |
-  // 8 of its hot values (group.hip sorts on them)
+  // 8 of its hot values (group.hip sorts on the top 24). Round-5 A/B of the field order
+  // (profiles/r05/ab/r05x): hot values before the principal, 0.52-0.54 ms of scan for 0.45;
+  // the principal first, 0.51 ms and a 0.04 ms slower candidate pass.
   {
     auto mix = [](uint32_t h, uint32_t x) {
       h ^= x;
