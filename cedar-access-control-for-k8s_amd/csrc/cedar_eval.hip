@@ -1729,6 +1729,8 @@ constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
 // the flag of a listed key the bitsets found (image.h "scope bitsets")
 constexpr uint32_t CTX_CAP = 16, LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;
 constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the rest read from the row)
+constexpr uint32_t SCAN_ROW = 56;  // scan LDS row words (64 - 8: see s_kid; the LDS stays under 1/24 of a CU for 6 waves per SIMD)
+static_assert(SCAN_ANC + 2 <= SCAN_ROW && SCAN_POS_B + 2 <= SCAN_ROW, "scan LDS rows");
 constexpr uint32_t SCAN_PB = 8;    // bit tests per lane per round (loads in flight)
 constexpr uint32_t MEMB_U = 4;     // duplicate-class members a lane copies per round (loads in flight)
 constexpr uint32_t HM_CLASS = 1u << 24;  // hit-slot word (wl.hm): the slot holds a whole duplicate class
@@ -1769,12 +1771,16 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   __shared__ uint2 s_anc[BITS ? 1 : 64 / SEG][ANC_ST + 1];
   __shared__ uint2 s_hot[64 / SEG][SCAN_HOT + 1];  // the first SCAN_HOT hot values
   // BITS: the key-entity index of the principal ([0]) and of each staged key ancestor ([j]: j - 1),
-  // the request's contexts (combo | hs << 8, v0, v1, bitset row) and its listed keys
+  // the request's contexts (combo | hs << 8, bitset row) and its listed keys
   // (LIST_EXACT | combo << 26 | the bit's rank in svals, or combo << 11 for a type / wildcard
   // principal combo's single key)
-  __shared__ uint32_t s_kid[BITS ? 64 / SEG : 1][SCAN_ANC + 2];
-  __shared__ uint4 s_cx[BITS ? 64 / SEG : 1][CTX_CAP];
-  __shared__ uint32_t s_pos[BITS ? 64 / SEG : 1][SCAN_POS_B + 2];
+  // (rows of SCAN_ROW words: the 8 lanes of each of the 8 segments read consecutive entries at
+  // once, so rows 8 banks apart (56 words) take all 64 banks without a conflict)
+  __shared__ uint32_t s_kid[BITS ? 64 / SEG : 1][SCAN_ROW];
+  // (found contexts: combo and bitset row; 8-byte entries, rows padded off a multiple of the 64
+  // banks: the wave's segments read the same context index in lockstep)
+  __shared__ uint2 s_cx[BITS ? 64 / SEG : 1][CTX_CAP + 1];
+  __shared__ uint32_t s_pos[BITS ? 64 / SEG : 1][SCAN_ROW];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t seg = lane / SEG, sl = lane % SEG, sbase = seg * SEG;
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
@@ -1958,7 +1964,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       }
       const bool got = on && j < nctx && row_ != KIDX_NONE;
       const uint64_t mk = sballot(got);
-      if (got) s_cx[seg][nf + mbcnt64(mk)] = make_uint4(cb | (hs << 8), v0, v1, row_);
+      if (got) s_cx[seg][nf + mbcnt64(mk)] = make_uint2(cb | (hs << 8), row_);
       nf += popc64(mk);
     }
     wave_lds_sync();
@@ -1987,11 +1993,11 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           const uint32_t j = divp(t), ip = t - j * nP;
           const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
           const uint32_t kid = jk <= SCAN_ANC ? s_kid[seg][jk] : kl[jk];
-          const uint4 c = s_cx[seg][j];
+          const uint2 c = s_cx[seg][j];
           fk[u] = kid;
           fc[u] = c.x & 0xFFu;
           // the bit's word and the rank of the word's first bit, in one 8-byte load
-          if (kid < a.n_kent) fw[u] = *reinterpret_cast<const uint2*>(a.sbits + 2 * ((size_t)c.w * a.sbits_words + (kid >> 5)));
+          if (kid < a.n_kent) fw[u] = *reinterpret_cast<const uint2*>(a.sbits + 2 * ((size_t)c.y * a.sbits_words + (kid >> 5)));
           else badk = badk || kid != KIDX_NONE;
         }
       }
