@@ -377,7 +377,8 @@ template <class F>  // f(element k, EncodedRequest& e, BulkOut& o): encodes e, o
 int bulk_add(cg_batch* b, size_t n, F&& f) {
   LatTrace tr("bulk");
   const unsigned t = host_workers(n);
-  const size_t per = std::max<size_t>(256, (n + 8 * (size_t)t - 1) / (8 * (size_t)t));
+  static const size_t cpt = [] { const char* e = std::getenv("CEDARGPU_ENCODE_CHUNKS"); return e ? (size_t)std::max(1, std::atoi(e)) : 2u; }();
+  const size_t per = std::max<size_t>(256, (n + cpt * t - 1) / (cpt * t));
   const size_t nc = (n + per - 1) / per;
   struct Chunk {
     Batch part;

@@ -3646,8 +3646,8 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   // the grouping keys travel only when the step groups the batch on the device
   const bool grp = b.dev_group && b.n() >= 2 && b.gkeys.size() == b.n();
   constexpr int NSEC = 6;
-  const void* src[NSEC] = {b.heap.data(), b.req_base.data(), b.rows.data(), b.bstr_off.data(), b.bstr_bytes.data(), b.gkeys.data()};
-  const size_t len[NSEC] = {b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.bstr_off.size() * 4, b.bstr_bytes.size(),
+  const void* src[NSEC] = {b.heap.data(), b.req_base.data(), b.rows.data(), b.dev_str_off().data(), b.dev_str_bytes().data(), b.gkeys.data()};
+  const size_t len[NSEC] = {b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.dev_str_off().size() * 4, b.dev_str_bytes().size(),
                             grp ? b.gkeys.size() * 4 : 0};
   // Sections the encoder wrote into pinned blocks (engine.h pinned_take: a small batch's heap and
   // rows) are copied from there directly ("direct"); the rest is staged into one pinned block and

@@ -479,8 +479,10 @@ struct Compiler {
           w[2] = (uint32_t)(b >> 32);
           w[3] = (uint32_t)pre.size() | ((uint32_t)suf.size() << 4) | (star ? 1u << 8 : 0u);
           if (like_words) I.lslot_mask |= 1u << h;
+          I.lread_mask |= h < 32 ? 1u << h : 0xFFFFFFFFu;
           return put(AK_LIKEI, (uint32_t)h);
         }
+        I.lread_mask |= h < 32 ? 1u << h : 0xFFFFFFFFu;
         w[1] = pattern_into(e->pat, adata);
         *patch = true;
         return put(AK_LIKE, (uint32_t)h);
@@ -1891,6 +1893,7 @@ static std::shared_ptr<Image> compile_incremental(LowerState& S, const std::vect
   // then never files prefix keys on them, as a fresh build would not
   img->cslot_mask = A.cslot_mask;
   img->lslot_mask = A.lslot_mask;  // (the same: removed documents' like slots linger)
+  img->lread_mask = A.lread_mask;
   std::vector<Compiler::AttrKey> akeys;
   size_t total = 0;
   for (auto& tp : parsed) total += tp.size();
@@ -2072,6 +2075,7 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     A.ext_msgs = img->ext_msgs; A.act = img->act; A.hot = img->hot; A.amask_ok = img->amask_ok;
     A.cslot_mask = img->cslot_mask;
     A.lslot_mask = img->lslot_mask;
+    A.lread_mask = img->lread_mask;
     S.C.hot = C.hot; S.C.hot_depth = C.hot_depth; S.C.act_index = C.act_index;
     S.gen++;
     std::vector<uint32_t> kept(docs.size(), 0);
@@ -2179,7 +2183,7 @@ void Image::write_blob(void* wp) const {
   w.put64(table + 16 * DS_COUNT + 8, w.n);
   w.vec(pol); w.vec(tier_end); w.vec(code);
   w.u32(amask_ok); w.u32(n_atomic); w.u32(indexed); w.u32(combo_mask); w.u32(lane_need); w.u32(cslot_mask);
-  w.u32(pslot_mask); w.u32(lslot_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words); w.u32(l2_vmask); w.u32(l2_lmask);
+  w.u32(pslot_mask); w.u32(lslot_mask); w.u32(lread_mask); w.vec(pfx); w.u32(btab_slots); w.u32(sbits_words); w.u32(l2_vmask); w.u32(l2_lmask);
   w.u32((uint32_t)key_ents.size());
   w.raw(key_ents.data(), key_ents.size() * 8);
   w.u32((uint32_t)strings.size());
@@ -2284,6 +2288,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   img->cslot_mask = r.u32();
   img->pslot_mask = r.u32();
   img->lslot_mask = r.u32();
+  img->lread_mask = r.u32();
   if (img->n_hot() < 32 && (img->lslot_mask >> img->n_hot())) throw CedarError("corrupt image (like slots)");
   img->pfx = r.vec();
   img->btab_slots = r.u32();

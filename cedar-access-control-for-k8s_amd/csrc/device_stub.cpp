@@ -150,13 +150,13 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   for (uint32_t x : b.heap) h = h * 31 + x;
   for (uint32_t x : b.req_base) h = h * 31 + x;
   for (uint32_t x : b.rows) h = h * 31 + x;
-  for (uint32_t x : b.bstr_off) h = h * 31 + x;
-  for (uint8_t x : b.bstr_bytes) h = h * 31 + x;
+  for (uint32_t x : b.dev_str_off()) h = h * 31 + x;
+  for (uint8_t x : b.dev_str_bytes()) h = h * 31 + x;
   g_sink += h;
   if (std::getenv("CEDARGPU_STUB_SECTIONS"))  // upload composition per section (layout studies)
     std::fprintf(stderr, "sections n=%u heap=%zu req_base=%zu rows=%zu bstr_off=%zu bstr_bytes=%zu gkeys=%zu anc=%llu shared=%llu\n",
-                 b.n(), b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.bstr_off.size() * 4,
-                 b.bstr_bytes.size(), b.gkeys.size() * 4, (unsigned long long)b.anc_words,
+                 b.n(), b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.dev_str_off().size() * 4,
+                 b.dev_str_bytes().size(), b.gkeys.size() * 4, (unsigned long long)b.anc_words,
                  (unsigned long long)b.anc_shared_words);
   const size_t n = std::max<uint32_t>(d.n, 1);
   const size_t words = n * 2 + 2 * n * d.capr + n * d.cape * ERR_WORDS + FU_KINDS + 1;

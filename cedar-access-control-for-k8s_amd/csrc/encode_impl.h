@@ -689,6 +689,17 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       lw[3] = (uint32_t)suf; lw[4] = (uint32_t)(suf >> 32);
     }
   }
+  // the request-local strings whose bytes the device reads: the values of the image's like-read
+  // slots (Image::lread_mask); none of the others is ever read as bytes there
+  if (!img.dev_all_strings() && !E.strs.empty()) {
+    E.str_dev.assign(E.strs.size(), 0);
+    for (uint32_t m = img.lread_mask; m; m &= m - 1) {
+      const uint32_t h = (uint32_t)__builtin_ctz(m);
+      if (h >= nh) break;
+      const uint32_t w0 = row[RW_HDR + 2 * h], w1 = row[RW_HDR + 2 * h + 1];
+      if ((w0 >> TAG_SHIFT) == T_STR && w1 >= img.n_gstr() && w1 - img.n_gstr() < E.strs.size()) E.str_dev[w1 - img.n_gstr()] = 1;
+    }
+  }
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
   // grouping key: 8 bits of (action, resource type) | 16 of the principal's type and key ancestors |
   // 8 of its hot values (group.hip sorts on the top 24). Round-5 A/B of the field order

@@ -135,6 +135,13 @@ void Batch::append(EncodedRequest& e) {
     bstr_bytes.insert(bstr_bytes.end(), s.begin(), s.end());
     bstr_off.push_back((uint32_t)bstr_bytes.size());
   }
+  if (!img->dev_all_strings()) {  // the device's table: the same ids, bytes of the read strings only
+    dstr = true;
+    for (size_t k = 0; k < e.strs.size(); k++) {
+      if (k < e.str_dev.size() && e.str_dev[k]) dstr_bytes.insert(dstr_bytes.end(), e.strs[k].begin(), e.strs[k].end());
+      dstr_off.push_back((uint32_t)dstr_bytes.size());
+    }
+  }
 }
 
 // One ancestor-list record into the heap, or the copy an earlier block appended (equal words,
@@ -188,25 +195,31 @@ uint32_t Batch::intern_list(const uint32_t* w, uint32_t n, uint64_t room, uint64
 void Batch::concat(std::vector<Batch>& parts, unsigned threads) {
   if (!row_words) row_words = img->row_words();
   const size_t np = parts.size();
-  std::vector<size_t> ho(np), ro(np), so(np), bo(np);
-  size_t H = heap.size(), R = req_base.size(), S = n_bstr(), SB = bstr_bytes.size();
+  std::vector<size_t> ho(np), ro(np), so(np), bo(np), dbo(np);
+  size_t H = heap.size(), R = req_base.size(), S = n_bstr(), SB = bstr_bytes.size(), DB = dstr_bytes.size();
+  dstr = dstr || !img->dev_all_strings();
   for (size_t k = 0; k < np; k++) {
     const Batch& p = parts[k];
     if (p.n() && p.row_words != row_words) throw CedarError("request encoded for another image");
-    ho[k] = H; ro[k] = R; so[k] = S; bo[k] = SB;
-    H += p.heap.size(); R += p.n(); S += p.n_bstr(); SB += p.bstr_bytes.size();
+    if (dstr && p.dstr_off.size() != p.bstr_off.size()) throw CedarError("batch part without its device string table");
+    ho[k] = H; ro[k] = R; so[k] = S; bo[k] = SB; dbo[k] = DB;
+    H += p.heap.size(); R += p.n(); S += p.n_bstr(); SB += p.bstr_bytes.size(); DB += p.dstr_bytes.size();
     anc_words += p.anc_words;
     anc_shared_words += p.anc_shared_words;
   }
   if (H > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
   if (R * row_words > 0xFFFFFFFFull) throw CedarError("batch rows exceed 16 GiB");
-  if (S >= 0xFFFFFFFFull || SB > 0xFFFFFFFFull) throw CedarError("batch string table overflow");
+  if (S >= 0xFFFFFFFFull || SB > 0xFFFFFFFFull || DB > 0xFFFFFFFFull) throw CedarError("batch string table overflow");
   heap.resize(H);
   req_base.resize(R);
   rows.resize(R * row_words);
   gkeys.resize(R);
   bstr_off.resize(S + 1);
   bstr_bytes.resize(SB);
+  if (dstr) {
+    dstr_off.resize(S + 1);
+    dstr_bytes.resize(DB);
+  }
   auto copy = [&](size_t k) {
     Batch& p = parts[k];
     const uint32_t hs = (uint32_t)ho[k], ss = (uint32_t)so[k], bs = (uint32_t)bo[k];
@@ -222,6 +235,11 @@ void Batch::concat(std::vector<Batch>& parts, unsigned threads) {
     }
     for (uint32_t j = 0; j < p.n_bstr(); j++) bstr_off[ss + 1 + j] = p.bstr_off[1 + j] + bs;
     if (!p.bstr_bytes.empty()) std::memcpy(bstr_bytes.data() + bo[k], p.bstr_bytes.data(), p.bstr_bytes.size());
+    if (dstr) {
+      const uint32_t ds = (uint32_t)dbo[k];
+      for (uint32_t j = 0; j < p.n_bstr(); j++) dstr_off[ss + 1 + j] = p.dstr_off[1 + j] + ds;
+      if (!p.dstr_bytes.empty()) std::memcpy(dstr_bytes.data() + dbo[k], p.dstr_bytes.data(), p.dstr_bytes.size());
+    }
     p = Batch();  // its memory goes back as soon as it is copied
   };
   threads = std::max(1u, std::min<unsigned>(threads, (unsigned)np));
@@ -246,6 +264,7 @@ void Batch::add(const std::vector<EntityIn>& ents, const RequestIn& req) {
 // The string table is built as requests are appended; the device reads at least one byte and word.
 void Batch::finalize_strings() {
   if (bstr_bytes.empty()) bstr_bytes.push_back(0);
+  if (dstr && dstr_bytes.empty()) dstr_bytes.push_back(0);
   if (heap.empty()) heap.push_back(0);
 }
 

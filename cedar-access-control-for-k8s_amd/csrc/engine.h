@@ -183,6 +183,11 @@ struct Image {
   // after the list offsets
   uint32_t lslot_mask = 0;
   uint32_t n_like() const { return (uint32_t)__builtin_popcount(lslot_mask); }
+  // hot slots some `like` atom reads (~0: one past slot 31). The device reads a request string's
+  // bytes only there when every policy is atomic (bytecode may read any string, ip() / decimal()
+  // parse them), so a batch then uploads the bytes of those slots' strings alone (Batch dstr_*)
+  uint32_t lread_mask = 0;
+  bool dev_all_strings() const { return n_atomic < n_pol() || lread_mask == 0xFFFFFFFFu || n_hot() > 32; }
   uint32_t like_off() const { return cgi::RW_HDR + 2 * n_hot() + (list_mask() ? n_hot() : 0u); }
   uint32_t row_words() const { return (like_off() + cgi::LIKE_WORDS * n_like() + 3) & ~3u; }
   // string -> id over a string_view: open addressing, entries (hash high 32 bits << 32 | id + 1),
@@ -320,6 +325,7 @@ struct EncodedRequest {
   // hashed fields of the row, most significant first; the device bucket-sorts on its top bits
   uint32_t gkey = 0;
   std::vector<std::string> strs;   // request-local strings (few per request: found by linear scan)
+  std::vector<uint8_t> str_dev;    // per string: its bytes are read on the device (Image::lread_mask)
   static constexpr size_t STRS_SCAN = 16;
   std::unordered_multimap<uint64_t, uint32_t> strs_ix;  // str_hash -> index, once strs outgrows STRS_SCAN
   // interning memo over the source bytes' address: a value repeated from the same bytes (a group
@@ -327,7 +333,7 @@ struct EncodedRequest {
   static constexpr uint32_t MEMO = 32;
   const char* memo_p[MEMO];
   uint32_t memo_len[MEMO], memo_id[MEMO], n_memo = 0;
-  void clear() { blk.clear(); row.clear(); anc.clear(); anc_at.clear(); anc_hash.clear(); strs.clear(); strs_ix.clear(); n_memo = 0; }
+  void clear() { blk.clear(); row.clear(); anc.clear(); anc_at.clear(); anc_hash.clear(); strs.clear(); str_dev.clear(); strs_ix.clear(); n_memo = 0; }
   // words of record k / the first pair of the list a row word (k + 1) names
   const uint32_t* anc_rec(uint32_t k) const { return anc.data() + anc_at[k]; }
   const uint32_t* anc_pairs(uint32_t row_word) const { return anc_rec(row_word - 1) + 1; }
@@ -353,6 +359,14 @@ struct Batch {
   PinVec<uint32_t> bstr_off{0};
   PinVec<uint8_t> bstr_bytes;
   uint32_t n_bstr() const { return (uint32_t)bstr_off.size() - 1; }
+  // the device's copy of the table when the image reads few strings (Image::dev_all_strings false):
+  // the same numbering, and bytes only for the strings a `like` atom reads (the rest empty); the
+  // host renders diagnostics from the full table above
+  bool dstr = false;
+  PinVec<uint32_t> dstr_off{0};
+  PinVec<uint8_t> dstr_bytes;
+  const PinVec<uint32_t>& dev_str_off() const { return dstr ? dstr_off : bstr_off; }
+  const PinVec<uint8_t>& dev_str_bytes() const { return dstr ? dstr_bytes : bstr_bytes; }
   // Interned ancestor lists (EncodedRequest::anc): content hash -> heap offset of the copy that
   // later blocks reference (image.h "ancestor lists"). Requests of one principal share one list,
   // so a batch carries each distinct list once and grouped neighbours read the same lines.
