@@ -232,3 +232,25 @@ def test_two_step_build_writes_the_same_blob():
     assert lib.cg_compiler_write_image(c._h, big, n.value) == 0
     assert big.raw == two
     c.close()
+
+
+def test_duplicate_class_table_survives_the_blob():
+    """The image's host-side duplicate-class table (image.h RS_CLASS: the host lists a class the
+    candidate pass reports by its representative) is the blob's tail: an image with classes loads,
+    a rebuild writes it again, and a member index past the policies is refused at load."""
+    dup = "\n".join('forbid (principal, action == A::"w", resource) when { resource.owner != principal.name };'
+                    for _ in range(150))
+    singles = "\n".join(f'permit (principal, action == A::"r", resource) when {{ resource.level == {i} }};' for i in range(50))
+    likes = 'permit (principal, action == A::"l", resource) when { resource.name like "prod-*" };\n' \
+            'permit (principal, action == A::"l", resource) when { resource.path like "/a*b*c" };'
+    stores = [cedargpu.MemoryStore("a.cedar", dup), cedargpu.MemoryStore("b.cedar", singles), cedargpu.MemoryStore("c.cedar", likes)]
+    img = cedargpu.build_image(stores, epoch=3)
+    assert cedargpu.index_stats(img)["entries"] > 0
+    assert cedargpu.build_image(stores, epoch=3) == img
+    n_pol = 202
+    # the tail: [n, class offsets (n_pol + 1)] [n, members (n_pol)]; the last member, past the set
+    assert int.from_bytes(img[-4 * (n_pol + 1):-4 * n_pol], "little") == n_pol
+    bad = bytearray(img)
+    bad[-4:] = (n_pol + 5).to_bytes(4, "little")
+    with pytest.raises(ValueError):  # (deserialize: "corrupt image (duplicate classes)")
+        cedargpu.index_stats(bytes(bad))
