@@ -4387,7 +4387,9 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
     k.ovf_cap = f.cap; k.ovf_capr = f.capr; k.ovf_cape = f.cape;
   }
   if (b.ord) {  // grouped batch: this step's order and its rows in that order (group.hip)
-    if (group_enqueue(b.gkeys, b.rows, b.n, b.row_words, b.grows, b.ord, b.gkeys2, b.gvals, b.grp_temp, b.grp_temp_bytes, s)) {
+    // (the worklist counters and the scan's bad-index count cleared by the grouping's first kernel)
+    if (group_enqueue(b.gkeys, b.rows, b.n, b.row_words, b.grows, b.ord, b.gkeys2, b.gvals, b.grp_temp, b.grp_temp_bytes, s,
+                      b.fu_cnt, b.fu_cnt ? FU_KINDS + 1 : 0u)) {
       g_err = "request grouping failed";
       return -4;
     }
@@ -4396,7 +4398,7 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
   }
   mark(PH_GROUP, s);
   // the worklist counters and the scan's bad-index count start at zero before the first pass
-  if (b.fu_cnt) HIPCHK(hipMemsetAsync(b.fu_cnt, 0, (FU_KINDS + 1) * 4, s), "memset worklists");
+  if (b.fu_cnt && !b.ord) HIPCHK(hipMemsetAsync(b.fu_cnt, 0, (FU_KINDS + 1) * 4, s), "memset worklists");
   const bool two = img.indexed && split_on() && !probe_stats() && probe_seg() == 8 && probe_occ() == 3;
   launch_eval(img, k, b.n, s);
   HIPCHK(hipGetLastError(), "launch");

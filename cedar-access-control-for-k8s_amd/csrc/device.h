@@ -217,7 +217,10 @@ int dev_time_split(const DevImage& img, DevBatch& b, uint32_t iters, void* strea
 uint32_t group_bits();
 bool group_gather();  // the grouped rows are copied into order (else read through the order)
 size_t group_temp_bytes(uint32_t n);
+// (zero: zero_n words the step's later kernels count into, cleared by the grouping's first kernel
+// instead of a fill launch of their own)
 int group_enqueue(const uint32_t* keys, const uint32_t* rows, uint32_t n, uint32_t row_words, uint32_t* grows,
-                  uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream);
+                  uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream,
+                  uint32_t* zero = nullptr, uint32_t zero_n = 0);
 
 }  // namespace cg

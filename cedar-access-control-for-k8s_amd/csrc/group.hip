@@ -46,9 +46,11 @@ __global__ __launch_bounds__(256) void cedar_group_gather(const uint32_t* __rest
 }
 
 // vals[i] = i, four per lane (vals 16-byte aligned; the tail of the last uint4 past n is scratch)
-__global__ __launch_bounds__(256) void cedar_group_iota(uint4* __restrict__ vals, uint32_t n) {
+__global__ __launch_bounds__(256) void cedar_group_iota(uint4* __restrict__ vals, uint32_t n, uint32_t* __restrict__ zero,
+                                                        uint32_t zero_n) {
   const uint32_t i = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (i < n) vals[i / 4] = make_uint4(i, i + 1, i + 2, i + 3);
+  if (blockIdx.x == 0 && threadIdx.x < zero_n) zero[threadIdx.x] = 0u;
 }
 
 }  // namespace
@@ -129,13 +131,16 @@ size_t group_temp_bytes(uint32_t n) {
 // Enqueues the grouping of n requests on `stream`: ord[k] = the request evaluated k-th, grows its
 // row (row_words a multiple of 4). keys2 / vals: n words of scratch each; temp: group_temp_bytes.
 int group_enqueue(const uint32_t* keys, const uint32_t* rows, uint32_t n, uint32_t row_words, uint32_t* grows,
-                  uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream) {
+                  uint32_t* ord, uint32_t* keys2, uint32_t* vals, void* temp, size_t temp_bytes, void* stream,
+                  uint32_t* zero, uint32_t zero_n) {
   hipStream_t s = (hipStream_t)stream;
   if (row_words % 4) return -1;
   // The request indices are written out (one pass over n words) rather than read from a counting
   // iterator: rocPRIM copies a counting iterator and the keys into its buffers (two passes) before
   // an odd number of digit places.
-  hipLaunchKernelGGL(cedar_group_iota, dim3((n + 1023) / 1024), dim3(256), 0, s, reinterpret_cast<uint4*>(vals), n);
+  if (zero_n > 256) return -1;
+  hipLaunchKernelGGL(cedar_group_iota, dim3((n + 1023) / 1024), dim3(256), 0, s, reinterpret_cast<uint4*>(vals), n, zero,
+                     zero ? zero_n : 0u);
   size_t bytes = temp_bytes;
   if (group_sort(temp, bytes, const_cast<uint32_t*>(keys), keys2, vals, ord, n, 32 - group_bits(), s) != hipSuccess)
     return -1;
