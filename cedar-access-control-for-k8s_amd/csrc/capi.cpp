@@ -1400,6 +1400,11 @@ int cg_batch_submit(cg_batch* b) {
     b->host.capr = std::max(b->host.capr, std::min<uint32_t>(1024u, std::max<uint32_t>(32u, (uint32_t)((512u << 10) / (4ull * n)))) & ~7u);
     b->host.cape = std::max(b->host.cape, std::min<uint32_t>(32u, std::max<uint32_t>(2u, (uint32_t)((64u << 10) / (24ull * n)))));
   }
+  // First-pass error details per request: indexed batches past the one-launch size keep one in their
+  // result block (a request with more takes a long-list slot, with up to 8), so the results copy
+  // carries 24 instead of 96 bytes of mostly empty error slots per request. CEDARGPU_FIRST_CAPE pins it.
+  if (b->img->host->indexed && n > dev_small_n()) b->host.cape = 1;
+  if (const char* e = std::getenv("CEDARGPU_FIRST_CAPE")) b->host.cape = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
   if (const char* e = std::getenv("CEDARGPU_FIRST_CAPR")) b->host.capr = (uint32_t)std::max(1, std::min(4096, std::atoi(e)));
   GUARD(b->err, { group_requests(b); })
   tr.mark("group");
