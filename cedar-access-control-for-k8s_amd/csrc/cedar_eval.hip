@@ -3793,7 +3793,14 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     }
   };
   static const bool pooled = !(std::getenv("CEDARGPU_STAGE_POOL") && *std::getenv("CEDARGPU_STAGE_POOL") == '0');
-  if (nt <= 1 && pooled && total_len >= (256u << 10) &&
+  // Throughput batches (>= 64 MB to stage) are staged and copied in pieces: each piece's H2D copy
+  // is enqueued as soon as its bytes are staged, so the staging memcpy runs under the copy engine's
+  // transfer instead of ahead of it (CEDARGPU_STAGE_PIPE=0: stage everything, then one copy)
+  static const bool pipe_on = !(std::getenv("CEDARGPU_STAGE_PIPE") && *std::getenv("CEDARGPU_STAGE_PIPE") == '0');
+  const bool pipe = pipe_on && !d.zc && nt > 1 && total_len >= (64u << 20);
+  if (pipe) {
+    // (staged below, with the copies)
+  } else if (nt <= 1 && pooled && total_len >= (256u << 10) &&
       stage_pool().run([&](unsigned t) { part_copy(t, StagePool::HELPERS + 1); })) {
     // (staged by the pool)
   } else if (nt <= 1) {
@@ -3866,9 +3873,42 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     }
   *out = d;  // blocks owned by the batch from here on (freed by dev_batch_free on any error)
   if (d.pev[0]) HIPCHK(hipEventRecord((hipEvent_t)d.pev[0], s), "event record");
-  // (one copy: staging in pieces with an H2D per piece, to overlap the two, made 1-2k-request
-  // batches 0.06-0.07 ms slower on the box, gpurun_out/r04flat3)
-  HIPCHK(hipMemcpyAsync(in, st, stage_in, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  // (one copy below 64 MB: staging in pieces with an H2D per piece, to overlap the two, made
+  // 1-2k-request batches 0.06-0.07 ms slower on the box, gpurun_out/r04flat3)
+  if (pipe) {
+    // pieces of <= 16 MB of the staged sections, in order; nt workers take (piece, part) items in
+    // order and this thread enqueues each piece's copy once all its parts are staged
+    constexpr size_t PIECE = 16u << 20;
+    struct Piece { int k; size_t a, b; };
+    std::vector<Piece> pcs;
+    for (int k = 0; k < NSEC; k++)
+      if (len[k] && !direct[k])
+        for (size_t a = 0; a < len[k]; a += PIECE) pcs.push_back({k, a, std::min(len[k], a + PIECE)});
+    std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[pcs.size()]);
+    for (size_t i = 0; i < pcs.size(); i++) done[i].store(0, std::memory_order_relaxed);
+    std::atomic<size_t> next{0};
+    const size_t items = pcs.size() * nt;
+    auto work = [&] {
+      for (size_t it; (it = next.fetch_add(1, std::memory_order_relaxed)) < items;) {
+        const Piece& pc = pcs[it / nt];
+        const size_t t = it % nt, n_ = pc.b - pc.a, lo = pc.a + n_ * t / nt, hi = pc.a + n_ * (t + 1) / nt;
+        if (lo < hi) std::memcpy(st + off[pc.k] + lo, (const uint8_t*)src[pc.k] + lo, hi - lo);
+        done[it / nt].fetch_add(1, std::memory_order_release);
+      }
+    };
+    std::vector<std::thread> ts;
+    for (unsigned t = 0; t < nt; t++) ts.emplace_back(work);
+    hipError_t ce = hipSuccess;
+    for (size_t i = 0; i < pcs.size(); i++) {
+      while (done[i].load(std::memory_order_acquire) < nt) std::this_thread::yield();
+      const Piece& pc = pcs[i];
+      if (ce == hipSuccess) ce = hipMemcpyAsync(in + off[pc.k] + pc.a, st + off[pc.k] + pc.a, pc.b - pc.a, hipMemcpyHostToDevice, s);
+    }
+    for (auto& th : ts) th.join();
+    HIPCHK(ce, "hipMemcpyAsync H2D (piece)");
+  } else {
+    HIPCHK(hipMemcpyAsync(in, st, stage_in, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+  }
   // (the direct sources belong to the host batch, which keeps them until this stream has drained:
   // cg_batch's destructor hands them to the retired batch, DevBatch::keep)
   for (int k = 0; k < NSEC; k++)
