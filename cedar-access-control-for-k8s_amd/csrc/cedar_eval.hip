@@ -66,7 +66,6 @@ struct KArgs {
   const uint32_t* __restrict__ hot;
   const uint32_t* __restrict__ act;
   const uint32_t* __restrict__ heap;
-  const uint32_t* __restrict__ req_base;
   const uint32_t* __restrict__ req_idx;
   const uint32_t* __restrict__ bstr_off;
   const uint8_t* __restrict__ bstr_bytes;
@@ -1324,7 +1323,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
 
   uint32_t lane_scratch[GLANE ? 1 : LANE_WORDS];
   Ctx c;
-  c.blk = a.heap + (valid ? a.req_base[r] : 0);
+  c.blk = a.heap + (valid ? a.rows[(size_t)r * a.row_words + RW_BLK] : 0);  // (the row's block offset: no req_base upload)
   c.cpool = a.cpool;
   c.lh = GLANE ? a.lane + (size_t)(valid ? gid : 0) * a.lane_stride : lane_scratch;
   c.hot = a.hot;
@@ -3647,7 +3646,8 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   const bool grp = b.dev_group && b.n() >= 2 && b.gkeys.size() == b.n();
   constexpr int NSEC = 6;
   const void* src[NSEC] = {b.heap.data(), b.req_base.data(), b.rows.data(), b.dev_str_off().data(), b.dev_str_bytes().data(), b.gkeys.data()};
-  const size_t len[NSEC] = {b.heap.size() * 4, b.req_base.size() * 4, b.rows.size() * 4, b.dev_str_off().size() * 4, b.dev_str_bytes().size(),
+  // (req_base stays on the host: the kernels read a request's block offset from its row, RW_BLK)
+  const size_t len[NSEC] = {b.heap.size() * 4, 0, b.rows.size() * 4, b.dev_str_off().size() * 4, b.dev_str_bytes().size(),
                             grp ? b.gkeys.size() * 4 : 0};
   // Sections the encoder wrote into pinned blocks (engine.h pinned_take: a small batch's heap and
   // rows) are copied from there directly ("direct"); the rest is staged into one pinned block and
@@ -3840,7 +3840,6 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     std::memset(d.zc_out + o_res, 0, n * 2 * 4);        // res: RF_VALID clear until written
   }
   d.heap = (uint32_t*)(in + off[0]);
-  d.req_base = (uint32_t*)(in + off[1]);
   d.rows = (uint32_t*)(in + off[2]);
   d.bstr_off = (uint32_t*)(in + off[3]);
   d.bstr_bytes = in + off[4];
@@ -4078,7 +4077,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   KArgs k;
   k.pstream = img.pstream; k.tier_cend = img.tier_cend; k.chunks = img.chunks; k.cpool = img.cpool;
   k.gstr_off = img.gstr_off; k.gstr_bytes = img.gstr_bytes; k.hot = img.hot;
-  k.heap = b.heap; k.req_base = b.req_base; k.req_idx = req_idx;
+  k.heap = b.heap; k.req_idx = req_idx;
   k.bstr_off = b.bstr_off; k.bstr_bytes = b.bstr_bytes;
   k.res = res; k.reasons_f = rf; k.reasons_p = rp; k.errs = er;
   k.n_pol = img.n_pol; k.n_tiers = img.n_tiers; k.n_gstr = img.n_gstr; k.n_hot = img.n_hot;

@@ -48,8 +48,8 @@ struct DevPool;
 struct DevBatch {
   int device = -1;
   DevPool* pool = nullptr;
-  // inputs: one device block (heap | req_base | rows | bstr_off | bstr_bytes), one copy
-  uint32_t *heap = nullptr, *req_base = nullptr, *rows = nullptr, *req_idx = nullptr, *bstr_off = nullptr;
+  // inputs: one device block (heap | rows | bstr_off | bstr_bytes | grouping keys), one copy
+  uint32_t *heap = nullptr, *rows = nullptr, *req_idx = nullptr, *bstr_off = nullptr;
   uint8_t* bstr_bytes = nullptr;
   // results: one device block (res | reasons_f | reasons_p | errs), one copy back
   uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
