@@ -87,7 +87,8 @@ struct KArgs {
   const uint32_t* ord;
   const uint32_t* __restrict__ grows;  // ... and its rows in that order (launch position k: grows + k * row_words)
   uint32_t n_pol, n_tiers, n_gstr, n_hot, n_act, amask_ok, n_req, capr, cape, bmask, fmask, row_words, combo_mask;
-  uint32_t hlists;  // rows carry element-hash lists (image.h "set-membership keys")
+  uint32_t hlists;  // hot slots whose rows carry element-hash / prefix lists (image.h "set-membership
+                    // keys"): the row's list-offset word of slot h is at its rank among them
   uint32_t l1filt;  // level-1 probes consult the key filter first (CEDARGPU_L1_FILTER=1: on, A/B)
   uint32_t l2filt;  // level-2 probes too, after the level-1 entry's own bloom (CEDARGPU_L2_FILTER)
   uint32_t slot_split;  // probes load a slot's first 16 B, the rest only on a key match (CEDARGPU_SLOT_SPLIT)
@@ -177,8 +178,11 @@ struct Ctx {
   uint32_t t0, i0, t1, i1, t2, i2, t3, i3, t4, i4, t5, i5, t6, i6, t7, i7;
   uint32_t pb0, pb1, pb2, pb3;            // principal ancestor-or-self Bloom
   uint32_t rb0, rb1, rb2, rb3;            // resource ancestor-or-self Bloom
-  const uint32_t* rowx;                   // the row's element-hash list offsets per hot slot, or null
-  __device__ uint32_t hlist(uint32_t h) const { return rowx ? rowx[h] : 0xFFFFFFFFu; }
+  const uint32_t* rowx;                   // the row's element-hash list offsets (one per list slot), or null
+  uint32_t lmask;                         // the list slots (KArgs::hlists)
+  __device__ uint32_t hlist(uint32_t h) const {
+    return (rowx && ((lmask >> h) & 1u)) ? rowx[__popc(lmask & ((1u << h) - 1u))] : 0xFFFFFFFFu;
+  }
   static constexpr uint32_t lkb = 0xFFFFFFFFu;  // like words not staged (AK_LIKEI reads the bytes)
   static constexpr uint32_t lslot = 0u;
 };
@@ -1390,6 +1394,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
     for (uint32_t h = 0; h < a.n_hot; h++)
       c.hotl[h * c.hstride] = valid ? make_uint2(row[RW_HDR + 2 * h], row[RW_HDR + 2 * h + 1]) : make_uint2(0u, 0u);
     c.rowx = (valid && a.hlists) ? row + RW_HDR + 2 * a.n_hot : nullptr;
+    c.lmask = a.hlists;
   }
 
   bool decided = !valid;
@@ -1629,7 +1634,10 @@ struct PCtx {
   // per-request part is one 32-bit word: a 64-bit pointer here was the candidate pass's spill)
   const uint32_t* rowb;
   uint32_t rowo;  // 0xFFFFFFFF: none
-  __device__ uint32_t hlist(uint32_t h) const { return rowo != 0xFFFFFFFFu ? rowb[rowo + h] : 0xFFFFFFFFu; }
+  uint32_t lmask;  // the list slots (KArgs::hlists): slot h's word at its rank among them
+  __device__ uint32_t hlist(uint32_t h) const {
+    return (rowo != 0xFFFFFFFFu && ((lmask >> h) & 1u)) ? rowb[rowo + __popc(lmask & ((1u << h) - 1u))] : 0xFFFFFFFFu;
+  }
   uint32_t lkb, lslot;  // like words staged at hot index lkb (0xFFFFFFFF: not), like slots (KArgs)
 };
 
@@ -1828,7 +1836,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     // BITS: lane k < popc(l2_lmask) reads the k-th list slot's head and first LW words after it
     // (element count or marker, elements) in the same trip
     if (BITS && klist && a.hlists && sl < (uint32_t)__builtin_popcount(a.l2_lmask)) {
-      l_lo = row[RW_HDR + 2 * a.n_hot + nth_bit(a.l2_lmask, sl)];
+      l_lo = row[RW_HDR + 2 * a.n_hot + __popc(a.hlists & ((1u << nth_bit(a.l2_lmask, sl)) - 1u))];
       l_hd = blk[l_lo];
 #pragma unroll
       for (uint32_t k = 0; k < LW; k++) l_w[k] = blk[l_lo + 1 + k];  // (past a short list: its block's next words)
@@ -2064,7 +2072,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           if (ck >= cn) {
             ch = __builtin_ctz(csl);
             csl &= csl - 1;
-            const uint32_t lo = row[RW_HDR + 2 * a.n_hot + ch];
+            const uint32_t lo = row[RW_HDR + 2 * a.n_hot + __popc(a.hlists & ((1u << ch) - 1u))];
             const uint32_t hd = blk[lo];
             ck = cn = 0;
             if (hd & 0x80000000u) {
@@ -2218,6 +2226,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   c.blk = a.heap + hdr(RW_BLK);
   c.rowb = (a.grows && !a.req_idx) ? a.grows : a.rows;
   c.rowo = (valid && a.hlists) ? (uint32_t)(row - c.rowb) + RW_HDR + 2 * a.n_hot : 0xFFFFFFFFu;
+  c.lmask = a.hlists;
   c.cpool = a.cpool;
   c.lh = wl.he[seg];  // atoms never address lane scratch (any valid pointer)
   c.gstr_off = a.gstr_off;
@@ -2533,6 +2542,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       tc.r_anc = x2.x; tc.a_anc = x2.y; tc.p_nanc = x2.z & 0xFFFFu; tc.r_nanc = x2.z >> 16; tc.a_nanc = x2.w & 0xFFFFu;
       tc.rowb = c.rowb;
       tc.rowo = x3.x;
+      tc.lmask = a.hlists;
       tc.lkb = a.like_base;
       tc.lslot = a.lslot;
       const uint64_t tam = ((uint64_t)x3.z << 32) | x3.y;
@@ -2714,7 +2724,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
             if (ck >= cn) {  // the next set-membership slot: its list header
               ch = __builtin_ctz(csl);
               csl &= csl - 1;
-              const uint32_t lo = row[RW_HDR + 2 * a.n_hot + ch];
+              const uint32_t lo = row[RW_HDR + 2 * a.n_hot + __popc(a.hlists & ((1u << ch) - 1u))];
               const uint32_t hd = c.blk[lo];
               ck = cn = 0;
               if (hd & 0x80000000u) {
@@ -4094,7 +4104,7 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.rows = b.rows; k.row_words = b.row_words; k.combo_mask = img.combo_mask;
   k.srows = img.srows; k.shash = reinterpret_cast<const uint4*>(img.shash); k.n_static = img.n_static; k.smask = img.smask;
   k.lane = b.lane; k.lane_stride = img.lane_need;
-  k.hlists = img.cslot_mask ? 1u : 0u;
+  k.hlists = img.cslot_mask;  // (DevImage::cslot_mask: the image's list slots)
   // like words staged behind the hot values while both fit the probe kernel's hot rows (32 entries;
   // CEDARGPU_LIKE_STAGE=0: never, A/B): else AK_LIKEI reads the string's bytes
   static const bool like_stage = !(std::getenv("CEDARGPU_LIKE_STAGE") && *std::getenv("CEDARGPU_LIKE_STAGE") == '0');

@@ -643,7 +643,6 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   // set-membership keys (image.h BT_CKEY): each such slot's element hashes, after the hot slots;
   // prefix keys (image.h "prefix level-2 keys"): a string's prefix hashes at the slot's lengths
   if (img.list_mask()) {
-    for (uint32_t h = 0; h < nh; h++) row[RW_HDR + 2 * nh + h] = 0xFFFFFFFFu;  // no list
     std::vector<uint32_t>& hs = S.hs;
     for (uint32_t m = img.list_mask(); m; m &= m - 1) {
       const uint32_t h = (uint32_t)__builtin_ctz(m);
@@ -666,7 +665,8 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
         head = n;
         for (uint32_t k = 0; k < n; k++) hs.push_back(mem_chash(blk, img.cpool, mm[off + 1 + 2 * k], mm[off + 2 + 2 * k]));
       }
-      row[RW_HDR + 2 * nh + h] = (uint32_t)blk.size();
+      // (the slot's word: its rank among the image's list slots)
+      row[RW_HDR + 2 * nh + (uint32_t)__builtin_popcount(img.list_mask() & ((1u << h) - 1u))] = (uint32_t)blk.size();
       blk.push_back(head);
       blk.insert(blk.end(), hs.begin(), hs.end());
     }

@@ -188,7 +188,8 @@ struct Image {
   // parse them), so a batch then uploads the bytes of those slots' strings alone (Batch dstr_*)
   uint32_t lread_mask = 0;
   bool dev_all_strings() const { return n_atomic < n_pol() || lread_mask == 0xFFFFFFFFu || n_hot() > 32; }
-  uint32_t like_off() const { return cgi::RW_HDR + 2 * n_hot() + (list_mask() ? n_hot() : 0u); }
+  // (one list-offset word per slot of list_mask, in slot order: image.h "set-membership keys")
+  uint32_t like_off() const { return cgi::RW_HDR + 2 * n_hot() + (uint32_t)__builtin_popcount(list_mask()); }
   uint32_t row_words() const { return (like_off() + cgi::LIKE_WORDS * n_like() + 3) & ~3u; }
   // string -> id over a string_view: open addressing, entries (hash high 32 bits << 32 | id + 1),
   // 0 = empty; size is a power of two. Built by build_lookup once the table is final.

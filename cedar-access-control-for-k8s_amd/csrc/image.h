@@ -325,9 +325,10 @@ constexpr uint32_t MISSING_W0 = 0xFFFFFFFFu;  // level-2 index key of an absent 
 // (c a primitive, or a record template of primitive constants) is filed under (h | BT_CKEY,
 // element hash of c, 1), and also under (h | BT_CKEY, NOTSET_W0, 0) (a value that is no set makes
 // contains raise) and, unguarded, (h | BT_CKEY, MISSING_W0, 0). A level-1 entry's word 7 (cmask)
-// lists such slots. The request row then carries, after the hot slots, one word per hot slot:
-// for a slot of the image's cslot_mask (every slot a contains / containsAny atom reads) the block
-// offset of [n | CL_*, element hash x n], else ~0. The probe kernel probes each element of the
+// lists such slots. The request row then carries, after the hot slots, one word per list slot
+// (the image's cslot_mask and pslot_mask: every slot a contains / containsAny atom reads, and the
+// prefix-keyed ones), in slot order: the block offset of [n | CL_*, element hash x n]; slot h's
+// word is at its rank among the list slots. The probe kernel probes each element of the
 // request's set; contains atoms compare element hashes first and the values only on a match
 // (image.h chash_*: equal values hash alike on both sides; a collision costs one exact compare).
 constexpr uint32_t BT_CKEY = 0x40, NOTSET_W0 = 0xFFFFFFFEu;
