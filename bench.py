@@ -484,7 +484,9 @@ def main():
         io = b.io()
     except AttributeError:  # an A/B build (CEDARGPU_AB_LIB) that predates cg_batch_io
         io = {"h2d_bytes": 0, "d2h_bytes": 0, "list_words": 0, "list_words_shared": 0}
-    n_reasons = [b.reasons(i)[0].__len__() for i in range(len(b))]
+    # the deciding lists as the device wrote them (a duplicate class reported whole is one word;
+    # its members are listed on the host, not by the step)
+    n_reasons = [b.route_words(i)[1] for i in range(len(b))]
     alg_bytes = algorithmic_bytes(sars, n_reasons, has_like=True)
 
     if args.warmup:
@@ -679,7 +681,7 @@ def main():
                          "valu": valu,
                          "launch": "one complete step on one stream: the device grouping (rocPRIM onesweep sort of the encoder's "
                                    "keys), cedar_scan_kernel, the SPLIT candidate pass, cedar_fu_gather and the follow-up "
-                                   "launches (rocprofv3 kernel stats in profiles/r04/)",
+                                   "launches (rocprofv3 kernel stats in profiles/r06/)",
                          "achieved_is": "SURVEY §8(d) algorithmic bytes of every decision in the step / the dominant kernel's "
                                         "time (HIP events at its phase boundaries); step_achieved: over the whole step",
                          "traffic_source": "PMC FETCH_SIZE x2 + WRITE_SIZE summed over one step's dispatches "

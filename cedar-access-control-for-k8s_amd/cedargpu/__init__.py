@@ -13,3 +13,4 @@ from .store import (ALLOW_ALL_ADMISSION, FAULT_BAD_KIDX, FAULT_DEVICE_ERROR, FAU
                     Authorizer, AVPStore, Batch, Compiler, Context, CRDStore, DirectoryStore, MemoryStore, PolicyStore,
                     Queue, StaticStore, TieredPolicyStores, admission_to_cedar_json, atomic_policies, build_image,
                     delta_info, device_count, image_delta, image_patch, image_stats, index_stats, pinned_stats)
+from .store import (ROUTE_CLASS, ROUTE_FIRST_SLOT, ROUTE_FU_BIG, ROUTE_FU_GEN, ROUTE_FU_OVF, ROUTE_RERUN)  # noqa: F401

@@ -83,6 +83,7 @@ _SIGS = {
     "cg_image_policy_atomic": (ctypes.c_int, [P, sz, u32, ctypes.POINTER(ctypes.c_int)]),
     "cg_image_indexed": (ctypes.c_int, [P, sz, ctypes.POINTER(ctypes.c_int)]),
     "cg_image_index_stats": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u32)] * 6),
+    "cg_image_like_slots": (ctypes.c_int, [P, sz] + [ctypes.POINTER(u32)] * 2),
     "cg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "cg_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "cg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(P)]),
@@ -120,6 +121,7 @@ _SIGS = {
     "cg_batch_time": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_float)]),
     "cg_batch_time_split": (ctypes.c_int, [P, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "cg_batch_reruns": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
+    "cg_batch_route": (ctypes.c_int, [P, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]),
     "cg_batch_followups": (ctypes.c_int, [P, ctypes.POINTER(u32)]),
     "cg_batch_bytes": (ctypes.c_int, [P, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     "cg_batch_io": (ctypes.c_int, [P] + [ctypes.POINTER(ctypes.c_uint64)] * 4),

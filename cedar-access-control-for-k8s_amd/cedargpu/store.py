@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import json
 import threading
+import weakref
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
 from ._lib import CG_E_RANGE, CompileError, DeadlineError, DeviceError, _err, lib
@@ -25,6 +26,8 @@ _new_bytes.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
 
 FAULT_NONE, FAULT_DEVICE_ERROR, FAULT_STALL, FAULT_BAD_KIDX = 0, 1, 2, 3
 DOC_SKIP_INVALID = 1
+# Batch.route bits (include/cedargpu.h CG_ROUTE_*)
+ROUTE_FU_BIG, ROUTE_FU_OVF, ROUTE_FU_GEN, ROUTE_FIRST_SLOT, ROUTE_RERUN, ROUTE_CLASS = 1, 2, 4, 8, 16, 32
 
 
 def _timeout_ns(timeout: Optional[float]) -> int:
@@ -265,8 +268,11 @@ def image_stats(image: bytes) -> dict:
     lib.cg_image_stats(image, len(image), *(ctypes.byref(x) for x in u[2:]))
     ix = ctypes.c_int(0)
     lib.cg_image_indexed(image, len(image), ctypes.byref(ix))
+    lw, lr = ctypes.c_uint32(), ctypes.c_uint32()
+    lib.cg_image_like_slots(image, len(image), ctypes.byref(lw), ctypes.byref(lr))
     return {"policies": u[0].value, "tiers": u[1].value, "epoch": ep.value, "atomic": u[2].value,
-            "hot": u[3].value, "actions": u[4].value, "stream_words": u[5].value, "indexed": bool(ix.value)}
+            "hot": u[3].value, "actions": u[4].value, "stream_words": u[5].value, "indexed": bool(ix.value),
+            "row_like_slots": bin(lw.value).count("1"), "like_read_mask": lr.value}
 
 
 def _buf(b: bytes):
@@ -331,12 +337,17 @@ class Context:
     def __init__(self, device: int = 0):
         self.device = device
         self._h = _P()
+        self._batches = weakref.WeakSet()  # open batches: a batch never outlives its context
         rc = lib.cg_ctx_create(device, ctypes.byref(self._h))
         if rc:
             raise DeviceError(rc, f"no usable GPU {device}: {lib.cg_last_error(None).decode()}")
 
     def close(self):
         if self._h:
+            # (cg_batch_destroy needs its context: a batch still referenced somewhere, e.g. by a
+            # failed test's traceback, is closed here rather than later against a freed context)
+            for b in list(self._batches):
+                b.close()
             lib.cg_ctx_destroy(self._h)
             self._h = _P()
 
@@ -408,6 +419,7 @@ class Batch:
         rc = lib.cg_batch_create(ctx._h, ctypes.byref(self._h))
         if rc:
             raise _err(rc, ctx.last_error())
+        ctx._batches.add(self)
 
     def close(self):
         if self._h:
@@ -513,6 +525,18 @@ class Batch:
         if rc:
             raise _err(rc, "reasons failed")
         return list(arr[:n.value]), ne.value
+
+    def route(self, i: int) -> int:
+        """How request i was finished: CG_ROUTE_* bits (ROUTE_* below; 0: the first pass alone)."""
+        return self.route_words(i)[0]
+
+    def route_words(self, i: int) -> Tuple[int, int]:
+        """(route bits, reason words the device wrote for request i's deciding list)."""
+        r, w = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        rc = lib.cg_batch_route(self._h, i, ctypes.byref(r), ctypes.byref(w))
+        if rc:
+            raise _err(rc, "route failed")
+        return r.value, w.value
 
     def reruns(self) -> int:
         """Requests whose result lists overflowed the first pass and were re-run (cg_batch_reruns)."""

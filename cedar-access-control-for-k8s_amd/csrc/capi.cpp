@@ -755,6 +755,18 @@ int cg_image_index_stats(const void* image, size_t len, uint32_t* cslot_mask, ui
 }
 
 // ---------------------------------------------------------------------------------------------
+int cg_image_like_slots(const void* image, size_t len, uint32_t* row_like_mask, uint32_t* like_read_mask) {
+  if (!image) return CG_E_ARG;
+  try {
+    auto img = Image::deserialize((const uint8_t*)image, len);
+    if (row_like_mask) *row_like_mask = img->lslot_mask;
+    if (like_read_mask) *like_read_mask = img->lread_mask;
+    return CG_OK;
+  } catch (const std::exception&) {
+    return CG_E_ARG;
+  }
+}
+
 int cg_image_policy_atomic(const void* image, size_t len, uint32_t i, int* atomic) {
   if (!image || !atomic) return CG_E_ARG;
   try {
@@ -1164,7 +1176,7 @@ int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t 
     if (!b->done) return CG_E_STATE;
     // authorizer.go:73-84 + diagnosticToReason (authorizer.go:113-124)
     std::vector<uint32_t> rs;
-    b->host.reason_ids((uint32_t)it.dev, rs);
+    GUARD_RESULT(b->err, { b->host.reason_ids((uint32_t)it.dev, rs); })
     if (b->host.decision((uint32_t)it.dev)) {
       *decision = AUTHZ_ALLOW;
     } else if (!rs.empty()) {
@@ -1173,7 +1185,7 @@ int cg_batch_authz(cg_batch* b, uint32_t i, int* decision, char* reason, size_t 
       *decision = AUTHZ_NO_OPINION;
     }
     if (*decision != AUTHZ_NO_OPINION && !rs.empty()) {
-      GUARD(b->err, { b->host.diagnostic_json((uint32_t)it.dev, r, false); })
+      GUARD_RESULT(b->err, { b->host.diagnostic_json((uint32_t)it.dev, r, false); })
     }
   }
   if (need) *need = r.size() + 1;
@@ -1307,9 +1319,9 @@ int cg_batch_admit(cg_batch* b, uint32_t i, int* allowed, int* code, char* msg, 
     const uint32_t d = (uint32_t)it.dev;
     *allowed = b->host.decision(d) ? 1 : 0;
     std::vector<uint32_t> rs;
-    b->host.reason_ids(d, rs);
+    GUARD_RESULT(b->err, { b->host.reason_ids(d, rs); })
     if (!*allowed && !rs.empty()) {  // json.Marshal(diagnostics.Reasons) (handler.go:62-66)
-      GUARD(b->err, { b->host.diagnostic_json(d, m, true); })
+      GUARD_RESULT(b->err, { b->host.diagnostic_json(d, m, true); })
     }
   }
   if (code) *code = c;
@@ -1509,6 +1521,7 @@ int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
       for (uint32_t k = 0; k < cnt; k++) {
         const uint32_t i = fu.ids[k] & ~0x80000000u;  // (FU_DONE: an entry the first pass finished)
         if (i >= n) { b->err = "follow-up worklist out of range"; return CG_E_DEVICE; }
+        b->routes.push_back((uint64_t)i << 8 | ((fu.ids[k] & 0x80000000u) ? CG_ROUTE_FIRST_SLOT : (CG_ROUTE_FU_BIG << q)));
         const uint32_t fl = fu.res[2 * k] >> 16;
         if (!(fl & cgi::RF_VALID) || (fl & (cgi::RF_GENERAL | cgi::RF_BIG))) continue;
         const uint32_t nr = fu.res[2 * k + 1] & 0xFFFF, ne = fu.res[2 * k + 1] >> 16;
@@ -1618,6 +1631,8 @@ int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
     return CG_OK;
   };
   b->n_rerun = (uint32_t)(idx_probe.size() + idx_big.size() + idx_gen.size());
+  for (const auto* v : {&idx_probe, &idx_big, &idx_gen})
+    for (const uint32_t i : *v) b->routes.push_back((uint64_t)i << 8 | CG_ROUTE_RERUN);
   int rc;
   tr.mark("scan");
   // First round: the three subsets are known from the first pass's flags, so their re-runs are
@@ -1689,6 +1704,32 @@ int cg::batch_wait(cg_batch* b, int64_t download_deadline, int64_t deadline) {
 
 extern "C" {
 
+int cg_batch_route(cg_batch* b, uint32_t i, uint32_t* route, uint32_t* reason_words) {
+  if (!b || !route) return CG_E_ARG;
+  if (!b->done) return CG_E_STATE;
+  if (i >= b->items.size()) return CG_E_RANGE;
+  if (b->items[i].dev < 0) return CG_E_STATE;
+  const uint32_t p = b->host.slot((uint32_t)b->items[i].dev);
+  if (!b->routes_sorted) {  // (position << 8 | bit) records of the fold, sorted once
+    std::sort(b->routes.begin(), b->routes.end());
+    b->routes_sorted = true;
+  }
+  uint32_t r = 0;
+  for (auto it = std::lower_bound(b->routes.begin(), b->routes.end(), (uint64_t)p << 8);
+       it != b->routes.end() && (*it >> 8) == p; ++it)
+    r |= (uint32_t)(*it & 0xFF);
+  // a duplicate class reported whole (RS_CLASS: its members listed on the host, Batch::reason_ids)
+  const uint32_t nr = b->host.res[2 * (size_t)p + 1] & 0xFFFF;
+  const Batch::BigRef* big = b->host.big_of(p);
+  const uint32_t* src = big ? big->r : (((b->host.res[2 * (size_t)p] >> 16) & cgi::RF_FORBID) ? b->host.reasons_f : b->host.reasons_p) + (size_t)p * b->host.capr;
+  const uint32_t cnt = big ? big->nr : std::min(nr, b->host.capr);
+  for (uint32_t k = 0; k < cnt; k++)
+    if (src[k] & cgi::RS_CLASS) { r |= CG_ROUTE_CLASS; break; }
+  *route = r;
+  if (reason_words) *reason_words = cnt;
+  return CG_OK;
+}
+
 int cg_batch_reruns(cg_batch* b, uint32_t* n) {
   if (!b || !n) return CG_E_ARG;
   if (!b->done) return CG_E_STATE;
@@ -1710,7 +1751,7 @@ int cg_batch_decision(cg_batch* b, uint32_t i, int* allow, uint32_t* tier) {
   if (b->items[i].dev < 0) return CG_E_STATE;
   i = (uint32_t)b->items[i].dev;
   *allow = b->host.decision(i) ? 1 : 0;
-  if (tier) *tier = (b->host.res[2 * (size_t)i] >> 8) & 0xFF;
+  if (tier) *tier = b->host.tier(i);
   return CG_OK;
 }
 
@@ -1721,7 +1762,7 @@ int cg_batch_diagnostic(cg_batch* b, uint32_t i, int reasons_only, char* buf, si
   if (b->items[i].dev < 0) return CG_E_STATE;
   i = (uint32_t)b->items[i].dev;
   std::string s;
-  GUARD(b->err, { b->host.diagnostic_json(i, s, reasons_only != 0); })
+  GUARD_RESULT(b->err, { b->host.diagnostic_json(i, s, reasons_only != 0); })
   if (need) *need = s.size() + 1;
   if (!buf || cap < s.size() + 1) return CG_E_RANGE;
   std::memcpy(buf, s.c_str(), s.size() + 1);
@@ -1735,8 +1776,10 @@ int cg_batch_reasons(cg_batch* b, uint32_t i, uint32_t* idx, uint32_t cap, uint3
   if (b->items[i].dev < 0) return CG_E_STATE;
   i = (uint32_t)b->items[i].dev;
   std::vector<uint32_t> rs, es;
-  b->host.reason_ids(i, rs);
-  b->host.error_recs(i, es);
+  GUARD_RESULT(b->err, {
+    b->host.reason_ids(i, rs);
+    b->host.error_recs(i, es);
+  })
   *n = (uint32_t)rs.size();
   if (n_errors) *n_errors = (uint32_t)(es.size() / cgi::ERR_WORDS);
   if (idx) for (uint32_t k = 0; k < cap && k < rs.size(); k++) idx[k] = rs[k];

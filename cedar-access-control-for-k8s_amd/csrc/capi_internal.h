@@ -44,6 +44,20 @@ struct CapHint {
     return CG_E_ARG;                                              \
   }
 
+// Result readers over device output (Batch::reason_ids, diagnostic_json): a malformed result word
+// (e.g. a reason naming no duplicate class) is a device fault, reported as CG_E_DEVICE, never an
+// exception across the C ABI.
+#define GUARD_RESULT(errstr, body)                                \
+  try {                                                           \
+    body                                                          \
+  } catch (const std::bad_alloc&) {                               \
+    errstr = "out of host memory";                                \
+    return CG_E_ARG;                                              \
+  } catch (const std::exception& e) {                             \
+    errstr = std::string("malformed device result: ") + e.what(); \
+    return CG_E_DEVICE;                                           \
+  }
+
 }  // namespace cg
 
 using cg::LoadedImage;
@@ -83,6 +97,10 @@ struct cg_batch {
   bool downloaded = false;  // the first pass's results (and follow-ups) are in the pinned block
   int failed = 0;        // a host re-run missed its deadline: every later wait returns this
   uint32_t n_rerun = 0;  // requests re-run by cg_batch_wait
+  // cg_batch_route: (slot << 8 | CG_ROUTE_* bit) per request a follow-up worklist or a host re-run
+  // finished, appended by the fold (27k of C3's 1M), sorted on the first query
+  std::vector<uint64_t> routes;
+  bool routes_sorted = false;
   uint32_t n_fu[cg::FU_KINDS] = {0, 0, 0};  // requests finished by each on-device follow-up worklist
   std::string err;
   // items: caller-visible entries; dev >= 0 is the device request index, else a fast-path result
@@ -97,11 +115,17 @@ struct cg_batch {
     if (dev.direct && dev.pending) {
       // inputs were copied straight from these arrays (pinned blocks) and the copy may still run:
       // they go with the retired batch and return to the pinned pool once its stream drains
-      struct Arrays { cg::PinVec<uint32_t> heap, req_base, rows, gkeys, bstr_off; cg::PinVec<uint8_t> bstr_bytes; };
+      // (dstr_off / dstr_bytes: the device string table of an all-atomic image, uploaded in place
+      // of bstr_* and as liable to be copied straight from its pinned block)
+      struct Arrays {
+        cg::PinVec<uint32_t> heap, req_base, rows, gkeys, bstr_off, dstr_off;
+        cg::PinVec<uint8_t> bstr_bytes, dstr_bytes;
+      };
       try {
         auto a = std::make_shared<Arrays>();
         a->heap.swap(host.heap); a->req_base.swap(host.req_base); a->rows.swap(host.rows);
         a->gkeys.swap(host.gkeys); a->bstr_off.swap(host.bstr_off); a->bstr_bytes.swap(host.bstr_bytes);
+        a->dstr_off.swap(host.dstr_off); a->dstr_bytes.swap(host.dstr_bytes);
         dev.keep = std::move(a);
         cg::g_pinned_kept.fetch_add(1, std::memory_order_relaxed);
       } catch (...) {

@@ -106,10 +106,14 @@ struct KArgs {
   uint32_t scan_heavy;  // more candidate heads than this: straight to the large stage (CEDARGPU_SCAN_HEAVY)
   uint32_t cnt_rank;    // merges of <= this many hits per request rank by counting (CEDARGPU_CNT_RANK)
   uint32_t n_static, smask, lane_stride;
-  // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>): per request its bucket
-  // count at scan[i] (SCAN_OVF: more than SCAN_CAP), its (first head, count | combo) pairs at
-  // scan + scan_n + i * 2 * SCAN_CAP
+  // split first pass (cedar_scan_kernel -> cedar_probe_kernel<.., SPLIT>), by position p of the
+  // launch order (wave w = p / 8 holds positions 8w .. 8w + 7): p's bucket count at scan[p]
+  // (SCAN_OVF: some of its buckets did not fit its wave's list); wave w's list total at scan_tot[w]
+  // and its list at scan_list + w * 2 * WAVE_CAP: the wave's (first head | p % 8 << SCAN_SEG_SHIFT,
+  // count | combo << SCAN_COMBO_SHIFT) pairs, packed in the order the scan found them
   uint32_t* scan;
+  uint32_t* scan_tot;
+  uint32_t* scan_list;
   uint32_t scan_n;
   // one-launch small batches (DevBatch::small): a request whose deciding list outgrows capr takes
   // an overflow slot (ovf_cnt: slots taken) and writes its whole result there, laid out like a
@@ -137,14 +141,16 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
   const uint32_t x = b & 7u, j = b >> 3;
   return ((j / C) * 8u + x) * C + (j % C);
 }
-// SCAN_CAP: bucket pairs a request's list holds (more: SCAN_OVF, the large stage probes the index
+// SCAN_CAP: bucket pairs per request of a wave's list (WAVE_CAP per wave of 8 requests, packed:
+// a request whose buckets do not all fit gets SCAN_OVF, and the large stage probes the index
 // itself); a request with more than KArgs::scan_big buckets skips the candidate pass and goes to
 // the large stage, which reads the list when it holds them all
 // a follow-up worklist entry the first pass already finished (its id | FU_DONE): the follow-up
 // launch skips it, the host folds its result as any other
 constexpr uint32_t FU_DONE = 0x80000000u;
 constexpr uint32_t SCAN_CAP = 96, SCAN_OVF = 0xFFFFFFFFu, SCAN_COUNT = (1u << 27) - 1, SCAN_COMBO_SHIFT = 27;
-static_assert(SCAN_CAP >= 64, "the SPLIT probe kernel reads one pair per lane (up to 64) before it knows the count");
+constexpr uint32_t WAVE_CAP = 8 * SCAN_CAP, SCAN_SEG_SHIFT = 27;  // (first heads stay below 2^27: EF_FIRST)
+static_assert(WAVE_CAP >= 128, "the candidate pass reads two pairs per lane (128) before it knows the total");
 // scan[i] | SCAN_HEAVY: the request's buckets hold more than a.scan_heavy candidate heads, so it
 // goes straight to the large stage (the candidate pass would overflow its 64 hits and be redone)
 constexpr uint32_t SCAN_HEAVY = 0x40000000u;
@@ -620,7 +626,9 @@ template <class CT>
 __device__ __forceinline__ bool likei(const CT& c, uint32_t h, uint32_t sid, uint32_t p0, uint32_t p1, uint32_t f) {
   uint32_t len;
   uint64_t pre = 0, suf = 0;
-  if (c.lkb != 0xFFFFFFFFu) {
+  // (only a slot of c.lslot has staged words: an atom lowered without them, e.g. one an incremental
+  // build kept from an image compiled with another like-words choice, reads the string)
+  if (c.lkb != 0xFFFFFFFFu && h < 32u && ((c.lslot >> h) & 1u)) {
     const uint32_t k = c.lkb + 3u * (uint32_t)__popc(c.lslot & ((1u << h) - 1u));
     const uint2 x = hot_get(c, k), y = hot_get(c, k + 1), z = hot_get(c, k + 2);
     len = x.x;
@@ -1322,8 +1330,12 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;  // follow-up: count on the device
   const bool valid = gid < n_req;
-  const uint32_t r = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0;
-  const uint32_t wo = a.req_idx ? gid : r;  // result slot: the worklist entry, or the request itself
+  // position p in the first pass's launch order (first pass: gid; follow-up: its worklist entry's),
+  // the request's row r (ord[p] for a batch grouped on the device); the result slot is the worklist
+  // entry, or the position
+  const uint32_t p = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0;
+  const uint32_t r = valid ? (a.ord ? a.ord[p] : p) : 0;
+  const uint32_t wo = a.req_idx ? gid : p;
 
   uint32_t lane_scratch[GLANE ? 1 : LANE_WORDS];
   Ctx c;
@@ -1569,6 +1581,10 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t lane) {
 
 // bucket words in LDS: first head index | key combo << EF_COMBO (the image keeps heads below 2^27)
 constexpr uint32_t EF_COMBO = 27, EF_FIRST = (1u << EF_COMBO) - 1u;
+// the pooled candidate pass's staged prefixes: exclusive candidate prefix | segment << FP_SEG (a
+// round's candidates stay below 2^24: its requests hold <= KArgs::scan_heavy heads each), and the
+// list pairs it stages per round
+constexpr uint32_t FP_SEG = 24, FP_PRE = (1u << FP_SEG) - 1u, FLAT_PAIRS = 128;
 // segments with a FLAT state region (only the 8-lane candidate pass uses it)
 constexpr uint32_t FLAT_NS(uint32_t seg) { return seg == 8 ? 8u : 1u; }
 // Per-wave LDS of the probe kernel, one region per request segment of SEG lanes.
@@ -1734,7 +1750,7 @@ constexpr uint32_t SCAN_ANC = 40;
 constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
 // contexts a request looks up in the scope-bitset pass (more: it enumerates every key instead), and
 // the flag of a listed key the bitsets found (image.h "scope bitsets")
-constexpr uint32_t CTX_CAP = 16, LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;
+constexpr uint32_t LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;  // (CTX_CAP: image.h)
 constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the rest read from the row)
 constexpr uint32_t SCAN_ROW = 56;  // scan LDS row words (64 - 8: see s_kid; the LDS stays under 1/24 of a CU for 6 waves per SIMD)
 static_assert(SCAN_ANC + 2 <= SCAN_ROW && SCAN_POS_B + 2 <= SCAN_ROW, "scan LDS rows");
@@ -1793,10 +1809,14 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sbase);
   auto sballot = [&](bool p) -> uint64_t { return __ballot(p) & smask; };
   auto sbcast = [&](uint32_t x, uint32_t k) -> uint32_t { return (uint32_t)__shfl((int)x, (int)(sbase + k)); };
-  const uint32_t gid_ = xcd_block(blockIdx.x, gridDim.x, a.ord ? a.xcd_chunk : 0u) * (64 / SEG) + seg;
+  static_assert(SEG == 8, "a wave's list is shared by its 8 requests");
+  // this request's position in the launch order (its count word and its wave's list; the request
+  // itself, its row, is ord[position] when the batch was grouped)
+  const uint32_t wv = xcd_block(blockIdx.x, gridDim.x, a.ord ? a.xcd_chunk : 0u);
+  const uint32_t gid_ = wv * (64 / SEG) + seg;
   const bool valid = gid_ < a.n_req;
-  const uint32_t gid = valid ? (a.ord ? a.ord[gid_] : gid_) : 0u;  // the request (its list and results)
-  const uint32_t* row = a.grows ? a.grows + (size_t)(valid ? gid_ : 0u) * a.row_words : a.rows + (size_t)gid * a.row_words;
+  const uint32_t* row = a.grows ? a.grows + (size_t)(valid ? gid_ : 0u) * a.row_words
+                                : a.rows + (size_t)(valid ? (a.ord ? a.ord[gid_] : gid_) : 0u) * a.row_words;
   const uint32_t rw = (valid && sl < RW_HDR) ? row[sl] : 0u;
   const uint32_t rw_hi = (SEG < RW_HDR && valid && SEG + sl < RW_HDR) ? row[SEG + sl] : 0u;
   auto hdr = [&](uint32_t k) -> uint32_t { return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG); };
@@ -1813,7 +1833,10 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       const uint32_t cb = __builtin_ctz(m);
       n_keys += ((cb & 3) == KC_ENT ? nP : 1u) * (((cb >> 2) & 1) == KC_ENT ? nA : 1u) * ((cb >> 3) == KC_ENT ? nR : 1u);
     }
-  uint32_t* pairs = a.scan + a.scan_n + (size_t)gid * (2 * SCAN_CAP);
+  // the wave's list: its 8 requests' buckets packed together in found order (each pair tagged with
+  // its request's segment), so the wave writes a few whole lines and the candidate pass, which
+  // pools the wave's candidates anyway, reads them back in one or two coalesced loads
+  uint32_t* pairs = a.scan_list + (size_t)wv * (2 * WAVE_CAP);
   // scope-bitset pass (image.h "scope bitsets"): the principal's list carries the kidx of its owner
   // and key ancestors after its pairs (p_anc == 0: the principal has no entity, no list)
   const bool kbits = BITS && a.scan_filt && a.sbits_words != 0;
@@ -1823,7 +1846,12 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const uint32_t nk = (pn >> AN_KEYS_SHIFT) & AN_KEYS;
   constexpr uint32_t LW = 3;  // list elements loaded with a list head
   uint32_t l_lo = 0, l_hd = 0, l_w[LW] = {0, 0, 0};
+  // contexts the encoder resolved (image.h RH_SCTX; the row says so): lanes sl < CTXR_SLOTS read
+  // them with the key-entity list, and the list slots' heads are not needed
+  const bool hres = BITS && klist && (hdr(RW_ASELF) & ASELF_CTXR) != 0;
+  uint32_t hcx = CTXR_EMPTY;
   {
+    if (hres && sl < CTXR_SLOTS) hcx = blk[RH_SCTX + sl];
     if (stl) {
       const uint32_t n_st = valid ? min(nk, ANC_ST) : 0u;
       for (uint32_t j = sl; j < n_st; j += SEG)
@@ -1835,7 +1863,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     }
     // BITS: lane k < popc(l2_lmask) reads the k-th list slot's head and first LW words after it
     // (element count or marker, elements) in the same trip
-    if (BITS && klist && a.hlists && sl < (uint32_t)__builtin_popcount(a.l2_lmask)) {
+    if (BITS && klist && !hres && a.hlists && sl < (uint32_t)__builtin_popcount(a.l2_lmask)) {
       l_lo = row[RW_HDR + 2 * a.n_hot + __popc(a.hlists & ((1u << nth_bit(a.l2_lmask, sl)) - 1u))];
       l_hd = blk[l_lo];
 #pragma unroll
@@ -1907,13 +1935,20 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       if (sl >= o) linc += y;
     }
     const uint32_t per = 1u + nvs + sbcast(linc, SEG - 1), nctx = ncb * per;
-    on = on && nctx <= CTX_CAP;
-    // the contexts, looked up side by side (lane j % SEG takes context j); a found one is kept
+    on = on && (hres || nctx <= CTX_CAP);
     uint32_t nf = 0;  // contexts found (segment-uniform)
-    for (uint32_t j0 = 0; __ballot(on && j0 < nctx) != 0; j0 += SEG) {
+    const bool look = on && !hres;
+    if (hres) {  // resolved by the encoder: CTXR_EMPTY after the last
+      const bool got = sl < CTXR_SLOTS && hcx != CTXR_EMPTY;
+      const uint64_t mk = sballot(got);
+      if (got) s_cx[seg][mbcnt64(mk)] = make_uint2(hcx & ((1u << CTXR_ROW) - 1u), hcx >> CTXR_ROW);
+      nf = popc64(mk);
+    }
+    // the contexts, looked up side by side (lane j % SEG takes context j); a found one is kept
+    for (uint32_t j0 = 0; __ballot(look && j0 < nctx) != 0; j0 += SEG) {
       const uint32_t j = j0 + sl;
       uint32_t cb = 0, hs = SCTX_L1, v0 = 0, v1 = 0, row_ = KIDX_NONE;
-      const uint32_t ci = on ? j / per : 0u, t = on ? j - ci * per : 0u;
+      const uint32_t ci = look ? j / per : 0u, t = look ? j - ci * per : 0u;
       // (the list entry, by shuffles from the lane that read its slot: every lane takes part)
       uint32_t li = 0, lb = 0, llo = 0, lhd = 0, lw = 0;
       for (uint32_t k = 0; k < nls; k++) {
@@ -1929,7 +1964,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
         const uint32_t lo_k = sbcast(l_lo, k), hd_k = sbcast(l_hd, k);
         if (mine) { li = k; lb = inc_k - c_k; llo = lo_k; lhd = hd_k; lw = w; }
       }
-      if (on && j < nctx) {
+      if (look && j < nctx) {
         cb = nth_bit(pe, ci);
         if (t > 0 && t <= nvs) {
           hs = nth_bit(vm, t - 1);
@@ -1969,7 +2004,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           }
         }
       }
-      const bool got = on && j < nctx && row_ != KIDX_NONE;
+      const bool got = look && j < nctx && row_ != KIDX_NONE;
       const uint64_t mk = sballot(got);
       if (got) s_cx[seg][nf + mbcnt64(mk)] = make_uint2(cb | (hs << 8), row_);
       nf += popc64(mk);
@@ -2043,6 +2078,8 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const uint64_t t1 = STATS ? clock64() : 0;
   if (STATS && valid && sl == 0) { st[0] = 1; st[10] = n_keys; }
   uint32_t kb = 0, hm = 0, h1 = 0, w0 = 0, combo = 0, nb = 0, unused = 0, heads = 0;
+  uint32_t wn = 0;        // the wave's list length so far (wave-uniform)
+  bool dropped = false;   // a bucket of this lane's request found no room in the wave's list
   uint2 kp = make_uint2(0, 0), ka = kp, kr = kp;
   uint4 blm = make_uint4(0, 0, 0, 0);
   uint32_t csl = 0, ch = 0, cl = 0, ck = 0, cn = 0;
@@ -2129,16 +2166,24 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       }
     }
     if (STATS && l2 && e.y) st[4]++;
-    // found buckets go to the request's list in segment order
-    const uint64_t m = sballot(e.y != 0);
-    const uint32_t pos = nb + mbcnt64(m);
-    if (e.y && pos < SCAN_CAP)
-      *reinterpret_cast<uint2*>(pairs + 2 * pos) = make_uint2(e.x, min(e.y, SCAN_COUNT) | (combo << SCAN_COMBO_SHIFT));
-    nb += popc64(m);
+    // found buckets go to the wave's list in lane order
+    const uint64_t m = __ballot(e.y != 0);
+    const uint32_t pos = wn + mbcnt64(m);
+    if (e.y) {
+      if (pos < WAVE_CAP)
+        *reinterpret_cast<uint2*>(pairs + 2 * pos) =
+            make_uint2(e.x | (seg << SCAN_SEG_SHIFT), min(e.y, SCAN_COUNT) | (combo << SCAN_COMBO_SHIFT));
+      else
+        dropped = true;
+    }
+    wn += popc64(m);
+    nb += popc64(m & smask);
     heads += min(e.y, SCAN_COUNT);
   }
   for (uint32_t o = SEG / 2; o > 0; o >>= 1) heads += (uint32_t)__shfl_xor((int)heads, (int)o);  // over the segment
-  if (valid && sl == 0) a.scan[gid] = nb <= SCAN_CAP ? (nb | (heads > a.scan_heavy ? SCAN_HEAVY : 0u)) : SCAN_OVF;
+  const bool ovf = sballot(dropped) != 0;
+  if (valid && sl == 0) a.scan[gid_] = ovf ? SCAN_OVF : (nb | (heads > a.scan_heavy ? SCAN_HEAVY : 0u));
+  if (lane == 0) a.scan_tot[wv] = min(wn, WAVE_CAP);
   if (STATS) {
     const uint64_t t2 = clock64();
     if (lane == 0) { st[8] = (uint32_t)(t1 - t0); st[9] = (uint32_t)(t2 - t1); }
@@ -2193,10 +2238,21 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   const uint32_t gid = (blk_w * PW + (threadIdx.x >> 6)) * NS + seg;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;
   bool valid = gid < n_req;
-  const uint32_t r0 = valid ? (a.req_idx ? a.req_idx[gid] : (a.ord ? a.ord[gid] : gid)) : 0u;
-  if (a.req_idx && (r0 & FU_DONE)) valid = false;  // finished by the first pass (its overflow slot)
-  const uint32_t r = valid ? r0 : 0u;
-  const uint32_t* row = (a.grows && !a.req_idx) ? a.grows + (size_t)(valid ? gid : 0u) * a.row_words : a.rows + (size_t)r * a.row_words;
+  // the request's position p in the first pass's launch order (first pass: gid; follow-up: its
+  // worklist entry): its scan list and first-pass results are at p, its row at ord[p] when the
+  // batch was grouped on the device (grows[p] when the rows were copied into that order)
+  const uint32_t p0 = valid ? (a.req_idx ? a.req_idx[gid] : gid) : 0u;
+  if (a.req_idx && (p0 & FU_DONE)) valid = false;  // finished by the first pass (its overflow slot)
+  if constexpr (SEG == 64 && !STATS) {
+    if (!valid) return;  // (a one-request wave with no request: wave-level work only, no block barrier)
+  }
+  const uint32_t p = valid ? p0 : 0u;
+  const uint32_t* row = a.grows ? a.grows + (size_t)p * a.row_words : a.rows + (size_t)(a.ord ? a.ord[p] : p) * a.row_words;
+  // FLAT (the SPLIT candidate pass with 8-lane segments): the wave's lanes take candidates from a
+  // pool over all of its requests, so each segment's request context and running state live in LDS
+  constexpr bool FLAT = SPLIT && SEG == 8;
+  static_assert(!SPLIT || FLAT || SEG == 64, "the split pass's list readers: the pooled candidate pass or the large stage");
+  static_assert(!FLAT || (NS == 8 && NS * L::EC >= 128), "the pooled candidate pass stages 128 list pairs of its wave");
 
   // the request row streams through once: non-temporal loads, header broadcast in the segment
   const uint32_t rw = (valid && sl < RW_HDR) ? __builtin_nontemporal_load(row + sl) : 0u;
@@ -2208,23 +2264,23 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     if constexpr (SEG == 64) return (uint32_t)__builtin_amdgcn_readlane((int)rw, (int)k);
     return (SEG >= RW_HDR || k < SEG) ? sbcast(rw, k) : sbcast(rw_hi, k - SEG);
   };
-  // SPLIT: the scan list's count and each lane's first bucket pair, issued with the row loads (they
-  // depend only on r), so the staging below does not wait for a second trip after the row's
-  uint32_t scan_nb0 = 0;
+  // SPLIT: the request's count word, its wave's list total and the list's first 64 (FLAT: 128)
+  // pairs, one or two per lane, issued with the row loads (they depend only on the position), so
+  // the staging below does not wait for a second trip after the row's. (Past the total the loads
+  // read stale pairs of the list's fixed WAVE_CAP region, which the staging ignores.)
+  uint32_t scan_nb0 = 0, scan_tot0 = 0;
   uint2 scan_q0 = make_uint2(0u, 0u), scan_q1 = make_uint2(0u, 0u);
+  const uint32_t scan_w = FLAT ? gid / NS : p / 8u;  // the wave of the scan that listed the request
+  const uint2* scan_l = SPLIT ? reinterpret_cast<const uint2*>(a.scan_list + (size_t)scan_w * (2 * WAVE_CAP)) : nullptr;
   if constexpr (SPLIT) {
-    if (valid) {
-      scan_nb0 = a.scan[r];
-      scan_q0 = *reinterpret_cast<const uint2*>(a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP) + 2 * sl);
-      // 8-lane segments: each lane's second pair too (a request of 9..16 buckets then stages with no
-      // second trip; SCAN_CAP >= 64 keeps it inside the request's list)
-      if constexpr (SEG == 8)
-        scan_q1 = *reinterpret_cast<const uint2*>(a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP) + 2 * (sl + SEG));
-    }
+    if (valid) scan_nb0 = a.scan[p];
+    scan_tot0 = a.scan_tot[scan_w];
+    scan_q0 = scan_l[lane];
+    if constexpr (FLAT) scan_q1 = scan_l[64 + lane];
   }
   PCtx c;
   c.blk = a.heap + hdr(RW_BLK);
-  c.rowb = (a.grows && !a.req_idx) ? a.grows : a.rows;
+  c.rowb = a.grows ? a.grows : a.rows;
   c.rowo = (valid && a.hlists) ? (uint32_t)(row - c.rowb) + RW_HDR + 2 * a.n_hot : 0xFFFFFFFFu;
   c.lmask = a.hlists;
   c.cpool = a.cpool;
@@ -2260,13 +2316,10 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   uint32_t aself = 0xFFFFu;
   if (a.amask_ok) {
     am = ((uint64_t)hdr(RW_AM1) << 32) | hdr(RW_AM0);
-    const uint32_t self = hdr(RW_ASELF);
+    const uint32_t self = hdr(RW_ASELF) & ASELF_MASK;
     as = (valid && self < 64u) ? (1ull << self) : 0ull;
     aself = (valid && self < 64u) ? self : 0xFFFFu;
   }
-  // FLAT (the SPLIT candidate pass with 8-lane segments): the wave's lanes take candidates from a
-  // pool over all of its requests, so each segment's request context and running state live in LDS
-  constexpr bool FLAT = SPLIT && SEG == 8;
   if constexpr (FLAT) {
     // (every value here was read with the whole wave active: hdr() is a cross-lane read)
     const uint32_t blk_off = (uint32_t)(c.blk - a.heap);
@@ -2274,7 +2327,7 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
       wl.cx[seg][0] = make_uint4(blk_off, c.pt, c.pi, c.at);
       wl.cx[seg][1] = make_uint4(c.ai, c.rt, c.ri, c.p_anc);
       wl.cx[seg][2] = make_uint4(c.r_anc, c.a_anc, c.p_nanc | (c.r_nanc << 16), c.a_nanc | (aself << 16));
-      wl.cx[seg][3] = make_uint4(c.rowo, (uint32_t)am, (uint32_t)(am >> 32), r);  // (r: the merge's result slot)
+      wl.cx[seg][3] = make_uint4(c.rowo, (uint32_t)am, (uint32_t)(am >> 32), 0u);
       wl.sst[seg][0] = 0u;
       wl.sst[seg][1] = 0u;
       wl.sst[seg][2] = a.n_tiers - 1;
@@ -2478,41 +2531,27 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   // its candidate's request context from LDS; hits, error details, the lowest hit tier and the
   // structural flag go to that request's region through LDS atomics (the merge orders hits by policy,
   // so their slots' order does not matter).
-  auto flush_flat = [&]() {
+  // The staged pairs (n_e of them, FLAT_PAIRS at most) are flat LDS arrays over the wave: ff[i] the
+  // bucket word (first head | combo), fp[i] the exclusive prefix of the candidate counts | the
+  // pair's segment << FP_SEG; W candidates in all (a request whose hits overflowed staged none).
+  auto flush_flat = [&](uint32_t W, uint32_t n_e) {
     const uint64_t t_c0 = STATS ? clock64() : 0;
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; __ballot(b0 < ne); b0 += SEG) {
-      const uint32_t b = b0 + sl;
-      const uint32_t cnt = b < ne ? wl.u.b.epre[seg][b] : 0u;
-      const uint32_t inc = sscan(cnt);
-      wave_lds_sync();
-      if (b < ne) wl.u.b.epre[seg][b] = carry + inc - cnt;
-      carry += sbcast(inc, SEG - 1);
-      wave_lds_sync();
-    }
-    // a request whose hits already overflowed takes no more candidates (the large stage redoes it)
-    const uint32_t mine = wl.sst[seg][0] > L::HC ? 0u : carry;
-    uint32_t cum[NS + 1];
-    cum[0] = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < NS; k++) cum[k + 1] = cum[k] + (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)(k * SEG));
-    const uint32_t W = cum[NS];
+    const uint32_t* ff = &wl.u.b.efirst[0][0];
+    const uint32_t* fp = &wl.u.b.epre[0][0];
     for (uint32_t base = 0; base < W; base += 64) {
       const uint32_t g = base + lane;
       bool ok = g < W;
-      uint32_t s = 0, cb = 0;
-#pragma unroll
-      for (uint32_t k = 1; k < NS; k++)
-        if (g >= cum[k]) { s = k; cb = cum[k]; }
-      const uint32_t idx = g - cb;
-      uint32_t lo = 0, hi = ok ? wl.sne[s] : 1u;  // bucket of candidate idx: last b with epre[b] <= idx
+      uint32_t lo = 0, hi = n_e;  // the pair of candidate g: the last i with prefix[i] <= g (a pair
+                                  // of no candidates shares its prefix with the next one, so never)
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (wl.u.b.epre[s][mid] <= idx) lo = mid;
+        if ((fp[mid] & FP_PRE) <= g) lo = mid;
         else hi = mid;
       }
-      const uint32_t ef = ok ? wl.u.b.efirst[s][lo] : 0u;
-      const uint32_t hidx = ok ? (ef & EF_FIRST) + (idx - wl.u.b.epre[s][lo]) : 0u;
+      const uint32_t fw = fp[lo];
+      const uint32_t s = ok ? fw >> FP_SEG : 0u;
+      const uint32_t ef = ok ? ff[lo] : 0u;
+      const uint32_t hidx = ok ? (ef & EF_FIRST) + (g - (fw & FP_PRE)) : 0u;
       const uint32_t bcombo = ef >> EF_COMBO;
       const uint32_t* head = a.bstream + (size_t)(CG_DBG == 4 ? 0u : hidx) * HEAD_WORDS;
       const uint4* d4 = reinterpret_cast<const uint4*>(head);
@@ -2669,33 +2708,81 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
     const bool heavy = nb0 != SCAN_OVF && (nb0 & SCAN_HEAVY);
     const uint32_t nb = nb0 == SCAN_OVF ? SCAN_OVF : (nb0 & ~SCAN_HEAVY);
     if (SEG == 64 && nb == SCAN_OVF) probe_loop = true;
-    uint32_t nbk = nb == SCAN_OVF ? 0u : nb;
     const bool skip = SEG < 64 && nb != SCAN_OVF && (nb > a.scan_big || heavy) && !a.req_idx;
-    if (skip) nbk = 0;
     if (SEG < 64 && (nb == SCAN_OVF || skip)) nh = L::HC + 1;
+    const uint32_t tot = scan_tot0;
     if constexpr (FLAT) {
+      // The wave's list, FLAT_PAIRS pairs a round: each pair's candidates counted unless its request
+      // is out (skipped, overflowed list, or more hits than this pass holds: the large stage redoes
+      // it), prefix-summed over the wave into LDS, then run as one pool (flush_flat).
       if (sl == 0) wl.sst[seg][0] = nh;
       wave_lds_sync();
-    }
-    const uint32_t* pairs = a.scan + a.scan_n + (size_t)r * (2 * SCAN_CAP);
-    for (uint32_t b0 = 0; __ballot(b0 < nbk); b0 += L::EC) {
-      for (uint32_t i = sl; i < L::EC; i += SEG)
-        if (b0 + i < nbk) {
-          const uint2 q = (b0 == 0 && i == sl) ? scan_q0
-                          : (SEG == 8 && b0 == 0 && i == sl + SEG) ? scan_q1
-                                                                   : *reinterpret_cast<const uint2*>(pairs + 2 * (b0 + i));
-          wl.u.b.efirst[seg][i] = q.x | ((q.y >> SCAN_COMBO_SHIFT) << EF_COMBO);
-          wl.u.b.epre[seg][i] = q.y & SCAN_COUNT;
+      uint32_t* ff = &wl.u.b.efirst[0][0];
+      uint32_t* fp = &wl.u.b.epre[0][0];
+      for (uint32_t b0 = 0; b0 < tot; b0 += FLAT_PAIRS) {
+        const uint32_t i0 = b0 + lane, i1 = b0 + 64 + lane;
+        const uint2 qa = b0 == 0 ? scan_q0 : (i0 < tot ? scan_l[i0] : make_uint2(0u, 0u));
+        const uint2 qb = b0 == 0 ? scan_q1 : (i1 < tot ? scan_l[i1] : make_uint2(0u, 0u));
+        const uint32_t sa = (qa.x >> SCAN_SEG_SHIFT) & 7u, sb = (qb.x >> SCAN_SEG_SHIFT) & 7u;
+        const uint32_t ca = (i0 < tot && wl.sst[sa][0] <= L::HC) ? (qa.y & SCAN_COUNT) : 0u;
+        const uint32_t cb = (i1 < tot && wl.sst[sb][0] <= L::HC) ? (qb.y & SCAN_COUNT) : 0u;
+        const uint32_t ia = wave_scan(ca, lane);
+        const uint32_t ta = (uint32_t)__builtin_amdgcn_readlane((int)ia, 63);
+        const uint32_t ib = wave_scan(cb, lane) + ta;
+        ff[lane] = (qa.x & EF_FIRST) | ((qa.y >> SCAN_COMBO_SHIFT) << EF_COMBO);
+        ff[64 + lane] = (qb.x & EF_FIRST) | ((qb.y >> SCAN_COMBO_SHIFT) << EF_COMBO);
+        fp[lane] = (ia - ca) | (sa << FP_SEG);
+        fp[64 + lane] = (ib - cb) | (sb << FP_SEG);
+        const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)ib, 63);
+        wave_lds_sync();
+        if constexpr (STATS) {
+          // candidate sharing (profiling): the round's candidates, and those of its distinct buckets
+          // (a bucket's heads are one range, so the wave's pairs of one bucket share every head),
+          // summed over the launch behind the per-wave counters
+          const uint32_t n_e = min(FLAT_PAIRS, tot - b0);
+          uint32_t tc = 0, dc = 0;
+          for (uint32_t u = 0; u < 2; u++) {
+            const uint32_t i = u * 64 + lane, c = u ? cb : ca;
+            if (i >= n_e || !c) continue;
+            bool first = true;
+            for (uint32_t j = 0; j < i && first; j++) {
+              const uint32_t pj = fp[j] & FP_PRE, pn = j + 1 < n_e ? (fp[j + 1] & FP_PRE) : W;
+              first = !(pn > pj && (ff[j] & EF_FIRST) == (ff[i] & EF_FIRST));
+            }
+            tc += c;
+            dc += first ? c : 0u;
+          }
+          for (uint32_t o = 32; o > 0; o >>= 1) {
+            tc += (uint32_t)__shfl_xor((int)tc, (int)o);
+            dc += (uint32_t)__shfl_xor((int)dc, (int)o);
+          }
+          if (lane == 0) {
+            atomicAdd(a.stats + (size_t)gridDim.x * 16, (unsigned long long)tc);
+            atomicAdd(a.stats + (size_t)gridDim.x * 16 + 1, (unsigned long long)dc);
+          }
         }
-      ne = b0 < nbk ? min(L::EC, nbk - b0) : 0u;
-      if constexpr (FLAT) {
-        if (sl == 0) wl.sne[seg] = ne;
+        flush_flat(W, min(FLAT_PAIRS, tot - b0));
       }
-      wave_lds_sync();
-      if constexpr (FLAT) flush_flat();
-      else flush();
-      // more hits than this pass holds: the large stage redoes the request, so stop here
-      if (SEG < 64 && nh > L::HC) nbk = 0;
+    } else if (nb != SCAN_OVF) {
+      // the large stage (one request per wave): this request's pairs of its wave's list, picked by
+      // their segment tag 64 at a time and staged in found order
+      const uint32_t t = p & 7u;
+      for (uint32_t b0 = 0; b0 < tot; b0 += 64) {
+        const uint32_t i = b0 + lane;
+        const uint2 q = b0 == 0 ? scan_q0 : (i < tot ? scan_l[i] : make_uint2(0u, 0u));
+        const bool mine = i < tot && ((q.x >> SCAN_SEG_SHIFT) & 7u) == t;
+        const uint64_t m = __ballot(mine);
+        if (mine) {
+          const uint32_t at = ne + mbcnt64(m);
+          wl.u.b.efirst[0][at] = (q.x & EF_FIRST) | ((q.y >> SCAN_COMBO_SHIFT) << EF_COMBO);
+          wl.u.b.epre[0][at] = q.y & SCAN_COUNT;
+        }
+        ne += popc64(m);
+        if (ne + 64 > L::EC || b0 + 64 >= tot) {
+          wave_lds_sync();
+          if (ne) flush();
+        }
+      }
     }
   }
   if (probe_loop)
@@ -2815,7 +2902,8 @@ __global__ __launch_bounds__(PW * 64, MINW) void cedar_probe_kernel(KArgs a) {
   valid = gid_m < n_req && !(a.req_idx && (a.req_idx[gid_m] & FU_DONE));
   // result slot (FLAT: the request index parked in its context row, an LDS read instead of a
   // dependent reload of the order)
-  const uint32_t wo = a.req_idx ? gid_m : (valid ? (FLAT ? wl.cx[seg][3].w : (a.ord ? a.ord[gid_m] : gid_m)) : 0u);
+  // result slot: the request's position (first pass) or its worklist entry (follow-up)
+  const uint32_t wo = valid ? gid_m : 0u;
   const uint32_t t = min_tier;
   const bool structural = sballot(general) != 0;
   const bool undecided = (CG_DBG == 3 && FLAT) ? false : (nh > L::HC || nx > L::XC || structural);
@@ -3639,6 +3727,8 @@ StagePool& stage_pool() {
 }
 }  // namespace
 
+static size_t scan_words(uint32_t n);
+
 int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, DevPool* pool) {
   HIPCHK(hipSetDevice(device), "hipSetDevice");
   hipStream_t s = (hipStream_t)stream;
@@ -3698,7 +3788,10 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   const size_t budget_k[FU_KINDS] = {std::min<size_t>(256u << 20, std::max<size_t>(16u << 20, (size_t)b.n() * 2048)),
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024)),
                                      std::min<size_t>(64u << 20, std::max<size_t>(8u << 20, (size_t)b.n() * 1024))};
-  size_t o_fu = o_er + al(n * d.cape * ERR_WORDS * 4);
+  // a grouped batch's pos_of (the gather kernel writes it; the host's accessors read through it)
+  const bool with_pos = grp && !d.small;
+  const size_t o_pos = o_er + al(n * d.cape * ERR_WORDS * 4);
+  size_t o_fu = o_pos + (with_pos ? al(n * 4) : 0);
   size_t o_k[FU_KINDS][5];
   for (uint32_t k = 0; k < FU_KINDS; k++) {
     auto& f = d.fu[k];
@@ -3740,7 +3833,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
     d.lane = (uint32_t*)d.lane_blk;
   }
   if (b.img->indexed && split_on() && b.n() && !d.small) {  // the index scan's bucket lists
-    if ((rc = pool_get(pool, false, (size_t)b.n() * (1 + 2 * SCAN_CAP) * 4, &d.scan_blk, &d.scan_cls))) {
+    if ((rc = pool_get(pool, false, scan_words(b.n()) * 4, &d.scan_blk, &d.scan_cls))) {
       pool_put(pool, false, d.lane_blk, d.lane_cls);
       return rc;
     }
@@ -3858,6 +3951,7 @@ int dev_batch_upload(int device, const Batch& b, DevBatch* out, void* stream, De
   d.reasons_f = (uint32_t*)(o + o_rf);
   d.reasons_p = (uint32_t*)(o + o_rp);
   d.errs = (uint32_t*)(o + o_er);
+  d.pos_of = with_pos ? (uint32_t*)(o + o_pos) : nullptr;
   d.fu_cnt = (uint32_t*)(d.zc ? in + o_incnt : o + o_cnt);
   for (uint32_t k = 0; k < FU_KINDS; k++) {
     auto& f = d.fu[k];
@@ -4047,8 +4141,12 @@ __device__ __forceinline__ uint32_t fu_kind(uint32_t fl, uint32_t indexed) {
   if (!(fl & RF_OVERFLOW)) return FU_KINDS;
   return ((fl & RF_GENERAL) || !indexed) ? FU_GEN : (fl & RF_BIG) ? FU_BIG : FU_OVF;
 }
+// (grouped batches: every position i also inverts the order, pos_of[ord[i]] = i, for the host's
+// result accessors, engine.h Batch::slot; the order's reads are coalesced, the scattered 4-byte
+// writes are the one scatter left in the step)
 __global__ void __launch_bounds__(256) cedar_fu_gather(const uint32_t* __restrict__ res, uint32_t n, uint32_t indexed,
-                                                       uint32_t* __restrict__ cnt, FuLists wl) {
+                                                       uint32_t* __restrict__ cnt, FuLists wl,
+                                                       const uint32_t* __restrict__ ord, uint32_t* __restrict__ pos_of) {
   __shared__ uint32_t scan[FU_KINDS][256];
   __shared__ uint32_t base[FU_KINDS];
   const uint32_t t = threadIdx.x;
@@ -4058,6 +4156,7 @@ __global__ void __launch_bounds__(256) cedar_fu_gather(const uint32_t* __restric
     const size_t i = b0 + (size_t)k * 256 + t;
     const uint32_t q = i < n ? fu_kind(res[2 * i] >> 16, indexed) : FU_KINDS;
     if (q < FU_KINDS) c[q]++;
+    if (pos_of && i < n) pos_of[ord[i]] = (uint32_t)i;
   }
   for (uint32_t q = 0; q < FU_KINDS; q++) scan[q][t] = c[q];
   __syncthreads();
@@ -4080,6 +4179,20 @@ __global__ void __launch_bounds__(256) cedar_fu_gather(const uint32_t* __restric
       pos[q]++;
     }
   }
+}
+
+// the scan lists' layout in DevBatch::scan (KArgs::scan): n count words | a list total per wave of
+// 8 positions | a WAVE_CAP-pair list per wave
+static size_t scan_words(uint32_t n) {
+  const size_t nw = ((size_t)n + 7) / 8;
+  return (((size_t)n + 63) & ~(size_t)63) + ((nw + 63) & ~(size_t)63) + nw * 2 * WAVE_CAP;
+}
+static void set_scan(KArgs& k, const DevBatch& b) {
+  const size_t nw = ((size_t)b.n + 7) / 8;
+  k.scan = b.scan;
+  k.scan_tot = b.scan + (((size_t)b.n + 63) & ~(size_t)63);
+  k.scan_list = k.scan_tot + ((nw + 63) & ~(size_t)63);
+  k.scan_n = b.n;
 }
 
 static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* req_idx, uint32_t n, uint32_t* res,
@@ -4107,7 +4220,9 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   k.hlists = img.cslot_mask;  // (DevImage::cslot_mask: the image's list slots)
   // like words staged behind the hot values while both fit the probe kernel's hot rows (32 entries;
   // CEDARGPU_LIKE_STAGE=0: never, A/B): else AK_LIKEI reads the string's bytes
-  static const bool like_stage = !(std::getenv("CEDARGPU_LIKE_STAGE") && *std::getenv("CEDARGPU_LIKE_STAGE") == '0');
+  // (read on every call, as CEDARGPU_SMALL_N is: tests switch it within one process)
+  const char* ls_env = std::getenv("CEDARGPU_LIKE_STAGE");
+  const bool like_stage = !(ls_env && *ls_env == '0');
   static const uint32_t xcd_chunk = [] { const char* e = std::getenv("CEDARGPU_XCD_CHUNK"); return e ? (uint32_t)std::atoi(e) : 0u; }();
   k.xcd_chunk = xcd_chunk;
   static const uint32_t park = [] { const char* e = std::getenv("CEDARGPU_PARK_ATOMS"); return e && std::atoi(e) == 2 ? 2u : 4u; }();
@@ -4138,15 +4253,18 @@ static KArgs make_args(const DevImage& img, const DevBatch& b, const uint32_t* r
   // large stage measured 4.58e8 (43,485 large-stage requests instead of 25,005; profiles/r02/ab_scan_cap)
   static const uint32_t scan_big = [] { const char* e = std::getenv("CEDARGPU_SCAN_BIG"); return e ? (uint32_t)std::atoi(e) : 48u; }();
   static const uint32_t scan_heavy = [] { const char* e = std::getenv("CEDARGPU_SCAN_HEAVY"); return e ? (uint32_t)std::atoi(e) : 128u; }();
-  k.scan_heavy = scan_heavy;
+  k.scan_heavy = std::min<uint32_t>(scan_heavy, 1u << 20);  // (FP_PRE: a round's candidates below 2^24)
   static const uint32_t cnt_rank = [] { const char* e = std::getenv("CEDARGPU_CNT_RANK"); return e ? (uint32_t)std::atoi(e) : 32u; }();
   k.cnt_rank = cnt_rank;
   k.scan_big = scan_big;
   k.stats = nullptr;
   k.n_dev = nullptr;
-  k.ord = nullptr;
-  k.grows = nullptr;
+  // a grouped batch's order (the device sort's, set by the step's grouping): every kernel of the
+  // step and of its host re-runs finds the row of position p at ord[p]
+  k.ord = b.small ? nullptr : b.ord;
+  k.grows = (k.ord && group_gather()) ? b.grows : nullptr;
   k.scan = nullptr;
+  k.scan_tot = k.scan_list = nullptr;
   k.scan_n = 0;
   k.ovf_cnt = nullptr;
   k.ovf_ids = k.ovf_res = k.ovf_rf = k.ovf_er = nullptr;
@@ -4248,6 +4366,9 @@ static void print_probe_stats(const char* what, const std::vector<unsigned long 
 }
 
 static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = false) {
+  // (a follow-up over scanned requests runs on the large stage: the pooled candidate pass reads
+  // whole wave lists of the first pass, by its own launch position)
+  if (k.scan && k.req_idx) big = true;
   if (big && k.scan) {  // the large stage over the scan's buckets (probing only past SCAN_CAP)
     // one-wave blocks: a finished request's wave slot and LDS return at once (C3 DAG 4.996e8 vs
     // 4.919e8 with 4-wave blocks, profiles/r02/ab_big_occ)
@@ -4320,16 +4441,18 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
     if (cstats && !k.req_idx) {  // the candidate pass's work counters (profiling)
       const size_t nw = (n + 7) / 8;
       unsigned long long* d = nullptr;
-      if (hipMalloc((void**)&d, nw * 16 * 8) == hipSuccess) {
+      if (hipMalloc((void**)&d, (nw * 16 + 2) * 8) == hipSuccess) {
         KArgs ks = k;
         ks.stats = d;
-        (void)hipMemsetAsync(d, 0, nw * 16 * 8, s);
+        (void)hipMemsetAsync(d, 0, (nw * 16 + 2) * 8, s);
         hipLaunchKernelGGL((cedar_probe_kernel<8, 64, 4, true, 1, true>), dim3((n + 7) / 8), dim3(64), 0, s, ks);
-        std::vector<unsigned long long> h(nw * 16);
+        std::vector<unsigned long long> h(nw * 16 + 2);
         (void)hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
         (void)hipFree(d);
         print_probe_stats("candidate pass", h, nw);
+        std::fprintf(stderr, "candidate sharing: %llu candidates, %llu of distinct buckets per wave round (distinct / total %.3f)\n",
+                     h[nw * 16], h[nw * 16 + 1], h[nw * 16] ? (double)h[nw * 16 + 1] / (double)h[nw * 16] : 0.0);
       }
       return;
     }
@@ -4423,8 +4546,7 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
     for (uint32_t p = PH_SCAN; p < STEP_PHASES; p++) mark(p, s);
     return 0;
   }
-  k.scan = b.scan;
-  k.scan_n = b.n;
+  set_scan(k, b);
   // the candidate pass finishes long reason lists itself, into the long-list follow-up's worklist
   // (entries flagged FU_DONE: that launch skips them, the host folds them); CEDARGPU_LONG_SLOTS=0
   // leaves them to the follow-up launch
@@ -4442,8 +4564,6 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
       g_err = "request grouping failed";
       return -4;
     }
-    k.ord = b.ord;
-    k.grows = group_gather() ? b.grows : nullptr;
   }
   mark(PH_GROUP, s);
   // the worklist counters and the scan's bad-index count start at zero before the first pass
@@ -4460,17 +4580,18 @@ static int enqueue_step(const DevImage& img, DevBatch& b, hipStream_t s) {
   FuLists wl;
   for (uint32_t q = 0; q < FU_KINDS; q++) { wl.ids[q] = b.fu[q].ids; wl.cap[q] = b.fu[q].cap; }
   hipLaunchKernelGGL(cedar_fu_gather, dim3((b.n + GATHER_ITEMS * 256 - 1) / (GATHER_ITEMS * 256)), dim3(256), 0, s, b.res,
-                     b.n, img.indexed, b.fu_cnt, wl);
+                     b.n, img.indexed, b.fu_cnt, wl, (const uint32_t*)b.ord, b.ord ? b.pos_of : nullptr);
   mark(PH_GATHER, s);
   for (uint32_t q = 0; q < FU_KINDS; q++) {
     const auto& f = b.fu[q];
     if (f.cap) {
       KArgs fk = make_args(img, b, f.ids, f.cap, f.res, f.rf, f.rp, f.er, f.capr, f.cape);
       fk.n_dev = b.fu_cnt + q;
-      fk.scan = b.scan;  // the probe-kernel follow-ups read the first pass's buckets
-      fk.scan_n = b.n;
+      set_scan(fk, b);  // the probe-kernel follow-ups read the first pass's buckets
+      // (long lists too run on the large stage: it reads its request's pairs out of the wave's
+      // list; the pooled candidate pass reads whole lists of first-pass waves only)
       if (q == FU_GEN) launch_stream(img, fk, f.cap, s);
-      else launch_probe(fk, f.cap, s, q == FU_BIG);
+      else launch_probe(fk, f.cap, s, true);
     }
     mark(PH_FU_BIG + q, s);
   }
@@ -4605,6 +4726,7 @@ static void bind_results(const DevBatch& b, Batch& host) {
   host.reasons_f = b.n ? at(b.reasons_f) : nullptr;
   host.reasons_p = b.n ? at(b.reasons_p) : nullptr;
   host.errs = b.n ? at(b.errs) : nullptr;
+  host.pos_of = (b.n && b.pos_of) ? at(b.pos_of) : nullptr;
   host.fu_cnt = (b.n && b.fu_cnt) ? (b.zc ? b.zc_cnt : at(b.fu_cnt)) : nullptr;
   for (uint32_t k = 0; k < FU_KINDS; k++) {
     host.fu[k] = Batch::FollowUp();

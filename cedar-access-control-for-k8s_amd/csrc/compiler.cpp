@@ -460,7 +460,10 @@ struct Compiler {
         // LIKE_WORDS): neutral on the step in the round-5 A/B, and 48 B more per C3
         // request to upload, so off by default.
         static const bool no_likei = std::getenv("CEDARGPU_NO_LIKEI") != nullptr;
-        static const bool like_words = [] { const char* v = std::getenv("CEDARGPU_LIKE_WORDS"); return v && *v == '1'; }();
+        // (read per atom, not once per process: a test can build images both ways in one process;
+        // the device reads staged words only for slots in the image's lslot_mask)
+        const char* lw_env = std::getenv("CEDARGPU_LIKE_WORDS");
+        const bool like_words = lw_env && *lw_env == '1';
         std::string pre, suf;
         bool star = false, inl = !no_likei;
         for (auto& pc : e->pat) {
@@ -2264,8 +2267,8 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     v.resize(len / 4);
     if (len) std::memcpy(v.data(), p + off, len);  // an empty section (no static entities) has no storage
   };
-  // The host keeps the sections it reads (encoder tables, string table, static entities); the
-  // device-only ones (policy stream, scope index, bitsets: ~85 % of a large image) are validated
+  // The host keeps the sections it reads (encoder tables, string table, static entities, the
+  // context table); the device-only ones (policy stream, scope index, bitsets: ~85 % of a large image) are validated
   // in place and only their sizes kept (Image::dev_len), so a load copies them once, to the device
   auto sec_view = [&](uint32_t k) -> std::pair<const uint32_t*, size_t> {
     const uint64_t off = img->dev_off[k], len = img->dev_len[k];
@@ -2276,6 +2279,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
   sec_words(DS_TIER_CEND, img->tier_cend); sec_words(DS_CHUNKS, img->chunks);
   sec_words(DS_CPOOL, img->cpool); sec_words(DS_GSTR_OFF, img->gstr_off); sec_words(DS_HOT, img->hot);
   sec_words(DS_ACT, img->act); sec_words(DS_SROWS, img->srows); sec_words(DS_SHASH, img->shash);
+  sec_words(DS_SCTX, img->sctx);  // (the encoder resolves requests' scope contexts, image.h RH_SCTX)
   {
     const uint64_t off = img->dev_off[DS_GSTR_BYTES], len = img->dev_len[DS_GSTR_BYTES];
     if (off % DS_ALIGN || off < img->dev_begin || off + len + 4 > img->dev_end) throw CedarError("corrupt image (section)");

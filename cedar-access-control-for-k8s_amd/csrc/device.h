@@ -51,8 +51,11 @@ struct DevBatch {
   // inputs: one device block (heap | rows | bstr_off | bstr_bytes | grouping keys), one copy
   uint32_t *heap = nullptr, *rows = nullptr, *req_idx = nullptr, *bstr_off = nullptr;
   uint8_t* bstr_bytes = nullptr;
-  // results: one device block (res | reasons_f | reasons_p | errs), one copy back
-  uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
+  // results: one device block (res | reasons_f | reasons_p | errs | pos_of), one copy back. A
+  // request's results sit at its position in the first pass's launch order: the grouped order of a
+  // grouped batch (so that a wave's requests write neighbouring slots), else the request index.
+  // pos_of[i] (grouped batches only; the gather kernel inverts ord into it) is request i's position.
+  uint32_t *res = nullptr, *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr, *pos_of = nullptr;
   // On-device follow-up (every batch size): right behind the first pass a gather kernel sorts the
   // requests it left unfinished (RF_OVERFLOW) into three worklists, and each worklist is
   // evaluated again on the device into its own results, all inside the result block, so one D2H
@@ -71,7 +74,9 @@ struct DevBatch {
     uint32_t *ids = nullptr, *res = nullptr, *rf = nullptr, *rp = nullptr, *er = nullptr;
     uint32_t cap = 0, capr = 0, cape = 0;
   } fu[3];
-  // split first pass: the index scan's bucket lists (cedar_eval.hip SCAN_*), device only
+  // split first pass: the index scan's bucket lists (cedar_eval.hip SCAN_*), device only: per
+  // position its count word, per wave of 8 positions its list total and its list (the 8 requests'
+  // buckets packed together, each tagged with its request's place in the wave)
   uint32_t* scan = nullptr;
   void* scan_blk = nullptr;
   size_t scan_cls = 0;

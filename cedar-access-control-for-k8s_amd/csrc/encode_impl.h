@@ -252,6 +252,100 @@ inline bool static_attrs_equal(const Image& img, uint32_t sw0, uint32_t sw1, con
   return true;
 }
 
+// CEDARGPU_HOST_CTX=0: the scan looks every request's contexts up itself (A/B)
+inline bool host_ctx_on() {
+  static const bool on = [] { const char* e = std::getenv("CEDARGPU_HOST_CTX"); return !(e && *e == '0'); }();
+  return on;
+}
+
+// The request's scope contexts (image.h RH_SCTX), looked up in the image's context table exactly as
+// cedar_scan_kernel's bitset pass would: per entity-principal combo its level-1 context, one per
+// value slot of l2_vmask with the request's value, one per element (or marker) of each list slot
+// of l2_lmask. Written only when the scan would take its bitset path with these contexts (the SAR
+// shape: at most one action / resource key entity, a principal list, at most CTX_CAP contexts) and
+// at most CTXR_SLOTS of them exist; the row's RW_ASELF then carries ASELF_CTXR.
+inline void resolve_contexts(const Image& img, EncodedRequest& E) {
+  std::vector<uint32_t>& blk = E.blk;
+  uint32_t* row = E.row.data();
+  for (uint32_t k = 0; k < CTXR_SLOTS; k++) blk[RH_SCTX + k] = CTXR_EMPTY;
+  const size_t slots = img.sctx.size() / SCTX_WORDS;
+  if (!host_ctx_on() || !img.indexed || !img.sbits_words || slots < 2 || !row[RW_PANC]) return;
+  const uint32_t cm = img.combo_mask;
+  uint32_t pe = 0, ae = 0, re = 0;  // combos with an entity principal / action / resource component
+  for (uint32_t cb = 0; cb < 32; cb++) {
+    if ((cb & 3) == KC_ENT) pe |= 1u << cb;
+    if (((cb >> 2) & 1) == KC_ENT) ae |= 1u << cb;
+    if ((cb >> 3) == KC_ENT) re |= 1u << cb;
+  }
+  pe &= cm;
+  const uint32_t pn = row[RW_PN], an = row[RW_AN], rn = row[RW_RN];
+  auto nkeys = [](uint32_t w) { return (w >> 31) + ((w >> AN_KEYS_SHIFT) & AN_KEYS); };
+  const uint32_t nP = nkeys(pn), nA = nkeys(an), nR = nkeys(rn);
+  if (!pe || !((!(cm & ae) || nA <= 1) && (!(cm & re) || nR <= 1) && nP < 2048)) return;
+  // the action / resource component of the keys: the UID when it is a key entity, else its one key
+  // ancestor (the first of its list)
+  auto key1 = [&](uint32_t n, uint32_t w_n, uint32_t w_anc, uint32_t t, uint32_t i) -> std::pair<uint32_t, uint32_t> {
+    if (n != 1) return {KW_ANY, KW_ANY};
+    if (row[w_n] & AN_SELF) return {t, i};
+    const uint32_t* l = E.anc_pairs(row[w_anc]);
+    return {l[0], l[1]};
+  };
+  const auto ka1 = key1(nA, RW_AN, RW_AANC, row[RW_A], row[RW_A + 1]);
+  const auto kr1 = key1(nR, RW_RN, RW_RANC, row[RW_R], row[RW_R + 1]);
+  const uint32_t nh = img.n_hot(), vm = img.l2_vmask, lm = img.l2_lmask, hl = img.list_mask();
+  // per combo: level 1, the value slots, the list entries (CTX_CAP in all at most)
+  struct Key { uint32_t hs, v0, v1; };
+  Key keys[CTX_CAP];
+  uint32_t per = 1;
+  keys[0] = {SCTX_L1, 0u, 0u};
+  for (uint32_t m = vm; m; m &= m - 1) {
+    const uint32_t h = (uint32_t)__builtin_ctz(m);
+    const uint32_t w0 = row[RW_HDR + 2 * h], w1 = row[RW_HDR + 2 * h + 1];
+    const bool ok = (w0 >> TAG_SHIFT) != T_NONE;
+    if (per < CTX_CAP) keys[per] = {h, ok ? w0 : MISSING_W0, ok ? w1 : 0u};
+    per++;
+  }
+  for (uint32_t m = lm; m && hl; m &= m - 1) {
+    const uint32_t h = (uint32_t)__builtin_ctz(m);
+    const uint32_t lo = row[RW_HDR + 2 * nh + (uint32_t)__builtin_popcount(hl & ((1u << h) - 1u))];
+    const uint32_t hd = blk[lo];
+    if (hd & 0x80000000u) {
+      if (per < CTX_CAP) keys[per] = {h | BT_CKEY, hd == CL_MISSING ? MISSING_W0 : NOTSET_W0, 0u};
+      per++;
+    } else {
+      for (uint32_t e = 0; e < hd; e++) {
+        if (per < CTX_CAP) keys[per] = {h | BT_CKEY, blk[lo + 1 + e], 1u};
+        per++;
+      }
+    }
+  }
+  if ((uint64_t)__builtin_popcount(pe) * per > CTX_CAP) return;  // the scan enumerates this request's keys
+  uint32_t found[CTXR_SLOTS], nf = 0;
+  for (uint32_t m = pe; m; m &= m - 1) {
+    const uint32_t cb = (uint32_t)__builtin_ctz(m);
+    const auto q = ((cb >> 2) & 1) == KC_ENT ? ka1 : std::make_pair(KW_ANY, KW_ANY);
+    const uint32_t rkc = cb >> 3;
+    const auto r = rkc == KC_ENT ? kr1 : rkc == KC_TYPE ? std::make_pair(row[RW_R], KW_ANY) : std::make_pair(KW_ANY, KW_ANY);
+    const uint32_t pre = key_pre(cb, q.first, q.second, r.first, r.second);
+    for (uint32_t t = 0; t < per; t++) {
+      const Key& k = keys[t];
+      const uint32_t w0c = ctx_w0(cb, k.hs);
+      for (size_t h = ctx_key(pre, k.hs, k.v0, k.v1) & (slots - 1);; h = (h + 1) & (slots - 1)) {
+        const uint32_t* x = &img.sctx[h * SCTX_WORDS];
+        if (!x[0]) break;
+        if (x[0] == w0c && x[1] == q.first && x[2] == q.second && x[3] == r.first && x[4] == r.second && x[5] == k.v0 &&
+            x[6] == k.v1) {
+          if (nf == CTXR_SLOTS || x[7] >= (1u << (32 - CTXR_ROW))) return;  // (more than the block holds)
+          found[nf++] = cb | (x[7] << CTXR_ROW);
+          break;
+        }
+      }
+    }
+  }
+  for (uint32_t k = 0; k < nf; k++) blk[RH_SCTX + k] = found[k];
+  row[RW_ASELF] |= ASELF_CTXR;
+}
+
 inline void emit_empty_record(std::vector<uint32_t>& out, uint32_t& w0, uint32_t& w1) {
   const uint32_t off = (uint32_t)out.size();
   out.push_back(0);
@@ -700,6 +794,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
       if ((w0 >> TAG_SHIFT) == T_STR && w1 >= img.n_gstr() && w1 - img.n_gstr() < E.strs.size()) E.str_dev[w1 - img.n_gstr()] = 1;
     }
   }
+  resolve_contexts(img, E);
   if (blk.size() > OFF_MASK) throw CedarError("request too large for the device heap format");
   // grouping key: 8 bits of (action, resource type) | 16 of the principal's type and key ancestors |
   // 8 of its hot values (group.hip sorts on the top 24). Round-5 A/B of the field order

@@ -392,6 +392,12 @@ struct Batch {
   // error records. res is written back by overflow re-runs.
   uint32_t* res = nullptr;
   const uint32_t *reasons_f = nullptr, *reasons_p = nullptr, *errs = nullptr;
+  // Results are laid out by position in the device's launch order (device.h DevBatch::res): request
+  // i's slot is pos_of[i] for a batch grouped on the device, else i. Everything indexed by slot
+  // (res, the lists, bigs, the worklists' and re-runs' ids) uses positions; only the accessors
+  // below take request indices.
+  const uint32_t* pos_of = nullptr;
+  uint32_t slot(uint32_t i) const { return pos_of ? pos_of[i] : i; }
   // per-request overflow re-run results (index -> reasons / errors)
   // Re-run results: request i's reason / error list read in place from the re-run's pinned result
   // block, which the owning cg_batch keeps until it is destroyed (big stays empty until a re-run
@@ -406,9 +412,9 @@ struct Batch {
   const uint32_t* fu_cnt = nullptr;
   struct BigRef { const uint32_t *r = nullptr, *e = nullptr; uint32_t nr = 0, ne_words = 0; };
   std::vector<BigRef> bigs;      // lists held outside the first pass's slots
-  std::vector<uint32_t> big_ix;  // per request: 1 + its index in bigs, or 0 (empty: none)
-  const BigRef* big_of(uint32_t i) const { return (!big_ix.empty() && big_ix[i]) ? &bigs[big_ix[i] - 1] : nullptr; }
-  void set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words);
+  std::vector<uint32_t> big_ix;  // per slot: 1 + its index in bigs, or 0 (empty: none)
+  const BigRef* big_of(uint32_t p) const { return (!big_ix.empty() && big_ix[p]) ? &bigs[big_ix[p] - 1] : nullptr; }
+  void set_big(uint32_t p, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words);
 
   uint32_t n() const { return (uint32_t)req_base.size(); }
   // string `id` as request i sees it
@@ -420,8 +426,10 @@ struct Batch {
   // (request bases, RW_BLK and RH_SBASE are shifted). `threads` copy the parts side by side.
   void concat(std::vector<Batch>& parts, unsigned threads);
   void finalize_strings();
-  // decision: 1 allow, 0 deny; fills the Go-JSON rendering of the cedar.Diagnostic
+  // (by request index i) decision: 1 allow, 0 deny; the deciding tier; the Go-JSON rendering of
+  // the cedar.Diagnostic
   bool decision(uint32_t i) const;
+  uint32_t tier(uint32_t i) const;
   void diagnostic_json(uint32_t i, std::string& out, bool reasons_only) const;
   void reason_ids(uint32_t i, std::vector<uint32_t>& out) const;
   void error_recs(uint32_t i, std::vector<uint32_t>& out) const;

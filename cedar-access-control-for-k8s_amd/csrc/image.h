@@ -62,8 +62,17 @@ enum ReqHdr : uint32_t {
   RH_AIDX = 10,
   RH_RIDX = 11,
   RH_SBASE = 12, // index of the request's first string in the batch string table (bstr_off)
-  RH_WORDS = 13, // entity table follows: n_ent * ENT_WORDS
+  RH_SCTX = 13,  // the request's scope contexts, resolved by the encoder (CTXR_SLOTS words, below)
+  RH_WORDS = 17, // entity table follows: n_ent * ENT_WORDS
 };
+// Host-resolved scope contexts (image.h "scope bitsets"). A request's contexts depend on its
+// action, resource and hot values only, never on its principal, so the encoder looks them up in
+// the image's context table (Image::sctx, the host keeps a copy) exactly as cedar_scan_kernel
+// would, and writes the ones it finds into RH_SCTX: combo | bitset row << CTXR_ROW each, CTXR_EMPTY
+// after the last. The row's RW_ASELF carries ASELF_CTXR when it did (the scan then skips the
+// context filter, the table probes and the list-slot reads they need); when the request's
+// contexts are more than CTX_CAP or it finds more than CTXR_SLOTS, the scan looks them up itself.
+constexpr uint32_t CTXR_SLOTS = 4, CTXR_EMPTY = 0xFFFFFFFFu, CTXR_ROW = 5, CTX_CAP = 16;
 enum EntRow : uint32_t { ER_TYPE = 0, ER_ID = 1, ER_ATTR0 = 2, ER_ATTR1 = 3, ER_ANC = 4, ER_PAD = 5, ENT_WORDS = 6 };
 constexpr uint32_t NO_ENT = 0xFFFFFFFFu;
 // Ancestor lists of request entities live outside their blocks: the batch heap holds each distinct
@@ -317,7 +326,8 @@ enum RowW : uint32_t {
   RW_BLK = 12,   // heap word offset of the request block
   RW_AM0 = 13,   // action mask over the image action table (`in`: the action or an ancestor), low
   RW_AM1 = 14,   //   ... high word (valid when the image's amask_ok)
-  RW_ASELF = 15, // index of the action itself in the action table (`==`), ~0u when absent
+  RW_ASELF = 15, // index of the action itself in the action table (`==`) in the low 16 bits (0xFFFF
+                 // when absent) | ASELF_CTXR: the block's RH_SCTX words hold its scope contexts
   RW_HDR = 16,   // hot slots follow: (w0, w1) per hot path
 };
 constexpr uint32_t MISSING_W0 = 0xFFFFFFFFu;  // level-2 index key of an absent hot value
@@ -372,6 +382,7 @@ inline uint32_t pfx_hash(const uint8_t* s, uint32_t len) {
 }
 // RW_PN / RW_RN / RW_AN fields
 constexpr uint32_t AN_COUNT = 0xFFFFu, AN_KEYS_SHIFT = 16, AN_KEYS = 0x7FFFu, AN_SELF = 0x80000000u;
+constexpr uint32_t ASELF_MASK = 0xFFFFu, ASELF_CTXR = 0x80000000u;
 
 // ---- bytecode -------------------------------------------------------------------------------
 // word0 = op | d << 8 | a << 14 | b << 20 | c << 26 (6-bit slot fields); word1 = imm

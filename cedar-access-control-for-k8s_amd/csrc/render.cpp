@@ -14,17 +14,19 @@
 namespace cg {
 using namespace cgi;
 
-bool Batch::decision(uint32_t i) const { return (res[2 * (size_t)i] & 0xFF) == DEC_ALLOW; }
+bool Batch::decision(uint32_t i) const { return (res[2 * (size_t)slot(i)] & 0xFF) == DEC_ALLOW; }
+uint32_t Batch::tier(uint32_t i) const { return (res[2 * (size_t)slot(i)] >> 8) & 0xFF; }
 
 void Batch::reason_ids(uint32_t i, std::vector<uint32_t>& out) const {
   out.clear();
-  uint32_t n = res[2 * (size_t)i + 1] & 0xFFFF;
-  if (const BigRef* b = big_of(i)) {
+  const uint32_t p = slot(i);
+  uint32_t n = res[2 * (size_t)p + 1] & 0xFFFF;
+  if (const BigRef* b = big_of(p)) {
     out.assign(b->r, b->r + b->nr);
   } else {
-    uint32_t flags = res[2 * (size_t)i] >> 16;
+    uint32_t flags = res[2 * (size_t)p] >> 16;
     const uint32_t* src = (flags & RF_FORBID) ? reasons_f : reasons_p;
-    for (uint32_t k = 0; k < n && k < capr; k++) out.push_back(src[(size_t)i * capr + k]);
+    for (uint32_t k = 0; k < n && k < capr; k++) out.push_back(src[(size_t)p * capr + k]);
   }
   // duplicate classes reported by their representative: every member, then policy order again
   // (the classes and the single policies are disjoint, so the list stays duplicate-free)
@@ -36,32 +38,36 @@ void Batch::reason_ids(uint32_t i, std::vector<uint32_t>& out) const {
     const uint32_t r = out[k];
     if (!(r & RS_CLASS)) continue;
     const uint32_t p = r & ~RS_CLASS;
-    if (img->cls_off.empty() || p + 1 >= img->cls_off.size()) throw CedarError("reason names an unknown duplicate class");
+    // (a word naming no class representative: an empty member range would be read past its end)
+    if (img->cls_off.empty() || p + 1 >= img->cls_off.size() || img->cls_off[p] >= img->cls_off[p + 1] ||
+        img->cls_off[p + 1] > img->cls_mem.size())
+      throw CedarError("reason names an unknown duplicate class");
     out[k] = img->cls_mem[img->cls_off[p]];
     out.insert(out.end(), img->cls_mem.begin() + img->cls_off[p] + 1, img->cls_mem.begin() + img->cls_off[p + 1]);
   }
   std::sort(out.begin(), out.end());
 }
 
-void Batch::set_big(uint32_t i, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words) {
+void Batch::set_big(uint32_t p, const uint32_t* reasons, uint32_t nr, const uint32_t* errs, uint32_t nerr_words) {
   if (big_ix.empty()) big_ix.assign(n(), 0u);
-  if (big_ix[i]) {
-    bigs[big_ix[i] - 1] = BigRef{reasons, errs, nr, nerr_words};
+  if (big_ix[p]) {
+    bigs[big_ix[p] - 1] = BigRef{reasons, errs, nr, nerr_words};
   } else {
     bigs.push_back(BigRef{reasons, errs, nr, nerr_words});
-    big_ix[i] = (uint32_t)bigs.size();
+    big_ix[p] = (uint32_t)bigs.size();
   }
 }
 
 void Batch::error_recs(uint32_t i, std::vector<uint32_t>& out) const {
   out.clear();
-  uint32_t n = res[2 * (size_t)i + 1] >> 16;
-  if (const BigRef* b = big_of(i)) {
+  const uint32_t p = slot(i);
+  uint32_t n = res[2 * (size_t)p + 1] >> 16;
+  if (const BigRef* b = big_of(p)) {
     out.assign(b->e, b->e + b->ne_words);
     return;
   }
   for (uint32_t k = 0; k < n && k < cape; k++)
-    for (uint32_t w = 0; w < ERR_WORDS; w++) out.push_back(errs[((size_t)i * cape + k) * ERR_WORDS + w]);
+    for (uint32_t w = 0; w < ERR_WORDS; w++) out.push_back(errs[((size_t)p * cape + k) * ERR_WORDS + w]);
 }
 
 static const char* type_name(uint32_t t) {

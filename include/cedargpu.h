@@ -127,6 +127,11 @@ int cg_image_stats(const void* image, size_t len, uint32_t* n_atomic, uint32_t* 
 int cg_image_index_stats(const void* image, size_t len, uint32_t* cslot_mask, uint32_t* pslot_mask,
                          uint32_t* combo_mask, uint32_t* entries, uint32_t* contexts, uint32_t* sbits_words);
 
+/* Hot slots whose rows carry like words (Image::lslot_mask: each such slot's length and first / last
+ * 8 bytes shipped in the request row, CEDARGPU_LIKE_WORDS=1 at compile time) and the slots any
+ * `like` atom reads as bytes (Image::lread_mask). Host only; introspection for tests and tooling. */
+int cg_image_like_slots(const void* image, size_t len, uint32_t* row_like_mask, uint32_t* like_read_mask);
+
 /* 1 when policy i (image order) lowered to predicate atoms, 0 when it runs as bytecode. */
 int cg_image_policy_atomic(const void* image, size_t len, uint32_t i, int* atomic);
 /* 1 when the image is evaluated by the probe kernel over the scope index (all policies atomic). */
@@ -220,6 +225,21 @@ int cg_broadcast_image(cg_ctx* ctx, cg_comm* comm, int root, const void* image, 
  * cg_broadcast_image. *out_len (may be NULL) receives the delta's size. */
 int cg_broadcast_delta(cg_ctx* ctx, cg_comm* comm, int root, uint64_t base_epoch, const void* delta, size_t len,
                        uint64_t epoch, int activate, size_t* out_len);
+
+/* How request i of a waited batch was finished (introspection for tests and tooling): a bit set
+ * of CG_ROUTE_*. 0: the first pass alone. FIRST_SLOT: the first pass wrote its long list into a
+ * long-list worklist slot; FU_BIG / FU_OVF / FU_GEN: the large stage, the long-list follow-up or
+ * the policy-stream follow-up on the device; RERUN: a host-driven re-run; CLASS: its reasons
+ * include a duplicate class the device reported whole (its members listed on the host).
+ * reason_words (optional): the deciding list's length as the device wrote it (a class reported
+ * whole is one word; cg_batch_reasons lists its members). */
+#define CG_ROUTE_FU_BIG 1u
+#define CG_ROUTE_FU_OVF 2u
+#define CG_ROUTE_FU_GEN 4u
+#define CG_ROUTE_FIRST_SLOT 8u
+#define CG_ROUTE_RERUN 16u
+#define CG_ROUTE_CLASS 32u
+int cg_batch_route(cg_batch* b, uint32_t i, uint32_t* route, uint32_t* reason_words);
 
 /* ---- batches of (EntityMap, Request) ---- */
 /* Creates a batch bound to the currently active image. */

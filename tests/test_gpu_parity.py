@@ -546,6 +546,59 @@ def test_c3_full_size_dag(ctx):
     check_items_ref(ctx, stores, items, want_indexed=True, entities=ents)
 
 
+def test_c3_grouped_path_65536(ctx, monkeypatch):
+    """The headline's own code path at C3's shape: 65,536 requests (10k ABAC policies over the
+    bench's 5k-group depth-12 DAG) in one batch, which the step groups on the device (batches of
+    >= 65,536). The scan writes packed per-wave lists by grouped position, the pooled candidate
+    pass reads them and writes results by position, the large stage picks its request's pairs out
+    of the wave's list, long lists land in worklist slots, and the host binds every result back to
+    its request through pos_of. Checked against the C++ oracle (decision and full diagnostic):
+    every request that a follow-up, a long-list slot or a re-run finished, every one whose reasons
+    hold a duplicate class reported whole, and a 2,000-request random sample."""
+    import random
+    from cedar_ref import RefPolicySet, items_json
+    monkeypatch.delenv("CEDARGPU_GROUP", raising=False)
+    monkeypatch.delenv("CEDARGPU_SMALL_N", raising=False)
+    # 8 first-pass reasons per request, as the bench's 1M-request batch gets (its 32 MB budget): the
+    # long deciding lists then take worklist slots as they do there
+    monkeypatch.setenv("CEDARGPU_FIRST_CAPR", "8")
+    pop = synth.Population(seed=7, dag_depth=12)
+    ents = pop.static_entities()
+    stores = [cedargpu.MemoryStore("c3.cedar", synth.abac_policies(10_000, seed=31, pop=pop))]
+    items = _dag_items(pop, 66_000, 2024)[:65_536]
+    assert len(items) == 65_536
+    ctx.load(cedargpu.build_image(stores, epoch=963, entities=ents), 963)
+    payload = json.dumps([{"entities": e, "request": r} for e, r in items])
+    runs = []
+    for _ in range(2):  # (the first batch on an image sizes the follow-up worklists of the next)
+        b = ctx.batch()
+        b.add_json(payload)
+        b.submit()
+        b.wait()
+        n = len(b)
+        routes = [b.route(i) for i in range(n)]
+        kinds = {name: sum(1 for r in routes if r & bit) for name, bit in
+                 (("large_stage", cedargpu.ROUTE_FU_BIG), ("long_list_slot", cedargpu.ROUTE_FIRST_SLOT),
+                  ("long_list_fu", cedargpu.ROUTE_FU_OVF), ("rerun", cedargpu.ROUTE_RERUN), ("class", cedargpu.ROUTE_CLASS))}
+        print("routes", kinds)
+        picked = sorted({i for i, r in enumerate(routes) if r} | set(random.Random(5).sample(range(n), 2000)))
+        runs.append((kinds, picked, [(b.decision(i)[0], b.diagnostic(i)) for i in picked]))
+        b.close()
+    # (C3's shape, once sized: a few hundred many-hit requests on the large stage, long deciding
+    # lists in worklist slots, class hits; the unsized first batch re-ran most of them from the host)
+    kinds = runs[1][0]
+    assert kinds["large_stage"] >= 50 and kinds["long_list_slot"] >= 200 and kinds["class"] >= 100, kinds
+    assert runs[0][0]["rerun"] > 0
+    picked = sorted(set(runs[0][1]) | set(runs[1][1]))
+    res = [dict(zip(r[1], r[2])) for r in runs]
+    ref = RefPolicySet.from_stores(stores, ents)
+    ref.load_items(items_json([items[i] for i in picked]))
+    want = ref.evaluate(min(16, os.cpu_count() or 8))
+    ref.close()
+    bad = [(k, i) for i, (wok, _, wdiag, _) in zip(picked, want) for k in (0, 1) if i in res[k] and res[k][i] != (wok, wdiag)]
+    assert not bad, (len(bad), bad[:10], kinds)
+
+
 def test_c2_full_size_rbac(ctx):
     """C2 at its stated size: 1k RBAC-converted policies plus the demo tier x 4k SARs vs the C++
     oracle."""
@@ -560,13 +613,20 @@ def test_c2_full_size_rbac(ctx):
     check_items_ref(ctx, stores, items, want_indexed=True)
 
 
+@pytest.mark.parametrize("path", ["small", "split", "grouped"])
 @pytest.mark.parametrize("chain", [20, 40, 70, 130])
-def test_scan_list_thresholds(ctx, chain):
+def test_scan_list_thresholds(ctx, chain, path, monkeypatch):
     """A static group chain whose every level carries permits / forbids: a principal at the bottom
-    finds one bucket per level. 20: the candidate pass; 40: over the large stage's hand-off (48)
-    only with both effects; 70: the large stage reads the scan list (<= 96 buckets); 130: the list
-    overflows and the large stage probes the index itself. Hits past 64 / 1,024 and long reason
-    lists included; vs the C++ oracle."""
+    finds one bucket per level. On the split first pass (path split: launch order = request order;
+    grouped: the device's grouped order, results bound back through pos_of): 20: the candidate
+    pass; 40: over the large stage's hand-off (48) only with both effects; 70: the large stage picks
+    its pairs out of its wave's list; 130: the wave's list (768 pairs for 8 requests) overflows, so
+    some requests probe the index themselves on the large stage. path small: the one-launch kernel,
+    which always probes. Hits past 64 / 1,024 and long reason lists included; vs the C++ oracle."""
+    if path != "small":
+        monkeypatch.setenv("CEDARGPU_SMALL_N", "0")
+    if path == "grouped":
+        monkeypatch.setenv("CEDARGPU_GROUP", "1")
     G = lambda g: {"type": "k8s::Group", "id": g}
     ents = [{"uid": G(f"c{k}"), "attrs": {"name": f"c{k}"}, "parents": [G(f"c{k + 1}")] if k + 1 < chain else []}
             for k in range(chain)]
