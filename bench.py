@@ -338,7 +338,8 @@ def hot_reload(ctx, policies, rank, world, device, dist_on, timeout_s=180.0, ent
     return out
 
 
-def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96, 192, 256, 384, 512)):
+def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96, 192, 256, 384, 512),
+          batched_sweep=(8, 16, 24, 32, 48, 64)):
     """End-to-end webhook path through the serving queue: `threads` native caller threads each
     issue blocking cg_queue_authorize_sar calls (SAR JSON in, Decision + reason out), which the
     queue batches onto the GPU. Host JSON parsing, SAR conversion and encoding are inside. Then the
@@ -351,9 +352,9 @@ def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96, 192, 
     q.loadgen(enc[:4096], threads, 8192)  # warm the pool's buffer classes
     q.close()
 
-    def point(nt, n):
+    def point(nt, n, per_call=1):
         q = cedargpu.Queue(ctx, max_batch=max_batch, max_delay_us=0)
-        r = q.loadgen(enc, nt, n)
+        r = q.loadgen(enc, nt, n, per_call=per_call)
         st = q.stats()
         q.close()
         return {"decisions_per_s": n / r["seconds"], "requests": n, "threads": nt,
@@ -372,6 +373,20 @@ def serve(ctx, sars, threads, total, max_batch, sweep=(16, 32, 48, 64, 96, 192, 
     out["best_under_1ms_threads"] = max(ok, key=lambda p: p["decisions_per_s"])["threads"] if ok else None
     out["what"] = ("cg_queue_authorize_sar per request from native threads (JSON parse, SAR conversion, columnar encode, "
                    "batched H2D + kernel + D2H, reason rendering)")
+    # a host-side batcher's path (north_star's batching layer: one goroutine gathers the webhook
+    # goroutines' requests and crosses into cgo once per group): cg_queue_authorize_sar_n calls of
+    # `per_call` SARs from fewer caller threads; each request's latency is its call's
+    per_call = 8
+    bcurve = [point(nt, max(16384, total // 4), per_call) for nt in batched_sweep]
+    bok = [p for p in bcurve if p["p99_us"] < 1000.0]
+    best = max(bok, key=lambda p: p["decisions_per_s"]) if bok else None
+    out["batched"] = {"per_call": per_call,
+                      "curve": [{k: p[k] for k in ("threads", "decisions_per_s", "p50_us", "p99_us", "max_us", "mean_batch",
+                                                    "device_busy_frac")} for p in bcurve],
+                      "best_under_1ms": best["decisions_per_s"] if best else None,
+                      "best_under_1ms_threads": best["threads"] if best else None,
+                      "what": f"cg_queue_authorize_sar_n: {per_call} SAR bodies per call, per-request encode and rendering "
+                              "on the calling thread, one wait per call"}
     return out
 
 

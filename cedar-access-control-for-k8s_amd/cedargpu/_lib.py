@@ -153,6 +153,11 @@ _SIGS = {
     "cg_queue_loadgen": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), u32, u32, u64,
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u64),
                                         ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+    "cg_queue_loadgen_n": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), u32, u32, u32, u64,
+                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                          ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+    "cg_queue_authorize_sar_n": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), u32, i64,
+                                                ctypes.POINTER(ctypes.c_int), P, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
 }
 
 for _name, (_res, _args) in _SIGS.items():

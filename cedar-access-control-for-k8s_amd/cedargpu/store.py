@@ -707,16 +707,39 @@ class Queue:
             "abandoned": m.abandoned, "active_epoch": m.active_epoch, "activations": m.activations,
         }
 
-    def loadgen(self, sars_json: Sequence[str], threads: int, total: int) -> dict:
-        """Bench support: `threads` native threads issue `total` blocking authorize calls."""
+    def authorize_many(self, sars: Sequence[Union[dict, str]], timeout: Optional[float] = None) -> List[Tuple[int, str]]:
+        """cg_queue_authorize_sar_n: several SubjectAccessReviews in one blocking call (a host-side
+        batcher's entry point); [(decision, reason)] in order."""
+        enc = [_b(s if isinstance(s, str) else json.dumps(s)) for s in sars]
+        n = len(enc)
+        arr = (ctypes.c_char_p * max(n, 1))(*enc)
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(e) for e in enc])
+        dec = (ctypes.c_int * max(n, 1))()
+        offs = (ctypes.c_size_t * max(n, 1))()
+        need = ctypes.c_size_t(0)
+        buf = ctypes.create_string_buffer(max(4096, 512 * n))
+        for _ in range(2):
+            rc = lib.cg_queue_authorize_sar_n(self._h, arr, lens, n, _timeout_ns(timeout), dec, buf, len(buf), offs,
+                                              ctypes.byref(need))
+            if rc != CG_E_RANGE:
+                break
+            buf = ctypes.create_string_buffer(need.value)
+        if rc:
+            raise _err(rc, lib.cg_queue_last_error().decode())
+        raw = buf.raw
+        return [(dec[k], raw[offs[k]:raw.index(b"\0", offs[k])].decode("utf-8")) for k in range(n)]
+
+    def loadgen(self, sars_json: Sequence[str], threads: int, total: int, per_call: int = 1) -> dict:
+        """Bench support: `threads` native threads issue `total` blocking authorize calls
+        (`per_call` > 1: cg_queue_authorize_sar_n calls of that many requests each)."""
         enc = [_b(s) for s in sars_json]
         arr = (ctypes.c_char_p * len(enc))(*enc)
         lens = (ctypes.c_size_t * len(enc))(*[len(e) for e in enc])
         secs = ctypes.c_double()
         p50, p99, mx = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         counts = (ctypes.c_uint64 * 3)()
-        rc = lib.cg_queue_loadgen(self._h, arr, lens, len(enc), threads, total, ctypes.byref(secs), ctypes.byref(p50),
-                                  ctypes.byref(p99), ctypes.byref(mx), counts)
+        rc = lib.cg_queue_loadgen_n(self._h, arr, lens, len(enc), threads, per_call, total, ctypes.byref(secs),
+                                    ctypes.byref(p50), ctypes.byref(p99), ctypes.byref(mx), counts)
         if rc:
             raise _err(rc, lib.cg_queue_last_error().decode())
         return {"seconds": secs.value, "p50_us": p50.value / 1e3, "p99_us": p99.value / 1e3, "max_us": mx.value / 1e3,

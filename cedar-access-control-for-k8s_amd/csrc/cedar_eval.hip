@@ -1038,11 +1038,10 @@ __device__ __forceinline__ void run_bytecode(const Ctx& c, const uint32_t* code,
       RV out = va;
       bool wr = true;
       switch (op) {
-        case OP_LDV: {
-          const uint32_t o = imm == 0 ? RH_P : imm == 1 ? RH_A : imm == 2 ? RH_R : RH_CTX;
-          out = RV{c.blk[o], c.blk[o + 1], 0};
+        case OP_LDV:  // principal / action / resource (their UIDs, from the row), context
+          out = imm < 3 ? RV{mk_w0(T_ENT, pick3(imm, c.pt, c.at, c.rt)), pick3(imm, c.pi, c.ai, c.ri), 0}
+                        : RV{c.blk[RH_CTX], c.blk[RH_CTX + 1], 0};
           break;
-        }
         case OP_LDC: out = load_val(c, c.cpool[imm], c.cpool[imm + 1]); break;
         case OP_LDB: out = mk_bool(imm != 0); break;
         case OP_LDS: out = RV{mk_w0(T_STR, 0), imm, 0}; break;
@@ -1339,7 +1338,8 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
 
   uint32_t lane_scratch[GLANE ? 1 : LANE_WORDS];
   Ctx c;
-  c.blk = a.heap + (valid ? a.rows[(size_t)r * a.row_words + RW_BLK] : 0);  // (the row's block offset: no req_base upload)
+  const uint32_t* rowp = a.rows + (size_t)r * a.row_words;
+  c.blk = a.heap + (valid ? rowp[RW_BLK] : 0);  // (the row's block offset: no req_base upload)
   c.cpool = a.cpool;
   c.lh = GLANE ? a.lane + (size_t)(valid ? gid : 0) * a.lane_stride : lane_scratch;
   c.hot = a.hot;
@@ -1363,9 +1363,9 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   uint32_t as0 = 0, as1 = 0;  // action == act[k]
   if (valid) {
     c.nent = c.blk[RH_NENT];
-    c.pt = c.blk[RH_P] & X_MASK; c.pi = c.blk[RH_P + 1];
-    c.at = c.blk[RH_A] & X_MASK; c.ai = c.blk[RH_A + 1];
-    c.rt = c.blk[RH_R] & X_MASK; c.ri = c.blk[RH_R + 1];
+    c.pt = rowp[RW_P]; c.pi = rowp[RW_P + 1];
+    c.at = rowp[RW_A]; c.ai = rowp[RW_A + 1];
+    c.rt = rowp[RW_R]; c.ri = rowp[RW_R + 1];
     c.pidx = c.blk[RH_PIDX]; c.aidx = c.blk[RH_AIDX]; c.ridx = c.blk[RH_RIDX];
     anc_of(c, c.pidx, c.p_base, c.p_anc, c.p_nanc);
 #define CG_ANC(k) \
@@ -2069,7 +2069,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     if (STATS && sl == 0 && valid) {
       st[11] += flt;
       st[12] += nf;
-      st[13] += on ? 1u : 0u;
+      st[13] += hres ? 1u : 0u;
       st[14] += npos;
       st[15] += (kbits && klist && simple) ? 1u : 0u;
     }
@@ -4424,7 +4424,7 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
         std::fprintf(stderr,
                      "scan stats: requests %llu | per request: keys %.2f L1 probes %.2f found %.2f | L2 probes %.2f found %.2f | "
                      "per wave: iterations %.2f, segment-iterations %.2f (L2 %.2f) | cycles prologue %.0f loop %.0f | bitsets: "
-                     "eligible %llu within caps %llu listed-path %llu, contexts found %.2f listed %.2f per request\n",
+                     "eligible %llu encoder-resolved %llu listed-path %llu, contexts found %.2f listed %.2f per request\n",
                      h[0], h[10] / r, h[1] / r, h[2] / r, h[3] / r, h[4] / r, h[5] / w, h[7] / w, h[6] / w, h[8] / w, h[9] / w,
                      h[15], h[13], h[11], h[12] / r, h[14] / r);
       }

@@ -480,9 +480,6 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   for (auto* u : {&pu, &au, &ru})
     if (u->first > X_MASK) throw CedarError("string table overflow");
   blk[RH_NENT] = n;
-  blk[RH_P] = mk_w0(T_ENT, pu.first); blk[RH_P + 1] = pu.second;
-  blk[RH_A] = mk_w0(T_ENT, au.first); blk[RH_A + 1] = au.second;
-  blk[RH_R] = mk_w0(T_ENT, ru.first); blk[RH_R + 1] = ru.second;
   // entity index of a UID: the request's table, else the image's static entities (ENT_STATIC)
   auto idx_of = [&](const std::pair<uint32_t, uint32_t>& u) {
     const int32_t i = index.find(uid_key(u.first, u.second));
@@ -680,7 +677,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
   anc_into(blk[RH_RIDX], ru, RW_RANC, RW_RN);
   anc_into(blk[RH_AIDX], au, RW_AANC, RW_AN);
   // action masks over the image action table, as the probe kernel tests scopes against them
-  row[RW_ASELF] = 0xFFFFFFFFu;
+  row[RW_ASELF] = ASELF_MASK;  // (absent; bit 31, ASELF_CTXR, is resolve_contexts')
   if (img.amask_ok) {
     uint64_t am = 0;
     const uint32_t n_act = (uint32_t)img.act.size() / 2;
@@ -703,7 +700,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     const uint32_t var = hp[0], depth = hp[1];
     uint32_t w0, w1;
     if (var == 3) { w0 = blk[RH_CTX]; w1 = blk[RH_CTX + 1]; }
-    else { const uint32_t o = var == 0 ? RH_P : var == 1 ? RH_A : RH_R; w0 = blk[o]; w1 = blk[o + 1]; }
+    else { const auto& u = var == 0 ? pu : var == 1 ? au : ru; w0 = mk_w0(T_ENT, u.first); w1 = u.second; }
     uint32_t code = E_NONE, aux = 0, k = 0, et = 0, ei = 0;
     bool fin = false;
     for (uint32_t j = 0; j < depth && code == E_NONE; j++) {

@@ -52,18 +52,17 @@ __host__ __device__ constexpr inline uint32_t mk_w0(uint32_t tag, uint32_t x) { 
 __host__ __device__ constexpr inline uint32_t mk_ref(uint32_t space, uint32_t off) { return (space << SPACE_SHIFT) | (off & OFF_MASK); }
 
 // ---- request block header -------------------------------------------------------------------
+// (the principal / action / resource UIDs are the row's RW_P / RW_A / RW_R: every kernel reads the
+// row before the block, so the block does not repeat them)
 enum ReqHdr : uint32_t {
   RH_NENT = 0,
-  RH_P = 1,      // principal (ENT value, 2 words)
-  RH_A = 3,      // action
-  RH_R = 5,      // resource
-  RH_CTX = 7,    // context value (REC, 2 words)
-  RH_PIDX = 9,   // entity-table index of principal / action / resource (NO_ENT if absent)
-  RH_AIDX = 10,
-  RH_RIDX = 11,
-  RH_SBASE = 12, // index of the request's first string in the batch string table (bstr_off)
-  RH_SCTX = 13,  // the request's scope contexts, resolved by the encoder (CTXR_SLOTS words, below)
-  RH_WORDS = 17, // entity table follows: n_ent * ENT_WORDS
+  RH_CTX = 1,    // context value (REC, 2 words)
+  RH_PIDX = 3,   // entity-table index of principal / action / resource (NO_ENT if absent)
+  RH_AIDX = 4,
+  RH_RIDX = 5,
+  RH_SBASE = 6,  // index of the request's first string in the batch string table (bstr_off)
+  RH_SCTX = 7,   // the request's scope contexts, resolved by the encoder (CTXR_SLOTS words, below)
+  RH_WORDS = 11, // entity table follows: n_ent * ENT_WORDS
 };
 // Host-resolved scope contexts (image.h "scope bitsets"). A request's contexts depend on its
 // action, resource and hot values only, never on its principal, so the encoder looks them up in

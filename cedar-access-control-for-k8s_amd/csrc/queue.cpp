@@ -504,6 +504,30 @@ const char* cg_queue_last_error(void) { return t_err.c_str(); }
 
 namespace {
 
+// One SubjectAccessReview body on the caller's thread: GetAuthorizerAttributes, Authorize's fast
+// paths and RecordToCedarResource into t.e (returns 1), or a fast-path decision (returns 2, *fast
+// and *reason set), or a CG_E_* error (< 0, t_err set).
+int encode_sar(const LoadedImage& li, const char* sar_json, size_t len, Ticket& t, int* fast, std::string& reason) {
+  EncodedRequest& e = t.e;
+  int d = 0;
+  *fast = -1;
+  GUARD(t_err, { d = encode_sar_direct(*li.host, sar_json, len, e, *fast, reason); })
+  if (d == 2) return 2;
+  if (d == 0) {  // the general path: JSON tree, Attributes, entities
+    std::vector<EntityIn> ents;
+    RequestIn req;
+    GUARD(t_err, {
+      JVal v = json_parse(sar_json, len);
+      Attributes a = attributes_from_sar(v);
+      *fast = authorize_fast_path(a, reason);
+      if (*fast >= 0) return 2;
+      record_to_cedar(a, ents, req);
+      encode_request(*li.host, ents, req, e);
+    })
+  }
+  return 1;
+}
+
 int authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout_ns, int* decision, char* reason,
                   size_t cap, size_t* need) {
   const int64_t deadline = timeout_ns < 0 ? -1 : now_ns() + timeout_ns;
@@ -511,36 +535,103 @@ int authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout
   Ticket& t = *tp;
   t.img = active_image(q->ctxs[0], t_err);
   if (!t.img) return CG_E_STATE;
-  const std::shared_ptr<LoadedImage>& li = t.img;
-  EncodedRequest& e = t.e;
-  {
-    int fast = -1;
-    std::string r;
-    int d;
-    GUARD(t_err, { d = encode_sar_direct(*li->host, sar_json, len, e, fast, r); })
-    if (d == 2) {
-      q->n_fast++;
-      *decision = fast;
-      return put_string(r, reason, cap, need);
-    }
-    if (d == 0) {  // the general path: JSON tree, Attributes, entities
-      std::vector<EntityIn> ents;
-      RequestIn req;
-      GUARD(t_err, {
-        JVal v = json_parse(sar_json, len);
-        Attributes a = attributes_from_sar(v);
-        fast = authorize_fast_path(a, r);
-        if (fast >= 0) {
-          q->n_fast++;
-          *decision = fast;
-          return put_string(r, reason, cap, need);
-        }
-        record_to_cedar(a, ents, req);
-        encode_request(*li->host, ents, req, e);
-      })
-    }
+  std::string r;
+  const int d = encode_sar(*t.img, sar_json, len, t, decision, r);
+  if (d < 0) return d;
+  if (d == 2) {
+    q->n_fast++;
+    return put_string(r, reason, cap, need);
   }
   return submit_ticket(q, tp, deadline, decision, reason, cap, need, true);
+}
+
+// cg_queue_authorize_sar_n: the n requests encoded on the caller's thread, queued under one stripe
+// lock, one sleep until every one's batch is published, then rendered into `out`.
+int authorize_sar_n(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, int64_t timeout_ns,
+                    int* decisions, char* out, size_t cap, size_t* offsets, size_t* need) {
+  const int64_t deadline = timeout_ns < 0 ? -1 : now_ns() + timeout_ns;
+  std::shared_ptr<LoadedImage> img = active_image(q->ctxs[0], t_err);
+  if (!img) return CG_E_STATE;
+  std::vector<TicketP> tps(n);
+  std::vector<std::string> fast_reason(n);
+  std::vector<TicketP> queued;
+  queued.reserve(n);
+  for (uint32_t k = 0; k < n; k++) {
+    tps[k] = std::make_shared<Ticket>();
+    tps[k]->img = img;
+    const int d = encode_sar(*img, sars[k], lens[k], *tps[k], &decisions[k], fast_reason[k]);
+    if (d < 0) return d;
+    if (d == 2) {
+      q->n_fast++;
+      tps[k].reset();
+    } else {
+      queued.push_back(tps[k]);
+    }
+  }
+  if (!queued.empty()) {
+    if (q->stop.load()) { t_err = "queue closed"; return CG_E_STATE; }
+    if (t_stripe == 0xFFFFFFFFu) t_stripe = q->next_stripe.fetch_add(1) % STRIPES;
+    const auto t0 = Clock::now();
+    {
+      Stripe& st = q->stripes[t_stripe];
+      std::lock_guard<std::mutex> g(st.mu);
+      for (auto& tp : queued) {
+        tp->t = t0;
+        st.q.push_back(tp);
+      }
+    }
+    if (q->pending.fetch_add((uint32_t)queued.size(), std::memory_order_release) == 0) q->pending.notify_one();
+    for (size_t left = 0;;) {  // every queued request's batch published (or the deadline)
+      const uint32_t w = q->pub.load(std::memory_order_acquire);
+      while (left < queued.size() && queued[left]->ready.load(std::memory_order_acquire)) left++;
+      if (left == queued.size()) break;
+      int64_t rel = -1;
+      if (deadline >= 0) {
+        rel = deadline - now_ns();
+        if (rel <= 0) {
+          for (auto& tp : queued) {
+            uint32_t s0 = T_QUEUED;
+            (void)tp->state.compare_exchange_strong(s0, T_ABANDONED);
+          }
+          t_err = "deadline exceeded waiting for the device batch";
+          return CG_E_TIMEOUT;
+        }
+      }
+      futex_wait(&q->pub, w, rel);
+    }
+    for (auto& tp : queued) {
+      if (tp->rc) { t_err = tp->err; return tp->rc; }
+      if (tp->qb->rc) { t_err = tp->qb->err; return tp->qb->rc; }
+    }
+  }
+  // the reasons, NUL-terminated, side by side in `out` (offsets[k]: request k's)
+  size_t pos = 0;
+  std::vector<char> buf(4096);
+  for (uint32_t k = 0; k < n; k++) {
+    const char* r = nullptr;
+    size_t rl = 0;
+    if (!tps[k]) {
+      r = fast_reason[k].c_str();
+      rl = fast_reason[k].size();
+    } else {
+      const Ticket& t = *tps[k];
+      q->n_requests++;
+      size_t nd = 0;
+      int rc = cg_batch_authz(t.qb->b, t.idx, &decisions[k], buf.data(), buf.size(), &nd);
+      if (rc == CG_E_RANGE) {
+        buf.resize(nd);
+        rc = cg_batch_authz(t.qb->b, t.idx, &decisions[k], buf.data(), buf.size(), &nd);
+      }
+      if (rc) { t_err = t.qb->b->err; return rc; }
+      r = buf.data();
+      rl = nd ? nd - 1 : 0;
+    }
+    if (offsets) offsets[k] = pos;
+    if (out && pos + rl + 1 <= cap) std::memcpy(out + pos, r, rl + 1);
+    pos += rl + 1;
+  }
+  if (need) *need = pos;
+  return (out && pos > cap) ? CG_E_RANGE : CG_OK;
 }
 
 int is_authorized_json(cg_queue* q, const char* item_json, size_t len, int64_t timeout_ns, int* allow, char* diag,
@@ -579,6 +670,16 @@ int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_
   const int rc = authorize_sar(q, sar_json, len, timeout_ns, decision, reason, cap, need);
   q->m.request(outcome(rc, *decision, false),
                (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
+  return rc;
+}
+
+int cg_queue_authorize_sar_n(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, int64_t timeout_ns,
+                             int* decisions, char* reasons, size_t cap, size_t* offsets, size_t* need) {
+  if (!q || (n && (!sars || !lens || !decisions))) return CG_E_ARG;
+  const auto t0 = Clock::now();
+  const int rc = authorize_sar_n(q, sars, lens, n, timeout_ns, decisions, reasons, cap, offsets, need);
+  const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+  for (uint32_t k = 0; k < n; k++) q->m.request(outcome(rc, rc ? 0 : decisions[k], false), ns);
   return rc;
 }
 
@@ -644,7 +745,13 @@ int cg_queue_dropped(cg_queue* q, uint64_t* abandoned) {
 int cg_queue_loadgen(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, uint32_t threads,
                      uint64_t total, double* seconds, uint64_t* lat_p50, uint64_t* lat_p99, uint64_t* lat_max,
                      uint64_t* counts) {
-  if (!q || !sars || !lens || !n || !threads) return CG_E_ARG;
+  return cg_queue_loadgen_n(q, sars, lens, n, threads, 1, total, seconds, lat_p50, lat_p99, lat_max, counts);
+}
+
+int cg_queue_loadgen_n(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, uint32_t threads,
+                       uint32_t per_call, uint64_t total, double* seconds, uint64_t* lat_p50, uint64_t* lat_p99,
+                       uint64_t* lat_max, uint64_t* counts) {
+  if (!q || !sars || !lens || !n || !threads || !per_call) return CG_E_ARG;
   std::atomic<uint64_t> next{0};
   std::atomic<int> first_rc{0};
   std::mutex err_mu;
@@ -653,18 +760,35 @@ int cg_queue_loadgen(cg_queue* q, const char* const* sars, const size_t* lens, u
   std::vector<std::array<uint64_t, 3>> cnt(threads, {0, 0, 0});
   auto work = [&](uint32_t t) {
     std::vector<char> buf(4096);
+    std::vector<const char*> ps(per_call);
+    std::vector<size_t> ls(per_call), offs(per_call);
+    std::vector<int> ds(per_call);
     lat[t].reserve(total / threads + 1);
-    for (uint64_t i; (i = next++) < total;) {
-      const uint32_t k = (uint32_t)(i % n);
-      int d = 0;
+    for (uint64_t i; (i = next.fetch_add(per_call)) < total;) {
+      const uint32_t m = (uint32_t)std::min<uint64_t>(per_call, total - i);
+      for (uint32_t j = 0; j < m; j++) {
+        const uint32_t k = (uint32_t)((i + j) % n);
+        ps[j] = sars[k];
+        ls[j] = lens[k];
+      }
       size_t need = 0;
       const auto t1 = Clock::now();
-      int rc = cg_queue_authorize_sar(q, sars[k], lens[k], -1, &d, buf.data(), buf.size(), &need);
-      if (rc == CG_E_RANGE) {
-        buf.resize(need);
-        rc = cg_queue_authorize_sar(q, sars[k], lens[k], -1, &d, buf.data(), buf.size(), &need);
+      int rc;
+      if (per_call == 1) {
+        rc = cg_queue_authorize_sar(q, ps[0], ls[0], -1, &ds[0], buf.data(), buf.size(), &need);
+        if (rc == CG_E_RANGE) {
+          buf.resize(need);
+          rc = cg_queue_authorize_sar(q, ps[0], ls[0], -1, &ds[0], buf.data(), buf.size(), &need);
+        }
+      } else {
+        rc = cg_queue_authorize_sar_n(q, ps.data(), ls.data(), m, -1, ds.data(), buf.data(), buf.size(), offs.data(), &need);
+        if (rc == CG_E_RANGE) {
+          buf.resize(need);
+          rc = cg_queue_authorize_sar_n(q, ps.data(), ls.data(), m, -1, ds.data(), buf.data(), buf.size(), offs.data(), &need);
+        }
       }
-      lat[t].push_back((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t1).count());
+      const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t1).count();
+      for (uint32_t j = 0; j < m; j++) lat[t].push_back(ns);  // (each request's latency is its call's)
       if (rc) {
         int z = 0;
         if (first_rc.compare_exchange_strong(z, rc)) {
@@ -674,7 +798,8 @@ int cg_queue_loadgen(cg_queue* q, const char* const* sars, const size_t* lens, u
         next = total;  // stop every worker
         return;
       }
-      if (d >= 0 && d < 3) cnt[t][d]++;
+      for (uint32_t j = 0; j < m; j++)
+        if (ds[j] >= 0 && ds[j] < 3) cnt[t][(size_t)ds[j]]++;
     }
   };
   const auto t0 = Clock::now();

@@ -375,6 +375,17 @@ const char* cg_queue_last_error(void);
  * CG_E_DEVICE the caller answers NoOpinion (authorizer.go:80-84; the apiserver's failurePolicy). */
 int cg_queue_authorize_sar(cg_queue* q, const char* sar_json, size_t len, int64_t timeout_ns, int* decision,
                            char* reason, size_t cap, size_t* need);
+/* cg_queue_authorize_sar for n SubjectAccessReview bodies in one call: the entry point of a host-side
+ * batcher (north_star's batching layer in internal/server: one goroutine collects the webhook
+ * goroutines' requests and crosses into cgo once per group). The n requests are encoded on the
+ * calling thread, join the open device batches together and the call blocks until all are
+ * evaluated. decisions[k] as cg_queue_authorize_sar's; the reasons are written NUL-terminated side
+ * by side into reasons[0..cap) with request k's at offsets[k] (any of reasons / offsets may be
+ * NULL); *need receives the bytes they take, and CG_E_RANGE means reasons was too small (call
+ * again with room). A deadline miss or device error fails the whole call (every request answers
+ * NoOpinion). */
+int cg_queue_authorize_sar_n(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, int64_t timeout_ns,
+                             int* decisions, char* reasons, size_t cap, size_t* offsets, size_t* need);
 /* TieredPolicyStores.IsAuthorized for one Cedar-JSON item (cg_batch_add_json's format) through
  * the queue: *allow and, when diag or need is given, json.Marshal(cedar.Diagnostic). timeout_ns as
  * for cg_queue_authorize_sar; on CG_E_TIMEOUT / CG_E_DEVICE the admission caller allows. */
@@ -426,6 +437,11 @@ int cg_queue_metrics_get(cg_queue* q, cg_queue_metrics* out, size_t size);
 int cg_queue_loadgen(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, uint32_t threads,
                      uint64_t total, double* seconds, uint64_t* lat_p50, uint64_t* lat_p99, uint64_t* lat_max,
                      uint64_t* counts);
+/* The same with each caller thread carrying per_call requests per cg_queue_authorize_sar_n call
+ * (a request's latency is its call's). */
+int cg_queue_loadgen_n(cg_queue* q, const char* const* sars, const size_t* lens, uint32_t n, uint32_t threads,
+                       uint32_t per_call, uint64_t total, double* seconds, uint64_t* lat_p50, uint64_t* lat_p99,
+                       uint64_t* lat_max, uint64_t* counts);
 
 #ifdef __cplusplus
 }

@@ -142,6 +142,46 @@ def test_queue_loadgen_counts_match_batch(ctx):
     assert m["active_epoch"] == 103 and m["activations"] >= 1
 
 
+@pytest.mark.parametrize("per_call", [1, 3, 16])
+def test_queue_authorize_many_matches_oracle(ctx, per_call):
+    """cg_queue_authorize_sar_n (a host-side batcher's entry point): groups of SARs per call from
+    several threads, fast paths mixed in, every (decision, reason) equal to the oracle's Authorize;
+    the native load generator's batched mode counts the same decisions as per-request calls."""
+    text = _demo()
+    _load(ctx, [cedargpu.MemoryStore("demo.cedar", text)], 105)
+    sars = synth.random_sars(600, seed=31, pop=synth.Population(seed=31, n_users=500, n_groups=60))
+    sars.insert(7, synth.make_sar("system:authorizer:cedar-authorizer", "", [], "get", group="rbac.authorization.k8s.io",
+                                  resource="roles"))
+    otiers = _oracle_tiers(text)
+    want = [km.authorize(otiers, km.attributes_from_sar(s)) for s in sars]
+    got = [None] * len(sars)
+    q = cedargpu.Queue(ctx, max_batch=64)
+    errors = []
+    groups = [list(range(i, min(i + per_call, len(sars)))) for i in range(0, len(sars), per_call)]
+
+    def work(t):
+        try:
+            for g in groups[t::6]:
+                for i, r in zip(g, q.authorize_many([sars[i] for i in g])):
+                    got[i] = r
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    ws = [threading.Thread(target=work, args=(t,)) for t in range(6)]
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join(120)
+    assert not errors, errors[0]
+    for s, g, w in zip(sars, got, want):
+        assert g == w, s
+    one = q.loadgen([json.dumps(s) for s in sars], threads=8, total=len(sars))
+    many = q.loadgen([json.dumps(s) for s in sars], threads=8, total=len(sars), per_call=per_call)
+    q.close()
+    assert [many[k] for k in ("deny", "allow", "no_opinion")] == [one[k] for k in ("deny", "allow", "no_opinion")]
+    assert [one[k] for k in ("deny", "allow", "no_opinion")] == [sum(1 for d, _ in want if d == k) for k in (0, 1, 2)]
+
+
 def test_queue_errors(ctx):
     q = cedargpu.Queue(ctx, max_batch=16)
     with pytest.raises(cedargpu.CedarGPUError):
