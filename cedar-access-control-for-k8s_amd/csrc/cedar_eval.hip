@@ -1780,7 +1780,10 @@ constexpr uint32_t COMBO_AENT = combo_mask_of(KC_ENT, 2, 1), COMBO_RENT = combo_
 // [1] level-1 probes [2] level-1 entries found [3] level-2 probes [4] level-2 buckets found
 // [5] loop iterations (per wave) [6] segment iterations spent on level-2 probes [7] segment
 // iterations in all [8] prologue cycles [9] loop cycles (per wave, s_memtime) [10] keys enumerated
-template <uint32_t SEG, uint32_t MINW = 1, bool BITS = false, bool STATS = false>
+// LOOKUP (BITS only): the scan looks up the contexts the encoder did not resolve (image.h RH_SCTX)
+// in the context table itself; without it such a request enumerates its keys instead, and the
+// kernel carries none of the lookup's registers (CEDARGPU_SCAN_LOOKUP=1: with it, A/B)
+template <uint32_t SEG, uint32_t MINW = 1, bool BITS = false, bool STATS = false, bool LOOKUP = false>
 __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
   const uint64_t t0 = STATS ? clock64() : 0;
   uint32_t st[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1863,7 +1866,7 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     }
     // BITS: lane k < popc(l2_lmask) reads the k-th list slot's head and first LW words after it
     // (element count or marker, elements) in the same trip
-    if (BITS && klist && !hres && a.hlists && sl < (uint32_t)__builtin_popcount(a.l2_lmask)) {
+    if (LOOKUP && BITS && klist && !hres && a.hlists && sl < (uint32_t)__builtin_popcount(a.l2_lmask)) {
       l_lo = row[RW_HDR + 2 * a.n_hot + __popc(a.hlists & ((1u << nth_bit(a.l2_lmask, sl)) - 1u))];
       l_hd = blk[l_lo];
 #pragma unroll
@@ -1928,16 +1931,16 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     bool on = kbits && klist && simple;
     const uint32_t vm = a.l2_vmask, lm = a.l2_lmask, pe = cm & COMBO_PENT;  // wave-uniform
     const uint32_t nvs = __builtin_popcount(vm), nls = __builtin_popcount(lm), ncb = __builtin_popcount(pe);
-    const uint32_t lc = (on && sl < nls && a.hlists) ? ((l_hd & 0x80000000u) ? 1u : l_hd) : 0u;  // list entries
+    const uint32_t lc = (LOOKUP && on && sl < nls && a.hlists) ? ((l_hd & 0x80000000u) ? 1u : l_hd) : 0u;  // list entries
     uint32_t linc = lc;  // inclusive prefix over the segment's lanes
     for (uint32_t o = 1; o < SEG; o <<= 1) {
       const uint32_t y = (uint32_t)__shfl_up((int)linc, o);
       if (sl >= o) linc += y;
     }
     const uint32_t per = 1u + nvs + sbcast(linc, SEG - 1), nctx = ncb * per;
-    on = on && (hres || nctx <= CTX_CAP);
+    on = on && (hres || (LOOKUP && nctx <= CTX_CAP));
     uint32_t nf = 0;  // contexts found (segment-uniform)
-    const bool look = on && !hres;
+    const bool look = LOOKUP && on && !hres;
     if (hres) {  // resolved by the encoder: CTXR_EMPTY after the last
       const bool got = sl < CTXR_SLOTS && hcx != CTXR_EMPTY;
       const uint64_t mk = sballot(got);
@@ -4429,7 +4432,9 @@ static void launch_probe(const KArgs& k, uint32_t n, hipStream_t s, bool big = f
                      h[15], h[13], h[11], h[12] / r, h[14] / r);
       }
     } else if (k.scan_filt && k.sbits_words) {
-      if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6, true>), sg, sb, 0, s, k);
+      static const bool lookup = std::getenv("CEDARGPU_SCAN_LOOKUP") && *std::getenv("CEDARGPU_SCAN_LOOKUP") == '1';
+      if (lookup) hipLaunchKernelGGL((cedar_scan_kernel<8, 6, true, false, true>), sg, sb, 0, s, k);
+      else if (socc == 6) hipLaunchKernelGGL((cedar_scan_kernel<8, 6, true>), sg, sb, 0, s, k);
       else if (socc == 7) hipLaunchKernelGGL((cedar_scan_kernel<8, 7, true>), sg, sb, 0, s, k);
       else if (socc == 8) hipLaunchKernelGGL((cedar_scan_kernel<8, 8, true>), sg, sb, 0, s, k);
       else hipLaunchKernelGGL((cedar_scan_kernel<8, 1, true>), sg, sb, 0, s, k);

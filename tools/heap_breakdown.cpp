@@ -4,6 +4,7 @@
 // element-hash lists), plus the row and the ancestor-list records the batch interns.
 // Build: make -C tools heap_breakdown
 // Usage: heap_breakdown <policies.cedar> <static entities.json> <sars.jsonl>
+#include <chrono>
 #include <cstdio>
 #include <fstream>
 #include <sstream>
@@ -35,12 +36,17 @@ int main(int argc, char** argv) {
   b.img = img;
   double n = 0, hdr = 0, ents = 0, rest = 0, row = 0, strs = 0, fast = 0;
   EncodedRequest e;
-  for (std::string line; std::getline(f, line);) {
+  std::vector<std::string> lines;
+  for (std::string line; std::getline(f, line);) lines.push_back(line);
+  double enc_s = 0;
+  for (const std::string& line : lines) {
     if (line.empty()) continue;
     e.clear();
     int fp = -1;
     std::string reason;
+    const auto t0 = std::chrono::steady_clock::now();
     const int r = encode_sar_direct(*img, line.data(), line.size(), e, fp, reason);
+    enc_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (r != 1) { fast++; continue; }
     n++;
     const uint32_t ne = e.blk[cgi::RH_NENT];
@@ -52,7 +58,7 @@ int main(int argc, char** argv) {
     b.append(e);
   }
   const double heap = b.heap.size() * 4.0;
-  std::printf("requests %.0f (fast path %.0f)\n", n, fast);
+  std::printf("requests %.0f (fast path %.0f), encode %.2f us per request on one thread\n", n, fast, enc_s / (n + fast) * 1e6);
   std::printf("per request: block header %.1f B, entity table %.1f B, records / errors / lists %.1f B, row %.1f B, "
               "strings %.1f B\n", hdr / n, ents / n, rest / n, row / n, strs / n);
   std::printf("heap %.1f B per request, of which ancestor-list records %.1f B (list words %llu, shared %llu)\n", heap / n,
