@@ -45,7 +45,8 @@ namespace {
 constexpr int BLOCK = 256;
 // Diagnostic builds only (never the shipped library): CG_DBG removes one part of the pooled
 // candidate pass to time the rest (results are wrong): 1 no atom evaluation, 2 no hit recording
-// past the count, 3 no merge, 4 every lane loads the same head (tools/gpu_session.sh dbg step).
+// past the count, 3 no merge, 4 every lane loads the same head, 5 a set atom's element-hash match
+// taken without the exact record compare (tools/gpu_session.sh dbg step).
 #ifndef CG_DBG
 #define CG_DBG 0
 #endif
@@ -814,7 +815,7 @@ __device__ __forceinline__ uint32_t eval_atom(const CT& c, const uint32_t* rec, 
             th = chash_mix(chash_mix(th, fl[0]), fh);
           }
           for (uint32_t i = 0; i < n && !f && hashable; i++)
-            if (c.blk[hl + 1 + i] == th) f = rs_rec_eq<STRUCT>(c, rec, load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i)), t, deep);
+            if (c.blk[hl + 1 + i] == th) f = CG_DBG == 5 ? true : rs_rec_eq<STRUCT>(c, rec, load_val(c, rd(c, ref, 1 + 2 * i), rd(c, ref, 2 + 2 * i)), t, deep);
           t += 1 + RS_FIELD_WORDS * nk;
         }
         if (hashable) {
