@@ -1091,6 +1091,33 @@ static void parallel_range(size_t n, const std::function<void(size_t)>& fn) {
   for (auto& t : ts) t.join();
 }
 
+// fn(k) for each of n coarse tasks on up to 16 threads (one task at a time; fn must not throw)
+static void parallel_tasks(size_t n, const std::function<void(size_t)>& fn) {
+  const unsigned nt = (unsigned)std::min<size_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())), n);
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t k; (k = next.fetch_add(1)) < n;) fn(k);
+  };
+  std::vector<std::thread> ts;
+  for (unsigned t = 1; t < nt; t++) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+}
+
+// v = n zero words, zeroed on several threads (1 MB pieces: the pages fault in side by side)
+static void zeroed(RawWords& v, size_t n) {
+  v.clear();
+  v.resize(n);
+  const size_t piece = 1u << 18;
+  parallel_tasks((n + piece - 1) / piece, [&](size_t k) {
+    std::fill(v.begin() + (long)(k * piece), v.begin() + (long)std::min(n, (k + 1) * piece), 0u);
+  });
+}
+
 // Scope index (image.h "scope index"): file each policy of an all-atomic image under the key set
 // with the fewest competing policies (a level-1 scope key, refined by the policy's attribute key
 // when it has one), then lay out fixed record heads bucket by bucket and the full records in the
@@ -1221,50 +1248,85 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   std::vector<std::pair<L1, uint32_t>> r1;
   std::vector<std::pair<L2, uint32_t>> r2;
   std::vector<uint64_t> kents;  // entity components of the level-1 keys
-  r1.reserve(n);
-  r2.reserve(2 * (size_t)n);
-  std::vector<std::pair<uint32_t, uint32_t>> acts;  // a policy's action components
-  for (uint32_t p = 0; p < n; p++) {
-    if (rep[p] != p) continue;  // filed through its class representative
-    const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
-    const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
-    auto comp = [](uint32_t kind, uint32_t ty, uint32_t et, uint32_t ei, uint32_t& kc, uint32_t& t, uint32_t& i) {
-      if (kind == SK_EQ || kind == SK_IN || kind == SK_ISIN) { kc = KC_ENT; t = et; i = ei; }
-      else if (kind == SK_IS) { kc = KC_TYPE; t = ty; i = KW_ANY; }
-      else { kc = KC_WILD; t = KW_ANY; i = KW_ANY; }
-    };
-    uint32_t pkc, pt, pi, rkc, rt, ri;
-    comp(pk, d[PW_P_TYPE], d[PW_P_ET], d[PW_P_EI], pkc, pt, pi);
-    comp(rk, d[PW_R_TYPE], d[PW_R_ET], d[PW_R_EI], rkc, rt, ri);
-    acts.clear();
-    uint32_t akc = KC_ENT;
-    if (ak == SK_EQ || ak == SK_IN) acts.emplace_back(d[PW_A_ET], d[PW_A_EI]);
-    else if (ak == SK_INSET) {
-      for (uint32_t k = 0; k < d[PW_A_ET]; k++) acts.emplace_back(img.cpool[d[PW_A_EI] + 2 * k], img.cpool[d[PW_A_EI] + 2 * k + 1]);
-      std::sort(acts.begin(), acts.end());
-      acts.erase(std::unique(acts.begin(), acts.end()), acts.end());  // empty: `action in []` never applies
-    } else {
-      akc = KC_WILD;
-      acts.emplace_back(KW_ANY, KW_ANY);
-    }
-    const uint32_t combo = key_combo(pkc, akc, rkc);
-    if (pkc == KC_ENT) kents.push_back(((uint64_t)pt << 32) | pi);
-    if (rkc == KC_ENT) kents.push_back(((uint64_t)rt << 32) | ri);
-    for (auto& a : acts) {
-      if (akc == KC_ENT) kents.push_back(((uint64_t)a.first << 32) | a.second);
-      const L1 k{combo, pt, pi, a.first, a.second, rt, ri};
-      if ((pt != KW_ANY && pt >= (1u << 28)) || (rt != KW_ANY && rt >= (1u << 28))) throw CedarError("string table too large for the scope index");
-      img.combo_mask |= 1u << combo;
-      if (!akeys[p].ok) { r1.emplace_back(k, p); continue; }
-      r1.emplace_back(k, NO_POLICY);  // the level-1 entry carries the hmask even without unkeyed policies
-      const uint32_t hk = akeys[p].h | (akeys[p].contains ? BT_CKEY : 0u);
-      r2.emplace_back(L2(k, {hk, akeys[p].v0, akeys[p].v1}), p);
-      if (!akeys[p].guarded) r2.emplace_back(L2(k, {hk, MISSING_W0, 0u}), p);
-      if (akeys[p].contains) {
-        r2.emplace_back(L2(k, {hk, NOTSET_W0, 0u}), p);  // contains on a non-set (like on a non-string) raises
-        if (!akeys[p].plen) img.cslot_mask |= 1u << akeys[p].h;
+  // filed in blocks of policies side by side, the blocks' records then concatenated in order
+  // (the same records in the same order as one walk)
+  struct Filed {
+    std::vector<std::pair<L1, uint32_t>> r1;
+    std::vector<std::pair<L2, uint32_t>> r2;
+    std::vector<uint64_t> kents;
+    uint32_t combo_mask = 0, cslot_mask = 0;
+    bool too_large = false;
+  };
+  const uint32_t fblk = 2048;
+  std::vector<Filed> filed((n + fblk - 1) / fblk);
+  parallel_tasks(filed.size(), [&](size_t b) {
+    Filed& F = filed[b];
+    auto& r1 = F.r1;
+    auto& r2 = F.r2;
+    auto& kents = F.kents;
+    std::vector<std::pair<uint32_t, uint32_t>> acts;  // a policy's action components
+    for (uint32_t p = (uint32_t)b * fblk; p < std::min<uint32_t>(n, (uint32_t)(b + 1) * fblk); p++) {
+      if (rep[p] != p) continue;  // filed through its class representative
+      const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
+      const uint32_t pk = d[PW_KINDS] & 0xFF, ak = (d[PW_KINDS] >> 8) & 0xFF, rk = (d[PW_KINDS] >> 16) & 0xFF;
+      auto comp = [](uint32_t kind, uint32_t ty, uint32_t et, uint32_t ei, uint32_t& kc, uint32_t& t, uint32_t& i) {
+        if (kind == SK_EQ || kind == SK_IN || kind == SK_ISIN) { kc = KC_ENT; t = et; i = ei; }
+        else if (kind == SK_IS) { kc = KC_TYPE; t = ty; i = KW_ANY; }
+        else { kc = KC_WILD; t = KW_ANY; i = KW_ANY; }
+      };
+      uint32_t pkc, pt, pi, rkc, rt, ri;
+      comp(pk, d[PW_P_TYPE], d[PW_P_ET], d[PW_P_EI], pkc, pt, pi);
+      comp(rk, d[PW_R_TYPE], d[PW_R_ET], d[PW_R_EI], rkc, rt, ri);
+      acts.clear();
+      uint32_t akc = KC_ENT;
+      if (ak == SK_EQ || ak == SK_IN) acts.emplace_back(d[PW_A_ET], d[PW_A_EI]);
+      else if (ak == SK_INSET) {
+        for (uint32_t k = 0; k < d[PW_A_ET]; k++) acts.emplace_back(img.cpool[d[PW_A_EI] + 2 * k], img.cpool[d[PW_A_EI] + 2 * k + 1]);
+        std::sort(acts.begin(), acts.end());
+        acts.erase(std::unique(acts.begin(), acts.end()), acts.end());  // empty: `action in []` never applies
+      } else {
+        akc = KC_WILD;
+        acts.emplace_back(KW_ANY, KW_ANY);
+      }
+      const uint32_t combo = key_combo(pkc, akc, rkc);
+      if (pkc == KC_ENT) kents.push_back(((uint64_t)pt << 32) | pi);
+      if (rkc == KC_ENT) kents.push_back(((uint64_t)rt << 32) | ri);
+      for (auto& a : acts) {
+        if (akc == KC_ENT) kents.push_back(((uint64_t)a.first << 32) | a.second);
+        const L1 k{combo, pt, pi, a.first, a.second, rt, ri};
+        if ((pt != KW_ANY && pt >= (1u << 28)) || (rt != KW_ANY && rt >= (1u << 28))) { F.too_large = true; return; }
+        F.combo_mask |= 1u << combo;
+        if (!akeys[p].ok) { r1.emplace_back(k, p); continue; }
+        r1.emplace_back(k, NO_POLICY);  // the level-1 entry carries the hmask even without unkeyed policies
+        const uint32_t hk = akeys[p].h | (akeys[p].contains ? BT_CKEY : 0u);
+        r2.emplace_back(L2(k, {hk, akeys[p].v0, akeys[p].v1}), p);
+        if (!akeys[p].guarded) r2.emplace_back(L2(k, {hk, MISSING_W0, 0u}), p);
+        if (akeys[p].contains) {
+          r2.emplace_back(L2(k, {hk, NOTSET_W0, 0u}), p);  // contains on a non-set (like on a non-string) raises
+          if (!akeys[p].plen) F.cslot_mask |= 1u << akeys[p].h;
+        }
       }
     }
+  });
+  {
+    size_t n1 = 0, n2 = 0, nk = 0;
+    std::vector<std::array<size_t, 3>> at(filed.size());
+    for (size_t b = 0; b < filed.size(); b++) {
+      const Filed& F = filed[b];
+      if (F.too_large) throw CedarError("string table too large for the scope index");
+      img.combo_mask |= F.combo_mask;
+      img.cslot_mask |= F.cslot_mask;
+      at[b] = {n1, n2, nk};
+      n1 += F.r1.size(); n2 += F.r2.size(); nk += F.kents.size();
+    }
+    r1.resize(n1); r2.resize(n2); kents.resize(nk);
+    parallel_tasks(filed.size(), [&](size_t b) {
+      Filed& F = filed[b];
+      std::copy(F.r1.begin(), F.r1.end(), r1.begin() + (long)at[b][0]);
+      std::copy(F.r2.begin(), F.r2.end(), r2.begin() + (long)at[b][1]);
+      std::copy(F.kents.begin(), F.kents.end(), kents.begin() + (long)at[b][2]);
+      F = Filed();
+    });
   }
   if (times) std::fprintf(stderr, "  index filings: r1 %zu r2 %zu kents %zu\n", r1.size(), r2.size(), kents.size());
   mark("filings");
@@ -1459,7 +1521,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   if (ext_end >= (1ull << 32)) throw CedarError("scope index exceeds 16 GiB");
   // (the candidate pass packs a bucket's first head with its key combination: 27 bits, cedar_eval.hip EF_COMBO)
   if (n_heads >= (1u << 27)) throw CedarError("scope index exceeds 2^27 policy heads");
-  img.bstream.assign(std::max<uint64_t>(ext_end, HEAD_WORDS), 0);
+  zeroed(img.bstream, std::max<uint64_t>(ext_end, HEAD_WORDS));
   parallel_range(n, [&](size_t p) {
     std::copy(img.pstream.begin() + rec_off[p], img.pstream.begin() + rec_off[p] + rec_len[p], img.bstream.begin() + ext[p]);
     if (mlist[p]) {
@@ -1523,7 +1585,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       head++;
     }
   };
-  img.btab.assign(n_entries * BT_WORDS, 0);
+  zeroed(img.btab, n_entries * BT_WORDS);
   parallel_range(g1.size(), [&](size_t gi) {
     const G& g = g1[gi];
     const L1& k = r1[g.b].first;
@@ -1554,9 +1616,10 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   // (a listed key carries its bit's rank in 26 bits: cedar_scan_kernel)
   if (!ctx.empty() && words && (uint64_t)ctx.size() * words * 8 <= SBITS_MAX_BYTES && sbit.size() < (1u << 26)) {
     img.sbits_words = (uint32_t)words;
-    std::vector<uint32_t> bitw((size_t)ctx.size() * words, 0);
+    RawWords bitw;
+    zeroed(bitw, (size_t)ctx.size() * words);
     for (auto& b : sbit) bitw[(size_t)b.row * words + (b.kidx >> 5)] |= 1u << (b.kidx & 31);
-    img.sbits.assign(2 * bitw.size(), 0);
+    zeroed(img.sbits, 2 * bitw.size());
     uint32_t rank = 0;
     for (size_t w = 0; w < bitw.size(); w++) {
       img.sbits[2 * w] = bitw[w];
@@ -1740,40 +1803,46 @@ std::map<Compiler::Path, uint32_t> hot_slots(const std::map<Compiler::Path, uint
 template <class AK>
 static void finish_image(Image& img, const std::vector<AK>& akeys, const std::function<void()>& statics,
                          const std::function<void(const char*)>& mark) {
-  // device policy stream + chunk table
+  // device policy stream + chunk table: the layout (record offsets, chunks) in order, then the
+  // records written side by side (padding words stay zero)
   {
+    const uint32_t np = img.n_pol();
+    std::vector<size_t> at(np);
+    size_t size = 0;
     uint32_t p = 0;
     for (uint32_t t = 0; t < img.n_tiers(); t++) {
       uint32_t pend = img.tier_end[t];
-      uint32_t c_off = (uint32_t)img.pstream.size(), c_p0 = p;
+      uint32_t c_off = (uint32_t)size, c_p0 = p;
       auto close = [&](uint32_t flag) {
-        uint32_t nw = (uint32_t)img.pstream.size() - c_off;
+        uint32_t nw = (uint32_t)size - c_off;
         if (p > c_p0) {
           img.chunks.push_back(c_off); img.chunks.push_back(nw | flag);
           img.chunks.push_back(c_p0); img.chunks.push_back(p);
         }
-        c_off = (uint32_t)img.pstream.size();
+        c_off = (uint32_t)size;
         c_p0 = p;
       };
       for (; p < pend;) {
-        const uint32_t* d = &img.pol[(size_t)p * POL_WORDS];
-        uint32_t ncode = d[PW_CODE_N];
-        uint32_t rec = (POL_WORDS + ncode + 3) & ~3u;
+        uint32_t rec = (POL_WORDS + img.pol[(size_t)p * POL_WORDS + PW_CODE_N] + 3) & ~3u;
         // a record larger than an LDS chunk gets a chunk of its own, read in place (CHUNK_GLOBAL)
         const bool big = rec > CHUNK_WORDS;
-        if (big || (uint32_t)img.pstream.size() - c_off + rec > CHUNK_WORDS) close(0);
-        size_t base = img.pstream.size();
-        img.pstream.insert(img.pstream.end(), d, d + POL_WORDS);
-        img.pstream[base + PW_CODE] = p;
-        img.pstream.insert(img.pstream.end(), img.code.begin() + d[PW_CODE], img.code.begin() + d[PW_CODE] + ncode);
-        while ((img.pstream.size() - base) % 4) img.pstream.push_back(0);
+        if (big || (uint32_t)size - c_off + rec > CHUNK_WORDS) close(0);
+        at[p] = size;
+        size += rec;
         p++;
         if (big) close(CHUNK_GLOBAL);
       }
       close(0);
       img.tier_cend.push_back((uint32_t)img.chunks.size() / 4);
     }
-    if (img.pstream.empty()) img.pstream.resize(4, 0);
+    zeroed(img.pstream, std::max<size_t>(size, 4));
+    parallel_range(np, [&](size_t q) {
+      const uint32_t* d = &img.pol[q * POL_WORDS];
+      uint32_t* o = &img.pstream[at[q]];
+      std::copy(d, d + POL_WORDS, o);
+      o[PW_CODE] = (uint32_t)q;
+      std::copy(img.code.begin() + d[PW_CODE], img.code.begin() + d[PW_CODE] + d[PW_CODE_N], o + POL_WORDS);
+    });
   }
   mark("stream");
   build_scope_index(img, akeys);
@@ -1972,6 +2041,46 @@ std::shared_ptr<Image> compile_image(const std::vector<std::vector<DocSpec>>& ti
     for (size_t t = 0; t < tiers.size(); t++) {
       size_t n = 0;
       for (size_t k = 0; k < tiers[t].size(); k++) n += docs[di + k]->size();
+      for (size_t k = 0; k < tiers[t].size(); k++)
+        if (!tiers[t][k].explicit_id.empty() && docs[di + k]->size() != 1)
+          throw CedarError("document for policy " + tiers[t][k].explicit_id + " must hold exactly one policy");
+      // every ID built side by side; when no two IDs hash alike (so none repeats) the tier is its
+      // documents' policies in order, as the replacing walk below would leave it
+      {
+        std::vector<size_t> start(tiers[t].size() + 1, 0);
+        for (size_t k = 0; k < tiers[t].size(); k++) start[k + 1] = start[k] + docs[di + k]->size();
+        parsed[t].resize(n);
+        std::vector<std::pair<uint64_t, uint32_t>> hs(n);
+        parallel_range(n, [&](size_t q) {
+          const size_t k = (size_t)(std::upper_bound(start.begin(), start.end(), q) - start.begin()) - 1;
+          const DocSpec& doc = tiers[t][k];
+          const std::vector<Policy>& ps = *docs[di + k];
+          const size_t i = q - start[k];
+          PRef& r = parsed[t][q];
+          if (doc.explicit_id.empty()) {
+            char nb[24];
+            const auto tc = std::to_chars(nb, nb + sizeof nb, i);
+            r.id.reserve(doc.id_prefix.size() + (size_t)(tc.ptr - nb) + doc.id_suffix.size());
+            r.id.append(doc.id_prefix).append(nb, tc.ptr).append(doc.id_suffix);
+          } else {
+            r.id = doc.explicit_id;
+          }
+          r.p = &ps[i];
+          r.filename = doc.zero_position ? &k_empty_name : &ps[i].filename;
+          r.pos = doc.zero_position ? Position{} : ps[i].pos;
+          r.doc = (uint32_t)(di + k);
+          r.idx = (uint32_t)i;
+          hs[q] = {std::hash<std::string_view>()(r.id), (uint32_t)q};
+        });
+        parallel_sort(hs, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+        bool dup = false;
+        for (size_t j = 1; j < n && !dup; j++) dup = hs[j].first == hs[j - 1].first;
+        if (!dup) {
+          di += tiers[t].size();
+          continue;
+        }
+        parsed[t].clear();
+      }
       parsed[t].reserve(n);
       // (keys view the IDs in parsed[t], which never reallocates: reserved above)
       std::unordered_map<std::string_view, size_t> ids;
@@ -2167,7 +2276,7 @@ void Image::write_blob(void* wp) const {
   w.u32(IMG_MAGIC); w.u32(IMG_VERSION); w.u64(epoch);
   const size_t table = w.n;
   for (uint32_t k = 0; k < 2 * DS_COUNT + 2; k++) w.u64(0);  // (offset, bytes) per section, begin, end
-  auto words = [](const std::vector<uint32_t>& v) { return std::make_pair((const void*)v.data(), v.size() * 4); };
+  auto words = [](const auto& v) { return std::make_pair((const void*)v.data(), v.size() * 4); };
   const std::pair<const void*, size_t> sec[DS_COUNT] = {
       words(pstream), words(tier_cend), words(chunks), words(cpool), words(gstr_off), words(hot), words(act),
       words(btab), words(bfilt), words(bstream), words(srows), words(shash), words(sctx), words(sbits), words(svals),

@@ -101,6 +101,23 @@ struct PolicyMeta {
 
 struct EncCache;  // encode_impl.h
 
+// Word arrays whose resize() leaves new words unwritten: the builder zeroes or fills a large
+// section on several threads (a serial zero fill faults in every page on one thread: ~45 ms of a
+// 100k-policy build's 70 MB record stream)
+template <class T>
+struct RawAlloc : std::allocator<T> {
+  RawAlloc() = default;
+  template <class U>
+  RawAlloc(const RawAlloc<U>&) {}
+  template <class U>
+  struct rebind { using other = RawAlloc<U>; };
+  template <class U>
+  void construct(U* p) noexcept { ::new ((void*)p) U; }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+using RawWords = std::vector<uint32_t, RawAlloc<uint32_t>>;
+
 // A compiled, immutable policy image (one per policy epoch). Device sections are the vectors
 // uploaded verbatim; the rest is host-side metadata for rendering diagnostics. An image read from a
 // blob (deserialize) leaves the device-only sections empty (pstream, btab, bfilt, bstream, sctx,
@@ -112,7 +129,8 @@ struct Image {
   // with PW_CODE relative to the record; records grouped into chunks of <= CHUNK_WORDS words
   // that never cross a tier. chunks: (word offset, words, first policy, end policy) per chunk;
   // tier_cend[t] = end chunk index of tier t.
-  std::vector<uint32_t> pstream, chunks, tier_cend;
+  RawWords pstream;
+  std::vector<uint32_t> chunks, tier_cend;
   std::vector<uint32_t> act;  // action table: (type sid, id sid) pairs of every action entity in scopes
   uint32_t amask_ok = 0;      // 1 when act has <= MAX_ACT entries (PW_AMASK* valid)
   uint32_t n_atomic = 0;      // policies compiled to atoms (statistics)
@@ -121,7 +139,8 @@ struct Image {
   // btab: the scope index's entries, BT_WORDS each (one all-zero entry when it has none). The
   // open-addressed table of btab_slots slots (image.h "scope index") is built on the device from
   // them at load (cedar_btab_build), so blobs and reload broadcasts carry no empty slots.
-  std::vector<uint32_t> btab, bfilt, bstream;  // bfilt: key filter, 2 words per block
+  RawWords btab, bstream;
+  std::vector<uint32_t> bfilt;  // bfilt: key filter, 2 words per block
   // duplicate classes (host side, image.h "duplicate classes"): the members of the class whose
   // representative (lowest member) is policy p are cls_mem[cls_off[p] .. cls_off[p + 1]), ascending;
   // both empty when no two policies share a record. The first pass may report a class by its
@@ -134,7 +153,8 @@ struct Image {
   // encoder lists a request's ancestors that are among them first (image.h RW_PN)
   std::vector<uint64_t> key_ents;
   // scope bitsets (image.h "scope bitsets"): context table and one row of sbits_words per context
-  std::vector<uint32_t> sctx, sbits, svals;  // sbits: (bits, rank) per word; svals: (first, count) per set bit
+  RawWords sbits;
+  std::vector<uint32_t> sctx, svals;  // sbits: (bits, rank) per word; svals: (first, count) per set bit
   std::vector<uint32_t> sbloom;              // context filter (image.h ctx_bloom_*), 64-bit words
   uint32_t sbits_words = 0;
   uint32_t l2_vmask = 0, l2_lmask = 0;  // hot slots with level-2 value keys / list keys under entity-principal combos
