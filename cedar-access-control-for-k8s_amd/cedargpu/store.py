@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import json
 import threading
+import time
 import weakref
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
@@ -202,6 +203,7 @@ class Compiler:
         """Compiles the tiers. `entities`: the image's static entities (Cedar JSON entity list, e.g.
         a group hierarchy), merged into every request's EntityMap (cg_compiler_set_entities)."""
         c = self._h
+        t0 = time.perf_counter()
         lib.cg_compiler_clear(c)
         eb = _b(json.dumps(entities)) if entities else b""
         rc = lib.cg_compiler_set_entities(c, eb, len(eb))
@@ -225,13 +227,17 @@ class Compiler:
         # cg_compiler_write_image into its storage before anything else can see it): no second
         # copy of a 100 MB image
         n = ctypes.c_size_t(0)
+        t1 = time.perf_counter()
         rc = lib.cg_compiler_build_sized(c, epoch, ctypes.byref(n))
         if rc:
             raise _err(rc, lib.cg_compiler_last_error(c).decode())
+        t2 = time.perf_counter()
         blob = _new_bytes(None, n.value)
         rc = lib.cg_compiler_write_image(c, ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p), n.value)
         if rc:
             raise _err(rc, lib.cg_compiler_last_error(c).decode())
+        # seconds spent handing over the documents, compiling, and writing the blob
+        self.last_times = {"documents": t1 - t0, "compile": t2 - t1, "blob": time.perf_counter() - t2}
         return blob
 
     def doc_errors(self) -> List[dict]:

@@ -1586,6 +1586,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     }
   };
   zeroed(img.btab, n_entries * BT_WORDS);
+  std::vector<uint32_t> h2g(g2.size());  // level-2 bucket hashes (the filter's)
   parallel_range(g1.size(), [&](size_t gi) {
     const G& g = g1[gi];
     const L1& k = r1[g.b].first;
@@ -1599,15 +1600,13 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     const L1& k = r2[g.b].first.first;
     const auto& x = r2[g.b].first.second;
     put_heads(r2.begin() + (long)g.b, r2.begin() + (long)g.e, g2_first[gi]);
+    h2g[gi] = bucket_hash2(l1_hash(k), x[0], x[1], x[2]);
     const uint32_t e[BT_WORDS] = {BT_USED | (k[0] << 16) | BT_L2 | x[0], k[1], k[2], k[3], k[4], k[5], k[6], x[1], x[2],
                                   g2_first[gi], g2_cnt[gi], 0, 0, 0, 0, 0};
     std::copy(e, e + BT_WORDS, img.btab.begin() + (long)((g1.size() + gi) * BT_WORDS));
   });
-  for (size_t gi = 0; gi < g1.size(); gi++) filt_add(l1_hash(r1[g1[gi].b].first));
-  for (size_t gi = 0; gi < g2.size(); gi++) {
-    const auto& x = r2[g2[gi].b].first.second;
-    filt_add(bucket_hash2(l1_hash(r2[g2[gi].b].first.first), x[0], x[1], x[2]));
-  }
+  for (uint32_t h : h1g) filt_add(h);
+  for (uint32_t h : h2g) filt_add(h);
   if (img.btab.empty()) img.btab.assign(BT_WORDS, 0);  // never empty buffers
   mark("heads+slots");
   // the bitset rows as (bits, rank) word pairs, every set bit's bucket at its rank, and the context

@@ -21,4 +21,5 @@ for rep in range(3):
     t0 = time.perf_counter()
     img = comp.build([cedargpu.CRDStore(docs)], epoch=301 + rep)
     times.append((time.perf_counter() - t0) * 1e3)
+    print("split ms", {k: round(v * 1e3, 1) for k, v in comp.last_times.items()}, flush=True)
 print("incremental rebuild ms", [round(t, 1) for t in times], hashlib.sha1(img).hexdigest(), len(img), flush=True)
