@@ -2028,20 +2028,18 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     bool badk = false;
     for (uint32_t rb = 0; __ballot(rb < tot) != 0; rb += SEG * SCAN_PB) {
       uint2 fw[SCAN_PB];
-      uint32_t fk[SCAN_PB], fc[SCAN_PB];
+      uint32_t fb[SCAN_PB];  // the bit's index in its word | combo << 8 (one register per load in flight)
 #pragma unroll
       for (uint32_t u = 0; u < SCAN_PB; u++) {
         const uint32_t t = rb + u * SEG + sl;
         fw[u] = make_uint2(0u, 0u);
-        fk[u] = 0;
-        fc[u] = 0;
+        fb[u] = 0;
         if (t < tot) {
           const uint32_t j = divp(t), ip = t - j * nP;
           const uint32_t jk = ip + 1 - self;  // kid index: 0 the principal, j key ancestor j - 1
           const uint32_t kid = jk <= SCAN_ANC ? s_kid[seg][jk] : kl[jk];
           const uint2 c = s_cx[seg][j];
-          fk[u] = kid;
-          fc[u] = c.x & 0xFFu;
+          fb[u] = (kid & 31u) | ((c.x & 0xFFu) << 8);
           // the bit's word and the rank of the word's first bit, in one 8-byte load
           if (kid < a.n_kent) fw[u] = *reinterpret_cast<const uint2*>(a.sbits + 2 * ((size_t)c.y * a.sbits_words + (kid >> 5)));
           else badk = badk || kid != KIDX_NONE;
@@ -2049,11 +2047,11 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
       }
 #pragma unroll
       for (uint32_t u = 0; u < SCAN_PB; u++) {
-        const uint32_t b = fk[u] & 31u;
+        const uint32_t b = fb[u] & 31u;
         const bool ok = (fw[u].x >> b) & 1u;
         const uint64_t mk = sballot(ok);
         const uint32_t at_ = npos + mbcnt64(mk);
-        if (ok && at_ < SCAN_POS_B) s_pos[seg][at_] = LIST_EXACT | (fc[u] << 26) | (fw[u].y + __popc(fw[u].x & ((1u << b) - 1u)));
+        if (ok && at_ < SCAN_POS_B) s_pos[seg][at_] = LIST_EXACT | ((fb[u] >> 8) << 26) | (fw[u].y + __popc(fw[u].x & ((1u << b) - 1u)));
         npos += popc64(mk);
       }
     }
