@@ -31,6 +31,7 @@
 #include <thread>
 #include <algorithm>
 #include <atomic>
+#include <queue>
 #include <vector>
 #include <string>
 
@@ -4355,7 +4356,29 @@ static void print_probe_stats(const char* what, const std::vector<unsigned long 
     for (int i = 0; i < 16; i++) sum[i] += (double)h[w * 16 + i];
     tot[w] = h[w * 16 + 12] + h[w * 16 + 13] + h[w * 16 + 14] + h[w * 16 + 15];
   }
+  // the launch's makespan if its waves took these cycles, handed in launch order (and, for
+  // comparison, longest first) to 256 CUs x 16 wave slots as each slot frees: how much of the
+  // kernel's time a dispatch order could win back from its slowest waves
+  auto makespan = [&](const std::vector<unsigned long long>& d) {
+    std::priority_queue<unsigned long long, std::vector<unsigned long long>, std::greater<unsigned long long>> free_at;
+    for (int i = 0; i < 256 * 16; i++) free_at.push(0);
+    unsigned long long end = 0;
+    for (unsigned long long x : d) {
+      const unsigned long long t = free_at.top() + x;
+      free_at.pop();
+      free_at.push(t);
+      end = std::max(end, t);
+    }
+    return end;
+  };
+  double all = 0;
+  for (unsigned long long x : tot) all += (double)x;
+  const unsigned long long in_order = makespan(tot);
+  const unsigned long long reversed = makespan(std::vector<unsigned long long>(tot.rbegin(), tot.rend()));
   std::sort(tot.begin(), tot.end());
+  const unsigned long long longest_first = makespan(std::vector<unsigned long long>(tot.rbegin(), tot.rend()));
+  std::fprintf(stderr, "%s dispatch: makespan in launch order %llu, reversed %llu, longest first %llu, bound %.0f (cycles)\n",
+               what, in_order, reversed, longest_first, all / (256.0 * 16.0));
   const double r = sum[0] > 0 ? sum[0] : 1.0, W = (double)nw;
   std::fprintf(stderr,
                "%s stats: requests %.0f | per request: L1 keys %.2f found %.2f | L2 probes %.2f found %.2f | "
