@@ -2544,9 +2544,9 @@ void Image::build_lookup() {
   sindex.clear();
   static_targets.clear();
   for (uint32_t r = 0; r < n_static(); r++) {
-    sindex.emplace(((uint64_t)srows[(size_t)r * ENT_WORDS + ER_TYPE] << 32) | srows[(size_t)r * ENT_WORDS + ER_ID], r);
+    sindex.put(((uint64_t)srows[(size_t)r * ENT_WORDS + ER_TYPE] << 32) | srows[(size_t)r * ENT_WORDS + ER_ID], r);
     const uint32_t pl = srows[(size_t)r * ENT_WORDS + ER_PAD];  // direct parents [n, pairs]
-    for (uint32_t k = 0; k < cpool[pl]; k++) static_targets.insert(((uint64_t)cpool[pl + 1 + 2 * k] << 32) | cpool[pl + 2 + 2 * k]);
+    for (uint32_t k = 0; k < cpool[pl]; k++) static_targets.put(((uint64_t)cpool[pl + 1 + 2 * k] << 32) | cpool[pl + 2 + 2 * k], 0);
   }
   key_bloom.assign(std::max<size_t>(1, key_ents.size() / 4 + 1), 0);  // ~16 bits per key entity
   for (uint64_t k : key_ents) {

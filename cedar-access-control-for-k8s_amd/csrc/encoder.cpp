@@ -128,17 +128,17 @@ void Batch::append(EncodedRequest& e) {
   e.blk[RH_SBASE] = n_bstr();
   e.row[RW_BLK] = B;
   req_base.push_back(B);
-  heap.insert(heap.end(), e.blk.begin(), e.blk.end());
-  rows.insert(rows.end(), e.row.begin(), e.row.end());
+  append_pod(heap, e.blk.data(), e.blk.size());
+  append_pod(rows, e.row.data(), e.row.size());
   gkeys.push_back(e.gkey);
   for (auto& s : e.strs) {
-    bstr_bytes.insert(bstr_bytes.end(), s.begin(), s.end());
+    append_pod(bstr_bytes, (const uint8_t*)s.data(), s.size());
     bstr_off.push_back((uint32_t)bstr_bytes.size());
   }
   if (!img->dev_all_strings()) {  // the device's table: the same ids, bytes of the read strings only
     dstr = true;
     for (size_t k = 0; k < e.strs.size(); k++) {
-      if (k < e.str_dev.size() && e.str_dev[k]) dstr_bytes.insert(dstr_bytes.end(), e.strs[k].begin(), e.strs[k].end());
+      if (k < e.str_dev.size() && e.str_dev[k]) append_pod(dstr_bytes, (const uint8_t*)e.strs[k].data(), e.strs[k].size());
       dstr_off.push_back((uint32_t)dstr_bytes.size());
     }
   }
@@ -186,7 +186,7 @@ uint32_t Batch::intern_list(const uint32_t* w, uint32_t n, uint64_t room, uint64
   }
   if (heap.size() + n > 0xFFFFFFFFull) throw CedarError("batch heap exceeds 16 GiB");
   const uint32_t o = (uint32_t)heap.size();
-  heap.insert(heap.end(), w, w + n);
+  append_pod(heap, w, n);
   memo[2 * s] = key;
   memo[2 * s + 1] = o;
   return o;
