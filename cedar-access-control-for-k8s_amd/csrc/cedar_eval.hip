@@ -1755,7 +1755,7 @@ constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
 constexpr uint32_t LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;  // (CTX_CAP: image.h)
 constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the rest read from the row)
 constexpr uint32_t SCAN_ROW = 56;  // scan LDS row words (64 - 8: see s_kid; the LDS stays under 1/24 of a CU for 6 waves per SIMD)
-static_assert(SCAN_ANC + 2 <= SCAN_ROW && SCAN_POS_B + 2 <= SCAN_ROW, "scan LDS rows");
+static_assert(SCAN_ANC + 2 <= SCAN_ROW - 1 && SCAN_POS_B + 2 <= SCAN_ROW, "scan LDS rows (s_kid's last word: the presence mask)");
 constexpr uint32_t SCAN_PB = 8;    // bit tests per lane per round (loads in flight)
 constexpr uint32_t MEMB_U = 4;     // duplicate-class members a lane copies per round (loads in flight)
 constexpr uint32_t HM_CLASS = 1u << 24;  // hit-slot word (wl.hm): the slot holds a whole duplicate class
@@ -1877,6 +1877,13 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
     for (uint32_t h = sl; h < min(a.n_hot, SCAN_HOT); h += SEG)
       s_hot[seg][h] = valid ? *reinterpret_cast<const uint2*>(row + RW_HDR + 2 * h) : make_uint2(0u, 0u);
     wave_lds_sync();
+  }
+  // BITS: the request's presence mask (image.h "presence masks": the encoder's, in the row), which
+  // the bitset path tests each listed bucket's mask against; parked in its LDS row's last word, so
+  // no register carries it through the key loop
+  if constexpr (BITS) {
+    const uint32_t pm = (hdr(RW_ASELF) >> ASELF_PRES_SHIFT) & ((1u << ASELF_PRES_SLOTS) - 1u);
+    if (sl == 0) s_kid[seg][SCAN_ROW - 1] = pm;
   }
   // level-1 key k of the request: its combo and (principal, action, resource) components
   auto key_at = [&](uint32_t k, uint32_t& cbo, uint2& p, uint2& q, uint2& r) {
@@ -2148,9 +2155,11 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
             key_at(kk, combo, kp, ka, kr);
           }
           uint32_t cmv = 0;
-          if (BITS && (x & LIST_EXACT)) {  // a key the bitsets found: its bucket at the bit's rank
-            const uint2 v = *reinterpret_cast<const uint2*>(a.svals + 2 * (size_t)(x & 0x3FFFFFFu));
-            e = make_uint3(v.x, v.y, 0u);
+          if (BITS && (x & LIST_EXACT)) {  // a key the bitsets found: its bucket at the bit's rank,
+                                           // unless it needs an attribute the request lacks
+            const uint3 v = *reinterpret_cast<const uint3*>(a.svals + SVAL_WORDS * (size_t)(x & 0x3FFFFFFu));
+            const uint32_t pm = s_kid[seg][SCAN_ROW - 1];
+            e = (v.z & ~pm) ? make_uint3(0u, 0u, 0u) : make_uint3(v.x, v.y, 0u);
           } else {
             if (BITS && flt) {
               kp = comb_p(combo, 0u);

@@ -775,13 +775,40 @@ struct Compiler {
     bool contains = false;  // a set-membership key (image.h BT_CKEY): v0 = element hash, v1 = 1
     uint32_t plen = 0;      // a prefix key (image.h "prefix level-2 keys"): prefix bytes hashed into v0
     uint32_t h = 0, v0 = 0, v1 = 0;
+    // required presence (image.h "presence masks"): single-level hot slots a `has` atom of the
+    // entry spine requires, where no atom before it can raise: mpre before the key atom (or on the
+    // whole spine of an unkeyed policy), mpost also after it (exact in a bucket of the key's value,
+    // where the key atom cannot raise)
+    uint32_t mpre = 0, mpost = 0;
   };
+
+  // `has` slots the spine requires from atom i on, up to the first atom that can raise
+  uint32_t spine_has(const std::vector<uint32_t>& at, uint32_t n, uint32_t i) const {
+    uint32_t m = 0;
+    while (i < n) {
+      const uint32_t* a = &at[ATOM_WORDS * i];
+      const uint32_t kind = a[0] & 0xFF, h = (a[0] >> 8) & 0xFF, t = (a[0] >> 16) & 0xFF, f = a[0] >> 24;
+      const bool no_error = kind == AK_IS || kind == AK_IN || kind == AK_INANY || kind == AK_TRUE || kind == AK_EQV ||
+                            (kind == AK_HAS && hot_depth[h] == 1);
+      if (!no_error) break;
+      if (f == AT_UNSAT && t < AT_UNSAT) {
+        if (kind == AK_HAS && h < ASELF_PRES_SLOTS) m |= 1u << h;  // (the row carries slots 0..14)
+        i = t;
+      } else if (t == AT_UNSAT && f < AT_UNSAT) {
+        i = f;
+      } else {
+        break;
+      }
+    }
+    return m;
+  }
 
   AttrKey attr_key(const std::vector<uint32_t>& at, uint32_t n_atom_words) const {
     AttrKey k;
     const uint32_t n = n_atom_words / ATOM_WORDS;
     std::vector<uint32_t> present;  // single-level hot slots known present on the spine
     uint32_t i = 0;
+    k.mpre = k.mpost = spine_has(at, n, 0);
     while (i < n) {
       const uint32_t* a = &at[ATOM_WORDS * i];
       const uint32_t kind = a[0] & 0xFF, h = (a[0] >> 8) & 0xFF, t = (a[0] >> 16) & 0xFF, f = a[0] >> 24;
@@ -794,6 +821,7 @@ struct Compiler {
           k.v0 = tag == T_LONG ? mk_w0(T_LONG, 0) : a[1];
           k.v1 = a[2];
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
+          k.mpost = k.mpre | spine_has(at, n, t);
         }
         return k;
       }
@@ -825,6 +853,7 @@ struct Compiler {
           k.v0 = hv;
           k.v1 = 1;
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
+          k.mpost = k.mpre | spine_has(at, n, t);
         }
         return k;
       }
@@ -849,6 +878,7 @@ struct Compiler {
           k.v0 = pfx_hash(bytes, len);
           k.v1 = 1;
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
+          k.mpost = k.mpre | spine_has(at, n, t);
         }
         return k;
       }
@@ -1129,7 +1159,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   const uint32_t n = img.n_pol();
   img.btab.clear(); img.bfilt.clear(); img.bstream.clear();
   img.key_ents.clear();
-  img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0; img.sbloom.assign(2 * ctx_bloom_words(2), 0);
+  img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(SVAL_WORDS, 0); img.sbits_words = 0; img.sbloom.assign(2 * ctx_bloom_words(2), 0);
   img.combo_mask = 0;
   img.pslot_mask = 0;
   img.pfx.assign((size_t)img.n_hot() * PFX_LENS, 0);
@@ -1162,7 +1192,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   if (!img.indexed) {
     img.btab.assign(BT_WORDS, 0); img.bfilt.assign(2, 0); img.bstream.assign(HEAD_WORDS, 0);
     img.btab_slots = 2;
-    img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(2, 0); img.sbits_words = 0; img.sbloom.assign(2 * ctx_bloom_words(2), 0);
+    img.sctx.assign(2 * SCTX_WORDS, 0); img.sbits.assign(2, 0); img.svals.assign(SVAL_WORDS, 0); img.sbits_words = 0; img.sbloom.assign(2 * ctx_bloom_words(2), 0);
     return;
   }
   static const bool times = std::getenv("CEDARGPU_COMPILE_TIMES") != nullptr;
@@ -1608,6 +1638,22 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   for (uint32_t h : h1g) filt_add(h);
   for (uint32_t h : h2g) filt_add(h);
   if (img.btab.empty()) img.btab.assign(BT_WORDS, 0);  // never empty buffers
+  // each bucket's required presence (image.h "presence masks"): the slots every policy filed in it
+  // requires, a value key's bucket with the slots its policies' `has` atoms after the key atom name
+  std::vector<uint32_t> g1_need(g1.size()), g2_need(g2.size());
+  parallel_range(g1.size(), [&](size_t gi) {
+    uint32_t m = ~0u;
+    for (size_t i = g1[gi].b; i < g1[gi].e; i++)
+      if (r1[i].second != NO_POLICY) m &= akeys[r1[i].second].mpre;
+    g1_need[gi] = g1_cnt[gi] ? m : 0u;
+  });
+  parallel_range(g2.size(), [&](size_t gi) {
+    const auto& x = r2[g2[gi].b].first.second;
+    const bool value = x[1] != MISSING_W0 && x[1] != NOTSET_W0;
+    uint32_t m = ~0u;
+    for (size_t i = g2[gi].b; i < g2[gi].e; i++) m &= value ? akeys[r2[i].second].mpost : akeys[r2[i].second].mpre;
+    g2_need[gi] = g2_cnt[gi] ? m : 0u;
+  });
   mark("heads+slots");
   // the bitset rows as (bits, rank) word pairs, every set bit's bucket at its rank, and the context
   // table (image.h "scope bitsets")
@@ -1625,14 +1671,16 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       img.sbits[2 * w + 1] = rank;
       rank += (uint32_t)__builtin_popcount(bitw[w]);
     }
-    img.svals.assign(2 * (size_t)std::max<uint32_t>(rank, 1u), 0);
+    img.svals.assign(SVAL_WORDS * (size_t)std::max<uint32_t>(rank, 1u), 0);
     for (auto& b : sbit) {
       const size_t w = (size_t)b.row * words + (b.kidx >> 5);
       const uint32_t r = img.sbits[2 * w + 1] + (uint32_t)__builtin_popcount(bitw[w] & ((1u << (b.kidx & 31)) - 1u));
       const bool l2 = (b.grp & SB_L2) != 0;
       const uint32_t gi = b.grp & ~SB_L2;
-      img.svals[2 * (size_t)r] = l2 ? g2_first[gi] : g1_first[gi];
-      img.svals[2 * (size_t)r + 1] = l2 ? g2_cnt[gi] : g1_cnt[gi];
+      uint32_t* sv = &img.svals[SVAL_WORDS * (size_t)r];
+      sv[0] = l2 ? g2_first[gi] : g1_first[gi];
+      sv[1] = l2 ? g2_cnt[gi] : g1_cnt[gi];
+      sv[2] = l2 ? g2_need[gi] : g1_need[gi];
     }
     uint32_t slots = 2;
     while (slots < 2 * ctx.size()) slots <<= 1;
@@ -1660,10 +1708,13 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       img.sbloom[2 * (size_t)w + 1] |= (uint32_t)(b >> 32);
     }
   }
-  if (times)
-    std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities, %zu set bits): %.1f MB%s\n", ctx.size(),
-                 (unsigned long long)words, img.key_ents.size(), sbit.size(), ctx.size() * words * 8 / 1e6,
+  if (times) {
+    size_t masked = 0;
+    for (size_t r = 2; r < img.svals.size(); r += SVAL_WORDS) masked += img.svals[r] != 0;
+    std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities, %zu set bits, %zu with a presence mask): %.1f MB%s\n",
+                 ctx.size(), (unsigned long long)words, img.key_ents.size(), sbit.size(), masked, ctx.size() * words * 8 / 1e6,
                  img.sbits_words ? "" : " (over the cap: none)");
+  }
   mark("bitsets");
 }
 
@@ -2423,7 +2474,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
     const size_t svals_n = sec_view(DS_SVALS).second;
     const size_t nc = sctx_n / SCTX_WORDS;
     if (!nc || (nc & (nc - 1)) || sctx_n % SCTX_WORDS || sbits_n % 2 ||
-        (img->sbits_words && (sbits_n / 2) % img->sbits_words) || svals_n < 2 || svals_n % 2 ||
+        (img->sbits_words && (sbits_n / 2) % img->sbits_words) || svals_n < SVAL_WORDS || svals_n % SVAL_WORDS ||
         sec_view(DS_SBLOOM).second != 2 * (size_t)ctx_bloom_words((uint32_t)nc))
       throw CedarError("corrupt image (scope bitsets)");
     // every context row in range, a free slot that ends every probe chain, and ranks that number
@@ -2442,7 +2493,7 @@ std::shared_ptr<Image> Image::deserialize(const uint8_t* p, size_t n) {
       if (sbits[2 * w + 1] != rank) throw CedarError("corrupt image (scope bitsets)");
       rank += (uint32_t)__builtin_popcount(sbits[2 * w]);
     }
-    if ((size_t)rank * 2 > svals_n) throw CedarError("corrupt image (scope bitsets)");
+    if ((size_t)rank * SVAL_WORDS > svals_n) throw CedarError("corrupt image (scope bitsets)");
   }
   {
     const size_t ns = img->shash.size() / SH_WORDS;

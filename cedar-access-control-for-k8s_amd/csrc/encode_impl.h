@@ -724,6 +724,7 @@ void encode_impl(const Image& img, const Src& src, EncodedRequest& E) {
     if (code == E_NONE) {
       row[RW_HDR + 2 * h] = w0;
       row[RW_HDR + 2 * h + 1] = w1;
+      if (h < ASELF_PRES_SLOTS) row[RW_ASELF] |= 1u << (ASELF_PRES_SHIFT + h);  // (image.h "presence masks")
     } else {
       const uint32_t off = (uint32_t)blk.size();
       blk.push_back(code | (aux << 8)); blk.push_back(k); blk.push_back(et); blk.push_back(ei);

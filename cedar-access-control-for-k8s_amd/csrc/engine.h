@@ -199,7 +199,7 @@ struct Image {
   std::vector<uint64_t> key_ents;
   // scope bitsets (image.h "scope bitsets"): context table and one row of sbits_words per context
   RawWords sbits;
-  std::vector<uint32_t> sctx, svals;  // sbits: (bits, rank) per word; svals: (first, count) per set bit
+  std::vector<uint32_t> sctx, svals;  // sbits: (bits, rank) per word; svals: SVAL_WORDS per set bit
   std::vector<uint32_t> sbloom;              // context filter (image.h ctx_bloom_*), 64-bit words
   uint32_t sbits_words = 0;
   uint32_t l2_vmask = 0, l2_lmask = 0;  // hot slots with level-2 value keys / list keys under entity-principal combos

@@ -215,8 +215,9 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 // Each context in use has a row of sbits_words words, one bit per key entity (index into
 // Image::key_ents, "kidx"), stored as (bits, rank) word pairs: rank = the set bits of every earlier
 // word of every row, so a set bit's global rank is rank + popcount of the word's lower bits. svals
-// holds each set bit's bucket at its rank: (first head, head count) of the key's own scope-index
-// entry, what a probe of that key in btab would return. sctx: an open-addressed table of S slots (S
+// holds each set bit's bucket at its rank, SVAL_WORDS each: (first head, head count) of the key's
+// own scope-index entry, what a probe of that key in btab would return, and the bucket's presence
+// mask (below). sctx: an open-addressed table of S slots (S
 // a power of two) at ctx_key(key_pre(combo, at, ai, rt, ri), hs, v0, v1) & (S - 1), SCTX_WORDS
 // each: [SCTX_USED | combo << 16 | hs, at, ai, rt, ri, v0, v1, row] (0 = empty; 32 bytes, one
 // round trip, compared whole). A request looks up its contexts (per entity-principal combo: level
@@ -227,6 +228,16 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 // btab probe. On C3 that is ~8 bucket reads from a ~0.1 MB table per request instead of ~62
 // level-1 probes of 64-byte slots and their level-2 follow-ups; the grouped requests of a wave
 // share the rows. Images whose bitsets would exceed SBITS_MAX_BYTES have none (sbits_words == 0).
+// Presence masks: a policy whose entry spine reaches `hot(h) has` (a single-level slot, so the
+// test cannot raise) with its false edge UNSAT, before any atom that can raise, is UNSAT on every
+// request without that attribute. A bucket's mask is the AND of its policies' such slots (in a
+// bucket of a level-2 key's value, where the key atom cannot raise, also the `has` atoms after the
+// key atom; slots 0..ASELF_PRES_SLOTS - 1 only); the scan lists a bucket from svals only when the
+// request has every slot of its mask (the encoder's presence bits in the row's RW_ASELF), so such a
+// request's candidates never include it.
+// (Only the bitset path filters: a bucket reached by a btab probe is evaluated as before, which is
+// the same answer.)
+constexpr uint32_t SVAL_WORDS = 4;  // (first head, head count, presence mask, 0)
 constexpr uint32_t SCTX_WORDS = 8, SCTX_USED = 0x80000000u, SCTX_L1 = 0xFFFFu, KIDX_NONE = 0xFFFFFFFFu;
 constexpr uint64_t SBITS_MAX_BYTES = 64ull << 20;
 __host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {
@@ -326,7 +337,8 @@ enum RowW : uint32_t {
   RW_AM0 = 13,   // action mask over the image action table (`in`: the action or an ancestor), low
   RW_AM1 = 14,   //   ... high word (valid when the image's amask_ok)
   RW_ASELF = 15, // index of the action itself in the action table (`==`) in the low 16 bits (0xFFFF
-                 // when absent) | ASELF_CTXR: the block's RH_SCTX words hold its scope contexts
+                 // when absent) | the presence mask << ASELF_PRES_SHIFT (ASELF_PRES_SLOTS bits)
+                 // | ASELF_CTXR: the block's RH_SCTX words hold its scope contexts
   RW_HDR = 16,   // hot slots follow: (w0, w1) per hot path
 };
 constexpr uint32_t MISSING_W0 = 0xFFFFFFFFu;  // level-2 index key of an absent hot value
@@ -382,6 +394,9 @@ inline uint32_t pfx_hash(const uint8_t* s, uint32_t len) {
 // RW_PN / RW_RN / RW_AN fields
 constexpr uint32_t AN_COUNT = 0xFFFFu, AN_KEYS_SHIFT = 16, AN_KEYS = 0x7FFFu, AN_SELF = 0x80000000u;
 constexpr uint32_t ASELF_MASK = 0xFFFFu, ASELF_CTXR = 0x80000000u;
+// RW_ASELF bits 16..30: the request's presence mask over hot slots 0..14 (image.h "presence
+// masks": slot h's bit when its value is present, i.e. `has` finds it); masks name no other slot
+constexpr uint32_t ASELF_PRES_SHIFT = 16, ASELF_PRES_SLOTS = 15;
 
 // ---- bytecode -------------------------------------------------------------------------------
 // word0 = op | d << 8 | a << 14 | b << 20 | c << 26 (6-bit slot fields); word1 = imm
@@ -483,7 +498,7 @@ enum TypeName : uint32_t {
 
 // ---- image blob header (host serialization) ----------------------------------------------
 constexpr uint32_t IMG_MAGIC = 0x47444543u;  // "CEDG"
-constexpr uint32_t IMG_VERSION = 16;
+constexpr uint32_t IMG_VERSION = 17;
 // The blob's device region: the arrays the kernels read, each at a 256-byte-aligned blob offset
 // in one contiguous range [dev_begin, dev_end) listed by a section table after the header. A device
 // copy of the image is that range in one allocation (one H2D copy, one peer copy, or the blob
