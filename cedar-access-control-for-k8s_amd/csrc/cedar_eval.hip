@@ -1754,6 +1754,7 @@ constexpr uint32_t SCAN_PU = 4, SCAN_POS = 64;
 // the flag of a listed key the bitsets found (image.h "scope bitsets")
 constexpr uint32_t LIST_EXACT = 0x80000000u, SCAN_POS_B = 40;  // (CTX_CAP: image.h)
 constexpr uint32_t SCAN_HOT = 16;  // hot values the scan stages in LDS (the rest read from the row)
+static_assert(EQF_SLOTS <= SCAN_HOT, "equality-filter slots are staged in the scan's LDS");
 constexpr uint32_t SCAN_ROW = 56;  // scan LDS row words (64 - 8: see s_kid; the LDS stays under 1/24 of a CU for 6 waves per SIMD)
 static_assert(SCAN_ANC + 2 <= SCAN_ROW - 1 && SCAN_POS_B + 2 <= SCAN_ROW, "scan LDS rows (s_kid's last word: the presence mask)");
 constexpr uint32_t SCAN_PB = 8;    // bit tests per lane per round (loads in flight)
@@ -2157,9 +2158,14 @@ __global__ __launch_bounds__(64, MINW) void cedar_scan_kernel(KArgs a) {
           uint32_t cmv = 0;
           if (BITS && (x & LIST_EXACT)) {  // a key the bitsets found: its bucket at the bit's rank,
                                            // unless it needs an attribute the request lacks
-            const uint3 v = *reinterpret_cast<const uint3*>(a.svals + SVAL_WORDS * (size_t)(x & 0x3FFFFFFu));
+            const uint4 v = *reinterpret_cast<const uint4*>(a.svals + SVAL_WORDS * (size_t)(x & 0x3FFFFFFu));
             const uint32_t pm = s_kid[seg][SCAN_ROW - 1];
-            e = (v.z & ~pm) ? make_uint3(0u, 0u, 0u) : make_uint3(v.x, v.y, 0u);
+            bool keep = (v.z & ~pm) == 0u;
+            if (keep && (v.w & EQF_ON)) {  // its policies' equality after the key (image.h "equality filters")
+              const uint2 hv = s_hot[seg][(v.w >> EQF_SLOT_SHIFT) & (EQF_SLOTS - 1u)];
+              keep = !hot_ok(hv) || eqf_hash(hv.x, hv.y) == (v.w & EQF_HASH);
+            }
+            e = keep ? make_uint3(v.x, v.y, 0u) : make_uint3(0u, 0u, 0u);
           } else {
             if (BITS && flt) {
               kp = comb_p(combo, 0u);

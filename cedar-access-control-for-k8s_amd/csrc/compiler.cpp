@@ -780,17 +780,25 @@ struct Compiler {
     // whole spine of an unkeyed policy), mpost also after it (exact in a bucket of the key's value,
     // where the key atom cannot raise)
     uint32_t mpre = 0, mpost = 0;
+    uint32_t filt = 0;  // the equality after the key atom (image.h "equality filters"), 0: none
   };
 
-  // `has` slots the spine requires from atom i on, up to the first atom that can raise
-  uint32_t spine_has(const std::vector<uint32_t>& at, uint32_t n, uint32_t i) const {
+  // `has` slots the spine requires from atom i on, up to the first atom that can raise; with
+  // `filt`, that atom's equality filter when it is `hot(h) == constant` (image.h "equality filters")
+  uint32_t spine_has(const std::vector<uint32_t>& at, uint32_t n, uint32_t i, uint32_t* filt = nullptr) const {
     uint32_t m = 0;
     while (i < n) {
       const uint32_t* a = &at[ATOM_WORDS * i];
       const uint32_t kind = a[0] & 0xFF, h = (a[0] >> 8) & 0xFF, t = (a[0] >> 16) & 0xFF, f = a[0] >> 24;
       const bool no_error = kind == AK_IS || kind == AK_IN || kind == AK_INANY || kind == AK_TRUE || kind == AK_EQV ||
                             (kind == AK_HAS && hot_depth[h] == 1);
-      if (!no_error) break;
+      if (!no_error) {
+        const uint32_t tag = a[1] >> TAG_SHIFT;
+        if (filt && kind == AK_EQ && f == AT_UNSAT && t != AT_UNSAT && h < EQF_SLOTS &&
+            (tag == T_STR || tag == T_BOOL || tag == T_ENT))
+          *filt = EQF_ON | (h << EQF_SLOT_SHIFT) | eqf_hash(a[1], a[2]);
+        break;
+      }
       if (f == AT_UNSAT && t < AT_UNSAT) {
         if (kind == AK_HAS && h < ASELF_PRES_SLOTS) m |= 1u << h;  // (the row carries slots 0..14)
         i = t;
@@ -821,7 +829,7 @@ struct Compiler {
           k.v0 = tag == T_LONG ? mk_w0(T_LONG, 0) : a[1];
           k.v1 = a[2];
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
-          k.mpost = k.mpre | spine_has(at, n, t);
+          k.mpost = k.mpre | spine_has(at, n, t, &k.filt);
         }
         return k;
       }
@@ -853,7 +861,7 @@ struct Compiler {
           k.v0 = hv;
           k.v1 = 1;
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
-          k.mpost = k.mpre | spine_has(at, n, t);
+          k.mpost = k.mpre | spine_has(at, n, t, &k.filt);
         }
         return k;
       }
@@ -878,7 +886,7 @@ struct Compiler {
           k.v0 = pfx_hash(bytes, len);
           k.v1 = 1;
           k.guarded = std::find(present.begin(), present.end(), h) != present.end();
-          k.mpost = k.mpre | spine_has(at, n, t);
+          k.mpost = k.mpre | spine_has(at, n, t, &k.filt);
         }
         return k;
       }
@@ -1640,7 +1648,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   if (img.btab.empty()) img.btab.assign(BT_WORDS, 0);  // never empty buffers
   // each bucket's required presence (image.h "presence masks"): the slots every policy filed in it
   // requires, a value key's bucket with the slots its policies' `has` atoms after the key atom name
-  std::vector<uint32_t> g1_need(g1.size()), g2_need(g2.size());
+  std::vector<uint32_t> g1_need(g1.size()), g2_need(g2.size()), g2_filt(g2.size());
   parallel_range(g1.size(), [&](size_t gi) {
     uint32_t m = ~0u;
     for (size_t i = g1[gi].b; i < g1[gi].e; i++)
@@ -1650,9 +1658,13 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
   parallel_range(g2.size(), [&](size_t gi) {
     const auto& x = r2[g2[gi].b].first.second;
     const bool value = x[1] != MISSING_W0 && x[1] != NOTSET_W0;
-    uint32_t m = ~0u;
-    for (size_t i = g2[gi].b; i < g2[gi].e; i++) m &= value ? akeys[r2[i].second].mpost : akeys[r2[i].second].mpre;
+    uint32_t m = ~0u, fl = value && g2_cnt[gi] ? akeys[r2[g2[gi].b].second].filt : 0u;
+    for (size_t i = g2[gi].b; i < g2[gi].e; i++) {
+      m &= value ? akeys[r2[i].second].mpost : akeys[r2[i].second].mpre;
+      if (akeys[r2[i].second].filt != fl) fl = 0;  // the filter only when every policy has the same one
+    }
     g2_need[gi] = g2_cnt[gi] ? m : 0u;
+    g2_filt[gi] = fl;
   });
   mark("heads+slots");
   // the bitset rows as (bits, rank) word pairs, every set bit's bucket at its rank, and the context
@@ -1681,6 +1693,7 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
       sv[0] = l2 ? g2_first[gi] : g1_first[gi];
       sv[1] = l2 ? g2_cnt[gi] : g1_cnt[gi];
       sv[2] = l2 ? g2_need[gi] : g1_need[gi];
+      sv[3] = l2 ? g2_filt[gi] : 0u;
     }
     uint32_t slots = 2;
     while (slots < 2 * ctx.size()) slots <<= 1;
@@ -1709,10 +1722,14 @@ static void build_scope_index(Image& img, const std::vector<AK>& akeys_in) {
     }
   }
   if (times) {
-    size_t masked = 0;
-    for (size_t r = 2; r < img.svals.size(); r += SVAL_WORDS) masked += img.svals[r] != 0;
-    std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities, %zu set bits, %zu with a presence mask): %.1f MB%s\n",
-                 ctx.size(), (unsigned long long)words, img.key_ents.size(), sbit.size(), masked, ctx.size() * words * 8 / 1e6,
+    size_t masked = 0, filtered = 0;
+    for (size_t r = 0; r + SVAL_WORDS <= img.svals.size(); r += SVAL_WORDS) {
+      masked += img.svals[r + 2] != 0;
+      filtered += img.svals[r + 3] != 0;
+    }
+    std::fprintf(stderr, "  scope bitsets: %zu contexts x %llu words (%zu key entities, %zu set bits, %zu with a presence mask, "
+                 "%zu with an equality filter): %.1f MB%s\n",
+                 ctx.size(), (unsigned long long)words, img.key_ents.size(), sbit.size(), masked, filtered, ctx.size() * words * 8 / 1e6,
                  img.sbits_words ? "" : " (over the cap: none)");
   }
   mark("bitsets");

@@ -237,7 +237,23 @@ __host__ __device__ constexpr inline uint64_t filt_need(uint32_t h) {  // the 3 
 // request's candidates never include it.
 // (Only the bitset path filters: a bucket reached by a btab probe is evaluated as before, which is
 // the same answer.)
-constexpr uint32_t SVAL_WORDS = 4;  // (first head, head count, presence mask, 0)
+// Equality filters: in a bucket of a level-2 key's value, a policy whose spine after the key atom
+// reaches `hot(h) == c` (c a string, Boolean or entity) with only atoms that cannot raise before
+// it is UNSAT on every request whose slot h holds a value other than c. When every policy of the
+// bucket has the same such (h, c), the bucket carries EQF_ON | h << EQF_SLOT_SHIFT | eqf_hash(c),
+// and the scan skips it for a request whose hot value h is present (a missing or erroneous value
+// makes the atom raise: the bucket stays) with another hash (equal values hash alike).
+constexpr uint32_t EQF_ON = 0x80000000u, EQF_SLOT_SHIFT = 26, EQF_SLOTS = 16, EQF_HASH = (1u << EQF_SLOT_SHIFT) - 1u;
+__host__ __device__ constexpr inline uint32_t eqf_hash(uint32_t w0, uint32_t w1) {
+  // (the words prim_eq compares: an entity's type and id, another value's tag and word 1)
+  const uint32_t a = (w0 >> TAG_SHIFT) == T_ENT ? w0 : (w0 >> TAG_SHIFT) << TAG_SHIFT;
+  uint32_t h = (a * 0x9E3779B1u) ^ ((w1 + 0x7F4A7C15u) * 0x85EBCA77u);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h & EQF_HASH;
+}
+constexpr uint32_t SVAL_WORDS = 4;  // (first head, head count, presence mask, equality filter)
 constexpr uint32_t SCTX_WORDS = 8, SCTX_USED = 0x80000000u, SCTX_L1 = 0xFFFFu, KIDX_NONE = 0xFFFFFFFFu;
 constexpr uint64_t SBITS_MAX_BYTES = 64ull << 20;
 __host__ __device__ constexpr inline uint32_t ctx_hash(uint32_t pre) {

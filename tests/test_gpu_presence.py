@@ -1,6 +1,7 @@
-"""Presence masks (image.h "presence masks"): the scan lists a bucket from the scope bitsets only
-when the request has every attribute its policies' `has` atoms require, where those atoms come
-before anything that can raise (and, in a bucket of a key's value, after the key atom). Policies
+"""Presence masks and equality filters (image.h): the scan lists a bucket from the scope bitsets
+only when the request has every attribute its policies' `has` atoms require, where those atoms
+come before anything that can raise (and, in a bucket of a key's value, after the key atom), and
+when no equality after the key atom that all its policies share is false for the request. Policies
 with `has` before, after and instead of their key atom, on a false path, and behind atoms that
 raise, against SubjectAccessReviews with and without those attributes: every decision and
 diagnostic equal to the C++ oracle's (oracle/cedar_ref.cpp), on the split first pass (the bitset
@@ -40,7 +41,14 @@ def _policies(groups):
             # a selector read with no guard: raises without one (never masked)
             f'permit (\n  {scope}\n)\nwhen {{ resource.resource == "deployments" && '
             f'resource.labelSelector.containsAny({sel}) }};',
+            # equality filters: an equality after the key on an attribute a request may lack (the
+            # atom raises: never skipped) ...
+            f'permit (\n  {scope}\n)\nwhen {{ resource.resource == "configmaps" && resource.name == "configmap-5" }};',
+            # ... and buckets whose policies agree on the filter or do not
+            f'permit (\n  {scope}\n)\nwhen {{ resource.namespace == "ns-002" && resource.apiGroup == "apps" }};',
         ]
+        if int(g[-1]) % 2 == 0:
+            out.append(f'forbid (\n  {scope}\n)\nwhen {{ resource.namespace == "ns-002" && resource.apiGroup == "" }};')
     return "\n".join(out)
 
 
