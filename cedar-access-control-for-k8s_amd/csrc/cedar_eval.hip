@@ -4387,13 +4387,16 @@ static void print_probe_stats(const char* what, const std::vector<unsigned long 
     return end;
   };
   double all = 0;
+  size_t idle = 0;  // waves whose requests have no candidate head at all
+  for (size_t w = 0; w < nw; w++) idle += h[w * 16 + 6] == 0;
   for (unsigned long long x : tot) all += (double)x;
   const unsigned long long in_order = makespan(tot);
   const unsigned long long reversed = makespan(std::vector<unsigned long long>(tot.rbegin(), tot.rend()));
   std::sort(tot.begin(), tot.end());
   const unsigned long long longest_first = makespan(std::vector<unsigned long long>(tot.rbegin(), tot.rend()));
-  std::fprintf(stderr, "%s dispatch: makespan in launch order %llu, reversed %llu, longest first %llu, bound %.0f (cycles)\n",
-               what, in_order, reversed, longest_first, all / (256.0 * 16.0));
+  std::fprintf(stderr, "%s dispatch: makespan in launch order %llu, reversed %llu, longest first %llu, bound %.0f (cycles); "
+               "waves without candidates %.3f\n", what, in_order, reversed, longest_first, all / (256.0 * 16.0),
+               nw ? (double)idle / (double)nw : 0.0);
   const double r = sum[0] > 0 ? sum[0] : 1.0, W = (double)nw;
   std::fprintf(stderr,
                "%s stats: requests %.0f | per request: L1 keys %.2f found %.2f | L2 probes %.2f found %.2f | "
