@@ -1330,6 +1330,7 @@ __global__ __launch_bounds__(BLOCK) void cedar_eval_kernel(KArgs a) {
   extern __shared__ uint2 hot_lds[];                                          // [n_hot][BLOCK]
   const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t n_req = a.n_dev ? min(*a.n_dev, a.n_req) : a.n_req;  // follow-up: count on the device
+  if (blockIdx.x * BLOCK >= n_req) return;  // (block-uniform: a follow-up's unused blocks stage no policy)
   const bool valid = gid < n_req;
   // position p in the first pass's launch order (first pass: gid; follow-up: its worklist entry's),
   // the request's row r (ord[p] for a batch grouped on the device); the result slot is the worklist
